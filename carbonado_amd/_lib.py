@@ -1,0 +1,108 @@
+"""ctypes binding of libcarbonado_hip.so (include/carbonado_hip.h).
+
+The shared library is the product: HIP kernels for gfx950 behind a C-ABI.
+This module only loads it and declares signatures.  There is no fallback:
+if the library is missing, or no gfx950 device is visible, compute calls
+raise instead of silently running elsewhere.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libcarbonado_hip.so"
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+class EncodeInfoC(ctypes.Structure):
+    """chip_encode_info == structs.rs:12-44 EncodeInfo, field for field."""
+
+    _fields_ = [
+        ("input_len", ctypes.c_uint32),
+        ("output_len", ctypes.c_uint32),
+        ("bytes_compressed", ctypes.c_uint32),
+        ("compression_factor", ctypes.c_float),
+        ("bytes_encrypted", ctypes.c_uint32),
+        ("bytes_ecc", ctypes.c_uint32),
+        ("bytes_verifiable", ctypes.c_uint32),
+        ("amplification_factor", ctypes.c_float),
+        ("padding_len", ctypes.c_uint32),
+        ("chunk_len", ctypes.c_uint32),
+        ("verifiable_slice_count", ctypes.c_uint16),
+        ("chunk_slice_count", ctypes.c_uint16),
+    ]
+
+
+# name -> (restype, argtypes); mirrors include/carbonado_hip.h exactly
+SIGNATURES = {
+    "chip_abi_version": (ctypes.c_int, []),
+    "chip_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "chip_init": (ctypes.c_int, [ctypes.c_int]),
+    "chip_last_device_error": (ctypes.c_char_p, []),
+    "chip_calc_padding_len": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, c_u32p, c_u32p]),
+    "chip_zfec_encoded_len": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]),
+    "chip_bao_encoded_len": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "chip_encode_max_len": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "chip_zfec_encode": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_void_p, ctypes.c_uint64, c_u32p, c_u32p]),
+    "chip_zfec_decode": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
+    "chip_zfec_decode_shares": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.POINTER(ctypes.c_void_p), c_u32p, ctypes.c_uint32,
+                                               ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                               ctypes.c_uint64, c_u64p]),
+    "chip_bao_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                       c_u64p, ctypes.c_void_p]),
+    "chip_bao_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                       ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
+    "chip_blake3": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "chip_encode": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                   ctypes.c_uint64, c_u64p, ctypes.c_void_p, ctypes.POINTER(EncodeInfoC)]),
+    "chip_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                   ctypes.c_uint32, ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
+    "chip_zfec_encode_batch_dev": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                                  ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "chip_zfec_decode_batch_dev": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                                  ctypes.c_uint64, ctypes.c_uint64, c_u32p, ctypes.c_uint32,
+                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                                  ctypes.c_void_p]),
+    "chip_bao_scratch_len": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+    "chip_bao_encode_batch_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "chip_bao_decode_batch_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p]),
+}
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise if it is not built."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback for the carbonado hot path)")
+        # One HIP runtime per process.  torch's HIP libs NEED "libamdhip64.so"
+        # (unversioned, RPATH $ORIGIN) while this library NEEDs the soname
+        # "libamdhip64.so.7": loading torch first makes both bind to torch's
+        # copy; the reverse order would map two runtimes.
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # torch is plumbing only; the library does not need it
+            pass
+        l = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = l
+    return _LIB

@@ -1,0 +1,631 @@
+// chip_api.cpp — the C-ABI of libcarbonado_hip (include/carbonado_hip.h).
+//
+// Host-side orchestration only: argument checks and error mapping that mirror
+// the reference stage functions (file:line cited per entry point), staging of
+// host buffers into per-thread device scratch, and the encode()/decode() glue.
+// Every byte of shard/stream data is produced by the HIP kernels in
+// zfec_kernels.hip and bao_kernels.hip; there is no CPU compute path.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "chip_internal.hpp"
+#include "gf256.hpp"
+
+namespace chip {
+
+namespace {
+
+std::once_flag g_dev_once;
+int g_device = -1;
+int g_cus = 0;
+int g_dev_status = CHIP_ERR_NO_DEVICE;
+thread_local std::string t_last_err;
+
+void init_device_once() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        t_last_err = "no HIP device visible";
+        return;
+    }
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) {
+            g_device = d;
+            g_cus = prop.multiProcessorCount;
+            g_dev_status = CHIP_OK;
+            return;
+        }
+    }
+    t_last_err = "no gfx950 device visible";
+}
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+
+struct Ctx {
+    bool ready = false;
+    hipStream_t stream = nullptr;
+    DevBuf in, mid, out, scratch, small;
+    ~Ctx() {
+        // process teardown: the runtime may already be gone; best effort
+        for (DevBuf *b : {&in, &mid, &out, &scratch, &small})
+            if (b->p) (void)hipFree(b->p);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+thread_local Ctx t_ctx;
+
+hipError_t grow(DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        if (e != hipSuccess) return e;
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    size_t cap = bytes + (bytes >> 3);  // grow-only with headroom
+    cap = (cap + 255) & ~size_t(255);
+    hipError_t e = hipMalloc(&b.p, cap);
+    if (e != hipSuccess) return e;
+    b.cap = cap;
+    return hipSuccess;
+}
+
+}  // namespace
+
+int ensure_device() {
+    std::call_once(g_dev_once, init_device_once);
+    return g_dev_status;
+}
+
+void set_device_error(hipError_t e) { t_last_err = hipGetErrorString(e); }
+
+int num_cus() { return g_cus > 0 ? g_cus : 256; }
+
+}  // namespace chip
+
+using namespace chip;
+
+namespace {
+
+#define CHIP_HIP(expr)                                  \
+    do {                                                \
+        hipError_t e__ = (expr);                        \
+        if (e__ != hipSuccess) {                        \
+            set_device_error(e__);                      \
+            return CHIP_ERR_DEVICE;                     \
+        }                                               \
+    } while (0)
+
+int ctx_get(Ctx **out) {
+    int st = ensure_device();
+    if (st != CHIP_OK) return st;
+    Ctx &c = t_ctx;
+    if (!c.ready) {
+        CHIP_HIP(hipSetDevice(g_device));
+        CHIP_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        c.ready = true;
+    } else {
+        CHIP_HIP(hipSetDevice(g_device));
+    }
+    *out = &c;
+    return CHIP_OK;
+}
+
+bool valid_km(uint32_t k, uint32_t m) { return k >= 1 && m >= k && m <= 256; }
+
+void calc_pad(uint64_t n, uint32_t k, uint32_t *pad, uint64_t *C) {
+    const uint64_t unit = 1024ull * k;
+    const uint64_t target = (n + unit - 1) / unit * unit;
+    *pad = (uint32_t)(target - n);
+    *C = target / k;
+}
+
+// encode plan: rows 0..k-1 copied, k..m-1 computed from the enc_matrix
+GfPlan encode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint8_t> &enc) {
+    GfPlan p;
+    p.k = k;
+    p.np = m - k;
+    for (uint32_t j = 0; j < ZF_MAXK; ++j) {
+        p.in_off[j] = j < k ? (uint64_t)j * C : 0;
+        p.copy_off[j] = j < k ? (uint64_t)j * C : NO_OUT;
+    }
+    p.coef.assign(enc.begin() + (size_t)k * k, enc.end());
+    for (uint32_t q = 0; q < p.np; ++q) p.comp_off.push_back((uint64_t)(k + q) * C);
+    // generic description (all m rows as coefficient rows)
+    p.g_in_off.resize(k);
+    for (uint32_t j = 0; j < k; ++j) p.g_in_off[j] = (uint64_t)j * C;
+    p.g_out_off.resize(m);
+    for (uint32_t r = 0; r < m; ++r) p.g_out_off[r] = (uint64_t)r * C;
+    p.g_coef = enc;
+    return p;
+}
+
+// decode plan for k selected shares (slot s holds share sel[s], stored at
+// in_off[s]); output rows 0..k-1 at r*C
+int decode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint32_t> &sel,
+                const std::vector<uint64_t> &slot_off, GfPlan *out) {
+    std::vector<uint8_t> enc = zfec_enc_matrix(k, m);
+    std::vector<uint8_t> a((size_t)k * k);
+    for (uint32_t s = 0; s < k; ++s)
+        std::memcpy(&a[(size_t)s * k], &enc[(size_t)sel[s] * k], k);
+    if (!gf_invert(a, k)) return CHIP_ERR_ZFEC;
+    GfPlan p;
+    p.k = k;
+    p.np = 0;
+    std::vector<int> present(k, -1);
+    for (uint32_t s = 0; s < k; ++s)
+        if (sel[s] < k) present[sel[s]] = (int)s;
+    for (uint32_t j = 0; j < ZF_MAXK; ++j) {
+        p.in_off[j] = j < k ? slot_off[j] : 0;
+        p.copy_off[j] = NO_OUT;
+    }
+    p.g_in_off = slot_off;
+    for (uint32_t r = 0; r < k; ++r) {
+        p.g_out_off.push_back((uint64_t)r * C);
+        if (present[r] >= 0) {
+            if (k <= ZF_MAXK) p.copy_off[present[r]] = (uint64_t)r * C;
+            for (uint32_t s = 0; s < k; ++s) p.g_coef.push_back(s == (uint32_t)present[r] ? 1 : 0);
+        } else {
+            p.comp_off.push_back((uint64_t)r * C);
+            for (uint32_t s = 0; s < k; ++s) p.coef.push_back(a[(size_t)r * k + s]);
+            for (uint32_t s = 0; s < k; ++s) p.g_coef.push_back(a[(size_t)r * k + s]);
+            p.np++;
+        }
+    }
+    *out = p;
+    return CHIP_OK;
+}
+
+// choose k distinct shares: primaries first, then secondaries in given order
+int select_shares(uint32_t k, uint32_t m, const uint32_t *idx, uint32_t nshares,
+                  std::vector<uint32_t> *sel_pos) {
+    std::vector<char> have(m, 0);
+    sel_pos->clear();
+    for (uint32_t s = 0; s < nshares; ++s) {
+        if (idx[s] >= m) return CHIP_ERR_ZFEC;
+        if (idx[s] < k && !have[idx[s]]) { have[idx[s]] = 1; sel_pos->push_back(s); }
+    }
+    for (uint32_t s = 0; s < nshares && sel_pos->size() < k; ++s)
+        if (idx[s] >= k && !have[idx[s]]) { have[idx[s]] = 1; sel_pos->push_back(s); }
+    return sel_pos->size() == k ? CHIP_OK : CHIP_ERR_ZFEC;
+}
+
+}  // namespace
+
+extern "C" {
+
+int chip_abi_version(void) { return CHIP_ABI_VERSION; }
+
+const char *chip_strerror(int st) {
+    switch (st) {
+        case CHIP_OK: return "ok";
+        case CHIP_ERR_INVALID_ARG: return "invalid argument";
+        case CHIP_ERR_BUFFER_TOO_SMALL: return "output buffer too small";
+        case CHIP_ERR_UNEVEN_ZFEC_CHUNKS: return "Input bytes must divide evenly over number of zfec chunks.";
+        case CHIP_ERR_HASH_DECODE: return "Hash must be 32 bytes long.";
+        case CHIP_ERR_BAO_HASH_MISMATCH: return "bao decode error: hash mismatch";
+        case CHIP_ERR_BAO_TRUNCATED: return "bao decode error: encoding truncated";
+        case CHIP_ERR_ZFEC: return "zfec error";
+        case CHIP_ERR_ENCODE_ZFEC_PADDING: return "Padding from Zfec should always be zero.";
+        case CHIP_ERR_ENCODE_INVALID_CHUNK_LENGTH: return "Chunk length should be as calculated.";
+        case CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT: return "Verifiable slice count should be evenly divisible by 8.";
+        case CHIP_ERR_UNSUPPORTED_FORMAT: return "format bit handled by a host stage outside this path (ecies/snappy)";
+        case CHIP_ERR_NO_DEVICE: return "no usable gfx950 device";
+        case CHIP_ERR_DEVICE: return "HIP runtime error";
+        default: return "unknown status";
+    }
+}
+
+int chip_init(int device) {
+    (void)device;
+    Ctx *c;
+    return ctx_get(&c);
+}
+
+const char *chip_last_device_error(void) { return t_last_err.c_str(); }
+
+int chip_calc_padding_len(uint64_t input_len, uint32_t k, uint32_t *padding, uint32_t *chunk_len) {
+    if (!padding || !chunk_len || k == 0) return CHIP_ERR_INVALID_ARG;
+    uint64_t C;
+    calc_pad(input_len, k, padding, &C);
+    *chunk_len = (uint32_t)C;
+    return CHIP_OK;
+}
+
+uint64_t chip_zfec_encoded_len(uint64_t n, uint32_t k, uint32_t m) {
+    if (k == 0) return 0;
+    uint32_t pad;
+    uint64_t C;
+    calc_pad(n, k, &pad, &C);
+    return (uint64_t)m * C;
+}
+
+uint64_t chip_bao_encoded_len(uint64_t n) { return bao_encoded_len(n); }
+
+uint64_t chip_encode_max_len(uint64_t n) {
+    const uint64_t z = chip_zfec_encoded_len(n, CHIP_FEC_K, CHIP_FEC_M);
+    const uint64_t big = z > n ? z : n;
+    return bao_encoded_len(big);
+}
+
+uint64_t chip_bao_scratch_len(uint64_t n, uint64_t count) { return bao_scratch_len(n, count); }
+
+// ---- zfec --------------------------------------------------------------
+
+int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
+                               uint64_t n, uint64_t count, uint8_t *d_out, uint64_t out_stride,
+                               void *stream) {
+    if (!valid_km(k, m)) return CHIP_ERR_ZFEC;
+    if ((!d_in && n) || !d_out || (in_stride % 16) || (out_stride % 16)) return CHIP_ERR_INVALID_ARG;
+    int st = ensure_device();
+    if (st != CHIP_OK) return st;
+    uint32_t pad;
+    uint64_t C;
+    calc_pad(n, k, &pad, &C);
+    if (count > 1 && out_stride < (uint64_t)m * C) return CHIP_ERR_INVALID_ARG;
+    GfPlan p = encode_plan(k, m, C, zfec_enc_matrix(k, m));
+    GfLaunch L{d_in, d_out, in_stride, out_stride, n, C, count};
+    CHIP_HIP(gf_apply(p, L, static_cast<hipStream_t>(stream)));
+    return CHIP_OK;
+}
+
+int chip_zfec_encode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t n, uint8_t *out,
+                     uint64_t out_cap, uint32_t *padding, uint32_t *chunk_len) {
+    if (!valid_km(k, m)) return CHIP_ERR_ZFEC;
+    if ((!in && n) || !padding || !chunk_len) return CHIP_ERR_INVALID_ARG;
+    uint32_t pad;
+    uint64_t C;
+    calc_pad(n, k, &pad, &C);
+    const uint64_t total = (uint64_t)m * C;
+    if (total && (!out || out_cap < total)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    Ctx *c;
+    int st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    if (n) {
+        CHIP_HIP(grow(c->in, n));
+        CHIP_HIP(grow(c->out, total));
+        CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+        GfPlan p = encode_plan(k, m, C, zfec_enc_matrix(k, m));
+        GfLaunch L{static_cast<const uint8_t *>(c->in.p), static_cast<uint8_t *>(c->out.p), 0, 0, n, C, 1};
+        CHIP_HIP(gf_apply(p, L, c->stream));
+        CHIP_HIP(hipMemcpyAsync(out, c->out.p, total, hipMemcpyDeviceToHost, c->stream));
+        CHIP_HIP(hipStreamSynchronize(c->stream));
+    }
+    *padding = pad;
+    *chunk_len = (uint32_t)C;
+    return CHIP_OK;
+}
+
+// shares already on the device, contiguous slots of C bytes at d_shares
+static int zfec_decode_device(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
+                              const std::vector<uint64_t> &slot_off, const std::vector<uint32_t> &sel,
+                              uint64_t C, uint64_t count, uint8_t *d_out, uint64_t out_stride,
+                              hipStream_t s) {
+    GfPlan p;
+    int st = decode_plan(k, m, C, sel, slot_off, &p);
+    if (st != CHIP_OK) return st;
+    GfLaunch L{d_in, d_out, in_stride, out_stride, ~0ull, C, count};
+    CHIP_HIP(gf_apply(p, L, s));
+    return CHIP_OK;
+}
+
+int chip_zfec_decode_shares(uint32_t k, uint32_t m, const uint8_t *const *shares,
+                            const uint32_t *idx, uint32_t nshares, uint64_t chunk_len,
+                            uint32_t padding, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if (!valid_km(k, m)) return CHIP_ERR_ZFEC;
+    if (!shares || !idx || !out_len) return CHIP_ERR_INVALID_ARG;
+    const uint64_t kc = (uint64_t)k * chunk_len;
+    if (padding > kc) return CHIP_ERR_ZFEC;
+    if (chunk_len % 16) return CHIP_ERR_ZFEC;  // carbonado shards are multiples of 1 KiB
+    std::vector<uint32_t> pos;
+    int st = select_shares(k, m, idx, nshares, &pos);
+    if (st != CHIP_OK) return st;
+    const uint64_t olen = kc - padding;
+    if (olen && (!out || out_cap < olen)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    Ctx *c;
+    st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    if (kc) {
+        CHIP_HIP(grow(c->in, kc));
+        CHIP_HIP(grow(c->out, kc));
+        std::vector<uint32_t> sel(k);
+        std::vector<uint64_t> slot_off(k);
+        for (uint32_t s = 0; s < k; ++s) {
+            sel[s] = idx[pos[s]];
+            slot_off[s] = (uint64_t)s * chunk_len;
+            CHIP_HIP(hipMemcpyAsync(static_cast<uint8_t *>(c->in.p) + slot_off[s], shares[pos[s]],
+                                    chunk_len, hipMemcpyHostToDevice, c->stream));
+        }
+        st = zfec_decode_device(k, m, static_cast<const uint8_t *>(c->in.p), 0, slot_off, sel, chunk_len,
+                                1, static_cast<uint8_t *>(c->out.p), 0, c->stream);
+        if (st != CHIP_OK) return st;
+        if (olen) CHIP_HIP(hipMemcpyAsync(out, c->out.p, olen, hipMemcpyDeviceToHost, c->stream));
+        CHIP_HIP(hipStreamSynchronize(c->stream));
+    }
+    *out_len = olen;
+    return CHIP_OK;
+}
+
+int chip_zfec_decode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t len, uint32_t padding,
+                     uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if (!valid_km(k, m)) return CHIP_ERR_ZFEC;
+    if ((!in && len) || !out_len) return CHIP_ERR_INVALID_ARG;
+    if (len % m != 0) return CHIP_ERR_UNEVEN_ZFEC_CHUNKS;  // decoding.rs:39-41
+    const uint64_t C = len / m;
+    std::vector<const uint8_t *> ptrs(m);
+    std::vector<uint32_t> idx(m);
+    for (uint32_t i = 0; i < m; ++i) { ptrs[i] = in + i * C; idx[i] = i; }  // decoding.rs:24-25
+    return chip_zfec_decode_shares(k, m, ptrs.data(), idx.data(), m, C, padding, out, out_cap, out_len);
+}
+
+int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
+                               uint64_t chunk_len, const uint32_t *idx, uint32_t nshares,
+                               uint64_t count, uint8_t *d_out, uint64_t out_stride, void *stream) {
+    if (!valid_km(k, m)) return CHIP_ERR_ZFEC;
+    if (!d_in || !d_out || !idx || (in_stride % 16) || (out_stride % 16) || (chunk_len % 16))
+        return CHIP_ERR_INVALID_ARG;
+    int st = ensure_device();
+    if (st != CHIP_OK) return st;
+    std::vector<uint32_t> pos;
+    st = select_shares(k, m, idx, nshares, &pos);
+    if (st != CHIP_OK) return st;
+    std::vector<uint32_t> sel(k);
+    std::vector<uint64_t> slot_off(k);
+    for (uint32_t s = 0; s < k; ++s) {
+        sel[s] = idx[pos[s]];
+        slot_off[s] = (uint64_t)sel[s] * chunk_len;
+    }
+    return zfec_decode_device(k, m, d_in, in_stride, slot_off, sel, chunk_len, count, d_out, out_stride,
+                              static_cast<hipStream_t>(stream));
+}
+
+// ---- bao ---------------------------------------------------------------
+
+int chip_bao_encode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                              uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash,
+                              void *d_scratch, void *stream) {
+    if ((!d_in && n) || !d_hash || !d_scratch) return CHIP_ERR_INVALID_ARG;
+    int st = ensure_device();
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(bao_encode_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_scratch,
+                            static_cast<hipStream_t>(stream)));
+    return CHIP_OK;
+}
+
+int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                              const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
+                              uint32_t *d_status, void *d_scratch, void *stream) {
+    if (!d_in || !d_hash || !d_status || !d_scratch || (!d_out && n)) return CHIP_ERR_INVALID_ARG;
+    int st = ensure_device();
+    if (st != CHIP_OK) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    CHIP_HIP(hipMemsetAsync(d_status, 0, count * sizeof(uint32_t), s));
+    CHIP_HIP(bao_decode_dev(d_in, in_stride, n, count, d_hash, d_out, out_stride, d_status, d_scratch, s));
+    return CHIP_OK;
+}
+
+// bao-encode `n` device bytes into c->out; hash to host
+static int bao_encode_ctx(Ctx *c, const uint8_t *d_in, uint64_t n, bool want_stream,
+                          uint8_t hash[32]) {
+    const uint64_t blen = bao_encoded_len(n);
+    if (want_stream) CHIP_HIP(grow(c->out, blen));
+    CHIP_HIP(grow(c->scratch, bao_scratch_len(n, 1)));
+    CHIP_HIP(grow(c->small, 64));
+    uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
+    CHIP_HIP(bao_encode_dev(d_in, 0, n, 1, want_stream ? static_cast<uint8_t *>(c->out.p) : nullptr, 0,
+                            d_hash, c->scratch.p, c->stream));
+    CHIP_HIP(hipMemcpyAsync(hash, d_hash, 32, hipMemcpyDeviceToHost, c->stream));
+    return CHIP_OK;
+}
+
+int chip_bao_encode(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len,
+                    uint8_t hash[CHIP_HASH_LEN]) {
+    if ((!in && n) || !hash || !out_len) return CHIP_ERR_INVALID_ARG;
+    const uint64_t blen = bao_encoded_len(n);
+    if (!out || out_cap < blen) return CHIP_ERR_BUFFER_TOO_SMALL;
+    Ctx *c;
+    int st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(grow(c->in, n));
+    if (n) CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+    st = bao_encode_ctx(c, static_cast<const uint8_t *>(c->in.p), n, true, hash);
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(hipMemcpyAsync(out, c->out.p, blen, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    *out_len = blen;
+    return CHIP_OK;
+}
+
+int chip_blake3(const uint8_t *in, uint64_t n, uint8_t hash[CHIP_HASH_LEN]) {
+    if ((!in && n) || !hash) return CHIP_ERR_INVALID_ARG;
+    Ctx *c;
+    int st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(grow(c->in, n));
+    if (n) CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+    st = bao_encode_ctx(c, static_cast<const uint8_t *>(c->in.p), n, false, hash);
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    return CHIP_OK;
+}
+
+// verify-decode a device-resident stream of `len` bytes; content -> dst (device)
+static int bao_decode_ctx(Ctx *c, const uint8_t *d_enc, uint64_t len, uint64_t n, const uint8_t *hash,
+                          uint8_t *d_dst) {
+    (void)len;
+    CHIP_HIP(grow(c->scratch, bao_scratch_len(n, 1)));
+    CHIP_HIP(grow(c->small, 64));
+    uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
+    uint32_t *d_status = reinterpret_cast<uint32_t *>(d_hash + 32);
+    CHIP_HIP(hipMemcpyAsync(d_hash, hash, 32, hipMemcpyHostToDevice, c->stream));
+    CHIP_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
+    CHIP_HIP(bao_decode_dev(d_enc, 0, n, 1, d_hash, d_dst, 0, d_status, c->scratch.p, c->stream));
+    uint32_t status = 0;
+    CHIP_HIP(hipMemcpyAsync(&status, d_status, 4, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    return status ? (int)status : CHIP_OK;
+}
+
+static int bao_header(const uint8_t *enc, uint64_t len, uint64_t *n) {
+    if (len < 8) return CHIP_ERR_BAO_TRUNCATED;
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v |= (uint64_t)enc[i] << (8 * i);
+    // a stream shorter than its header implies is truncated (also guards overflow)
+    if (v > len || bao_encoded_len(v) > len) return CHIP_ERR_BAO_TRUNCATED;
+    *n = v;
+    return CHIP_OK;
+}
+
+int chip_bao_decode(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t hash_len,
+                    uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if (!out_len || (!enc && len)) return CHIP_ERR_INVALID_ARG;
+    if (!hash || hash_len != CHIP_HASH_LEN) return CHIP_ERR_HASH_DECODE;  // utils.rs:38-45
+    uint64_t n;
+    int st = bao_header(enc, len, &n);
+    if (st != CHIP_OK) return st;
+    if (n && (!out || out_cap < n)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    Ctx *c;
+    st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    const uint64_t blen = bao_encoded_len(n);
+    CHIP_HIP(grow(c->in, blen));
+    CHIP_HIP(grow(c->out, n));
+    CHIP_HIP(hipMemcpyAsync(c->in.p, enc, blen, hipMemcpyHostToDevice, c->stream));
+    st = bao_decode_ctx(c, static_cast<const uint8_t *>(c->in.p), blen, n, hash,
+                        static_cast<uint8_t *>(c->out.p));
+    if (st != CHIP_OK) return st;
+    if (n) CHIP_HIP(hipMemcpyAsync(out, c->out.p, n, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    *out_len = n;
+    return CHIP_OK;
+}
+
+// ---- pipeline glue -------------------------------------------------------
+
+int chip_encode(uint8_t format, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                uint64_t *out_len, uint8_t hash[CHIP_HASH_LEN], chip_encode_info *info) {
+    if ((!in && n) || !out_len || !hash) return CHIP_ERR_INVALID_ARG;
+    if (format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY)) return CHIP_ERR_UNSUPPORTED_FORMAT;
+    chip_encode_info inf;
+    std::memset(&inf, 0, sizeof inf);
+    inf.input_len = (uint32_t)n;  // encoding.rs:87 (as u32)
+    const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
+    uint64_t cur_len = n;
+    if (zfec) {
+        uint32_t pad;
+        uint64_t C;
+        calc_pad(n, CHIP_FEC_K, &pad, &C);
+        inf.padding_len = pad;
+        inf.chunk_len = (uint32_t)C;
+        cur_len = (uint64_t)CHIP_FEC_M * C;
+        inf.bytes_ecc = (uint32_t)cur_len;                                           // encoding.rs:123
+        inf.verifiable_slice_count = (uint16_t)(inf.bytes_ecc / CHIP_SLICE_LEN);     // encoding.rs:124
+        if (inf.verifiable_slice_count % 8 != 0) return CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT;
+        inf.chunk_slice_count = inf.verifiable_slice_count / 8;                     // encoding.rs:130
+    }
+    const uint64_t final_len = bao ? bao_encoded_len(cur_len) : cur_len;
+    if (final_len && (!out || out_cap < final_len)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (!zfec && !bao) {
+        if (n) std::memcpy(out, in, n);
+        std::memset(hash, 0, 32);
+    } else {
+        Ctx *c;
+        int st = ctx_get(&c);
+        if (st != CHIP_OK) return st;
+        CHIP_HIP(grow(c->in, n));
+        if (n) CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+        const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
+        if (zfec && cur_len) {
+            CHIP_HIP(grow(c->mid, cur_len));
+            GfPlan p = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M));
+            GfLaunch L{d_cur, static_cast<uint8_t *>(c->mid.p), 0, 0, n, inf.chunk_len, 1};
+            CHIP_HIP(gf_apply(p, L, c->stream));
+            d_cur = static_cast<const uint8_t *>(c->mid.p);
+        }
+        if (bao) {  // encoding.rs:140-142: the zfec output stays on the device
+            st = bao_encode_ctx(c, d_cur, cur_len, true, hash);
+            if (st != CHIP_OK) return st;
+            CHIP_HIP(hipMemcpyAsync(out, c->out.p, final_len, hipMemcpyDeviceToHost, c->stream));
+            inf.bytes_verifiable = (uint32_t)final_len;
+        } else {
+            std::memset(hash, 0, 32);  // encoding.rs:145
+            if (final_len) CHIP_HIP(hipMemcpyAsync(out, d_cur, final_len, hipMemcpyDeviceToHost, c->stream));
+        }
+        CHIP_HIP(hipStreamSynchronize(c->stream));
+    }
+    inf.compression_factor = (float)inf.bytes_compressed / (float)inf.input_len;      // encoding.rs:150
+    inf.amplification_factor = (float)inf.bytes_verifiable / (float)inf.input_len;    // encoding.rs:151
+    inf.output_len = (uint32_t)final_len;
+    *out_len = final_len;
+    if (info) *info = inf;
+    return CHIP_OK;
+}
+
+int chip_decode(const uint8_t *hash, uint64_t hash_len, const uint8_t *in, uint64_t n, uint32_t padding,
+                uint8_t format, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if ((!in && n) || !out_len) return CHIP_ERR_INVALID_ARG;
+    if (format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY)) return CHIP_ERR_UNSUPPORTED_FORMAT;
+    const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
+    if (!zfec && !bao) {
+        if (n && (!out || out_cap < n)) return CHIP_ERR_BUFFER_TOO_SMALL;
+        if (n) std::memcpy(out, in, n);
+        *out_len = n;
+        return CHIP_OK;
+    }
+    uint64_t cur_len = n;
+    if (bao) {
+        if (!hash || hash_len != CHIP_HASH_LEN) return CHIP_ERR_HASH_DECODE;
+        int st = bao_header(in, n, &cur_len);
+        if (st != CHIP_OK) return st;
+    }
+    uint64_t C = 0, olen = cur_len;
+    if (zfec) {
+        if (cur_len % CHIP_FEC_M != 0) return CHIP_ERR_UNEVEN_ZFEC_CHUNKS;  // decoding.rs:39-41
+        C = cur_len / CHIP_FEC_M;
+        if (padding > CHIP_FEC_K * C) return CHIP_ERR_ZFEC;
+        if (C % 16) return CHIP_ERR_ZFEC;
+        olen = CHIP_FEC_K * C - padding;
+    }
+    if (olen && (!out || out_cap < olen)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    Ctx *c;
+    int st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    const uint64_t in_bytes = bao ? bao_encoded_len(cur_len) : n;
+    CHIP_HIP(grow(c->in, in_bytes));
+    if (in_bytes) CHIP_HIP(hipMemcpyAsync(c->in.p, in, in_bytes, hipMemcpyHostToDevice, c->stream));
+    const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
+    if (bao) {  // decoding.rs:89-93
+        CHIP_HIP(grow(c->mid, cur_len));
+        st = bao_decode_ctx(c, d_cur, in_bytes, cur_len, hash, static_cast<uint8_t *>(c->mid.p));
+        if (st != CHIP_OK) return st;
+        d_cur = static_cast<const uint8_t *>(c->mid.p);
+    }
+    if (zfec && C) {  // decoding.rs:95-99: shards by position, primaries present
+        CHIP_HIP(grow(c->out, CHIP_FEC_K * C));
+        std::vector<uint32_t> sel(CHIP_FEC_K);
+        std::vector<uint64_t> slot_off(CHIP_FEC_K);
+        for (uint32_t s = 0; s < CHIP_FEC_K; ++s) { sel[s] = s; slot_off[s] = s * C; }
+        st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_cur, 0, slot_off, sel, C, 1,
+                                static_cast<uint8_t *>(c->out.p), 0, c->stream);
+        if (st != CHIP_OK) return st;
+        d_cur = static_cast<const uint8_t *>(c->out.p);
+    }
+    if (olen) CHIP_HIP(hipMemcpyAsync(out, d_cur, olen, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    *out_len = olen;
+    return CHIP_OK;
+}
+
+}  // extern "C"

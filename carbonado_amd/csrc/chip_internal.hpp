@@ -1,0 +1,78 @@
+// chip_internal.hpp — shared declarations of libcarbonado_hip (gfx950).
+//
+// Layering:
+//   gf256.hpp            host GF(2^8) arithmetic: zfec matrices, inverses,
+//                        packed LDS tables (built once per (k, m, pattern))
+//   zfec_kernels.hip     K1/K2: GF(2^8) stripe matrix-apply (encode and
+//                        erasure decode are the same kernel)
+//   bao_kernels.hip      K3/K4/K5: BLAKE3 chunk CVs, parent levels, bao
+//                        pre-order layout, verify-decode
+//   chip_api.cpp         the C-ABI (include/carbonado_hip.h): host staging,
+//                        per-thread streams, error mapping, pipeline glue
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstddef>
+#include <vector>
+
+#include "../../include/carbonado_hip.h"
+
+namespace chip {
+
+constexpr uint64_t NO_OUT = ~0ull;
+constexpr int ZF_MAXK = 16;  // fast kernel: up to 16 input shards
+constexpr int ZF_MAXP = 8;   // fast kernel: up to 8 computed rows (2 dword groups)
+
+// One GF(2^8) "matrix apply" over stripes of `count` objects:
+//   out_row[p] = XOR_j coef[p][j] * in_row[j]    (computed rows)
+//   out_row    = in_row[j]                       (copy rows, copy_off[j])
+// Encode: in rows = the k data shards (zero beyond `valid`), copies = data
+// shards, computed rows = parity.  Decode: in rows = k surviving shares,
+// copies = surviving primaries, computed rows = the lost primaries.
+struct GfPlan {
+    uint32_t k = 0;                 // input rows
+    uint32_t np = 0;                // computed rows
+    uint64_t in_off[ZF_MAXK];       // offset of input row j inside an input object
+    uint64_t copy_off[ZF_MAXK];     // output offset for a copy of input row j, or NO_OUT
+    std::vector<uint64_t> comp_off; // output offset of each computed row (np)
+    std::vector<uint8_t> coef;      // np x k
+    // generic path (k > 16 or np > 8): full row lists
+    std::vector<uint64_t> g_in_off;   // k
+    std::vector<uint64_t> g_out_off;  // rows
+    std::vector<uint8_t> g_coef;      // rows x k (copies expressed as unit rows)
+};
+
+struct GfLaunch {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t in_stride, out_stride;
+    uint64_t valid;   // bytes of each input object that are data (rest reads as 0)
+    uint64_t C;       // shard length (multiple of 16)
+    uint64_t count;   // objects
+};
+
+// Enqueue the matrix apply.  Tables are cached device-side per plan key.
+// Plans with more than ZF_MAXP computed rows run in passes of ZF_MAXP rows
+// (copies ride on the first pass); k > ZF_MAXK uses the generic kernel.
+hipError_t gf_apply(const GfPlan &plan, const GfLaunch &L, hipStream_t stream);
+
+// ---- bao / BLAKE3 ------------------------------------------------------
+uint64_t bao_encoded_len(uint64_t n);
+uint64_t bao_scratch_len(uint64_t n, uint64_t count);
+// Encode `count` objects of n bytes; hashes to d_hash (32 B each).
+hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                          uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,
+                          hipStream_t stream);
+// Verify-decode; d_status[o] = 0 or CHIP_ERR_BAO_HASH_MISMATCH.
+hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                          const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
+                          uint32_t *d_status, void *d_scratch, hipStream_t stream);
+
+// ---- context ------------------------------------------------------------
+int ensure_device();                 // CHIP_OK or CHIP_ERR_NO_DEVICE
+void set_device_error(hipError_t e); // remember for chip_last_device_error
+int num_cus();
+
+}  // namespace chip

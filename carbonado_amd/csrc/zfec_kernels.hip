@@ -1,0 +1,416 @@
+// zfec_kernels.hip — K1/K2: GF(2^8) stripe matrix-apply for gfx950.
+//
+// Replaces the arithmetic of zfec-rs 0.1.0's Fec::encode / Fec::decode
+// (called at /root/reference/src/encoding.rs:61-62 and decoding.rs:28-29).
+// Encode: parity S_i[t] = XOR_j E[i][j] * D_j[t] for k <= i < m, with the
+// k data shards D_j = contiguous C-byte slices of the zero-padded input
+// (encoding.rs:53-55); the output is shard-major [S0|..|S(m-1)] (encoding.rs:70-78).
+// Decode with erasures is the same apply with rows of the inverted share matrix.
+//
+// Design (HBM-bound byte streaming; no MFMA: GF(2^8) products are table work):
+//  * One lane owns 16 byte-columns of every input shard: k coalesced
+//    global_load_dwordx4 per tile, m global_store_dwordx4 (nontemporal) per tile.
+//  * Packed-coefficient table in LDS: entry T_s[x] holds the products of byte x
+//    with shard s's coefficient in each computed row, packed 4 rows per dword
+//    (NG dwords).  One ds_read per input byte yields 4*NG parity contributions;
+//    a 4x4 byte transpose (v_perm_b32) turns column-packed sums into row streams.
+//  * Bank-conflict-free lookups: the table is replicated R = 32/K times; lane
+//    group G = (lane&31)/R walks the shards in the rotated order (j+G) mod K, so
+//    the 32 lanes of an LDS lane-group read 32 distinct banks for any data.
+//  * Persistent grid (occupancy x CUs), grid-stride over (object, 4 KiB column
+//    tile).  No inter-workgroup communication, no atomics.
+#include "chip_internal.hpp"
+#include "gf256.hpp"
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace chip {
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr int VEC = 16;
+constexpr int TILE = TPB * VEC;  // byte-columns per workgroup tile
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+struct ApplyArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t in_stride, out_stride, valid, C;
+    uint64_t tiles_per_obj, total_tiles;
+    const void *table;                 // [K][256] entries of NG dwords
+    uint64_t in_off[ZF_MAXK];
+    uint64_t copy_off[ZF_MAXK];
+    uint64_t par_off[ZF_MAXP];
+};
+
+__host__ __device__ constexpr int replicas_for(int k) {
+    int r = 1;
+    while (r * 2 * k <= 32) r *= 2;
+    return r;
+}
+
+template <int NG> struct Entry;
+template <> struct Entry<1> { using T = uint32_t; };
+template <> struct Entry<2> { using T = u32x2; };
+
+__device__ __forceinline__ u32x4 load16_masked(const uint8_t *base, uint64_t off, uint64_t valid) {
+    if (off + VEC <= valid) return *reinterpret_cast<const u32x4 *>(base + off);
+    u32x4 r = {0u, 0u, 0u, 0u};
+    if (off >= valid) return r;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < VEC; ++i)
+        if (off + i < valid) w[i >> 2] |= (uint32_t)base[off + i] << (8 * (i & 3));
+    r.x = w[0]; r.y = w[1]; r.z = w[2]; r.w = w[3];
+    return r;
+}
+
+__device__ __forceinline__ void store16_nt(uint8_t *p, u32x4 v) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+}
+
+// rows[q] = byte q of a0..a3 (4x4 byte transpose, 8 v_perm_b32)
+__device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                           uint32_t &r0, uint32_t &r1, uint32_t &r2, uint32_t &r3) {
+    const uint32_t u0 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);  // a0b0 a1b0 a0b1 a1b1
+    const uint32_t u1 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);  // a0b2 a1b2 a0b3 a1b3
+    const uint32_t w0 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
+    const uint32_t w1 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+    r0 = __builtin_amdgcn_perm(w0, u0, 0x05040100u);
+    r1 = __builtin_amdgcn_perm(w0, u0, 0x07060302u);
+    r2 = __builtin_amdgcn_perm(w1, u1, 0x05040100u);
+    r3 = __builtin_amdgcn_perm(w1, u1, 0x07060302u);
+}
+
+__device__ __forceinline__ uint32_t comp(const u32x4 &v, int d) {
+    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+}
+
+template <int K, int NG>
+__global__ __launch_bounds__(TPB) void gf_apply_kernel(ApplyArgs a) {
+    constexpr int R = replicas_for(K);
+    using E = typename Entry<NG>::T;
+    constexpr int W = 4 * NG;            // bytes per table entry
+    constexpr int ROWB = K * R * W;      // bytes per table row (one byte value x)
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+
+    // ---- table fill: lds[x][s][r] = T_s[x] ----
+    {
+        const E *tab = reinterpret_cast<const E *>(a.table);
+        E *dst = reinterpret_cast<E *>(lds);
+        for (int i = threadIdx.x; i < 256 * K * R; i += TPB) {
+            const int x = i / (K * R);
+            const int s = (i - x * (K * R)) / R;
+            dst[i] = tab[s * 256 + x];
+        }
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int r = lane % R;
+    const int grp = (lane & 31) / R;
+    uint32_t tb[K];
+    uint64_t ioff[K], coff[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const int s = (j + grp) % K;
+        tb[j] = (uint32_t)((s * R + r) * W);
+        ioff[j] = a.in_off[s];
+        coff[j] = a.copy_off[s];
+    }
+
+    for (uint64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+        const uint64_t obj = tile / a.tiles_per_obj;
+        const uint64_t col = (tile - obj * a.tiles_per_obj) * TILE + threadIdx.x * VEC;
+        if (col >= a.C) continue;
+        const uint8_t *ib = a.in + obj * a.in_stride;
+        uint8_t *ob = a.out + obj * a.out_stride;
+
+        u32x4 v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) v[j] = load16_masked(ib, ioff[j] + col, a.valid);
+
+        // acc[c] = packed computed-row bytes of byte-column c (16 columns)
+        E acc[16];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t x = comp(v[j], d);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t byte = (x >> (8 * b)) & 0xFFu;
+                    const E e = *reinterpret_cast<const E *>(lds + byte * ROWB + tb[j]);
+                    if (j == 0) acc[d * 4 + b] = e;
+                    else acc[d * 4 + b] ^= e;
+                }
+            }
+        }
+
+        // copies (data shards for encode, surviving primaries for decode)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (coff[j] != NO_OUT) store16_nt(ob + coff[j] + col, v[j]);
+
+        // computed rows: transpose column-packed sums into row streams
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            uint32_t rows[4][4];  // [q][d]
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                uint32_t c0, c1, c2, c3;
+                if constexpr (NG == 1) {
+                    c0 = acc[d * 4 + 0]; c1 = acc[d * 4 + 1]; c2 = acc[d * 4 + 2]; c3 = acc[d * 4 + 3];
+                } else {
+                    c0 = acc[d * 4 + 0][g]; c1 = acc[d * 4 + 1][g]; c2 = acc[d * 4 + 2][g]; c3 = acc[d * 4 + 3][g];
+                }
+                transpose4(c0, c1, c2, c3, rows[0][d], rows[1][d], rows[2][d], rows[3][d]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t po = a.par_off[g * 4 + q];
+                if (po == NO_OUT) continue;
+                u32x4 o = {rows[q][0], rows[q][1], rows[q][2], rows[q][3]};
+                store16_nt(ob + po + col, o);
+            }
+        }
+    }
+}
+
+// ---- generic fallback: any k (<= 256) and any number of output rows ----
+// One thread = 16 columns of one output row; full 64 KiB GF multiplication
+// table in LDS.  Used only outside the fast kernel's (K <= 16, rows <= 8) range.
+struct GenericArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t in_stride, out_stride, valid, C, count;
+    uint32_t k, rows;
+    const uint64_t *in_off;   // [k]
+    const uint64_t *out_off;  // [rows]
+    const uint8_t *coef;      // [rows][k]
+    const uint8_t *multab;    // [256][256]
+};
+
+__global__ __launch_bounds__(TPB) void gf_apply_generic_kernel(GenericArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt[];
+    for (int i = threadIdx.x; i < 65536 / 16; i += TPB)
+        reinterpret_cast<u32x4 *>(mt)[i] = reinterpret_cast<const u32x4 *>(a.multab)[i];
+    __syncthreads();
+    const uint64_t cols = (a.C + VEC - 1) / VEC;
+    const uint64_t total = a.count * a.rows * cols;
+    for (uint64_t w = (uint64_t)blockIdx.x * TPB + threadIdx.x; w < total;
+         w += (uint64_t)gridDim.x * TPB) {
+        const uint64_t cidx = w % cols;
+        const uint64_t rr = (w / cols) % a.rows;
+        const uint64_t obj = w / cols / a.rows;
+        const uint64_t col = cidx * VEC;
+        const uint8_t *ib = a.in + obj * a.in_stride;
+        uint32_t acc[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t j = 0; j < a.k; ++j) {
+            const uint8_t c = a.coef[rr * a.k + j];
+            if (!c) continue;
+            const u32x4 x = load16_masked(ib, a.in_off[j] + col, a.valid);
+            const uint8_t *row = mt + c * 256;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t xd = comp(x, d);
+                acc[d] ^= (uint32_t)row[xd & 0xFF] | (uint32_t)row[(xd >> 8) & 0xFF] << 8 |
+                          (uint32_t)row[(xd >> 16) & 0xFF] << 16 | (uint32_t)row[xd >> 24] << 24;
+            }
+        }
+        u32x4 o = {acc[0], acc[1], acc[2], acc[3]};
+        *reinterpret_cast<u32x4 *>(a.out + obj * a.out_stride + a.out_off[rr] + col) = o;
+    }
+}
+
+// ---- host side ----------------------------------------------------------
+typedef void (*KernelFn)(ApplyArgs);
+
+template <int K, int NG>
+KernelFn kernel_ptr() { return gf_apply_kernel<K, NG>; }
+
+struct KernelInfo {
+    KernelFn fn;
+    size_t lds;
+    int grid;
+};
+
+template <int K, int NG>
+KernelInfo make_info() {
+    constexpr int R = replicas_for(K);
+    KernelInfo ki;
+    ki.fn = kernel_ptr<K, NG>();
+    ki.lds = (size_t)256 * K * R * 4 * NG;
+    ki.grid = 0;
+    return ki;
+}
+
+bool lookup_fast(int k, int ng, KernelInfo &out) {
+#define CHIP_CASE(KK)                                                        \
+    case KK:                                                                 \
+        out = (ng == 1) ? make_info<KK, 1>() : make_info<KK, 2>();           \
+        return true;
+    switch (k) {
+        CHIP_CASE(1) CHIP_CASE(2) CHIP_CASE(3) CHIP_CASE(4) CHIP_CASE(5)
+        CHIP_CASE(6) CHIP_CASE(7) CHIP_CASE(8) CHIP_CASE(16)
+        default: return false;
+    }
+#undef CHIP_CASE
+}
+
+struct DevTable {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+std::mutex g_mu;
+std::map<std::vector<uint8_t>, DevTable> g_tables;  // key: k, ng, coef bytes
+std::map<std::pair<KernelFn, size_t>, int> g_grid;
+uint8_t *g_multab = nullptr;
+
+int grid_for(const KernelInfo &ki) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto key = std::make_pair(ki.fn, ki.lds);
+    auto it = g_grid.find(key);
+    if (it != g_grid.end()) return it->second;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(ki.fn),
+                                                     TPB, ki.lds) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    const int g = per_cu * num_cus();
+    g_grid[key] = g;
+    return g;
+}
+
+// Packed table for the fast kernel: entry [s][x] = NG dwords, byte (4g+q) of
+// dword g = coef[4g+q][s] * x.
+hipError_t device_table(const GfPlan &p, int ng, const void **out) {
+    std::vector<uint8_t> key;
+    key.push_back((uint8_t)p.k);
+    key.push_back((uint8_t)ng);
+    key.insert(key.end(), p.coef.begin(), p.coef.end());
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_tables.find(key);
+    if (it != g_tables.end()) { *out = it->second.ptr; return hipSuccess; }
+    const Gf256 &gf = Gf256::get();
+    std::vector<uint32_t> host((size_t)p.k * 256 * ng, 0u);
+    for (uint32_t s = 0; s < p.k; ++s)
+        for (int x = 0; x < 256; ++x)
+            for (uint32_t row = 0; row < p.np; ++row) {
+                const uint8_t prod = gf.mul(p.coef[row * p.k + s], (uint8_t)x);
+                host[((size_t)s * 256 + x) * ng + row / 4] |= (uint32_t)prod << (8 * (row % 4));
+            }
+    DevTable t;
+    t.bytes = host.size() * 4;
+    hipError_t e = hipMalloc(&t.ptr, t.bytes);
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(t.ptr, host.data(), t.bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(t.ptr); return e; }
+    g_tables[key] = t;
+    *out = t.ptr;
+    return hipSuccess;
+}
+
+hipError_t multab_device(const uint8_t **out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_multab) {
+        const Gf256 &gf = Gf256::get();
+        std::vector<uint8_t> h(65536);
+        for (int a = 0; a < 256; ++a)
+            for (int b = 0; b < 256; ++b) h[a * 256 + b] = gf.mul((uint8_t)a, (uint8_t)b);
+        hipError_t e = hipMalloc(&g_multab, 65536);
+        if (e != hipSuccess) return e;
+        e = hipMemcpy(g_multab, h.data(), 65536, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return e;
+    }
+    *out = g_multab;
+    return hipSuccess;
+}
+
+hipError_t apply_generic(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
+    const uint8_t *mt = nullptr;
+    hipError_t e = multab_device(&mt);
+    if (e != hipSuccess) return e;
+    const uint32_t rows = (uint32_t)p.g_out_off.size();
+    // small per-launch descriptor block: in_off, out_off, coef
+    const size_t b_in = p.k * 8, b_out = rows * 8, b_coef = (size_t)rows * p.k;
+    std::vector<uint8_t> blob(b_in + b_out + b_coef);
+    std::memcpy(blob.data(), p.g_in_off.data(), b_in);
+    std::memcpy(blob.data() + b_in, p.g_out_off.data(), b_out);
+    std::memcpy(blob.data() + b_in + b_out, p.g_coef.data(), b_coef);
+    void *d = nullptr;
+    e = hipMallocAsync(&d, blob.size(), stream);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(d, blob.data(), blob.size(), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    GenericArgs a;
+    a.in = L.in; a.out = L.out; a.in_stride = L.in_stride; a.out_stride = L.out_stride;
+    a.valid = L.valid; a.C = L.C; a.count = L.count; a.k = p.k; a.rows = rows;
+    a.in_off = reinterpret_cast<const uint64_t *>(d);
+    a.out_off = reinterpret_cast<const uint64_t *>(static_cast<uint8_t *>(d) + b_in);
+    a.coef = static_cast<const uint8_t *>(d) + b_in + b_out;
+    a.multab = mt;
+    const uint64_t work = L.count * rows * ((L.C + VEC - 1) / VEC);
+    uint64_t blocks = (work + TPB - 1) / TPB;
+    const uint64_t cap = (uint64_t)num_cus() * 2;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(gf_apply_generic_kernel, dim3((unsigned)blocks), dim3(TPB), 65536, stream, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // the memcpy above captured `blob` synchronously into the stream order;
+    // free the descriptor once the kernel has consumed it
+    return hipFreeAsync(d, stream);
+}
+
+hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
+                                uint32_t row0, uint32_t nrows, bool copies) {
+    const int ng = nrows > 4 ? 2 : 1;
+    KernelInfo ki;
+    if (!lookup_fast((int)p.k, ng, ki)) return hipErrorInvalidValue;
+    ApplyArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.in = L.in; a.out = L.out;
+    a.in_stride = L.in_stride; a.out_stride = L.out_stride;
+    a.valid = L.valid; a.C = L.C;
+    a.tiles_per_obj = (L.C + TILE - 1) / TILE;
+    a.total_tiles = a.tiles_per_obj * L.count;
+    for (int j = 0; j < ZF_MAXK; ++j) {
+        a.in_off[j] = j < (int)p.k ? p.in_off[j] : 0;
+        a.copy_off[j] = (copies && j < (int)p.k) ? p.copy_off[j] : NO_OUT;
+    }
+    for (uint32_t q = 0; q < (uint32_t)ZF_MAXP; ++q) a.par_off[q] = q < nrows ? p.comp_off[row0 + q] : NO_OUT;
+    GfPlan sub;
+    sub.k = p.k;
+    sub.np = nrows;
+    sub.coef.assign(p.coef.begin() + (size_t)row0 * p.k, p.coef.begin() + (size_t)(row0 + nrows) * p.k);
+    hipError_t e = device_table(sub, ng, &a.table);
+    if (e != hipSuccess) return e;
+    const int grid_cap = grid_for(ki);
+    const uint64_t grid = a.total_tiles < (uint64_t)grid_cap ? a.total_tiles : (uint64_t)grid_cap;
+    hipLaunchKernelGGL(ki.fn, dim3((unsigned)grid), dim3(TPB), ki.lds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
+    if (L.count == 0 || L.C == 0) return hipSuccess;
+    if (p.k > (uint32_t)ZF_MAXK) return apply_generic(p, L, stream);
+    if (p.np == 0) return gf_apply_pass(p, L, stream, 0, 0, true);
+    for (uint32_t row0 = 0; row0 < p.np; row0 += ZF_MAXP) {
+        const uint32_t nrows = p.np - row0 < (uint32_t)ZF_MAXP ? p.np - row0 : (uint32_t)ZF_MAXP;
+        hipError_t e = gf_apply_pass(p, L, stream, row0, nrows, row0 == 0);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace chip

@@ -1,0 +1,76 @@
+"""decoding (mirror of /root/reference/src/decoding.rs), hot-path stages on
+the MI355X through libcarbonado_hip."""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+from ._buf import as_u8, check, ptr
+from .constants import FEC_K, FEC_M, HASH_SIZE, Format
+from .error import HashDecodeError
+
+
+def zfec_chunks(chunks: Sequence, padding: int, indices: Sequence[int] | None = None,
+                k: int = FEC_K, m: int = FEC_M) -> bytes:
+    """decoding.rs:21-32.  With `indices=None` the shares are numbered by
+    position exactly as the reference does (decoding.rs:24-25); pass the true
+    share indices to decode after losing data shards."""
+    arrs = [as_u8(c) for c in chunks]
+    if not arrs:
+        from .error import ZfecError
+        raise ZfecError("no chunks")
+    C = arrs[0].size
+    if any(x.size != C for x in arrs):
+        from .error import ZfecError
+        raise ZfecError("chunks differ in length")
+    idx = list(range(len(arrs))) if indices is None else list(indices)
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * n)(*[x.ctypes.data if x.size else 0 for x in arrs])
+    cidx = (ctypes.c_uint32 * n)(*idx)
+    olen_max = k * C
+    out = np.empty(max(olen_max, 1), dtype=np.uint8)
+    olen = ctypes.c_uint64()
+    check(_lib.lib().chip_zfec_decode_shares(k, m, ptrs, cidx, n, C, padding, ptr(out), olen_max,
+                                             ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def zfec(input, padding: int, k: int = FEC_K, m: int = FEC_M) -> bytes:
+    """decoding.rs:34-51: m contiguous shards (len % m == 0 else UnevenZfecChunks)."""
+    a = as_u8(input)
+    cap = (a.size // m) * k if m else 0
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    olen = ctypes.c_uint64()
+    check(_lib.lib().chip_zfec_decode(k, m, ptr(a), a.size, padding, ptr(out), cap, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def bao(input, hash: bytes) -> bytes:
+    """decoding.rs:53-60: verify the whole stream against `hash`, return content."""
+    if len(hash) != HASH_SIZE:
+        raise HashDecodeError(HASH_SIZE, len(hash))
+    a = as_u8(input)
+    n = int.from_bytes(a[:8].tobytes(), "little") if a.size >= 8 else 0
+    cap = min(n, a.size)
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    h = as_u8(hash)
+    olen = ctypes.c_uint64()
+    check(_lib.lib().chip_bao_decode(ptr(a), a.size, ptr(h), h.size, ptr(out), cap, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def decode(secret_key: bytes, hash: bytes, input, padding: int, format: int) -> bytes:
+    """decoding.rs:80-114 `decode(secret_key, hash, input, padding, format)`."""
+    del secret_key  # used only by the ECIES stage (out of scope)
+    a = as_u8(input)
+    h = as_u8(hash)
+    fmt = Format(format)
+    cap = a.size
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    olen = ctypes.c_uint64()
+    check(_lib.lib().chip_decode(ptr(h), h.size, ptr(a), a.size, padding, int(fmt), ptr(out), cap,
+                                 ctypes.byref(olen)))
+    return out[: olen.value].tobytes()

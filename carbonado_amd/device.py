@@ -1,0 +1,68 @@
+"""Device-resident batch API over torch tensors (the throughput path).
+
+torch provides HBM allocations and the stream; every byte of work is done by
+the HIP kernels behind the C-ABI batch entry points.  All functions enqueue
+on torch's current stream and return without synchronising.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._buf import check
+from .constants import FEC_K, FEC_M
+
+
+def _stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def zfec_encode_batch(inp: torch.Tensor, n: int, out: torch.Tensor, k: int = FEC_K, m: int = FEC_M) -> None:
+    """inp: uint8 [count, in_stride] (first n bytes of each row are data);
+    out: uint8 [count, >= m*chunk_len]."""
+    assert inp.dtype == torch.uint8 and out.dtype == torch.uint8 and inp.is_cuda and out.is_cuda
+    assert inp.is_contiguous() and out.is_contiguous() and inp.shape[0] == out.shape[0]
+    count = inp.shape[0]
+    need = _lib.lib().chip_zfec_encoded_len(n, k, m)
+    assert out.shape[1] >= need and inp.shape[1] >= n
+    check(_lib.lib().chip_zfec_encode_batch_dev(k, m, _p(inp), inp.shape[1], n, count, _p(out), out.shape[1],
+                                                _stream()))
+
+
+def zfec_decode_batch(enc: torch.Tensor, chunk_len: int, indices, out: torch.Tensor,
+                      k: int = FEC_K, m: int = FEC_M) -> None:
+    """enc: uint8 [count, >= m*chunk_len] (shard i at i*chunk_len); `indices`
+    lists the surviving shares; out: uint8 [count, >= k*chunk_len]."""
+    assert enc.is_contiguous() and out.is_contiguous() and enc.shape[0] == out.shape[0]
+    idx = list(indices)
+    cidx = (ctypes.c_uint32 * len(idx))(*idx)
+    check(_lib.lib().chip_zfec_decode_batch_dev(k, m, _p(enc), enc.shape[1], chunk_len, cidx, len(idx),
+                                                enc.shape[0], _p(out), out.shape[1], _stream()))
+
+
+def bao_scratch(n: int, count: int, device=None) -> torch.Tensor:
+    size = _lib.lib().chip_bao_scratch_len(n, count)
+    return torch.empty(size, dtype=torch.uint8, device=device or "cuda")
+
+
+def bao_encode_batch(inp: torch.Tensor, n: int, out: torch.Tensor | None, hashes: torch.Tensor,
+                     scratch: torch.Tensor) -> None:
+    """out: uint8 [count, >= bao_len(n)] or None (hash only); hashes: uint8 [count, 32]."""
+    count = inp.shape[0]
+    check(_lib.lib().chip_bao_encode_batch_dev(
+        _p(inp), inp.shape[1], n, count, _p(out) if out is not None else ctypes.c_void_p(0),
+        out.shape[1] if out is not None else 0, _p(hashes), _p(scratch), _stream()))
+
+
+def bao_decode_batch(enc: torch.Tensor, n: int, hashes: torch.Tensor, out: torch.Tensor,
+                     status: torch.Tensor, scratch: torch.Tensor) -> None:
+    """status: int32/uint32 [count]; 0 = verified, 5 = hash mismatch."""
+    count = enc.shape[0]
+    check(_lib.lib().chip_bao_decode_batch_dev(_p(enc), enc.shape[1], n, count, _p(hashes), _p(out),
+                                               out.shape[1], _p(status), _p(scratch), _stream()))

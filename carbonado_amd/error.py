@@ -1,0 +1,107 @@
+"""CarbonadoError (mirror of /root/reference/src/error.rs, hot-path variants).
+
+Each C-ABI status code maps to the variant the reference would return for
+the same condition; `status_to_error` is the single place that mapping lives.
+"""
+from __future__ import annotations
+
+
+class CarbonadoError(Exception):
+    """error.rs:4 `pub enum CarbonadoError`."""
+
+    status: int = -1
+
+
+class UnevenZfecChunks(CarbonadoError):
+    """error.rs:61-63"""
+    status = 3
+
+    def __init__(self, msg="Input bytes must divide evenly over number of zfec chunks."):
+        super().__init__(msg)
+
+
+class HashDecodeError(CarbonadoError):
+    """error.rs:77-79 HashDecodeError(expected, got)"""
+    status = 4
+
+    def __init__(self, expected: int = 32, got: int = -1):
+        super().__init__(f"Hash must be {expected} bytes long, an input of {got} bytes was provided.")
+        self.expected, self.got = expected, got
+
+
+class BaoDecodeError(CarbonadoError):
+    """error.rs:45-47 BaoDecodeError(bao::decode::Error) — HashMismatch or Truncated."""
+    status = 5
+
+    def __init__(self, kind: str = "HashMismatch"):
+        super().__init__(f"bao decode error: {kind}")
+        self.kind = kind
+
+
+class ZfecError(CarbonadoError):
+    """error.rs:49-51 ZfecError(zfec_rs::Error)"""
+    status = 7
+
+
+class EncodeZfecPaddingError(CarbonadoError):
+    """error.rs:85-87"""
+    status = 8
+
+
+class EncodeInvalidChunkLength(CarbonadoError):
+    """error.rs:89-91"""
+    status = 9
+
+
+class InvalidVerifiableSliceCount(CarbonadoError):
+    """error.rs:93-95"""
+    status = 10
+
+
+class UnsupportedFormat(CarbonadoError):
+    """Ecies/Snappy format bits: host stages outside this hot path."""
+    status = 11
+
+
+class BufferTooSmall(CarbonadoError):
+    status = 2
+
+
+class InvalidArgument(CarbonadoError):
+    status = 1
+
+
+class DeviceError(CarbonadoError):
+    """New variant: HIP runtime failure or no gfx950 device (no CPU fallback)."""
+    status = 101
+
+
+def status_to_error(status: int, detail: str = "") -> CarbonadoError:
+    if status == 3:
+        return UnevenZfecChunks()
+    if status == 4:
+        return HashDecodeError(32, -1)
+    if status == 5:
+        return BaoDecodeError("HashMismatch")
+    if status == 6:
+        return BaoDecodeError("Truncated")
+    if status == 7:
+        return ZfecError("zfec error" + (f": {detail}" if detail else ""))
+    if status == 8:
+        return EncodeZfecPaddingError("zfec padding should always be zero")
+    if status == 9:
+        return EncodeInvalidChunkLength("chunk length should be as calculated")
+    if status == 10:
+        return InvalidVerifiableSliceCount("Verifiable slice count should be evenly divisible by 8.")
+    if status == 11:
+        return UnsupportedFormat("format bit handled by a host stage outside this path")
+    if status == 2:
+        return BufferTooSmall("output buffer too small")
+    if status == 1:
+        return InvalidArgument("invalid argument")
+    if status in (100, 101):
+        e = DeviceError(("no usable gfx950 device" if status == 100 else "HIP runtime error")
+                        + (f": {detail}" if detail else ""))
+        e.status = status
+        return e
+    return CarbonadoError(f"status {status}")

@@ -1,0 +1,202 @@
+/*
+ * carbonado_hip.h — C-ABI of libcarbonado_hip.so, the MI355X (gfx950) hot
+ * path of carbonado's encode()/decode(): zfec k-of-m Reed-Solomon erasure
+ * coding over GF(2^8) and bao/BLAKE3 verifiable-stream encoding.
+ *
+ * Drop-in boundary.  carbonado 0.6.0 routes its hot path through five
+ * crate-internal stage functions; each entry point
+ * below replaces exactly one of them (citations are /root/reference paths):
+ *
+ *   chip_zfec_encode        <- encoding::zfec        src/encoding.rs:46-81
+ *   chip_bao_encode         <- encoding::bao         src/encoding.rs:38-44
+ *   chip_zfec_decode        <- decoding::zfec        src/decoding.rs:34-51
+ *   chip_zfec_decode_shares <- decoding::zfec_chunks src/decoding.rs:21-32
+ *                              (with explicit share indices; see below)
+ *   chip_bao_decode         <- decoding::bao         src/decoding.rs:53-60
+ *
+ * plus the glue that calls them (for the Bao|Zfec format bits):
+ *   chip_encode             <- encoding::encode      src/encoding.rs:86-172
+ *   chip_decode             <- decoding::decode      src/decoding.rs:80-114
+ * and helpers:
+ *   chip_calc_padding_len   <- utils::calc_padding_len src/utils.rs:47-58
+ *
+ * Conventions
+ *   - Plain pointers and sizes, no torch/HIP types in signatures.  Streams are
+ *     passed as `void*` (a hipStream_t; NULL = the library's per-thread stream).
+ *   - Output buffers are caller-allocated (the Rust shim does
+ *     Vec::with_capacity + set_len).  Sizes are computable up front with the
+ *     *_len helpers.  A too-small buffer returns CHIP_ERR_BUFFER_TOO_SMALL.
+ *   - Every function returns a chip_status (0 = OK).  The mapping to
+ *     CarbonadoError (src/error.rs) is given per code.
+ *   - Host-pointer entry points are synchronous and thread-safe (one HIP
+ *     stream + grow-only device scratch per calling thread).  The *_dev batch
+ *     entry points take device pointers, enqueue on the given stream and
+ *     return without synchronising.
+ *   - There is no CPU fallback: with no usable gfx950 device every compute
+ *     entry point returns CHIP_ERR_NO_DEVICE.
+ */
+#ifndef CARBONADO_HIP_H
+#define CARBONADO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__) || defined(__clang__)
+#define CHIP_API __attribute__((visibility("default")))
+#else
+#define CHIP_API
+#endif
+
+#define CHIP_ABI_VERSION 1
+#define CHIP_HASH_LEN 32   /* bao::HASH_SIZE */
+#define CHIP_SLICE_LEN 1024 /* constants.rs:9 SLICE_LEN */
+#define CHIP_FEC_K 4        /* constants.rs:11 FEC_K */
+#define CHIP_FEC_M 8        /* constants.rs:13 FEC_M */
+
+/* constants.rs:49-56 (bitmask_enum, declaration order) */
+#define CHIP_FORMAT_ECIES 1u
+#define CHIP_FORMAT_SNAPPY 2u
+#define CHIP_FORMAT_BAO 4u
+#define CHIP_FORMAT_ZFEC 8u
+
+typedef enum chip_status {
+    CHIP_OK = 0,
+    CHIP_ERR_INVALID_ARG = 1,        /* null pointer / impossible size          */
+    CHIP_ERR_BUFFER_TOO_SMALL = 2,   /* caller buffer shorter than required     */
+    CHIP_ERR_UNEVEN_ZFEC_CHUNKS = 3, /* CarbonadoError::UnevenZfecChunks  error.rs:61-63 */
+    CHIP_ERR_HASH_DECODE = 4,        /* CarbonadoError::HashDecodeError   error.rs:77-79 */
+    CHIP_ERR_BAO_HASH_MISMATCH = 5,  /* CarbonadoError::BaoDecodeError(HashMismatch) error.rs:45-47 */
+    CHIP_ERR_BAO_TRUNCATED = 6,      /* CarbonadoError::BaoDecodeError(Truncated)    error.rs:45-47 */
+    CHIP_ERR_ZFEC = 7,               /* CarbonadoError::ZfecError          error.rs:49-51 */
+    CHIP_ERR_ENCODE_ZFEC_PADDING = 8,/* CarbonadoError::EncodeZfecPaddingError error.rs:85-87 */
+    CHIP_ERR_ENCODE_INVALID_CHUNK_LENGTH = 9, /* error.rs:89-91 */
+    CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT = 10, /* error.rs:93-95 */
+    CHIP_ERR_UNSUPPORTED_FORMAT = 11,/* Ecies/Snappy bits: host stages, not on this path */
+    CHIP_ERR_NO_DEVICE = 100,        /* new variant: no usable gfx950 device     */
+    CHIP_ERR_DEVICE = 101            /* new variant: HIP runtime error            */
+} chip_status;
+
+/* structs.rs:12-44 EncodeInfo, field for field (u32 / f32 / u16) */
+typedef struct chip_encode_info {
+    uint32_t input_len;
+    uint32_t output_len;
+    uint32_t bytes_compressed;
+    float compression_factor;
+    uint32_t bytes_encrypted;
+    uint32_t bytes_ecc;
+    uint32_t bytes_verifiable;
+    float amplification_factor;
+    uint32_t padding_len;
+    uint32_t chunk_len;
+    uint16_t verifiable_slice_count;
+    uint16_t chunk_slice_count;
+} chip_encode_info;
+
+/* ---- library ---------------------------------------------------------- */
+CHIP_API int chip_abi_version(void);
+CHIP_API const char *chip_strerror(int status);
+/* Initialise the HIP context on `device` (idempotent).  CHIP_ERR_NO_DEVICE if
+ * no gfx950 device is visible. */
+CHIP_API int chip_init(int device);
+/* Last HIP error string seen by this thread (for CHIP_ERR_DEVICE). */
+CHIP_API const char *chip_last_device_error(void);
+
+/* ---- size helpers (host only, no device needed) ----------------------- */
+/* utils.rs:47-58 with FEC_K generalised to k: target = ceil(n/(1024k))*1024k,
+ * padding = target - n, chunk_len = target / k (integer maths; the reference's
+ * f64 is exact for every length it can hold). */
+CHIP_API int chip_calc_padding_len(uint64_t input_len, uint32_t k, uint32_t *padding, uint32_t *chunk_len);
+/* m * chunk_len */
+CHIP_API uint64_t chip_zfec_encoded_len(uint64_t input_len, uint32_t k, uint32_t m);
+/* 8 + n + 64 * (max(1, ceil(n/1024)) - 1) */
+CHIP_API uint64_t chip_bao_encoded_len(uint64_t content_len);
+/* upper bound of chip_encode's output for an n-byte input (format-independent) */
+CHIP_API uint64_t chip_encode_max_len(uint64_t input_len);
+
+/* ---- stage functions (host buffers) ----------------------------------- */
+/* encoding::zfec (encoding.rs:48-81).  out receives m*chunk_len bytes laid out
+ * shard-major [S0|S1|...|S(m-1)]; S0..S(k-1) are the zero-padded input.
+ * The reference fixes (k, m) = (FEC_K, FEC_M) = (4, 8); other values expose
+ * the kernel layer (1 <= k <= m <= 256). */
+CHIP_API int chip_zfec_encode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t n, uint8_t *out,
+                     uint64_t out_cap, uint32_t *padding, uint32_t *chunk_len);
+
+/* decoding::zfec (decoding.rs:34-51): len % m != 0 -> CHIP_ERR_UNEVEN_ZFEC_CHUNKS;
+ * shards are indexed by position 0..m as the reference does (decoding.rs:24-25).
+ * out receives k*(len/m) - padding bytes. */
+CHIP_API int chip_zfec_decode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t len, uint32_t padding,
+                     uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* decoding::zfec_chunks (decoding.rs:21-32) with EXPLICIT share indices:
+ * shares[s] holds chunk_len bytes of share idx[s].  The reference numbers the
+ * surviving shares by position, which mislabels them once a data shard is
+ * lost; this entry point takes the true
+ * indices.  Primary shares are used where present, secondaries fill the gaps
+ * in the order given.  Fewer than k distinct shares -> CHIP_ERR_ZFEC. */
+CHIP_API int chip_zfec_decode_shares(uint32_t k, uint32_t m, const uint8_t *const *shares,
+                            const uint32_t *idx, uint32_t nshares, uint64_t chunk_len,
+                            uint32_t padding, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* encoding::bao (encoding.rs:38-44 -> bao::encode::encode): combined pre-order
+ * encoding (u64 LE length, 64-byte parents, 1 KiB chunks) and the root hash
+ * (== BLAKE3(in)). */
+CHIP_API int chip_bao_encode(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                    uint64_t *out_len, uint8_t hash[CHIP_HASH_LEN]);
+
+/* decoding::bao (decoding.rs:53-60): hash_len != 32 -> CHIP_ERR_HASH_DECODE
+ * (utils.rs:37-45); any node mismatch -> CHIP_ERR_BAO_HASH_MISMATCH; stream
+ * shorter than its header implies -> CHIP_ERR_BAO_TRUNCATED. */
+CHIP_API int chip_bao_decode(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t hash_len,
+                    uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* BLAKE3 of a host buffer, computed on the device (bao root hash). */
+CHIP_API int chip_blake3(const uint8_t *in, uint64_t n, uint8_t hash[CHIP_HASH_LEN]);
+
+/* ---- pipeline glue (host buffers) -------------------------------------- */
+/* encoding::encode (encoding.rs:86-172) for format bits Bao|Zfec; the zfec
+ * output stays device-resident for the bao stage.  Ecies/Snappy bits ->
+ * CHIP_ERR_UNSUPPORTED_FORMAT (host stages, out of this path's scope). */
+CHIP_API int chip_encode(uint8_t format, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                uint64_t *out_len, uint8_t hash[CHIP_HASH_LEN], chip_encode_info *info);
+/* decoding::decode (decoding.rs:80-114) for format bits Bao|Zfec. */
+CHIP_API int chip_decode(const uint8_t *hash, uint64_t hash_len, const uint8_t *in, uint64_t n,
+                uint32_t padding, uint8_t format, uint8_t *out, uint64_t out_cap,
+                uint64_t *out_len);
+
+/* ---- device-resident batch API (the throughput path) ------------------ */
+/* `count` objects of `n` bytes each; object o's input at d_in + o*in_stride
+ * (bytes beyond n inside the padded object read as zero, exactly as
+ * encoding.rs:53-55 pads), its m*chunk_len-byte output at d_out + o*out_stride.
+ * in_stride and out_stride must be multiples of 16. */
+CHIP_API int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
+                               uint64_t n, uint64_t count, uint8_t *d_out, uint64_t out_stride,
+                               void *stream);
+/* Erasure decode of `count` encoded objects (chunk_len-byte shards, shard i of
+ * object o at d_in + o*in_stride + i*chunk_len).  idx[0..nshares) names the
+ * shares that survive (same pattern for every object); the k*chunk_len data
+ * bytes of object o go to d_out + o*out_stride (caller truncates `padding`). */
+CHIP_API int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
+                               uint64_t chunk_len, const uint32_t *idx, uint32_t nshares,
+                               uint64_t count, uint8_t *d_out, uint64_t out_stride, void *stream);
+/* bao encode of `count` objects of n bytes: object o's stream (length
+ * chip_bao_encoded_len(n)) at d_out + o*out_stride, its hash at
+ * d_hash + 32*o.  d_scratch must hold chip_bao_scratch_len(n, count) bytes. */
+CHIP_API uint64_t chip_bao_scratch_len(uint64_t n, uint64_t count);
+CHIP_API int chip_bao_encode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                              uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash,
+                              void *d_scratch, void *stream);
+/* bao verify-decode of `count` streams whose content length is n (checked
+ * against each header): content of object o to d_out + o*out_stride; per
+ * object status (0 or a chip_status) to d_status[o] (uint32). */
+CHIP_API int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                              const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
+                              uint32_t *d_status, void *d_scratch, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CARBONADO_HIP_H */

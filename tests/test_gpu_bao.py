@@ -1,0 +1,106 @@
+"""GPU parity: BLAKE3 / bao kernels (K3/K4/K5) vs the CPU oracle."""
+import json
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 2049, 3073, 8192, 8193, 65 * 1024 + 7,
+         (1 << 20) + 3, 3 * (1 << 20) + 1024 * 5]
+
+
+def rnd(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+def test_blake3_published_vectors(gpu, golden_dir):
+    from carbonado_amd import encoding
+    kat = json.loads((golden_dir / "blake3_kat.json").read_text())
+    for s, h in kat["strings"].items():
+        assert encoding.blake3(s.encode()).hex() == h
+    for n, h in kat["pattern_251"].items():
+        assert encoding.blake3(bytes(i % 251 for i in range(int(n)))).hex() == h, n
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_bao_encode_matches_oracle(gpu, n):
+    from carbonado_amd import encoding
+    d = rnd(n, n)
+    enc, h = encoding.bao(d)
+    oe, oh = O.bao_encode(d)
+    assert h == oh
+    assert enc == oe
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_bao_decode_roundtrip(gpu, n):
+    from carbonado_amd import decoding
+    d = rnd(n, n + 1)
+    enc, h = O.bao_encode(d)
+    assert decoding.bao(enc, h) == d
+
+
+def test_bao_decode_rejects_tampering(gpu):
+    from carbonado_amd import decoding
+    from carbonado_amd.error import BaoDecodeError
+    d = rnd(10_000, 9)
+    enc, h = O.bao_encode(d)
+    # header, root parent, inner parent, first/last chunk bytes
+    for pos in [0, 3, 8, 40, 72 + 10, 200, 4000, len(enc) - 1]:
+        t = bytearray(enc)
+        t[pos] ^= 0x40
+        with pytest.raises(BaoDecodeError):
+            decoding.bao(bytes(t), h)
+    with pytest.raises(BaoDecodeError) as ei:
+        decoding.bao(enc[:-1], h)
+    assert ei.value.kind == "Truncated"
+    bad = bytearray(h)
+    bad[0] ^= 1
+    with pytest.raises(BaoDecodeError):
+        decoding.bao(enc, bytes(bad))
+
+
+def test_bao_single_chunk_root_mismatch(gpu):
+    from carbonado_amd import decoding
+    from carbonado_amd.error import BaoDecodeError
+    enc, h = O.bao_encode(b"hello world")
+    t = bytearray(enc)
+    t[9] ^= 1
+    with pytest.raises(BaoDecodeError):
+        decoding.bao(bytes(t), h)
+
+
+def test_batch_bao_full_size(gpu):
+    """32 MiB streams (the cfg2 zfec output size, N = 32768 chunks) and a
+    non-power-of-two chunk count (cfg4's 32776)."""
+    import torch
+    from carbonado_amd import device
+    for n, count in [(32 << 20, 3), (32776 * 1024, 2)]:
+        gen = torch.Generator(device="cuda").manual_seed(n % 1000)
+        inp = torch.randint(0, 256, (count, n), dtype=torch.uint8, device="cuda", generator=gen)
+        blen = O.lib().orc_bao_encoded_len(n)
+        out = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+        hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+        scratch = device.bao_scratch(n, count)
+        device.bao_encode_batch(inp, n, out, hashes, scratch)
+        torch.cuda.synchronize()
+        d0 = inp[0].cpu().numpy().tobytes()
+        oe, oh = O.bao_encode(d0)
+        assert hashes[0].cpu().numpy().tobytes() == oh
+        assert out[0, :blen].cpu().numpy().tobytes() == oe
+        for o in range(1, count):
+            assert hashes[o].cpu().numpy().tobytes() == O.blake3(inp[o].cpu().numpy().tobytes())
+        # verify-decode the whole batch, then corrupt one object
+        dec = torch.empty((count, n), dtype=torch.uint8, device="cuda")
+        status = torch.empty(count, dtype=torch.int32, device="cuda")
+        device.bao_decode_batch(out, n, hashes, dec, status, scratch)
+        torch.cuda.synchronize()
+        assert torch.equal(dec, inp) and int(status.abs().sum()) == 0
+        out[count - 1, 12345] ^= 1
+        device.bao_decode_batch(out, n, hashes, dec, status, scratch)
+        torch.cuda.synchronize()
+        st = status.cpu().tolist()
+        assert st[:-1] == [0] * (count - 1) and st[-1] == 5

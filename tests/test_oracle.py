@@ -1,0 +1,156 @@
+"""CPU tests: pin the oracle (test infrastructure) before trusting it.
+
+* BLAKE3 restatement vs published known-answer vectors;
+* C oracle vs the independent Python oracle (different algorithms);
+* zfec invariants (systematic identity, MDS over every k-subset, decode of
+  every erasure pattern) — zfec-rs itself is absent, so this is the pinning
+  we have (DESIGN.md "parity unpinned" note);
+* bao layout: size formula, round trip, tamper detection;
+* the reference's own samples at levels 4 / 8 / 12 against golden.json
+  (the reference's codec/apocalypse tests only pin round trips).
+"""
+import itertools
+import json
+import os
+import random
+
+import pytest
+
+from oracle import oracle as O
+from oracle import pyoracle as P
+
+
+@pytest.fixture(scope="module")
+def kat(golden_dir):
+    return json.loads((golden_dir / "blake3_kat.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    return json.loads((golden_dir / "golden.json").read_text())
+
+
+def test_blake3_published_strings(kat):
+    for s, h in kat["strings"].items():
+        assert O.blake3(s.encode()).hex() == h
+
+
+def test_blake3_published_pattern_vectors(kat):
+    for n, h in kat["pattern_251"].items():
+        data = bytes(i % 251 for i in range(int(n)))
+        assert O.blake3(data).hex() == h, n
+
+
+def test_python_oracle_blake3_matches_kat(kat):
+    for n in ["0", "1", "1024", "1025", "2049", "8193"]:
+        data = bytes(i % 251 for i in range(int(n)))
+        assert P.blake3(data).hex() == kat["pattern_251"][n]
+
+
+@pytest.mark.parametrize("n", [0, 1, 64, 1023, 1024, 1025, 2047, 2048, 2049, 4097, 7000, 16385])
+def test_bao_c_vs_python(n):
+    d = random.Random(n).randbytes(n)
+    e1, h1 = O.bao_encode(d)
+    e2, h2 = P.bao_encode(d)
+    assert e1 == e2 and h1 == h2
+    assert h1 == O.blake3(d)  # bao hash == BLAKE3(content)
+    chunks = max(1, -(-n // 1024))
+    assert len(e1) == 8 + n + 64 * (chunks - 1)
+    assert O.bao_decode(e1, h1) == d
+
+
+def test_bao_decode_detects_tampering():
+    d = random.Random(7).randbytes(5000)
+    e, h = O.bao_encode(d)
+    for pos in [0, 7, 8, 40, 71, 72, 100, len(e) - 1]:
+        t = bytearray(e)
+        t[pos] ^= 0x40
+        with pytest.raises(O.OracleError):
+            O.bao_decode(bytes(t), h)
+    with pytest.raises(O.OracleError) as ei:
+        O.bao_decode(e[:-1], h)
+    assert ei.value.status == 6  # truncated
+    with pytest.raises(O.OracleError) as ei:
+        O.bao_decode(e, h[:31])
+    assert ei.value.status == 4  # HashDecodeError
+
+
+def test_enc_matrix_against_fec_c_route(golden):
+    for key, rows in golden["enc_matrix"].items():
+        k, m = map(int, key.split("of"))
+        assert [bytes(r).hex() for r in O.enc_matrix(k, m).tolist()] == rows
+        assert P.enc_matrix(k, m) == [list(bytes.fromhex(r)) for r in rows]
+
+
+def test_enc_matrix_survey_rows():
+    # SURVEY.md section 8a (a3), derived from the fec.c construction
+    E = O.enc_matrix(4, 8)
+    assert [bytes(r).hex() for r in E[4:].tolist()] == ["7740380e", "c7a70d6c", "53026f3f", "f17b8308"]
+
+
+@pytest.mark.parametrize("k,m", [(4, 8), (8, 16), (3, 5), (2, 4)])
+def test_zfec_mds_every_subset_decodes(k, m):
+    d = random.Random(k * 100 + m).randbytes(1024 * k * 2 - 77)
+    z, pad, C = O.zfec_encode(d, k, m)
+    shards = [z[i * C:(i + 1) * C] for i in range(m)]
+    assert b"".join(shards[:k])[: len(d)] == d  # systematic
+    subsets = list(itertools.combinations(range(m), k))
+    if len(subsets) > 80:
+        subsets = random.Random(1).sample(subsets, 80)
+    for sub in subsets:
+        got = O.zfec_decode_shares([shards[i] for i in sub], list(sub), pad, k, m)
+        assert got == d, sub
+
+
+def test_calc_padding_len_matches_reference_f64():
+    # utils.rs:50-58 in f64, restated in integers
+    import math
+    for n in [0, 1, 1023, 1024, 4095, 4096, 4097, 10240, 616565, 16 << 20, (16 << 20) + 1]:
+        target = math.ceil(n / 4096.0) * 4096.0
+        assert O.calc_padding_len(n) == (int(target - n), int(target / 4))
+
+
+def test_samples_golden(golden, golden_dir):
+    for name, entry in golden["samples"].items():
+        data = (golden_dir / "samples" / name).read_bytes()
+        assert len(data) == entry["input_len"]
+        for level in (4, 8, 12):
+            g = entry[f"level{level}"]
+            enc, h, info = O.encode(data, level)
+            assert len(enc) == g["output_len"]
+            assert O.blake3(enc).hex() == g["output_blake3"]
+            assert h.hex() == g["hash"]
+            for k, v in g["info"].items():
+                assert info[k] == pytest.approx(v, rel=1e-6), (name, level, k)
+            # reference tests/codec.rs:84-101 — round trip
+            assert O.decode(h, enc, info["padding_len"], level) == data
+
+
+def test_survey_appendix_b_sizes(golden):
+    s = golden["samples"]
+    assert s["contract.rgbc"]["level12"]["info"]["padding_len"] == 2853
+    assert s["contract.rgbc"]["level12"]["output_len"] == 8648
+    assert s["content.png"]["level12"]["info"]["chunk_len"] == 154624
+    assert s["content.png"]["level12"]["output_len"] == 1314248
+    assert s["code.tar"]["level12"]["output_len"] == 26056
+
+
+def test_generated_vectors(golden):
+    for v in golden["generated_vectors"]:
+        d = O.fill_object(v["seed"], 0, v["n"]).tobytes()
+        z, pad, C = O.zfec_encode(d)
+        assert (pad, C) == (v["padding"], v["chunk_len"])
+        assert O.blake3(z).hex() == v["zfec_blake3"]
+        b, h = O.bao_encode(z)
+        assert h.hex() == v["bao_hash"] and len(b) == v["bao_len"]
+
+
+def test_level8_scrub_style_recovery():
+    """reference tests/apocalypse.rs flips a bit and recovers through zfec;
+    restated at the oracle level with explicit share indices."""
+    d = (os.urandom(3000))
+    z, pad, C = O.zfec_encode(d)
+    shards = [z[i * C:(i + 1) * C] for i in range(8)]
+    # lose data shard 0 and 1 (the case the reference mislabels)
+    keep = [2, 3, 4, 5, 6, 7]
+    assert O.zfec_decode_shares([shards[i] for i in keep], keep, pad) == d
