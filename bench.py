@@ -48,8 +48,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (profiles/*.json) with measured HBM bytes per launch")
+    ap.add_argument("--traffic-json", default="auto",
+                    help="PMC summary (profiles/*_pmc.json, tools/pmc_summary.py) with the measured HBM "
+                         "bytes per launch of this kernel; 'auto' = newest matching file, 'none' = null")
     return ap.parse_args()
 
 
@@ -78,6 +79,24 @@ def fill_random(t: torch.Tensor, seed: int) -> None:
     for off in range(0, flat.numel(), slab):
         n = min(slab, flat.numel() - off)
         flat[off:off + n].copy_(torch.randint(0, 256, (n,), dtype=torch.uint8, device=t.device, generator=g))
+
+
+def measured_traffic(spec: str, kernel_sym: str, alg_bytes: int):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary of the same
+    kernel and workload (profiles/<tag>_pmc.json), else None."""
+    if spec == "none":
+        return None
+    files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=lambda p: p.stat().st_mtime) if spec == "auto" \
+        else [Path(spec)]
+    for f in reversed(files):
+        try:
+            tj = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        hb = tj.get("hbm_bytes_per_launch")
+        if hb and kernel_sym in (tj.get("kernel") or "") and abs(hb - alg_bytes) < 0.25 * alg_bytes:
+            return round(hb), str(f.relative_to(ROOT))
+    return None, None
 
 
 def cpu_baseline(args, n: int, sample_obj: bytes | None):
@@ -128,6 +147,7 @@ def main():
         step = lambda: device.zfec_encode_batch(inp, n, out, k, m)  # noqa: E731
         alg_bytes = count * (n + m * C)  # read input + write all m shards
         kernel = f"gf_apply_kernel<{k},{(m - k + 3) // 4}>"
+        kernel_sym = f"gf_apply_kernel<{k}, {(m - k + 3) // 4},"
         unit_bytes = n
     elif args.mode == "decode":
         enc = torch.empty((count, m * C), dtype=torch.uint8, device=dev)
@@ -138,6 +158,7 @@ def main():
         step = lambda: device.zfec_decode_batch(enc, C, keep, out, k, m)  # noqa: E731
         alg_bytes = count * (2 * k * C)  # read k shares + write k data shards
         kernel = f"gf_apply_kernel<{k},1> (decode, erased {sorted(erased)})"
+        kernel_sym = f"gf_apply_kernel<{k}, 1,"
         unit_bytes = n
     else:
         blen = L.chip_bao_encoded_len(n)
@@ -147,6 +168,7 @@ def main():
         step = lambda: device.bao_encode_batch(inp, n, out, hashes, scratch)  # noqa: E731
         alg_bytes = count * (n + blen)
         kernel = "bao_chunk_kernel<0> + bao_parent_kernel<0> levels"
+        kernel_sym = "bao_chunk_kernel"
         unit_bytes = n
     torch.cuda.synchronize()
 
@@ -190,10 +212,7 @@ def main():
         value = total_units / max_elapsed / 2**30
         avg_ms = sum(launch_ms) / len(launch_ms)
         achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-        traffic = None
-        if args.traffic_json and Path(args.traffic_json).exists():
-            tj = json.loads(Path(args.traffic_json).read_text())
-            traffic = tj.get("hbm_bytes_per_launch")
+        traffic, traffic_src = measured_traffic(args.traffic_json, kernel_sym, alg_bytes)
         res = {
             "metric": METRIC if args.mode == "encode" and (k, m) == (4, 8) else
             f"GiB/s device-resident {args.mode} ({k}-of-{m}), {args.object_mib:g} MiB objects",
@@ -215,6 +234,7 @@ def main():
                        "parallelism": f"objects partitioned over {world} rank(s), no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": kernel, "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": round(avg_ms, 4), "min_launch_ms": round(min(launch_ms), 4)},
             "verified_object0": verified,

@@ -1,0 +1,233 @@
+// zfec_device.hpp — device code of K1/K2 (GF(2^8) stripe matrix-apply),
+// shared by the product (zfec_kernels.hip) and tools/zfec_tune.hip.
+// See zfec_kernels.hip for the design notes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "chip_internal.hpp"
+
+namespace chip {
+namespace zf {
+
+constexpr int TPB = 256;
+constexpr int VEC = 16;
+constexpr int TILE = TPB * VEC;  // byte-columns per workgroup tile
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+struct ApplyArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t in_stride, out_stride, valid, C;
+    uint64_t tiles_per_obj, total_tiles, count;
+    uint64_t chunk;                    // MAP 3: tiles per XCD-grouped run (>= 1)
+    const void *table;                 // [K][256] entries of NG dwords
+    uint64_t in_off[ZF_MAXK];
+    uint64_t copy_off[ZF_MAXK];
+    uint64_t par_off[ZF_MAXP];
+};
+
+__host__ __device__ constexpr int replicas_for(int k) {
+    int r = 1;
+    while (r * 2 * k <= 32) r *= 2;
+    return r;
+}
+
+template <int NG> struct Entry;
+template <> struct Entry<1> { using T = uint32_t; };
+template <> struct Entry<2> { using T = u32x2; };
+
+__device__ __forceinline__ u32x4 load16_masked(const uint8_t *base, uint64_t off, uint64_t valid) {
+    if (off + VEC <= valid) return *reinterpret_cast<const u32x4 *>(base + off);
+    u32x4 r = {0u, 0u, 0u, 0u};
+    if (off >= valid) return r;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < VEC; ++i)
+        if (off + i < valid) w[i >> 2] |= (uint32_t)base[off + i] << (8 * (i & 3));
+    r.x = w[0]; r.y = w[1]; r.z = w[2]; r.w = w[3];
+    return r;
+}
+
+template <bool NT>
+__device__ __forceinline__ void store16(uint8_t *p, u32x4 v) {
+    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    else *reinterpret_cast<u32x4 *>(p) = v;
+}
+
+// rows[q] = byte q of a0..a3 (4x4 byte transpose, 8 v_perm_b32)
+__device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                           uint32_t &r0, uint32_t &r1, uint32_t &r2, uint32_t &r3) {
+    const uint32_t u0 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);  // a0b0 a1b0 a0b1 a1b1
+    const uint32_t u1 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);  // a0b2 a1b2 a0b3 a1b3
+    const uint32_t w0 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
+    const uint32_t w1 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+    r0 = __builtin_amdgcn_perm(w0, u0, 0x05040100u);
+    r1 = __builtin_amdgcn_perm(w0, u0, 0x07060302u);
+    r2 = __builtin_amdgcn_perm(w1, u1, 0x05040100u);
+    r3 = __builtin_amdgcn_perm(w1, u1, 0x07060302u);
+}
+
+__device__ __forceinline__ uint32_t comp(const u32x4 &v, int d) {
+    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+}
+
+// Tile schedule (MAP), per workgroup b of G:
+//   0  grid-stride: tile = b, b + G, b + 2G, ...
+//   1  XCD-grouped grid-stride: the G/8 workgroups that share an XCD
+//      (b % 8, observed round-robin dispatch; speed only, never correctness)
+//      take G/8 consecutive tiles each round
+//   2  one contiguous range per workgroup
+//   3  XCD-grouped chunks: runs of CH consecutive tiles dealt as in 1, each
+//      run walked in order by one workgroup (long sequential streams per
+//      shard; tools/write_probe: HBM writes 5.0 -> 5.9 TB/s)
+// Falls back to 0 when G is not a multiple of 8.
+template <int MAP>
+struct TileIter {
+    uint64_t T, c, t_in, end, stride, base, CH;
+    int mode;
+    __device__ TileIter(uint64_t total, uint64_t ch) : T(total), t_in(0), CH(ch < 1 ? 1 : ch) {
+        const uint64_t G = gridDim.x, b = blockIdx.x;
+        mode = ((MAP == 1 || MAP == 3) && (G & 7)) ? 0 : MAP;
+        if (mode == 2) {
+            const uint64_t chunk = (T + G - 1) / G;
+            c = b * chunk;
+            end = c + chunk < T ? c + chunk : T;
+            stride = 1;
+            base = 0;
+        } else if (mode == 1 || mode == 3) {
+            base = (b % 8) * (G / 8) + b / 8;
+            c = base;
+            stride = G;
+            end = T;
+        } else {
+            c = b;
+            stride = G;
+            end = T;
+            base = 0;
+        }
+    }
+    __device__ bool next(uint64_t &t) {
+        if (mode == 3) {
+            if (t_in == CH) { c += stride; t_in = 0; }
+            t = c * CH + t_in;
+            ++t_in;
+            return t < T;
+        }
+        t = c;
+        c += stride;
+        return t < end;
+    }
+};
+
+template <int K, int NG, int U, int MAP, bool NT>
+__global__ __launch_bounds__(TPB) void gf_apply_kernel(ApplyArgs a) {
+    constexpr int R = replicas_for(K);
+    using E = typename Entry<NG>::T;
+    constexpr int W = 4 * NG;            // bytes per table entry
+    constexpr int ROWB = K * R * W;      // bytes per table row (one byte value x)
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+
+    // ---- table fill: lds[x][s][r] = T_s[x] ----
+    {
+        const E *tab = reinterpret_cast<const E *>(a.table);
+        E *dst = reinterpret_cast<E *>(lds);
+        for (int i = threadIdx.x; i < 256 * K * R; i += TPB) {
+            const int x = i / (K * R);
+            const int s = (i - x * (K * R)) / R;
+            dst[i] = tab[s * 256 + x];
+        }
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int r = lane % R;
+    const int grp = (lane & 31) / R;
+    uint32_t tb[K];
+    uint64_t ioff[K], coff[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const int s = (j + grp) % K;
+        tb[j] = (uint32_t)((s * R + r) * W);
+        ioff[j] = a.in_off[s];
+        coff[j] = a.copy_off[s];
+    }
+
+    // super-tiles of U adjacent column tiles of one object
+    const uint64_t spo = (a.tiles_per_obj + U - 1) / U;
+    TileIter<MAP> iter(spo * a.count, a.chunk);
+    uint64_t st;
+    while (iter.next(st)) {
+        const uint64_t obj = st / spo;
+        const uint64_t col0 = (st - obj * spo) * (uint64_t)(U * TILE) + threadIdx.x * VEC;
+        const uint8_t *ib = a.in + obj * a.in_stride;
+        uint8_t *ob = a.out + obj * a.out_stride;
+
+        u32x4 v[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint64_t col = col0 + (uint64_t)u * TILE;
+                v[u][j] = col < a.C ? load16_masked(ib, ioff[j] + col, a.valid) : u32x4{0u, 0u, 0u, 0u};
+            }
+
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t col = col0 + (uint64_t)u * TILE;
+            if (col >= a.C) continue;
+            // acc[c] = packed computed-row bytes of byte-column c (16 columns)
+            E acc[16];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t x = comp(v[u][j], d);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const uint32_t byte = (x >> (8 * b)) & 0xFFu;
+                        const E e = *reinterpret_cast<const E *>(lds + byte * ROWB + tb[j]);
+                        if (j == 0) acc[d * 4 + b] = e;
+                        else acc[d * 4 + b] ^= e;
+                    }
+                }
+            }
+
+            // copies (data shards for encode, surviving primaries for decode)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (coff[j] != NO_OUT) store16<NT>(ob + coff[j] + col, v[u][j]);
+
+            // computed rows: transpose column-packed sums into row streams
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                uint32_t rows[4][4];  // [q][d]
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    uint32_t c0, c1, c2, c3;
+                    if constexpr (NG == 1) {
+                        c0 = acc[d * 4 + 0]; c1 = acc[d * 4 + 1]; c2 = acc[d * 4 + 2]; c3 = acc[d * 4 + 3];
+                    } else {
+                        c0 = acc[d * 4 + 0][g]; c1 = acc[d * 4 + 1][g];
+                        c2 = acc[d * 4 + 2][g]; c3 = acc[d * 4 + 3][g];
+                    }
+                    transpose4(c0, c1, c2, c3, rows[0][d], rows[1][d], rows[2][d], rows[3][d]);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint64_t po = a.par_off[g * 4 + q];
+                    if (po == NO_OUT) continue;
+                    u32x4 o = {rows[q][0], rows[q][1], rows[q][2], rows[q][3]};
+                    store16<NT>(ob + po + col, o);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace zf
+}  // namespace chip

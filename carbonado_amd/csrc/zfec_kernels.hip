@@ -21,6 +21,7 @@
 //    tile).  No inter-workgroup communication, no atomics.
 #include "chip_internal.hpp"
 #include "gf256.hpp"
+#include "zfec_device.hpp"
 
 #include <cstring>
 #include <map>
@@ -31,157 +32,7 @@ namespace chip {
 
 namespace {
 
-constexpr int TPB = 256;
-constexpr int VEC = 16;
-constexpr int TILE = TPB * VEC;  // byte-columns per workgroup tile
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-struct ApplyArgs {
-    const uint8_t *in;
-    uint8_t *out;
-    uint64_t in_stride, out_stride, valid, C;
-    uint64_t tiles_per_obj, total_tiles;
-    const void *table;                 // [K][256] entries of NG dwords
-    uint64_t in_off[ZF_MAXK];
-    uint64_t copy_off[ZF_MAXK];
-    uint64_t par_off[ZF_MAXP];
-};
-
-__host__ __device__ constexpr int replicas_for(int k) {
-    int r = 1;
-    while (r * 2 * k <= 32) r *= 2;
-    return r;
-}
-
-template <int NG> struct Entry;
-template <> struct Entry<1> { using T = uint32_t; };
-template <> struct Entry<2> { using T = u32x2; };
-
-__device__ __forceinline__ u32x4 load16_masked(const uint8_t *base, uint64_t off, uint64_t valid) {
-    if (off + VEC <= valid) return *reinterpret_cast<const u32x4 *>(base + off);
-    u32x4 r = {0u, 0u, 0u, 0u};
-    if (off >= valid) return r;
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int i = 0; i < VEC; ++i)
-        if (off + i < valid) w[i >> 2] |= (uint32_t)base[off + i] << (8 * (i & 3));
-    r.x = w[0]; r.y = w[1]; r.z = w[2]; r.w = w[3];
-    return r;
-}
-
-__device__ __forceinline__ void store16_nt(uint8_t *p, u32x4 v) {
-    __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
-}
-
-// rows[q] = byte q of a0..a3 (4x4 byte transpose, 8 v_perm_b32)
-__device__ __forceinline__ void transpose4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                           uint32_t &r0, uint32_t &r1, uint32_t &r2, uint32_t &r3) {
-    const uint32_t u0 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);  // a0b0 a1b0 a0b1 a1b1
-    const uint32_t u1 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);  // a0b2 a1b2 a0b3 a1b3
-    const uint32_t w0 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
-    const uint32_t w1 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
-    r0 = __builtin_amdgcn_perm(w0, u0, 0x05040100u);
-    r1 = __builtin_amdgcn_perm(w0, u0, 0x07060302u);
-    r2 = __builtin_amdgcn_perm(w1, u1, 0x05040100u);
-    r3 = __builtin_amdgcn_perm(w1, u1, 0x07060302u);
-}
-
-__device__ __forceinline__ uint32_t comp(const u32x4 &v, int d) {
-    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-}
-
-template <int K, int NG>
-__global__ __launch_bounds__(TPB) void gf_apply_kernel(ApplyArgs a) {
-    constexpr int R = replicas_for(K);
-    using E = typename Entry<NG>::T;
-    constexpr int W = 4 * NG;            // bytes per table entry
-    constexpr int ROWB = K * R * W;      // bytes per table row (one byte value x)
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-
-    // ---- table fill: lds[x][s][r] = T_s[x] ----
-    {
-        const E *tab = reinterpret_cast<const E *>(a.table);
-        E *dst = reinterpret_cast<E *>(lds);
-        for (int i = threadIdx.x; i < 256 * K * R; i += TPB) {
-            const int x = i / (K * R);
-            const int s = (i - x * (K * R)) / R;
-            dst[i] = tab[s * 256 + x];
-        }
-    }
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63;
-    const int r = lane % R;
-    const int grp = (lane & 31) / R;
-    uint32_t tb[K];
-    uint64_t ioff[K], coff[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const int s = (j + grp) % K;
-        tb[j] = (uint32_t)((s * R + r) * W);
-        ioff[j] = a.in_off[s];
-        coff[j] = a.copy_off[s];
-    }
-
-    for (uint64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
-        const uint64_t obj = tile / a.tiles_per_obj;
-        const uint64_t col = (tile - obj * a.tiles_per_obj) * TILE + threadIdx.x * VEC;
-        if (col >= a.C) continue;
-        const uint8_t *ib = a.in + obj * a.in_stride;
-        uint8_t *ob = a.out + obj * a.out_stride;
-
-        u32x4 v[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) v[j] = load16_masked(ib, ioff[j] + col, a.valid);
-
-        // acc[c] = packed computed-row bytes of byte-column c (16 columns)
-        E acc[16];
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const uint32_t x = comp(v[j], d);
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint32_t byte = (x >> (8 * b)) & 0xFFu;
-                    const E e = *reinterpret_cast<const E *>(lds + byte * ROWB + tb[j]);
-                    if (j == 0) acc[d * 4 + b] = e;
-                    else acc[d * 4 + b] ^= e;
-                }
-            }
-        }
-
-        // copies (data shards for encode, surviving primaries for decode)
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            if (coff[j] != NO_OUT) store16_nt(ob + coff[j] + col, v[j]);
-
-        // computed rows: transpose column-packed sums into row streams
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            uint32_t rows[4][4];  // [q][d]
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                uint32_t c0, c1, c2, c3;
-                if constexpr (NG == 1) {
-                    c0 = acc[d * 4 + 0]; c1 = acc[d * 4 + 1]; c2 = acc[d * 4 + 2]; c3 = acc[d * 4 + 3];
-                } else {
-                    c0 = acc[d * 4 + 0][g]; c1 = acc[d * 4 + 1][g]; c2 = acc[d * 4 + 2][g]; c3 = acc[d * 4 + 3][g];
-                }
-                transpose4(c0, c1, c2, c3, rows[0][d], rows[1][d], rows[2][d], rows[3][d]);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint64_t po = a.par_off[g * 4 + q];
-                if (po == NO_OUT) continue;
-                u32x4 o = {rows[q][0], rows[q][1], rows[q][2], rows[q][3]};
-                store16_nt(ob + po + col, o);
-            }
-        }
-    }
-}
+using namespace zf;
 
 // ---- generic fallback: any k (<= 256) and any number of output rows ----
 // One thread = 16 columns of one output row; full 64 KiB GF multiplication
@@ -232,8 +83,17 @@ __global__ __launch_bounds__(TPB) void gf_apply_generic_kernel(GenericArgs a) {
 // ---- host side ----------------------------------------------------------
 typedef void (*KernelFn)(ApplyArgs);
 
+// tuned schedule (tools/zfec_tune.hip on MI355X; DESIGN.md "K1 tuning")
+// MI355X sweeps (gpurun_out logs summarised in DESIGN.md): XCD-grouped runs of
+// 64 tiles (256 KiB per shard per workgroup) with nontemporal stores reach
+// ~97% of the bandwidth of the bare 4-read/8-write stream pattern.
+constexpr int ZF_U = 1;
+constexpr int ZF_MAP = 3;
+constexpr bool ZF_NT = true;
+constexpr uint64_t ZF_CHUNK = 64;
+
 template <int K, int NG>
-KernelFn kernel_ptr() { return gf_apply_kernel<K, NG>; }
+KernelFn kernel_ptr() { return gf_apply_kernel<K, NG, ZF_U, ZF_MAP, ZF_NT>; }
 
 struct KernelInfo {
     KernelFn fn;
@@ -382,6 +242,7 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     a.valid = L.valid; a.C = L.C;
     a.tiles_per_obj = (L.C + TILE - 1) / TILE;
     a.total_tiles = a.tiles_per_obj * L.count;
+    a.count = L.count;
     for (int j = 0; j < ZF_MAXK; ++j) {
         a.in_off[j] = j < (int)p.k ? p.in_off[j] : 0;
         a.copy_off[j] = (copies && j < (int)p.k) ? p.copy_off[j] : NO_OUT;
@@ -394,7 +255,11 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     hipError_t e = device_table(sub, ng, &a.table);
     if (e != hipSuccess) return e;
     const int grid_cap = grid_for(ki);
-    const uint64_t grid = a.total_tiles < (uint64_t)grid_cap ? a.total_tiles : (uint64_t)grid_cap;
+    uint64_t grid = a.total_tiles < (uint64_t)grid_cap ? a.total_tiles : (uint64_t)grid_cap;
+    if (grid >= 8) grid = grid / 8 * 8;  // XCD grouping needs a multiple of 8
+    // runs short enough that every workgroup gets work on small jobs
+    const uint64_t per_wg = a.total_tiles / (grid ? grid : 1);
+    a.chunk = per_wg < 1 ? 1 : (per_wg < ZF_CHUNK ? per_wg : ZF_CHUNK);
     hipLaunchKernelGGL(ki.fn, dim3((unsigned)grid), dim3(TPB), ki.lds, stream, a);
     return hipGetLastError();
 }

@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU session: parity tests, bench lines for every mode, rocprofv3 kernel
+# stats and the FETCH_SIZE / WRITE_SIZE passes for the headline kernel.
+# Usage (from the repo root, on the GPU box): bash tools/gpu_round.sh TAG
+set -e -o pipefail
+TAG=${1:-r1}
+R=$PWD
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python3 -m pytest tests -m gpu -x -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 600 python3 bench.py > $O/bench_encode.log 2>&1
+timeout -k 10 600 python3 bench.py --mode decode --no-cpu-baseline > $O/bench_decode.log 2>&1
+timeout -k 10 600 python3 bench.py --k 8 --m 16 --no-cpu-baseline > $O/bench_8of16.log 2>&1
+timeout -k 10 600 python3 bench.py --mode bao --objects 512 --object-mib 32 --no-cpu-baseline > $O/bench_bao.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o stats --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-verify > $O/prof.log 2>&1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o fetch --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify > $O/pmc_fetch.log 2>&1
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o write --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify > $O/pmc_write.log 2>&1
+echo done > $O/done

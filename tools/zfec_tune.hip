@@ -1,0 +1,137 @@
+// zfec_tune.hip — sweep schedule variants of the product's K1 kernel
+// (carbonado_amd/csrc/zfec_device.hpp) on the cfg2 workload, interleaved in
+// one process (cdna_hip_programming.md rule 24).  Calibration tool, not product.
+//   zfec_tune [objects=1024] [rounds=5]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../carbonado_amd/csrc/gf256.hpp"
+#include "../carbonado_amd/csrc/zfec_device.hpp"
+
+using namespace chip;
+using namespace chip::zf;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t e = (x);                                                                   \
+        if (e != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));          \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+namespace chip {
+int num_cus() { return 256; }
+}
+
+__global__ void fill_kernel(uint64_t *p, size_t n, uint64_t seed) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+__global__ void checksum_kernel(const uint64_t *p, size_t n, unsigned long long *out) {
+    uint64_t acc = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        acc += p[i] * (2 * i + 1);
+    atomicAdd(out, (unsigned long long)acc);
+}
+
+struct Variant {
+    std::string name;
+    void (*fn)(ApplyArgs);
+    int blocks_per_cu;
+    int chunk;
+};
+
+template <int U, int MAP, bool NT, int CH = 1>
+Variant V(int bpc) {
+    char buf[64];
+    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d %s bpc%d", U, MAP, CH, NT ? "nt " : "pln", bpc);
+    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT>, bpc, CH};
+}
+
+int main(int argc, char **argv) {
+    const uint64_t count = argc > 1 ? atoll(argv[1]) : 1024;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+    const uint64_t n = 16ull << 20, C = n / 4;
+    uint8_t *in, *out;
+    CK(hipMalloc(&in, count * n));
+    CK(hipMalloc(&out, count * 2 * n));
+    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xCA4B0AD0ull);
+    CK(hipMemset(out, 0, count * 2 * n));
+
+    // packed 4-of-8 parity table [s][x]
+    std::vector<uint8_t> enc = zfec_enc_matrix(4, 8);
+    const Gf256 &gf = Gf256::get();
+    std::vector<uint32_t> tab(4 * 256, 0);
+    for (int s = 0; s < 4; ++s)
+        for (int x = 0; x < 256; ++x)
+            for (int r = 0; r < 4; ++r)
+                tab[s * 256 + x] |= (uint32_t)gf.mul(enc[(4 + r) * 4 + s], (uint8_t)x) << (8 * r);
+    uint32_t *dtab;
+    CK(hipMalloc(&dtab, tab.size() * 4));
+    CK(hipMemcpy(dtab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+
+    ApplyArgs a{};
+    a.in = in; a.out = out; a.in_stride = n; a.out_stride = 2 * n; a.valid = n; a.C = C;
+    a.tiles_per_obj = C / TILE; a.total_tiles = a.tiles_per_obj * count; a.count = count;
+    a.table = dtab;
+    for (int j = 0; j < ZF_MAXK; ++j) { a.in_off[j] = j < 4 ? j * C : 0; a.copy_off[j] = j < 4 ? j * C : NO_OUT; }
+    for (int q = 0; q < ZF_MAXP; ++q) a.par_off[q] = q < 4 ? (4 + q) * C : NO_OUT;
+
+    std::vector<Variant> vs = {
+        V<1, 0, true>(4),        V<1, 1, true>(4),        V<1, 1, false>(4),       V<1, 2, false>(4),
+        V<1, 3, false, 16>(4),   V<1, 3, false, 64>(4),   V<1, 3, false, 256>(4),  V<1, 3, true, 64>(4),
+        V<2, 3, false, 32>(4),   V<1, 3, false, 64>(2),   V<1, 3, false, 64>(8),   V<2, 3, false, 32>(2),
+        V<1, 3, false, 8>(4),    V<2, 1, false>(4),
+    };
+    const size_t lds = 256 * 4 * 8 * 4;
+    unsigned long long *dsum;
+    CK(hipMalloc(&dsum, 8));
+    std::vector<std::vector<float>> ms(vs.size());
+    unsigned long long ref = 0;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int rd = 0; rd < rounds; ++rd) {
+        for (size_t v = 0; v < vs.size(); ++v) {
+            const int grid = 256 * vs[v].blocks_per_cu;
+            a.chunk = vs[v].chunk;
+            if (rd == 0) CK(hipMemset(out, 0, count * 2 * n));  // a variant that skips bytes fails the checksum
+            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(TPB), lds, 0, a);  // warm
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(TPB), lds, 0, a);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            ms[v].push_back(t);
+            if (rd == 0) {
+                CK(hipMemset(dsum, 0, 8));
+                hipLaunchKernelGGL(checksum_kernel, dim3(4096), dim3(256), 0, 0, (const uint64_t *)out,
+                                   count * 2 * n / 8, dsum);
+                unsigned long long h;
+                CK(hipMemcpy(&h, dsum, 8, hipMemcpyDeviceToHost));
+                if (v == 0) ref = h;
+                if (h != ref) printf("!! %s checksum mismatch\n", vs[v].name.c_str());
+            }
+        }
+    }
+    const double bytes = (double)count * 3 * n;
+    for (size_t v = 0; v < vs.size(); ++v) {
+        auto t = ms[v];
+        std::sort(t.begin(), t.end());
+        printf("%-22s median %7.3f ms  min %7.3f ms  -> %7.1f GB/s (median)  %7.1f (best)\n", vs[v].name.c_str(),
+               t[t.size() / 2], t[0], bytes / (t[t.size() / 2] * 1e-3) / 1e9, bytes / (t[0] * 1e-3) / 1e9);
+    }
+    return 0;
+}
