@@ -1,5 +1,5 @@
-// bao_kernels.hip — K3/K4/K5: BLAKE3 chunk chaining values, parent levels and
-// the bao combined (pre-order) layout on gfx950.
+// bao_kernels.hip — K3/K4/K5 host side: BLAKE3 chunk chaining values, parent
+// levels and the bao combined (pre-order) layout on gfx950.
 //
 // Replaces bao 0.12.1 -> blake3 1.x as called from
 //   encoding::bao  /root/reference/src/encoding.rs:38-44  (bao::encode::encode)
@@ -18,410 +18,40 @@
 //         chunk i           at 8 + 1024 i + 64 (P(i) + c(i))
 //         parent (level l, first chunk s) at 8 + 1024 s + 64 (P(s) + c(s) - l)
 //
-// K3 (chunk kernel): one lane = one chunk; a wave owns 64 consecutive chunks.
-// Each step stages 128 bytes of every chunk (full 128-byte lines, coalesced
-// dwordx4 loads) through LDS and transposes them so each lane reads its own
-// chunk's message words; the same loaded registers are written straight to
-// the chunk's place in the bao stream (encode) or the content buffer (decode),
-// so the data is read from HBM once.  BLAKE3 is VALU work (~11 int ops/byte):
-// K3 is bounded by VALU issue, not by HBM.
-// K4 (parent kernel): one lane = one parent of one level; writes the 64-byte
-// parent node (encode) or compares it with the stored one (decode: K5).
-#include "chip_internal.hpp"
+// K3 (bao_chunk_kernel, bao_device.hpp): lane = CPL consecutive chunks, the
+// first log2(CPL) levels folded in registers; chunk bytes staged through LDS
+// once and written straight to their stream slot (encode) or content slot
+// (decode).  BLAKE3 is VALU work (~11 int ops/byte): K3 is VALU-bound.
+// K4 (bao_parent_kernel): one launch per remaining level, lane = one node.
+// K5 (verify-decode) = the same kernels in MODE 1: every stored parent node is
+// compared with the recomputed children, the root with the expected hash.
+#include "bao_device.hpp"
+
+#include <algorithm>
 
 namespace chip {
 
+using namespace bao;
+
 namespace {
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-constexpr uint32_t F_CHUNK_START = 1, F_CHUNK_END = 2, F_PARENT = 4, F_ROOT = 8;
-constexpr int K3_WAVES = 4;
-constexpr int K3_TPB = 64 * K3_WAVES;
-constexpr int ROWW = 36;  // LDS words per staged chunk row (32 used): conflict-free b128 reads
-
-__host__ __device__ constexpr uint32_t IV(int i) {
-    return i == 0 ? 0x6A09E667u : i == 1 ? 0xBB67AE85u : i == 2 ? 0x3C6EF372u
-         : i == 3 ? 0xA54FF53Au : i == 4 ? 0x510E527Fu : i == 5 ? 0x9B05688Cu
-         : i == 6 ? 0x1F83D9ABu : 0x5BE0CD19u;
-}
-
-// message schedule: round r reads word SCHED(r, i); round 0 is the identity and
-// each round applies the permutation [2,6,3,10,7,0,4,13,1,11,12,5,9,14,15,8].
-__host__ __device__ constexpr int PERM(int i) {
-    constexpr int p[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
-    return p[i];
-}
-__host__ __device__ constexpr int SCHED(int r, int i) { return r == 0 ? i : SCHED(r - 1, PERM(i)); }
-
-__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) {
-    return __builtin_amdgcn_alignbit(x, x, n);
-}
-
-#define B3G(a, b, c, d, x, y)            \
-    do {                                 \
-        a = a + b + (x);                 \
-        d = rotr(d ^ a, 16);             \
-        c = c + d;                       \
-        b = rotr(b ^ c, 12);             \
-        a = a + b + (y);                 \
-        d = rotr(d ^ a, 8);              \
-        c = c + d;                       \
-        b = rotr(b ^ c, 7);              \
-    } while (0)
-
-template <int R>
-__device__ __forceinline__ void b3_round(uint32_t (&v)[16], const uint32_t (&m)[16]) {
-    B3G(v[0], v[4], v[8], v[12], m[SCHED(R, 0)], m[SCHED(R, 1)]);
-    B3G(v[1], v[5], v[9], v[13], m[SCHED(R, 2)], m[SCHED(R, 3)]);
-    B3G(v[2], v[6], v[10], v[14], m[SCHED(R, 4)], m[SCHED(R, 5)]);
-    B3G(v[3], v[7], v[11], v[15], m[SCHED(R, 6)], m[SCHED(R, 7)]);
-    B3G(v[0], v[5], v[10], v[15], m[SCHED(R, 8)], m[SCHED(R, 9)]);
-    B3G(v[1], v[6], v[11], v[12], m[SCHED(R, 10)], m[SCHED(R, 11)]);
-    B3G(v[2], v[7], v[8], v[13], m[SCHED(R, 12)], m[SCHED(R, 13)]);
-    B3G(v[3], v[4], v[9], v[14], m[SCHED(R, 14)], m[SCHED(R, 15)]);
-}
-
-// h <- first 8 output words of compress(h, m, counter, blen, flags)
-__device__ __forceinline__ void b3_compress(uint32_t (&h)[8], const uint32_t (&m)[16], uint64_t ctr,
-                                            uint32_t blen, uint32_t flags) {
-    uint32_t v[16] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7],
-                      IV(0), IV(1), IV(2), IV(3),
-                      (uint32_t)ctr, (uint32_t)(ctr >> 32), blen, flags};
-    b3_round<0>(v, m); b3_round<1>(v, m); b3_round<2>(v, m); b3_round<3>(v, m);
-    b3_round<4>(v, m); b3_round<5>(v, m); b3_round<6>(v, m);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) h[i] = v[i] ^ v[i + 8];
-}
-
-__device__ __forceinline__ void b3_parent(const uint32_t (&l)[8], const uint32_t (&r)[8], bool root,
-                                          uint32_t (&out)[8]) {
-    uint32_t m[16];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { m[i] = l[i]; m[8 + i] = r[i]; out[i] = IV(i); }
-    b3_compress(out, m, 0, 64, F_PARENT | (root ? F_ROOT : 0));
-}
-
-__host__ __device__ __forceinline__ int ceil_log2(uint64_t x) {  // x >= 1
-#if defined(__HIP_DEVICE_COMPILE__)
-    return x <= 1 ? 0 : 64 - __clzll((long long)(x - 1));
-#else
-    return x <= 1 ? 0 : 64 - __builtin_clzll(x - 1);
-#endif
-}
-
-__host__ __device__ __forceinline__ int ctz64(uint64_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __ffsll((long long)x) - 1;
-#else
-    return __builtin_ctzll(x);
-#endif
-}
-
-// c(s): parents whose leftmost chunk is s
-__host__ __device__ __forceinline__ int parents_at(uint64_t s, uint64_t N) {
-    const int cl = ceil_log2(N - s);
-    if (s == 0) return cl;
-    const int tz = ctz64(s);
-    return tz < cl ? tz : cl;
-}
-
-// P(s): parents whose leftmost chunk is < s
-__host__ __device__ __forceinline__ uint64_t parents_before(uint64_t s, uint64_t N) {
-    uint64_t total = 0, cnt = N;
-    for (int L = 1; cnt > 1; ++L) {
-        const uint64_t np = cnt / 2;
-        const uint64_t before = (s + (1ull << L) - 1) >> L;
-        total += before < np ? before : np;
-        cnt = (cnt + 1) / 2;
-    }
-    return total;
-}
-
-__host__ __device__ __forceinline__ uint64_t chunk_stream_off(uint64_t i, uint64_t N) {
-    return 8 + 1024 * i + 64 * (parents_before(i, N) + parents_at(i, N));
-}
-
-__host__ __device__ __forceinline__ uint64_t parent_stream_off(uint64_t s, int level, uint64_t N) {
-    return 8 + 1024 * s + 64 * (parents_before(s, N) + parents_at(s, N) - level);
-}
-
-__device__ __forceinline__ u32x4 load16_partial(const uint8_t *p, uint32_t valid) {
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if ((uint32_t)i < valid) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
-    u32x4 r = {w[0], w[1], w[2], w[3]};
-    return r;
-}
-
-__device__ __forceinline__ void store16_partial(uint8_t *p, u32x4 v, uint32_t valid) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if ((uint32_t)i < valid) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-}
-
-// 16 bytes at an 8-byte-aligned address
-__device__ __forceinline__ u32x4 load16_a8(const uint8_t *p) {
-    const u32x2 lo = *reinterpret_cast<const u32x2 *>(p);
-    const u32x2 hi = *reinterpret_cast<const u32x2 *>(p + 8);
-    u32x4 r = {lo.x, lo.y, hi.x, hi.y};
-    return r;
-}
-
-__device__ __forceinline__ void store16_a8_nt(uint8_t *p, u32x4 v) {
-    u32x2 lo = {v.x, v.y}, hi = {v.z, v.w};
-    __builtin_nontemporal_store(lo, reinterpret_cast<u32x2 *>(p));
-    __builtin_nontemporal_store(hi, reinterpret_cast<u32x2 *>(p + 8));
-}
-
-struct ChunkArgs {
-    const uint8_t *in;
-    uint8_t *out;          // encode: stream (may be null = hash only); decode: content
-    uint64_t in_stride, out_stride;
-    uint64_t n, N, count;
-    uint8_t *cv;           // [count][N] x 32 B
-    uint8_t *hash;         // encode: out (written iff N == 1); decode: expected
-    uint32_t *status;      // decode only
-};
-
-// MODE 0 = encode (in = content), MODE 1 = verify-decode (in = bao stream)
-template <int MODE>
-__global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage[K3_WAVES][64 * ROWW];
-    __shared__ uint64_t soff[K3_WAVES][64];
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const uint64_t tpo = (a.N + 63) / 64;
-    const uint64_t wt = (uint64_t)blockIdx.x * K3_WAVES + wave;
-    const bool wave_on = wt < a.count * tpo;
-    const uint64_t obj = wave_on ? wt / tpo : 0;
-    const uint64_t c0 = wave_on ? (wt - obj * tpo) * 64 : 0;
-    const uint64_t i = c0 + lane;
-    const bool mine = wave_on && i < a.N;
-    const uint32_t len = mine ? (uint32_t)((a.n - i * 1024) < 1024 ? (a.n - i * 1024) : 1024) : 0;
-    const uint32_t nb = len == 0 ? 1 : (len + 63) / 64;
-    const bool root = a.N == 1;
-
-    soff[wave][lane] = mine ? chunk_stream_off(i, a.N) : 0;
-    // the u64 LE content-length header of the stream
-    if (MODE == 0 && a.out && wave_on && c0 == 0 && lane == 0)
-        *reinterpret_cast<uint64_t *>(a.out + obj * a.out_stride) = a.n;
-    __syncthreads();
-
-    const uint8_t *ib = a.in + obj * a.in_stride;
-    uint8_t *ob = a.out ? a.out + obj * a.out_stride : nullptr;
-    uint32_t *st = stage[wave];
-    uint32_t h[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) h[w] = IV(w);
-
-    for (int s = 0; s < 8; ++s) {
-        // ---- stage 128 bytes of each of the wave's 64 chunks ----
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int cc = t * 8 + (lane >> 3);
-            const uint64_t ci = c0 + cc;
-            const uint32_t byte = (uint32_t)(s * 128 + (lane & 7) * 16);
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (wave_on && ci < a.N) {
-                const uint64_t rem = a.n - ci * 1024;
-                const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
-                if (byte < clen) {
-                    const uint32_t valid = clen - byte;
-                    if (MODE == 0) {
-                        const uint8_t *src = ib + ci * 1024 + byte;
-                        v = valid >= 16 ? *reinterpret_cast<const u32x4 *>(src) : load16_partial(src, valid);
-                        if (ob) {
-                            uint8_t *dst = ob + soff[wave][cc] + byte;
-                            if (valid >= 16) store16_a8_nt(dst, v);
-                            else store16_partial(dst, v, valid);
-                        }
-                    } else {
-                        const uint8_t *src = ib + soff[wave][cc] + byte;
-                        v = valid >= 16 ? load16_a8(src) : load16_partial(src, valid);
-                        uint8_t *dst = ob + ci * 1024 + byte;
-                        if (valid >= 16) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(dst));
-                        else store16_partial(dst, v, valid);
-                    }
-                }
-            }
-            *reinterpret_cast<u32x4 *>(st + cc * ROWW + (lane & 7) * 4) = v;
-        }
-        __syncthreads();
-        // ---- compress this lane's two blocks ----
-        for (int hh = 0; hh < 2; ++hh) {
-            const uint32_t b = (uint32_t)(2 * s + hh);
-            if (mine && b < nb) {
-                uint32_t m[16];
-                const u32x4 *row = reinterpret_cast<const u32x4 *>(st + lane * ROWW + hh * 16);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const u32x4 x = row[q];
-                    m[4 * q] = x.x; m[4 * q + 1] = x.y; m[4 * q + 2] = x.z; m[4 * q + 3] = x.w;
-                }
-                const bool last = b + 1 == nb;
-                const uint32_t blen = last ? len - 64 * b : 64u;
-                uint32_t flags = (b == 0 ? F_CHUNK_START : 0u) |
-                                 (last ? (F_CHUNK_END | (root ? F_ROOT : 0u)) : 0u);
-                b3_compress(h, m, i, blen, flags);
-            }
-        }
-        __syncthreads();
-    }
-
-    if (!mine) return;
-    u32x4 *cvp = reinterpret_cast<u32x4 *>(a.cv + (obj * a.N + i) * 32);
-    cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
-    cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
-    if (root) {
-        u32x4 *hp = reinterpret_cast<u32x4 *>(a.hash + obj * 32);
-        if (MODE == 0) {
-            hp[0] = u32x4{h[0], h[1], h[2], h[3]};
-            hp[1] = u32x4{h[4], h[5], h[6], h[7]};
-        } else {
-            const u32x4 e0 = hp[0], e1 = hp[1];
-            const bool ok = e0.x == h[0] && e0.y == h[1] && e0.z == h[2] && e0.w == h[3] &&
-                            e1.x == h[4] && e1.y == h[5] && e1.z == h[6] && e1.w == h[7];
-            if (!ok) __hip_atomic_store(a.status + obj, (uint32_t)CHIP_ERR_BAO_HASH_MISMATCH,
-                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-struct ParentArgs {
-    const uint8_t *cv_prev;
-    uint8_t *cv_next;
-    uint64_t stride_prev, stride_next;  // nodes per object in each buffer
-    uint64_t cnt_prev, cnt;             // nodes per object at level-1 and level
-    int level;
-    uint64_t N, count;
-    uint8_t *stream;                    // encode: write parents (may be null); decode: read
-    uint64_t stream_stride;
-    uint8_t *hash;                      // encode: out; decode: expected
-    uint32_t *status;
-};
-
-__device__ __forceinline__ void load_cv(const uint8_t *p, uint32_t (&c)[8]) {
-    const u32x4 a = reinterpret_cast<const u32x4 *>(p)[0];
-    const u32x4 b = reinterpret_cast<const u32x4 *>(p)[1];
-    c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
-}
-
-__device__ __forceinline__ void store_cv(uint8_t *p, const uint32_t (&c)[8]) {
-    reinterpret_cast<u32x4 *>(p)[0] = u32x4{c[0], c[1], c[2], c[3]};
-    reinterpret_cast<u32x4 *>(p)[1] = u32x4{c[4], c[5], c[6], c[7]};
-}
-
-template <int MODE>
-__global__ __launch_bounds__(256) void bao_parent_kernel(ParentArgs a) {
-    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (gid >= a.count * a.cnt) return;
-    const uint64_t obj = gid / a.cnt;
-    const uint64_t q = gid - obj * a.cnt;
-    const uint8_t *src = a.cv_prev + (obj * a.stride_prev + 2 * q) * 32;
-    uint32_t l[8];
-    load_cv(src, l);
-    if (2 * q + 1 >= a.cnt_prev) {  // odd last node: promoted unchanged
-        store_cv(a.cv_next + (obj * a.stride_next + q) * 32, l);
-        return;
-    }
-    uint32_t r[8], p[8];
-    load_cv(src + 32, r);
-    const bool root = a.cnt == 1;
-    b3_parent(l, r, root, p);
-    const uint64_t s = q << a.level;
-    if (a.stream) {
-        uint8_t *node = a.stream + obj * a.stream_stride + parent_stream_off(s, a.level, a.N);
-        if (MODE == 0) {
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                u32x2 x = {l[2 * w], l[2 * w + 1]}, y = {r[2 * w], r[2 * w + 1]};
-                __builtin_nontemporal_store(x, reinterpret_cast<u32x2 *>(node + 8 * w));
-                __builtin_nontemporal_store(y, reinterpret_cast<u32x2 *>(node + 32 + 8 * w));
-            }
-        } else {
-            bool ok = true;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const u32x2 x = reinterpret_cast<const u32x2 *>(node)[w];
-                const u32x2 y = reinterpret_cast<const u32x2 *>(node + 32)[w];
-                ok &= x.x == l[2 * w] && x.y == l[2 * w + 1] && y.x == r[2 * w] && y.y == r[2 * w + 1];
-            }
-            if (!ok) __hip_atomic_store(a.status + obj, (uint32_t)CHIP_ERR_BAO_HASH_MISMATCH,
-                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if (root) {
-        if (MODE == 0) {
-            store_cv(a.hash + obj * 32, p);
-        } else {
-            uint32_t e[8];
-            load_cv(a.hash + obj * 32, e);
-            bool ok = true;
-#pragma unroll
-            for (int w = 0; w < 8; ++w) ok &= e[w] == p[w];
-            if (!ok) __hip_atomic_store(a.status + obj, (uint32_t)CHIP_ERR_BAO_HASH_MISMATCH,
-                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else {
-        store_cv(a.cv_next + (obj * a.stride_next + q) * 32, p);
-    }
-}
-
-uint64_t n_chunks(uint64_t n) { return n == 0 ? 1 : (n + 1023) / 1024; }
+// tuned on MI355X (tools/bao_tune.hip)
+constexpr int BAO_CPL = 8;
+constexpr bool BAO_NTS = false;
 
 template <int MODE>
 hipError_t run_bao(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
                    void *d_scratch, hipStream_t stream) {
-    if (count == 0) return hipSuccess;
-    const uint64_t N = n_chunks(n);
-    uint8_t *bufA = static_cast<uint8_t *>(d_scratch);
-    uint8_t *bufB = bufA + count * N * 32;
-    const uint64_t strideA = N, strideB = (N + 1) / 2;
-
-    ChunkArgs ca;
-    ca.in = d_in; ca.out = d_out; ca.in_stride = in_stride; ca.out_stride = out_stride;
-    ca.n = n; ca.N = N; ca.count = count; ca.cv = bufA; ca.hash = d_hash; ca.status = d_status;
-    const uint64_t waves = count * ((N + 63) / 64);
-    const uint64_t blocks = (waves + K3_WAVES - 1) / K3_WAVES;
-    hipLaunchKernelGGL(bao_chunk_kernel<MODE>, dim3((unsigned)blocks), dim3(K3_TPB), 0, stream, ca);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-
-    uint8_t *stream_buf = MODE == 0 ? d_out : const_cast<uint8_t *>(d_in);
-    const uint64_t sstride = MODE == 0 ? out_stride : in_stride;
-    uint8_t *prev = bufA, *next = bufB;
-    uint64_t sp = strideA, sn = strideB, cnt_prev = N;
-    for (int level = 1; cnt_prev > 1; ++level) {
-        ParentArgs pa;
-        pa.cv_prev = prev; pa.cv_next = next; pa.stride_prev = sp; pa.stride_next = sn;
-        pa.cnt_prev = cnt_prev; pa.cnt = (cnt_prev + 1) / 2; pa.level = level;
-        pa.N = N; pa.count = count; pa.stream = stream_buf; pa.stream_stride = sstride;
-        pa.hash = d_hash; pa.status = d_status;
-        const uint64_t work = count * pa.cnt;
-        hipLaunchKernelGGL(bao_parent_kernel<MODE>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
-                           stream, pa);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        cnt_prev = pa.cnt;
-        std::swap(prev, next);
-        std::swap(sp, sn);
-    }
-    return hipSuccess;
+    return run_bao_t<MODE, BAO_CPL, BAO_NTS>(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_status,
+                                            d_scratch, stream);
 }
 
 }  // namespace
 
 uint64_t bao_encoded_len(uint64_t n) { return 8 + n + 64 * (n_chunks(n) - 1); }
 
-uint64_t bao_scratch_len(uint64_t n, uint64_t count) {
-    const uint64_t N = n_chunks(n);
-    return count * 32 * (N + (N + 1) / 2);
-}
+uint64_t bao_scratch_len(uint64_t n, uint64_t count) { return bao_scratch_len_t<BAO_CPL>(n, count); }
 
 hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                           uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,

@@ -59,7 +59,7 @@ def test_size_helpers_match_oracle(n):
 
 def test_bao_scratch_len():
     L = _lib.lib()
-    assert L.chip_bao_scratch_len(32 << 20, 2) == 2 * 32 * (32768 + 16384)
+    assert L.chip_bao_scratch_len(32 << 20, 2) == 2 * 32 * (4096 + 2048)
 
 
 def _has_gfx950() -> bool:
