@@ -4,18 +4,20 @@
 
 A step = one zfec encode launch over the whole per-GPU batch (1024 objects x
 16 MiB = 16 GiB in, 32 GiB out), inputs already resident in HBM.  Objects
-are independent, so N ranks each encode their own batch (weak scaling, no
-data-path collective); the driver's N>1 launch uses torch.distributed only
-for the barrier and the max-over-ranks time.
+are independent, so N ranks each encode their own contiguous range of the
+global object set (weak scaling, no data-path collective).  torch.distributed
+(gloo) carries only the control plane: barrier and max-over-ranks time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--objects 1024]
                     [--object-mib 16] [--k 4 --m 8] [--mode encode|decode|bao]
+                    [--scatter] [--dry-run]
 
 Rank 0 prints one JSON line (metric/value/unit/... + roofline + cpu_baseline).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -28,10 +30,11 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-from carbonado_amd import _lib, device  # noqa: E402
+from carbonado_amd.sharding import max_over_ranks, object_range  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "GiB/s device-resident zfec 4-of-8 encode, 16 MiB objects; % HBM roofline"
+SEED = 0xCA4B0AD0
 
 
 def parse():
@@ -48,21 +51,22 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--scatter", action="store_true",
+                    help="N>1: rank 0 generates every object and scatters them over RCCL/xGMI (timed "
+                         "separately, outside `value`)")
+    ap.add_argument("--dry-run", action="store_true", help="no device: exercise the multi-rank control plane")
     ap.add_argument("--traffic-json", default="auto",
                     help="PMC summary (profiles/*_pmc.json, tools/pmc_summary.py) with the measured HBM "
                          "bytes per launch of this kernel; 'auto' = newest matching file, 'none' = null")
     return ap.parse_args()
 
 
-def setup_dist(args):
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")  # control plane only: no bytes of the path cross it
     return world, rank, local
 
 
@@ -83,9 +87,9 @@ def fill_random(t: torch.Tensor, seed: int) -> None:
 
 def measured_traffic(spec: str, kernel_sym: str, alg_bytes: int):
     """HBM bytes per launch from a committed rocprofv3 PMC summary of the same
-    kernel and workload (profiles/<tag>_pmc.json), else None."""
+    kernel and workload (profiles/<tag>_pmc.json), else (None, None)."""
     if spec == "none":
-        return None
+        return None, None
     files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=lambda p: p.stat().st_mtime) if spec == "auto" \
         else [Path(spec)]
     for f in reversed(files):
@@ -100,122 +104,181 @@ def measured_traffic(spec: str, kernel_sym: str, alg_bytes: int):
 
 
 def cpu_baseline(args, n: int, sample_obj: bytes | None):
-    """Time the CPU oracle (scalar fec.c-style restatement of zfec-rs) on
-    whole 16 MiB objects, 1 thread, until ~cpu_seconds of work."""
+    """Time the CPU oracle (scalar fec.c-style restatement of zfec-rs / the
+    BLAKE3+bao restatement) on whole objects, 1 thread, ~cpu_seconds of work."""
     from oracle import oracle as O
     import numpy as np
-    obj = np.frombuffer(sample_obj, np.uint8) if sample_obj is not None else O.fill_object(0xCA4B0AD0, 0, n)
+    obj = np.frombuffer(sample_obj, np.uint8) if sample_obj is not None else O.fill_object(SEED, 0, n)
+    if args.mode == "decode":
+        z, pad, C = O.zfec_encode(obj, args.k, args.m)
+        keep = [i for i in range(args.m) if str(i) not in args.erase.split(",")]
+        shares = [z[i * C:(i + 1) * C] for i in keep]
     done = 0
     t0 = time.perf_counter()
     while True:
         if args.mode == "bao":
             O.bao_encode(obj)
         elif args.mode == "decode":
-            pass
+            O.zfec_decode_shares(shares, keep, pad, args.k, args.m)
         else:
             O.zfec_encode(obj, args.k, args.m)
         done += 1
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or done >= 4096:
             break
-    return {"value": done * n / el / 2**30, "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{done} x {n} B objects ({'bao' if args.mode == 'bao' else 'zfec %d-of-%d encode' % (args.k, args.m)}), "
-                      f"oracle/carbonado_oracle.c scalar fec.c-style restatement, 1 thread, {el:.1f} s"}
+    what = {"bao": "bao encode", "decode": f"zfec {args.k}-of-{args.m} decode, erased {args.erase}"}.get(
+        args.mode, f"zfec {args.k}-of-{args.m} encode")
+    return {"value": round(done * n / el / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{done} x {n} B objects ({what}) through oracle/carbonado_oracle.c, scalar "
+                      f"fec.c-style restatement of the reference crates, 1 thread, {el:.1f} s"}
+
+
+class Workload:
+    """The per-rank batch and its step function (device buffers from torch)."""
+
+    def __init__(self, args, rank: int, local: int, world: int):
+        from carbonado_amd import _lib, device
+        self.args = args
+        L = _lib.lib()
+        self.dev = dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(dev)
+        if L.chip_init(dev.index) != 0:
+            raise SystemExit(f"libcarbonado_hip: no usable gfx950 device: {L.chip_last_device_error().decode()}")
+        self.k, self.m = k, m = args.k, args.m
+        self.n = n = int(args.object_mib * (1 << 20))
+        self.count = count = args.objects
+        p32, c32 = ctypes.c_uint32(), ctypes.c_uint32()
+        L.chip_calc_padding_len(n, k, ctypes.byref(p32), ctypes.byref(c32))
+        self.C = C = c32.value
+        self.inp = torch.empty((count, n), dtype=torch.uint8, device=dev)
+        self.scatter_s = None
+        rng = object_range(rank, world, world * count)
+        if args.scatter and world > 1:
+            self.scatter_s = self._scatter_inputs(rank, world)
+        else:
+            fill_random(self.inp, SEED + rng.start)
+        if args.mode == "encode":
+            self.out = torch.empty((count, m * C), dtype=torch.uint8, device=dev)
+            self.step = lambda: device.zfec_encode_batch(self.inp, n, self.out, k, m)
+            self.alg_bytes = count * (n + m * C)  # read the input + write all m shards
+            ng = (m - k + 3) // 4
+            self.kernel = f"gf_apply_kernel<{k},{ng}>"
+            self.kernel_sym = f"gf_apply_kernel<{k}, {ng},"
+        elif args.mode == "decode":
+            self.enc = torch.empty((count, m * C), dtype=torch.uint8, device=dev)
+            device.zfec_encode_batch(self.inp, n, self.enc, k, m)
+            erased = {int(x) for x in args.erase.split(",") if x}
+            self.keep = [i for i in range(m) if i not in erased]
+            self.out = torch.empty((count, k * C), dtype=torch.uint8, device=dev)
+            self.step = lambda: device.zfec_decode_batch(self.enc, C, self.keep, self.out, k, m)
+            self.alg_bytes = count * (2 * k * C)  # read k shares + write k data shards
+            self.kernel = f"gf_apply_kernel<{k},1> (decode, erased {sorted(erased)})"
+            self.kernel_sym = f"gf_apply_kernel<{k}, 1,"
+        else:
+            blen = L.chip_bao_encoded_len(n)
+            self.out = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device=dev)
+            self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
+            self.scratch = device.bao_scratch(n, count, dev)
+            self.step = lambda: device.bao_encode_batch(self.inp, n, self.out, self.hashes, self.scratch)
+            self.alg_bytes = count * (n + blen)
+            self.kernel = "bao_chunk_kernel + bao_parent_kernel levels"
+            self.kernel_sym = "bao_chunk_kernel"
+        torch.cuda.synchronize()
+
+    def _scatter_inputs(self, rank: int, world: int) -> float:
+        """Rank 0 generates all world*count objects and scatters them (RCCL)."""
+        grp = dist.new_group(backend="nccl")
+        full = None
+        if rank == 0:
+            full = torch.empty((world * self.count, self.n), dtype=torch.uint8, device=self.dev)
+            fill_random(full, SEED)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        chunks = [c.contiguous() for c in full.chunk(world, dim=0)] if rank == 0 else None
+        dist.scatter(self.inp, chunks, src=0, group=grp)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        del full, chunks
+        torch.cuda.empty_cache()
+        return el
+
+    def time_steps(self, steps: int, warmup: int, world: int):
+        for _ in range(warmup):
+            self.step()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            evs[i][0].record(stream)  # the library launches on torch's current stream
+            self.step()
+            evs[i][1].record(stream)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier(world)
+        return t1 - t0, [a.elapsed_time(b) for a, b in evs]
+
+    def verify_object0(self):
+        from oracle import oracle as O
+        sample = self.inp[0].cpu().numpy().tobytes()
+        if self.args.mode == "encode":
+            ok = self.out[0].cpu().numpy().tobytes() == O.zfec_encode(sample, self.k, self.m)[0]
+        elif self.args.mode == "decode":
+            ok = self.out[0, :self.n].cpu().numpy().tobytes() == sample
+        else:
+            ok = self.hashes[0].cpu().numpy().tobytes() == O.blake3(sample)
+        return ok, sample
+
+
+class DryRun:
+    """Control-plane rehearsal without a device (CPU gloo tests)."""
+
+    def __init__(self, args, rank: int):
+        n = int(args.object_mib * (1 << 20))
+        self.rank = rank
+        self.alg_bytes = args.objects * 3 * n
+        self.kernel = self.kernel_sym = "dry-run"
+        self.C = n // args.k
+        self.scatter_s = None
+
+    def time_steps(self, steps: int, warmup: int, world: int):
+        barrier(world)
+        t0 = time.perf_counter()
+        time.sleep(0.01 * steps * (1 + 0.1 * self.rank))
+        t1 = time.perf_counter()
+        barrier(world)
+        return t1 - t0, [10.0] * steps
 
 
 def main():
     args = parse()
-    world, rank, local = setup_dist(args)
-    L = _lib.lib()
-    rc = L.chip_init(local)
-    if rc != 0:
-        raise SystemExit(f"libcarbonado_hip: no usable gfx950 device ({rc})")
-    k, m = args.k, args.m
+    world, rank, local = setup_dist()
     n = int(args.object_mib * (1 << 20))
-    count = args.objects
-    pad, C = 0, 0
-    import ctypes
-    p32, c32 = ctypes.c_uint32(), ctypes.c_uint32()
-    L.chip_calc_padding_len(n, k, ctypes.byref(p32), ctypes.byref(c32))
-    pad, C = p32.value, c32.value
-    dev = torch.device("cuda", local)
+    wl = DryRun(args, rank) if args.dry_run else Workload(args, rank, local, world)
+    elapsed, launch_ms = wl.time_steps(args.steps, args.warmup, world)
+    max_elapsed = max_over_ranks(elapsed)
 
-    inp = torch.empty((count, n), dtype=torch.uint8, device=dev)
-    fill_random(inp, 0xCA4B0AD0 + rank)
-    if args.mode == "encode":
-        out = torch.empty((count, m * C), dtype=torch.uint8, device=dev)
-        step = lambda: device.zfec_encode_batch(inp, n, out, k, m)  # noqa: E731
-        alg_bytes = count * (n + m * C)  # read input + write all m shards
-        kernel = f"gf_apply_kernel<{k},{(m - k + 3) // 4}>"
-        kernel_sym = f"gf_apply_kernel<{k}, {(m - k + 3) // 4},"
-        unit_bytes = n
-    elif args.mode == "decode":
-        enc = torch.empty((count, m * C), dtype=torch.uint8, device=dev)
-        device.zfec_encode_batch(inp, n, enc, k, m)
-        erased = {int(x) for x in args.erase.split(",") if x}
-        keep = [i for i in range(m) if i not in erased]
-        out = torch.empty((count, k * C), dtype=torch.uint8, device=dev)
-        step = lambda: device.zfec_decode_batch(enc, C, keep, out, k, m)  # noqa: E731
-        alg_bytes = count * (2 * k * C)  # read k shares + write k data shards
-        kernel = f"gf_apply_kernel<{k},1> (decode, erased {sorted(erased)})"
-        kernel_sym = f"gf_apply_kernel<{k}, 1,"
-        unit_bytes = n
-    else:
-        blen = L.chip_bao_encoded_len(n)
-        out = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device=dev)
-        hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
-        scratch = device.bao_scratch(n, count, dev)
-        step = lambda: device.bao_encode_batch(inp, n, out, hashes, scratch)  # noqa: E731
-        alg_bytes = count * (n + blen)
-        kernel = "bao_chunk_kernel<0> + bao_parent_kernel<0> levels"
-        kernel_sym = "bao_chunk_kernel"
-        unit_bytes = n
-    torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    stream = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record(stream)
-        step()
-        evs[i][1].record(stream)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier(world)
-    elapsed = t1 - t0
-    launch_ms = [a.elapsed_time(b) for a, b in evs]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    max_elapsed = float(t.item())
-
-    verified = None
-    sample = None
-    if rank == 0 and not args.no_verify:
-        from oracle import oracle as O
-        sample = inp[0].cpu().numpy().tobytes()
-        if args.mode == "encode":
-            verified = out[0].cpu().numpy().tobytes() == O.zfec_encode(sample, k, m)[0]
-        elif args.mode == "decode":
-            verified = out[0, :n].cpu().numpy().tobytes() == sample
-        else:
-            verified = hashes[0].cpu().numpy().tobytes() == O.blake3(sample)
+    verified, sample = None, None
+    if rank == 0 and not args.no_verify and not args.dry_run:
+        verified, sample = wl.verify_object0()
 
     if rank == 0:
-        total_units = world * count * unit_bytes * args.steps
+        k, m = args.k, args.m
+        total_units = world * args.objects * n * args.steps
         value = total_units / max_elapsed / 2**30
         avg_ms = sum(launch_ms) / len(launch_ms)
-        achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = measured_traffic(args.traffic_json, kernel_sym, alg_bytes)
+        achieved = wl.alg_bytes / (avg_ms * 1e-3) / 1e9
+        traffic, traffic_src = measured_traffic(args.traffic_json, wl.kernel_sym, wl.alg_bytes)
+        if args.mode == "bao":
+            workload = f"bao encode, {args.objects} x {args.object_mib:g} MiB objects per GPU"
+        else:
+            workload = f"zfec {k}-of-{m} {args.mode}, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         res = {
-            "metric": METRIC if args.mode == "encode" and (k, m) == (4, 8) else
-            f"GiB/s device-resident {args.mode} ({k}-of-{m}), {args.object_mib:g} MiB objects",
+            "metric": METRIC if args.mode == "encode" and (k, m) == (4, 8) and n == 16 << 20 else
+            f"GiB/s device-resident {workload}",
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -227,19 +290,27 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (uniform random bytes generated on device)",
-            "config": {"workload": f"zfec {k}-of-{m} {args.mode}, {count} x {args.object_mib:g} MiB objects per GPU"
-                       if args.mode != "bao" else f"bao encode, {count} x {args.object_mib:g} MiB objects per GPU",
-                       "objects_per_gpu": count, "object_bytes": n, "chunk_len": C, "k": k, "m": m,
-                       "global_objects": world * count,
+            "config": {"workload": workload, "objects_per_gpu": args.objects, "object_bytes": n,
+                       "chunk_len": wl.C, "k": k, "m": m, "global_objects": world * args.objects,
                        "parallelism": f"objects partitioned over {world} rank(s), no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": kernel, "alg_bytes_per_launch": alg_bytes,
-                         "avg_launch_ms": round(avg_ms, 4), "min_launch_ms": round(min(launch_ms), 4)},
+                         "traffic_source": traffic_src, "kernel": wl.kernel,
+                         "alg_bytes_per_launch": wl.alg_bytes, "avg_launch_ms": round(avg_ms, 4),
+                         "min_launch_ms": round(min(launch_ms), 4)},
             "verified_object0": verified,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if args.mode == "bao":
+            res["roofline"]["bound"] = "valu"
+            res["roofline"]["note"] = ("BLAKE3 is VALU-bound (~11 int ops/byte, ceiling ~6 TB/s hashed); "
+                                       "achieved/peak are HBM figures for reference")
+        if wl.scatter_s is not None:
+            res["scatter"] = {"seconds": round(wl.scatter_s, 4),
+                              "GiB_per_s": round(world * args.objects * n / wl.scatter_s / 2**30, 2),
+                              "how": "RCCL scatter from rank 0 over xGMI (outside the timed region)"}
+        if args.dry_run:
+            res["dry_run"] = True
+        elif not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args, n, sample)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -19,7 +19,8 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t F_CHUNK_START = 1, F_CHUNK_END = 2, F_PARENT = 4, F_ROOT = 8;
 constexpr int K3_WAVES = 4;
 constexpr int K3_TPB = 64 * K3_WAVES;
-constexpr int ROWW = 36;  // LDS words per staged chunk row (32 used): conflict-free b128 reads
+constexpr int ROWW = 36;  // LDS words per staged chunk row: [_, _, carry w30, w31 | 32 data words]
+constexpr int ROW0 = 4;   // first data word (16-B aligned; stride 36 keeps b128 reads conflict-free)
 
 __host__ __device__ constexpr uint32_t IV(int i) {
     return i == 0 ? 0x6A09E667u : i == 1 ? 0xBB67AE85u : i == 2 ? 0x3C6EF372u
@@ -280,8 +281,8 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
             }
         }
     };
-    auto copy_step = [&](int g, const u32x4 (&v)[8]) {
-        if (!ob) return;
+    // decode: content is 16-B aligned, store straight from the loaded registers
+    auto content_step = [&](int g, const u32x4 (&v)[8]) {
         const int j = g >> 3, s = g & 7;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -293,19 +294,57 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
             const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
             if (byte >= clen) continue;
             const uint32_t valid = clen - byte;
-            if (MODE == 0) {
-                uint8_t *dst = ob + soff[j & 1][wave][cc] + byte;
-                if (valid >= 16) store16_a8<NTS>(dst, v[t]);
-                else store16_partial(dst, v[t], valid);
+            uint8_t *dst = ob + ci * 1024 + byte;
+            if (valid >= 16) {
+                if (NTS) __builtin_nontemporal_store(v[t], reinterpret_cast<u32x4 *>(dst));
+                else *reinterpret_cast<u32x4 *>(dst) = v[t];
             } else {
-                uint8_t *dst = ob + ci * 1024 + byte;
-                if (valid >= 16) {
-                    if (NTS) __builtin_nontemporal_store(v[t], reinterpret_cast<u32x4 *>(dst));
-                    else *reinterpret_cast<u32x4 *>(dst) = v[t];
-                } else {
-                    store16_partial(dst, v[t], valid);
-                }
+                store16_partial(dst, v[t], valid);
             }
+        }
+    };
+    // encode: chunks sit at stream offsets = 8 (mod 16), so lane g of a chunk's
+    // 8-lane group emits the 16-B ALIGNED piece k = 8s+g covering chunk bytes
+    // [16k-8, 16k+8): the previous step's last 8 bytes live in the row's carry
+    // words, so every full piece is one aligned dwordx4 store read from LDS.
+    auto emit_piece = [&](uint8_t *base, const uint32_t *row, int k, int i, uint32_t clen) {
+        const int lo = 16 * k - 8;
+        const uint32_t *w = row + 2 + 4 * i;
+        if (lo >= 0 && (uint32_t)lo + 16 <= clen) {
+            const u32x2 a2 = *reinterpret_cast<const u32x2 *>(w);
+            const u32x2 b2 = *reinterpret_cast<const u32x2 *>(w + 2);
+            const u32x4 v = {a2.x, a2.y, b2.x, b2.y};
+            if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(base + lo));
+            else *reinterpret_cast<u32x4 *>(base + lo) = v;
+            return;
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int hlo = lo + 8 * half;
+            if (hlo < 0 || (uint32_t)hlo >= clen) continue;
+            const u32x2 x = *reinterpret_cast<const u32x2 *>(w + 2 * half);
+            if ((uint32_t)hlo + 8 <= clen) {
+                store8<NTS>(base + hlo, x);
+            } else {
+                const uint32_t cnt = clen - (uint32_t)hlo;
+                for (uint32_t q = 0; q < cnt; ++q)
+                    base[hlo + q] = (uint8_t)((q < 4 ? x.x : x.y) >> (8 * (q & 3)));
+            }
+        }
+    };
+    auto stream_step = [&](int g) {
+        const int j = g >> 3, s = g & 7, gl = lane & 7;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int cc = t * 8 + (lane >> 3);
+            const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
+            if (!(wave_on && ci < a.N)) continue;
+            const uint64_t rem = a.n - ci * 1024;
+            const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+            uint8_t *base = ob + soff[j & 1][wave][cc];
+            const uint32_t *row = st + cc * ROWW;
+            emit_piece(base, row, 8 * s + gl, gl, clen);
+            if (s == 7 && gl == 7) emit_piece(base, row, 64, 8, clen);  // chunk bytes [1016, 1024)
         }
     };
 
@@ -320,9 +359,13 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     for (int g = 0; g < NSTEP; ++g) {
         const int j = g >> 3, s = g & 7;
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
-            *reinterpret_cast<u32x4 *>(st + (t * 8 + (lane >> 3)) * ROWW + (lane & 7) * 4) = pre[t];
-        copy_step(g, pre);
+        for (int t = 0; t < 8; ++t) {
+            uint32_t *row = st + (t * 8 + (lane >> 3)) * ROWW;
+            if (MODE == 0 && (lane & 7) == 7)  // carry the previous step's last 8 bytes
+                *reinterpret_cast<u32x2 *>(row + 2) = *reinterpret_cast<const u32x2 *>(row + ROW0 + 30);
+            *reinterpret_cast<u32x4 *>(row + ROW0 + (lane & 7) * 4) = pre[t];
+        }
+        if (MODE == 1 && ob) content_step(g, pre);
         if (s == 7 && j + 1 < CPL) {  // stream offset of my next chunk, for the loads issued below
             const uint64_t ni = lb + j + 1;
             if ((uint64_t)(j + 1) < nmine) my_off += 1024 + 64 * (uint64_t)parents_at(ni, a.N);
@@ -330,6 +373,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         }
         wave_sync();
         if (g + 1 < NSTEP) load_step(g + 1, pre);  // in flight during the compressions
+        if (MODE == 0 && ob) stream_step(g);
 
         const uint64_t i = lb + j;
         const bool mine = (uint64_t)j < nmine;
@@ -339,7 +383,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
             const uint32_t b = (uint32_t)(2 * s + hh);
             if (mine && b < nb) {
                 uint32_t m[16];
-                const u32x4 *row = reinterpret_cast<const u32x4 *>(st + lane * ROWW + hh * 16);
+                const u32x4 *row = reinterpret_cast<const u32x4 *>(st + lane * ROWW + ROW0 + hh * 16);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const u32x4 x = row[q];

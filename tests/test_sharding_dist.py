@@ -1,0 +1,87 @@
+"""Multi-rank control plane on CPU (gloo, world_size 2): object partition,
+max-over-ranks timing, sum of processed objects and the input scatter used
+by bench.py for N > 1.  No GPU needed."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from carbonado_amd.sharding import (max_over_ranks, object_range, scatter_objects,
+                                    sum_over_ranks)
+
+
+def test_object_range_partition():
+    for total in [0, 1, 7, 1024, 8192, 8193]:
+        for world in [1, 2, 3, 4, 8]:
+            rs = [object_range(r, world, total) for r in range(world)]
+            assert rs[0].start == 0 and rs[-1].stop == total
+            assert all(a.stop == b.start for a, b in zip(rs, rs[1:]))
+            assert max(r.count for r in rs) - min(r.count for r in rs) <= 1
+    assert object_range(3, 8, 8192).start == 3072  # cfg5: 1024 per GPU
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = object_range(rank, world, 10)
+        got_max = max_over_ranks(1.5 + rank)
+        got_sum = sum_over_ranks(rng.count)
+        per = 3
+        full = torch.arange(world * per * 4, dtype=torch.uint8).reshape(world * per, 4) if rank == 0 else None
+        local = torch.empty((per, 4), dtype=torch.uint8)
+        scatter_objects(local, full, src=0)
+        expect = torch.arange(world * per * 4, dtype=torch.uint8).reshape(world * per, 4)[rank * per:(rank + 1) * per]
+        q.put((rank, got_max, got_sum, bool(torch.equal(local, expect))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_control_plane():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, mx, sm, ok in res:
+        assert mx == 2.5 and sm == 10 and ok, (rank, mx, sm, ok)
+
+
+@pytest.mark.parametrize("world", [2])
+def test_bench_world2_cpu_dry_run(world):
+    """bench.py's multi-rank reduction logic (value = all ranks' bytes / max
+    time) exercised with gloo on CPU via --dry-run (no device)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(root / "bench.py"), "--gpus", str(world),
+           "--steps", "3", "--warmup", "1", "--dry-run"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import json
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == world and res["scaling"] == "weak"
+    assert res["config"]["global_objects"] == world * res["config"]["objects_per_gpu"]

@@ -76,6 +76,18 @@ int main(int argc, char **argv) {
                          mk<0, 8, false>(true), mk<0, 8, true>(true),  mk<0, 4, true>(true),
                          mk<0, 8, false>(false), mk<0, 1, false>(false), mk<1, 8, false>(true),
                          mk<1, 4, false>(true), mk<1, 1, false>(true)};
+    if (argc > 4) {  // comma-separated subset of variant indices (profiling)
+        std::vector<V> keep;
+        std::string sel = argv[4];
+        size_t pos = 0;
+        while (pos <= sel.size()) {
+            size_t e = sel.find(',', pos);
+            if (e == std::string::npos) e = sel.size();
+            keep.push_back(vs[atoi(sel.substr(pos, e - pos).c_str())]);
+            pos = e + 1;
+        }
+        vs = keep;
+    }
     unsigned long long *dsum;
     CK(hipMalloc(&dsum, 8));
     std::vector<std::vector<float>> ms(vs.size());
