@@ -78,6 +78,10 @@ SIGNATURES = {
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_void_p]),
+    "chip_encode_host_batch": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p,
+                                              ctypes.c_void_p, ctypes.POINTER(EncodeInfoC), ctypes.c_uint32,
+                                              ctypes.c_uint64]),
 }
 
 _LIB = None

@@ -258,6 +258,8 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     soff[0][wave][lane] = my_off;
     if (MODE == 0 && ob && wave_on && c0 == 0 && lane == 0)  // u64 LE content-length header
         *reinterpret_cast<uint64_t *>(ob) = a.n;
+    if (MODE == 1 && wave_on && c0 == 0 && lane == 0 && *reinterpret_cast<const uint64_t *>(ib) != a.n)
+        flag_mismatch(a.status, obj);  // header disagrees with the batch's content length
     wave_sync();
 
     // loader view: step g covers chunk j = g/8 of every lane, bytes [128*(g%8), +128)
@@ -307,34 +309,10 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     // 8-lane group emits the 16-B ALIGNED piece k = 8s+g covering chunk bytes
     // [16k-8, 16k+8): the previous step's last 8 bytes live in the row's carry
     // words, so every full piece is one aligned dwordx4 store read from LDS.
-    auto emit_piece = [&](uint8_t *base, const uint32_t *row, int k, int i, uint32_t clen) {
-        const int lo = 16 * k - 8;
-        const uint32_t *w = row + 2 + 4 * i;
-        if (lo >= 0 && (uint32_t)lo + 16 <= clen) {
-            const u32x2 a2 = *reinterpret_cast<const u32x2 *>(w);
-            const u32x2 b2 = *reinterpret_cast<const u32x2 *>(w + 2);
-            const u32x4 v = {a2.x, a2.y, b2.x, b2.y};
-            if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(base + lo));
-            else *reinterpret_cast<u32x4 *>(base + lo) = v;
-            return;
-        }
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const int hlo = lo + 8 * half;
-            if (hlo < 0 || (uint32_t)hlo >= clen) continue;
-            const u32x2 x = *reinterpret_cast<const u32x2 *>(w + 2 * half);
-            if ((uint32_t)hlo + 8 <= clen) {
-                store8<NTS>(base + hlo, x);
-            } else {
-                const uint32_t cnt = clen - (uint32_t)hlo;
-                for (uint32_t q = 0; q < cnt; ++q)
-                    base[hlo + q] = (uint8_t)((q < 4 ? x.x : x.y) >> (8 * (q & 3)));
-            }
-        }
-    };
+    // Chunk head (k = 0) and tail (k = 64) are 8-byte halves.
     auto stream_step = [&](int g) {
         const int j = g >> 3, s = g & 7, gl = lane & 7;
-#pragma unroll
+#pragma unroll 1
         for (int t = 0; t < 8; ++t) {
             const int cc = t * 8 + (lane >> 3);
             const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
@@ -342,9 +320,30 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
             const uint64_t rem = a.n - ci * 1024;
             const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
             uint8_t *base = ob + soff[j & 1][wave][cc];
-            const uint32_t *row = st + cc * ROWW;
-            emit_piece(base, row, 8 * s + gl, gl, clen);
-            if (s == 7 && gl == 7) emit_piece(base, row, 64, 8, clen);  // chunk bytes [1016, 1024)
+            const uint32_t *w = st + cc * ROWW + 2 + 4 * gl;  // carry/previous half, then this piece
+            const int lo = 16 * (8 * s + gl) - 8;             // chunk byte of the piece's first half
+            if (clen == 1024) {
+                if (lo >= 0) {
+                    const u32x2 x = *reinterpret_cast<const u32x2 *>(w);
+                    const u32x2 y = *reinterpret_cast<const u32x2 *>(w + 2);
+                    const u32x4 v = {x.x, x.y, y.x, y.y};
+                    if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(base + lo));
+                    else *reinterpret_cast<u32x4 *>(base + lo) = v;
+                } else {  // head: chunk bytes [0, 8)
+                    store8<NTS>(base, *reinterpret_cast<const u32x2 *>(w + 2));
+                }
+                if (s == 7 && gl == 7)  // tail: chunk bytes [1016, 1024)
+                    store8<NTS>(base + 1016, *reinterpret_cast<const u32x2 *>(w + 4));
+            } else {  // short last chunk of the object: byte stores
+                for (int q = 0; q < 16; ++q) {
+                    const int cb = lo + q;
+                    if (cb >= 0 && (uint32_t)cb < clen)
+                        base[cb] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+                }
+                if (s == 7 && gl == 7)
+                    for (int q = 0; q < 8; ++q)
+                        if (1016u + q < clen) base[1016 + q] = (uint8_t)(w[4 + (q >> 2)] >> (8 * (q & 3)));
+            }
         }
     };
 

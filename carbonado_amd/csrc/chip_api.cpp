@@ -51,15 +51,27 @@ struct DevBuf {
     size_t cap = 0;
 };
 
+// one pipeline slot of chip_encode_host_batch: its own stream and buffers
+struct Slot {
+    hipStream_t stream = nullptr;
+    DevBuf in, mid, out, hash, scratch;
+};
+
 struct Ctx {
     bool ready = false;
     hipStream_t stream = nullptr;
     DevBuf in, mid, out, scratch, small;
+    std::vector<Slot> slots;
     ~Ctx() {
         // process teardown: the runtime may already be gone; best effort
         for (DevBuf *b : {&in, &mid, &out, &scratch, &small})
             if (b->p) (void)hipFree(b->p);
         if (stream) (void)hipStreamDestroy(stream);
+        for (Slot &sl : slots) {
+            for (DevBuf *b : {&sl.in, &sl.mid, &sl.out, &sl.hash, &sl.scratch})
+                if (b->p) (void)hipFree(b->p);
+            if (sl.stream) (void)hipStreamDestroy(sl.stream);
+        }
     }
 };
 
@@ -200,6 +212,34 @@ int select_shares(uint32_t k, uint32_t m, const uint32_t *idx, uint32_t nshares,
     for (uint32_t s = 0; s < nshares && sel_pos->size() < k; ++s)
         if (idx[s] >= k && !have[idx[s]]) { have[idx[s]] = 1; sel_pos->push_back(s); }
     return sel_pos->size() == k ? CHIP_OK : CHIP_ERR_ZFEC;
+}
+
+// EncodeInfo of encode() for format bits Bao|Zfec (encoding.rs:86-172); no device
+int encode_info_for(uint8_t format, uint64_t n, chip_encode_info *inf, uint64_t *zlen, uint64_t *final_len) {
+    std::memset(inf, 0, sizeof *inf);
+    inf->input_len = (uint32_t)n;  // encoding.rs:87 (as u32)
+    const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
+    uint64_t cur_len = n;
+    if (zfec) {
+        uint32_t pad;
+        uint64_t C;
+        calc_pad(n, CHIP_FEC_K, &pad, &C);
+        inf->padding_len = pad;
+        inf->chunk_len = (uint32_t)C;
+        cur_len = (uint64_t)CHIP_FEC_M * C;
+        inf->bytes_ecc = (uint32_t)cur_len;                                        // encoding.rs:123
+        inf->verifiable_slice_count = (uint16_t)(inf->bytes_ecc / CHIP_SLICE_LEN);  // encoding.rs:124
+        if (inf->verifiable_slice_count % 8 != 0) return CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT;
+        inf->chunk_slice_count = inf->verifiable_slice_count / 8;                  // encoding.rs:130
+    }
+    const uint64_t fl = bao ? bao_encoded_len(cur_len) : cur_len;
+    if (bao) inf->bytes_verifiable = (uint32_t)fl;
+    inf->compression_factor = (float)inf->bytes_compressed / (float)inf->input_len;    // encoding.rs:150
+    inf->amplification_factor = (float)inf->bytes_verifiable / (float)inf->input_len;  // encoding.rs:151
+    inf->output_len = (uint32_t)fl;
+    *zlen = cur_len;
+    *final_len = fl;
+    return CHIP_OK;
 }
 
 }  // namespace
@@ -519,30 +559,17 @@ int chip_encode(uint8_t format, const uint8_t *in, uint64_t n, uint8_t *out, uin
     if ((!in && n) || !out_len || !hash) return CHIP_ERR_INVALID_ARG;
     if (format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY)) return CHIP_ERR_UNSUPPORTED_FORMAT;
     chip_encode_info inf;
-    std::memset(&inf, 0, sizeof inf);
-    inf.input_len = (uint32_t)n;  // encoding.rs:87 (as u32)
+    uint64_t cur_len, final_len;
+    int st = encode_info_for(format, n, &inf, &cur_len, &final_len);
+    if (st != CHIP_OK) return st;
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
-    uint64_t cur_len = n;
-    if (zfec) {
-        uint32_t pad;
-        uint64_t C;
-        calc_pad(n, CHIP_FEC_K, &pad, &C);
-        inf.padding_len = pad;
-        inf.chunk_len = (uint32_t)C;
-        cur_len = (uint64_t)CHIP_FEC_M * C;
-        inf.bytes_ecc = (uint32_t)cur_len;                                           // encoding.rs:123
-        inf.verifiable_slice_count = (uint16_t)(inf.bytes_ecc / CHIP_SLICE_LEN);     // encoding.rs:124
-        if (inf.verifiable_slice_count % 8 != 0) return CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT;
-        inf.chunk_slice_count = inf.verifiable_slice_count / 8;                     // encoding.rs:130
-    }
-    const uint64_t final_len = bao ? bao_encoded_len(cur_len) : cur_len;
     if (final_len && (!out || out_cap < final_len)) return CHIP_ERR_BUFFER_TOO_SMALL;
     if (!zfec && !bao) {
         if (n) std::memcpy(out, in, n);
         std::memset(hash, 0, 32);
     } else {
         Ctx *c;
-        int st = ctx_get(&c);
+        st = ctx_get(&c);
         if (st != CHIP_OK) return st;
         CHIP_HIP(grow(c->in, n));
         if (n) CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
@@ -558,18 +585,95 @@ int chip_encode(uint8_t format, const uint8_t *in, uint64_t n, uint8_t *out, uin
             st = bao_encode_ctx(c, d_cur, cur_len, true, hash);
             if (st != CHIP_OK) return st;
             CHIP_HIP(hipMemcpyAsync(out, c->out.p, final_len, hipMemcpyDeviceToHost, c->stream));
-            inf.bytes_verifiable = (uint32_t)final_len;
         } else {
             std::memset(hash, 0, 32);  // encoding.rs:145
             if (final_len) CHIP_HIP(hipMemcpyAsync(out, d_cur, final_len, hipMemcpyDeviceToHost, c->stream));
         }
         CHIP_HIP(hipStreamSynchronize(c->stream));
     }
-    inf.compression_factor = (float)inf.bytes_compressed / (float)inf.input_len;      // encoding.rs:150
-    inf.amplification_factor = (float)inf.bytes_verifiable / (float)inf.input_len;    // encoding.rs:151
-    inf.output_len = (uint32_t)final_len;
     *out_len = final_len;
     if (info) *info = inf;
+    return CHIP_OK;
+}
+
+int chip_encode_host_batch(uint8_t format, const uint8_t *in, uint64_t n, uint64_t count, uint64_t in_stride,
+                           uint8_t *out, uint64_t out_stride, uint64_t *out_len, uint8_t *hashes,
+                           chip_encode_info *info, uint32_t nslots, uint64_t slice_bytes) {
+    if ((!in && n && count) || !out_len || (!hashes && count)) return CHIP_ERR_INVALID_ARG;
+    if (format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY)) return CHIP_ERR_UNSUPPORTED_FORMAT;
+    if (count > 1 && in_stride < n) return CHIP_ERR_INVALID_ARG;
+    chip_encode_info inf;
+    uint64_t zlen, final_len;
+    int st = encode_info_for(format, n, &inf, &zlen, &final_len);
+    if (st != CHIP_OK) return st;
+    if (count > 1 && out_stride < final_len) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (final_len && count && !out) return CHIP_ERR_BUFFER_TOO_SMALL;
+    const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
+    *out_len = final_len;
+    if (info) *info = inf;
+    if (count == 0) return CHIP_OK;
+    if (!zfec && !bao) {  // format 0: identity, nothing for the device to do
+        for (uint64_t o = 0; o < count; ++o) {
+            if (n) std::memcpy(out + o * out_stride, in + o * in_stride, n);
+            std::memset(hashes + 32 * o, 0, 32);
+        }
+        return CHIP_OK;
+    }
+    Ctx *c;
+    st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    nslots = nslots < 1 ? 3 : (nslots > 8 ? 8 : nslots);
+    if (slice_bytes == 0) slice_bytes = 256ull << 20;
+    const uint64_t n_al = (n + 15) / 16 * 16;           // device input stride
+    const uint64_t z_al = (zlen + 15) / 16 * 16;         // device zfec-output stride
+    const uint64_t f_al = (final_len + 15) / 16 * 16;    // device stream stride
+    uint64_t S = slice_bytes / (n ? n : 1);
+    S = S < 1 ? 1 : (S > count ? count : S);
+    if (c->slots.size() < nslots) c->slots.resize(nslots);
+    for (uint32_t k = 0; k < nslots; ++k) {
+        Slot &sl = c->slots[k];
+        if (!sl.stream) CHIP_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        CHIP_HIP(grow(sl.in, S * n_al));
+        if (zfec) CHIP_HIP(grow(sl.mid, S * z_al));
+        if (bao) {
+            CHIP_HIP(grow(sl.out, S * f_al));
+            CHIP_HIP(grow(sl.scratch, bao_scratch_len(zlen, S)));
+        }
+        CHIP_HIP(grow(sl.hash, S * 32));
+    }
+    const GfPlan plan = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M));
+    const uint64_t nslices = (count + S - 1) / S;
+    for (uint64_t i = 0; i < nslices; ++i) {
+        Slot &sl = c->slots[i % nslots];
+        if (i >= nslots) CHIP_HIP(hipStreamSynchronize(sl.stream));  // slot's previous slice is done
+        const uint64_t o0 = i * S, cnt = (count - o0) < S ? (count - o0) : S;
+        uint8_t *d_in = static_cast<uint8_t *>(sl.in.p);
+        if (n) CHIP_HIP(hipMemcpy2DAsync(d_in, n_al, in + o0 * in_stride, count > 1 ? in_stride : n, n, cnt,
+                                         hipMemcpyHostToDevice, sl.stream));
+        const uint8_t *d_cur = d_in;
+        uint64_t cur_stride = n_al;
+        if (zfec) {
+            GfLaunch L{d_in, static_cast<uint8_t *>(sl.mid.p), n_al, z_al, n, inf.chunk_len, cnt};
+            CHIP_HIP(gf_apply(plan, L, sl.stream));
+            d_cur = static_cast<const uint8_t *>(sl.mid.p);
+            cur_stride = z_al;
+        }
+        const uint8_t *d_res = d_cur;
+        uint64_t res_stride = cur_stride;
+        if (bao) {
+            CHIP_HIP(bao_encode_dev(d_cur, cur_stride, zlen, cnt, static_cast<uint8_t *>(sl.out.p), f_al,
+                                    static_cast<uint8_t *>(sl.hash.p), sl.scratch.p, sl.stream));
+            d_res = static_cast<const uint8_t *>(sl.out.p);
+            res_stride = f_al;
+            CHIP_HIP(hipMemcpyAsync(hashes + 32 * o0, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, sl.stream));
+        } else {
+            for (uint64_t o = 0; o < cnt; ++o) std::memset(hashes + 32 * (o0 + o), 0, 32);
+        }
+        if (final_len)
+            CHIP_HIP(hipMemcpy2DAsync(out + o0 * out_stride, count > 1 ? out_stride : final_len, d_res, res_stride,
+                                      final_len, cnt, hipMemcpyDeviceToHost, sl.stream));
+    }
+    for (uint32_t k = 0; k < nslots; ++k) CHIP_HIP(hipStreamSynchronize(c->slots[k].stream));
     return CHIP_OK;
 }
 

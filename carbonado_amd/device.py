@@ -66,3 +66,21 @@ def bao_decode_batch(enc: torch.Tensor, n: int, hashes: torch.Tensor, out: torch
     count = enc.shape[0]
     check(_lib.lib().chip_bao_decode_batch_dev(_p(enc), enc.shape[1], n, count, _p(hashes), _p(out),
                                                out.shape[1], _p(status), _p(scratch), _stream()))
+
+
+def encode_host_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes: torch.Tensor,
+                      nslots: int = 3, slice_bytes: int = 256 << 20):
+    """End-to-end encode() of `count` objects held in HOST memory (pinned
+    tensors reach the full PCIe rate): inp uint8 [count, >= n], out uint8
+    [count, >= encoded length], hashes uint8 [count, 32].  Synchronous.
+    Returns (encoded length per object, EncodeInfo)."""
+    from .structs import EncodeInfo
+    assert not inp.is_cuda and not out.is_cuda and not hashes.is_cuda
+    assert inp.is_contiguous() and out.is_contiguous() and hashes.is_contiguous()
+    count = inp.shape[0]
+    olen = ctypes.c_uint64()
+    info = _lib.EncodeInfoC()
+    check(_lib.lib().chip_encode_host_batch(fmt, _p(inp), n, count, inp.shape[1], _p(out), out.shape[1],
+                                            ctypes.byref(olen), _p(hashes), ctypes.byref(info), nslots,
+                                            slice_bytes))
+    return olen.value, EncodeInfo.from_c(info)

@@ -196,6 +196,20 @@ CHIP_API int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, 
                               const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                               uint32_t *d_status, void *d_scratch, void *stream);
 
+/* ---- host-memory batch (end-to-end: host -> HBM -> host) -------------- */
+/* encode() for `count` objects of n bytes that live in HOST memory (object o
+ * at in + o*in_stride) into host memory (stream o at out + o*out_stride,
+ * length *out_len each; hash o at hashes + 32*o).  Objects are processed in
+ * slices over `nslots` device slots, each with its own stream, so the H2D
+ * copy of one slice, the kernels of the next and the D2H copy of a third
+ * overlap (PCIe full duplex).  Pinned (page-locked) host buffers reach the
+ * full PCIe rate; pageable ones are staged by the runtime.  Format bits as
+ * chip_encode (Bao|Zfec).  `info` receives the (identical) EncodeInfo. */
+CHIP_API int chip_encode_host_batch(uint8_t format, const uint8_t *in, uint64_t n, uint64_t count,
+                                    uint64_t in_stride, uint8_t *out, uint64_t out_stride,
+                                    uint64_t *out_len, uint8_t *hashes, chip_encode_info *info,
+                                    uint32_t nslots, uint64_t slice_bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,3 +70,44 @@ def test_levels_random(gpu, n):
         oenc, oh, oinfo = O.encode(d, level)
         assert enc == oenc and h == oh
         assert ca.decode(b"", h, enc, info.padding_len, level) == d
+
+
+@pytest.mark.parametrize("level", [4, 8, 12])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_encode_host_batch(gpu, level, pinned):
+    """chip_encode_host_batch (pipelined host->HBM->host) == encode() per object."""
+    import torch
+    from carbonado_amd import device
+    n, count = 70_001, 7
+    rng = np.random.default_rng(level)
+    inp = torch.from_numpy(rng.integers(0, 256, (count, n + 9), dtype=np.uint8))  # ragged stride
+    if pinned:
+        inp = inp.pin_memory()
+    cap = device._lib.lib().chip_encode_max_len(n)
+    out = torch.zeros((count, cap + 5), dtype=torch.uint8)
+    hashes = torch.zeros((count, 32), dtype=torch.uint8)
+    if pinned:
+        out, hashes = out.pin_memory(), hashes.pin_memory()
+    olen, info = device.encode_host_batch(level, inp, n, out, hashes, nslots=2, slice_bytes=3 * n)
+    for o in range(count):
+        enc, h, oinfo = O.encode(inp[o, :n].numpy().tobytes(), level)
+        assert olen == len(enc)
+        assert out[o, :olen].numpy().tobytes() == enc, o
+        assert hashes[o].numpy().tobytes() == (h if level & 4 else b"\0" * 32)
+    assert info.output_len == olen and info.padding_len == oinfo["padding_len"]
+
+
+def test_bao_decode_batch_header_mismatch(gpu):
+    import torch
+    from carbonado_amd import device
+    n = 5000
+    d = np.random.default_rng(3).integers(0, 256, n, dtype=np.uint8).tobytes()
+    enc, h = O.bao_encode(d)
+    t = torch.from_numpy(np.frombuffer(enc + b"\0" * 8, np.uint8).copy()).cuda().reshape(1, -1)
+    t[0, 0] ^= 1  # header says n ^ 1
+    hashes = torch.from_numpy(np.frombuffer(h, np.uint8).copy()).cuda().reshape(1, 32)
+    out = torch.empty((1, n), dtype=torch.uint8, device="cuda")
+    status = torch.empty(1, dtype=torch.int32, device="cuda")
+    device.bao_decode_batch(t, n, hashes, out, status, device.bao_scratch(n, 1))
+    torch.cuda.synchronize()
+    assert int(status[0]) == 5
