@@ -8,13 +8,13 @@ functions in `encoding` / `decoding`.  Compute happens only in
 """
 from . import constants, decoding, encoding, error, structs, utils
 from .constants import FEC_K, FEC_M, HASH_SIZE, SLICE_LEN, Format
-from .decoding import decode
+from .decoding import decode, extract_slice, scrub, verify_slice
 from .encoding import encode
 from .error import CarbonadoError
 from .structs import EncodeInfo, Encoded
 
 __all__ = [
-    "encode", "decode", "Encoded", "EncodeInfo", "Format", "CarbonadoError",
+    "encode", "decode", "extract_slice", "verify_slice", "scrub", "Encoded", "EncodeInfo", "Format", "CarbonadoError",
     "FEC_K", "FEC_M", "SLICE_LEN", "HASH_SIZE",
     "constants", "decoding", "encoding", "error", "structs", "utils",
 ]

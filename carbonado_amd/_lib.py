@@ -78,6 +78,14 @@ SIGNATURES = {
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_void_p]),
+    "chip_bao_slice_len": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+    "chip_bao_extract_slice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
+    "chip_bao_verify_slice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                             c_u64p]),
+    "chip_scrub": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
     "chip_encode_host_batch": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                               ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p,
                                               ctypes.c_void_p, ctypes.POINTER(EncodeInfoC), ctypes.c_uint32,

@@ -154,6 +154,35 @@ __device__ __forceinline__ u32x4 load16_a8(const uint8_t *p) {
 
 
 
+// Nearest real parent above the node (level lv, leftmost chunk sx): the lowest
+// level lp > lv whose node containing sx has two children.  Returns 0 when the
+// node is the root.  The node is that parent's left child iff sx is the
+// parent's leftmost chunk (a promoted node keeps its leftmost chunk).
+__host__ __device__ __forceinline__ int nearest_parent(uint64_t sx, int lv, uint64_t N, uint64_t *sp) {
+    for (int lp = lv + 1; lp < 64; ++lp) {
+        const uint64_t s0 = (sx >> lp) << lp;
+        if (s0 + (1ull << (lp - 1)) < N) { *sp = s0; return lp; }
+        if (s0 == 0 && (1ull << lp) >= N) return 0;
+    }
+    return 0;
+}
+
+// bao's top-down check of one node, restated per node: does the CV `cv` of
+// the node (level lv, leftmost chunk sx) equal the copy stored in its parent?
+__device__ __forceinline__ bool stored_slot_matches(const uint8_t *stream, uint64_t sx, int lv, uint64_t N,
+                                                    const uint32_t (&cv)[8]) {
+    uint64_t sp = 0;
+    const int lp = nearest_parent(sx, lv, N, &sp);
+    const uint8_t *slot = stream + parent_stream_off(sp, lp, N) + (sx == sp ? 0 : 32);
+    bool ok = true;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const u32x2 x = reinterpret_cast<const u32x2 *>(slot)[w];
+        ok &= x.x == cv[2 * w] && x.y == cv[2 * w + 1];
+    }
+    return ok;
+}
+
 struct ChunkArgs {
     const uint8_t *in;
     uint8_t *out;          // encode: stream (may be null = hash only); decode: content
@@ -258,7 +287,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     soff[0][wave][lane] = my_off;
     if (MODE == 0 && ob && wave_on && c0 == 0 && lane == 0)  // u64 LE content-length header
         *reinterpret_cast<uint64_t *>(ob) = a.n;
-    if (MODE == 1 && wave_on && c0 == 0 && lane == 0 && *reinterpret_cast<const uint64_t *>(ib) != a.n)
+    if (MODE != 0 && wave_on && c0 == 0 && lane == 0 && *reinterpret_cast<const uint64_t *>(ib) != a.n && a.status)
         flag_mismatch(a.status, obj);  // header disagrees with the batch's content length
     wave_sync();
 
@@ -276,7 +305,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
                 const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
                 if (byte < clen) {
                     const uint32_t valid = clen - byte;
-                    const uint8_t *src = MODE == 0 ? ib + ci * 1024 + byte : ib + soff[j & 1][wave][cc] + byte;
+                    const uint8_t *src = MODE == 0 ? ib + ci * 1024 + byte : ib + soff[j & 1][wave][cc] + byte;  // 1, 2: stream
                     if (valid >= 16) v[t] = MODE == 0 ? *reinterpret_cast<const u32x4 *>(src) : load16_a8(src);
                     else v[t] = load16_partial(src, valid);
                 }
@@ -397,7 +426,22 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         }
         wave_sync();
 
-        if (s == 7) {  // chunk j of every lane is complete
+        if (MODE == 2 && s == 7) {  // node check: chunk CV vs its stored slot (or the hash)
+            if (mine) {
+                bool cok;
+                if (a.N == 1) {
+                    const u32x4 *hp = reinterpret_cast<const u32x4 *>(a.hash + obj * 32);
+                    const u32x4 e0 = hp[0], e1 = hp[1];
+                    cok = e0.x == h[0] && e0.y == h[1] && e0.z == h[2] && e0.w == h[3] && e1.x == h[4] &&
+                          e1.y == h[5] && e1.z == h[6] && e1.w == h[7];
+                } else {
+                    cok = stored_slot_matches(ib, i, 0, a.N, h);
+                }
+                a.cv[obj * a.cv_stride + i] = cok ? 1 : 0;
+            }
+#pragma unroll
+            for (int w = 0; w < 8; ++w) h[w] = IV(w);
+        } else if (s == 7) {  // chunk j of every lane is complete
             if (mine) {
                 const bool final = (uint64_t)j + 1 == nmine;
                 // CV stack: merge while the chunk count below this point is odd;
@@ -506,6 +550,58 @@ __global__ __launch_bounds__(256) void bao_parent_kernel(ParentArgs a) {
     }
 }
 
+struct CheckArgs {
+    const uint8_t *stream;
+    uint64_t stream_stride, N, count, nparents;
+    const uint8_t *hash;  // expected root hashes [count][32]
+    uint8_t *flags;       // [count][nparents], indexed in stream (pre-)order
+};
+
+// K5b: every parent node re-hashed from its STORED 64 bytes and compared with
+// the copy in its own parent (the root: with the hash).  Independent per node,
+// so one launch checks the whole tree; flags are indexed in stream order,
+// pidx = P(s) + c(s) - level.
+__global__ __launch_bounds__(256) void bao_parent_check_kernel(CheckArgs a) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= a.count * a.nparents) return;
+    const uint64_t obj = gid / a.nparents;
+    uint64_t r = gid - obj * a.nparents, cnt = a.N;
+    int level = 1;
+    for (;; ++level) {  // locate (level, q) of the r-th parent in level order
+        const uint64_t np = cnt / 2;
+        if (r < np) break;
+        r -= np;
+        cnt = (cnt + 1) / 2;
+    }
+    const uint64_t sx = r << level;
+    const uint8_t *st = a.stream + obj * a.stream_stride;
+    const uint64_t pidx = parents_before(sx, a.N) + parents_at(sx, a.N) - level;
+    const uint8_t *node = st + 8 + 1024 * sx + 64 * pidx;
+    uint32_t l[8], rr[8], cv[8];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const u32x2 x = reinterpret_cast<const u32x2 *>(node)[w];
+        const u32x2 y = reinterpret_cast<const u32x2 *>(node + 32)[w];
+        l[2 * w] = x.x; l[2 * w + 1] = x.y; rr[2 * w] = y.x; rr[2 * w + 1] = y.y;
+    }
+    const bool root = (cnt + 1) / 2 == 1;  // this level has a single node
+    b3_parent(l, rr, root, cv);
+    bool ok;
+    if (root) {
+        ok = true;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const uint32_t e = (uint32_t)a.hash[obj * 32 + 4 * w] | (uint32_t)a.hash[obj * 32 + 4 * w + 1] << 8 |
+                               (uint32_t)a.hash[obj * 32 + 4 * w + 2] << 16 |
+                               (uint32_t)a.hash[obj * 32 + 4 * w + 3] << 24;
+            ok &= e == cv[w];
+        }
+    } else {
+        ok = stored_slot_matches(st, sx, level, a.N, cv);
+    }
+    a.flags[obj * a.nparents + pidx] = ok ? 1 : 0;
+}
+
 __host__ __device__ inline uint64_t n_chunks(uint64_t n) { return n == 0 ? 1 : (n + 1023) / 1024; }
 
 template <int CPL>
@@ -558,6 +654,44 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
         std::swap(sp, sn);
     }
     return hipSuccess;
+}
+
+// Gather the content of chunks [c0, c1) of one stream into a contiguous buffer
+// (the inverse of the layout: strips the interleaved parent nodes).
+__global__ __launch_bounds__(256) void bao_gather_kernel(const uint8_t *stream, uint64_t n, uint64_t N,
+                                                         uint64_t c0, uint64_t c1, uint8_t *out) {
+    const uint64_t bytes = (c1 * 1024 < n ? c1 * 1024 : n) - c0 * 1024;
+    for (uint64_t b = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; b < bytes;
+         b += (uint64_t)gridDim.x * 256 * 16) {
+        const uint64_t ci = c0 + b / 1024;
+        const uint8_t *src = stream + chunk_stream_off(ci, N) + (b % 1024);
+        if (b + 16 <= bytes) {
+            *reinterpret_cast<u32x4 *>(out + b) = load16_a8(src);
+        } else {
+            for (uint64_t q = 0; b + q < bytes; ++q) out[b + q] = src[q];
+        }
+    }
+}
+
+// Per-node verification flags of `count` streams of content length n:
+// chunk_flags [count][N], parent_flags [count][N-1] (stream order).
+template <int BAO_NTS_UNUSED = 0>
+hipError_t run_node_check(const uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count,
+                          const uint8_t *d_hash, uint8_t *chunk_flags, uint8_t *parent_flags, hipStream_t stream) {
+    const uint64_t N = n_chunks(n);
+    ChunkArgs ca;
+    ca.in = d_stream; ca.out = nullptr; ca.in_stride = stride; ca.out_stride = 0;
+    ca.n = n; ca.N = N; ca.count = count; ca.cv = chunk_flags; ca.cv_stride = N;
+    ca.hash = const_cast<uint8_t *>(d_hash); ca.status = nullptr;
+    const uint64_t waves = count * ((N + 63) / 64);
+    hipLaunchKernelGGL((bao_chunk_kernel<2, 1, false>), dim3((unsigned)((waves + K3_WAVES - 1) / K3_WAVES)),
+                       dim3(K3_TPB), 0, stream, ca);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || N < 2) return e;
+    CheckArgs pa{d_stream, stride, N, count, N - 1, d_hash, parent_flags};
+    const uint64_t work = count * (N - 1);
+    hipLaunchKernelGGL(bao_parent_check_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, pa);
+    return hipGetLastError();
 }
 
 }  // namespace bao

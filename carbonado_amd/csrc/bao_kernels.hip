@@ -66,4 +66,27 @@ hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
                       d_status, d_scratch, stream);
 }
 
+hipError_t bao_node_check(const uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count,
+                          const uint8_t *d_hash, uint8_t *chunk_flags, uint8_t *parent_flags, hipStream_t stream) {
+    return run_node_check(d_stream, stride, n, count, d_hash, chunk_flags, parent_flags, stream);
+}
+
+hipError_t bao_gather_content(const uint8_t *d_stream, uint64_t n, uint64_t c0, uint64_t c1, uint8_t *d_out,
+                              hipStream_t stream) {
+    const uint64_t N = n_chunks(n);
+    if (c1 > N) c1 = N;
+    if (c0 >= c1 || c0 * 1024 >= n) return hipSuccess;
+    const uint64_t bytes = (c1 * 1024 < n ? c1 * 1024 : n) - c0 * 1024;
+    uint64_t blocks = (bytes / 16 + 255) / 256;
+    blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
+    hipLaunchKernelGGL(bao_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d_stream, n, N, c0, c1, d_out);
+    return hipGetLastError();
+}
+
+uint64_t bao_chunk_offset(uint64_t i, uint64_t N) { return chunk_stream_off(i, N); }
+uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N) { return parent_stream_off(s, level, N); }
+uint64_t bao_parent_index(uint64_t s, int level, uint64_t N) {
+    return parents_before(s, N) + parents_at(s, N) - level;
+}
+
 }  // namespace chip

@@ -60,11 +60,11 @@ struct Slot {
 struct Ctx {
     bool ready = false;
     hipStream_t stream = nullptr;
-    DevBuf in, mid, out, scratch, small;
+    DevBuf in, mid, out, scratch, small, x1, x2, flags;
     std::vector<Slot> slots;
     ~Ctx() {
         // process teardown: the runtime may already be gone; best effort
-        for (DevBuf *b : {&in, &mid, &out, &scratch, &small})
+        for (DevBuf *b : {&in, &mid, &out, &scratch, &small, &x1, &x2, &flags})
             if (b->p) (void)hipFree(b->p);
         if (stream) (void)hipStreamDestroy(stream);
         for (Slot &sl : slots) {
@@ -214,6 +214,50 @@ int select_shares(uint32_t k, uint32_t m, const uint32_t *idx, uint32_t nshares,
     return sel_pos->size() == k ? CHIP_OK : CHIP_ERR_ZFEC;
 }
 
+uint64_t n_chunks_of(uint64_t n) { return n == 0 ? 1 : (n + 1023) / 1024; }
+
+int ceil_log2_u64(uint64_t x) { return x <= 1 ? 0 : 64 - __builtin_clzll(x - 1); }
+
+// chunk range [c0, c1) of a slice request, bao's rules
+void slice_chunks(uint64_t n, uint64_t start, uint64_t len, uint64_t *c0, uint64_t *c1) {
+    const uint64_t N = n_chunks_of(n);
+    uint64_t a = start / 1024;
+    if (a >= N) a = N - 1;
+    uint64_t end = start + len;  // exclusive byte end
+    uint64_t b = end / 1024 + (end % 1024 ? 1 : 0);
+    if (b > N) b = N;
+    if (b < a + 1) b = a + 1;
+    *c0 = a;
+    *c1 = b;
+}
+
+struct SliceNode {
+    bool parent;
+    uint64_t off, len, index;  // stream offset, bytes, chunk index or parent index (stream order)
+};
+
+// pre-order walk of the nodes whose subtree intersects chunks [c0, c1)
+void slice_nodes(uint64_t n, uint64_t c0, uint64_t c1, std::vector<SliceNode> *out) {
+    const uint64_t N = n_chunks_of(n);
+    struct Item { uint64_t s, cnt; };
+    std::vector<Item> stack{{0, N}};
+    while (!stack.empty()) {
+        const Item it = stack.back();
+        stack.pop_back();
+        if (it.s >= c1 || it.s + it.cnt <= c0) continue;
+        if (it.cnt == 1) {
+            const uint64_t len = (it.s + 1) * 1024 <= n ? 1024 : n - it.s * 1024;
+            out->push_back({false, bao_chunk_offset(it.s, N), len, it.s});
+            continue;
+        }
+        const int level = ceil_log2_u64(it.cnt);
+        out->push_back({true, bao_parent_offset(it.s, level, N), 64, bao_parent_index(it.s, level, N)});
+        const uint64_t left = 1ull << (level - 1);
+        stack.push_back({it.s + left, it.cnt - left});  // right after left (LIFO)
+        stack.push_back({it.s, left});
+    }
+}
+
 // EncodeInfo of encode() for format bits Bao|Zfec (encoding.rs:86-172); no device
 int encode_info_for(uint8_t format, uint64_t n, chip_encode_info *inf, uint64_t *zlen, uint64_t *final_len) {
     std::memset(inf, 0, sizeof *inf);
@@ -262,6 +306,10 @@ const char *chip_strerror(int st) {
         case CHIP_ERR_ENCODE_INVALID_CHUNK_LENGTH: return "Chunk length should be as calculated.";
         case CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT: return "Verifiable slice count should be evenly divisible by 8.";
         case CHIP_ERR_UNSUPPORTED_FORMAT: return "format bit handled by a host stage outside this path (ecies/snappy)";
+        case CHIP_ERR_UNNECESSARY_SCRUB: return "Data does not need to be scrubbed.";
+        case CHIP_ERR_SCRUBBED_PADDING_MISMATCH: return "Scrubbed padding should remain the same.";
+        case CHIP_ERR_SCRUBBED_LENGTH_MISMATCH: return "Mismatch between scrubbed data length and input length";
+        case CHIP_ERR_INVALID_SCRUBBED_HASH: return "Scrubbed hash is not equal to original hash.";
         case CHIP_ERR_NO_DEVICE: return "no usable gfx950 device";
         case CHIP_ERR_DEVICE: return "HIP runtime error";
         default: return "unknown status";
@@ -549,6 +597,176 @@ int chip_bao_decode(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint6
     if (n) CHIP_HIP(hipMemcpyAsync(out, c->out.p, n, hipMemcpyDeviceToHost, c->stream));
     CHIP_HIP(hipStreamSynchronize(c->stream));
     *out_len = n;
+    return CHIP_OK;
+}
+
+// ---- slices and scrub (decoding.rs:116-212) ----------------------------------
+
+// node check of one host stream (already H2D'd to c->in); flags to host
+static int node_check_ctx(Ctx *c, uint64_t n, const uint8_t *hash, std::vector<uint8_t> *cf,
+                          std::vector<uint8_t> *pf) {
+    const uint64_t N = n_chunks_of(n);
+    CHIP_HIP(grow(c->small, 64));
+    CHIP_HIP(grow(c->flags, 2 * N + 16));
+    uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
+    uint8_t *d_cf = static_cast<uint8_t *>(c->flags.p), *d_pf = d_cf + N;
+    CHIP_HIP(hipMemcpyAsync(d_hash, hash, 32, hipMemcpyHostToDevice, c->stream));
+    CHIP_HIP(bao_node_check(static_cast<const uint8_t *>(c->in.p), 0, n, 1, d_hash, d_cf, d_pf, c->stream));
+    cf->resize(N);
+    pf->resize(N - 1);
+    CHIP_HIP(hipMemcpyAsync(cf->data(), d_cf, N, hipMemcpyDeviceToHost, c->stream));
+    if (N > 1) CHIP_HIP(hipMemcpyAsync(pf->data(), d_pf, N - 1, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    return CHIP_OK;
+}
+
+static bool slice_ok(uint64_t n, uint64_t c0, uint64_t c1, const std::vector<uint8_t> &cf,
+                     const std::vector<uint8_t> &pf) {
+    std::vector<SliceNode> nodes;
+    slice_nodes(n, c0, c1, &nodes);
+    for (const SliceNode &sn : nodes)
+        if (!(sn.parent ? pf[sn.index] : cf[sn.index])) return false;
+    return true;
+}
+
+uint64_t chip_bao_slice_len(uint64_t n, uint64_t start, uint64_t len) {
+    uint64_t c0, c1, total = 8;
+    slice_chunks(n, start, len, &c0, &c1);
+    std::vector<SliceNode> nodes;
+    slice_nodes(n, c0, c1, &nodes);
+    for (const SliceNode &sn : nodes) total += sn.len;
+    return total;
+}
+
+int chip_bao_extract_slice(const uint8_t *enc, uint64_t len, uint64_t index, uint64_t slice_len, uint8_t *out,
+                           uint64_t out_cap, uint64_t *out_len) {
+    if (!out_len || (!enc && len)) return CHIP_ERR_INVALID_ARG;
+    if (index > (~0ull >> 10)) return CHIP_ERR_INVALID_ARG;
+    uint64_t n;
+    int st = bao_header(enc, len, &n);
+    if (st != CHIP_OK) return st;
+    uint64_t c0, c1;
+    slice_chunks(n, index * 1024, slice_len, &c0, &c1);
+    std::vector<SliceNode> nodes;
+    slice_nodes(n, c0, c1, &nodes);
+    uint64_t total = 8;
+    for (const SliceNode &sn : nodes) total += sn.len;
+    if (!out || out_cap < total) return CHIP_ERR_BUFFER_TOO_SMALL;
+    std::memcpy(out, enc, 8);  // the length header, then the nodes in pre-order
+    uint64_t w = 8;
+    for (const SliceNode &sn : nodes) {
+        std::memcpy(out + w, enc + sn.off, sn.len);
+        w += sn.len;
+    }
+    *out_len = total;
+    return CHIP_OK;
+}
+
+int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const uint8_t *enc, uint64_t len,
+                          uint64_t index, uint64_t count, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if (!out_len || (!enc && len)) return CHIP_ERR_INVALID_ARG;
+    if (!hash || hash_len != CHIP_HASH_LEN) return CHIP_ERR_HASH_DECODE;
+    if (index > (~0ull >> 11) || count > (~0ull >> 11)) return CHIP_ERR_INVALID_ARG;
+    uint64_t n;
+    int st = bao_header(enc, len, &n);
+    if (st != CHIP_OK) return st;
+    const uint64_t start = index * 1024, slen = count * 1024;  // decoding.rs:138-139 (u64 maths)
+    const uint64_t end = start + slen < n ? start + slen : n;
+    const uint64_t olen = start < n ? end - start : 0;
+    if (olen && (!out || out_cap < olen)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    Ctx *c;
+    st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    const uint64_t blen = bao_encoded_len(n);
+    CHIP_HIP(grow(c->in, blen));
+    CHIP_HIP(hipMemcpyAsync(c->in.p, enc, blen, hipMemcpyHostToDevice, c->stream));
+    std::vector<uint8_t> cf, pf;
+    st = node_check_ctx(c, n, hash, &cf, &pf);
+    if (st != CHIP_OK) return st;
+    uint64_t c0, c1;
+    slice_chunks(n, start, slen, &c0, &c1);
+    if (!slice_ok(n, c0, c1, cf, pf)) return CHIP_ERR_BAO_HASH_MISMATCH;
+    if (olen) {
+        const uint64_t g0 = start / 1024, g1 = (end + 1023) / 1024;
+        CHIP_HIP(grow(c->out, (g1 - g0) * 1024));
+        CHIP_HIP(bao_gather_content(static_cast<const uint8_t *>(c->in.p), n, g0, g1,
+                                    static_cast<uint8_t *>(c->out.p), c->stream));
+        CHIP_HIP(hipMemcpyAsync(out, static_cast<uint8_t *>(c->out.p) + (start - g0 * 1024), olen,
+                                hipMemcpyDeviceToHost, c->stream));
+        CHIP_HIP(hipStreamSynchronize(c->stream));
+    }
+    *out_len = olen;
+    return CHIP_OK;
+}
+
+int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t hash_len, uint32_t padding,
+               uint32_t chunk_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if (!out_len || (!enc && len)) return CHIP_ERR_INVALID_ARG;
+    if (!hash || hash_len != CHIP_HASH_LEN) return CHIP_ERR_HASH_DECODE;  // decoding.rs:164
+    uint64_t n;
+    int st = bao_header(enc, len, &n);
+    if (st != CHIP_OK) return st;
+    Ctx *c;
+    st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    const uint64_t blen = bao_encoded_len(n);
+    CHIP_HIP(grow(c->in, blen));
+    CHIP_HIP(hipMemcpyAsync(c->in.p, enc, blen, hipMemcpyHostToDevice, c->stream));
+    std::vector<uint8_t> cf, pf;
+    st = node_check_ctx(c, n, hash, &cf, &pf);
+    if (st != CHIP_OK) return st;
+    bool all = true;
+    for (uint8_t f : cf) all &= f != 0;
+    for (uint8_t f : pf) all &= f != 0;
+    if (all) return CHIP_ERR_UNNECESSARY_SCRUB;  // decoding.rs:169-170
+    const uint64_t C = chunk_len;
+    if (C == 0 || C % 1024 || n != (uint64_t)CHIP_FEC_M * C) return CHIP_ERR_ZFEC;
+    const uint64_t spc = C / 1024;  // slices per chunk, decoding.rs:166
+    std::vector<uint32_t> good;
+    for (uint32_t i = 0; i < CHIP_FEC_M; ++i)  // decoding.rs:173-183
+        if (slice_ok(n, i * spc, (i + 1) * spc, cf, pf)) good.push_back(i);
+    if (good.size() < CHIP_FEC_K) return CHIP_ERR_ZFEC;
+    const uint64_t kc = (uint64_t)CHIP_FEC_K * C;
+    if (padding > kc) return CHIP_ERR_ZFEC;
+    // content of all shards, parents stripped
+    CHIP_HIP(grow(c->mid, n));
+    uint8_t *d_z = static_cast<uint8_t *>(c->mid.p);
+    CHIP_HIP(bao_gather_content(static_cast<const uint8_t *>(c->in.p), n, 0, n_chunks_of(n), d_z, c->stream));
+    // zfec decode from the good shards, TRUE indices (decoding.rs:187)
+    std::vector<uint32_t> pos;
+    st = select_shares(CHIP_FEC_K, CHIP_FEC_M, good.data(), (uint32_t)good.size(), &pos);
+    if (st != CHIP_OK) return st;
+    std::vector<uint32_t> sel(CHIP_FEC_K);
+    std::vector<uint64_t> slot_off(CHIP_FEC_K);
+    for (uint32_t s2 = 0; s2 < CHIP_FEC_K; ++s2) { sel[s2] = good[pos[s2]]; slot_off[s2] = sel[s2] * C; }
+    CHIP_HIP(grow(c->x1, kc));
+    uint8_t *d_dec = static_cast<uint8_t *>(c->x1.p);
+    st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_z, 0, slot_off, sel, C, 1, d_dec, 0, c->stream);
+    if (st != CHIP_OK) return st;
+    const uint64_t dl = kc - padding;
+    // re-encode: encoding::zfec then encoding::bao (decoding.rs:191-196)
+    uint32_t pad2;
+    uint64_t C2;
+    calc_pad(dl, CHIP_FEC_K, &pad2, &C2);
+    if (pad2 != padding) return CHIP_ERR_SCRUBBED_PADDING_MISMATCH;  // decoding.rs:192-194
+    CHIP_HIP(grow(c->x2, CHIP_FEC_M * C2));
+    uint8_t *d_z2 = static_cast<uint8_t *>(c->x2.p);
+    {
+        GfPlan p = encode_plan(CHIP_FEC_K, CHIP_FEC_M, C2, zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M));
+        GfLaunch L{d_dec, d_z2, 0, 0, dl, C2, 1};
+        CHIP_HIP(gf_apply(p, L, c->stream));
+    }
+    uint8_t h2[32];
+    st = bao_encode_ctx(c, d_z2, CHIP_FEC_M * C2, true, h2);
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    const uint64_t blen2 = bao_encoded_len(CHIP_FEC_M * C2);
+    if (blen2 != len) return CHIP_ERR_SCRUBBED_LENGTH_MISMATCH;  // decoding.rs:198-203
+    if (std::memcmp(h2, hash, 32) != 0) return CHIP_ERR_INVALID_SCRUBBED_HASH;  // decoding.rs:205-207
+    if (!out || out_cap < blen2) return CHIP_ERR_BUFFER_TOO_SMALL;
+    CHIP_HIP(hipMemcpyAsync(out, c->out.p, blen2, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    *out_len = blen2;
     return CHIP_OK;
 }
 

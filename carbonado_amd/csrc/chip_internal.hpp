@@ -70,6 +70,19 @@ hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
                           const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                           uint32_t *d_status, void *d_scratch, hipStream_t stream);
 
+// Per-node bao verification (K5b): chunk_flags [count][N], parent_flags
+// [count][N-1] in stream order; 1 = the node matches the copy stored in its
+// parent (the root: the hash).
+hipError_t bao_node_check(const uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count,
+                          const uint8_t *d_hash, uint8_t *chunk_flags, uint8_t *parent_flags, hipStream_t stream);
+// Content of chunks [c0, c1) of one stream, parents stripped, to d_out.
+hipError_t bao_gather_content(const uint8_t *d_stream, uint64_t n, uint64_t c0, uint64_t c1, uint8_t *d_out,
+                              hipStream_t stream);
+// Stream layout (host side, same formulas as the kernels).
+uint64_t bao_chunk_offset(uint64_t i, uint64_t N);
+uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N);
+uint64_t bao_parent_index(uint64_t s, int level, uint64_t N);
+
 // ---- context ------------------------------------------------------------
 int ensure_device();                 // CHIP_OK or CHIP_ERR_NO_DEVICE
 void set_device_error(hipError_t e); // remember for chip_last_device_error

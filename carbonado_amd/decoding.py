@@ -74,3 +74,51 @@ def decode(secret_key: bytes, hash: bytes, input, padding: int, format: int) -> 
     check(_lib.lib().chip_decode(ptr(h), h.size, ptr(a), a.size, padding, int(fmt), ptr(out), cap,
                                  ctypes.byref(olen)))
     return out[: olen.value].tobytes()
+
+
+def extract_slice(encoded, index: int, slice_len: int = 1024) -> bytes:
+    """decoding.rs:116-127 `extract_slice(encoded, index)`: the bao slice
+    (header, parents on the path, chunks) of 1 KiB slice `index`.  The
+    reference multiplies `index * SLICE_LEN` in u16 (wraps for index >= 64);
+    this takes the index as an unbounded integer."""
+    a = as_u8(encoded)
+    n = int.from_bytes(a[:8].tobytes(), "little") if a.size >= 8 else 0
+    L = _lib.lib()
+    cap = L.chip_bao_slice_len(n, index * 1024, slice_len) if a.size >= 8 else 0
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    olen = ctypes.c_uint64()
+    check(L.chip_bao_extract_slice(ptr(a), a.size, index, slice_len, ptr(out), cap, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def verify_slice(hash: bytes, input, index: int, count: int) -> bytes:
+    """decoding.rs:129-149 `verify_slice(hash, input, index, count)`: verify
+    `count` 1 KiB slices from slice `index` of the combined encoding and return
+    their content (the nodes are re-hashed on the device)."""
+    if len(hash) != HASH_SIZE:
+        raise HashDecodeError(HASH_SIZE, len(hash))
+    a = as_u8(input)
+    h = as_u8(hash)
+    cap = count * 1024
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    olen = ctypes.c_uint64()
+    check(_lib.lib().chip_bao_verify_slice(ptr(h), h.size, ptr(a), a.size, index, count, ptr(out), cap,
+                                           ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def scrub(input, hash: bytes, encode_info) -> bytes:
+    """decoding.rs:151-212 `scrub(input, hash, encode_info)`: repair a level
+    12/14/15 stream from its intact shards.  Raises UnnecessaryScrub when the
+    stream verifies.  Surviving shards are decoded with their true indices
+    (the reference numbers them by position, which only works while the lost
+    shards are parity shards)."""
+    if len(hash) != HASH_SIZE:
+        raise HashDecodeError(HASH_SIZE, len(hash))
+    a = as_u8(input)
+    h = as_u8(hash)
+    out = np.empty(max(a.size, 1), dtype=np.uint8)
+    olen = ctypes.c_uint64()
+    check(_lib.lib().chip_scrub(ptr(a), a.size, ptr(h), h.size, encode_info.padding_len, encode_info.chunk_len,
+                                ptr(out), a.size, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()

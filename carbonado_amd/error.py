@@ -63,6 +63,29 @@ class UnsupportedFormat(CarbonadoError):
     status = 11
 
 
+class UnnecessaryScrub(CarbonadoError):
+    """error.rs:65-67"""
+    status = 12
+
+    def __init__(self, msg="Data does not need to be scrubbed."):
+        super().__init__(msg)
+
+
+class ScrubbedPaddingMismatch(CarbonadoError):
+    """error.rs:69-71"""
+    status = 13
+
+
+class ScrubbedLengthMismatch(CarbonadoError):
+    """error.rs:73-75"""
+    status = 14
+
+
+class InvalidScrubbedHash(CarbonadoError):
+    """error.rs:81-83"""
+    status = 15
+
+
 class BufferTooSmall(CarbonadoError):
     status = 2
 
@@ -95,6 +118,14 @@ def status_to_error(status: int, detail: str = "") -> CarbonadoError:
         return InvalidVerifiableSliceCount("Verifiable slice count should be evenly divisible by 8.")
     if status == 11:
         return UnsupportedFormat("format bit handled by a host stage outside this path")
+    if status == 12:
+        return UnnecessaryScrub()
+    if status == 13:
+        return ScrubbedPaddingMismatch("Scrubbed padding should remain the same.")
+    if status == 14:
+        return ScrubbedLengthMismatch("Mismatch between scrubbed data length and input length")
+    if status == 15:
+        return InvalidScrubbedHash("Scrubbed hash is not equal to original hash.")
     if status == 2:
         return BufferTooSmall("output buffer too small")
     if status == 1:

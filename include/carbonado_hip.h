@@ -76,6 +76,10 @@ typedef enum chip_status {
     CHIP_ERR_ENCODE_INVALID_CHUNK_LENGTH = 9, /* error.rs:89-91 */
     CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT = 10, /* error.rs:93-95 */
     CHIP_ERR_UNSUPPORTED_FORMAT = 11,/* Ecies/Snappy bits: host stages, not on this path */
+    CHIP_ERR_UNNECESSARY_SCRUB = 12, /* CarbonadoError::UnnecessaryScrub       error.rs:65-67 */
+    CHIP_ERR_SCRUBBED_PADDING_MISMATCH = 13, /* ScrubbedPaddingMismatch         error.rs:69-71 */
+    CHIP_ERR_SCRUBBED_LENGTH_MISMATCH = 14,  /* ScrubbedLengthMismatch          error.rs:73-75 */
+    CHIP_ERR_INVALID_SCRUBBED_HASH = 15,     /* InvalidScrubbedHash             error.rs:81-83 */
     CHIP_ERR_NO_DEVICE = 100,        /* new variant: no usable gfx950 device     */
     CHIP_ERR_DEVICE = 101            /* new variant: HIP runtime error            */
 } chip_status;
@@ -195,6 +199,33 @@ CHIP_API int chip_bao_encode_batch_dev(const uint8_t *d_in, uint64_t in_stride, 
 CHIP_API int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                               const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                               uint32_t *d_status, void *d_scratch, void *stream);
+
+/* ---- slices and scrub (decoding.rs:116-212) ----------------------------- */
+/* Chunk range of a bao slice request [start, start+len) over n content bytes,
+ * bao's rules: at least one chunk; a start at/after the end selects the last
+ * chunk.  Byte length of the extracted slice (header + parents + chunks). */
+CHIP_API uint64_t chip_bao_slice_len(uint64_t content_len, uint64_t start, uint64_t len);
+/* extract_slice (decoding.rs:116-127) with a u64 slice index (the reference
+ * computes `index * SLICE_LEN` in u16, which wraps for index >= 64): the bao
+ * slice for content bytes [index*1024, index*1024 + slice_len) of the
+ * combined encoding `enc`.  Pure byte selection along the tree. */
+CHIP_API int chip_bao_extract_slice(const uint8_t *enc, uint64_t len, uint64_t index, uint64_t slice_len,
+                                    uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+/* verify_slice (decoding.rs:129-149): verify the `count` 1 KiB slices starting
+ * at slice `index` of the combined encoding against `hash` (every chunk in the
+ * range and every parent above it, re-hashed on the device) and return their
+ * content.  Corruption outside the range does not fail the slice. */
+CHIP_API int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const uint8_t *enc, uint64_t len,
+                                   uint64_t index, uint64_t count, uint8_t *out, uint64_t out_cap,
+                                   uint64_t *out_len);
+/* scrub (decoding.rs:151-212) for a level-12/14/15 stream: if the stream
+ * verifies -> CHIP_ERR_UNNECESSARY_SCRUB; else verify each of the 8 shards'
+ * slices, zfec-decode from the good shards with their TRUE share indices
+ * (the reference numbers survivors by position, decoding.rs:187 -> :24-25),
+ * re-encode zfec + bao and return the stream if its length and hash match.
+ * out must hold `len` bytes. */
+CHIP_API int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t hash_len,
+                        uint32_t padding, uint32_t chunk_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 
 /* ---- host-memory batch (end-to-end: host -> HBM -> host) -------------- */
 /* encode() for `count` objects of n bytes that live in HOST memory (object o

@@ -240,3 +240,34 @@ def bao_encode(data: bytes) -> tuple[bytes, bytes]:
 
     root = rec(0, len(data), True)
     return b"".join(parts), struct.pack("<8I", *root)
+
+
+def bao_slice(encoded: bytes, start: int, length: int) -> bytes:
+    """bao combined-encoding slice: header + pre-order parents/chunks whose
+    subtree overlaps [start, start+length); at least one chunk; a start at or
+    past the end selects the final chunk."""
+    n = struct.unpack("<Q", encoded[:8])[0]
+    chunks = max(1, -(-n // 1024))
+    first = min(start // 1024, chunks - 1)
+    last = max(first + 1, min(-(-(start + length) // 1024), chunks))  # exclusive
+    out = [encoded[:8]]
+    pos = 8
+
+    def walk(c_lo, c_cnt):
+        nonlocal pos
+        if c_cnt == 1:
+            size = min(1024, n - c_lo * 1024) if n else 0
+            if first <= c_lo < last:
+                out.append(encoded[pos:pos + size])
+            pos += size
+            return
+        left = 1 << ((c_cnt - 1).bit_length() - 1)
+        hit = c_lo < last and c_lo + c_cnt > first
+        if hit:
+            out.append(encoded[pos:pos + 64])
+        pos += 64
+        walk(c_lo, left)
+        walk(c_lo + left, c_cnt - left)
+
+    walk(0, chunks)
+    return b"".join(out)
