@@ -41,15 +41,21 @@ template <int NG> struct Entry;
 template <> struct Entry<1> { using T = uint32_t; };
 template <> struct Entry<2> { using T = u32x2; };
 
+// 16 bytes at base+off with bytes at or past `valid` zeroed.  base+off is
+// 16-B aligned (the C-ABI requires aligned pointers and strides), so the
+// aligned block holding any valid byte lies inside a mapped page: one vector
+// load + a byte mask, no byte-wise loads (they inflated K=8 to 350+ VGPRs).
 __device__ __forceinline__ u32x4 load16_masked(const uint8_t *base, uint64_t off, uint64_t valid) {
-    if (off + VEC <= valid) return *reinterpret_cast<const u32x4 *>(base + off);
-    u32x4 r = {0u, 0u, 0u, 0u};
-    if (off >= valid) return r;
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int i = 0; i < VEC; ++i)
-        if (off + i < valid) w[i >> 2] |= (uint32_t)base[off + i] << (8 * (i & 3));
-    r.x = w[0]; r.y = w[1]; r.z = w[2]; r.w = w[3];
+    if (off >= valid) return u32x4{0u, 0u, 0u, 0u};
+    u32x4 r = *reinterpret_cast<const u32x4 *>(base + off);
+    if (off + VEC > valid) {
+        const int rem = (int)(valid - off);  // 1..15
+        auto keep = [rem](int i) -> uint32_t {
+            const int b = rem - 4 * i;
+            return b >= 4 ? ~0u : b <= 0 ? 0u : ((1u << (8 * b)) - 1u);
+        };
+        r.x &= keep(0); r.y &= keep(1); r.z &= keep(2); r.w &= keep(3);
+    }
     return r;
 }
 
@@ -124,9 +130,12 @@ struct TileIter {
     }
 };
 
-template <int K, int NG, int U, int MAP, bool NT>
-__global__ __launch_bounds__(TPB) void gf_apply_kernel(ApplyArgs a) {
-    constexpr int R = replicas_for(K);
+// RO: replica-count override, WPE: waves/EU hint, SB: scheduling fence every SB
+// shards (bounds the table lookups in flight; 0 = none), PF: load the next
+// super-tile's shards before computing the current one — tools/zfec_tune.
+template <int K, int NG, int U, int MAP, bool NT, int RO = 0, int WPE = 1, int SB = 0, bool PF = false>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_kernel(ApplyArgs a) {
+    constexpr int R = RO ? RO : replicas_for(K);
     using E = typename Entry<NG>::T;
     constexpr int W = 4 * NG;            // bytes per table entry
     constexpr int ROWB = K * R * W;      // bytes per table row (one byte value x)
@@ -160,14 +169,10 @@ __global__ __launch_bounds__(TPB) void gf_apply_kernel(ApplyArgs a) {
     // super-tiles of U adjacent column tiles of one object
     const uint64_t spo = (a.tiles_per_obj + U - 1) / U;
     TileIter<MAP> iter(spo * a.count, a.chunk);
-    uint64_t st;
-    while (iter.next(st)) {
-        const uint64_t obj = st / spo;
-        const uint64_t col0 = (st - obj * spo) * (uint64_t)(U * TILE) + threadIdx.x * VEC;
+    auto load_tile = [&](uint64_t t, u32x4 (&v)[U][K]) {
+        const uint64_t obj = t / spo;
+        const uint64_t col0 = (t - obj * spo) * (uint64_t)(U * TILE) + threadIdx.x * VEC;
         const uint8_t *ib = a.in + obj * a.in_stride;
-        uint8_t *ob = a.out + obj * a.out_stride;
-
-        u32x4 v[U][K];
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -175,6 +180,24 @@ __global__ __launch_bounds__(TPB) void gf_apply_kernel(ApplyArgs a) {
                 const uint64_t col = col0 + (uint64_t)u * TILE;
                 v[u][j] = col < a.C ? load16_masked(ib, ioff[j] + col, a.valid) : u32x4{0u, 0u, 0u, 0u};
             }
+    };
+
+    uint64_t st;
+    bool have = iter.next(st);
+    u32x4 v[U][K];
+    if (PF && have) load_tile(st, v);
+    while (have) {
+        uint64_t st_next;
+        const bool have_next = iter.next(st_next);
+        u32x4 vn[U][K];
+        if constexpr (PF) {
+            if (have_next) load_tile(st_next, vn);
+        } else {
+            load_tile(st, v);
+        }
+        const uint64_t obj = st / spo;
+        const uint64_t col0 = (st - obj * spo) * (uint64_t)(U * TILE) + threadIdx.x * VEC;
+        uint8_t *ob = a.out + obj * a.out_stride;
 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -195,6 +218,14 @@ __global__ __launch_bounds__(TPB) void gf_apply_kernel(ApplyArgs a) {
                         else acc[d * 4 + b] ^= e;
                     }
                 }
+                // Pin the partial sums every SB shards: otherwise LLVM's
+                // reassociation rebuilds each K-term XOR chain at its root, so
+                // all K*16 lookups are live at once (K=8: 350+ VGPRs, spills).
+                if constexpr (SB > 0)
+                    if ((j + 1) % SB == 0 && j + 1 < K) {
+#pragma unroll
+                        for (int c = 0; c < 16; ++c) asm volatile("" : "+v"(acc[c]));
+                    }
             }
 
             // copies (data shards for encode, surviving primaries for decode)
@@ -226,6 +257,14 @@ __global__ __launch_bounds__(TPB) void gf_apply_kernel(ApplyArgs a) {
                 }
             }
         }
+        if constexpr (PF) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < K; ++j) v[u][j] = vn[u][j];
+        }
+        st = st_next;
+        have = have_next;
     }
 }
 

@@ -92,8 +92,18 @@ constexpr int ZF_MAP = 3;
 constexpr bool ZF_NT = true;
 constexpr uint64_t ZF_CHUNK = 64;
 
+// Wide stripes (K > 4): pin the XOR partial sums every shard (SB = 1) so the
+// K*16 table lookups are not all live at once — without it K = 8 compiles to
+// 256 VGPR + 90 AGPR, one wave per SIMD — and prefetch the next tile's shards
+// into registers (K <= 8; K = 16 has no registers to spare).  8 computed rows (NG = 2): plain stores measured +1-3% over
+// nontemporal at 2 workgroups/CU (tools/zfec_tune, 8-of-16 sweep in DESIGN.md).
 template <int K, int NG>
-KernelFn kernel_ptr() { return gf_apply_kernel<K, NG, ZF_U, ZF_MAP, ZF_NT>; }
+KernelFn kernel_ptr() {
+    if constexpr (K > 4)
+        return gf_apply_kernel<K, NG, ZF_U, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
+    else
+        return gf_apply_kernel<K, NG, ZF_U, ZF_MAP, ZF_NT>;
+}
 
 struct KernelInfo {
     KernelFn fn;

@@ -2,7 +2,7 @@
 // per object, read 4 streams (shards at j*C) and write 8 streams (shards at
 // j*SP, SP = C or C + pad), 16 B per lane per stream.  Sweeps workgroup size,
 // tile schedule and store policy.  Calibration tool (not product code).
-//   stream_probe [objects=1024]
+//   stream_probe [objects=1024] [K=4|8]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,7 +28,7 @@ struct Args {
 };
 
 // MAP 0: grid-stride over tiles; 1: XCD-grouped; 3: XCD-grouped chunks of CH tiles
-template <int TPB, int MAP, int CH, bool NT, bool SPLIT>
+template <int TPB, int MAP, int CH, bool NT, bool SPLIT, int KS = 4>
 __global__ __launch_bounds__(TPB) void k_stream(Args a) {
     constexpr uint64_t TILE = TPB * 16;
     const uint64_t tpo = a.C / TILE, T = tpo * a.count;
@@ -50,14 +50,14 @@ __global__ __launch_bounds__(TPB) void k_stream(Args a) {
         const uint64_t col = (t - obj * tpo) * TILE + threadIdx.x * 16;
         const uint8_t *ib = a.in + obj * a.in_stride;
         uint8_t *ob = a.out + obj * a.out_stride;
-        u32x4 v[4];
+        u32x4 v[KS];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = *(const u32x4 *)(ib + j * a.C + col);
+        for (int j = 0; j < KS; ++j) v[j] = *(const u32x4 *)(ib + j * a.C + col);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            u32x4 w = j < 4 ? v[j] : (v[j - 4] ^ 0x01020304u);
+        for (int j = 0; j < 2 * KS; ++j) {
+            u32x4 w = j < KS ? v[j] : (v[j - KS] ^ 0x01020304u);
             uint8_t *p = ob + j * a.SP + col;
-            if (SPLIT && j == 4) __builtin_amdgcn_s_waitcnt(0);
+            if (SPLIT && j == KS) __builtin_amdgcn_s_waitcnt(0);
             if (NT) __builtin_nontemporal_store(w, (u32x4 *)p);
             else *(u32x4 *)p = w;
         }
@@ -66,13 +66,14 @@ __global__ __launch_bounds__(TPB) void k_stream(Args a) {
 
 int main(int argc, char **argv) {
     const uint64_t count = argc > 1 ? atoll(argv[1]) : 1024;
-    const uint64_t C = 4ull << 20, n = 4 * C;
+    const int KS = argc > 2 ? atoi(argv[2]) : 4;  // 4: 4-of-8 pattern, 8: 8-of-16
+    const uint64_t C = (16ull << 20) / KS, n = KS * C;
     uint8_t *in, *out;
     const uint64_t PAD = 64 * 1024 + 4096;  // non-power-of-two shard spacing variant
     CK(hipMalloc(&in, count * n));
-    CK(hipMalloc(&out, count * 8 * (C + PAD)));
+    CK(hipMalloc(&out, count * 2 * KS * (C + PAD)));
     CK(hipMemset(in, 7, count * n));
-    CK(hipMemset(out, 0, count * 8 * (C + PAD)));
+    CK(hipMemset(out, 0, count * 2 * KS * (C + PAD)));
     struct V {
         const char *name;
         void (*fn)(Args);
@@ -81,7 +82,14 @@ int main(int argc, char **argv) {
     };
 #define VV(TPB, MAP, CH, NT, SPLIT, bpc, pad) \
     V{#TPB " MAP" #MAP " CH" #CH " NT" #NT " SPLIT" #SPLIT " bpc" #bpc " pad" #pad, k_stream<TPB, MAP, CH, NT, SPLIT>, TPB, bpc, pad}
-    std::vector<V> vs = {
+#define V8(TPB, MAP, CH, NT, bpc) \
+    V{"K8 " #TPB " MAP" #MAP " CH" #CH " NT" #NT " bpc" #bpc, k_stream<TPB, MAP, CH, NT, false, 8>, TPB, bpc, false}
+    std::vector<V> vs8 = {
+        V8(256, 3, 64, true, 1), V8(256, 3, 64, true, 2), V8(256, 3, 64, true, 4), V8(256, 3, 64, false, 2),
+        V8(256, 3, 16, true, 2), V8(256, 1, 1, true, 2),  V8(256, 3, 64, false, 4), V8(512, 3, 32, true, 1),
+        V8(128, 3, 128, true, 4), V8(128, 3, 128, true, 8),
+    };
+    std::vector<V> vs4 = {
         VV(256, 0, 1, true, false, 4, false),  VV(256, 1, 1, true, false, 4, false),
         VV(256, 3, 64, true, false, 4, false), VV(256, 3, 64, false, false, 4, false),
         VV(256, 1, 1, true, false, 4, true),   VV(256, 3, 64, true, false, 4, true),
@@ -90,13 +98,14 @@ int main(int argc, char **argv) {
         VV(512, 1, 1, true, false, 2, false),  VV(256, 1, 1, true, true, 4, false),
         VV(256, 1, 1, true, false, 2, false),  VV(256, 1, 1, true, false, 8, false),
     };
+    std::vector<V> &vs = KS == 8 ? vs8 : vs4;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<std::vector<float>> ms(vs.size());
     for (int rd = 0; rd < 5; ++rd)
         for (size_t i = 0; i < vs.size(); ++i) {
-            Args a{in, out, C, vs[i].pad ? C + PAD : C, n, 8 * (C + PAD), count};
+            Args a{in, out, C, vs[i].pad ? C + PAD : C, n, 2 * KS * (C + PAD), count};
             const int grid = 256 * vs[i].bpc;
             hipLaunchKernelGGL(vs[i].fn, dim3(grid), dim3(vs[i].tpb), 0, 0, a);
             CK(hipEventRecord(e0));

@@ -50,33 +50,45 @@ struct Variant {
     void (*fn)(ApplyArgs);
     int blocks_per_cu;
     int chunk;
+    size_t lds;
 };
 
-template <int U, int MAP, bool NT, int CH = 1>
+template <int U, int MAP, bool NT, int CH = 1, int WPE = 1, int SB = 0, bool PF = false>
 Variant V(int bpc) {
-    char buf[64];
-    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d %s bpc%d", U, MAP, CH, NT ? "nt " : "pln", bpc);
-    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT>, bpc, CH};
+    char buf[80];
+    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d wpe%d sb%d pf%d %s bpc%d", U, MAP, CH, WPE, SB, PF, NT ? "nt " : "pln", bpc);
+    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT, 0, WPE, SB, PF>, bpc, CH, (size_t)256 * 4 * 8 * 4};
+}
+
+// 8-of-16 variants (K = 8, NG = 2), replica count R
+template <int U, int MAP, bool NT, int R, int CH = 1, int WPE = 1, int SB = 0, bool PF = false>
+Variant V16(int bpc) {
+    char buf[80];
+    snprintf(buf, sizeof buf, "8of16 U%d MAP%d CH%-3d R%d wpe%d sb%d pf%d %s bpc%d", U, MAP, CH, R, WPE, SB, PF, NT ? "nt " : "pln", bpc);
+    return Variant{buf, gf_apply_kernel<8, 2, U, MAP, NT, R, WPE, SB, PF>, bpc, CH, (size_t)256 * 8 * R * 8};
 }
 
 int main(int argc, char **argv) {
     const uint64_t count = argc > 1 ? atoll(argv[1]) : 1024;
     const int rounds = argc > 2 ? atoi(argv[2]) : 5;
-    const uint64_t n = 16ull << 20, C = n / 4;
+    const int shape = argc > 3 ? atoi(argv[3]) : 4;  // 4 = 4-of-8, 8 = 8-of-16
+    const int K = shape == 8 ? 8 : 4, M = 2 * K;
+    const uint64_t n = 16ull << 20, C = n / K;
     uint8_t *in, *out;
     CK(hipMalloc(&in, count * n));
     CK(hipMalloc(&out, count * 2 * n));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xCA4B0AD0ull);
     CK(hipMemset(out, 0, count * 2 * n));
 
-    // packed 4-of-8 parity table [s][x]
-    std::vector<uint8_t> enc = zfec_enc_matrix(4, 8);
+    // packed parity table [s][x] of NG dwords
+    const int NG = K / 4;
+    std::vector<uint8_t> enc = zfec_enc_matrix(K, M);
     const Gf256 &gf = Gf256::get();
-    std::vector<uint32_t> tab(4 * 256, 0);
-    for (int s = 0; s < 4; ++s)
+    std::vector<uint32_t> tab(K * 256 * NG, 0);
+    for (int s = 0; s < K; ++s)
         for (int x = 0; x < 256; ++x)
-            for (int r = 0; r < 4; ++r)
-                tab[s * 256 + x] |= (uint32_t)gf.mul(enc[(4 + r) * 4 + s], (uint8_t)x) << (8 * r);
+            for (int r = 0; r < K; ++r)
+                tab[(s * 256 + x) * NG + r / 4] |= (uint32_t)gf.mul(enc[(K + r) * K + s], (uint8_t)x) << (8 * (r % 4));
     uint32_t *dtab;
     CK(hipMalloc(&dtab, tab.size() * 4));
     CK(hipMemcpy(dtab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
@@ -84,17 +96,21 @@ int main(int argc, char **argv) {
     ApplyArgs a{};
     a.in = in; a.out = out; a.in_stride = n; a.out_stride = 2 * n; a.valid = n; a.C = C;
     a.tiles_per_obj = C / TILE; a.total_tiles = a.tiles_per_obj * count; a.count = count;
+    a.out_stride = M * C;
     a.table = dtab;
-    for (int j = 0; j < ZF_MAXK; ++j) { a.in_off[j] = j < 4 ? j * C : 0; a.copy_off[j] = j < 4 ? j * C : NO_OUT; }
-    for (int q = 0; q < ZF_MAXP; ++q) a.par_off[q] = q < 4 ? (4 + q) * C : NO_OUT;
+    for (int j = 0; j < ZF_MAXK; ++j) { a.in_off[j] = j < K ? j * C : 0; a.copy_off[j] = j < K ? j * C : NO_OUT; }
+    for (int q = 0; q < ZF_MAXP; ++q) a.par_off[q] = q < K ? (K + q) * C : NO_OUT;
 
-    std::vector<Variant> vs = {
-        V<1, 0, true>(4),        V<1, 1, true>(4),        V<1, 1, false>(4),       V<1, 2, false>(4),
-        V<1, 3, false, 16>(4),   V<1, 3, false, 64>(4),   V<1, 3, false, 256>(4),  V<1, 3, true, 64>(4),
-        V<2, 3, false, 32>(4),   V<1, 3, false, 64>(2),   V<1, 3, false, 64>(8),   V<2, 3, false, 32>(2),
-        V<1, 3, false, 8>(4),    V<2, 1, false>(4),
-    };
-    const size_t lds = 256 * 4 * 8 * 4;
+    std::vector<Variant> vs;
+    if (K == 4)
+        vs = {V<1, 3, true, 64>(4),             V<1, 3, true, 64, 1, 0, true>(4), V<1, 3, true, 64, 4, 1, true>(4),
+              V<1, 3, true, 64, 3, 1, true>(3), V<1, 3, true, 64, 2, 0, true>(2), V<2, 3, true, 32, 2, 0, true>(2),
+              V<1, 3, true, 64, 1, 0, true>(3)};
+    else
+        vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
+              V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
+              V16<1, 3, true, 4, 64, 2, 2, true>(2),    V16<1, 3, true, 4, 16, 2, 1, true>(2),
+              V16<1, 3, true, 4, 64, 3, 1>(2),          V16<1, 3, false, 4, 64, 2, 1, true>(2)};
     unsigned long long *dsum;
     CK(hipMalloc(&dsum, 8));
     std::vector<std::vector<float>> ms(vs.size());
@@ -107,9 +123,9 @@ int main(int argc, char **argv) {
             const int grid = 256 * vs[v].blocks_per_cu;
             a.chunk = vs[v].chunk;
             if (rd == 0) CK(hipMemset(out, 0, count * 2 * n));  // a variant that skips bytes fails the checksum
-            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(TPB), lds, 0, a);  // warm
+            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(TPB), vs[v].lds, 0, a);  // warm
             CK(hipEventRecord(e0));
-            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(TPB), lds, 0, a);
+            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(TPB), vs[v].lds, 0, a);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float t;
