@@ -36,6 +36,12 @@ class EncodeInfoC(ctypes.Structure):
     ]
 
 
+class EciesInjectC(ctypes.Structure):
+    """chip_ecies_inject: the values ecies::encrypt draws from thread_rng."""
+
+    _fields_ = [("ephemeral_sk", ctypes.c_void_p), ("nonce", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes); mirrors include/carbonado_hip.h exactly
 SIGNATURES = {
     "chip_abi_version": (ctypes.c_int, []),
@@ -59,10 +65,23 @@ SIGNATURES = {
     "chip_bao_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                        ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
     "chip_blake3": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
-    "chip_encode": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
-                                   ctypes.c_uint64, c_u64p, ctypes.c_void_p, ctypes.POINTER(EncodeInfoC)]),
+    "chip_snap_max_len": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "chip_snap_compress": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                          c_u64p]),
+    "chip_snap_decompress": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                            c_u64p]),
+    "chip_ecies_encrypt": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(EciesInjectC),
+                                          ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                          c_u64p]),
+    "chip_ecies_decrypt": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
+    "chip_ecies_public_key": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "chip_encode": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(EciesInjectC),
+                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p,
+                                   ctypes.c_void_p, ctypes.POINTER(EncodeInfoC)]),
     "chip_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
-                                   ctypes.c_uint32, ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
+                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint8,
+                                   ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
     "chip_zfec_encode_batch_dev": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
                                                   ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
@@ -86,10 +105,11 @@ SIGNATURES = {
                                              c_u64p]),
     "chip_scrub": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
-    "chip_encode_host_batch": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
-                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p,
-                                              ctypes.c_void_p, ctypes.POINTER(EncodeInfoC), ctypes.c_uint32,
-                                              ctypes.c_uint64]),
+    "chip_encode_host_batch": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.POINTER(EciesInjectC), ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                              c_u64p, ctypes.c_void_p, ctypes.POINTER(EncodeInfoC),
+                                              ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32]),
 }
 
 _LIB = None

@@ -263,7 +263,10 @@ __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x
 // the 8*CPL steps stages 128 B of the current chunk of every lane in the
 // wave through LDS (coalesced 16-B loads, 8 lanes = one 128-B line), with the
 // next step's loads prefetched into registers while the lane compresses.
-template <int MODE, int CPL, bool NTS>
+// SP (stream path, MODE 0): 0 = aligned pieces re-read from the LDS rows;
+// 1 = pieces built in registers from the loaded data (DPP neighbour exchange);
+// 2 = diagnostic for tools/bao_tune only (128-B aligned bases, wrong layout).
+template <int MODE, int CPL, bool NTS, int SP = 0>
 __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     constexpr int LOG = ilog2(CPL);
     constexpr int NSTEP = 8 * CPL;
@@ -376,6 +379,46 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         }
     };
 
+    // encode, SP 1: straight from the loaded registers.  Lane g of a chunk's
+    // 8-lane group holds chunk bytes [128s+16g, +16) at stream offset 8 (mod 16);
+    // it stores the ALIGNED 16 B [128s+16g+8, +16) = its upper half + the next
+    // lane's lower half (DPP row_shl:1), lane 0 adds the 8-B head of the step
+    // and lane 7 the 8-B tail, so a step needs no bytes of its neighbours.
+    auto stream_regs = [&](int g, const u32x4 (&v)[8]) {
+        const int j = g >> 3, s = g & 7, gl = lane & 7;
+        uint64_t bo[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bo[t] = soff[j & 1][wave][t * 8 + (lane >> 3)];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v[t].x, 0x101, 0xF, 0xF, false);
+            const uint32_t ny = __builtin_amdgcn_update_dpp(0u, v[t].y, 0x101, 0xF, 0xF, false);
+            const int cc = t * 8 + (lane >> 3);
+            const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
+            if (!(wave_on && ci < a.N)) continue;
+            const uint64_t rem = a.n - ci * 1024;
+            const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+            if (SP == 2) {
+                uint8_t *q = ob + (bo[t] & ~127ull) + 128 * s + 16 * gl;
+                if (clen == 1024) *reinterpret_cast<u32x4 *>(q) = v[t];
+                continue;
+            }
+            uint8_t *p = ob + bo[t] + 128 * s + 16 * gl;
+            if (clen == 1024) {
+                if (gl < 7) {
+                    const u32x4 o = {v[t].z, v[t].w, nx, ny};
+                    if (NTS) __builtin_nontemporal_store(o, reinterpret_cast<u32x4 *>(p + 8));
+                    else *reinterpret_cast<u32x4 *>(p + 8) = o;
+                }
+                if (gl == 0 || gl == 7)
+                    store8<NTS>(gl == 0 ? p : p + 8, gl == 0 ? u32x2{v[t].x, v[t].y} : u32x2{v[t].z, v[t].w});
+            } else {  // short last chunk of the object
+                const uint32_t cb = 128u * s + 16u * gl;
+                if (cb < clen) store16_partial(p, v[t], clen - cb);
+            }
+        }
+    };
+
     uint32_t h[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) h[w] = IV(w);
@@ -389,11 +432,12 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             uint32_t *row = st + (t * 8 + (lane >> 3)) * ROWW;
-            if (MODE == 0 && (lane & 7) == 7)  // carry the previous step's last 8 bytes
+            if (MODE == 0 && SP == 0 && (lane & 7) == 7)  // carry the previous step's last 8 bytes
                 *reinterpret_cast<u32x2 *>(row + 2) = *reinterpret_cast<const u32x2 *>(row + ROW0 + 30);
             *reinterpret_cast<u32x4 *>(row + ROW0 + (lane & 7) * 4) = pre[t];
         }
         if (MODE == 1 && ob) content_step(g, pre);
+        if (MODE == 0 && ob && SP != 0) stream_regs(g, pre);
         if (s == 7 && j + 1 < CPL) {  // stream offset of my next chunk, for the loads issued below
             const uint64_t ni = lb + j + 1;
             if ((uint64_t)(j + 1) < nmine) my_off += 1024 + 64 * (uint64_t)parents_at(ni, a.N);
@@ -401,7 +445,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         }
         wave_sync();
         if (g + 1 < NSTEP) load_step(g + 1, pre);  // in flight during the compressions
-        if (MODE == 0 && ob) stream_step(g);
+        if (MODE == 0 && ob && SP == 0) stream_step(g);
 
         const uint64_t i = lb + j;
         const bool mine = (uint64_t)j < nmine;
@@ -611,7 +655,7 @@ inline uint64_t bao_scratch_len_t(uint64_t n, uint64_t count) {
 }
 
 // Enqueue K3 then one K4 launch per remaining level.
-template <int MODE, int BAO_CPL, bool BAO_NTS>
+template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0>
 hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
                    void *d_scratch, hipStream_t stream) {
@@ -629,7 +673,7 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
     ca.hash = d_hash; ca.status = d_status;
     const uint64_t waves = count * ((N + 64ull * BAO_CPL - 1) / (64ull * BAO_CPL));
     const uint64_t blocks = (waves + K3_WAVES - 1) / K3_WAVES;
-    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS>), dim3((unsigned)blocks), dim3(K3_TPB), 0,
+    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP>), dim3((unsigned)blocks), dim3(K3_TPB), 0,
                        stream, ca);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

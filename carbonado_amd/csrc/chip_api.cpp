@@ -4,18 +4,23 @@
 // the reference stage functions (file:line cited per entry point), staging of
 // host buffers into per-thread device scratch, and the encode()/decode() glue.
 // Every byte of shard/stream data is produced by the HIP kernels in
-// zfec_kernels.hip and bao_kernels.hip; there is no CPU compute path.
+// zfec_kernels.hip and bao_kernels.hip; there is no CPU compute path for
+// zfec or bao.  The snappy/ECIES stages that the reference runs before zfec
+// (and after it on decode) are host stages by design (host_stages.cpp).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "chip_internal.hpp"
 #include "gf256.hpp"
+#include "host_stages.hpp"
 
 namespace chip {
 
@@ -52,9 +57,11 @@ struct DevBuf {
 };
 
 // one pipeline slot of chip_encode_host_batch: its own stream and buffers
+// (`stage` is pinned host memory holding the host-stage output of a slice)
 struct Slot {
     hipStream_t stream = nullptr;
     DevBuf in, mid, out, hash, scratch;
+    DevBuf stage;
 };
 
 struct Ctx {
@@ -70,6 +77,7 @@ struct Ctx {
         for (Slot &sl : slots) {
             for (DevBuf *b : {&sl.in, &sl.mid, &sl.out, &sl.hash, &sl.scratch})
                 if (b->p) (void)hipFree(b->p);
+            if (sl.stage.p) (void)hipHostFree(sl.stage.p);
             if (sl.stream) (void)hipStreamDestroy(sl.stream);
         }
     }
@@ -89,6 +97,22 @@ hipError_t grow(DevBuf &b, size_t bytes) {
     size_t cap = bytes + (bytes >> 3);  // grow-only with headroom
     cap = (cap + 255) & ~size_t(255);
     hipError_t e = hipMalloc(&b.p, cap);
+    if (e != hipSuccess) return e;
+    b.cap = cap;
+    return hipSuccess;
+}
+
+hipError_t grow_pinned(DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipHostFree(b.p);
+        if (e != hipSuccess) return e;
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    size_t cap = ((bytes + (bytes >> 3)) + 4095) & ~size_t(4095);
+    hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
     if (e != hipSuccess) return e;
     b.cap = cap;
     return hipSuccess;
@@ -259,15 +283,21 @@ void slice_nodes(uint64_t n, uint64_t c0, uint64_t c1, std::vector<SliceNode> *o
 }
 
 // EncodeInfo of encode() for format bits Bao|Zfec (encoding.rs:86-172); no device
-int encode_info_for(uint8_t format, uint64_t n, chip_encode_info *inf, uint64_t *zlen, uint64_t *final_len) {
+// EncodeInfo of encode() (encoding.rs:86-171): `input_len` is the caller's
+// input, `cur` the length entering zfec (after snap/ecies), bc/be the
+// snap/ecies output lengths (0 when the stage is off, encoding.rs:101-115).
+int encode_info_for(uint8_t format, uint64_t input_len, uint64_t cur, uint64_t bc, uint64_t be,
+                    chip_encode_info *inf, uint64_t *zlen, uint64_t *final_len) {
     std::memset(inf, 0, sizeof *inf);
-    inf->input_len = (uint32_t)n;  // encoding.rs:87 (as u32)
+    inf->input_len = (uint32_t)input_len;  // encoding.rs:87 (as u32)
+    inf->bytes_compressed = (uint32_t)bc;
+    inf->bytes_encrypted = (uint32_t)be;
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
-    uint64_t cur_len = n;
+    uint64_t cur_len = cur;
     if (zfec) {
         uint32_t pad;
         uint64_t C;
-        calc_pad(n, CHIP_FEC_K, &pad, &C);
+        calc_pad(cur, CHIP_FEC_K, &pad, &C);
         inf->padding_len = pad;
         inf->chunk_len = (uint32_t)C;
         cur_len = (uint64_t)CHIP_FEC_M * C;
@@ -283,6 +313,47 @@ int encode_info_for(uint8_t format, uint64_t n, chip_encode_info *inf, uint64_t 
     inf->output_len = (uint32_t)fl;
     *zlen = cur_len;
     *final_len = fl;
+    return CHIP_OK;
+}
+
+bool has_host_stages(uint8_t format) { return format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY); }
+
+// bound of the host stages' output for an n-byte input
+uint64_t host_stage_max(uint8_t format, uint64_t n) {
+    uint64_t m = (format & CHIP_FORMAT_SNAPPY) ? host::snap_max_len(n) : n;
+    if (format & CHIP_FORMAT_ECIES) m += host::ECIES_OVERHEAD;
+    return m;
+}
+
+// snap -> ecies (encoding.rs:101-115) of one object into dst[0..cap); tmp is
+// the snap output when both stages run.
+int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const uint8_t *eph, const uint8_t *nonce,
+                     const uint8_t *in, uint64_t n, uint8_t *dst, uint64_t cap, std::vector<uint8_t> &tmp,
+                     uint64_t *len, uint64_t *bc, uint64_t *be) {
+    const bool snap = format & CHIP_FORMAT_SNAPPY, ecies = format & CHIP_FORMAT_ECIES;
+    const uint8_t *cur = in;
+    uint64_t cur_n = n;
+    *bc = *be = 0;
+    if (snap) {
+        uint8_t *sd = dst;
+        uint64_t scap = cap;
+        if (ecies) {
+            tmp.resize(host::snap_max_len(n) + 1);
+            sd = tmp.data();
+            scap = tmp.size();
+        }
+        int st = host::snap_compress(in, n, sd, scap, &cur_n);
+        if (st != CHIP_OK) return st;
+        cur = sd;
+        *bc = cur_n;
+    }
+    if (ecies) {
+        if (!pk) return CHIP_ERR_INVALID_ARG;
+        int st = host::ecies_encrypt(pk, pklen, eph, nonce, cur, cur_n, dst, cap, &cur_n);
+        if (st != CHIP_OK) return st;
+        *be = cur_n;
+    }
+    *len = cur_n;
     return CHIP_OK;
 }
 
@@ -305,11 +376,13 @@ const char *chip_strerror(int st) {
         case CHIP_ERR_ENCODE_ZFEC_PADDING: return "Padding from Zfec should always be zero.";
         case CHIP_ERR_ENCODE_INVALID_CHUNK_LENGTH: return "Chunk length should be as calculated.";
         case CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT: return "Verifiable slice count should be evenly divisible by 8.";
-        case CHIP_ERR_UNSUPPORTED_FORMAT: return "format bit handled by a host stage outside this path (ecies/snappy)";
+        case CHIP_ERR_UNSUPPORTED_FORMAT: return "unsupported format";
         case CHIP_ERR_UNNECESSARY_SCRUB: return "Data does not need to be scrubbed.";
         case CHIP_ERR_SCRUBBED_PADDING_MISMATCH: return "Scrubbed padding should remain the same.";
         case CHIP_ERR_SCRUBBED_LENGTH_MISMATCH: return "Mismatch between scrubbed data length and input length";
         case CHIP_ERR_INVALID_SCRUBBED_HASH: return "Scrubbed hash is not equal to original hash.";
+        case CHIP_ERR_SNAP: return "snappy framing error";
+        case CHIP_ERR_ECIES: return "ecies error";
         case CHIP_ERR_NO_DEVICE: return "no usable gfx950 device";
         case CHIP_ERR_DEVICE: return "HIP runtime error";
         default: return "unknown status";
@@ -343,20 +416,59 @@ uint64_t chip_zfec_encoded_len(uint64_t n, uint32_t k, uint32_t m) {
 uint64_t chip_bao_encoded_len(uint64_t n) { return bao_encoded_len(n); }
 
 uint64_t chip_encode_max_len(uint64_t n) {
-    const uint64_t z = chip_zfec_encoded_len(n, CHIP_FEC_K, CHIP_FEC_M);
-    const uint64_t big = z > n ? z : n;
+    const uint64_t h = host_stage_max(CHIP_FORMAT_SNAPPY | CHIP_FORMAT_ECIES, n);  // >= n
+    const uint64_t z = chip_zfec_encoded_len(h, CHIP_FEC_K, CHIP_FEC_M);
+    const uint64_t big = z > h ? z : h;
     return bao_encoded_len(big);
+}
+
+uint64_t chip_snap_max_len(uint64_t n) { return host::snap_max_len(n); }
+
+// ---- host stages --------------------------------------------------------
+
+int chip_snap_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if ((!in && n) || !out_len || (n && !out)) return CHIP_ERR_INVALID_ARG;
+    return host::snap_compress(in, n, out, out_cap, out_len);
+}
+
+int chip_snap_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if ((!in && n) || !out_len) return CHIP_ERR_INVALID_ARG;
+    return host::snap_decompress(in, n, out, out_cap, out_len);
+}
+
+int chip_ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const chip_ecies_inject *inject,
+                       const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if (!pubkey || (!in && n) || !out || !out_len) return CHIP_ERR_INVALID_ARG;
+    return host::ecies_encrypt(pubkey, pubkey_len, inject ? inject->ephemeral_sk : nullptr,
+                               inject ? inject->nonce : nullptr, in, n, out, out_cap, out_len);
+}
+
+int chip_ecies_decrypt(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *in, uint64_t n, uint8_t *out,
+                       uint64_t out_cap, uint64_t *out_len) {
+    if (!secret_key || (!in && n) || !out_len) return CHIP_ERR_INVALID_ARG;
+    return host::ecies_decrypt(secret_key, sk_len, in, n, out, out_cap, out_len);
+}
+
+int chip_ecies_public_key(const uint8_t *secret_key, uint8_t pubkey[65]) {
+    if (!secret_key || !pubkey) return CHIP_ERR_INVALID_ARG;
+    return host::ecies_public_key(secret_key, pubkey);
 }
 
 uint64_t chip_bao_scratch_len(uint64_t n, uint64_t count) { return bao_scratch_len(n, count); }
 
 // ---- zfec --------------------------------------------------------------
 
+// K1 reads and writes 16-B vectors and its tail load relies on 16-B aligned
+// shard addresses (zfec_device.hpp load16_masked).
+static bool misaligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
+
 int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
                                uint64_t n, uint64_t count, uint8_t *d_out, uint64_t out_stride,
                                void *stream) {
     if (!valid_km(k, m)) return CHIP_ERR_ZFEC;
-    if ((!d_in && n) || !d_out || (in_stride % 16) || (out_stride % 16)) return CHIP_ERR_INVALID_ARG;
+    if ((!d_in && n) || !d_out || (in_stride % 16) || (out_stride % 16) || misaligned16(d_in) ||
+        misaligned16(d_out))
+        return CHIP_ERR_INVALID_ARG;
     int st = ensure_device();
     if (st != CHIP_OK) return st;
     uint32_t pad;
@@ -462,7 +574,8 @@ int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
                                uint64_t chunk_len, const uint32_t *idx, uint32_t nshares,
                                uint64_t count, uint8_t *d_out, uint64_t out_stride, void *stream) {
     if (!valid_km(k, m)) return CHIP_ERR_ZFEC;
-    if (!d_in || !d_out || !idx || (in_stride % 16) || (out_stride % 16) || (chunk_len % 16))
+    if (!d_in || !d_out || !idx || (in_stride % 16) || (out_stride % 16) || (chunk_len % 16) ||
+        misaligned16(d_in) || misaligned16(d_out))
         return CHIP_ERR_INVALID_ARG;
     int st = ensure_device();
     if (st != CHIP_OK) return st;
@@ -772,30 +885,43 @@ int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t h
 
 // ---- pipeline glue -------------------------------------------------------
 
-int chip_encode(uint8_t format, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
-                uint64_t *out_len, uint8_t hash[CHIP_HASH_LEN], chip_encode_info *info) {
+int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, const chip_ecies_inject *inject,
+                const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len,
+                uint8_t hash[CHIP_HASH_LEN], chip_encode_info *info) {
     if ((!in && n) || !out_len || !hash) return CHIP_ERR_INVALID_ARG;
-    if (format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY)) return CHIP_ERR_UNSUPPORTED_FORMAT;
+    if ((format & CHIP_FORMAT_ECIES) && !pubkey) return CHIP_ERR_INVALID_ARG;
+    // host stages (encoding.rs:101-115)
+    thread_local std::vector<uint8_t> t_stage, t_tmp;
+    const uint8_t *cur = in;
+    uint64_t cur_n = n, bc = 0, be = 0;
+    if (has_host_stages(format)) {
+        t_stage.resize(host_stage_max(format, n) + 1);
+        int st = host_stages_into(format, pubkey, pubkey_len, inject ? inject->ephemeral_sk : nullptr,
+                                  inject ? inject->nonce : nullptr, in, n, t_stage.data(), t_stage.size(), t_tmp,
+                                  &cur_n, &bc, &be);
+        if (st != CHIP_OK) return st;
+        cur = t_stage.data();
+    }
     chip_encode_info inf;
     uint64_t cur_len, final_len;
-    int st = encode_info_for(format, n, &inf, &cur_len, &final_len);
+    int st = encode_info_for(format, n, cur_n, bc, be, &inf, &cur_len, &final_len);
     if (st != CHIP_OK) return st;
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
     if (final_len && (!out || out_cap < final_len)) return CHIP_ERR_BUFFER_TOO_SMALL;
     if (!zfec && !bao) {
-        if (n) std::memcpy(out, in, n);
+        if (cur_n) std::memcpy(out, cur, cur_n);
         std::memset(hash, 0, 32);
     } else {
         Ctx *c;
         st = ctx_get(&c);
         if (st != CHIP_OK) return st;
-        CHIP_HIP(grow(c->in, n));
-        if (n) CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+        CHIP_HIP(grow(c->in, cur_n));
+        if (cur_n) CHIP_HIP(hipMemcpyAsync(c->in.p, cur, cur_n, hipMemcpyHostToDevice, c->stream));
         const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
         if (zfec && cur_len) {
             CHIP_HIP(grow(c->mid, cur_len));
             GfPlan p = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M));
-            GfLaunch L{d_cur, static_cast<uint8_t *>(c->mid.p), 0, 0, n, inf.chunk_len, 1};
+            GfLaunch L{d_cur, static_cast<uint8_t *>(c->mid.p), 0, 0, cur_n, inf.chunk_len, 1};
             CHIP_HIP(gf_apply(p, L, c->stream));
             d_cur = static_cast<const uint8_t *>(c->mid.p);
         }
@@ -814,139 +940,301 @@ int chip_encode(uint8_t format, const uint8_t *in, uint64_t n, uint8_t *out, uin
     return CHIP_OK;
 }
 
-int chip_encode_host_batch(uint8_t format, const uint8_t *in, uint64_t n, uint64_t count, uint64_t in_stride,
-                           uint8_t *out, uint64_t out_stride, uint64_t *out_len, uint8_t *hashes,
-                           chip_encode_info *info, uint32_t nslots, uint64_t slice_bytes) {
-    if ((!in && n && count) || !out_len || (!hashes && count)) return CHIP_ERR_INVALID_ARG;
-    if (format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY)) return CHIP_ERR_UNSUPPORTED_FORMAT;
-    if (count > 1 && in_stride < n) return CHIP_ERR_INVALID_ARG;
-    chip_encode_info inf;
-    uint64_t zlen, final_len;
-    int st = encode_info_for(format, n, &inf, &zlen, &final_len);
-    if (st != CHIP_OK) return st;
-    if (count > 1 && out_stride < final_len) return CHIP_ERR_BUFFER_TOO_SMALL;
-    if (final_len && count && !out) return CHIP_ERR_BUFFER_TOO_SMALL;
+namespace {
+
+// Device part of one slice of chip_encode_host_batch: cnt objects of cur_n
+// bytes at src (host, pitch src_pitch) -> zfec -> bao -> out (host).
+int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_encode_info &inf,
+                       const uint8_t *src, uint64_t src_pitch, uint64_t cur_n, uint64_t zlen, uint64_t final_len,
+                       uint64_t cnt, uint8_t *out, uint64_t out_pitch, uint8_t *hashes) {
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
-    *out_len = final_len;
-    if (info) *info = inf;
-    if (count == 0) return CHIP_OK;
-    if (!zfec && !bao) {  // format 0: identity, nothing for the device to do
-        for (uint64_t o = 0; o < count; ++o) {
-            if (n) std::memcpy(out + o * out_stride, in + o * in_stride, n);
-            std::memset(hashes + 32 * o, 0, 32);
-        }
-        return CHIP_OK;
+    const uint64_t n_al = (cur_n + 15) / 16 * 16, z_al = (zlen + 15) / 16 * 16, f_al = (final_len + 15) / 16 * 16;
+    uint8_t *d_in = static_cast<uint8_t *>(sl.in.p);
+    if (cur_n)
+        CHIP_HIP(hipMemcpy2DAsync(d_in, n_al, src, src_pitch, cur_n, cnt, hipMemcpyHostToDevice, sl.stream));
+    const uint8_t *d_cur = d_in;
+    uint64_t cur_stride = n_al;
+    if (zfec) {
+        GfLaunch L{d_in, static_cast<uint8_t *>(sl.mid.p), n_al, z_al, cur_n, inf.chunk_len, cnt};
+        CHIP_HIP(gf_apply(*plan, L, sl.stream));
+        d_cur = static_cast<const uint8_t *>(sl.mid.p);
+        cur_stride = z_al;
     }
-    Ctx *c;
-    st = ctx_get(&c);
-    if (st != CHIP_OK) return st;
-    nslots = nslots < 1 ? 3 : (nslots > 8 ? 8 : nslots);
-    if (slice_bytes == 0) slice_bytes = 256ull << 20;
-    const uint64_t n_al = (n + 15) / 16 * 16;           // device input stride
-    const uint64_t z_al = (zlen + 15) / 16 * 16;         // device zfec-output stride
-    const uint64_t f_al = (final_len + 15) / 16 * 16;    // device stream stride
-    uint64_t S = slice_bytes / (n ? n : 1);
-    S = S < 1 ? 1 : (S > count ? count : S);
-    if (c->slots.size() < nslots) c->slots.resize(nslots);
-    for (uint32_t k = 0; k < nslots; ++k) {
-        Slot &sl = c->slots[k];
-        if (!sl.stream) CHIP_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-        CHIP_HIP(grow(sl.in, S * n_al));
-        if (zfec) CHIP_HIP(grow(sl.mid, S * z_al));
-        if (bao) {
-            CHIP_HIP(grow(sl.out, S * f_al));
-            CHIP_HIP(grow(sl.scratch, bao_scratch_len(zlen, S)));
-        }
-        CHIP_HIP(grow(sl.hash, S * 32));
+    const uint8_t *d_res = d_cur;
+    uint64_t res_stride = cur_stride;
+    if (bao) {
+        CHIP_HIP(bao_encode_dev(d_cur, cur_stride, zlen, cnt, static_cast<uint8_t *>(sl.out.p), f_al,
+                                static_cast<uint8_t *>(sl.hash.p), sl.scratch.p, sl.stream));
+        d_res = static_cast<const uint8_t *>(sl.out.p);
+        res_stride = f_al;
+        CHIP_HIP(hipMemcpyAsync(hashes, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, sl.stream));
+    } else {
+        for (uint64_t o = 0; o < cnt; ++o) std::memset(hashes + 32 * o, 0, 32);
     }
-    const GfPlan plan = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M));
-    const uint64_t nslices = (count + S - 1) / S;
-    for (uint64_t i = 0; i < nslices; ++i) {
-        Slot &sl = c->slots[i % nslots];
-        if (i >= nslots) CHIP_HIP(hipStreamSynchronize(sl.stream));  // slot's previous slice is done
-        const uint64_t o0 = i * S, cnt = (count - o0) < S ? (count - o0) : S;
-        uint8_t *d_in = static_cast<uint8_t *>(sl.in.p);
-        if (n) CHIP_HIP(hipMemcpy2DAsync(d_in, n_al, in + o0 * in_stride, count > 1 ? in_stride : n, n, cnt,
-                                         hipMemcpyHostToDevice, sl.stream));
-        const uint8_t *d_cur = d_in;
-        uint64_t cur_stride = n_al;
-        if (zfec) {
-            GfLaunch L{d_in, static_cast<uint8_t *>(sl.mid.p), n_al, z_al, n, inf.chunk_len, cnt};
-            CHIP_HIP(gf_apply(plan, L, sl.stream));
-            d_cur = static_cast<const uint8_t *>(sl.mid.p);
-            cur_stride = z_al;
-        }
-        const uint8_t *d_res = d_cur;
-        uint64_t res_stride = cur_stride;
-        if (bao) {
-            CHIP_HIP(bao_encode_dev(d_cur, cur_stride, zlen, cnt, static_cast<uint8_t *>(sl.out.p), f_al,
-                                    static_cast<uint8_t *>(sl.hash.p), sl.scratch.p, sl.stream));
-            d_res = static_cast<const uint8_t *>(sl.out.p);
-            res_stride = f_al;
-            CHIP_HIP(hipMemcpyAsync(hashes + 32 * o0, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, sl.stream));
-        } else {
-            for (uint64_t o = 0; o < cnt; ++o) std::memset(hashes + 32 * (o0 + o), 0, 32);
-        }
-        if (final_len)
-            CHIP_HIP(hipMemcpy2DAsync(out + o0 * out_stride, count > 1 ? out_stride : final_len, d_res, res_stride,
-                                      final_len, cnt, hipMemcpyDeviceToHost, sl.stream));
-    }
-    for (uint32_t k = 0; k < nslots; ++k) CHIP_HIP(hipStreamSynchronize(c->slots[k].stream));
+    if (final_len)
+        CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, d_res, res_stride, final_len, cnt, hipMemcpyDeviceToHost,
+                                  sl.stream));
     return CHIP_OK;
 }
 
-int chip_decode(const uint8_t *hash, uint64_t hash_len, const uint8_t *in, uint64_t n, uint32_t padding,
-                uint8_t format, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
-    if ((!in && n) || !out_len) return CHIP_ERR_INVALID_ARG;
-    if (format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY)) return CHIP_ERR_UNSUPPORTED_FORMAT;
+}  // namespace
+
+int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len,
+                           const chip_ecies_inject *inject, const uint8_t *in, uint64_t n, uint64_t count,
+                           uint64_t in_stride, uint8_t *out, uint64_t out_stride, uint64_t *out_len,
+                           uint8_t *hashes, chip_encode_info *info, uint32_t nslots, uint64_t slice_bytes,
+                           uint32_t host_threads) {
+    if ((!in && n && count) || (!out_len && count) || (!hashes && count)) return CHIP_ERR_INVALID_ARG;
+    if ((format & CHIP_FORMAT_ECIES) && !pubkey) return CHIP_ERR_INVALID_ARG;
+    if (count > 1 && in_stride < n) return CHIP_ERR_INVALID_ARG;
+    if (count == 0) return CHIP_OK;
+    const bool hs = has_host_stages(format);
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
-    if (!zfec && !bao) {
-        if (n && (!out || out_cap < n)) return CHIP_ERR_BUFFER_TOO_SMALL;
-        if (n) std::memcpy(out, in, n);
-        *out_len = n;
+    // sizes: exact without host stages, bounds with them
+    const uint64_t h_max = hs ? host_stage_max(format, n) : n;
+    chip_encode_info inf_max;
+    uint64_t zlen_max, final_max;
+    int st = encode_info_for(format, n, h_max, 0, 0, &inf_max, &zlen_max, &final_max);
+    if (st != CHIP_OK && !hs) return st;
+    if (hs) {  // bound without the slice-count check (a smaller object may still pass it)
+        uint32_t pad;
+        uint64_t C;
+        calc_pad(h_max, CHIP_FEC_K, &pad, &C);
+        zlen_max = zfec ? (uint64_t)CHIP_FEC_M * C : h_max;
+        final_max = bao ? bao_encoded_len(zlen_max) : zlen_max;
+    }
+    if (count > 1 && out_stride < final_max) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (final_max && !out) return CHIP_ERR_BUFFER_TOO_SMALL;
+
+    if (!hs && !zfec && !bao) {  // format 0: identity, nothing for the device to do
+        for (uint64_t o = 0; o < count; ++o) {
+            if (n) std::memcpy(out + o * out_stride, in + o * in_stride, n);
+            std::memset(hashes + 32 * o, 0, 32);
+            out_len[o] = n;
+            if (info) info[o] = inf_max;
+        }
         return CHIP_OK;
     }
-    uint64_t cur_len = n;
-    if (bao) {
-        if (!hash || hash_len != CHIP_HASH_LEN) return CHIP_ERR_HASH_DECODE;
-        int st = bao_header(in, n, &cur_len);
+    Ctx *c = nullptr;
+    if (zfec || bao) {
+        st = ctx_get(&c);
         if (st != CHIP_OK) return st;
     }
-    uint64_t C = 0, olen = cur_len;
-    if (zfec) {
-        if (cur_len % CHIP_FEC_M != 0) return CHIP_ERR_UNEVEN_ZFEC_CHUNKS;  // decoding.rs:39-41
-        C = cur_len / CHIP_FEC_M;
-        if (padding > CHIP_FEC_K * C) return CHIP_ERR_ZFEC;
-        if (C % 16) return CHIP_ERR_ZFEC;
-        olen = CHIP_FEC_K * C - padding;
+    nslots = nslots < 1 ? 3 : (nslots > 8 ? 8 : nslots);
+    if (slice_bytes == 0) slice_bytes = 256ull << 20;
+    uint32_t T = host_threads ? host_threads : std::max(1u, std::thread::hardware_concurrency());
+    T = std::min<uint32_t>(T, 64);
+    const uint64_t h_al = (h_max + 15) / 16 * 16;  // pinned staging pitch
+    uint64_t S = slice_bytes / (h_max ? h_max : 1);
+    S = S < 1 ? 1 : (S > count ? count : S);
+    if (c) {
+        if (c->slots.size() < nslots) c->slots.resize(nslots);
+        for (uint32_t k = 0; k < nslots; ++k) {
+            Slot &sl = c->slots[k];
+            if (!sl.stream) CHIP_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+            CHIP_HIP(grow(sl.in, S * h_al));
+            if (zfec) CHIP_HIP(grow(sl.mid, S * ((zlen_max + 15) / 16 * 16)));
+            if (bao) {
+                CHIP_HIP(grow(sl.out, S * ((final_max + 15) / 16 * 16)));
+                CHIP_HIP(grow(sl.scratch, bao_scratch_len(zlen_max, S)));
+            }
+            CHIP_HIP(grow(sl.hash, S * 32));
+            if (hs) CHIP_HIP(grow_pinned(sl.stage, S * h_al));
+        }
     }
-    if (olen && (!out || out_cap < olen)) return CHIP_ERR_BUFFER_TOO_SMALL;
-    Ctx *c;
-    int st = ctx_get(&c);
-    if (st != CHIP_OK) return st;
-    const uint64_t in_bytes = bao ? bao_encoded_len(cur_len) : n;
-    CHIP_HIP(grow(c->in, in_bytes));
-    if (in_bytes) CHIP_HIP(hipMemcpyAsync(c->in.p, in, in_bytes, hipMemcpyHostToDevice, c->stream));
-    const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
-    if (bao) {  // decoding.rs:89-93
-        CHIP_HIP(grow(c->mid, cur_len));
-        st = bao_decode_ctx(c, d_cur, in_bytes, cur_len, hash, static_cast<uint8_t *>(c->mid.p));
+    const std::vector<uint8_t> enc = zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M);
+    std::vector<uint8_t> stage_host;  // host stages without a device part
+    if (!c) stage_host.resize(S * h_al);
+    std::vector<uint64_t> len(S), bc(S), be(S);
+    std::vector<int> sts(S);
+    auto drain = [&]() {
+        if (c)
+            for (uint32_t k = 0; k < nslots; ++k) (void)hipStreamSynchronize(c->slots[k].stream);
+    };
+    const uint64_t nslices = (count + S - 1) / S;
+    for (uint64_t i = 0; i < nslices; ++i) {
+        Slot *sl = c ? &c->slots[i % nslots] : nullptr;
+        if (sl && i >= nslots) CHIP_HIP(hipStreamSynchronize(sl->stream));  // slot's previous slice is done
+        const uint64_t o0 = i * S, cnt = (count - o0) < S ? (count - o0) : S;
+        const uint8_t *src = in + o0 * in_stride;
+        uint64_t src_pitch = count > 1 ? in_stride : n;
+        uint64_t cur_n = n;
+        bool uniform = true;
+        if (hs) {
+            // host stages of this slice on T threads while earlier slices run on the device
+            uint8_t *stage = sl ? static_cast<uint8_t *>(sl->stage.p) : stage_host.data();
+            const uint32_t nt = (uint32_t)std::min<uint64_t>(T, cnt);
+            auto work = [&](uint32_t t) {
+                std::vector<uint8_t> tmp;
+                for (uint64_t j = t; j < cnt; j += nt) {
+                    const uint64_t o = o0 + j;
+                    sts[j] = host_stages_into(format, pubkey, pubkey_len,
+                                              inject && inject->ephemeral_sk ? inject->ephemeral_sk + 32 * o : nullptr,
+                                              inject && inject->nonce ? inject->nonce + 16 * o : nullptr,
+                                              in + o * in_stride, n, stage + j * h_al, h_al, tmp, &len[j], &bc[j],
+                                              &be[j]);
+                }
+            };
+            std::vector<std::thread> pool;
+            for (uint32_t t = 1; t < nt; ++t) pool.emplace_back(work, t);
+            work(0);
+            for (auto &th : pool) th.join();
+            for (uint64_t j = 0; j < cnt; ++j)
+                if (sts[j] != CHIP_OK) {
+                    drain();
+                    return sts[j];
+                }
+            src = stage;
+            src_pitch = h_al;
+            cur_n = len[0];
+            for (uint64_t j = 1; j < cnt; ++j) uniform &= len[j] == cur_n;
+        } else {
+            for (uint64_t j = 0; j < cnt; ++j) len[j] = n, bc[j] = be[j] = 0;
+        }
+        // per-object EncodeInfo (identical for a uniform slice)
+        for (uint64_t j = 0; j < cnt; ++j) {
+            chip_encode_info inf;
+            uint64_t zl, fl;
+            st = encode_info_for(format, n, len[j], bc[j], be[j], &inf, &zl, &fl);
+            if (st != CHIP_OK) {
+                drain();
+                return st;
+            }
+            out_len[o0 + j] = fl;
+            if (info) info[o0 + j] = inf;
+        }
+        if (!sl) {  // host stages only (no Zfec/Bao bit)
+            for (uint64_t j = 0; j < cnt; ++j) {
+                std::memcpy(out + (o0 + j) * out_stride, src + j * src_pitch, len[j]);
+                std::memset(hashes + 32 * (o0 + j), 0, 32);
+            }
+            continue;
+        }
+        if (uniform) {
+            chip_encode_info inf;
+            uint64_t zl, fl;
+            (void)encode_info_for(format, n, cur_n, 0, 0, &inf, &zl, &fl);
+            const GfPlan p2 = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, enc);
+            st = batch_slice_device(*sl, format, &p2, inf, src, src_pitch, cur_n, zl, fl, cnt, out + o0 * out_stride,
+                                    count > 1 ? out_stride : fl, hashes + 32 * o0);
+            if (st != CHIP_OK) {
+                drain();
+                return st;
+            }
+        } else {  // ragged host-stage output (compressible data): one object at a time
+            for (uint64_t j = 0; j < cnt; ++j) {
+                chip_encode_info inf;
+                uint64_t zl, fl;
+                (void)encode_info_for(format, n, len[j], 0, 0, &inf, &zl, &fl);
+                const GfPlan pj = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, enc);
+                st = batch_slice_device(*sl, format, &pj, inf, src + j * src_pitch, src_pitch, len[j], zl, fl, 1,
+                                        out + (o0 + j) * out_stride, fl, hashes + 32 * (o0 + j));
+                if (st != CHIP_OK) {
+                    drain();
+                    return st;
+                }
+            }
+        }
+    }
+    if (c)
+        for (uint32_t k = 0; k < nslots; ++k) CHIP_HIP(hipStreamSynchronize(c->slots[k].stream));
+    return CHIP_OK;
+}
+
+int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash, uint64_t hash_len,
+                const uint8_t *in, uint64_t n, uint32_t padding, uint8_t format, uint8_t *out, uint64_t out_cap,
+                uint64_t *out_len) {
+    if ((!in && n) || !out_len) return CHIP_ERR_INVALID_ARG;
+    const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
+    const bool ecies = format & CHIP_FORMAT_ECIES, snap = format & CHIP_FORMAT_SNAPPY;
+    if (ecies && !secret_key) return CHIP_ERR_INVALID_ARG;
+    // device stages write to `out` directly unless host stages follow
+    thread_local std::vector<uint8_t> t_dev, t_mid;
+    const uint8_t *cur = in;
+    uint64_t cur_n = n;
+    if (zfec || bao) {
+        uint64_t blen = n;
+        if (bao) {
+            if (!hash || hash_len != CHIP_HASH_LEN) return CHIP_ERR_HASH_DECODE;
+            int st = bao_header(in, n, &blen);
+            if (st != CHIP_OK) return st;
+        }
+        uint64_t C = 0, olen = blen;
+        if (zfec) {
+            if (blen % CHIP_FEC_M != 0) return CHIP_ERR_UNEVEN_ZFEC_CHUNKS;  // decoding.rs:39-41
+            C = blen / CHIP_FEC_M;
+            if (padding > CHIP_FEC_K * C) return CHIP_ERR_ZFEC;
+            if (C % 16) return CHIP_ERR_ZFEC;
+            olen = CHIP_FEC_K * C - padding;
+        }
+        uint8_t *dst = out;
+        if (ecies || snap) {
+            t_dev.resize(olen + 1);
+            dst = t_dev.data();
+        } else if (olen && (!out || out_cap < olen)) {
+            *out_len = olen;
+            return CHIP_ERR_BUFFER_TOO_SMALL;
+        }
+        Ctx *c;
+        int st = ctx_get(&c);
         if (st != CHIP_OK) return st;
-        d_cur = static_cast<const uint8_t *>(c->mid.p);
+        const uint64_t in_bytes = bao ? bao_encoded_len(blen) : n;
+        CHIP_HIP(grow(c->in, in_bytes));
+        if (in_bytes) CHIP_HIP(hipMemcpyAsync(c->in.p, in, in_bytes, hipMemcpyHostToDevice, c->stream));
+        const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
+        if (bao) {  // decoding.rs:89-93
+            CHIP_HIP(grow(c->mid, blen));
+            st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p));
+            if (st != CHIP_OK) return st;
+            d_cur = static_cast<const uint8_t *>(c->mid.p);
+        }
+        if (zfec && C) {  // decoding.rs:95-99: shards by position, primaries present
+            CHIP_HIP(grow(c->out, CHIP_FEC_K * C));
+            std::vector<uint32_t> sel(CHIP_FEC_K);
+            std::vector<uint64_t> slot_off(CHIP_FEC_K);
+            for (uint32_t s = 0; s < CHIP_FEC_K; ++s) { sel[s] = s; slot_off[s] = s * C; }
+            st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_cur, 0, slot_off, sel, C, 1,
+                                    static_cast<uint8_t *>(c->out.p), 0, c->stream);
+            if (st != CHIP_OK) return st;
+            d_cur = static_cast<const uint8_t *>(c->out.p);
+        }
+        if (olen) CHIP_HIP(hipMemcpyAsync(dst, d_cur, olen, hipMemcpyDeviceToHost, c->stream));
+        CHIP_HIP(hipStreamSynchronize(c->stream));
+        cur = dst;
+        cur_n = olen;
     }
-    if (zfec && C) {  // decoding.rs:95-99: shards by position, primaries present
-        CHIP_HIP(grow(c->out, CHIP_FEC_K * C));
-        std::vector<uint32_t> sel(CHIP_FEC_K);
-        std::vector<uint64_t> slot_off(CHIP_FEC_K);
-        for (uint32_t s = 0; s < CHIP_FEC_K; ++s) { sel[s] = s; slot_off[s] = s * C; }
-        st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_cur, 0, slot_off, sel, C, 1,
-                                static_cast<uint8_t *>(c->out.p), 0, c->stream);
-        if (st != CHIP_OK) return st;
-        d_cur = static_cast<const uint8_t *>(c->out.p);
+    if (!ecies && !snap) {
+        if (!(zfec || bao)) {
+            if (n && (!out || out_cap < n)) {
+                *out_len = n;
+                return CHIP_ERR_BUFFER_TOO_SMALL;
+            }
+            if (n) std::memcpy(out, in, n);
+        }
+        *out_len = cur_n;
+        return CHIP_OK;
     }
-    if (olen) CHIP_HIP(hipMemcpyAsync(out, d_cur, olen, hipMemcpyDeviceToHost, c->stream));
-    CHIP_HIP(hipStreamSynchronize(c->stream));
-    *out_len = olen;
+    if (ecies) {  // decoding.rs:101-105
+        uint8_t *dst = out;
+        uint64_t cap = out_cap;
+        if (snap) {
+            t_mid.resize(cur_n + 1);
+            dst = t_mid.data();
+            cap = t_mid.size();
+        }
+        uint64_t got = 0;
+        int st = host::ecies_decrypt(secret_key, sk_len, cur, cur_n, dst, cap, &got);
+        if (st != CHIP_OK) {
+            if (st == CHIP_ERR_BUFFER_TOO_SMALL) *out_len = got;
+            return st;
+        }
+        cur = dst;
+        cur_n = got;
+    }
+    if (snap) {  // decoding.rs:107-111
+        return host::snap_decompress(cur, cur_n, out, out_cap, out_len);
+    }
+    *out_len = cur_n;
     return CHIP_OK;
 }
 

@@ -1,0 +1,577 @@
+// host_stages.cpp — snappy framing and ECIES for the host side of
+// encode()/decode() (encoding.rs:16-36 `snap`, `ecies`; decoding.rs:62-77).
+//
+// Snappy: the framing format of snap 1.1.0's FrameEncoder — stream identifier,
+// then one chunk per 64 KiB block: masked CRC-32C of the block, the block
+// compressed, or stored raw when compression saves less than 1/8 (the
+// `compress_len >= len - len/8` rule).  The block compressor restates the
+// published snappy encodeBlock (Go snappy; snap 1.x is a port of it): hash
+// table of 2^8..2^14 u16 entries, hash (u32 * 0x1E35A7BD) >> shift, the
+// skip/32 search acceleration, 15-byte input margin, copies split 64/60 and
+// encoded as copy-1 when len < 12 and offset < 2048.  Output for incompressible
+// data is canonical (raw chunks); for compressible data it follows the
+// restated algorithm (parity vs the snap crate itself is unpinned — DESIGN.md).
+//
+// ECIES: ecies 0.2.6 with its default config — receiver key parsed from 33 or
+// 65 bytes, ephemeral secp256k1 key, shared point = receiver * ephemeral,
+// key = HKDF-SHA256(salt = none, ikm = eph_pub65 || shared65, info = none),
+// AES-256-GCM with a 16-byte nonce and no AAD; output
+// eph_pub65 || nonce16 || tag16 || ciphertext.  Built on OpenSSL 3 libcrypto
+// (AES-NI/VAES GCM, EC arithmetic); both values the reference draws from its
+// RNG can be injected for bit-exact tests.
+#include "host_stages.hpp"
+
+#include <openssl/ec.h>
+#include <openssl/evp.h>
+#include <openssl/hmac.h>
+#include <openssl/obj_mac.h>
+#include <openssl/rand.h>
+
+#include <immintrin.h>
+
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../include/carbonado_hip.h"
+
+#pragma GCC diagnostic ignored "-Wdeprecated-declarations"
+
+namespace chip {
+namespace host {
+
+// ---------------------------------------------------------------- CRC-32C
+__attribute__((target("sse4.2"))) uint32_t crc32c(const uint8_t *p, size_t n) {
+    uint64_t c = 0xFFFFFFFFu;
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        c = _mm_crc32_u64(c, v);
+        p += 8;
+        n -= 8;
+    }
+    uint32_t c32 = (uint32_t)c;
+    while (n--) c32 = _mm_crc32_u8(c32, *p++);
+    return c32 ^ 0xFFFFFFFFu;
+}
+
+static uint32_t crc_masked(const uint8_t *p, size_t n) {
+    const uint32_t c = crc32c(p, n);
+    return ((c >> 15) | (c << 17)) + 0xA282EAD8u;
+}
+
+// ---------------------------------------------------------------- snappy block
+namespace {
+
+constexpr size_t MAX_BLOCK = 65536;
+constexpr size_t INPUT_MARGIN = 15;
+constexpr size_t MIN_NON_LITERAL_BLOCK = 1 + 1 + INPUT_MARGIN;
+constexpr size_t MAX_COMPRESS_BLOCK = 32 + MAX_BLOCK + MAX_BLOCK / 6;  // max_compress_len(64 KiB)
+constexpr uint8_t STREAM_ID[10] = {0xFF, 0x06, 0x00, 0x00, 's', 'N', 'a', 'P', 'p', 'Y'};
+
+inline uint32_t load32(const uint8_t *p) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;
+}
+inline uint64_t load64(const uint8_t *p) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+
+size_t put_varint(uint8_t *d, uint64_t v) {
+    size_t i = 0;
+    while (v >= 0x80) {
+        d[i++] = (uint8_t)(v | 0x80);
+        v >>= 7;
+    }
+    d[i++] = (uint8_t)v;
+    return i;
+}
+
+size_t emit_literal(uint8_t *d, const uint8_t *lit, size_t len) {
+    const size_t n = len - 1;
+    size_t i;
+    if (n < 60) {
+        d[0] = (uint8_t)(n << 2);
+        i = 1;
+    } else if (n < 256) {
+        d[0] = 60 << 2;
+        d[1] = (uint8_t)n;
+        i = 2;
+    } else {
+        d[0] = 61 << 2;
+        d[1] = (uint8_t)n;
+        d[2] = (uint8_t)(n >> 8);
+        i = 3;
+    }
+    std::memcpy(d + i, lit, len);
+    return i + len;
+}
+
+size_t emit_copy(uint8_t *d, size_t offset, size_t len) {
+    size_t i = 0;
+    while (len >= 68) {  // length-64 copy-2
+        d[i] = (63 << 2) | 2;
+        d[i + 1] = (uint8_t)offset;
+        d[i + 2] = (uint8_t)(offset >> 8);
+        i += 3;
+        len -= 64;
+    }
+    if (len > 64) {  // length-60 copy-2, leaving 5..8 for a short copy
+        d[i] = (59 << 2) | 2;
+        d[i + 1] = (uint8_t)offset;
+        d[i + 2] = (uint8_t)(offset >> 8);
+        i += 3;
+        len -= 60;
+    }
+    if (len >= 12 || offset >= 2048) {
+        d[i] = (uint8_t)(((len - 1) << 2) | 2);
+        d[i + 1] = (uint8_t)offset;
+        d[i + 2] = (uint8_t)(offset >> 8);
+        return i + 3;
+    }
+    d[i] = (uint8_t)(((offset >> 8) << 5) | ((len - 4) << 2) | 1);
+    d[i + 1] = (uint8_t)offset;
+    return i + 2;
+}
+
+// One block (n >= MIN_NON_LITERAL_BLOCK, n <= 64 KiB) without the varint header.
+size_t encode_block(uint8_t *dst, const uint8_t *src, size_t n) {
+    uint32_t shift = 24;
+    size_t tsize = 256;
+    while (tsize < 16384 && tsize < n) {
+        --shift;
+        tsize <<= 1;
+    }
+    uint16_t table[16384];
+    std::memset(table, 0, tsize * sizeof(uint16_t));
+    auto hash = [shift](uint32_t u) -> size_t { return (size_t)((u * 0x1E35A7BDu) >> shift); };
+
+    const size_t s_limit = n - INPUT_MARGIN;
+    size_t next_emit = 0, d = 0, s = 1;
+    size_t next_hash = hash(load32(src + s));
+    for (;;) {
+        size_t skip = 32, s_next = s, cand;
+        for (;;) {
+            s = s_next;
+            const size_t step = skip >> 5;
+            s_next = s + step;
+            skip += step;
+            if (s_next > s_limit) goto remainder;
+            cand = table[next_hash];
+            table[next_hash] = (uint16_t)s;
+            next_hash = hash(load32(src + s_next));
+            if (load32(src + s) == load32(src + cand)) break;
+        }
+        d += emit_literal(dst + d, src + next_emit, s - next_emit);
+        for (;;) {
+            const size_t base = s;
+            s += 4;
+            for (size_t i = cand + 4; s < n && src[i] == src[s]; ++i, ++s) {
+            }
+            d += emit_copy(dst + d, base - cand, s - base);
+            next_emit = s;
+            if (s >= s_limit) goto remainder;
+            const uint64_t x = load64(src + s - 1);
+            table[hash((uint32_t)x)] = (uint16_t)(s - 1);
+            const size_t ch = hash((uint32_t)(x >> 8));
+            cand = table[ch];
+            table[ch] = (uint16_t)s;
+            if ((uint32_t)(x >> 8) != load32(src + cand)) {
+                next_hash = hash((uint32_t)(x >> 16));
+                ++s;
+                break;
+            }
+        }
+    }
+remainder:
+    if (next_emit < n) d += emit_literal(dst + d, src + next_emit, n - next_emit);
+    return d;
+}
+
+// Raw snappy of one block (<= 64 KiB), varint header included.
+size_t compress_raw(uint8_t *dst, const uint8_t *src, size_t n) {
+    if (n == 0) {
+        dst[0] = 0;
+        return 1;
+    }
+    size_t d = put_varint(dst, n);
+    if (n < MIN_NON_LITERAL_BLOCK) return d + emit_literal(dst + d, src, n);
+    return d + encode_block(dst + d, src, n);
+}
+
+bool get_varint(const uint8_t *p, size_t n, uint64_t *v, size_t *used) {
+    uint64_t r = 0;
+    for (size_t i = 0; i < n && i < 10; ++i) {
+        r |= (uint64_t)(p[i] & 0x7F) << (7 * i);
+        if (!(p[i] & 0x80)) {
+            *v = r;
+            *used = i + 1;
+            return true;
+        }
+    }
+    return false;
+}
+
+// Raw snappy block decode into out[0..cap); returns false on corrupt input.
+bool decompress_raw(const uint8_t *src, size_t n, uint8_t *out, size_t cap, size_t *out_len) {
+    uint64_t dlen;
+    size_t used;
+    if (!get_varint(src, n, &dlen, &used) || dlen > cap) return false;
+    size_t s = used, d = 0;
+    while (s < n) {
+        const uint8_t tag = src[s];
+        size_t len, off;
+        switch (tag & 3) {
+            case 0: {  // literal
+                size_t x = tag >> 2;
+                if (x < 60) {
+                    s += 1;
+                } else {
+                    const size_t nb = x - 59;  // 1..4 length bytes
+                    if (s + 1 + nb > n) return false;
+                    x = 0;
+                    for (size_t b = 0; b < nb; ++b) x |= (size_t)src[s + 1 + b] << (8 * b);
+                    s += 1 + nb;
+                }
+                len = x + 1;
+                if (len > n - s || len > dlen - d) return false;
+                std::memcpy(out + d, src + s, len);
+                s += len;
+                d += len;
+                continue;
+            }
+            case 1:
+                if (s + 2 > n) return false;
+                len = 4 + ((tag >> 2) & 7);
+                off = ((size_t)(tag >> 5) << 8) | src[s + 1];
+                s += 2;
+                break;
+            case 2:
+                if (s + 3 > n) return false;
+                len = 1 + (tag >> 2);
+                off = (size_t)src[s + 1] | ((size_t)src[s + 2] << 8);
+                s += 3;
+                break;
+            default:
+                if (s + 5 > n) return false;
+                len = 1 + (tag >> 2);
+                off = (size_t)load32(src + s + 1);
+                s += 5;
+                break;
+        }
+        if (off == 0 || off > d || len > dlen - d) return false;
+        for (size_t i = 0; i < len; ++i, ++d) out[d] = out[d - off];  // overlapping copies
+    }
+    if (d != dlen) return false;
+    *out_len = d;
+    return true;
+}
+
+}  // namespace
+
+uint64_t snap_max_len(uint64_t n) {
+    if (n == 0) return 0;
+    return sizeof(STREAM_ID) + 8 * ((n + MAX_BLOCK - 1) / MAX_BLOCK) + n;
+}
+
+int snap_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    // FrameEncoder writes nothing at all for an empty input (no stream id).
+    if (n == 0) {
+        *out_len = 0;
+        return CHIP_OK;
+    }
+    if (cap < snap_max_len(n)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    std::vector<uint8_t> tmp(MAX_COMPRESS_BLOCK);
+    uint64_t d = 0;
+    std::memcpy(out, STREAM_ID, sizeof(STREAM_ID));
+    d += sizeof(STREAM_ID);
+    for (uint64_t o = 0; o < n; o += MAX_BLOCK) {
+        const size_t len = (size_t)((n - o) < MAX_BLOCK ? (n - o) : MAX_BLOCK);
+        const uint8_t *src = in + o;
+        const uint32_t crc = crc_masked(src, len);
+        const size_t clen = compress_raw(tmp.data(), src, len);
+        const bool raw = clen >= len - len / 8;
+        const size_t body = raw ? len : clen;
+        const uint32_t chunk_len = (uint32_t)(4 + body);
+        out[d] = raw ? 0x01 : 0x00;
+        out[d + 1] = (uint8_t)chunk_len;
+        out[d + 2] = (uint8_t)(chunk_len >> 8);
+        out[d + 3] = (uint8_t)(chunk_len >> 16);
+        std::memcpy(out + d + 4, &crc, 4);
+        std::memcpy(out + d + 8, raw ? src : tmp.data(), body);
+        d += 8 + body;
+    }
+    *out_len = d;
+    return CHIP_OK;
+}
+
+// Walk the chunks; if `out` is null only sizes are computed.
+static int snap_walk(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    uint64_t s = 0, d = 0;
+    bool ident = false;
+    while (s < n) {
+        if (n - s < 4) return CHIP_ERR_SNAP;
+        const uint8_t ty = in[s];
+        const uint64_t clen = (uint64_t)in[s + 1] | ((uint64_t)in[s + 2] << 8) | ((uint64_t)in[s + 3] << 16);
+        s += 4;
+        if (clen > n - s) return CHIP_ERR_SNAP;
+        const uint8_t *body = in + s;
+        if (!ident && ty != 0xFF) return CHIP_ERR_SNAP;  // stream must open with the identifier
+        if (ty == 0xFF) {
+            if (clen != 6 || std::memcmp(body, STREAM_ID + 4, 6) != 0) return CHIP_ERR_SNAP;
+            ident = true;
+        } else if (ty == 0x00 || ty == 0x01) {
+            if (clen < 4) return CHIP_ERR_SNAP;
+            uint32_t want;
+            std::memcpy(&want, body, 4);
+            const uint8_t *data = body + 4;
+            const uint64_t dl = clen - 4;
+            if (ty == 0x01) {
+                if (dl > MAX_BLOCK) return CHIP_ERR_SNAP;
+                if (out) {
+                    if (dl > cap - d) return CHIP_ERR_BUFFER_TOO_SMALL;
+                    if (crc_masked(data, dl) != want) return CHIP_ERR_SNAP;
+                    std::memcpy(out + d, data, dl);
+                }
+                d += dl;
+            } else {
+                uint64_t ulen;
+                size_t used;
+                if (!get_varint(data, dl, &ulen, &used) || ulen > MAX_BLOCK) return CHIP_ERR_SNAP;
+                if (out) {
+                    if (ulen > cap - d) return CHIP_ERR_BUFFER_TOO_SMALL;
+                    size_t got;
+                    if (!decompress_raw(data, dl, out + d, ulen, &got) || got != ulen) return CHIP_ERR_SNAP;
+                    if (crc_masked(out + d, ulen) != want) return CHIP_ERR_SNAP;
+                }
+                d += ulen;
+            }
+        } else if (ty >= 0x02 && ty <= 0x7F) {
+            return CHIP_ERR_SNAP;  // reserved unskippable
+        }  // 0x80..0xFE: padding / reserved skippable
+        s += clen;
+    }
+    *out_len = d;
+    return CHIP_OK;
+}
+
+int snap_decompressed_len(const uint8_t *in, uint64_t n, uint64_t *len) {
+    return snap_walk(in, n, nullptr, 0, len);
+}
+
+int snap_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    uint64_t need;
+    int st = snap_walk(in, n, nullptr, 0, &need);
+    if (st != CHIP_OK) return st;
+    if (need > cap || (need && !out)) {
+        *out_len = need;
+        return CHIP_ERR_BUFFER_TOO_SMALL;
+    }
+    return snap_walk(in, n, out, cap, out_len);
+}
+
+// ---------------------------------------------------------------- ECIES
+namespace {
+
+struct EcCtx {
+    EC_GROUP *g = nullptr;
+    BN_CTX *bn = nullptr;
+    EcCtx() {
+        g = EC_GROUP_new_by_curve_name(NID_secp256k1);
+        bn = BN_CTX_new();
+    }
+    ~EcCtx() {
+        BN_CTX_free(bn);
+        EC_GROUP_free(g);
+    }
+};
+
+EcCtx &ec() {
+    thread_local EcCtx c;
+    return c;
+}
+
+struct BnPtr {
+    BIGNUM *p;
+    explicit BnPtr(BIGNUM *x) : p(x) {}
+    ~BnPtr() { BN_clear_free(p); }
+};
+struct PtPtr {
+    EC_POINT *p;
+    explicit PtPtr(EC_POINT *x) : p(x) {}
+    ~PtPtr() { EC_POINT_free(p); }
+};
+
+// libsecp256k1 SecretKey::parse: 32 bytes, 0 < k < n
+BIGNUM *parse_secret(const uint8_t *sk, uint64_t len) {
+    if (len != 32) return nullptr;
+    BIGNUM *k = BN_bin2bn(sk, 32, nullptr);
+    if (!k) return nullptr;
+    if (BN_is_zero(k) || BN_cmp(k, EC_GROUP_get0_order(ec().g)) >= 0) {
+        BN_clear_free(k);
+        return nullptr;
+    }
+    return k;
+}
+
+// libsecp256k1 PublicKey::parse_slice(.., None): 33 (compressed), 64 (raw x||y) or 65 bytes
+EC_POINT *parse_public(const uint8_t *pk, uint64_t len) {
+    uint8_t buf[65];
+    const uint8_t *p = pk;
+    size_t l = (size_t)len;
+    if (len == 64) {
+        buf[0] = 0x04;
+        std::memcpy(buf + 1, pk, 64);
+        p = buf;
+        l = 65;
+    } else if (len != 33 && len != 65) {
+        return nullptr;
+    }
+    EC_POINT *pt = EC_POINT_new(ec().g);
+    if (!pt) return nullptr;
+    if (EC_POINT_oct2point(ec().g, pt, p, l, ec().bn) != 1 || EC_POINT_is_at_infinity(ec().g, pt)) {
+        EC_POINT_free(pt);
+        return nullptr;
+    }
+    return pt;
+}
+
+bool point65(const EC_POINT *pt, uint8_t out[65]) {
+    return EC_POINT_point2oct(ec().g, pt, POINT_CONVERSION_UNCOMPRESSED, out, 65, ec().bn) == 65;
+}
+
+// HKDF-SHA256 (RFC 5869) with no salt and no info, 32-byte output: one HMAC
+// for the extract step, one for T(1).
+bool hkdf_sha256_32(const uint8_t *ikm, size_t n, uint8_t out[32]) {
+    uint8_t zero[32] = {0}, prk[32];
+    unsigned int l = 0;
+    if (!HMAC(EVP_sha256(), zero, 32, ikm, n, prk, &l) || l != 32) return false;
+    const uint8_t one = 0x01;
+    uint8_t t[32];
+    if (!HMAC(EVP_sha256(), prk, 32, &one, 1, t, &l) || l != 32) return false;
+    std::memcpy(out, t, 32);
+    OPENSSL_cleanse(prk, 32);
+    OPENSSL_cleanse(t, 32);
+    return true;
+}
+
+// encapsulate / decapsulate: key = HKDF(eph_pub65 || (peer * secret)65)
+bool derive_key(const BIGNUM *secret, const EC_POINT *peer, const uint8_t eph_pub[65], uint8_t key[32]) {
+    PtPtr shared(EC_POINT_new(ec().g));
+    if (!shared.p || EC_POINT_mul(ec().g, shared.p, nullptr, peer, secret, ec().bn) != 1) return false;
+    uint8_t master[130];
+    std::memcpy(master, eph_pub, 65);
+    if (!point65(shared.p, master + 65)) return false;
+    const bool ok = hkdf_sha256_32(master, 130, key);
+    OPENSSL_cleanse(master, sizeof master);
+    return ok;
+}
+
+struct CipherCtx {
+    EVP_CIPHER_CTX *c = EVP_CIPHER_CTX_new();
+    ~CipherCtx() { EVP_CIPHER_CTX_free(c); }
+};
+
+// AES-256-GCM over arbitrarily long buffers (EVP takes int lengths)
+bool gcm_update(EVP_CIPHER_CTX *c, bool enc, const uint8_t *in, uint64_t n, uint8_t *out) {
+    constexpr uint64_t STEP = 1ull << 30;
+    for (uint64_t o = 0; o < n; o += STEP) {
+        const int len = (int)((n - o) < STEP ? (n - o) : STEP);
+        int got = 0;
+        const int ok = enc ? EVP_EncryptUpdate(c, out + o, &got, in + o, len)
+                           : EVP_DecryptUpdate(c, out + o, &got, in + o, len);
+        if (ok != 1 || got != len) return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+int ecies_public_key(const uint8_t *secret, uint8_t out[65]) {
+    BnPtr k(parse_secret(secret, 32));
+    if (!k.p) return CHIP_ERR_ECIES;
+    PtPtr pub(EC_POINT_new(ec().g));
+    if (!pub.p || EC_POINT_mul(ec().g, pub.p, k.p, nullptr, nullptr, ec().bn) != 1 || !point65(pub.p, out))
+        return CHIP_ERR_ECIES;
+    return CHIP_OK;
+}
+
+int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                  const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    if (cap < n + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
+    PtPtr peer(parse_public(pubkey, pubkey_len));
+    if (!peer.p) return CHIP_ERR_ECIES;
+    uint8_t sk[32];
+    if (eph_sk) {
+        std::memcpy(sk, eph_sk, 32);
+    } else {
+        for (;;) {  // SecretKey::random: rejection-sample a valid scalar
+            if (RAND_bytes(sk, 32) != 1) return CHIP_ERR_ECIES;
+            BnPtr t(parse_secret(sk, 32));
+            if (t.p) break;
+        }
+    }
+    BnPtr k(parse_secret(sk, 32));
+    OPENSSL_cleanse(sk, 32);
+    if (!k.p) return CHIP_ERR_ECIES;
+    PtPtr eph(EC_POINT_new(ec().g));
+    if (!eph.p || EC_POINT_mul(ec().g, eph.p, k.p, nullptr, nullptr, ec().bn) != 1 || !point65(eph.p, out))
+        return CHIP_ERR_ECIES;
+    uint8_t key[32];
+    if (!derive_key(k.p, peer.p, out, key)) return CHIP_ERR_ECIES;
+
+    uint8_t *iv = out + 65, *tag = out + 81, *ct = out + 97;
+    if (nonce) std::memcpy(iv, nonce, 16);
+    else if (RAND_bytes(iv, 16) != 1) return CHIP_ERR_ECIES;
+    CipherCtx cc;
+    bool ok = cc.c && EVP_EncryptInit_ex(cc.c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+              EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
+              EVP_EncryptInit_ex(cc.c, nullptr, nullptr, key, iv) == 1 && gcm_update(cc.c, true, in, n, ct);
+    OPENSSL_cleanse(key, 32);
+    int fin = 0;
+    ok = ok && EVP_EncryptFinal_ex(cc.c, ct + n, &fin) == 1 && fin == 0 &&
+         EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_GET_TAG, 16, tag) == 1;
+    if (!ok) return CHIP_ERR_ECIES;
+    *out_len = n + ECIES_OVERHEAD;
+    return CHIP_OK;
+}
+
+int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
+                  uint64_t cap, uint64_t *out_len) {
+    BnPtr k(parse_secret(secret, secret_len));
+    if (!k.p) return CHIP_ERR_ECIES;
+    if (n < ECIES_OVERHEAD) return CHIP_ERR_ECIES;  // InvalidMessage
+    const uint64_t m = n - ECIES_OVERHEAD;
+    if (cap < m || (m && !out)) {
+        *out_len = m;
+        return CHIP_ERR_BUFFER_TOO_SMALL;
+    }
+    PtPtr eph(parse_public(in, 65));
+    if (!eph.p) return CHIP_ERR_ECIES;
+    uint8_t key[32];
+    if (!derive_key(k.p, eph.p, in, key)) return CHIP_ERR_ECIES;
+    const uint8_t *iv = in + 65, *tag = in + 81, *ct = in + 97;
+    CipherCtx cc;
+    uint8_t tagbuf[16];
+    std::memcpy(tagbuf, tag, 16);
+    bool ok = cc.c && EVP_DecryptInit_ex(cc.c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+              EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
+              EVP_DecryptInit_ex(cc.c, nullptr, nullptr, key, iv) == 1 && gcm_update(cc.c, false, ct, m, out) &&
+              EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_TAG, 16, tagbuf) == 1;
+    OPENSSL_cleanse(key, 32);
+    int fin = 0;
+    uint8_t dummy[16];
+    ok = ok && EVP_DecryptFinal_ex(cc.c, m ? out + m : dummy, &fin) == 1;
+    if (!ok) {
+        if (m) OPENSSL_cleanse(out, m);  // never hand back unauthenticated plaintext
+        return CHIP_ERR_ECIES;
+    }
+    *out_len = m;
+    return CHIP_OK;
+}
+
+}  // namespace host
+}  // namespace chip

@@ -1,0 +1,39 @@
+// host_stages.hpp — the host-side stages that bracket the GPU path in
+// encode()/decode() (encoding.rs:16-36, decoding.rs:62-77): snappy framing and
+// ECIES.  They run on host threads, overlapped with the device pipeline by
+// chip_encode_host_batch; the GPU path itself starts at zfec.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+namespace chip {
+namespace host {
+
+// CRC-32C (Castagnoli), as used by the snappy framing format.
+uint32_t crc32c(const uint8_t *p, size_t n);
+
+// ---- snappy (snap 1.1.0: write::FrameEncoder / read::FrameDecoder) -------
+// Upper bound of snap_compress's output for n input bytes.
+uint64_t snap_max_len(uint64_t n);
+// Framed stream of `in` into out[0..cap).  0 = ok, else a CHIP status.
+int snap_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+// Decompressed size of a framed stream (validates chunk structure, not CRCs).
+int snap_decompressed_len(const uint8_t *in, uint64_t n, uint64_t *len);
+// Full decode with CRC checks.
+int snap_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+
+// ---- ECIES (ecies 0.2.6 defaults: secp256k1, uncompressed keys, HKDF-SHA256,
+// AES-256-GCM with a 16-byte nonce) ----------------------------------------
+constexpr uint64_t ECIES_OVERHEAD = 65 + 16 + 16;
+// eph_sk / nonce: injected ephemeral secret (32 B) and nonce (16 B), or null
+// for fresh random values (the reference draws both from thread_rng).
+int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                  const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
+                  uint64_t cap, uint64_t *out_len);
+// Public key (65 B uncompressed) of a 32-byte secret; for tests and tooling.
+int ecies_public_key(const uint8_t *secret, uint8_t out[65]);
+
+}  // namespace host
+}  // namespace chip

@@ -62,18 +62,52 @@ def bao(input, hash: bytes) -> bytes:
     return out[: olen.value].tobytes()
 
 
-def decode(secret_key: bytes, hash: bytes, input, padding: int, format: int) -> bytes:
-    """decoding.rs:80-114 `decode(secret_key, hash, input, padding, format)`."""
-    del secret_key  # used only by the ECIES stage (out of scope)
+def ecies(input, secret_key: bytes) -> bytes:
+    """decoding.rs:62-68: ecies::decrypt(secret_key, input)."""
     a = as_u8(input)
-    h = as_u8(hash)
-    fmt = Format(format)
-    cap = a.size
+    sk = as_u8(secret_key)
+    cap = max(a.size - 97, 0)
     out = np.empty(max(cap, 1), dtype=np.uint8)
     olen = ctypes.c_uint64()
-    check(_lib.lib().chip_decode(ptr(h), h.size, ptr(a), a.size, padding, int(fmt), ptr(out), cap,
-                                 ctypes.byref(olen)))
+    check(_lib.lib().chip_ecies_decrypt(ptr(sk), sk.size, ptr(a), a.size, ptr(out), cap, ctypes.byref(olen)))
     return out[: olen.value].tobytes()
+
+
+def _grow_call(fn, cap: int) -> bytes:
+    """Call fn(out, cap, olen); on BUFFER_TOO_SMALL retry once with the size
+    the library reports (snappy output size is known only after parsing)."""
+    from .error import BufferTooSmall
+    for _ in range(2):
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        olen = ctypes.c_uint64()
+        st = fn(out, cap, olen)
+        if st == BufferTooSmall.status and olen.value > cap:
+            cap = olen.value
+            continue
+        check(st)
+        return out[: olen.value].tobytes()
+    check(st)
+
+
+def snap(input) -> bytes:
+    """decoding.rs:70-77: snap::read::FrameDecoder::read_to_end."""
+    a = as_u8(input)
+    return _grow_call(lambda out, cap, olen: _lib.lib().chip_snap_decompress(ptr(a), a.size, ptr(out), cap,
+                                                                             ctypes.byref(olen)),
+                      2 * a.size + 1024)
+
+
+def decode(secret_key: bytes, hash: bytes, input, padding: int, format: int) -> bytes:
+    """decoding.rs:80-114 `decode(secret_key, hash, input, padding, format)`:
+    bao → zfec on the device, then ecies → snap as host stages."""
+    a = as_u8(input)
+    h = as_u8(hash)
+    sk = as_u8(secret_key)
+    fmt = Format(format)
+    cap = a.size * (3 if fmt & Format.Snappy else 1) + 1024
+    return _grow_call(lambda out, c, olen: _lib.lib().chip_decode(
+        ptr(sk) if sk.size else None, sk.size, ptr(h), h.size, ptr(a), a.size, padding, int(fmt), ptr(out), c,
+        ctypes.byref(olen)), cap)
 
 
 def extract_slice(encoded, index: int, slice_len: int = 1024) -> bytes:

@@ -69,18 +69,30 @@ def bao_decode_batch(enc: torch.Tensor, n: int, hashes: torch.Tensor, out: torch
 
 
 def encode_host_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes: torch.Tensor,
-                      nslots: int = 3, slice_bytes: int = 256 << 20):
+                      nslots: int = 3, slice_bytes: int = 256 << 20, pubkey: bytes = b"",
+                      ephemeral_sk=None, nonce=None, host_threads: int = 0):
     """End-to-end encode() of `count` objects held in HOST memory (pinned
     tensors reach the full PCIe rate): inp uint8 [count, >= n], out uint8
-    [count, >= encoded length], hashes uint8 [count, 32].  Synchronous.
-    Returns (encoded length per object, EncodeInfo)."""
+    [count, >= chip_encode_max_len(n)], hashes uint8 [count, 32].  The
+    Snappy/Ecies host stages of a slice run on `host_threads` threads while
+    earlier slices are on the device.  `ephemeral_sk` [count, 32] / `nonce`
+    [count, 16] (uint8 tensors or arrays) inject the ECIES randomness (tests).
+    Synchronous.  Returns (encoded length per object, EncodeInfo per object)."""
+    import numpy as np
     from .structs import EncodeInfo
     assert not inp.is_cuda and not out.is_cuda and not hashes.is_cuda
     assert inp.is_contiguous() and out.is_contiguous() and hashes.is_contiguous()
     count = inp.shape[0]
-    olen = ctypes.c_uint64()
-    info = _lib.EncodeInfoC()
-    check(_lib.lib().chip_encode_host_batch(fmt, _p(inp), n, count, inp.shape[1], _p(out), out.shape[1],
-                                            ctypes.byref(olen), _p(hashes), ctypes.byref(info), nslots,
-                                            slice_bytes))
-    return olen.value, EncodeInfo.from_c(info)
+    olen = (ctypes.c_uint64 * max(count, 1))()
+    info = (_lib.EncodeInfoC * max(count, 1))()
+    keep = [np.ascontiguousarray(np.asarray(x, dtype=np.uint8)) if x is not None else None
+            for x in (ephemeral_sk, nonce)]
+    inj = None
+    if any(k is not None for k in keep):
+        inj = _lib.EciesInjectC(*[k.ctypes.data if k is not None else None for k in keep])
+    pk = np.frombuffer(bytes(pubkey), dtype=np.uint8)
+    check(_lib.lib().chip_encode_host_batch(fmt, pk.ctypes.data if pk.size else None, pk.size,
+                                            ctypes.byref(inj) if inj is not None else None, _p(inp), n, count,
+                                            inp.shape[1], _p(out), out.shape[1], olen, _p(hashes), info,
+                                            nslots, slice_bytes, host_threads))
+    return [olen[o] for o in range(count)], [EncodeInfo.from_c(info[o]) for o in range(count)]

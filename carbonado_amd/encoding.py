@@ -1,6 +1,6 @@
-"""encoding (mirror of /root/reference/src/encoding.rs), hot-path stages on
-the MI355X through libcarbonado_hip.  Snappy/ECIES are host stages outside
-this path: their format bits raise UnsupportedFormat."""
+"""encoding (mirror of /root/reference/src/encoding.rs) through
+libcarbonado_hip: zfec and bao on the MI355X, snap and ecies as the
+library's host stages (host_stages.cpp)."""
 from __future__ import annotations
 
 import ctypes
@@ -11,6 +11,54 @@ from . import _lib
 from ._buf import as_u8, check, ptr
 from .constants import FEC_K, FEC_M, Format
 from .structs import EncodeInfo, Encoded
+
+
+def _inject(ephemeral_sk: bytes | None, nonce: bytes | None):
+    """chip_ecies_inject for test determinism; None = the reference's RNG."""
+    if ephemeral_sk is None and nonce is None:
+        return None, ()
+    keep = tuple(as_u8(x) for x in (ephemeral_sk, nonce) if x is not None)
+    inj = _lib.EciesInjectC(
+        ptr(as_u8(ephemeral_sk)) if ephemeral_sk is not None else None,
+        ptr(as_u8(nonce)) if nonce is not None else None)
+    if ephemeral_sk is not None:
+        assert len(ephemeral_sk) == 32
+    if nonce is not None:
+        assert len(nonce) == 16
+    return inj, keep
+
+
+def snap(input) -> bytes:
+    """encoding.rs:16-28: snap::write::FrameEncoder output."""
+    a = as_u8(input)
+    L = _lib.lib()
+    cap = L.chip_snap_max_len(a.size)
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    olen = ctypes.c_uint64()
+    check(L.chip_snap_compress(ptr(a), a.size, ptr(out), cap, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def ecies(pubkey: bytes, input, *, ephemeral_sk: bytes | None = None, nonce: bytes | None = None) -> bytes:
+    """encoding.rs:30-36: ecies::encrypt(pubkey, input); n + 97 bytes.
+    `ephemeral_sk`/`nonce` inject the two random values (tests only)."""
+    a = as_u8(input)
+    pk = as_u8(pubkey)
+    cap = a.size + 97
+    out = np.empty(cap, dtype=np.uint8)
+    olen = ctypes.c_uint64()
+    inj, _keep = _inject(ephemeral_sk, nonce)
+    check(_lib.lib().chip_ecies_encrypt(ptr(pk), pk.size, ctypes.byref(inj) if inj is not None else None,
+                                        ptr(a), a.size, ptr(out), cap, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def public_key(secret_key: bytes) -> bytes:
+    """secp256k1 public key (65 bytes, uncompressed) of a 32-byte secret."""
+    sk = as_u8(secret_key)
+    out = np.empty(65, dtype=np.uint8)
+    check(_lib.lib().chip_ecies_public_key(ptr(sk), ptr(out)))
+    return out.tobytes()
 
 
 def zfec(input, k: int = FEC_K, m: int = FEC_M) -> tuple[bytes, int, int]:
@@ -44,19 +92,23 @@ def blake3(input) -> bytes:
     return h.tobytes()
 
 
-def encode(pubkey: bytes, input, format: int) -> Encoded:
+def encode(pubkey: bytes, input, format: int, *, ephemeral_sk: bytes | None = None,
+           nonce: bytes | None = None) -> Encoded:
     """encoding.rs:86-172 `encode(pubkey, input, format) -> Encoded`.
 
-    The zfec → bao chain runs device-resident (the zfec output never returns
-    to the host).  `pubkey` is only used by the ECIES stage (out of scope)."""
-    del pubkey
+    snap → ecies run as host stages, then zfec → bao device-resident (the
+    zfec output never returns to the host).  `pubkey` is used by the ECIES
+    stage only; `ephemeral_sk`/`nonce` inject its random values (tests)."""
     a = as_u8(input)
+    pk = as_u8(pubkey)
     L = _lib.lib()
     cap = L.chip_encode_max_len(a.size)
     out = np.empty(max(cap, 1), dtype=np.uint8)
     h = np.empty(32, dtype=np.uint8)
     olen = ctypes.c_uint64()
     info = _lib.EncodeInfoC()
-    check(L.chip_encode(int(Format(format)), ptr(a), a.size, ptr(out), cap, ctypes.byref(olen), ptr(h),
-                        ctypes.byref(info)))
+    inj, _keep = _inject(ephemeral_sk, nonce)
+    check(L.chip_encode(int(Format(format)), ptr(pk) if pk.size else None, pk.size,
+                        ctypes.byref(inj) if inj is not None else None, ptr(a), a.size, ptr(out), cap,
+                        ctypes.byref(olen), ptr(h), ctypes.byref(info)))
     return Encoded(out[: olen.value].tobytes(), h.tobytes(), EncodeInfo.from_c(info))

@@ -59,8 +59,18 @@ class InvalidVerifiableSliceCount(CarbonadoError):
 
 
 class UnsupportedFormat(CarbonadoError):
-    """Ecies/Snappy format bits: host stages outside this hot path."""
+    """Reserved status (ABI 1 rejected the Ecies/Snappy bits with it)."""
     status = 11
+
+
+class SnapError(CarbonadoError):
+    """error.rs:7,35 StdIoError / SnapError: FrameDecoder rejected the stream."""
+    status = 16
+
+
+class EciesError(CarbonadoError):
+    """error.rs:43 EciesError: bad key, short input or AES-GCM tag mismatch."""
+    status = 17
 
 
 class UnnecessaryScrub(CarbonadoError):
@@ -117,7 +127,11 @@ def status_to_error(status: int, detail: str = "") -> CarbonadoError:
     if status == 10:
         return InvalidVerifiableSliceCount("Verifiable slice count should be evenly divisible by 8.")
     if status == 11:
-        return UnsupportedFormat("format bit handled by a host stage outside this path")
+        return UnsupportedFormat("unsupported format")
+    if status == 16:
+        return SnapError("snappy framing error")
+    if status == 17:
+        return EciesError("ecies error")
     if status == 12:
         return UnnecessaryScrub()
     if status == 13:

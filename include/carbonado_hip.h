@@ -14,9 +14,14 @@
  *                              (with explicit share indices; see below)
  *   chip_bao_decode         <- decoding::bao         src/decoding.rs:53-60
  *
- * plus the glue that calls them (for the Bao|Zfec format bits):
+ * plus the glue that calls them:
  *   chip_encode             <- encoding::encode      src/encoding.rs:86-172
  *   chip_decode             <- decoding::decode      src/decoding.rs:80-114
+ * the host stages that bracket the GPU path (run on host threads):
+ *   chip_snap_compress      <- encoding::snap        src/encoding.rs:16-28
+ *   chip_snap_decompress    <- decoding::snap        src/decoding.rs:70-77
+ *   chip_ecies_encrypt      <- encoding::ecies       src/encoding.rs:30-36
+ *   chip_ecies_decrypt      <- decoding::ecies       src/decoding.rs:62-68
  * and helpers:
  *   chip_calc_padding_len   <- utils::calc_padding_len src/utils.rs:47-58
  *
@@ -51,7 +56,7 @@ extern "C" {
 #define CHIP_API
 #endif
 
-#define CHIP_ABI_VERSION 1
+#define CHIP_ABI_VERSION 2
 #define CHIP_HASH_LEN 32   /* bao::HASH_SIZE */
 #define CHIP_SLICE_LEN 1024 /* constants.rs:9 SLICE_LEN */
 #define CHIP_FEC_K 4        /* constants.rs:11 FEC_K */
@@ -75,11 +80,13 @@ typedef enum chip_status {
     CHIP_ERR_ENCODE_ZFEC_PADDING = 8,/* CarbonadoError::EncodeZfecPaddingError error.rs:85-87 */
     CHIP_ERR_ENCODE_INVALID_CHUNK_LENGTH = 9, /* error.rs:89-91 */
     CHIP_ERR_INVALID_VERIFIABLE_SLICE_COUNT = 10, /* error.rs:93-95 */
-    CHIP_ERR_UNSUPPORTED_FORMAT = 11,/* Ecies/Snappy bits: host stages, not on this path */
+    CHIP_ERR_UNSUPPORTED_FORMAT = 11,/* reserved (ABI 1: Ecies/Snappy bits)       */
     CHIP_ERR_UNNECESSARY_SCRUB = 12, /* CarbonadoError::UnnecessaryScrub       error.rs:65-67 */
     CHIP_ERR_SCRUBBED_PADDING_MISMATCH = 13, /* ScrubbedPaddingMismatch         error.rs:69-71 */
     CHIP_ERR_SCRUBBED_LENGTH_MISMATCH = 14,  /* ScrubbedLengthMismatch          error.rs:73-75 */
     CHIP_ERR_INVALID_SCRUBBED_HASH = 15,     /* InvalidScrubbedHash             error.rs:81-83 */
+    CHIP_ERR_SNAP = 16,              /* snappy framing error: StdIoError / SnapError error.rs:7,35 */
+    CHIP_ERR_ECIES = 17,             /* CarbonadoError::EciesError (bad key, bad tag) error.rs:43 */
     CHIP_ERR_NO_DEVICE = 100,        /* new variant: no usable gfx950 device     */
     CHIP_ERR_DEVICE = 101            /* new variant: HIP runtime error            */
 } chip_status;
@@ -100,6 +107,15 @@ typedef struct chip_encode_info {
     uint16_t chunk_slice_count;
 } chip_encode_info;
 
+/* The two values ecies::encrypt draws from thread_rng (ephemeral secret key,
+ * AES-GCM nonce).  NULL fields (or a NULL struct) = fresh random values, as the
+ * reference; injected values make encode() deterministic for parity tests.
+ * For batch calls the arrays hold one value per object. */
+typedef struct chip_ecies_inject {
+    const uint8_t *ephemeral_sk; /* 32 bytes per object, 0 < k < n */
+    const uint8_t *nonce;        /* 16 bytes per object */
+} chip_ecies_inject;
+
 /* ---- library ---------------------------------------------------------- */
 CHIP_API int chip_abi_version(void);
 CHIP_API const char *chip_strerror(int status);
@@ -118,8 +134,10 @@ CHIP_API int chip_calc_padding_len(uint64_t input_len, uint32_t k, uint32_t *pad
 CHIP_API uint64_t chip_zfec_encoded_len(uint64_t input_len, uint32_t k, uint32_t m);
 /* 8 + n + 64 * (max(1, ceil(n/1024)) - 1) */
 CHIP_API uint64_t chip_bao_encoded_len(uint64_t content_len);
-/* upper bound of chip_encode's output for an n-byte input (format-independent) */
+/* upper bound of chip_encode's output for an n-byte input (any format bits) */
 CHIP_API uint64_t chip_encode_max_len(uint64_t input_len);
+/* upper bound of chip_snap_compress's output */
+CHIP_API uint64_t chip_snap_max_len(uint64_t input_len);
 
 /* ---- stage functions (host buffers) ----------------------------------- */
 /* encoding::zfec (encoding.rs:48-81).  out receives m*chunk_len bytes laid out
@@ -160,29 +178,59 @@ CHIP_API int chip_bao_decode(const uint8_t *enc, uint64_t len, const uint8_t *ha
 /* BLAKE3 of a host buffer, computed on the device (bao root hash). */
 CHIP_API int chip_blake3(const uint8_t *in, uint64_t n, uint8_t hash[CHIP_HASH_LEN]);
 
+/* ---- host stages (host buffers, host threads; no device) --------------- */
+/* encoding::snap (encoding.rs:16-28): snap 1.1 FrameEncoder output (stream
+ * identifier, one chunk per 64 KiB block with the masked CRC-32C, raw when
+ * compression saves < 1/8).  An empty input gives an empty output. */
+CHIP_API int chip_snap_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                                uint64_t *out_len);
+/* decoding::snap (decoding.rs:70-77): FrameDecoder::read_to_end.  Corrupt
+ * frames or CRC mismatch -> CHIP_ERR_SNAP.  A short buffer returns
+ * CHIP_ERR_BUFFER_TOO_SMALL with *out_len = the decompressed size. */
+CHIP_API int chip_snap_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                                  uint64_t *out_len);
+/* encoding::ecies (encoding.rs:30-36 -> ecies 0.2.6 encrypt): receiver key of
+ * 33/64/65 bytes; output eph_pub(65) || nonce(16) || tag(16) || ciphertext,
+ * n + 97 bytes.  inject = NULL for random ephemeral key and nonce. */
+CHIP_API int chip_ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const chip_ecies_inject *inject,
+                                const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                                uint64_t *out_len);
+/* decoding::ecies (decoding.rs:62-68 -> ecies::decrypt): bad key, short input
+ * or tag mismatch -> CHIP_ERR_ECIES. */
+CHIP_API int chip_ecies_decrypt(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *in, uint64_t n,
+                                uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+/* secp256k1 public key (65 bytes, uncompressed) of a 32-byte secret key. */
+CHIP_API int chip_ecies_public_key(const uint8_t *secret_key, uint8_t pubkey[65]);
+
 /* ---- pipeline glue (host buffers) -------------------------------------- */
-/* encoding::encode (encoding.rs:86-172) for format bits Bao|Zfec; the zfec
- * output stays device-resident for the bao stage.  Ecies/Snappy bits ->
- * CHIP_ERR_UNSUPPORTED_FORMAT (host stages, out of this path's scope). */
-CHIP_API int chip_encode(uint8_t format, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
-                uint64_t *out_len, uint8_t hash[CHIP_HASH_LEN], chip_encode_info *info);
-/* decoding::decode (decoding.rs:80-114) for format bits Bao|Zfec. */
-CHIP_API int chip_decode(const uint8_t *hash, uint64_t hash_len, const uint8_t *in, uint64_t n,
-                uint32_t padding, uint8_t format, uint8_t *out, uint64_t out_cap,
-                uint64_t *out_len);
+/* encoding::encode (encoding.rs:86-172): snap -> ecies on the host, then
+ * zfec -> bao on the device (the zfec output stays device-resident for the
+ * bao stage).  pubkey is used only with the Ecies bit. */
+CHIP_API int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len,
+                const chip_ecies_inject *inject, const uint8_t *in, uint64_t n, uint8_t *out,
+                uint64_t out_cap, uint64_t *out_len, uint8_t hash[CHIP_HASH_LEN], chip_encode_info *info);
+/* decoding::decode (decoding.rs:80-114): bao -> zfec on the device, then
+ * ecies -> snap on the host.  With the Snappy bit the output size is only
+ * known after decompression: a short buffer returns CHIP_ERR_BUFFER_TOO_SMALL
+ * with *out_len = the size needed. */
+CHIP_API int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash, uint64_t hash_len,
+                const uint8_t *in, uint64_t n, uint32_t padding, uint8_t format, uint8_t *out,
+                uint64_t out_cap, uint64_t *out_len);
 
 /* ---- device-resident batch API (the throughput path) ------------------ */
 /* `count` objects of `n` bytes each; object o's input at d_in + o*in_stride
  * (bytes beyond n inside the padded object read as zero, exactly as
  * encoding.rs:53-55 pads), its m*chunk_len-byte output at d_out + o*out_stride.
- * in_stride and out_stride must be multiples of 16. */
+ * d_in, d_out, in_stride and out_stride must be multiples of 16
+ * (CHIP_ERR_INVALID_ARG otherwise). */
 CHIP_API int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
                                uint64_t n, uint64_t count, uint8_t *d_out, uint64_t out_stride,
                                void *stream);
 /* Erasure decode of `count` encoded objects (chunk_len-byte shards, shard i of
  * object o at d_in + o*in_stride + i*chunk_len).  idx[0..nshares) names the
  * shares that survive (same pattern for every object); the k*chunk_len data
- * bytes of object o go to d_out + o*out_stride (caller truncates `padding`). */
+ * bytes of object o go to d_out + o*out_stride (caller truncates `padding`).
+ * Pointers, strides and chunk_len must be multiples of 16. */
 CHIP_API int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
                                uint64_t chunk_len, const uint32_t *idx, uint32_t nshares,
                                uint64_t count, uint8_t *d_out, uint64_t out_stride, void *stream);
@@ -230,16 +278,19 @@ CHIP_API int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, u
 /* ---- host-memory batch (end-to-end: host -> HBM -> host) -------------- */
 /* encode() for `count` objects of n bytes that live in HOST memory (object o
  * at in + o*in_stride) into host memory (stream o at out + o*out_stride,
- * length *out_len each; hash o at hashes + 32*o).  Objects are processed in
- * slices over `nslots` device slots, each with its own stream, so the H2D
- * copy of one slice, the kernels of the next and the D2H copy of a third
- * overlap (PCIe full duplex).  Pinned (page-locked) host buffers reach the
- * full PCIe rate; pageable ones are staged by the runtime.  Format bits as
- * chip_encode (Bao|Zfec).  `info` receives the (identical) EncodeInfo. */
-CHIP_API int chip_encode_host_batch(uint8_t format, const uint8_t *in, uint64_t n, uint64_t count,
-                                    uint64_t in_stride, uint8_t *out, uint64_t out_stride,
+ * length out_len[o]; hash o at hashes + 32*o; EncodeInfo o at info[o], info
+ * may be NULL).  Objects are processed in slices over `nslots` device slots,
+ * each with its own stream, so the H2D copy of one slice, the kernels of the
+ * next and the D2H copy of a third overlap (PCIe full duplex); the host
+ * stages (Snappy/Ecies bits) of a slice run on `host_threads` host threads
+ * (0 = one per hardware thread, at most 64) while earlier slices are on the
+ * device.  out_stride must hold chip_encode_max_len(n).  Pinned host buffers
+ * reach the full PCIe rate; pageable ones are staged by the runtime. */
+CHIP_API int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len,
+                                    const chip_ecies_inject *inject, const uint8_t *in, uint64_t n,
+                                    uint64_t count, uint64_t in_stride, uint8_t *out, uint64_t out_stride,
                                     uint64_t *out_len, uint8_t *hashes, chip_encode_info *info,
-                                    uint32_t nslots, uint64_t slice_bytes);
+                                    uint32_t nslots, uint64_t slice_bytes, uint32_t host_threads);
 
 #ifdef __cplusplus
 }

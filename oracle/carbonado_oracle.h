@@ -47,6 +47,8 @@ enum {
     ORC_ERR_ZFEC = 7,
     ORC_ERR_INVALID_VERIFIABLE_SLICE_COUNT = 10,
     ORC_ERR_UNSUPPORTED_FORMAT = 11,
+    ORC_ERR_SNAP = 16,
+    ORC_ERR_ECIES = 17,
 };
 
 /* GF(2^8) */
@@ -119,6 +121,22 @@ int orc_decode(const uint8_t *hash, uint64_t hash_len, const uint8_t *in, uint64
  * key = seed ^ (obj * 0xD1B54A32D192ED03); word w = mix64(key + (w+1) * 0x9E3779B97F4A7C15)
  * (mix64 = SplitMix64 finaliser); byte i = byte (i & 7) of word (i >> 3), little-endian. */
 void orc_fill_object(uint64_t seed, uint64_t obj, uint8_t *out, uint64_t n);
+
+/* host_oracle.c: host stages (snappy framing, ECIES) and the full pipeline */
+uint32_t orc_crc32c(const uint8_t *p, uint64_t n);
+uint64_t orc_snap_max_len(uint64_t n);
+int orc_snap_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+int orc_snap_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+void orc_sha256(const uint8_t *in, uint64_t n, uint8_t out[32]);
+void orc_hmac_sha256(const uint8_t *key, uint64_t kl, const uint8_t *msg, uint64_t n, uint8_t out[32]);
+int orc_ecies_public_key(const uint8_t sk[32], uint8_t out[65]);
+int orc_ecies_encrypt(const uint8_t *pub, uint64_t pklen, const uint8_t eph_sk[32], const uint8_t nonce[16],
+                      const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+int orc_ecies_decrypt(const uint8_t sk[32], const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap,
+                      uint64_t *out_len);
+int orc_encode_full(uint8_t format, const uint8_t *pub, uint64_t pklen, const uint8_t eph_sk[32],
+                    const uint8_t nonce[16], const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap,
+                    uint64_t *out_len, uint8_t hash[32], orc_encode_info *info);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,18 @@ def lib() -> ctypes.CDLL:
         l.orc_decode.argtypes = [vp, u64, vp, u64, u32, ctypes.c_uint8, vp, u64, ctypes.POINTER(u64)]
         l.orc_fill_object.argtypes = [u64, u64, vp, u64]
         l.orc_calc_padding_len.argtypes = [u64, ctypes.c_uint, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+        l.orc_crc32c.argtypes = [vp, u64]
+        l.orc_crc32c.restype = u32
+        l.orc_snap_max_len.argtypes = [u64]
+        l.orc_snap_max_len.restype = u64
+        l.orc_snap_compress.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64)]
+        l.orc_snap_decompress.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64)]
+        l.orc_sha256.argtypes = [vp, u64, vp]
+        l.orc_hmac_sha256.argtypes = [vp, u64, vp, u64, vp]
+        l.orc_ecies_public_key.argtypes = [vp, vp]
+        l.orc_ecies_encrypt.argtypes = [vp, u64, vp, vp, vp, u64, vp, u64, ctypes.POINTER(u64)]
+        l.orc_ecies_decrypt.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64)]
+        l.orc_encode_full.argtypes = [ctypes.c_uint8, vp, u64, vp, vp, vp, u64, vp, u64, ctypes.POINTER(u64), vp, vp]
         _L = l
     return _L
 
@@ -170,3 +182,84 @@ def fill_object(seed: int, obj: int, n: int) -> np.ndarray:
     out = np.empty(n, np.uint8)
     lib().orc_fill_object(seed, obj, _p(out), n)
     return out
+
+
+def encode_full(data, fmt: int, pubkey: bytes | None = None, eph_sk: bytes | None = None,
+                nonce: bytes | None = None) -> tuple[bytes, bytes, dict]:
+    """encoding.rs:86-172 with every format bit: the host stages restated in
+    host_oracle (snap, ecies with injected randomness), then this module's C
+    restatement of zfec -> bao.  EncodeInfo factors in f32 as encoding.rs:149-151."""
+    from . import host_oracle as H
+    data = bytes(_u8(data))
+    cur, bc, be = H.host_encode(data, fmt, pubkey, eph_sk, nonce)
+    enc, h, info = encode(cur, fmt & 12)
+    n = np.float32(len(data))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        info["compression_factor"] = float(np.float32(bc) / n)
+        info["amplification_factor"] = float(np.float32(info["bytes_verifiable"]) / n)
+    info.update(input_len=len(data), bytes_compressed=bc, bytes_encrypted=be)
+    return enc, h, info
+
+
+def decode_full(secret: bytes | None, hash: bytes, data, padding: int, fmt: int) -> bytes:
+    """decoding.rs:80-114: bao -> zfec (C restatement), then ecies -> snap."""
+    from . import host_oracle as H
+    cur = decode(hash, data, padding, fmt & 12) if fmt & 12 else bytes(_u8(data))
+    return H.host_decode(cur, fmt, secret)
+
+
+# ---- C restatement of the host stages (host_oracle.c): full-size checker ----
+def c_snap_compress(data) -> bytes:
+    a = _u8(data)
+    cap = lib().orc_snap_max_len(a.size) + 1
+    out = np.empty(cap, np.uint8)
+    olen = ctypes.c_uint64()
+    _chk(lib().orc_snap_compress(_p(a), a.size, _p(out), cap, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def c_snap_decompress(data, cap: int) -> bytes:
+    a = _u8(data)
+    out = np.empty(max(cap, 1), np.uint8)
+    olen = ctypes.c_uint64()
+    _chk(lib().orc_snap_decompress(_p(a), a.size, _p(out), cap, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def c_ecies_encrypt(pub: bytes, data, eph_sk: bytes, nonce: bytes) -> bytes:
+    a, pk = _u8(data), _u8(pub)
+    e, nn = _u8(eph_sk), _u8(nonce)
+    out = np.empty(a.size + 97, np.uint8)
+    olen = ctypes.c_uint64()
+    _chk(lib().orc_ecies_encrypt(_p(pk), pk.size, _p(e), _p(nn), _p(a), a.size, _p(out), out.size, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def c_ecies_decrypt(sk: bytes, data) -> bytes:
+    a, k = _u8(data), _u8(sk)
+    out = np.empty(max(a.size - 97, 1), np.uint8)
+    olen = ctypes.c_uint64()
+    _chk(lib().orc_ecies_decrypt(_p(k), _p(a), a.size, _p(out), out.size, ctypes.byref(olen)))
+    return out[: olen.value].tobytes()
+
+
+def c_public_key(sk: bytes) -> bytes:
+    k = _u8(sk)
+    out = np.empty(65, np.uint8)
+    _chk(lib().orc_ecies_public_key(_p(k), _p(out)))
+    return out.tobytes()
+
+
+def c_encode_full(data, fmt: int, pubkey: bytes = b"", eph_sk: bytes = bytes(32), nonce: bytes = bytes(16)):
+    """encoding.rs:86-172 for every format bit, all in C (snap, ecies with the
+    injected ephemeral key and nonce, zfec, bao)."""
+    a, pk = _u8(data), _u8(pubkey)
+    e, nn = _u8(eph_sk), _u8(nonce)
+    cap = lib().orc_encode_max_len(lib().orc_snap_max_len(a.size) + 97 + a.size) + 1
+    out = np.empty(cap, np.uint8)
+    h = np.empty(32, np.uint8)
+    olen = ctypes.c_uint64()
+    info = EncodeInfoC()
+    _chk(lib().orc_encode_full(fmt, _p(pk), pk.size, _p(e), _p(nn), _p(a), a.size, _p(out), cap, ctypes.byref(olen),
+                               _p(h), ctypes.byref(info)))
+    return out[: olen.value].tobytes(), h.tobytes(), {f: getattr(info, f) for f, _ in info._fields_}

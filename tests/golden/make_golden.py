@@ -3,6 +3,8 @@
 What is pinned where (see DESIGN.md "Oracle and parity"):
   * blake3_kat.json — published BLAKE3 vectors (hand-entered, not generated):
     pins the BLAKE3 restatement.
+  * host_kat.json — published SHA-256 / HMAC / HKDF / AES-256 / GCM /
+    CRC-32C / secp256k1 vectors (hand-entered): pins host_oracle.py.
   * golden.json (this script) — zfec encoding matrices and the level-4/8/12
     encodings of the reference's own sample files (tests/samples of the
     reference, copied under samples/): sizes, EncodeInfo, bao hash and the
@@ -23,10 +25,17 @@ ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 
 from oracle import oracle as O  # noqa: E402
+from oracle import host_oracle as H  # noqa: E402
 from oracle import pyoracle as P  # noqa: E402
 
 HERE = Path(__file__).resolve().parent
 SAMPLES = ["contract.rgbc", "content.png", "code.tar"]
+# Fixed ECIES material for the host-stage levels: the receiver's secret key and
+# the two values ecies::encrypt would draw from thread_rng (injected).
+GOLDEN_SK = H.sha256(b"carbonado-amd golden receiver key")
+GOLDEN_EPH = H.sha256(b"carbonado-amd golden ephemeral key")
+GOLDEN_NONCE = H.sha256(b"carbonado-amd golden nonce")[:16]
+HOST_LEVELS = (1, 2, 3, 14, 15)
 
 
 def main() -> None:
@@ -61,8 +70,20 @@ def main() -> None:
                 "output_blake3": O.blake3(enc).hex(),
                 "info": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in info.items()},
             }
+        pub = H.public_key(GOLDEN_SK)
+        for level in HOST_LEVELS:
+            enc, h, info = O.encode_full(data, level, pub, GOLDEN_EPH, GOLDEN_NONCE)
+            assert O.decode_full(GOLDEN_SK, h, enc, info["padding_len"], level) == data
+            entry[f"level{level}"] = {
+                "hash": h.hex(),
+                "output_len": len(enc),
+                "output_blake3": O.blake3(enc).hex(),
+                "info": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in info.items()},
+            }
         samples[name] = entry
     out["samples"] = samples
+    out["ecies_material"] = {"secret_key": GOLDEN_SK.hex(), "ephemeral_sk": GOLDEN_EPH.hex(),
+                             "nonce": GOLDEN_NONCE.hex(), "public_key": H.public_key(GOLDEN_SK).hex()}
     # small deterministic zfec/bao vectors (inputs from the shared generator)
     vec = []
     for n, seed in [(1, 1), (1000, 2), (4096, 3), (5000, 4), (12289, 5)]:

@@ -41,7 +41,7 @@ def test_library_loads_and_binds_every_symbol():
     L = _lib.lib()
     for name in header_symbols():
         assert getattr(L, name) is not None
-    assert L.chip_abi_version() == 1
+    assert L.chip_abi_version() == 2
     assert L.chip_strerror(3).decode().startswith("Input bytes must divide evenly")
 
 
@@ -88,8 +88,14 @@ def test_argument_errors_before_device():
     """Reference error variants that are decided before any compute."""
     import carbonado_amd
     from carbonado_amd import error as E
-    with pytest.raises(E.UnsupportedFormat):
-        carbonado_amd.encode(b"", b"x", 15)  # ecies/snappy are host stages (out of scope)
+    with pytest.raises(E.InvalidArgument):
+        carbonado_amd.encode(b"", b"x", 15)  # the Ecies bit needs a receiver key
+    with pytest.raises(E.EciesError):
+        carbonado_amd.encoding.ecies(b"\x04" + b"\0" * 64, b"x")  # not a curve point
+    with pytest.raises(E.EciesError):
+        carbonado_amd.decoding.ecies(b"\0" * 96, b"\1" * 32)  # shorter than the 97-byte envelope
+    with pytest.raises(E.SnapError):
+        carbonado_amd.decoding.snap(b"\x01\x05\x00\x00abcde")  # no stream identifier
     with pytest.raises(E.HashDecodeError):
         carbonado_amd.decoding.bao(b"\0" * 8, b"\0" * 31)  # utils.rs:38-45
     with pytest.raises(E.UnevenZfecChunks):

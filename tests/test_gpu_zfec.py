@@ -137,3 +137,46 @@ def test_full_size_16mib_objects(gpu):
         device.zfec_decode_batch(out, C, keep, dec)
         torch.cuda.synchronize()
         assert torch.equal(dec, inp)
+
+
+@pytest.mark.parametrize("n", [1, 15, 17, 4093, 1_000_003])
+def test_batch_bytes_past_n_read_as_zero(gpu, n):
+    """Bytes of an input row beyond n must count as zero padding
+    (encoding.rs:53-55) even when the row holds garbage there: K1's tail load
+    masks the partially valid 16-B block."""
+    import torch
+    from carbonado_amd import device
+    count = 3
+    stride = (n + 15) // 16 * 16 + 32
+    host = np.stack([np.frombuffer(rnd(n, 700 + o), np.uint8) for o in range(count)])
+    inp = torch.full((count, stride), 0xA5, dtype=torch.uint8, device="cuda")
+    inp[:, :n] = torch.from_numpy(host).cuda()
+    pad, C = O.calc_padding_len(n)
+    out = torch.empty((count, 8 * C), dtype=torch.uint8, device="cuda")
+    device.zfec_encode_batch(inp, n, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for o in range(count):
+        assert got[o].tobytes() == O.zfec_encode(host[o].tobytes())[0], o
+
+
+def test_batch_misaligned_pointer_rejected(gpu):
+    import ctypes
+    import torch
+    from carbonado_amd import _lib
+    from carbonado_amd.error import InvalidArgument
+    from carbonado_amd._buf import check
+    n = 4096
+    inp = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")
+    out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+    lib = _lib.lib()
+    p_in, p_out = inp.data_ptr(), out.data_ptr()
+    assert p_in % 16 == 0 and p_out % 16 == 0
+    for a, b in ((p_in + 1, p_out), (p_in, p_out + 8)):
+        with pytest.raises(InvalidArgument):
+            check(lib.chip_zfec_encode_batch_dev(4, 8, ctypes.c_void_p(a), n + 16, n, 1, ctypes.c_void_p(b),
+                                                 2 * n, None))
+    idx = (ctypes.c_uint32 * 4)(4, 5, 6, 7)
+    with pytest.raises(InvalidArgument):
+        check(lib.chip_zfec_decode_batch_dev(4, 8, ctypes.c_void_p(p_out + 4), 2 * n, n // 4, idx, 4, 1,
+                                             ctypes.c_void_p(p_in), n, None))

@@ -1,0 +1,226 @@
+"""Host stages of encode()/decode(): snappy framing and ECIES.
+
+CPU-only: these stages run on host threads by design (host_stages.cpp; the
+reference's encoding.rs:16-36 and decoding.rs:62-77), so the library's
+entry points are exercised here without a device, against
+  * published known answers (tests/golden/host_kat.json) for the restated
+    primitives in oracle/host_oracle.py (SHA-256, HMAC, HKDF, AES-256, GCM,
+    CRC-32C, secp256k1), and
+  * the oracle itself for the composed stages (byte-exact snap frames and
+    ECIES envelopes with injected ephemeral key and nonce), and
+  * golden.json's level 1/2/3/14/15 vectors of the reference's sample files.
+Parity vs the snap / ecies crates themselves is unpinned (neither builds
+here); see DESIGN.md.
+"""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import host_oracle as H
+from oracle import oracle as O
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+@pytest.fixture(scope="module")
+def kat():
+    return json.loads((GOLDEN / "host_kat.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return json.loads((GOLDEN / "golden.json").read_text())
+
+
+def _x(h):
+    return bytes.fromhex(h)
+
+
+# ---------------------------------------------------------------- oracle KATs
+def test_sha256_hmac_hkdf_kat(kat):
+    for v in kat["sha256"]:
+        assert H.sha256(_x(v["msg_hex"])).hex() == v["digest"]
+    t = kat["hmac_sha256_rfc4231_tc1"]
+    assert H.hmac_sha256(_x(t["key_hex"]), _x(t["data_hex"])).hex() == t["mac"]
+    for v in kat["hkdf_sha256_rfc5869"]:
+        salt = _x(v["salt_hex"]) or None
+        assert H.hkdf_sha256(_x(v["ikm_hex"]), salt, _x(v["info_hex"]), v["L"]).hex() == v["okm"]
+
+
+def test_aes_gcm_kat(kat):
+    a = kat["aes256_fips197_c3"]
+    assert H.aes256_block(H.aes256_expand(_x(a["key_hex"])), _x(a["pt_hex"])).hex() == a["ct"]
+    for v in kat["aes256_gcm"]:
+        ct, tag = H.aes256_gcm_encrypt(_x(v["key_hex"]), _x(v["iv_hex"]), _x(v["pt_hex"]))
+        assert ct.hex() == v["ct"] and tag.hex() == v["tag"]
+        assert H.aes256_gcm_decrypt(_x(v["key_hex"]), _x(v["iv_hex"]), ct, tag) == _x(v["pt_hex"])
+
+
+def test_crc32c_and_secp256k1_kat(kat):
+    assert H.crc32c(kat["crc32c_check"]["msg"].encode()) == int(kat["crc32c_check"]["crc"], 16)
+    g = tuple(int(c, 16) for c in kat["secp256k1"]["G"])
+    assert H.point_mul(1) == g and H.on_curve(g)
+    assert H.point_mul(2) == tuple(int(c, 16) for c in kat["secp256k1"]["2G"])
+    assert H.point_mul(H.N) is None  # the generator has order n
+
+
+def test_oracle_sha256_matches_hashlib():
+    import hashlib
+    rng = np.random.default_rng(3)
+    for n in [0, 1, 55, 56, 63, 64, 65, 127, 1000, 4097]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert H.sha256(d) == hashlib.sha256(d).digest()
+
+
+def test_oracle_snappy_roundtrip_and_framing(kat):
+    rng = np.random.default_rng(4)
+    assert H.snap_compress(b"") == _x(kat["snappy_framing"]["empty_input_frame"])
+    for d in [b"a", bytes(100), b"abc" * 30000, rng.integers(0, 256, 70000, dtype=np.uint8).tobytes(),
+              rng.integers(0, 3, 140000, dtype=np.uint8).tobytes()]:
+        f = H.snap_compress(d)
+        assert f.startswith(_x(kat["snappy_framing"]["stream_identifier"]))
+        assert H.snap_decompress(f) == d
+    # incompressible blocks are stored raw: 10 + n + 8 per 64 KiB block
+    r = rng.integers(0, 256, 3 * 65536 + 5, dtype=np.uint8).tobytes()
+    assert len(H.snap_compress(r)) == 10 + len(r) + 8 * 4
+
+
+def test_oracle_golden_host_levels(golden):
+    m = golden["ecies_material"]
+    sk, eph, nonce = _x(m["secret_key"]), _x(m["ephemeral_sk"]), _x(m["nonce"])
+    assert H.public_key(sk).hex() == m["public_key"]
+    for name in ["contract.rgbc", "code.tar"]:
+        data = (GOLDEN / "samples" / name).read_bytes()
+        for level in (1, 2, 3, 14, 15):
+            g = golden["samples"][name][f"level{level}"]
+            enc, h, info = O.encode_full(data, level, _x(m["public_key"]), eph, nonce)
+            assert h.hex() == g["hash"] and len(enc) == g["output_len"]
+            assert O.blake3(enc).hex() == g["output_blake3"], (name, level)
+            assert O.decode_full(sk, h, enc, info["padding_len"], level) == data
+
+
+# ---------------------------------------------------------------- product (host code)
+@pytest.fixture(scope="module")
+def ca():
+    import carbonado_amd
+    return carbonado_amd
+
+
+SAMPLES = ["contract.rgbc", "code.tar", "content.png"]
+
+
+def _inputs():
+    rng = np.random.default_rng(9)
+    out = [(GOLDEN / "samples" / s).read_bytes() for s in SAMPLES]
+    out += [b"", b"x", bytes(17), b"hello world " * 20000, rng.integers(0, 256, 200_003, dtype=np.uint8).tobytes(),
+            rng.integers(0, 4, 150_000, dtype=np.uint8).tobytes(), bytes(rng.integers(97, 100, 65536 * 2 + 7))]
+    return out
+
+
+@pytest.mark.parametrize("i", range(10))
+def test_snap_compress_matches_oracle(ca, i):
+    d = _inputs()[i]
+    f = ca.encoding.snap(d)
+    assert f == H.snap_compress(d)
+    assert ca.decoding.snap(f) == d
+
+
+def test_snap_decompress_rejects_corruption(ca):
+    from carbonado_amd.error import SnapError
+    f = bytearray(ca.encoding.snap(b"hello world " * 1000))
+    bad = bytearray(f)
+    bad[-1] ^= 1  # compressed body / checksum mismatch
+    with pytest.raises(SnapError):
+        ca.decoding.snap(bytes(bad))
+    with pytest.raises(SnapError):
+        ca.decoding.snap(bytes(f[:-3]))  # truncated chunk
+    with pytest.raises(SnapError):
+        ca.decoding.snap(b"\x02\x01\x00\x00x" + bytes(f))  # reserved unskippable chunk first
+    # skippable padding chunk after the identifier is ignored
+    assert ca.decoding.snap(bytes(f[:10]) + b"\xfe\x02\x00\x00\0\0" + bytes(f[10:])) == b"hello world " * 1000
+
+
+@pytest.mark.parametrize("keyform", ["uncompressed", "compressed", "raw64"])
+def test_ecies_matches_oracle(ca, keyform):
+    sk = H.sha256(b"test receiver")
+    pub = H.public_key(sk)
+    assert ca.encoding.public_key(sk) == pub
+    if keyform == "compressed":
+        pk = (b"\x02" if H.parse_pubkey(pub)[1] % 2 == 0 else b"\x03") + pub[1:33]
+    elif keyform == "raw64":
+        pk = pub[1:]
+    else:
+        pk = pub
+    eph, nonce = H.sha256(b"eph"), H.sha256(b"nonce")[:16]
+    for d in [b"", b"a", bytes(1000), np.random.default_rng(2).integers(0, 256, 4099, dtype=np.uint8).tobytes()]:
+        e = ca.encoding.ecies(pk, d, ephemeral_sk=eph, nonce=nonce)
+        assert e == H.ecies_encrypt(pk, d, eph, nonce)
+        assert ca.decoding.ecies(e, sk) == d
+        assert H.ecies_decrypt(sk, e) == d
+
+
+def test_ecies_random_envelopes_decrypt(ca):
+    """Without injection every call draws a fresh ephemeral key and nonce."""
+    sk = H.sha256(b"rng receiver")
+    pub = ca.encoding.public_key(sk)
+    a, b = ca.encoding.ecies(pub, b"same message"), ca.encoding.ecies(pub, b"same message")
+    assert a != b and a[:65] != b[:65] and a[65:81] != b[65:81]
+    assert H.ecies_decrypt(sk, a) == b"same message" == ca.decoding.ecies(b, sk)
+
+
+def test_ecies_errors(ca):
+    from carbonado_amd.error import EciesError
+    sk = H.sha256(b"err receiver")
+    e = ca.encoding.ecies(ca.encoding.public_key(sk), b"payload" * 10)
+    for pos in (0 + 40, 70, 90, 100, len(e) - 1):  # eph key, nonce, tag, ciphertext
+        bad = bytearray(e)
+        bad[pos] ^= 0x40
+        with pytest.raises(EciesError):
+            ca.decoding.ecies(bytes(bad), sk)
+    with pytest.raises(EciesError):
+        ca.decoding.ecies(e, H.sha256(b"someone else"))
+    with pytest.raises(EciesError):
+        ca.decoding.ecies(e, bytes(32))  # zero is not a valid secret key
+    with pytest.raises(EciesError):
+        ca.decoding.ecies(e, bytes.fromhex("FF" * 32))  # >= group order
+    with pytest.raises(EciesError):
+        ca.encoding.ecies(b"\x02" + bytes(31), b"x")  # wrong length
+
+
+# ---------------------------------------------------------------- C restatement
+def test_c_host_oracle_matches_python_oracle(kat):
+    """oracle/host_oracle.c (the full-size checker and CPU baseline) agrees
+    with the Python restatement and the published vectors."""
+    import ctypes
+    L = O.lib()
+    assert L.orc_crc32c(b"123456789", 9) == int(kat["crc32c_check"]["crc"], 16)
+    out = ctypes.create_string_buffer(32)
+    for v in kat["sha256"]:
+        m = _x(v["msg_hex"])
+        L.orc_sha256(m, len(m), out)
+        assert out.raw.hex() == v["digest"]
+    t = kat["hmac_sha256_rfc4231_tc1"]
+    L.orc_hmac_sha256(_x(t["key_hex"]), 20, _x(t["data_hex"]), 8, out)
+    assert out.raw.hex() == t["mac"]
+    sk = H.sha256(b"c oracle")
+    pub = H.public_key(sk)
+    assert O.c_public_key(sk) == pub
+    rng = np.random.default_rng(8)
+    for d in [b"", b"q", b"carbonado " * 9000, rng.integers(0, 256, 70_001, dtype=np.uint8).tobytes()]:
+        f = O.c_snap_compress(d)
+        assert f == H.snap_compress(d) and O.c_snap_decompress(f, len(d) + 1) == d
+        e = O.c_ecies_encrypt(pub, d[:3000], H.sha256(b"e"), bytes(range(16)))
+        assert e == H.ecies_encrypt(pub, d[:3000], H.sha256(b"e"), bytes(range(16)))
+        assert O.c_ecies_decrypt(sk, e) == d[:3000]
+
+
+def test_c_full_pipeline_golden(golden):
+    m = golden["ecies_material"]
+    for name in SAMPLES:
+        data = (GOLDEN / "samples" / name).read_bytes()
+        for level in (1, 2, 3, 14, 15):
+            enc, h, _ = O.c_encode_full(data, level, _x(m["public_key"]), _x(m["ephemeral_sk"]), _x(m["nonce"]))
+            g = golden["samples"][name][f"level{level}"]
+            assert O.blake3(enc).hex() == g["output_blake3"] and h.hex() == g["hash"], (name, level)

@@ -49,12 +49,12 @@ struct V {
     bool stream;
 };
 
-template <int MODE, int CPL, bool NTS>
+template <int MODE, int CPL, bool NTS, int SP = 0>
 V mk(bool stream) {
     char b[64];
-    snprintf(b, sizeof b, "%s CPL%d %s %s", MODE ? "decode" : "encode", CPL, NTS ? "nt " : "pln",
-             stream ? "stream" : "hash-only");
-    return V{b, run_bao_t<MODE, CPL, NTS>, CPL, stream};
+    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d", MODE ? "decode" : "encode", CPL, NTS ? "nt " : "pln",
+             stream ? "stream" : "hash-only", SP);
+    return V{b, run_bao_t<MODE, CPL, NTS, SP>, CPL, stream};
 }
 
 int main(int argc, char **argv) {
@@ -72,10 +72,9 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&status, count * 4));
     CK(hipMalloc(&scratch, bao_scratch_len_t<1>(n, count)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xB1A3ull);
-    std::vector<V> vs = {mk<0, 1, false>(true), mk<0, 2, false>(true), mk<0, 4, false>(true),
-                         mk<0, 8, false>(true), mk<0, 8, true>(true),  mk<0, 4, true>(true),
-                         mk<0, 8, false>(false), mk<0, 1, false>(false), mk<1, 8, false>(true),
-                         mk<1, 4, false>(true), mk<1, 1, false>(true)};
+    std::vector<V> vs = {mk<0, 8, false>(true),    mk<0, 8, false, 1>(true), mk<0, 8, true, 1>(true),
+                         mk<0, 8, false, 2>(true), mk<0, 4, false, 1>(true), mk<0, 8, false>(false),
+                         mk<1, 8, false>(true),    mk<0, 1, false>(true)};
     if (argc > 4) {  // comma-separated subset of variant indices (profiling)
         std::vector<V> keep;
         std::string sel = argv[4];
