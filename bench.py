@@ -50,6 +50,8 @@ def parse():
                     help="e2e: encode() at --level from pinned HOST memory to host memory (H2D+kernels+D2H)")
     ap.add_argument("--level", type=int, default=12, help="e2e mode: Format bits (Bao|Zfec = 12)")
     ap.add_argument("--slots", type=int, default=3, help="e2e mode: pipeline slots (streams)")
+    ap.add_argument("--host-threads", type=int, default=16,
+                    help="e2e mode: host threads for the Snappy/Ecies stages (the GPU box's CPU share is 16)")
     ap.add_argument("--erase", default="1,2", help="decode mode: shards dropped")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -112,6 +114,12 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
     from oracle import oracle as O
     import numpy as np
     obj = np.frombuffer(sample_obj, np.uint8) if sample_obj is not None else O.fill_object(SEED, 0, n)
+    if args.mode == "e2e" and args.level & 1:
+        import hashlib
+        eph = hashlib.sha256(b"cpu baseline eph").digest()
+        pub = O.c_public_key(hashlib.sha256(b"carbonado-amd bench receiver").digest())
+    else:
+        eph = pub = b""
     if args.mode == "decode":
         z, pad, C = O.zfec_encode(obj, args.k, args.m)
         keep = [i for i in range(args.m) if str(i) not in args.erase.split(",")]
@@ -122,7 +130,10 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
         if args.mode == "bao":
             O.bao_encode(obj)
         elif args.mode == "e2e":
-            O.encode(obj, args.level)
+            if args.level & 3:  # host stages too: the all-C restatement (oracle/host_oracle.c)
+                O.c_encode_full(obj, args.level, pub, eph, bytes(16))
+            else:
+                O.encode(obj, args.level)
         elif args.mode == "decode":
             O.zfec_decode_shares(shares, keep, pad, args.k, args.m)
         else:
@@ -135,8 +146,9 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
             "decode": f"zfec {args.k}-of-{args.m} decode, erased {args.erase}"}.get(
         args.mode, f"zfec {args.k}-of-{args.m} encode")
     return {"value": round(done * n / el / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{done} x {n} B objects ({what}) through oracle/carbonado_oracle.c, scalar "
-                      f"fec.c-style restatement of the reference crates, 1 thread, {el:.1f} s"}
+            "sample": f"{done} x {n} B objects ({what}) through oracle/carbonado_oracle.c"
+                      f"{' + host_oracle.c' if args.mode == 'e2e' and args.level & 3 else ''}, scalar "
+                      f"restatement of the reference crates, 1 thread, {el:.1f} s"}
 
 
 class Workload:
@@ -191,13 +203,32 @@ class Workload:
             self.h_hash = torch.empty((count, 32), dtype=torch.uint8, pin_memory=True)
             self.final_len = cap
             lv, slots = args.level, args.slots
+            # ECIES (level & 1): a fixed receiver key; the ephemeral key and
+            # nonce of every object are injected so object 0 can be checked
+            # bit for bit against the C oracle.
+            self.pub = b""
+            self.eph = self.nonce = None
+            if lv & 1:
+                import hashlib
+                import numpy as np
+                from carbonado_amd.encoding import public_key
+                self.pub = public_key(hashlib.sha256(b"carbonado-amd bench receiver").digest())
+                self.eph = np.stack([np.frombuffer(hashlib.sha256(b"eph%d" % o).digest(), np.uint8)
+                                     for o in range(count)])
+                self.nonce = np.stack([np.frombuffer(hashlib.sha256(b"nonce%d" % o).digest()[:16], np.uint8)
+                                       for o in range(count)])
 
             def step():
-                self.final_len, _ = device.encode_host_batch(lv, self.h_in, n, self.h_out, self.h_hash, slots)
+                olens, _ = device.encode_host_batch(lv, self.h_in, n, self.h_out, self.h_hash, slots,
+                                                    pubkey=self.pub, ephemeral_sk=self.eph, nonce=self.nonce,
+                                                    host_threads=args.host_threads)
+                self.final_len = max(olens)
             self.step = step
             step()
             self.alg_bytes = count * (n + self.final_len)  # PCIe bytes: H2D input + D2H encoding
-            self.kernel = f"encode() level {lv}: H2D + gf_apply + bao kernels + D2H, {slots} slots"
+            stages = ("snap + " if lv & 2 else "") + ("ecies + " if lv & 1 else "")
+            host = f"host {stages[:-3]} on {args.host_threads} threads + " if stages else ""
+            self.kernel = f"encode() level {lv}: {host}H2D + gf_apply + bao kernels + D2H, {slots} slots"
             self.kernel_sym = "e2e"
         else:
             blen = L.chip_bao_encoded_len(n)
@@ -252,8 +283,14 @@ class Workload:
         if self.args.mode == "encode":
             ok = self.out[0].cpu().numpy().tobytes() == O.zfec_encode(sample, self.k, self.m)[0]
         elif self.args.mode == "e2e":
-            enc, h, _ = O.encode(sample, self.args.level)
-            ok = (self.h_out[0, :self.final_len].numpy().tobytes() == enc and
+            lv = self.args.level
+            if lv & 3:
+                eph = self.eph[0].tobytes() if self.eph is not None else bytes(32)
+                nonce = self.nonce[0].tobytes() if self.nonce is not None else bytes(16)
+                enc, h, _ = O.c_encode_full(sample, lv, self.pub, eph, nonce)
+            else:
+                enc, h, _ = O.encode(sample, lv)
+            ok = (self.h_out[0, :len(enc)].numpy().tobytes() == enc and
                   self.h_hash[0].numpy().tobytes() == h)
         elif self.args.mode == "decode":
             ok = self.out[0, :self.n].cpu().numpy().tobytes() == sample
