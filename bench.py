@@ -32,6 +32,7 @@ sys.path.insert(0, str(ROOT))
 
 from carbonado_amd.sharding import max_over_ranks, object_range  # noqa: E402
 
+VALU_PEAK_TOPS = 39.3  # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz, one int32 op per lane-cycle
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "GiB/s device-resident zfec 4-of-8 encode, 16 MiB objects; % HBM roofline"
 SEED = 0xCA4B0AD0
@@ -56,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-aliased", action="store_true",
+                    help="encode mode: skip the second, in-place (aliased data shards) measurement")
     ap.add_argument("--scatter", action="store_true",
                     help="N>1: rank 0 generates every object and scatters them over RCCL/xGMI (timed "
                          "separately, outside `value`)")
@@ -259,9 +262,10 @@ class Workload:
         torch.cuda.empty_cache()
         return el
 
-    def time_steps(self, steps: int, warmup: int, world: int):
+    def time_steps(self, steps: int, warmup: int, world: int, step=None):
+        step = step or self.step
         for _ in range(warmup):
-            self.step()
+            step()
         torch.cuda.synchronize()
         stream = torch.cuda.current_stream()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -270,12 +274,25 @@ class Workload:
         t0 = time.perf_counter()
         for i in range(steps):
             evs[i][0].record(stream)  # the library launches on torch's current stream
-            self.step()
+            step()
             evs[i][1].record(stream)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         barrier(world)
         return t1 - t0, [a.elapsed_time(b) for a, b in evs]
+
+    def time_aliased(self, steps: int, warmup: int, world: int):
+        """the same encode with the data shards aliased (in
+        place: the input already sits in the first n bytes of each output
+        slot, only parity is written).  Reported next to, not instead of, the
+        48 MiB/object figure."""
+        from carbonado_amd import device
+        n, k, m = self.n, self.k, self.m
+        self.out[:, :n].copy_(self.inp)
+        el, ms = self.time_steps(steps, warmup, world, lambda: device.zfec_encode_batch(self.out, n, self.out, k, m))
+        from oracle import oracle as O
+        ok = self.out[0].cpu().numpy().tobytes() == O.zfec_encode(self.inp[0].cpu().numpy().tobytes(), k, m)[0]
+        return el, ms, ok
 
     def verify_object0(self):
         from oracle import oracle as O
@@ -330,6 +347,10 @@ def main():
     verified, sample = None, None
     if rank == 0 and not args.no_verify and not args.dry_run:
         verified, sample = wl.verify_object0()
+    aliased = None
+    if args.mode == "encode" and not args.dry_run and not args.no_aliased:
+        a_el, a_ms, a_ok = wl.time_aliased(args.steps, args.warmup, world)
+        aliased = (max_over_ranks(a_el), a_ms, a_ok)
 
     if rank == 0:
         k, m = args.k, args.m
@@ -375,9 +396,33 @@ def main():
                                     "note": "PCIe Gen5 x16, 63 GB/s per direction (spec), H2D and D2H overlapped"})
             res["data"] = "synthetic (uniform random bytes), pinned host buffers"
         if args.mode == "bao":
-            res["roofline"]["bound"] = "valu"
-            res["roofline"]["note"] = ("BLAKE3 is VALU-bound (~11 int ops/byte, ceiling ~6 TB/s hashed); "
-                                       "achieved/peak are HBM figures for reference")
+            # BLAKE3 compressions: one per 64-B block of content plus one per parent node;
+            # 7 rounds x 8 G x 12 VALU lane-ops (a+b+m as one v_add3_u32).
+            chunks = max(1, -(-n // 1024))
+            comps = args.objects * (max(1, -(-n // 64)) + (chunks - 1))
+            ops = comps * 7 * 8 * 12
+            tops = ops / (avg_ms * 1e-3) / 1e12
+            hbm = res["roofline"]
+            res["roofline"] = {"bound": "valu", "achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "TOPS",
+                               "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": hbm["traffic"],
+                               "traffic_source": hbm["traffic_source"], "kernel": wl.kernel,
+                               "alg_ops_per_launch": ops, "hbm_achieved_GBps": hbm["achieved"],
+                               "avg_launch_ms": hbm["avg_launch_ms"], "min_launch_ms": hbm["min_launch_ms"],
+                               "note": "int32 VALU peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; ops = 672 per "
+                                       "BLAKE3 compression (content blocks + parents)"}
+        if aliased is not None:
+            a_max, a_ms, a_ok = aliased
+            a_bytes = args.objects * (n + (m - k) * wl.C)
+            a_avg = sum(a_ms) / len(a_ms)
+            a_ach = a_bytes / (a_avg * 1e-3) / 1e9
+            res["aliased_data_shards"] = {
+                "value": round(world * args.objects * n * args.steps / a_max / 2**30, 2), "unit": "GiB/s",
+                "ms_per_step": round(a_max / args.steps * 1e3, 4), "alg_bytes_per_launch": a_bytes,
+                "achieved": round(a_ach, 1), "peak": HBM_PEAK_GBS, "frac": round(a_ach / HBM_PEAK_GBS, 4),
+                "verified_object0": a_ok,
+                "note": ("SURVEY.md 8d: in-place encode, the input already sits in the output slot and only the "
+                         "parity shards are written (16 MiB read + 16 MiB written per object); `value` above "
+                         "(all 8 shards written, 48 MiB per object) is the graded figure")}
         if wl.scatter_s is not None:
             res["scatter"] = {"seconds": round(wl.scatter_s, 4),
                               "GiB_per_s": round(world * args.objects * n / wl.scatter_s / 2**30, 2),

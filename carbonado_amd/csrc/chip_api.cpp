@@ -169,22 +169,24 @@ void calc_pad(uint64_t n, uint32_t k, uint32_t *pad, uint64_t *C) {
 }
 
 // encode plan: rows 0..k-1 copied, k..m-1 computed from the enc_matrix
-GfPlan encode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint8_t> &enc) {
+// aliased: the data shards already sit in the output (in-place encode), so
+// only the m-k parity rows are produced
+GfPlan encode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint8_t> &enc, bool aliased = false) {
     GfPlan p;
     p.k = k;
     p.np = m - k;
     for (uint32_t j = 0; j < ZF_MAXK; ++j) {
         p.in_off[j] = j < k ? (uint64_t)j * C : 0;
-        p.copy_off[j] = j < k ? (uint64_t)j * C : NO_OUT;
+        p.copy_off[j] = (j < k && !aliased) ? (uint64_t)j * C : NO_OUT;
     }
     p.coef.assign(enc.begin() + (size_t)k * k, enc.end());
     for (uint32_t q = 0; q < p.np; ++q) p.comp_off.push_back((uint64_t)(k + q) * C);
-    // generic description (all m rows as coefficient rows)
+    // generic description (output rows as coefficient rows; copies are unit rows)
     p.g_in_off.resize(k);
     for (uint32_t j = 0; j < k; ++j) p.g_in_off[j] = (uint64_t)j * C;
-    p.g_out_off.resize(m);
-    for (uint32_t r = 0; r < m; ++r) p.g_out_off[r] = (uint64_t)r * C;
-    p.g_coef = enc;
+    const uint32_t r0 = aliased ? k : 0;
+    for (uint32_t r = r0; r < m; ++r) p.g_out_off.push_back((uint64_t)r * C);
+    p.g_coef.assign(enc.begin() + (size_t)r0 * k, enc.end());
     return p;
 }
 
@@ -475,9 +477,16 @@ int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     uint64_t C;
     calc_pad(n, k, &pad, &C);
     if (count > 1 && out_stride < (uint64_t)m * C) return CHIP_ERR_INVALID_ARG;
-    GfPlan p = encode_plan(k, m, C, zfec_enc_matrix(k, m));
+    // in place (SURVEY 8d "aliased"): data shards are the input bytes themselves
+    const bool aliased = d_in == d_out && n;
+    if (aliased && count > 1 && in_stride != out_stride) return CHIP_ERR_INVALID_ARG;
+    GfPlan p = encode_plan(k, m, C, zfec_enc_matrix(k, m), aliased);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (aliased && (uint64_t)k * C > n)  // the zero padding of encoding.rs:53-55 becomes part of shard k-1
+        CHIP_HIP(hipMemset2DAsync(d_out + n, out_stride ? out_stride : (uint64_t)m * C, 0, (uint64_t)k * C - n,
+                                  count, s));
     GfLaunch L{d_in, d_out, in_stride, out_stride, n, C, count};
-    CHIP_HIP(gf_apply(p, L, static_cast<hipStream_t>(stream)));
+    CHIP_HIP(gf_apply(p, L, s));
     return CHIP_OK;
 }
 

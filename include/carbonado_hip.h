@@ -222,7 +222,11 @@ CHIP_API int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8
  * (bytes beyond n inside the padded object read as zero, exactly as
  * encoding.rs:53-55 pads), its m*chunk_len-byte output at d_out + o*out_stride.
  * d_in, d_out, in_stride and out_stride must be multiples of 16
- * (CHIP_ERR_INVALID_ARG otherwise). */
+ * (CHIP_ERR_INVALID_ARG otherwise).
+ * In place: d_out == d_in (and out_stride == in_stride) means each object's
+ * first n bytes already are its data shards; only the m-k parity shards are
+ * written and the padding bytes [n, k*chunk_len) are zeroed (SURVEY.md 8d
+ * "aliased": 32 MiB of traffic per 16 MiB object instead of 48). */
 CHIP_API int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
                                uint64_t n, uint64_t count, uint8_t *d_out, uint64_t out_stride,
                                void *stream);

@@ -180,3 +180,22 @@ def test_batch_misaligned_pointer_rejected(gpu):
     with pytest.raises(InvalidArgument):
         check(lib.chip_zfec_decode_batch_dev(4, 8, ctypes.c_void_p(p_out + 4), 2 * n, n // 4, idx, 4, 1,
                                              ctypes.c_void_p(p_in), n, None))
+
+
+@pytest.mark.parametrize("k,m,n", [(4, 8, 16 << 20), (4, 8, 1_000_003), (8, 16, 100_000), (4, 8, 5)])
+def test_batch_in_place_aliased_data_shards(gpu, k, m, n):
+    """d_out == d_in: the data shards stay where they are, only parity is
+    written and the padding tail is zeroed (SURVEY.md 8d 'aliased')."""
+    import torch
+    from carbonado_amd import device
+    count = 2
+    pad, C = O.calc_padding_len(n, k)
+    buf = torch.full((count, m * C), 0x5A, dtype=torch.uint8, device="cuda")  # garbage everywhere
+    host = [np.frombuffer(rnd(n, 900 + o), np.uint8) for o in range(count)]
+    for o in range(count):
+        buf[o, :n] = torch.from_numpy(host[o]).cuda()
+    device.zfec_encode_batch(buf, n, buf, k, m)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    for o in range(count):
+        assert got[o].tobytes() == O.zfec_encode(host[o].tobytes(), k, m)[0], o
