@@ -265,12 +265,21 @@ __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x
 // next step's loads prefetched into registers while the lane compresses.
 // SP (stream path, MODE 0): 0 = aligned pieces re-read from the LDS rows;
 // 1 = pieces built in registers from the loaded data (DPP neighbour exchange);
-// 2 = diagnostic for tools/bao_tune only (128-B aligned bases, wrong layout).
-template <int MODE, int CPL, bool NTS, int SP = 0>
+// 2 = diagnostic for tools/bao_tune only (128-B aligned bases, wrong layout);
+// 3 = rows hold two steps (ping-pong) and every step stores one whole aligned
+//     128-B line of the stream per chunk (plus the head at step 0 and the
+//     tail at step 7), so no line is written in two halves.
+// SU: unroll of the SP 3 store loop; SE: issue the SP 3 stores before (1) or
+// after (0) the next step's prefetch loads.
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0>
 __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     constexpr int LOG = ilog2(CPL);
     constexpr int NSTEP = 8 * CPL;
-    __shared__ __attribute__((aligned(16))) uint32_t stage[K3_WAVES][64 * ROWW];
+    // SP 3: [pad 4 | step-parity-0 data 32 | step-parity-1 data 32] words per row
+    // (68/4 = 17 is odd, so the lane-per-row ds_read_b128 stays conflict-free)
+    constexpr int RW = SP == 3 ? 68 : ROWW;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[K3_WAVES][64 * RW];
+    auto dofs = [](int step) { return ROW0 + (SP == 3 ? (step & 1) * 32 : 0); };
     __shared__ uint64_t soff[2][K3_WAVES][64];  // stream offset of each lane's current chunk (by parity)
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -352,7 +361,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
             const uint64_t rem = a.n - ci * 1024;
             const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
             uint8_t *base = ob + soff[j & 1][wave][cc];
-            const uint32_t *w = st + cc * ROWW + 2 + 4 * gl;  // carry/previous half, then this piece
+            const uint32_t *w = st + cc * RW + 2 + 4 * gl;  // carry/previous half, then this piece
             const int lo = 16 * (8 * s + gl) - 8;             // chunk byte of the piece's first half
             if (clen == 1024) {
                 if (lo >= 0) {
@@ -419,6 +428,62 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         }
     };
 
+    // encode, SP 3: chunk bytes x live in the row at word dofs(x >> 7) + (x & 127) / 4.
+    // The stream lines (128-B aligned in stream space) inside a chunk start at
+    // chunk byte d + 128 t, d = (-base) mod 128; at step s the line ending at
+    // d + 128 s is complete (its first part is in the other half of the row).
+    auto stream_lines = [&](int g) {
+        const int j = g >> 3, s = g & 7, gl = lane & 7;
+        auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x (8-aligned)
+            return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
+        };
+#pragma unroll SU
+        for (int t = 0; t < 8; ++t) {
+            const int cc = t * 8 + (lane >> 3);
+            const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
+            if (!(wave_on && ci < a.N)) continue;
+            const uint64_t rem = a.n - ci * 1024;
+            const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+            const uint64_t base = soff[j & 1][wave][cc];
+            uint8_t *sp = ob + base;
+            const uint32_t *row = st + cc * RW;
+            if (clen < 1024) {  // short last chunk of the object: this step's bytes, byte stores
+                const uint32_t *w = row + dofs(s) + 4 * gl;
+                for (int q = 0; q < 16; ++q) {
+                    const uint32_t cb = 128u * s + 16u * gl + q;
+                    if (cb < clen) sp[cb] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+                }
+                continue;
+            }
+            const uint32_t d = (uint32_t)((128u - (base & 127u)) & 127u);
+            if (s >= 1) {  // the whole line [d + 128(s-1), d + 128 s)
+                const uint32_t x = d + 128u * (s - 1) + 16u * gl;
+                const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+                if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(sp + x));
+                else *reinterpret_cast<u32x4 *>(sp + x) = v;
+            } else {  // head [0, d): 8 B at 0, then aligned 16-B pieces [16k - 8, 16k + 8)
+                if (gl == 0) store8<NTS>(sp, piece(row, 0));
+                const uint32_t x = 16u * gl + 8;
+                if (x + 16 <= d) {
+                    const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                    const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+                    *reinterpret_cast<u32x4 *>(sp + x) = v;
+                }
+            }
+            if (s == 7) {  // tail [896 + d, 1024): aligned pieces, 8 B at the end
+                const uint32_t x = 896u + d + 16u * gl;
+                if (x + 16 <= 1024) {
+                    const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                    const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+                    *reinterpret_cast<u32x4 *>(sp + x) = v;
+                } else if (x + 8 == 1024) {
+                    store8<NTS>(sp + x, piece(row, x));
+                }
+            }
+        }
+    };
+
     uint32_t h[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) h[w] = IV(w);
@@ -431,21 +496,23 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         const int j = g >> 3, s = g & 7;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            uint32_t *row = st + (t * 8 + (lane >> 3)) * ROWW;
+            uint32_t *row = st + (t * 8 + (lane >> 3)) * RW;
             if (MODE == 0 && SP == 0 && (lane & 7) == 7)  // carry the previous step's last 8 bytes
                 *reinterpret_cast<u32x2 *>(row + 2) = *reinterpret_cast<const u32x2 *>(row + ROW0 + 30);
-            *reinterpret_cast<u32x4 *>(row + ROW0 + (lane & 7) * 4) = pre[t];
+            *reinterpret_cast<u32x4 *>(row + dofs(s) + (lane & 7) * 4) = pre[t];
         }
         if (MODE == 1 && ob) content_step(g, pre);
-        if (MODE == 0 && ob && SP != 0) stream_regs(g, pre);
+        if (MODE == 0 && ob && (SP == 1 || SP == 2)) stream_regs(g, pre);
         if (s == 7 && j + 1 < CPL) {  // stream offset of my next chunk, for the loads issued below
             const uint64_t ni = lb + j + 1;
             if ((uint64_t)(j + 1) < nmine) my_off += 1024 + 64 * (uint64_t)parents_at(ni, a.N);
             soff[(j + 1) & 1][wave][lane] = my_off;
         }
         wave_sync();
+        if (MODE == 0 && ob && SP == 3 && SE) stream_lines(g);
         if (g + 1 < NSTEP) load_step(g + 1, pre);  // in flight during the compressions
         if (MODE == 0 && ob && SP == 0) stream_step(g);
+        if (MODE == 0 && ob && SP == 3 && !SE) stream_lines(g);
 
         const uint64_t i = lb + j;
         const bool mine = (uint64_t)j < nmine;
@@ -455,7 +522,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
             const uint32_t b = (uint32_t)(2 * s + hh);
             if (mine && b < nb) {
                 uint32_t m[16];
-                const u32x4 *row = reinterpret_cast<const u32x4 *>(st + lane * ROWW + ROW0 + hh * 16);
+                const u32x4 *row = reinterpret_cast<const u32x4 *>(st + lane * RW + dofs(s) + hh * 16);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const u32x4 x = row[q];
@@ -655,10 +722,10 @@ inline uint64_t bao_scratch_len_t(uint64_t n, uint64_t count) {
 }
 
 // Enqueue K3 then one K4 launch per remaining level.
-template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0>
+template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0>
 hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
-                   void *d_scratch, hipStream_t stream) {
+                   void *d_scratch, hipStream_t stream, size_t pad_lds = 0 /* tuning: occupancy probe */) {
     if (count == 0) return hipSuccess;
     const uint64_t N = n_chunks(n);
     constexpr int LOG = ilog2(BAO_CPL);
@@ -673,7 +740,7 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
     ca.hash = d_hash; ca.status = d_status;
     const uint64_t waves = count * ((N + 64ull * BAO_CPL - 1) / (64ull * BAO_CPL));
     const uint64_t blocks = (waves + K3_WAVES - 1) / K3_WAVES;
-    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP>), dim3((unsigned)blocks), dim3(K3_TPB), 0,
+    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE>), dim3((unsigned)blocks), dim3(K3_TPB), pad_lds,
                        stream, ca);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

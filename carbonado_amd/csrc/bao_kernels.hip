@@ -21,7 +21,10 @@
 // K3 (bao_chunk_kernel, bao_device.hpp): lane = CPL consecutive chunks, the
 // first log2(CPL) levels folded in registers; chunk bytes staged through LDS
 // once and written straight to their stream slot (encode) or content slot
-// (decode).  BLAKE3 is VALU work (~11 int ops/byte): K3 is VALU-bound.
+// (decode).  BLAKE3 is VALU work (672 lane-ops per 64-B block): hash-only K3
+// is VALU-bound; with the stream written, the store pattern costs ~40 %.
+// Encode keeps two steps per LDS row (SP 3) so every 128-B stream line is
+// stored whole; CPL 2 keeps a wave's 64 write fronts within 128 KiB.
 // K4 (bao_parent_kernel): one launch per remaining level, lane = one node.
 // K5 (verify-decode) = the same kernels in MODE 1: every stored parent node is
 // compared with the recomputed children, the root with the expected hash.
@@ -35,16 +38,19 @@ using namespace bao;
 
 namespace {
 
-// tuned on MI355X (tools/bao_tune.hip)
-constexpr int BAO_CPL = 8;
+// tuned on MI355X (tools/bao_tune.hip): CPL 8 / SP 0 1.38 TiB/s,
+// CPL 4 / SP 3 1.49, CPL 2 / SP 3 1.58 (encode with stream, 256 x 32 MiB);
+// decode CPL 2 1.88 vs CPL 8 1.77.
+constexpr int BAO_CPL = 2;
 constexpr bool BAO_NTS = false;
+constexpr int BAO_SP = 3;
 
 template <int MODE>
 hipError_t run_bao(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
                    void *d_scratch, hipStream_t stream) {
-    return run_bao_t<MODE, BAO_CPL, BAO_NTS>(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_status,
-                                            d_scratch, stream);
+    return run_bao_t<MODE, BAO_CPL, BAO_NTS, MODE == 0 ? BAO_SP : 0>(d_in, in_stride, n, count, d_out, out_stride,
+                                                                    d_hash, d_status, d_scratch, stream);
 }
 
 }  // namespace

@@ -59,7 +59,8 @@ def test_size_helpers_match_oracle(n):
 
 def test_bao_scratch_len():
     L = _lib.lib()
-    assert L.chip_bao_scratch_len(32 << 20, 2) == 2 * 32 * (4096 + 2048)
+    N0 = (32 << 10) // 2  # level-1 nodes (CPL = 2 chunks per lane)
+    assert L.chip_bao_scratch_len(32 << 20, 2) == 2 * 32 * (N0 + N0 // 2)
 
 
 def _has_gfx950() -> bool:

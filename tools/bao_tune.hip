@@ -40,21 +40,22 @@ __global__ void checksum_kernel(const uint64_t *p, size_t n, unsigned long long 
 }
 
 typedef hipError_t (*RunFn)(const uint8_t *, uint64_t, uint64_t, uint64_t, uint8_t *, uint64_t, uint8_t *,
-                            uint32_t *, void *, hipStream_t);
+                            uint32_t *, void *, hipStream_t, size_t);
 
 struct V {
     std::string name;
     RunFn fn;
     int cpl;
     bool stream;
+    size_t pad_lds;
 };
 
-template <int MODE, int CPL, bool NTS, int SP = 0>
-V mk(bool stream) {
-    char b[64];
-    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d", MODE ? "decode" : "encode", CPL, NTS ? "nt " : "pln",
-             stream ? "stream" : "hash-only", SP);
-    return V{b, run_bao_t<MODE, CPL, NTS, SP>, CPL, stream};
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0>
+V mk(bool stream, size_t pad_lds = 0) {
+    char b[96];
+    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d pad%zu", MODE ? "decode" : "encode", CPL,
+             NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, pad_lds);
+    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE>, CPL, stream, pad_lds};
 }
 
 int main(int argc, char **argv) {
@@ -72,9 +73,10 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&status, count * 4));
     CK(hipMalloc(&scratch, bao_scratch_len_t<1>(n, count)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xB1A3ull);
-    std::vector<V> vs = {mk<0, 8, false>(true),    mk<0, 8, false, 1>(true), mk<0, 8, true, 1>(true),
-                         mk<0, 8, false, 2>(true), mk<0, 4, false, 1>(true), mk<0, 8, false>(false),
-                         mk<1, 8, false>(true),    mk<0, 1, false>(true)};
+    std::vector<V> vs = {mk<0, 8, false>(true),       mk<0, 2, false, 3>(true), mk<0, 1, false, 3>(true),
+                         mk<0, 4, false, 3>(true),    mk<0, 2, false>(true),    mk<0, 1, false>(true),
+                         mk<0, 2, false, 3, 2>(true), mk<0, 2, false>(false),   mk<0, 8, false>(false),
+                         mk<1, 8, false>(true),       mk<1, 2, false>(true)};
     if (argc > 4) {  // comma-separated subset of variant indices (profiling)
         std::vector<V> keep;
         std::string sel = argv[4];
@@ -95,7 +97,7 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     // reference encode (CPL1) so decode variants have a stream + hashes to verify
-    CK((run_bao_t<0, 1, false>(in, n, n, count, out, ostride, hash, nullptr, scratch, 0)));
+    CK((run_bao_t<0, 1, false>(in, n, n, count, out, ostride, hash, nullptr, scratch, 0, 0)));
     CK(hipDeviceSynchronize());
     for (int rd = 0; rd < rounds; ++rd)
         for (size_t v = 0; v < vs.size(); ++v) {
@@ -103,9 +105,10 @@ int main(int argc, char **argv) {
             auto launch = [&] {
                 if (dec_mode) {
                     CK(hipMemsetAsync(status, 0, count * 4, 0));
-                    CK(vs[v].fn(out, ostride, n, count, dec, n, hash, status, scratch, 0));
+                    CK(vs[v].fn(out, ostride, n, count, dec, n, hash, status, scratch, 0, vs[v].pad_lds));
                 } else {
-                    CK(vs[v].fn(in, n, n, count, vs[v].stream ? out : nullptr, ostride, hash, nullptr, scratch, 0));
+                    CK(vs[v].fn(in, n, n, count, vs[v].stream ? out : nullptr, ostride, hash, nullptr, scratch, 0,
+                                vs[v].pad_lds));
                 }
             };
             launch();
