@@ -1247,4 +1247,132 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
     return CHIP_OK;
 }
 
+// ---- streaming bao hasher (utils.rs:104-137) ---------------------------
+
+}  // extern "C"
+
+struct chip_bao_hasher {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    DevBuf content, enc, scratch, hash;
+    uint64_t len = 0, enc_len = 0;
+    bool finalized = false;
+    uint8_t h[32] = {0};
+};
+
+namespace {
+
+// grow keeping the first `used` bytes (geometric, so appends are amortised O(1))
+hipError_t grow_keep(DevBuf &b, size_t need, size_t used, hipStream_t s) {
+    if (b.cap >= need) return hipSuccess;
+    size_t cap = std::max(need, 2 * b.cap);
+    cap = (cap + 4095) & ~size_t(4095);
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, cap);
+    if (e != hipSuccess) return e;
+    if (used) {
+        e = hipMemcpyAsync(p, b.p, used, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            (void)hipFree(p);
+            return e;
+        }
+    }
+    if (b.p) (void)hipFree(b.p);
+    b.p = p;
+    b.cap = cap;
+    return hipSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+int chip_bao_hasher_new(chip_bao_hasher **out) {
+    if (!out) return CHIP_ERR_INVALID_ARG;
+    Ctx *c;
+    int st = ctx_get(&c);  // device check + hipSetDevice
+    if (st != CHIP_OK) return st;
+    auto *h = new chip_bao_hasher();
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete h;
+        set_device_error(e);
+        return CHIP_ERR_DEVICE;
+    }
+    *out = h;
+    return CHIP_OK;
+}
+
+int chip_bao_hasher_update(chip_bao_hasher *h, const uint8_t *buf, uint64_t n) {
+    if (!h || (!buf && n)) return CHIP_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->finalized) return CHIP_ERR_INVALID_ARG;
+    if (!n) return CHIP_OK;
+    Ctx *c;
+    int st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(grow_keep(h->content, h->len + n, h->len, h->stream));
+    CHIP_HIP(hipMemcpyAsync(static_cast<uint8_t *>(h->content.p) + h->len, buf, n, hipMemcpyHostToDevice,
+                            h->stream));
+    CHIP_HIP(hipStreamSynchronize(h->stream));  // the caller may reuse buf on return
+    h->len += n;
+    return CHIP_OK;
+}
+
+int chip_bao_hasher_finalize(chip_bao_hasher *h, uint8_t hash[CHIP_HASH_LEN]) {
+    if (!h || !hash) return CHIP_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->finalized) {
+        Ctx *c;
+        int st = ctx_get(&c);
+        if (st != CHIP_OK) return st;
+        const uint64_t n = h->len;
+        h->enc_len = bao_encoded_len(n);
+        CHIP_HIP(grow_keep(h->content, 16, h->len, h->stream));
+        CHIP_HIP(grow(h->enc, h->enc_len));
+        CHIP_HIP(grow(h->scratch, bao_scratch_len(n, 1)));
+        CHIP_HIP(grow(h->hash, 32));
+        CHIP_HIP(bao_encode_dev(static_cast<const uint8_t *>(h->content.p), 0, n, 1,
+                                static_cast<uint8_t *>(h->enc.p), 0, static_cast<uint8_t *>(h->hash.p),
+                                h->scratch.p, h->stream));
+        CHIP_HIP(hipMemcpyAsync(h->h, h->hash.p, 32, hipMemcpyDeviceToHost, h->stream));
+        CHIP_HIP(hipStreamSynchronize(h->stream));
+        h->finalized = true;
+    }
+    std::memcpy(hash, h->h, 32);
+    return CHIP_OK;
+}
+
+uint64_t chip_bao_hasher_len(chip_bao_hasher *h) {
+    if (!h) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return h->len;
+}
+
+int chip_bao_hasher_read_all(chip_bao_hasher *h, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if (!h || !out_len) return CHIP_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->finalized) return CHIP_ERR_INVALID_ARG;
+    *out_len = h->enc_len;
+    if (out_cap < h->enc_len || !out) return CHIP_ERR_BUFFER_TOO_SMALL;
+    Ctx *c;
+    int st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(hipMemcpyAsync(out, h->enc.p, h->enc_len, hipMemcpyDeviceToHost, h->stream));
+    CHIP_HIP(hipStreamSynchronize(h->stream));
+    return CHIP_OK;
+}
+
+void chip_bao_hasher_free(chip_bao_hasher *h) {
+    if (!h) return;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        for (DevBuf *b : {&h->content, &h->enc, &h->scratch, &h->hash})
+            if (b->p) (void)hipFree(b->p);
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+    }
+    delete h;
+}
+
 }  // extern "C"

@@ -45,9 +45,11 @@ template <> struct Entry<2> { using T = u32x2; };
 // 16-B aligned (the C-ABI requires aligned pointers and strides), so the
 // aligned block holding any valid byte lies inside a mapped page: one vector
 // load + a byte mask, no byte-wise loads (they inflated K=8 to 350+ VGPRs).
+template <bool NTL = false>
 __device__ __forceinline__ u32x4 load16_masked(const uint8_t *base, uint64_t off, uint64_t valid) {
     if (off >= valid) return u32x4{0u, 0u, 0u, 0u};
-    u32x4 r = *reinterpret_cast<const u32x4 *>(base + off);
+    u32x4 r = NTL ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + off))
+                  : *reinterpret_cast<const u32x4 *>(base + off);
     if (off + VEC > valid) {
         const int rem = (int)(valid - off);  // 1..15
         auto keep = [rem](int i) -> uint32_t {
@@ -132,8 +134,10 @@ struct TileIter {
 
 // RO: replica-count override, WPE: waves/EU hint, SB: scheduling fence every SB
 // shards (bounds the table lookups in flight; 0 = none), PF: load the next
-// super-tile's shards before computing the current one — tools/zfec_tune.
-template <int K, int NG, int U, int MAP, bool NT, int RO = 0, int WPE = 1, int SB = 0, bool PF = false>
+// super-tile's shards before computing the current one, NTL: nontemporal
+// input loads — tools/zfec_tune.
+template <int K, int NG, int U, int MAP, bool NT, int RO = 0, int WPE = 1, int SB = 0, bool PF = false,
+          bool NTL = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_kernel(ApplyArgs a) {
     constexpr int R = RO ? RO : replicas_for(K);
     using E = typename Entry<NG>::T;
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const uint64_t col = col0 + (uint64_t)u * TILE;
-                v[u][j] = col < a.C ? load16_masked(ib, ioff[j] + col, a.valid) : u32x4{0u, 0u, 0u, 0u};
+                v[u][j] = col < a.C ? load16_masked<NTL>(ib, ioff[j] + col, a.valid) : u32x4{0u, 0u, 0u, 0u};
             }
     };
 

@@ -22,6 +22,8 @@
  *   chip_snap_decompress    <- decoding::snap        src/decoding.rs:70-77
  *   chip_ecies_encrypt      <- encoding::ecies       src/encoding.rs:30-36
  *   chip_ecies_decrypt      <- decoding::ecies       src/decoding.rs:62-68
+ * the streaming hasher:
+ *   chip_bao_hasher_*       <- utils::BaoHasher      src/utils.rs:104-137
  * and helpers:
  *   chip_calc_padding_len   <- utils::calc_padding_len src/utils.rs:47-58
  *
@@ -278,6 +280,23 @@ CHIP_API int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const
  * out must hold `len` bytes. */
 CHIP_API int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t hash_len,
                         uint32_t padding, uint32_t chunk_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* ---- streaming bao hasher (utils.rs:104-137 BaoHasher) ------------------ */
+/* A thread-safe append-only hasher (one mutex per hasher, as the reference's
+ * RwLock).  update() appends to a growing HBM buffer (the caller's bytes are
+ * copied before it returns); finalize() runs the bao kernels over everything
+ * appended and returns the root hash (== BLAKE3 of the content); read_all()
+ * returns the combined bao encoding (== bao::encode::encode of the content).
+ * update() after finalize() -> CHIP_ERR_INVALID_ARG (the reference's encoder
+ * panics); finalize() again returns the same hash; read_all() before
+ * finalize() -> CHIP_ERR_INVALID_ARG. */
+typedef struct chip_bao_hasher chip_bao_hasher;
+CHIP_API int chip_bao_hasher_new(chip_bao_hasher **out);
+CHIP_API int chip_bao_hasher_update(chip_bao_hasher *h, const uint8_t *buf, uint64_t n);
+CHIP_API int chip_bao_hasher_finalize(chip_bao_hasher *h, uint8_t hash[CHIP_HASH_LEN]);
+CHIP_API uint64_t chip_bao_hasher_len(chip_bao_hasher *h);
+CHIP_API int chip_bao_hasher_read_all(chip_bao_hasher *h, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+CHIP_API void chip_bao_hasher_free(chip_bao_hasher *h);
 
 /* ---- host-memory batch (end-to-end: host -> HBM -> host) -------------- */
 /* encode() for `count` objects of n bytes that live in HOST memory (object o

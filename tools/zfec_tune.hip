@@ -53,11 +53,12 @@ struct Variant {
     size_t lds;
 };
 
-template <int U, int MAP, bool NT, int CH = 1, int WPE = 1, int SB = 0, bool PF = false>
+template <int U, int MAP, bool NT, int CH = 1, int WPE = 1, int SB = 0, bool PF = false, bool NTL = false>
 Variant V(int bpc) {
-    char buf[80];
-    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d wpe%d sb%d pf%d %s bpc%d", U, MAP, CH, WPE, SB, PF, NT ? "nt " : "pln", bpc);
-    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT, 0, WPE, SB, PF>, bpc, CH, (size_t)256 * 4 * 8 * 4};
+    char buf[96];
+    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d wpe%d sb%d pf%d ntl%d %s bpc%d", U, MAP, CH, WPE, SB, PF, NTL,
+             NT ? "nt " : "pln", bpc);
+    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT, 0, WPE, SB, PF, NTL>, bpc, CH, (size_t)256 * 4 * 8 * 4};
 }
 
 // 8-of-16 variants (K = 8, NG = 2), replica count R
@@ -103,9 +104,10 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {V<1, 3, true, 64>(4),             V<1, 3, true, 64, 1, 0, true>(4), V<1, 3, true, 64, 4, 1, true>(4),
-              V<1, 3, true, 64, 3, 1, true>(3), V<1, 3, true, 64, 2, 0, true>(2), V<2, 3, true, 32, 2, 0, true>(2),
-              V<1, 3, true, 64, 1, 0, true>(3)};
+        vs = {V<1, 3, true, 64>(4),                       V<1, 3, true, 64, 1, 0, false, true>(4),
+              V<1, 3, false, 64, 1, 0, false, true>(4),   V<2, 3, true, 32, 2, 0, true>(2),
+              V<2, 3, true, 32, 2, 0, true, true>(2),     V<1, 3, true, 64, 2, 0, true, true>(2),
+              V<1, 1, true, 1, 1, 0, false, true>(4)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
