@@ -23,6 +23,7 @@
 #include "gf256.hpp"
 #include "zfec_device.hpp"
 
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -95,29 +96,42 @@ constexpr uint64_t ZF_CHUNK = 64;
 // Wide stripes (K > 4): pin the XOR partial sums every shard (SB = 1) so the
 // K*16 table lookups are not all live at once — without it K = 8 compiles to
 // 256 VGPR + 90 AGPR, one wave per SIMD — and prefetch the next tile's shards
-// into registers (K <= 8; K = 16 has no registers to spare).  8 computed rows (NG = 2): plain stores measured +1-3% over
-// nontemporal at 2 workgroups/CU (tools/zfec_tune, 8-of-16 sweep in DESIGN.md).
-template <int K, int NG>
-KernelFn kernel_ptr() {
-    if constexpr (K > 4)
-        return gf_apply_kernel<K, NG, ZF_U, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
-    else
-        return gf_apply_kernel<K, NG, ZF_U, ZF_MAP, ZF_NT>;
-}
-
+// into registers (K <= 8; K = 16 has no registers to spare).  8 computed
+// rows (NG = 2): plain stores measured +1-3% over nontemporal at 2
+// workgroups/CU (tools/zfec_tune, 8-of-16 sweep in DESIGN.md).
+// The 4-of-8 shape (K = 4, NG = 1): super-tiles of 2 column tiles with the
+// next super-tile prefetched, 2 workgroups/CU: +1.2-1.4% over one tile at
+// occupancy 4, on two boxes.
 struct KernelInfo {
     KernelFn fn;
     size_t lds;
     int grid;
+    int u;        // column tiles per super-tile (the kernel's U)
+    int bpc_cap;  // workgroups per CU to launch (0 = occupancy limit)
 };
 
 template <int K, int NG>
 KernelInfo make_info() {
     constexpr int R = replicas_for(K);
     KernelInfo ki;
-    ki.fn = kernel_ptr<K, NG>();
     ki.lds = (size_t)256 * K * R * 4 * NG;
     ki.grid = 0;
+    ki.u = 1;
+    ki.bpc_cap = 0;
+    if constexpr (K > 4) {
+        ki.fn = gf_apply_kernel<K, NG, ZF_U, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
+    } else if constexpr (K == 4 && NG == 1) {
+        static const bool u1 = std::getenv("CHIP_ZFEC_K4_U1") != nullptr;  // A/B tuning switch
+        if (u1) {
+            ki.fn = gf_apply_kernel<4, 1, 1, ZF_MAP, ZF_NT>;
+        } else {
+            ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true>;
+            ki.u = 2;
+            ki.bpc_cap = 2;
+        }
+    } else {
+        ki.fn = gf_apply_kernel<K, NG, ZF_U, ZF_MAP, ZF_NT>;
+    }
     return ki;
 }
 
@@ -154,6 +168,7 @@ int grid_for(const KernelInfo &ki) {
                                                      TPB, ki.lds) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
+    if (ki.bpc_cap > 0 && per_cu > ki.bpc_cap) per_cu = ki.bpc_cap;
     const int g = per_cu * num_cus();
     g_grid[key] = g;
     return g;
@@ -265,11 +280,14 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     hipError_t e = device_table(sub, ng, &a.table);
     if (e != hipSuccess) return e;
     const int grid_cap = grid_for(ki);
-    uint64_t grid = a.total_tiles < (uint64_t)grid_cap ? a.total_tiles : (uint64_t)grid_cap;
+    // the kernel walks super-tiles of ki.u column tiles (never across objects)
+    const uint64_t units = ((a.tiles_per_obj + ki.u - 1) / ki.u) * L.count;
+    uint64_t grid = units < (uint64_t)grid_cap ? units : (uint64_t)grid_cap;
     if (grid >= 8) grid = grid / 8 * 8;  // XCD grouping needs a multiple of 8
-    // runs short enough that every workgroup gets work on small jobs
-    const uint64_t per_wg = a.total_tiles / (grid ? grid : 1);
-    a.chunk = per_wg < 1 ? 1 : (per_wg < ZF_CHUNK ? per_wg : ZF_CHUNK);
+    // runs of up to ZF_CHUNK tiles, short enough that every workgroup gets work on small jobs
+    const uint64_t per_wg = units / (grid ? grid : 1);
+    const uint64_t run = ZF_CHUNK / ki.u;
+    a.chunk = per_wg < 1 ? 1 : (per_wg < run ? per_wg : run);
     hipLaunchKernelGGL(ki.fn, dim3((unsigned)grid), dim3(TPB), ki.lds, stream, a);
     return hipGetLastError();
 }
