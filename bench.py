@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--object-mib", type=float, default=16.0)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=8)
-    ap.add_argument("--mode", choices=["encode", "decode", "bao", "e2e"], default="encode",
+    ap.add_argument("--mode", choices=["encode", "decode", "bao", "e2e", "e2e-decode"], default="encode",
                     help="e2e: encode() at --level from pinned HOST memory to host memory (H2D+kernels+D2H)")
     ap.add_argument("--level", type=int, default=12, help="e2e mode: Format bits (Bao|Zfec = 12)")
     ap.add_argument("--slots", type=int, default=3, help="e2e mode: pipeline slots (streams)")
@@ -117,12 +117,16 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
     from oracle import oracle as O
     import numpy as np
     obj = np.frombuffer(sample_obj, np.uint8) if sample_obj is not None else O.fill_object(SEED, 0, n)
-    if args.mode == "e2e" and args.level & 1:
+    if args.mode in ("e2e", "e2e-decode") and args.level & 1:
         import hashlib
         eph = hashlib.sha256(b"cpu baseline eph").digest()
         pub = O.c_public_key(hashlib.sha256(b"carbonado-amd bench receiver").digest())
     else:
         eph = pub = b""
+    if args.mode == "e2e-decode":
+        import hashlib
+        sk = hashlib.sha256(b"carbonado-amd bench receiver").digest()
+        enc_obj, h_obj, inf_obj = O.c_encode_full(obj, args.level, pub, eph if eph else bytes(32), bytes(16))
     if args.mode == "decode":
         z, pad, C = O.zfec_encode(obj, args.k, args.m)
         keep = [i for i in range(args.m) if str(i) not in args.erase.split(",")]
@@ -132,6 +136,12 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
     while True:
         if args.mode == "bao":
             O.bao_encode(obj)
+        elif args.mode == "e2e-decode":
+            cur = O.decode(h_obj, enc_obj, inf_obj["padding_len"], args.level & 12) if args.level & 12 else enc_obj
+            if args.level & 1:
+                cur = O.c_ecies_decrypt(sk, cur)
+            if args.level & 2:
+                cur = O.c_snap_decompress(cur, n + 1024)
         elif args.mode == "e2e":
             if args.level & 3:  # host stages too: the all-C restatement (oracle/host_oracle.c)
                 O.c_encode_full(obj, args.level, pub, eph, bytes(16))
@@ -145,12 +155,12 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or done >= 4096:
             break
-    what = {"bao": "bao encode", "e2e": f"encode() level {args.level}",
+    what = {"bao": "bao encode", "e2e": f"encode() level {args.level}", "e2e-decode": f"decode() level {args.level}",
             "decode": f"zfec {args.k}-of-{args.m} decode, erased {args.erase}"}.get(
         args.mode, f"zfec {args.k}-of-{args.m} encode")
     return {"value": round(done * n / el / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{done} x {n} B objects ({what}) through oracle/carbonado_oracle.c"
-                      f"{' + host_oracle.c' if args.mode == 'e2e' and args.level & 3 else ''}, scalar "
+                      f"{' + host_oracle.c' if args.mode.startswith('e2e') and args.level & 3 else ''}, scalar "
                       f"restatement of the reference crates, 1 thread, {el:.1f} s"}
 
 
@@ -195,6 +205,35 @@ class Workload:
             self.alg_bytes = count * (2 * k * C)  # read k shares + write k data shards
             self.kernel = f"gf_apply_kernel<{k},1> (decode, erased {sorted(erased)})"
             self.kernel_sym = f"gf_apply_kernel<{k}, 1,"
+        elif args.mode == "e2e-decode":
+            import hashlib
+            from carbonado_amd.encoding import public_key
+            cap = L.chip_encode_max_len(n)
+            lv, slots = args.level, args.slots
+            self.sk = hashlib.sha256(b"carbonado-amd bench receiver").digest()
+            self.pub = public_key(self.sk) if lv & 1 else b""
+            h_in = torch.empty((count, n), dtype=torch.uint8, pin_memory=True)
+            h_in.copy_(self.inp.cpu())
+            del self.inp
+            torch.cuda.empty_cache()
+            self.inp = h_in
+            self.h_enc = torch.empty((count, cap), dtype=torch.uint8, pin_memory=True)
+            self.h_hash = torch.empty((count, 32), dtype=torch.uint8, pin_memory=True)
+            self.enc_len, infos = device.encode_host_batch(lv, h_in, n, self.h_enc, self.h_hash, slots,
+                                                           pubkey=self.pub, host_threads=args.host_threads)
+            self.pads = [i.padding_len for i in infos]
+            self.h_out = torch.empty((count, n + 1024), dtype=torch.uint8, pin_memory=True)
+
+            def step():
+                device.decode_host_batch(lv, self.h_enc, self.enc_len, self.h_hash, self.pads, self.h_out,
+                                         secret_key=self.sk, nslots=slots, host_threads=args.host_threads)
+            self.step = step
+            step()
+            self.alg_bytes = count * (max(self.enc_len) + n)  # PCIe bytes: H2D encoding + D2H content
+            stages = ("ecies + " if lv & 1 else "") + ("unsnap + " if lv & 2 else "")
+            host = f" + host {stages[:-3]} on {args.host_threads} threads" if stages else ""
+            self.kernel = f"decode() level {lv}: H2D + bao verify kernels + D2H{host}, {slots} slots"
+            self.kernel_sym = "e2e"
         elif args.mode == "e2e":
             cap = L.chip_encode_max_len(n)
             self.h_in = torch.empty((count, n), dtype=torch.uint8, pin_memory=True)
@@ -311,6 +350,8 @@ class Workload:
                   self.h_hash[0].numpy().tobytes() == h)
         elif self.args.mode == "decode":
             ok = self.out[0, :self.n].cpu().numpy().tobytes() == sample
+        elif self.args.mode == "e2e-decode":
+            ok = self.h_out[0, :self.n].numpy().tobytes() == sample
         else:
             ok = self.hashes[0].cpu().numpy().tobytes() == O.blake3(sample)
         return ok, sample
@@ -364,11 +405,14 @@ def main():
         elif args.mode == "e2e":
             workload = (f"encode() level {args.level} host->HBM->host (pinned), {args.objects} x "
                         f"{args.object_mib:g} MiB objects per GPU")
+        elif args.mode == "e2e-decode":
+            workload = (f"decode() level {args.level} host->HBM->host (pinned), {args.objects} x "
+                        f"{args.object_mib:g} MiB objects per GPU")
         else:
             workload = f"zfec {k}-of-{m} {args.mode}, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         res = {
             "metric": METRIC if args.mode == "encode" and (k, m) == (4, 8) and n == 16 << 20 else
-            (f"GiB/s {workload}" if args.mode == "e2e" else f"GiB/s device-resident {workload}"),
+            (f"GiB/s {workload}" if args.mode.startswith("e2e") else f"GiB/s device-resident {workload}"),
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -390,7 +434,7 @@ def main():
                          "min_launch_ms": round(min(launch_ms), 4)},
             "verified_object0": verified,
         }
-        if args.mode == "e2e":
+        if args.mode.startswith("e2e"):
             res["roofline"].update({"bound": "pcie", "peak": 2 * 63.0,
                                     "frac": round(achieved / 126.0, 4),
                                     "note": "PCIe Gen5 x16, 63 GB/s per direction (spec), H2D and D2H overlapped"})

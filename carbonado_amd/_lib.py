@@ -111,6 +111,11 @@ SIGNATURES = {
     "chip_bao_hasher_len": (ctypes.c_uint64, [ctypes.c_void_p]),
     "chip_bao_hasher_read_all": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
     "chip_bao_hasher_free": (None, [ctypes.c_void_p]),
+    "chip_decode_host_batch": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                              ctypes.c_void_p, c_u64p, ctypes.c_uint64, ctypes.c_uint64, c_u32p,
+                                              ctypes.c_void_p, ctypes.c_uint64, c_u64p,
+                                              ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint64,
+                                              ctypes.c_uint32]),
     "chip_encode_host_batch": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.POINTER(EciesInjectC), ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,

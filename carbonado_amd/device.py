@@ -96,3 +96,31 @@ def encode_host_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, ha
                                             inp.shape[1], _p(out), out.shape[1], olen, _p(hashes), info,
                                             nslots, slice_bytes, host_threads))
     return [olen[o] for o in range(count)], [EncodeInfo.from_c(info[o]) for o in range(count)]
+
+
+def decode_host_batch(fmt: int, enc: torch.Tensor, in_len, hashes: torch.Tensor, padding, out: torch.Tensor,
+                      secret_key: bytes = b"", nslots: int = 3, slice_bytes: int = 256 << 20,
+                      host_threads: int = 0, raise_first: bool = True):
+    """End-to-end decode() of `count` encoded objects held in HOST memory:
+    enc uint8 [count, >= max in_len], in_len / padding per object, hashes
+    uint8 [count, 32], out uint8 [count, out_stride].  Synchronous.  Returns
+    (decoded length per object, status per object); with raise_first the
+    first failing object's status is raised as its CarbonadoError."""
+    import numpy as np
+    from .error import status_to_error
+    assert not enc.is_cuda and not out.is_cuda and not hashes.is_cuda
+    assert enc.is_contiguous() and out.is_contiguous() and hashes.is_contiguous()
+    count = enc.shape[0]
+    n = max(count, 1)
+    lens = (ctypes.c_uint64 * n)(*[int(x) for x in in_len])
+    pads = (ctypes.c_uint32 * n)(*[int(x) for x in padding])
+    olen = (ctypes.c_uint64 * n)()
+    st = (ctypes.c_int32 * n)()
+    sk = np.frombuffer(bytes(secret_key), dtype=np.uint8)
+    rc = _lib.lib().chip_decode_host_batch(fmt, sk.ctypes.data if sk.size else None, sk.size, _p(hashes), _p(enc),
+                                           lens, count, enc.shape[1], pads, _p(out), out.shape[1], olen, st,
+                                           nslots, slice_bytes, host_threads)
+    statuses = [st[o] for o in range(count)]
+    if rc and (raise_first or not any(statuses)):
+        raise status_to_error(rc)
+    return [olen[o] for o in range(count)], statuses

@@ -315,6 +315,21 @@ CHIP_API int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint6
                                     uint64_t *out_len, uint8_t *hashes, chip_encode_info *info,
                                     uint32_t nslots, uint64_t slice_bytes, uint32_t host_threads);
 
+/* decode() for `count` encoded objects in HOST memory (object o: in_len[o]
+ * bytes at in + o*in_stride, bao hash at hashes + 32*o, zfec padding[o]) into
+ * host memory (out + o*out_stride, out_len[o] bytes).  Device part per slice:
+ * H2D, bao verify-decode, zfec (positional shards: the primaries' bytes,
+ * decoding.rs:95-99), D2H; the Ecies/Snappy host stages of a slice run on
+ * `host_threads` threads while the next slice is on the device.  Per-object
+ * results go to status[o] (a chip_status; a short out_stride gives
+ * CHIP_ERR_BUFFER_TOO_SMALL with out_len[o] = the size needed); the call
+ * returns CHIP_OK when every object decoded, else the first failing status. */
+CHIP_API int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t sk_len,
+                                    const uint8_t *hashes, const uint8_t *in, const uint64_t *in_len,
+                                    uint64_t count, uint64_t in_stride, const uint32_t *padding, uint8_t *out,
+                                    uint64_t out_stride, uint64_t *out_len, int32_t *status, uint32_t nslots,
+                                    uint64_t slice_bytes, uint32_t host_threads);
+
 #ifdef __cplusplus
 }
 #endif

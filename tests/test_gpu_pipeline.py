@@ -218,3 +218,34 @@ def test_bao_decode_batch_header_mismatch(gpu):
     device.bao_decode_batch(t, n, hashes, out, status, device.bao_scratch(n, 1))
     torch.cuda.synchronize()
     assert int(status[0]) == 5
+
+
+@pytest.mark.parametrize("level", [4, 8, 12, 14, 15])
+def test_decode_host_batch_roundtrip(gpu, level):
+    """chip_decode_host_batch (host -> HBM -> host decode()) inverts the batch
+    encode, objects compressible or not; a tampered object fails alone."""
+    import torch
+    from carbonado_amd import device
+    n, count = 60_001, 6
+    rng = np.random.default_rng(100 + level)
+    rows = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(count - 2)]
+    rows += [np.zeros(n, np.uint8), np.frombuffer((b"carbonado " * n)[:n], np.uint8)]
+    inp = torch.from_numpy(np.stack(rows))
+    cap = device._lib.lib().chip_encode_max_len(n)
+    enc = torch.zeros((count, cap), dtype=torch.uint8)
+    hashes = torch.zeros((count, 32), dtype=torch.uint8)
+    olen, info = device.encode_host_batch(level, inp, n, enc, hashes, nslots=2, slice_bytes=2 * n, pubkey=PUB)
+    out = torch.zeros((count, n + 64), dtype=torch.uint8)
+    pads = [i.padding_len for i in info]
+    dlen, st = device.decode_host_batch(level, enc, olen, hashes, pads, out, secret_key=SK, nslots=2,
+                                        slice_bytes=2 * n, host_threads=3)
+    assert st == [0] * count
+    for o in range(count):
+        assert dlen[o] == n and out[o, :n].numpy().tobytes() == rows[o].tobytes(), o
+    if level & 4:  # flip a content byte of object 2 only
+        enc[2, olen[2] // 2] ^= 1
+        dlen, st = device.decode_host_batch(level, enc, olen, hashes, pads, out, secret_key=SK, nslots=2,
+                                            slice_bytes=2 * n, raise_first=False)
+        assert st[2] == 5 and st[:2] == [0, 0] and st[3:] == [0] * (count - 3)
+        for o in (0, 1, 3):
+            assert out[o, :n].numpy().tobytes() == rows[o].tobytes()
