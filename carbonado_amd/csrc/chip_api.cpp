@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -320,6 +321,20 @@ int encode_info_for(uint8_t format, uint64_t input_len, uint64_t cur, uint64_t b
 
 bool has_host_stages(uint8_t format) { return format & (CHIP_FORMAT_ECIES | CHIP_FORMAT_SNAPPY); }
 
+// grow-only, uninitialised host scratch (std::vector::resize would zero-fill
+// and page-fault 16 MiB per object)
+struct Scratch {
+    std::unique_ptr<uint8_t[]> p;
+    size_t cap = 0;
+    uint8_t *get(size_t n) {
+        if (n > cap) {
+            p.reset(new uint8_t[n]);
+            cap = n;
+        }
+        return p.get();
+    }
+};
+
 // bound of the host stages' output for an n-byte input
 uint64_t host_stage_max(uint8_t format, uint64_t n) {
     uint64_t m = (format & CHIP_FORMAT_SNAPPY) ? host::snap_max_len(n) : n;
@@ -330,7 +345,7 @@ uint64_t host_stage_max(uint8_t format, uint64_t n) {
 // snap -> ecies (encoding.rs:101-115) of one object into dst[0..cap); tmp is
 // the snap output when both stages run.
 int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const uint8_t *eph, const uint8_t *nonce,
-                     const uint8_t *in, uint64_t n, uint8_t *dst, uint64_t cap, std::vector<uint8_t> &tmp,
+                     const uint8_t *in, uint64_t n, uint8_t *dst, uint64_t cap, Scratch &tmp,
                      uint64_t *len, uint64_t *bc, uint64_t *be) {
     const bool snap = format & CHIP_FORMAT_SNAPPY, ecies = format & CHIP_FORMAT_ECIES;
     const uint8_t *cur = in;
@@ -340,9 +355,8 @@ int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const ui
         uint8_t *sd = dst;
         uint64_t scap = cap;
         if (ecies) {
-            tmp.resize(host::snap_max_len(n) + 1);
-            sd = tmp.data();
-            scap = tmp.size();
+            scap = host::snap_max_len(n) + 1;
+            sd = tmp.get(scap);
         }
         int st = host::snap_compress(in, n, sd, scap, &cur_n);
         if (st != CHIP_OK) return st;
@@ -900,7 +914,8 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
     if ((!in && n) || !out_len || !hash) return CHIP_ERR_INVALID_ARG;
     if ((format & CHIP_FORMAT_ECIES) && !pubkey) return CHIP_ERR_INVALID_ARG;
     // host stages (encoding.rs:101-115)
-    thread_local std::vector<uint8_t> t_stage, t_tmp;
+    thread_local std::vector<uint8_t> t_stage;
+    thread_local Scratch t_tmp;
     const uint8_t *cur = in;
     uint64_t cur_n = n, bc = 0, be = 0;
     if (has_host_stages(format)) {
@@ -1056,6 +1071,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     if (!c) stage_host.resize(S * h_al);
     std::vector<uint64_t> len(S), bc(S), be(S);
     std::vector<int> sts(S);
+    std::vector<Scratch> scratch(T);  // per host thread, reused across slices
     auto drain = [&]() {
         if (c)
             for (uint32_t k = 0; k < nslots; ++k) (void)hipStreamSynchronize(c->slots[k].stream);
@@ -1074,7 +1090,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             uint8_t *stage = sl ? static_cast<uint8_t *>(sl->stage.p) : stage_host.data();
             const uint32_t nt = (uint32_t)std::min<uint64_t>(T, cnt);
             auto work = [&](uint32_t t) {
-                std::vector<uint8_t> tmp;
+                Scratch &tmp = scratch[t];
                 for (uint64_t j = t; j < cnt; j += nt) {
                     const uint64_t o = o0 + j;
                     sts[j] = host_stages_into(format, pubkey, pubkey_len,
@@ -1204,7 +1220,7 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
         olen_max = std::max(olen_max, geo[o].olen);
     }
     if (!zfec && !bao) {  // host stages only (or identity)
-        std::vector<uint8_t> tmp;
+        Scratch tmp;
         for (uint64_t o = 0; o < count; ++o) {
             if (status[o] != CHIP_OK) continue;
             const uint8_t *src = in + o * in_stride;
@@ -1219,10 +1235,10 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
             uint64_t got = 0;
             int st = CHIP_OK;
             if (format & CHIP_FORMAT_ECIES) {
-                tmp.resize(n + 1);
-                st = host::ecies_decrypt(secret_key, sk_len, src, n, (format & CHIP_FORMAT_SNAPPY) ? tmp.data() : dst,
-                                         (format & CHIP_FORMAT_SNAPPY) ? tmp.size() : out_stride, &got);
-                src = tmp.data();
+                uint8_t *t = tmp.get(n + 1);
+                st = host::ecies_decrypt(secret_key, sk_len, src, n, (format & CHIP_FORMAT_SNAPPY) ? t : dst,
+                                         (format & CHIP_FORMAT_SNAPPY) ? n + 1 : out_stride, &got);
+                src = t;
                 n = got;
             }
             if (st == CHIP_OK && (format & CHIP_FORMAT_SNAPPY)) st = host::snap_decompress(src, n, dst, out_stride, &got);
@@ -1257,6 +1273,7 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
         else if (bao) CHIP_HIP(grow_pinned(sl.stage, S * 4));
     }
     const uint64_t nslices = (count + S - 1) / S;
+    std::vector<Scratch> dscratch(T);  // per host thread, reused across slices
     // host part of slice i: device statuses -> status[], then ecies -> snap into out
     auto finish = [&](uint64_t i) {
         Slot &sl = c->slots[i % nslots];
@@ -1268,7 +1285,7 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
         if (!hs) return;
         const uint32_t nt = (uint32_t)std::min<uint64_t>(T, cnt);
         auto work = [&](uint32_t t) {
-            std::vector<uint8_t> tmp;
+            Scratch &tmp = dscratch[t];
             for (uint64_t j = t; j < cnt; j += nt) {
                 const uint64_t o = o0 + j;
                 if (status[o] != CHIP_OK) continue;
@@ -1278,10 +1295,10 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
                 int r = CHIP_OK;
                 if (format & CHIP_FORMAT_ECIES) {
                     const bool snap = format & CHIP_FORMAT_SNAPPY;
-                    if (snap) tmp.resize(n + 1);
-                    r = host::ecies_decrypt(secret_key, sk_len, src, n, snap ? tmp.data() : dst,
-                                            snap ? tmp.size() : out_stride, &got);
-                    src = tmp.data();
+                    uint8_t *tb = snap ? tmp.get(n + 1) : nullptr;
+                    r = host::ecies_decrypt(secret_key, sk_len, src, n, snap ? tb : dst, snap ? n + 1 : out_stride,
+                                            &got);
+                    src = tb;
                     n = got;
                 }
                 if (r == CHIP_OK && (format & CHIP_FORMAT_SNAPPY)) r = host::snap_decompress(src, n, dst, out_stride, &got);
