@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--verify-all", action="store_true",
+                    help="encode mode: check EVERY object bit-exact (SURVEY 8d): BLAKE3 of each object's "
+                         "shards on the GPU vs the C oracle's zfec + BLAKE3 on 16 host threads")
     ap.add_argument("--no-aliased", action="store_true",
                     help="encode mode: skip the second, in-place (aliased data shards) measurement")
     ap.add_argument("--scatter", action="store_true",
@@ -320,6 +323,33 @@ class Workload:
         barrier(world)
         return t1 - t0, [a.elapsed_time(b) for a, b in evs]
 
+    def verify_all(self, threads: int = 16):
+        """SURVEY.md 8d cfg2 check: all objects bit-exact, compared through
+        BLAKE3 digests of the m shards (computed on the device by the bao
+        kernels, hash-only) against oracle/carbonado_oracle.c's zfec + BLAKE3
+        of the same inputs (ctypes releases the GIL: the checks run in
+        parallel on `threads` host threads)."""
+        from concurrent.futures import ThreadPoolExecutor
+        from carbonado_amd import device
+        from oracle import oracle as O
+        t0 = time.perf_counter()
+        count, k, m, C = self.count, self.k, self.m, self.C
+        digests = torch.empty((count, 32), dtype=torch.uint8, device=self.dev)
+        scratch = device.bao_scratch(m * C, count, self.dev)
+        device.bao_encode_batch(self.out, m * C, None, digests, scratch)
+        torch.cuda.synchronize()
+        gpu = digests.cpu().numpy()
+        del scratch
+        host_in = self.inp.cpu().numpy()
+
+        def check(o):
+            return O.blake3(O.zfec_encode(host_in[o], k, m)[0]) == gpu[o].tobytes()
+        with ThreadPoolExecutor(threads) as ex:
+            oks = list(ex.map(check, range(count)))
+        bad = [o for o, ok in enumerate(oks) if not ok]
+        return {"ok": not bad, "objects": count, "mismatched": bad[:16], "seconds": round(time.perf_counter() - t0, 1),
+                "how": f"BLAKE3 of each object's {m} shards on the GPU vs oracle zfec + BLAKE3 on {threads} threads"}
+
     def time_aliased(self, steps: int, warmup: int, world: int):
         """the same encode with the data shards aliased (in
         place: the input already sits in the first n bytes of each output
@@ -388,6 +418,9 @@ def main():
     verified, sample = None, None
     if rank == 0 and not args.no_verify and not args.dry_run:
         verified, sample = wl.verify_object0()
+    verified_all = None
+    if rank == 0 and args.verify_all and args.mode == "encode" and not args.dry_run:
+        verified_all = wl.verify_all()
     aliased = None
     if args.mode == "encode" and not args.dry_run and not args.no_aliased:
         a_el, a_ms, a_ok = wl.time_aliased(args.steps, args.warmup, world)
@@ -454,6 +487,8 @@ def main():
                                "avg_launch_ms": hbm["avg_launch_ms"], "min_launch_ms": hbm["min_launch_ms"],
                                "note": "int32 VALU peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; ops = 672 per "
                                        "BLAKE3 compression (content blocks + parents)"}
+        if verified_all is not None:
+            res["verified_all_objects"] = verified_all
         if aliased is not None:
             a_max, a_ms, a_ok = aliased
             a_bytes = args.objects * (n + (m - k) * wl.C)
