@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <memory>
 #include <cstdio>
 #include <cstring>
@@ -1311,9 +1312,9 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
         work(0);
         for (auto &th : pool) th.join();
     };
-    for (uint64_t i = 0; i < nslices; ++i) {
+    // device part of slice i (H2D, bao verify, D2H) enqueued on its slot's stream
+    auto enqueue = [&](uint64_t i) -> int {
         Slot &sl = c->slots[i % nslots];
-        if (i >= nslots) CHIP_HIP(hipStreamSynchronize(sl.stream));  // slot free (its host part ran below)
         const uint64_t o0 = i * S, cnt = std::min(S, count - o0);
         uint8_t *stage = static_cast<uint8_t *>(sl.stage.p);
         uint32_t *h_st = reinterpret_cast<uint32_t *>(stage + (hs ? S * o_al : 0));
@@ -1357,13 +1358,58 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
                 CHIP_HIP(hipMemcpy2DAsync(dst, dpitch, d_res, res_pitch, olen, gcnt, hipMemcpyDeviceToHost, sl.stream));
             }
         }
-        if (i >= 1) {  // host part of the previous slice overlaps this slice's device work
-            CHIP_HIP(hipStreamSynchronize(c->slots[(i - 1) % nslots].stream));
-            finish(i - 1);
+        return CHIP_OK;
+    };
+    // A finisher thread completes slices in order (wait for the slot's stream,
+    // then the host stages on T threads) while this thread keeps the device
+    // queue full; a slot is reused only after its previous slice finished.
+    std::mutex fm;
+    std::condition_variable fcv;
+    uint64_t enqueued = 0, finished = 0;
+    bool abort_run = false;
+    std::string fin_err;
+    std::thread finisher([&] {
+        (void)hipSetDevice(g_device);
+        for (uint64_t i = 0; i < nslices; ++i) {
+            {
+                std::unique_lock<std::mutex> lk(fm);
+                fcv.wait(lk, [&] { return enqueued > i || abort_run; });
+                if (enqueued <= i) return;
+            }
+            hipError_t e = hipStreamSynchronize(c->slots[i % nslots].stream);
+            if (e == hipSuccess) finish(i);
+            std::lock_guard<std::mutex> lk(fm);
+            if (e != hipSuccess) {
+                fin_err = hipGetErrorString(e);
+                abort_run = true;
+            }
+            finished = i + 1;
+            fcv.notify_all();
+            if (abort_run) return;
         }
+    });
+    int run_st = CHIP_OK;
+    for (uint64_t i = 0; i < nslices && run_st == CHIP_OK; ++i) {
+        if (i >= nslots) {
+            std::unique_lock<std::mutex> lk(fm);
+            fcv.wait(lk, [&] { return finished > i - nslots || abort_run; });
+            if (abort_run) { run_st = CHIP_ERR_DEVICE; break; }
+        }
+        run_st = enqueue(i);
+        std::lock_guard<std::mutex> lk(fm);
+        if (run_st == CHIP_OK) enqueued = i + 1;
+        else abort_run = true;
+        fcv.notify_all();
     }
-    CHIP_HIP(hipStreamSynchronize(c->slots[(nslices - 1) % nslots].stream));
-    finish(nslices - 1);
+    finisher.join();
+    if (!fin_err.empty()) {
+        t_last_err = fin_err;
+        run_st = CHIP_ERR_DEVICE;
+    }
+    if (run_st != CHIP_OK) {
+        for (uint32_t k = 0; k < nslots; ++k) (void)hipStreamSynchronize(c->slots[k].stream);
+        return run_st;
+    }
     for (uint32_t k = 0; k < nslots; ++k) CHIP_HIP(hipStreamSynchronize(c->slots[k].stream));
     for (uint64_t o = 0; o < count; ++o)
         if (status[o] != CHIP_OK) return status[o];
