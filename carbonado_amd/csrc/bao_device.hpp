@@ -455,20 +455,21 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
                 }
                 continue;
             }
-            const uint32_t d = (uint32_t)((128u - (base & 127u)) & 127u);
+            // lines are aligned in memory, not in the stream: any 8-aligned object base
+            const uint32_t d = (uint32_t)(-(uintptr_t)sp) & 127u;
             if (s >= 1) {  // the whole line [d + 128(s-1), d + 128 s)
                 const uint32_t x = d + 128u * (s - 1) + 16u * gl;
                 const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
                 const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
                 if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(sp + x));
                 else *reinterpret_cast<u32x4 *>(sp + x) = v;
-            } else {  // head [0, d): 8 B at 0, then aligned 16-B pieces [16k - 8, 16k + 8)
-                if (gl == 0) store8<NTS>(sp, piece(row, 0));
-                const uint32_t x = 16u * gl + 8;
+            } else {  // head [0, d): 8 B at 0 when d is 8 mod 16, then aligned 16-B pieces
+                const uint32_t h = d & 8u;
+                if (h && gl == 0) store8<NTS>(sp, piece(row, 0));
+                const uint32_t x = 16u * gl + h;
                 if (x + 16 <= d) {
                     const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                    const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
-                    *reinterpret_cast<u32x4 *>(sp + x) = v;
+                    *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
                 }
             }
             if (s == 7) {  // tail [896 + d, 1024): aligned pieces, 8 B at the end

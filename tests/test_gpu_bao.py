@@ -104,3 +104,27 @@ def test_batch_bao_full_size(gpu):
         torch.cuda.synchronize()
         st = status.cpu().tolist()
         assert st[:-1] == [0] * (count - 1) and st[-1] == 5
+
+
+def test_batch_bao_every_line_phase(gpu):
+    """Output streams whose bases take every 8-B phase modulo a 128-B line:
+    the encode stream path aligns its whole-line stores to memory, so each
+    phase takes a different head/line/tail split (bao_device.hpp stream_lines)."""
+    import torch
+    from carbonado_amd import device
+    n, count = 9 * 1024 + 37, 16
+    blen = O.lib().orc_bao_encoded_len(n)
+    stride = (blen + 15) // 16 * 16 + 8  # 8 mod 16: o * stride mod 128 visits all 16 phases
+    gen = torch.Generator(device="cuda").manual_seed(77)
+    inp = torch.randint(0, 256, (count, n), dtype=torch.uint8, device="cuda", generator=gen)
+    out = torch.full((count, stride), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+    device.bao_encode_batch(inp, n, out, hashes, device.bao_scratch(n, count))
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    assert {(out.data_ptr() + o * stride) % 128 for o in range(count)} == set(range(0, 128, 8))
+    for o in range(count):
+        oe, oh = O.bao_encode(inp[o].cpu().numpy().tobytes())
+        assert hashes[o].cpu().numpy().tobytes() == oh, o
+        assert host[o, :blen].tobytes() == oe, o
+        assert (host[o, blen:] == 0xA5).all(), o  # nothing written past the stream

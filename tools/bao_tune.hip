@@ -63,7 +63,8 @@ int main(int argc, char **argv) {
     const uint64_t n = (argc > 2 ? atoll(argv[2]) : 32) << 20;
     const int rounds = argc > 3 ? atoi(argv[3]) : 5;
     const uint64_t blen = 8 + n + 64 * (n_chunks(n) - 1);
-    const uint64_t ostride = (blen + 255) / 256 * 256;
+    const uint64_t oal = argc > 5 ? atoll(argv[5]) : 256;  // output stride alignment (bytes)
+    const uint64_t ostride = (blen + oal - 1) / oal * oal;
     uint8_t *in, *out, *hash, *dec, *scratch;
     uint32_t *status;
     CK(hipMalloc(&in, count * n));
