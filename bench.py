@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--object-mib", type=float, default=16.0)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=8)
-    ap.add_argument("--mode", choices=["encode", "decode", "bao", "e2e", "e2e-decode"], default="encode",
-                    help="e2e: encode() at --level from pinned HOST memory to host memory (H2D+kernels+D2H)")
+    ap.add_argument("--mode", choices=["encode", "decode", "bao", "pipeline", "e2e", "e2e-decode"], default="encode",
+                    help="pipeline: device-resident encode() at --level (Bao/Zfec bits; 12 = zfec fused into "
+                         "bao); e2e: encode() at --level from pinned HOST memory to host memory (H2D+kernels+D2H)")
     ap.add_argument("--level", type=int, default=12, help="e2e mode: Format bits (Bao|Zfec = 12)")
     ap.add_argument("--slots", type=int, default=3, help="e2e mode: pipeline slots (streams)")
     ap.add_argument("--host-threads", type=int, default=16,
@@ -145,7 +146,7 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
                 cur = O.c_ecies_decrypt(sk, cur)
             if args.level & 2:
                 cur = O.c_snap_decompress(cur, n + 1024)
-        elif args.mode == "e2e":
+        elif args.mode in ("e2e", "pipeline"):
             if args.level & 3:  # host stages too: the all-C restatement (oracle/host_oracle.c)
                 O.c_encode_full(obj, args.level, pub, eph, bytes(16))
             else:
@@ -158,7 +159,7 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or done >= 4096:
             break
-    what = {"bao": "bao encode", "e2e": f"encode() level {args.level}", "e2e-decode": f"decode() level {args.level}",
+    what = {"bao": "bao encode", "e2e": f"encode() level {args.level}", "pipeline": f"encode() level {args.level}", "e2e-decode": f"decode() level {args.level}",
             "decode": f"zfec {args.k}-of-{args.m} decode, erased {args.erase}"}.get(
         args.mode, f"zfec {args.k}-of-{args.m} encode")
     return {"value": round(done * n / el / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
@@ -208,6 +209,23 @@ class Workload:
             self.alg_bytes = count * (2 * k * C)  # read k shares + write k data shards
             self.kernel = f"gf_apply_kernel<{k},1> (decode, erased {sorted(erased)})"
             self.kernel_sym = f"gf_apply_kernel<{k}, 1,"
+        elif args.mode == "pipeline":
+            lv = args.level
+            if lv & 3:
+                raise SystemExit("--mode pipeline runs the device-only levels (Bao/Zfec bits); use --mode e2e")
+            zlen = m * C if lv & 8 else n
+            self.blen = blen = L.chip_bao_encoded_len(zlen) if lv & 4 else zlen
+            self.out = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device=dev)
+            self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
+            self.scratch = device.encode_scratch(lv, n, count, dev)
+            self.step = lambda: device.encode_batch(lv, self.inp, n, self.out, self.hashes, self.scratch)
+            # HBM bytes of the fused level-12 path: K1 reads n and writes the m shards into
+            # their chunk slots; K3/K4 read them back and write the header and parents
+            self.alg_bytes = count * (n + zlen + zlen + (blen - zlen)) if lv & 12 == 12 else count * (n + blen)
+            self.zlen = zlen
+            fused = " (zfec writes the shards into their bao chunk slots; bao hashes in place)" if lv & 12 == 12 else ""
+            self.kernel = f"encode() level {lv} on the device: gf_apply_kernel + bao_chunk_kernel + parent levels{fused}"
+            self.kernel_sym = "pipeline"
         elif args.mode == "e2e-decode":
             import hashlib
             from carbonado_amd.encoding import public_key
@@ -380,6 +398,10 @@ class Workload:
                   self.h_hash[0].numpy().tobytes() == h)
         elif self.args.mode == "decode":
             ok = self.out[0, :self.n].cpu().numpy().tobytes() == sample
+        elif self.args.mode == "pipeline":
+            enc, h, _ = O.encode(sample, self.args.level)
+            ok = (self.out[0, :self.blen].cpu().numpy().tobytes() == enc and
+                  (self.hashes[0].cpu().numpy().tobytes() == h if self.args.level & 4 else True))
         elif self.args.mode == "e2e-decode":
             ok = self.h_out[0, :self.n].numpy().tobytes() == sample
         else:
@@ -435,6 +457,8 @@ def main():
         traffic, traffic_src = measured_traffic(args.traffic_json, wl.kernel_sym, wl.alg_bytes)
         if args.mode == "bao":
             workload = f"bao encode, {args.objects} x {args.object_mib:g} MiB objects per GPU"
+        elif args.mode == "pipeline":
+            workload = f"encode() level {args.level}, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "e2e":
             workload = (f"encode() level {args.level} host->HBM->host (pinned), {args.objects} x "
                         f"{args.object_mib:g} MiB objects per GPU")
@@ -472,11 +496,12 @@ def main():
                                     "frac": round(achieved / 126.0, 4),
                                     "note": "PCIe Gen5 x16, 63 GB/s per direction (spec), H2D and D2H overlapped"})
             res["data"] = "synthetic (uniform random bytes), pinned host buffers"
-        if args.mode == "bao":
+        if args.mode == "bao" or (args.mode == "pipeline" and args.level & 4):
             # BLAKE3 compressions: one per 64-B block of content plus one per parent node;
             # 7 rounds x 8 G x 12 VALU lane-ops (a+b+m as one v_add3_u32).
-            chunks = max(1, -(-n // 1024))
-            comps = args.objects * (max(1, -(-n // 64)) + (chunks - 1))
+            hashed = wl.zlen if args.mode == "pipeline" else n
+            chunks = max(1, -(-hashed // 1024))
+            comps = args.objects * (max(1, -(-hashed // 64)) + (chunks - 1))
             ops = comps * 7 * 8 * 12
             tops = ops / (avg_ms * 1e-3) / 1e12
             hbm = res["roofline"]
@@ -486,7 +511,9 @@ def main():
                                "alg_ops_per_launch": ops, "hbm_achieved_GBps": hbm["achieved"],
                                "avg_launch_ms": hbm["avg_launch_ms"], "min_launch_ms": hbm["min_launch_ms"],
                                "note": "int32 VALU peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; ops = 672 per "
-                                       "BLAKE3 compression (content blocks + parents)"}
+                                       "BLAKE3 compression (content blocks + parents)"
+                                       + ("; step = zfec kernel (HBM-bound) + bao kernels (VALU-bound), "
+                                          "achieved over the whole step" if args.mode == "pipeline" else "")}
         if verified_all is not None:
             res["verified_all_objects"] = verified_all
         if aliased is not None:

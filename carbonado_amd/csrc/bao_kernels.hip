@@ -31,6 +31,9 @@
 #include "bao_device.hpp"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <vector>
 
 namespace chip {
 
@@ -87,6 +90,37 @@ hipError_t bao_gather_content(const uint8_t *d_stream, uint64_t n, uint64_t c0, 
     blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
     hipLaunchKernelGGL(bao_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d_stream, n, N, c0, c1, d_out);
     return hipGetLastError();
+}
+
+hipError_t bao_encode_inplace_dev(uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count, uint8_t *d_hash,
+                                  void *d_scratch, hipStream_t stream) {
+    return run_bao_t<3, BAO_CPL, BAO_NTS, 0>(d_stream, stride, n, count, d_stream, stride, d_hash, nullptr,
+                                             d_scratch, stream);
+}
+
+namespace {
+std::mutex g_tab_mu;
+std::map<uint64_t, uint64_t *> g_chunk_tabs;  // N -> device table [N] of chunk stream offsets
+}  // namespace
+
+hipError_t bao_chunk_table(uint64_t N, const uint64_t **out) {
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    auto it = g_chunk_tabs.find(N);
+    if (it != g_chunk_tabs.end()) { *out = it->second; return hipSuccess; }
+    std::vector<uint64_t> h(N);
+    uint64_t off = chunk_stream_off(0, N);
+    for (uint64_t i = 0; i < N; ++i) {  // P and c advance incrementally: 1024 + 64 c(i) per chunk
+        if (i) off += 1024 + 64 * (uint64_t)parents_at(i, N);
+        h[i] = off;
+    }
+    uint64_t *d = nullptr;
+    hipError_t e = hipMalloc(&d, N * 8);
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(d, h.data(), N * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(d); return e; }
+    g_chunk_tabs[N] = d;
+    *out = d;
+    return hipSuccess;
 }
 
 uint64_t bao_chunk_offset(uint64_t i, uint64_t N) { return chunk_stream_off(i, N); }

@@ -192,6 +192,28 @@ GfPlan encode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint8_t
     return p;
 }
 
+// encode() with Zfec and Bao (encoding.rs:121-147) without the intermediate
+// zfec buffer: K1 writes the FEC_M shards of each object straight into their
+// chunk slots of the object's bao stream (GfLaunch::bao_off), then K3/K4 hash
+// that stream in place (header, parent nodes, hash).  HBM traffic per object:
+// n read + m*C written by K1, m*C read + the parents written by K3/K4 (vs an
+// extra m*C written and read through a zfec buffer).  C % 1024 == 0 always
+// (calc_padding_len pads to a multiple of 1024*k).
+hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
+                        uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s) {
+    const uint64_t zlen = (uint64_t)CHIP_FEC_M * C;
+    const uint64_t *tab = nullptr;
+    hipError_t e = bao_chunk_table(zlen / 1024, &tab);
+    if (e != hipSuccess) return e;
+    static const std::vector<uint8_t> enc = zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M);
+    const GfPlan p = encode_plan(CHIP_FEC_K, CHIP_FEC_M, C, enc);
+    GfLaunch L{d_in, d_out, in_stride, out_stride, n, C, count};
+    L.bao_off = tab;
+    e = gf_apply(p, L, s);
+    if (e != hipSuccess) return e;
+    return bao_encode_inplace_dev(d_out, out_stride, zlen, count, d_hash, d_scratch, s);
+}
+
 // decode plan for k selected shares (slot s holds share sel[s], stored at
 // in_off[s]); output rows 0..k-1 at r*C
 int decode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint32_t> &sel,
@@ -641,6 +663,55 @@ int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     return CHIP_OK;
 }
 
+uint64_t chip_encode_scratch_len(uint8_t format, uint64_t n, uint64_t count) {
+    chip_encode_info inf;
+    uint64_t zlen, fl;
+    if (encode_info_for(format, n, n, 0, 0, &inf, &zlen, &fl) != CHIP_OK) return 16;
+    return (format & CHIP_FORMAT_BAO) ? bao_scratch_len(zlen, count) + 16 : 16;
+}
+
+int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                          uint8_t *d_out, uint64_t out_stride, uint64_t *out_len, uint8_t *d_hash,
+                          chip_encode_info *info, void *d_scratch, void *stream) {
+    if (has_host_stages(format) || format > 15) return CHIP_ERR_INVALID_ARG;
+    if ((!d_in && n) || !out_len || (!d_hash && count) || (in_stride % 16) || (out_stride % 16) ||
+        misaligned16(d_in) || misaligned16(d_out))
+        return CHIP_ERR_INVALID_ARG;
+    chip_encode_info inf;
+    uint64_t zlen, fl;
+    int st = encode_info_for(format, n, n, 0, 0, &inf, &zlen, &fl);
+    if (st != CHIP_OK) return st;
+    if ((fl && !d_out) || (count > 1 && out_stride < fl)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
+    if (bao && !d_scratch) return CHIP_ERR_INVALID_ARG;
+    *out_len = fl;
+    if (info) *info = inf;
+    if (count == 0) return CHIP_OK;
+    st = ensure_device();
+    if (st != CHIP_OK) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (zfec && bao && zlen) {
+        CHIP_HIP(zfec_bao_dev(d_in, in_stride, n, count, inf.chunk_len, d_out, out_stride, d_hash, d_scratch, s));
+    } else if (zfec) {
+        if (zlen) {
+            const GfPlan p = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M));
+            GfLaunch L{d_in, d_out, in_stride, out_stride, n, inf.chunk_len, count};
+            CHIP_HIP(gf_apply(p, L, s));
+        }
+        if (bao)  // empty input: bao of the empty zfec output
+            CHIP_HIP(bao_encode_dev(d_in, in_stride, 0, count, d_out, out_stride, d_hash, d_scratch, s));
+        else
+            CHIP_HIP(hipMemsetAsync(d_hash, 0, 32 * count, s));
+    } else if (bao) {
+        CHIP_HIP(bao_encode_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_scratch, s));
+    } else {  // no device stage: the encoding is the input
+        if (n) CHIP_HIP(hipMemcpy2DAsync(d_out, count > 1 ? out_stride : n, d_in, count > 1 ? in_stride : n, n, count,
+                                         hipMemcpyDeviceToDevice, s));
+        CHIP_HIP(hipMemsetAsync(d_hash, 0, 32 * count, s));
+    }
+    return CHIP_OK;
+}
+
 // bao-encode `n` device bytes into c->out; hash to host
 static int bao_encode_ctx(Ctx *c, const uint8_t *d_in, uint64_t n, bool want_stream,
                           uint8_t hash[32]) {
@@ -943,6 +1014,20 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
         CHIP_HIP(grow(c->in, cur_n));
         if (cur_n) CHIP_HIP(hipMemcpyAsync(c->in.p, cur, cur_n, hipMemcpyHostToDevice, c->stream));
         const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
+        if (zfec && bao && cur_len) {  // fused: shards written into the bao stream, hashed in place
+            CHIP_HIP(grow(c->out, final_len));
+            CHIP_HIP(grow(c->scratch, bao_scratch_len(cur_len, 1)));
+            CHIP_HIP(grow(c->small, 64));
+            uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
+            CHIP_HIP(zfec_bao_dev(d_cur, 0, cur_n, 1, inf.chunk_len, static_cast<uint8_t *>(c->out.p), 0, d_hash,
+                                  c->scratch.p, c->stream));
+            CHIP_HIP(hipMemcpyAsync(hash, d_hash, 32, hipMemcpyDeviceToHost, c->stream));
+            CHIP_HIP(hipMemcpyAsync(out, c->out.p, final_len, hipMemcpyDeviceToHost, c->stream));
+            CHIP_HIP(hipStreamSynchronize(c->stream));
+            *out_len = final_len;
+            if (info) *info = inf;
+            return CHIP_OK;
+        }
         if (zfec && cur_len) {
             CHIP_HIP(grow(c->mid, cur_len));
             GfPlan p = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M));
@@ -979,6 +1064,15 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
         CHIP_HIP(hipMemcpy2DAsync(d_in, n_al, src, src_pitch, cur_n, cnt, hipMemcpyHostToDevice, sl.stream));
     const uint8_t *d_cur = d_in;
     uint64_t cur_stride = n_al;
+    if (zfec && bao && zlen) {  // fused: shards written into the bao streams, hashed in place
+        CHIP_HIP(zfec_bao_dev(d_in, n_al, cur_n, cnt, inf.chunk_len, static_cast<uint8_t *>(sl.out.p), f_al,
+                              static_cast<uint8_t *>(sl.hash.p), sl.scratch.p, sl.stream));
+        CHIP_HIP(hipMemcpyAsync(hashes, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, sl.stream));
+        if (final_len)
+            CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, sl.out.p, f_al, final_len, cnt, hipMemcpyDeviceToHost,
+                                      sl.stream));
+        return CHIP_OK;
+    }
     if (zfec) {
         GfLaunch L{d_in, static_cast<uint8_t *>(sl.mid.p), n_al, z_al, cur_n, inf.chunk_len, cnt};
         CHIP_HIP(gf_apply(*plan, L, sl.stream));
@@ -1058,7 +1152,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             Slot &sl = c->slots[k];
             if (!sl.stream) CHIP_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
             CHIP_HIP(grow(sl.in, S * h_al));
-            if (zfec) CHIP_HIP(grow(sl.mid, S * ((zlen_max + 15) / 16 * 16)));
+            if (zfec && !bao) CHIP_HIP(grow(sl.mid, S * ((zlen_max + 15) / 16 * 16)));  // Zfec|Bao: fused
             if (bao) {
                 CHIP_HIP(grow(sl.out, S * ((final_max + 15) / 16 * 16)));
                 CHIP_HIP(grow(sl.scratch, bao_scratch_len(zlen_max, S)));

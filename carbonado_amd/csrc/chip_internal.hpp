@@ -51,6 +51,9 @@ struct GfLaunch {
     uint64_t valid;   // bytes of each input object that are data (rest reads as 0)
     uint64_t C;       // shard length (multiple of 16)
     uint64_t count;   // objects
+    // optional: write the shard-major output in bao layout (encode() with
+    // Zfec|Bao): stream offset of each 1 KiB content chunk, device table
+    const uint64_t *bao_off = nullptr;
 };
 
 // Enqueue the matrix apply.  Tables are cached device-side per plan key.
@@ -69,6 +72,14 @@ hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
 hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                           const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                           uint32_t *d_status, void *d_scratch, hipStream_t stream);
+
+// bao encode in place: the stream's chunk slots already hold the content
+// (written there by gf_apply with GfLaunch::bao_off); writes the header, the
+// parent nodes and the hashes.
+hipError_t bao_encode_inplace_dev(uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count, uint8_t *d_hash,
+                                  void *d_scratch, hipStream_t stream);
+// Cached device table [N] of the stream offsets of the N content chunks.
+hipError_t bao_chunk_table(uint64_t N, const uint64_t **out);
 
 // Per-node bao verification (K5b): chunk_flags [count][N], parent_flags
 // [count][N-1] in stream order; 1 = the node matches the copy stored in its

@@ -26,6 +26,8 @@ struct ApplyArgs {
     uint64_t tiles_per_obj, total_tiles, count;
     uint64_t chunk;                    // MAP 3: tiles per XCD-grouped run (>= 1)
     const void *table;                 // [K][256] entries of NG dwords
+    const uint64_t *bao_off;           // BL: stream offset of each 1 KiB chunk of the shard-major output
+    uint64_t bao_n;                    // BL: number of chunks (bao_off entries)
     uint64_t in_off[ZF_MAXK];
     uint64_t copy_off[ZF_MAXK];
     uint64_t par_off[ZF_MAXP];
@@ -65,6 +67,64 @@ template <bool NT>
 __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) {
     if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
     else *reinterpret_cast<u32x4 *>(p) = v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void store8z(uint8_t *p, u32x2 v) {
+    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x2 *>(p));
+    else *reinterpret_cast<u32x2 *>(p) = v;
+}
+
+// Store the 16 B of output byte offset p (shard-major layout).  BL (bao
+// layout, encode() with Zfec|Bao): the output is a bao stream and shard byte p
+// lives in content chunk p >> 10 at bao_off[p >> 10] + (p & 1023).  A wave's
+// 64 lanes hold one whole chunk (TILE = 4 waves x 1 KiB, C % 1024 == 0), so
+// the chunk index is wave-uniform; slots sit at 8 (mod 16) for a 16-B aligned
+// stream base, so lane l stores the ALIGNED 16 B [16 l + 8, +16) = its upper
+// half + lane l+1's lower half (DPP wave_shl:1; lane 63 gets zeros).
+// Memory lines are written whole: the parent slots around a chunk (filled
+// by the bao kernel later) are written as zeros here, so a line shared by a
+// chunk and a parent is not left half-written (a half-written line costs a
+// read-modify-write at the memory side).  Chunk ci with c = its parents
+// before it: lanes 0..4c-1 store [d - 64c + 8 + 16 l, +16) (zeros, the last
+// one carrying the chunk's first 8 bytes); a chunk followed by parents lets
+// lane 63 store {tail, 0, 0} within the body store; otherwise the 8-B head /
+// tail go alone (their line is completed by the neighbouring chunk's wave).
+template <bool NT, bool BL>
+__device__ __forceinline__ void put16(const ApplyArgs &a, uint8_t *ob, uint64_t p, u32x4 v) {
+    if constexpr (!BL) {
+        store16<NT>(ob + p, v);
+    } else {
+        const uint32_t ci = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 10));
+        // constant address space: scalar loads (lgkmcnt), which do not wait for this
+        // wave's outstanding stores the way a vector load's vmcnt(0) would
+        typedef const __attribute__((address_space(4))) uint64_t *ctab_t;
+        const ctab_t tab = (ctab_t)a.bao_off;
+        const uint64_t off = tab[ci];
+        uint8_t *d = ob + off;
+        const int lane = threadIdx.x & 63;
+        const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v.x, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        const uint32_t ny = __builtin_amdgcn_update_dpp(0u, v.y, 0x130, 0xF, 0xF, false);
+        if (((uintptr_t)d & 15) != 8) {  // 8-B aligned stream base: slots are 16-B aligned
+            store16<NT>(d + 16 * lane, v);
+            return;
+        }
+        const uint32_t cprev = (uint32_t)((ci == 0 ? off - 8 : off - tab[ci - 1] - 1024) >> 6);
+        const bool par_after = ci + 1 < a.bao_n && tab[ci + 1] != off + 1024;
+        if (lane < 63 || par_after) store16<NT>(d + 16 * lane + 8, u32x4{v.z, v.w, nx, ny});
+        else store8z<NT>(d + 1016, u32x2{v.z, v.w});
+        if (cprev) {
+            const uint32_t hx = __builtin_amdgcn_readfirstlane(v.x), hy = __builtin_amdgcn_readfirstlane(v.y);
+            const uint32_t last = 4 * cprev - 1;  // pieces before the chunk's first 8 bytes
+            for (uint32_t b = 0; b <= last; b += 64) {  // > 64 pieces only past 16 parents (N > 2^16)
+                const uint32_t t = b + (uint32_t)lane;
+                if (t < last) store16<NT>(d - 64 * cprev + 8 + 16 * t, u32x4{0u, 0u, 0u, 0u});
+                else if (t == last) store16<NT>(d - 8, u32x4{0u, 0u, hx, hy});
+            }
+        } else if (lane == 0) {
+            store8z<NT>(d, u32x2{v.x, v.y});
+        }
+    }
 }
 
 // rows[q] = byte q of a0..a3 (4x4 byte transpose, 8 v_perm_b32)
@@ -137,7 +197,7 @@ struct TileIter {
 // super-tile's shards before computing the current one, NTL: nontemporal
 // input loads — tools/zfec_tune.
 template <int K, int NG, int U, int MAP, bool NT, int RO = 0, int WPE = 1, int SB = 0, bool PF = false,
-          bool NTL = false>
+          bool NTL = false, bool BL = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_kernel(ApplyArgs a) {
     constexpr int R = RO ? RO : replicas_for(K);
     using E = typename Entry<NG>::T;
@@ -233,9 +293,24 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
 
             // copies (data shards for encode, surviving primaries for decode)
+            if constexpr (BL) {
+                // bao layout needs a wave-uniform chunk per store: store shard s
+                // from every lane at once (lane group grp holds it in slot (s - grp) mod K)
 #pragma unroll
-            for (int j = 0; j < K; ++j)
-                if (coff[j] != NO_OUT) store16<NT>(ob + coff[j] + col, v[u][j]);
+                for (int sh = 0; sh < K; ++sh) {
+                    if (a.copy_off[sh] == NO_OUT) continue;
+                    const int jj = (sh - grp + K) % K;
+                    u32x4 w = v[u][0];
+#pragma unroll
+                    for (int j = 1; j < K; ++j)
+                        if (jj == j) w = v[u][j];
+                    put16<NT, true>(a, ob, a.copy_off[sh] + col, w);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    if (coff[j] != NO_OUT) store16<NT>(ob + coff[j] + col, v[u][j]);
+            }
 
             // computed rows: transpose column-packed sums into row streams
 #pragma unroll
@@ -257,7 +332,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     const uint64_t po = a.par_off[g * 4 + q];
                     if (po == NO_OUT) continue;
                     u32x4 o = {rows[q][0], rows[q][1], rows[q][2], rows[q][3]};
-                    store16<NT>(ob + po + col, o);
+                    put16<NT, BL>(a, ob, po + col, o);
                 }
             }
         }

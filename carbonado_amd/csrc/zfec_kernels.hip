@@ -104,6 +104,7 @@ constexpr uint64_t ZF_CHUNK = 64;
 // occupancy 4, on two boxes.
 struct KernelInfo {
     KernelFn fn;
+    KernelFn fn_bl;  // same schedule, output in bao layout (GfLaunch::bao_off); null = unsupported shape
     size_t lds;
     int grid;
     int u;        // column tiles per super-tile (the kernel's U)
@@ -118,6 +119,7 @@ KernelInfo make_info() {
     ki.grid = 0;
     ki.u = 1;
     ki.bpc_cap = 0;
+    ki.fn_bl = nullptr;
     if constexpr (K > 4) {
         ki.fn = gf_apply_kernel<K, NG, ZF_U, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
     } else if constexpr (K == 4 && NG == 1) {
@@ -126,6 +128,7 @@ KernelInfo make_info() {
             ki.fn = gf_apply_kernel<4, 1, 1, ZF_MAP, ZF_NT>;
         } else {
             ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true>;
+            ki.fn_bl = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true, false, true>;
             ki.u = 2;
             ki.bpc_cap = 2;
         }
@@ -264,6 +267,13 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     std::memset(&a, 0, sizeof a);
     a.in = L.in; a.out = L.out;
     a.in_stride = L.in_stride; a.out_stride = L.out_stride;
+    a.bao_off = L.bao_off;
+    a.bao_n = L.bao_off ? (L.C / 1024) * (p.k + p.np) : 0;  // m*C/1024 chunks
+    KernelFn fn = ki.fn;
+    if (L.bao_off) {  // bao layout: whole 1 KiB chunks per wave, one pass (copies + all computed rows)
+        if (!ki.fn_bl || L.C % 1024 || !copies || row0 + nrows != p.np) return hipErrorInvalidValue;
+        fn = ki.fn_bl;
+    }
     a.valid = L.valid; a.C = L.C;
     a.tiles_per_obj = (L.C + TILE - 1) / TILE;
     a.total_tiles = a.tiles_per_obj * L.count;
@@ -288,7 +298,7 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     const uint64_t per_wg = units / (grid ? grid : 1);
     const uint64_t run = ZF_CHUNK / ki.u;
     a.chunk = per_wg < 1 ? 1 : (per_wg < run ? per_wg : run);
-    hipLaunchKernelGGL(ki.fn, dim3((unsigned)grid), dim3(TPB), ki.lds, stream, a);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(TPB), ki.lds, stream, a);
     return hipGetLastError();
 }
 

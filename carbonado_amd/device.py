@@ -60,6 +60,29 @@ def bao_encode_batch(inp: torch.Tensor, n: int, out: torch.Tensor | None, hashes
         out.shape[1] if out is not None else 0, _p(hashes), _p(scratch), _stream()))
 
 
+def encode_scratch(fmt: int, n: int, count: int, device=None) -> torch.Tensor:
+    size = _lib.lib().chip_encode_scratch_len(fmt, n, count)
+    return torch.empty(size, dtype=torch.uint8, device=device or "cuda")
+
+
+def encode_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes: torch.Tensor,
+                 scratch: torch.Tensor):
+    """encode() of device-resident objects at a level without host stages
+    (Bao and/or Zfec bits): inp uint8 [count, in_stride] (first n bytes of each
+    row), out uint8 [count, >= encoded length], hashes uint8 [count, 32].
+    Zfec|Bao runs fused (shards written straight into the bao streams).
+    Returns (encoded length, EncodeInfoC)."""
+    assert inp.is_cuda and out.is_cuda and inp.is_contiguous() and out.is_contiguous()
+    assert inp.shape[0] == out.shape[0] == hashes.shape[0] and inp.shape[1] >= n
+    olen = ctypes.c_uint64()
+    info = _lib.EncodeInfoC()
+    check(_lib.lib().chip_encode_batch_dev(fmt, _p(inp), inp.shape[1], n, inp.shape[0], _p(out), out.shape[1],
+                                           ctypes.byref(olen), _p(hashes), ctypes.byref(info), _p(scratch),
+                                           _stream()))
+    assert olen.value <= out.shape[1]
+    return olen.value, info
+
+
 def bao_decode_batch(enc: torch.Tensor, n: int, hashes: torch.Tensor, out: torch.Tensor,
                      status: torch.Tensor, scratch: torch.Tensor) -> None:
     """status: int32/uint32 [count]; 0 = verified, 5 = hash mismatch."""

@@ -58,7 +58,7 @@ extern "C" {
 #define CHIP_API
 #endif
 
-#define CHIP_ABI_VERSION 2
+#define CHIP_ABI_VERSION 3
 #define CHIP_HASH_LEN 32   /* bao::HASH_SIZE */
 #define CHIP_SLICE_LEN 1024 /* constants.rs:9 SLICE_LEN */
 #define CHIP_FEC_K 4        /* constants.rs:11 FEC_K */
@@ -253,6 +253,24 @@ CHIP_API int chip_bao_encode_batch_dev(const uint8_t *d_in, uint64_t in_stride, 
 CHIP_API int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                               const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                               uint32_t *d_status, void *d_scratch, void *stream);
+
+/* encode() (encoding.rs:86-172) of `count` DEVICE-resident objects for the
+ * formats whose stages all run on the device (Bao and/or Zfec bits only;
+ * Snappy/Ecies bits give CHIP_ERR_INVALID_ARG — they are host stages, see
+ * chip_encode_host_batch).  Object o: n bytes at d_in + o*in_stride; its
+ * encoding (*out_len bytes, the same for every object) at d_out +
+ * o*out_stride, its hash at d_hash + 32*o (zeros without Bao,
+ * encoding.rs:145), *info = its EncodeInfo (may be NULL).  Zfec|Bao runs
+ * fused: the zfec kernel writes the 8 shards straight into their chunk slots
+ * of the bao stream, which is then hashed in place (no zfec buffer).
+ * d_scratch: chip_encode_scratch_len(format, n, count) bytes.  Pointers and
+ * strides must be multiples of 16; enqueued on `stream`, not synchronised.
+ * Replaces, for these levels, encode() = zfec (encoding.rs:121-138) -> bao
+ * (encoding.rs:140-147) in one call per batch. */
+CHIP_API uint64_t chip_encode_scratch_len(uint8_t format, uint64_t n, uint64_t count);
+CHIP_API int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_stride, uint64_t n,
+                                   uint64_t count, uint8_t *d_out, uint64_t out_stride, uint64_t *out_len,
+                                   uint8_t *d_hash, chip_encode_info *info, void *d_scratch, void *stream);
 
 /* ---- slices and scrub (decoding.rs:116-212) ----------------------------- */
 /* Chunk range of a bao slice request [start, start+len) over n content bytes,

@@ -249,3 +249,45 @@ def test_decode_host_batch_roundtrip(gpu, level):
         assert st[2] == 5 and st[:2] == [0, 0] and st[3:] == [0] * (count - 3)
         for o in (0, 1, 3):
             assert out[o, :n].numpy().tobytes() == rows[o].tobytes()
+
+
+@pytest.mark.parametrize("n", [0, 1, 4096, 12_288, 70_001, (1 << 20) + 1, 3 << 20])
+@pytest.mark.parametrize("level", [0, 4, 8, 12])
+def test_encode_batch_dev(gpu, level, n):
+    """chip_encode_batch_dev (device-resident encode(); Zfec|Bao fused: shards
+    written straight into the bao stream, hashed in place) == encode() of the
+    oracle per object.  n = 12 KiB gives N = 24 chunks (not a power of two)."""
+    import torch
+    from carbonado_amd import device
+    count = 5
+    rng = np.random.default_rng(1000 * level + n % 997)
+    stride = (n + 16 + 15) // 16 * 16
+    host = rng.integers(0, 256, (count, stride), dtype=np.uint8)
+    inp = torch.from_numpy(host).cuda()
+    oenc0, _, _ = O.encode(host[0, :n].tobytes(), level)
+    ostride = (len(oenc0) + 48 + 15) // 16 * 16
+    out = torch.full((count, ostride), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.full((count, 32), 0x5A, dtype=torch.uint8, device="cuda")
+    scratch = device.encode_scratch(level, n, count)
+    olen, info = device.encode_batch(level, inp, n, out, hashes, scratch)
+    torch.cuda.synchronize()
+    got, gh = out.cpu().numpy(), hashes.cpu().numpy()
+    for o in range(count):
+        enc, h, oinfo = O.encode(host[o, :n].tobytes(), level)
+        assert olen == len(enc)
+        assert got[o, :olen].tobytes() == enc, o
+        assert (got[o, olen:] == 0xA5).all(), "bytes past the encoding were written"
+        assert gh[o].tobytes() == (h if level & 4 else b"\0" * 32)
+    assert info.padding_len == oinfo["padding_len"] and info.output_len == olen
+
+
+def test_encode_batch_dev_rejects_host_stages(gpu):
+    import torch
+    from carbonado_amd import device
+    from carbonado_amd.error import CarbonadoError
+    inp = torch.zeros((2, 4096), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((2, 1 << 16), dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((2, 32), dtype=torch.uint8, device="cuda")
+    for level in (1, 2, 15):
+        with pytest.raises(CarbonadoError):
+            device.encode_batch(level, inp, 4096, out, hashes, device.encode_scratch(12, 4096, 2))

@@ -50,12 +50,12 @@ struct V {
     size_t pad_lds;
 };
 
-template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0>
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int CW = 0>
 V mk(bool stream, size_t pad_lds = 0) {
     char b[96];
-    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d pad%zu", MODE ? "decode" : "encode", CPL,
-             NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, pad_lds);
-    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE>, CPL, stream, pad_lds};
+    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d cw%d pad%zu", MODE ? "decode" : "encode", CPL,
+             NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, CW, pad_lds);
+    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE, CW>, CPL, stream, pad_lds};
 }
 
 int main(int argc, char **argv) {
@@ -74,10 +74,12 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&status, count * 4));
     CK(hipMalloc(&scratch, bao_scratch_len_t<1>(n, count)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xB1A3ull);
-    std::vector<V> vs = {mk<0, 8, false>(true),       mk<0, 2, false, 3>(true), mk<0, 1, false, 3>(true),
-                         mk<0, 4, false, 3>(true),    mk<0, 2, false>(true),    mk<0, 1, false>(true),
-                         mk<0, 2, false, 3, 2>(true), mk<0, 2, false>(false),   mk<0, 8, false>(false),
-                         mk<1, 8, false>(true),       mk<1, 2, false>(true)};
+    std::vector<V> vs = {mk<0, 2, false, 3>(true),             mk<0, 2, false, 4, 1, 0, 1>(true),
+                         mk<0, 2, false, 4, 1, 0, 2>(true),    mk<0, 2, false, 4, 1, 0, 4>(true),
+                         mk<0, 1, false, 4, 1, 0, 1>(true),    mk<0, 1, false, 4, 1, 0, 2>(true),
+                         mk<0, 2, true, 4, 1, 0, 2>(true),     mk<0, 2, false, 5, 1, 0, 4>(true),
+                         mk<0, 2, false>(false),               mk<0, 1, false>(false),
+                         mk<1, 2, false>(true)};
     if (argc > 4) {  // comma-separated subset of variant indices (profiling)
         std::vector<V> keep;
         std::string sel = argv[4];

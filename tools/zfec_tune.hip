@@ -12,6 +12,7 @@
 
 #include "../carbonado_amd/csrc/gf256.hpp"
 #include "../carbonado_amd/csrc/zfec_device.hpp"
+#include "../carbonado_amd/csrc/bao_device.hpp"
 
 using namespace chip;
 using namespace chip::zf;
@@ -51,14 +52,17 @@ struct Variant {
     int blocks_per_cu;
     int chunk;
     size_t lds;
+    bool bl = false;
 };
 
-template <int U, int MAP, bool NT, int CH = 1, int WPE = 1, int SB = 0, bool PF = false, bool NTL = false>
+template <int U, int MAP, bool NT, int CH = 1, int WPE = 1, int SB = 0, bool PF = false, bool NTL = false,
+          bool BL = false>
 Variant V(int bpc) {
     char buf[96];
-    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d wpe%d sb%d pf%d ntl%d %s bpc%d", U, MAP, CH, WPE, SB, PF, NTL,
-             NT ? "nt " : "pln", bpc);
-    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT, 0, WPE, SB, PF, NTL>, bpc, CH, (size_t)256 * 4 * 8 * 4};
+    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d wpe%d sb%d pf%d ntl%d %s bpc%d%s", U, MAP, CH, WPE, SB, PF, NTL,
+             NT ? "nt " : "pln", bpc, BL ? " BAO-LAYOUT" : "");
+    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT, 0, WPE, SB, PF, NTL, BL>, bpc, CH, (size_t)256 * 4 * 8 * 4,
+                   BL};
 }
 
 // 8-of-16 variants (K = 8, NG = 2), replica count R
@@ -77,7 +81,10 @@ int main(int argc, char **argv) {
     const uint64_t n = 16ull << 20, C = n / K;
     uint8_t *in, *out;
     CK(hipMalloc(&in, count * n));
-    CK(hipMalloc(&out, count * 2 * n));
+    // bao layout variants write a whole bao stream per object (8 + 2n + 64 (N - 1) bytes)
+    const uint64_t Nch = 2 * n / 1024;
+    const uint64_t blen = 8 + 2 * n + 64 * (Nch - 1), bstride = (blen + 255) / 256 * 256;
+    CK(hipMalloc(&out, count * (bstride > 2 * n ? bstride : 2 * n)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xCA4B0AD0ull);
     CK(hipMemset(out, 0, count * 2 * n));
 
@@ -94,6 +101,11 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&dtab, tab.size() * 4));
     CK(hipMemcpy(dtab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
 
+    std::vector<uint64_t> boff(Nch);
+    for (uint64_t i = 0; i < Nch; ++i) boff[i] = chip::bao::chunk_stream_off(i, Nch);
+    uint64_t *dboff;
+    CK(hipMalloc(&dboff, Nch * 8));
+    CK(hipMemcpy(dboff, boff.data(), Nch * 8, hipMemcpyHostToDevice));
     ApplyArgs a{};
     a.in = in; a.out = out; a.in_stride = n; a.out_stride = 2 * n; a.valid = n; a.C = C;
     a.tiles_per_obj = C / TILE; a.total_tiles = a.tiles_per_obj * count; a.count = count;
@@ -104,10 +116,9 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {V<1, 3, true, 64>(4),                       V<1, 3, true, 64, 1, 0, false, true>(4),
-              V<1, 3, false, 64, 1, 0, false, true>(4),   V<2, 3, true, 32, 2, 0, true>(2),
-              V<2, 3, true, 32, 2, 0, true, true>(2),     V<1, 3, true, 64, 2, 0, true, true>(2),
-              V<1, 1, true, 1, 1, 0, false, true>(4)};
+        vs = {V<2, 3, true, 32, 2, 0, true>(2),                     V<2, 3, true, 32, 2, 0, true, false, true>(2),
+              V<2, 3, false, 32, 2, 0, true, false, true>(2),       V<1, 3, true, 64, 1, 0, false, false, true>(4),
+              V<1, 3, false, 64, 1, 0, false, false, true>(4),      V<2, 3, true, 8, 2, 0, true, false, true>(2)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
@@ -124,7 +135,11 @@ int main(int argc, char **argv) {
         for (size_t v = 0; v < vs.size(); ++v) {
             const int grid = 256 * vs[v].blocks_per_cu;
             a.chunk = vs[v].chunk;
+            a.bao_off = vs[v].bl ? dboff : nullptr;
+            a.bao_n = Nch;
+            a.out_stride = vs[v].bl ? bstride : M * C;
             if (rd == 0) CK(hipMemset(out, 0, count * 2 * n));  // a variant that skips bytes fails the checksum
+            if (rd == 0 && vs[v].bl) CK(hipMemset(out, 0, count * bstride));
             hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(TPB), vs[v].lds, 0, a);  // warm
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(TPB), vs[v].lds, 0, a);
@@ -140,7 +155,7 @@ int main(int argc, char **argv) {
                 unsigned long long h;
                 CK(hipMemcpy(&h, dsum, 8, hipMemcpyDeviceToHost));
                 if (v == 0) ref = h;
-                if (h != ref) printf("!! %s checksum mismatch\n", vs[v].name.c_str());
+                if (!vs[v].bl && h != ref) printf("!! %s checksum mismatch\n", vs[v].name.c_str());
             }
         }
     }
