@@ -100,12 +100,13 @@ hipError_t bao_encode_inplace_dev(uint8_t *d_stream, uint64_t stride, uint64_t n
 
 namespace {
 std::mutex g_tab_mu;
-std::map<uint64_t, uint64_t *> g_chunk_tabs;  // N -> device table [N] of chunk stream offsets
+std::map<std::pair<int, uint64_t>, uint64_t *> g_chunk_tabs;  // (device, N) -> table [N] of chunk stream offsets
 }  // namespace
 
 hipError_t bao_chunk_table(uint64_t N, const uint64_t **out) {
     std::lock_guard<std::mutex> lk(g_tab_mu);
-    auto it = g_chunk_tabs.find(N);
+    const std::pair<int, uint64_t> key(selected_device(), N);
+    auto it = g_chunk_tabs.find(key);
     if (it != g_chunk_tabs.end()) { *out = it->second; return hipSuccess; }
     std::vector<uint64_t> h(N);
     uint64_t off = chunk_stream_off(0, N);
@@ -118,7 +119,7 @@ hipError_t bao_chunk_table(uint64_t N, const uint64_t **out) {
     if (e != hipSuccess) return e;
     e = hipMemcpy(d, h.data(), N * 8, hipMemcpyHostToDevice);
     if (e != hipSuccess) { (void)hipFree(d); return e; }
-    g_chunk_tabs[N] = d;
+    g_chunk_tabs[key] = d;
     *out = d;
     return hipSuccess;
 }

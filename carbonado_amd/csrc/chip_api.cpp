@@ -29,27 +29,42 @@ namespace chip {
 namespace {
 
 std::once_flag g_dev_once;
-int g_device = -1;
-int g_cus = 0;
+std::atomic<int> g_device{-1};  // the process's device (one GPU per process, see chip_init)
+std::atomic<int> g_cus{0};
 int g_dev_status = CHIP_ERR_NO_DEVICE;
 thread_local std::string t_last_err;
 
+bool is_gfx950(int d, int *cus) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) != hipSuccess) return false;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return false;
+    if (cus) *cus = prop.multiProcessorCount;
+    return true;
+}
+
+// Default device: the caller's current HIP device when it is a gfx950 (so a
+// process that selected its GPU first, e.g. torch.cuda.set_device(local_rank),
+// is followed), else the first gfx950.  chip_init(d) selects explicitly.
 void init_device_once() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
         t_last_err = "no HIP device visible";
         return;
     }
-    for (int d = 0; d < n; ++d) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
-        if (std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) {
+    int cur = -1, cus = 0;
+    if (hipGetDevice(&cur) == hipSuccess && cur >= 0 && cur < n && is_gfx950(cur, &cus)) {
+        g_device = cur;
+        g_cus = cus;
+        g_dev_status = CHIP_OK;
+        return;
+    }
+    for (int d = 0; d < n; ++d)
+        if (is_gfx950(d, &cus)) {
             g_device = d;
-            g_cus = prop.multiProcessorCount;
+            g_cus = cus;
             g_dev_status = CHIP_OK;
             return;
         }
-    }
     t_last_err = "no gfx950 device visible";
 }
 
@@ -68,21 +83,28 @@ struct Slot {
 
 struct Ctx {
     bool ready = false;
+    int dev = -1;  // device the stream and buffers live on
     hipStream_t stream = nullptr;
     DevBuf in, mid, out, scratch, small, x1, x2, flags;
     std::vector<Slot> slots;
-    ~Ctx() {
-        // process teardown: the runtime may already be gone; best effort
-        for (DevBuf *b : {&in, &mid, &out, &scratch, &small, &x1, &x2, &flags})
+    void release() {
+        // best effort (at process teardown the runtime may already be gone)
+        for (DevBuf *b : {&in, &mid, &out, &scratch, &small, &x1, &x2, &flags}) {
             if (b->p) (void)hipFree(b->p);
+            *b = DevBuf{};
+        }
         if (stream) (void)hipStreamDestroy(stream);
+        stream = nullptr;
         for (Slot &sl : slots) {
             for (DevBuf *b : {&sl.in, &sl.mid, &sl.out, &sl.hash, &sl.scratch})
                 if (b->p) (void)hipFree(b->p);
             if (sl.stage.p) (void)hipHostFree(sl.stage.p);
             if (sl.stream) (void)hipStreamDestroy(sl.stream);
         }
+        slots.clear();
+        ready = false;
     }
+    ~Ctx() { release(); }
 };
 
 thread_local Ctx t_ctx;
@@ -129,7 +151,20 @@ int ensure_device() {
 
 void set_device_error(hipError_t e) { t_last_err = hipGetErrorString(e); }
 
-int num_cus() { return g_cus > 0 ? g_cus : 256; }
+int num_cus() { return g_cus > 0 ? g_cus.load() : 256; }
+
+int selected_device() { return g_device; }
+
+int use_device() {
+    int st = ensure_device();
+    if (st != CHIP_OK) return st;
+    hipError_t e = hipSetDevice(g_device);
+    if (e != hipSuccess) {
+        set_device_error(e);
+        return CHIP_ERR_DEVICE;
+    }
+    return CHIP_OK;
+}
 
 }  // namespace chip
 
@@ -150,12 +185,16 @@ int ctx_get(Ctx **out) {
     int st = ensure_device();
     if (st != CHIP_OK) return st;
     Ctx &c = t_ctx;
+    const int dev = g_device;
+    if (c.ready && c.dev != dev) {  // the process switched devices (chip_init): drop the old context
+        (void)hipSetDevice(c.dev);
+        c.release();
+    }
+    CHIP_HIP(hipSetDevice(dev));
     if (!c.ready) {
-        CHIP_HIP(hipSetDevice(g_device));
         CHIP_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        c.dev = dev;
         c.ready = true;
-    } else {
-        CHIP_HIP(hipSetDevice(g_device));
     }
     *out = &c;
     return CHIP_OK;
@@ -429,7 +468,17 @@ const char *chip_strerror(int st) {
 }
 
 int chip_init(int device) {
-    (void)device;
+    int st = ensure_device();
+    if (st != CHIP_OK) return st;
+    if (device >= 0) {
+        int n = 0, cus = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || device >= n || !is_gfx950(device, &cus)) {
+            t_last_err = "device " + std::to_string(device) + " is not a visible gfx950";
+            return CHIP_ERR_NO_DEVICE;
+        }
+        g_cus = cus;
+        g_device = device;
+    }
     Ctx *c;
     return ctx_get(&c);
 }
@@ -508,7 +557,7 @@ int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     if ((!d_in && n) || !d_out || (in_stride % 16) || (out_stride % 16) || misaligned16(d_in) ||
         misaligned16(d_out))
         return CHIP_ERR_INVALID_ARG;
-    int st = ensure_device();
+    int st = use_device();
     if (st != CHIP_OK) return st;
     uint32_t pad;
     uint64_t C;
@@ -623,7 +672,7 @@ int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     if (!d_in || !d_out || !idx || (in_stride % 16) || (out_stride % 16) || (chunk_len % 16) ||
         misaligned16(d_in) || misaligned16(d_out))
         return CHIP_ERR_INVALID_ARG;
-    int st = ensure_device();
+    int st = use_device();
     if (st != CHIP_OK) return st;
     std::vector<uint32_t> pos;
     st = select_shares(k, m, idx, nshares, &pos);
@@ -644,7 +693,7 @@ int chip_bao_encode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
                               uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash,
                               void *d_scratch, void *stream) {
     if ((!d_in && n) || !d_hash || !d_scratch) return CHIP_ERR_INVALID_ARG;
-    int st = ensure_device();
+    int st = use_device();
     if (st != CHIP_OK) return st;
     CHIP_HIP(bao_encode_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_scratch,
                             static_cast<hipStream_t>(stream)));
@@ -655,7 +704,7 @@ int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
                               const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                               uint32_t *d_status, void *d_scratch, void *stream) {
     if (!d_in || !d_hash || !d_status || !d_scratch || (!d_out && n)) return CHIP_ERR_INVALID_ARG;
-    int st = ensure_device();
+    int st = use_device();
     if (st != CHIP_OK) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
     CHIP_HIP(hipMemsetAsync(d_status, 0, count * sizeof(uint32_t), s));
@@ -687,7 +736,7 @@ int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_strid
     *out_len = fl;
     if (info) *info = inf;
     if (count == 0) return CHIP_OK;
-    st = ensure_device();
+    st = use_device();
     if (st != CHIP_OK) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (zfec && bao && zlen) {
@@ -1463,7 +1512,7 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
     bool abort_run = false;
     std::string fin_err;
     std::thread finisher([&] {
-        (void)hipSetDevice(g_device);
+        (void)hipSetDevice(c->dev);
         for (uint64_t i = 0; i < nslices; ++i) {
             {
                 std::unique_lock<std::mutex> lk(fm);

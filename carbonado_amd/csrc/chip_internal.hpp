@@ -96,6 +96,8 @@ uint64_t bao_parent_index(uint64_t s, int level, uint64_t N);
 
 // ---- context ------------------------------------------------------------
 int ensure_device();                 // CHIP_OK or CHIP_ERR_NO_DEVICE
+int use_device();                    // ensure_device() + make the process's device current
+int selected_device();               // the process's device (chip_init / default)
 void set_device_error(hipError_t e); // remember for chip_last_device_error
 int num_cus();
 

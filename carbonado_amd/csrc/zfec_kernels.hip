@@ -157,9 +157,9 @@ struct DevTable {
 };
 
 std::mutex g_mu;
-std::map<std::vector<uint8_t>, DevTable> g_tables;  // key: k, ng, coef bytes
+std::map<std::vector<uint8_t>, DevTable> g_tables;  // key: device, k, ng, coef bytes
 std::map<std::pair<KernelFn, size_t>, int> g_grid;
-uint8_t *g_multab = nullptr;
+std::map<int, uint8_t *> g_multab;                  // per device
 
 int grid_for(const KernelInfo &ki) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -181,6 +181,7 @@ int grid_for(const KernelInfo &ki) {
 // dword g = coef[4g+q][s] * x.
 hipError_t device_table(const GfPlan &p, int ng, const void **out) {
     std::vector<uint8_t> key;
+    key.push_back((uint8_t)selected_device());  // device-side tables live on the process's device
     key.push_back((uint8_t)p.k);
     key.push_back((uint8_t)ng);
     key.insert(key.end(), p.coef.begin(), p.coef.end());
@@ -208,17 +209,20 @@ hipError_t device_table(const GfPlan &p, int ng, const void **out) {
 
 hipError_t multab_device(const uint8_t **out) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_multab) {
+    uint8_t *&mt = g_multab[selected_device()];
+    if (!mt) {
         const Gf256 &gf = Gf256::get();
         std::vector<uint8_t> h(65536);
         for (int a = 0; a < 256; ++a)
             for (int b = 0; b < 256; ++b) h[a * 256 + b] = gf.mul((uint8_t)a, (uint8_t)b);
-        hipError_t e = hipMalloc(&g_multab, 65536);
+        uint8_t *d = nullptr;
+        hipError_t e = hipMalloc(&d, 65536);
         if (e != hipSuccess) return e;
-        e = hipMemcpy(g_multab, h.data(), 65536, hipMemcpyHostToDevice);
-        if (e != hipSuccess) return e;
+        e = hipMemcpy(d, h.data(), 65536, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { (void)hipFree(d); return e; }
+        mt = d;
     }
-    *out = g_multab;
+    *out = mt;
     return hipSuccess;
 }
 

@@ -291,3 +291,21 @@ def test_encode_batch_dev_rejects_host_stages(gpu):
     for level in (1, 2, 15):
         with pytest.raises(CarbonadoError):
             device.encode_batch(level, inp, 4096, out, hashes, device.encode_scratch(12, 4096, 2))
+
+
+def test_chip_init_selects_the_process_device(gpu):
+    """One process per GPU (bench.py --gpus N): chip_init(d) selects device d
+    for every later call; a device that is not a visible gfx950 is refused
+    without changing the selection."""
+    import torch
+    from carbonado_amd import _lib
+    L = _lib.lib()
+    n = torch.cuda.device_count()
+    assert L.chip_init(n) != 0  # one past the last visible device
+    assert L.chip_init(n - 1) == 0
+    assert L.chip_init(-1) == 0  # keep the current selection
+    d = np.random.default_rng(7).integers(0, 256, 50_000, dtype=np.uint8).tobytes()
+    import carbonado_amd as ca
+    enc, h, _ = ca.encode(b"", d, 12)
+    assert (enc, h) == O.encode(d, 12)[:2]
+    assert L.chip_init(0) == 0

@@ -116,9 +116,10 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {V<2, 3, true, 32, 2, 0, true>(2),                     V<2, 3, true, 32, 2, 0, true, false, true>(2),
-              V<2, 3, false, 32, 2, 0, true, false, true>(2),       V<1, 3, true, 64, 1, 0, false, false, true>(4),
-              V<1, 3, false, 64, 1, 0, false, false, true>(4),      V<2, 3, true, 8, 2, 0, true, false, true>(2)};
+        vs = {V<2, 3, true, 32, 2, 0, true>(2),  V<1, 3, true, 64, 1, 0, true>(4),  V<1, 3, true, 64, 4, 0, true>(4),
+              V<1, 3, true, 64, 1, 0, true>(6),  V<1, 3, true, 64, 1, 0, true>(8),  V<1, 3, true, 32, 1, 0, true>(4),
+              V<1, 3, true, 128, 1, 0, true>(4), V<2, 3, true, 32, 2, 0, true>(4),  V<2, 3, true, 32, 2, 0, true>(3),
+              V<1, 3, true, 64, 3, 0, true>(4),  V<1, 3, true, 64, 1, 0, true>(3),  V<1, 3, true, 64, 1, 0, true, true>(4)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
