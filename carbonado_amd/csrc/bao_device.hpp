@@ -435,9 +435,33 @@ __global__ __launch_bounds__(64 * (K3_WAVES + CW)) void bao_chunk_kernel(ChunkAr
         flag_mismatch(a.status, obj);  // header disagrees with the batch's content length
     wave_sync();
 
+    // Fast path: every chunk of this wave is a full 1 KiB chunk of the object
+    // (all but the last wave of an object), so no per-load bounds logic: the
+    // content address is a wave-uniform base + a per-lane constant + t*8*CPL KiB,
+    // and stream-mode chunk offsets are fetched from LDS once per chunk round.
+    const bool full_wave = wave_on && c0 + span <= a.n / 1024;
+    const uint32_t lane_off = (uint32_t)((lane & 7) * 16 + (lane >> 3) * CPL * 1024);
+    uint64_t soff_t[8];  // MODE != 0: stream offset of chunk t*8 + lane/8 of the current round
     // loader view: step g covers chunk j = g/8 of every lane, bytes [128*(g%8), +128)
     auto load_step = [&](int g, u32x4 (&v)[8]) {
         const int j = g >> 3, s = g & 7;
+        if (full_wave) {
+            if (MODE == 0) {
+                const uint8_t *b = ib + (c0 + j) * 1024 + s * 128 + lane_off;
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    v[t] = *reinterpret_cast<const u32x4 *>(b + (uint64_t)t * 8 * CPL * 1024);
+            } else {
+                if (s == 0) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) soff_t[t] = soff[j & 1][wave][t * 8 + (lane >> 3)];
+                }
+                const uint8_t *b = ib + s * 128 + (lane & 7) * 16;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = load16_a8(b + soff_t[t]);
+            }
+            return;
+        }
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const int cc = t * 8 + (lane >> 3);
@@ -572,11 +596,53 @@ __global__ __launch_bounds__(64 * (K3_WAVES + CW)) void bao_chunk_kernel(ChunkAr
     // The stream lines (128-B aligned in stream space) inside a chunk start at
     // chunk byte d + 128 t, d = (-base) mod 128; at step s the line ending at
     // d + 128 s is complete (its first part is in the other half of the row).
+    uint8_t *lsp[8];  // SP 3 fast path: stream address and line phase of chunk t*8 + lane/8, per round
+    uint32_t ldd[8];
     auto stream_lines = [&](int g) {
         const int j = g >> 3, s = g & 7, gl = lane & 7;
         auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x (8-aligned)
             return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
         };
+        if (full_wave) {  // all chunks full: per-chunk values computed once per round
+            if (s == 0) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    lsp[t] = ob + soff[j & 1][wave][t * 8 + (lane >> 3)];
+                    ldd[t] = (uint32_t)(-(uintptr_t)lsp[t]) & 127u;
+                }
+            }
+#pragma unroll SU
+            for (int t = 0; t < 8; ++t) {
+                uint8_t *sp = lsp[t];
+                const uint32_t d = ldd[t];
+                const uint32_t *row = st + (t * 8 + (lane >> 3)) * RW;
+                if (s >= 1) {  // the whole line [d + 128(s-1), d + 128 s)
+                    const uint32_t x = d + 128u * (s - 1) + 16u * gl;
+                    const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                    const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+                    if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(sp + x));
+                    else *reinterpret_cast<u32x4 *>(sp + x) = v;
+                } else {  // head [0, d)
+                    const uint32_t h = d & 8u;
+                    if (h && gl == 0) store8<NTS>(sp, piece(row, 0));
+                    const uint32_t x = 16u * gl + h;
+                    if (x + 16 <= d) {
+                        const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                        *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                    }
+                }
+                if (s == 7) {  // tail [896 + d, 1024)
+                    const uint32_t x = 896u + d + 16u * gl;
+                    if (x + 16 <= 1024) {
+                        const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                        *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                    } else if (x + 8 == 1024) {
+                        store8<NTS>(sp + x, piece(row, x));
+                    }
+                }
+            }
+            return;
+        }
 #pragma unroll SU
         for (int t = 0; t < 8; ++t) {
             const int cc = t * 8 + (lane >> 3);

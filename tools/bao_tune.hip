@@ -53,7 +53,8 @@ struct V {
 template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int CW = 0>
 V mk(bool stream, size_t pad_lds = 0) {
     char b[96];
-    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d cw%d pad%zu", MODE ? "decode" : "encode", CPL,
+    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d cw%d pad%zu",
+             MODE == 3 ? "in-place" : MODE ? "decode" : "encode", CPL,
              NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, CW, pad_lds);
     return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE, CW>, CPL, stream, pad_lds};
 }
@@ -74,12 +75,9 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&status, count * 4));
     CK(hipMalloc(&scratch, bao_scratch_len_t<1>(n, count)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xB1A3ull);
-    std::vector<V> vs = {mk<0, 2, false, 3>(true),             mk<0, 2, false, 4, 1, 0, 1>(true),
-                         mk<0, 2, false, 4, 1, 0, 2>(true),    mk<0, 2, false, 4, 1, 0, 4>(true),
-                         mk<0, 1, false, 4, 1, 0, 1>(true),    mk<0, 1, false, 4, 1, 0, 2>(true),
-                         mk<0, 2, true, 4, 1, 0, 2>(true),     mk<0, 2, false, 5, 1, 0, 4>(true),
-                         mk<0, 2, false>(false),               mk<0, 1, false>(false),
-                         mk<1, 2, false>(true)};
+    std::vector<V> vs = {mk<0, 2, false, 3>(true),  mk<0, 2, false>(false), mk<0, 4, false>(false),
+                         mk<1, 2, false>(true),     mk<3, 2, false>(true),  mk<3, 4, false>(true),
+                         mk<3, 8, false>(true),     mk<0, 4, false, 3>(true)};
     if (argc > 4) {  // comma-separated subset of variant indices (profiling)
         std::vector<V> keep;
         std::string sel = argv[4];
@@ -105,8 +103,11 @@ int main(int argc, char **argv) {
     for (int rd = 0; rd < rounds; ++rd)
         for (size_t v = 0; v < vs.size(); ++v) {
             const bool dec_mode = vs[v].name[0] == 'd';
+            const bool inplace = vs[v].name[0] == 'i';
             auto launch = [&] {
-                if (dec_mode) {
+                if (inplace) {
+                    CK(vs[v].fn(out, ostride, n, count, out, ostride, hash, nullptr, scratch, 0, vs[v].pad_lds));
+                } else if (dec_mode) {
                     CK(hipMemsetAsync(status, 0, count * 4, 0));
                     CK(vs[v].fn(out, ostride, n, count, dec, n, hash, status, scratch, 0, vs[v].pad_lds));
                 } else {
@@ -127,7 +128,7 @@ int main(int argc, char **argv) {
                 CK(hipMemset(dsum, 0, 8));
                 hipLaunchKernelGGL(checksum_kernel, dim3(64), dim3(256), 0, 0, (const uint64_t *)hash, count * 4, dsum);
                 CK(hipMemcpy(&hs, dsum, 8, hipMemcpyDeviceToHost));
-                if (vs[v].stream && !dec_mode) {
+                if (vs[v].stream && !dec_mode && !inplace) {
                     CK(hipMemset(dsum, 0, 8));
                     hipLaunchKernelGGL(checksum_kernel, dim3(4096), dim3(256), 0, 0, (const uint64_t *)out,
                                        count * ostride / 8, dsum);
@@ -135,7 +136,7 @@ int main(int argc, char **argv) {
                 }
                 if (v == 0) { ref_hash = hs; ref_stream = ss; }
                 if (hs != ref_hash) printf("!! %s hash mismatch\n", vs[v].name.c_str());
-                if (vs[v].stream && !dec_mode && ss != ref_stream) printf("!! %s stream mismatch\n", vs[v].name.c_str());
+                if (vs[v].stream && !dec_mode && !inplace && ss != ref_stream) printf("!! %s stream mismatch\n", vs[v].name.c_str());
                 if (dec_mode) {
                     std::vector<uint32_t> st(count);
                     CK(hipMemcpy(st.data(), status, count * 4, hipMemcpyDeviceToHost));
