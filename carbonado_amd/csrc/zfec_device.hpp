@@ -75,56 +75,14 @@ __device__ __forceinline__ void store8z(uint8_t *p, u32x2 v) {
     else *reinterpret_cast<u32x2 *>(p) = v;
 }
 
-// Store the 16 B of output byte offset p (shard-major layout).  BL (bao
-// layout, encode() with Zfec|Bao): the output is a bao stream and shard byte p
-// lives in content chunk p >> 10 at bao_off[p >> 10] + (p & 1023).  A wave's
-// 64 lanes hold one whole chunk (TILE = 4 waves x 1 KiB, C % 1024 == 0), so
-// the chunk index is wave-uniform; slots sit at 8 (mod 16) for a 16-B aligned
-// stream base, so lane l stores the ALIGNED 16 B [16 l + 8, +16) = its upper
-// half + lane l+1's lower half (DPP wave_shl:1; lane 63 gets zeros).
-// Memory lines are written whole: the parent slots around a chunk (filled
-// by the bao kernel later) are written as zeros here, so a line shared by a
-// chunk and a parent is not left half-written (a half-written line costs a
-// read-modify-write at the memory side).  Chunk ci with c = its parents
-// before it: lanes 0..4c-1 store [d - 64c + 8 + 16 l, +16) (zeros, the last
-// one carrying the chunk's first 8 bytes); a chunk followed by parents lets
-// lane 63 store {tail, 0, 0} within the body store; otherwise the 8-B head /
-// tail go alone (their line is completed by the neighbouring chunk's wave).
-template <bool NT, bool BL>
-__device__ __forceinline__ void put16(const ApplyArgs &a, uint8_t *ob, uint64_t p, u32x4 v) {
-    if constexpr (!BL) {
-        store16<NT>(ob + p, v);
-    } else {
-        const uint32_t ci = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 10));
-        // constant address space: scalar loads (lgkmcnt), which do not wait for this
-        // wave's outstanding stores the way a vector load's vmcnt(0) would
-        typedef const __attribute__((address_space(4))) uint64_t *ctab_t;
-        const ctab_t tab = (ctab_t)a.bao_off;
-        const uint64_t off = tab[ci];
-        uint8_t *d = ob + off;
-        const int lane = threadIdx.x & 63;
-        const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v.x, 0x130, 0xF, 0xF, false);  // wave_shl:1
-        const uint32_t ny = __builtin_amdgcn_update_dpp(0u, v.y, 0x130, 0xF, 0xF, false);
-        if (((uintptr_t)d & 15) != 8) {  // 8-B aligned stream base: slots are 16-B aligned
-            store16<NT>(d + 16 * lane, v);
-            return;
-        }
-        const uint32_t cprev = (uint32_t)((ci == 0 ? off - 8 : off - tab[ci - 1] - 1024) >> 6);
-        const bool par_after = ci + 1 < a.bao_n && tab[ci + 1] != off + 1024;
-        if (lane < 63 || par_after) store16<NT>(d + 16 * lane + 8, u32x4{v.z, v.w, nx, ny});
-        else store8z<NT>(d + 1016, u32x2{v.z, v.w});
-        if (cprev) {
-            const uint32_t hx = __builtin_amdgcn_readfirstlane(v.x), hy = __builtin_amdgcn_readfirstlane(v.y);
-            const uint32_t last = 4 * cprev - 1;  // pieces before the chunk's first 8 bytes
-            for (uint32_t b = 0; b <= last; b += 64) {  // > 64 pieces only past 16 parents (N > 2^16)
-                const uint32_t t = b + (uint32_t)lane;
-                if (t < last) store16<NT>(d - 64 * cprev + 8 + 16 * t, u32x4{0u, 0u, 0u, 0u});
-                else if (t == last) store16<NT>(d - 8, u32x4{0u, 0u, hx, hy});
-            }
-        } else if (lane == 0) {
-            store8z<NT>(d, u32x2{v.x, v.y});
-        }
-    }
+// Store the 16 B of output byte offset p (shard-major layout).
+template <bool NT>
+__device__ __forceinline__ void put16(uint8_t *ob, uint64_t p, u32x4 v) {
+    store16<NT>(ob + p, v);
+}
+
+__device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
 }
 
 // rows[q] = byte q of a0..a3 (4x4 byte transpose, 8 v_perm_b32)
@@ -197,7 +155,7 @@ struct TileIter {
 // super-tile's shards before computing the current one, NTL: nontemporal
 // input loads — tools/zfec_tune.
 template <int K, int NG, int U, int MAP, bool NT, int RO = 0, int WPE = 1, int SB = 0, bool PF = false,
-          bool NTL = false, bool BL = false>
+          bool NTL = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_kernel(ApplyArgs a) {
     constexpr int R = RO ? RO : replicas_for(K);
     using E = typename Entry<NG>::T;
@@ -293,24 +251,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
 
             // copies (data shards for encode, surviving primaries for decode)
-            if constexpr (BL) {
-                // bao layout needs a wave-uniform chunk per store: store shard s
-                // from every lane at once (lane group grp holds it in slot (s - grp) mod K)
 #pragma unroll
-                for (int sh = 0; sh < K; ++sh) {
-                    if (a.copy_off[sh] == NO_OUT) continue;
-                    const int jj = (sh - grp + K) % K;
-                    u32x4 w = v[u][0];
-#pragma unroll
-                    for (int j = 1; j < K; ++j)
-                        if (jj == j) w = v[u][j];
-                    put16<NT, true>(a, ob, a.copy_off[sh] + col, w);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < K; ++j)
-                    if (coff[j] != NO_OUT) store16<NT>(ob + coff[j] + col, v[u][j]);
-            }
+            for (int j = 0; j < K; ++j)
+                if (coff[j] != NO_OUT) store16<NT>(ob + coff[j] + col, v[u][j]);
 
             // computed rows: transpose column-packed sums into row streams
 #pragma unroll
@@ -332,7 +275,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     const uint64_t po = a.par_off[g * 4 + q];
                     if (po == NO_OUT) continue;
                     u32x4 o = {rows[q][0], rows[q][1], rows[q][2], rows[q][3]};
-                    put16<NT, BL>(a, ob, po + col, o);
+                    put16<NT>(ob, po + col, o);
                 }
             }
         }
@@ -343,6 +286,182 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 for (int j = 0; j < K; ++j) v[u][j] = vn[u][j];
         }
         st = st_next;
+        have = have_next;
+    }
+}
+
+// BL (bao layout, encode() with Zfec|Bao): zfec 4-of-8 encode whose 8 output
+// shards go straight into their chunk slots of each object's bao stream
+// (shard byte p at bao_off[p >> 10] + (p & 1023)).  Slots are not line-aligned
+// (8 mod 64), and a 128-B memory line written in pieces by several store
+// instructions costs far more than one whole-line store (tools/layout_probe:
+// 13.6 vs 11.1 ms per 1024 x 16 MiB), so every line is written by ONE store
+// instruction wherever the bytes around a chunk are known:
+//  * A unit is one 1 KiB chunk-column (the same 1 KiB of columns of every
+//    shard); a WAVE walks runs of consecutive units on its own (no workgroup
+//    barrier: the 4 waves of a workgroup share only the LDS table), so the
+//    chunk before a chunk, in every shard, is the wave's previous unit.
+//  * Store A: the 8 lines [L0, L0 + 1024), L0 = the line holding the slot
+//    start d; lane l = stream bytes [L0 + 16 l, +16).  Chunk bytes come from a
+//    lane rotation by (d - L0)/16 (ds_bpermute); the bytes before d are the
+//    chunk's parent slots (written as zeros: the bao kernel fills them later)
+//    and, before those, the previous chunk's tail, which the previous unit's
+//    rotation left in the same lanes (kept in registers).
+//  * Store B: the spill line [L0 + 1024, +128) holding the chunk's last d - L0
+//    bytes: written here when the rest of it is parent slots (zeros), else by
+//    the next unit's store A when the wave runs that unit next; only at
+//    shard / object / run borders is a line written in two parts.
+// XCD-grouped runs of CH units per wave (MAP 3 at wave granularity); the
+// next unit's 4 data-shard loads are in flight while a unit is computed.
+template <bool NT>
+__global__ __launch_bounds__(TPB) void gf_apply_bl_kernel(ApplyArgs a) {
+    constexpr int K = 4, R = replicas_for(4), W = 4, ROWB = K * R * W;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    {
+        const uint32_t *tab = reinterpret_cast<const uint32_t *>(a.table);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
+        for (int i = threadIdx.x; i < 256 * K * R; i += TPB) {
+            const int x = i / (K * R);
+            const int s = (i - x * (K * R)) / R;
+            dst[i] = tab[s * 256 + x];
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int rep = lane % R, grp = (lane & 31) / R;
+    uint32_t tb[K];
+    uint64_t ioff[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        tb[j] = (uint32_t)((((j + grp) % K) * R + rep) * W);
+        ioff[j] = a.in_off[(j + grp) % K];
+    }
+
+    const uint64_t Cc = a.C >> 10;  // units (chunk-columns) per object
+    const uint64_t T = Cc * a.count;
+    const uint64_t CH = a.chunk < 1 ? 1 : a.chunk;
+    const uint64_t G = gridDim.x, b = blockIdx.x;
+    const uint64_t GW = G * 4;
+    // waves of one XCD (b % 8) take consecutive runs
+    uint64_t run = (G & 7) ? b * 4 + w : ((b % 8) * (G / 8) + b / 8) * 4 + w;
+    uint64_t t_in = 0;
+    auto next_unit = [&](uint64_t &t) {
+        if (t_in == CH) { run += GW; t_in = 0; }
+        t = run * CH + t_in;
+        ++t_in;
+        return t < T;
+    };
+    auto load_unit = [&](uint64_t t, u32x4 (&v)[K]) {
+        const uint64_t obj = t / Cc;
+        const uint64_t col = (t - obj * Cc) * 1024 + lane * 16;
+        const uint8_t *ib = a.in + obj * a.in_stride;
+#pragma unroll
+        for (int j = 0; j < K; ++j) v[j] = load16_masked(ib, ioff[j] + col, a.valid);
+    };
+    typedef const __attribute__((address_space(4))) uint64_t *ctab_t;  // scalar loads
+    const ctab_t tab = (ctab_t)a.bao_off;
+    const u32x2 zero = {0u, 0u};
+
+    u32x2 plo[8], phi[8];  // previous unit's rotated data (its spill line, lanes 0..7), per shard
+    uint64_t prev_t = ~0ull;
+    uint64_t t;
+    bool have = next_unit(t);
+    u32x4 v[K];
+    if (have) load_unit(t, v);
+    while (have) {
+        uint64_t tn;
+        const bool have_next = next_unit(tn);
+        u32x4 vn[K];
+        if (have_next) load_unit(tn, vn);
+        const uint64_t obj = t / Cc, uc = t - obj * Cc;
+        uint8_t *ob = a.out + obj * a.out_stride;
+        const bool prev_ok = prev_t + 1 == t && uc > 0;                  // the previous chunk, every shard
+        const bool next_ok = have_next && tn == t + 1 && uc + 1 < Cc;   // the next chunk, every shard
+
+        uint32_t acc[16];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+            for (int dd = 0; dd < 4; ++dd) {
+                const uint32_t x = comp(v[j], dd);
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    const uint32_t e = *reinterpret_cast<const uint32_t *>(lds + ((x >> (8 * bb)) & 0xFFu) * ROWB + tb[j]);
+                    if (j == 0) acc[dd * 4 + bb] = e;
+                    else acc[dd * 4 + bb] ^= e;
+                }
+            }
+        }
+        u32x4 ov[8];  // this lane's 16 B of every output shard, shard order
+#pragma unroll
+        for (int sh = 0; sh < K; ++sh) {
+            const int jj = (sh - grp + K) % K;
+            u32x4 x = v[0];
+#pragma unroll
+            for (int j = 1; j < K; ++j)
+                if (jj == j) x = v[j];
+            ov[sh] = x;
+        }
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+            uint32_t r0, r1, r2, r3;
+            transpose4(acc[dd * 4 + 0], acc[dd * 4 + 1], acc[dd * 4 + 2], acc[dd * 4 + 3], r0, r1, r2, r3);
+            if (dd == 0) { ov[4].x = r0; ov[5].x = r1; ov[6].x = r2; ov[7].x = r3; }
+            if (dd == 1) { ov[4].y = r0; ov[5].y = r1; ov[6].y = r2; ov[7].y = r3; }
+            if (dd == 2) { ov[4].z = r0; ov[5].z = r1; ov[6].z = r2; ov[7].z = r3; }
+            if (dd == 3) { ov[4].w = r0; ov[5].w = r1; ov[6].w = r2; ov[7].w = r3; }
+        }
+
+#pragma unroll
+        for (int sh = 0; sh < 8; ++sh) {
+            const uint64_t ci = (uint64_t)sh * Cc + uc;
+            const uint64_t off = tab[ci];
+            uint8_t *d = ob + off;
+            const int r = (int)((uintptr_t)d & 127);
+            uint8_t *L0 = d - r;
+            const bool last = ci + 1 >= a.bao_n;
+            const int pb = ci == 0 ? 0 : (int)(off - tab[ci - 1] - 1024);  // parent bytes before the slot
+            const uint64_t cnext = last ? 0 : (tab[ci + 1] - off - 1024) >> 6;
+            // bytes [L0, d): parent slots only (zeros)?  else, before the parents, the
+            // previous chunk's tail (chunk 0: never touched -- header / another stream)
+            const bool pre_zero = ci != 0 && pb >= r;
+            const bool pred_in = ci != 0 && !pre_zero && prev_ok;
+            const bool post_zero = !last && 64 * cnext >= (uint64_t)(128 - r);
+            const bool succ_takes = !last && !post_zero && next_ok;
+            // rotation: lane l gets chunk bytes [16 l - r, +16) (mod 1024)
+            const int rr = r >> 3;
+            const int src0 = ((2 * lane - rr) >> 1) & 63, src1 = ((2 * lane - rr + 1) >> 1) & 63;
+            const bool up0 = rr & 1;
+            u32x2 lo, hi;
+            lo.x = bperm(src0, up0 ? ov[sh].z : ov[sh].x);
+            lo.y = bperm(src0, up0 ? ov[sh].w : ov[sh].y);
+            hi.x = bperm(src1, up0 ? ov[sh].x : ov[sh].z);
+            hi.y = bperm(src1, up0 ? ov[sh].y : ov[sh].w);
+            const int b0 = 16 * lane - r, b1 = b0 + 8;  // chunk byte of each 8-B half of store A
+            // store A; the previous chunk's spill line == this L0 exactly when the
+            // previous unit left it to us, and its rotation holds those bytes in these lanes
+            u32x2 a0 = lo, a1 = hi;
+            if (b0 < 0) a0 = (pred_in && b0 < -pb) ? plo[sh] : zero;
+            if (b1 < 0) a1 = (pred_in && b1 < -pb) ? phi[sh] : zero;
+            if (b0 >= 0 || pre_zero || pred_in) store16<NT>(L0 + 16 * lane, u32x4{a0.x, a0.y, a1.x, a1.y});
+            else if (b1 >= 0) store8z<NT>(L0 + 16 * lane + 8, a1);
+            // store B: chunk bytes 1024 + b0, 1024 + b1 (< 1024: this chunk's tail)
+            if (r && lane < 8 && !succ_takes) {
+                const bool in0 = b0 < 0, in1 = b1 < 0;
+                uint8_t *q = L0 + 1024 + 16 * lane;
+                if (in1 || post_zero)
+                    store16<NT>(q, u32x4{in0 ? lo.x : 0u, in0 ? lo.y : 0u, in1 ? hi.x : 0u, in1 ? hi.y : 0u});
+                else if (in0)
+                    store8z<NT>(q, lo);
+            }
+            plo[sh] = lo;
+            phi[sh] = hi;
+        }
+        prev_t = t;
+#pragma unroll
+        for (int j = 0; j < K; ++j) v[j] = vn[j];
+        t = tn;
         have = have_next;
     }
 }

@@ -92,6 +92,7 @@ constexpr int ZF_U = 1;
 constexpr int ZF_MAP = 3;
 constexpr bool ZF_NT = true;
 constexpr uint64_t ZF_CHUNK = 64;
+constexpr uint64_t ZF_BL_RUN = 64;  // bao-layout kernel: consecutive 1 KiB units per wave run
 
 // Wide stripes (K > 4): pin the XOR partial sums every shard (SB = 1) so the
 // K*16 table lookups are not all live at once — without it K = 8 compiles to
@@ -104,7 +105,6 @@ constexpr uint64_t ZF_CHUNK = 64;
 // occupancy 4, on two boxes.
 struct KernelInfo {
     KernelFn fn;
-    KernelFn fn_bl;  // same schedule, output in bao layout (GfLaunch::bao_off); null = unsupported shape
     size_t lds;
     int grid;
     int u;        // column tiles per super-tile (the kernel's U)
@@ -119,7 +119,6 @@ KernelInfo make_info() {
     ki.grid = 0;
     ki.u = 1;
     ki.bpc_cap = 0;
-    ki.fn_bl = nullptr;
     if constexpr (K > 4) {
         ki.fn = gf_apply_kernel<K, NG, ZF_U, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
     } else if constexpr (K == 4 && NG == 1) {
@@ -128,7 +127,6 @@ KernelInfo make_info() {
             ki.fn = gf_apply_kernel<4, 1, 1, ZF_MAP, ZF_NT>;
         } else {
             ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true>;
-            ki.fn_bl = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true, false, true>;
             ki.u = 2;
             ki.bpc_cap = 2;
         }
@@ -274,9 +272,14 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     a.bao_off = L.bao_off;
     a.bao_n = L.bao_off ? (L.C / 1024) * (p.k + p.np) : 0;  // m*C/1024 chunks
     KernelFn fn = ki.fn;
-    if (L.bao_off) {  // bao layout: whole 1 KiB chunks per wave, one pass (copies + all computed rows)
-        if (!ki.fn_bl || L.C % 1024 || !copies || row0 + nrows != p.np) return hipErrorInvalidValue;
-        fn = ki.fn_bl;
+    size_t lds = ki.lds;
+    const bool bl = L.bao_off != nullptr;
+    if (bl) {  // bao layout: the dedicated 4-of-8 kernel, one pass (copies + all 4 parity rows)
+        if (p.k != 4 || p.np != 4 || L.C % 1024 || !copies || row0 != 0) return hipErrorInvalidValue;
+        fn = gf_apply_bl_kernel<ZF_NT>;
+        ki.fn = fn;  // occupancy of the kernel actually launched
+        ki.u = 1;
+        ki.bpc_cap = 0;
     }
     a.valid = L.valid; a.C = L.C;
     a.tiles_per_obj = (L.C + TILE - 1) / TILE;
@@ -302,7 +305,11 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     const uint64_t per_wg = units / (grid ? grid : 1);
     const uint64_t run = ZF_CHUNK / ki.u;
     a.chunk = per_wg < 1 ? 1 : (per_wg < run ? per_wg : run);
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(TPB), ki.lds, stream, a);
+    if (bl) {  // wave-level runs of 1 KiB units
+        const uint64_t per_wave = (L.C / 1024) * L.count / (4 * (grid ? grid : 1));
+        a.chunk = per_wave < 1 ? 1 : (per_wave < ZF_BL_RUN ? per_wave : ZF_BL_RUN);
+    }
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(TPB), lds, stream, a);
     return hipGetLastError();
 }
 

@@ -55,14 +55,20 @@ struct Variant {
     bool bl = false;
 };
 
-template <int U, int MAP, bool NT, int CH = 1, int WPE = 1, int SB = 0, bool PF = false, bool NTL = false,
-          bool BL = false>
+template <int U, int MAP, bool NT, int CH = 1, int WPE = 1, int SB = 0, bool PF = false, bool NTL = false>
 Variant V(int bpc) {
     char buf[96];
-    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d wpe%d sb%d pf%d ntl%d %s bpc%d%s", U, MAP, CH, WPE, SB, PF, NTL,
-             NT ? "nt " : "pln", bpc, BL ? " BAO-LAYOUT" : "");
-    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT, 0, WPE, SB, PF, NTL, BL>, bpc, CH, (size_t)256 * 4 * 8 * 4,
-                   BL};
+    snprintf(buf, sizeof buf, "U%d MAP%d CH%-3d wpe%d sb%d pf%d ntl%d %s bpc%d", U, MAP, CH, WPE, SB, PF, NTL,
+             NT ? "nt " : "pln", bpc);
+    return Variant{buf, gf_apply_kernel<4, 1, U, MAP, NT, 0, WPE, SB, PF, NTL>, bpc, CH, (size_t)256 * 4 * 8 * 4};
+}
+
+// bao-layout kernel (encode() Zfec|Bao): chunk slots of a bao stream, wave runs of CH 1 KiB units
+template <bool NT, int CH>
+Variant VBL(int bpc) {
+    char buf[96];
+    snprintf(buf, sizeof buf, "BAO-LAYOUT wave-runs CH%-3d %s bpc%d", CH, NT ? "nt " : "pln", bpc);
+    return Variant{buf, gf_apply_bl_kernel<NT>, bpc, CH, (size_t)256 * 4 * 8 * 4, true};
 }
 
 // 8-of-16 variants (K = 8, NG = 2), replica count R
@@ -116,10 +122,8 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {V<2, 3, true, 32, 2, 0, true>(2),  V<1, 3, true, 64, 1, 0, true>(4),  V<1, 3, true, 64, 4, 0, true>(4),
-              V<1, 3, true, 64, 1, 0, true>(6),  V<1, 3, true, 64, 1, 0, true>(8),  V<1, 3, true, 32, 1, 0, true>(4),
-              V<1, 3, true, 128, 1, 0, true>(4), V<2, 3, true, 32, 2, 0, true>(4),  V<2, 3, true, 32, 2, 0, true>(3),
-              V<1, 3, true, 64, 3, 0, true>(4),  V<1, 3, true, 64, 1, 0, true>(3),  V<1, 3, true, 64, 1, 0, true, true>(4)};
+        vs = {V<2, 3, true, 32, 2, 0, true>(2), VBL<true, 64>(3), VBL<true, 16>(3), VBL<true, 256>(3),
+              VBL<false, 64>(3),                 VBL<true, 64>(2)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
@@ -137,6 +141,7 @@ int main(int argc, char **argv) {
             const int grid = 256 * vs[v].blocks_per_cu;
             a.chunk = vs[v].chunk;
             a.bao_off = vs[v].bl ? dboff : nullptr;
+            a.tiles_per_obj = C / TILE;
             a.bao_n = Nch;
             a.out_stride = vs[v].bl ? bstride : M * C;
             if (rd == 0) CK(hipMemset(out, 0, count * 2 * n));  // a variant that skips bytes fails the checksum
