@@ -54,6 +54,9 @@ struct GfLaunch {
     // optional: write the shard-major output in bao layout (encode() with
     // Zfec|Bao): stream offset of each 1 KiB content chunk, device table
     const uint64_t *bao_off = nullptr;
+    // optional: at most this many workgroups per CU (0 = occupancy), leaving
+    // room for a kernel that runs beside it on another stream
+    int wg_per_cu = 0;
 };
 
 // Enqueue the matrix apply.  Tables are cached device-side per plan key.

@@ -92,7 +92,7 @@ constexpr int ZF_U = 1;
 constexpr int ZF_MAP = 3;
 constexpr bool ZF_NT = true;
 constexpr uint64_t ZF_CHUNK = 64;
-constexpr uint64_t ZF_BL_RUN = 64;  // bao-layout kernel: consecutive 1 KiB units per wave run
+constexpr uint64_t ZF_BL_RUN = 32;  // bao-layout kernel: consecutive 1 KiB units per wave run
 
 // Wide stripes (K > 4): pin the XOR partial sums every shard (SB = 1) so the
 // K*16 table lookups are not all live at once — without it K = 8 compiles to
@@ -296,7 +296,8 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     sub.coef.assign(p.coef.begin() + (size_t)row0 * p.k, p.coef.begin() + (size_t)(row0 + nrows) * p.k);
     hipError_t e = device_table(sub, ng, &a.table);
     if (e != hipSuccess) return e;
-    const int grid_cap = grid_for(ki);
+    int grid_cap = grid_for(ki);
+    if (L.wg_per_cu > 0 && grid_cap > L.wg_per_cu * num_cus()) grid_cap = L.wg_per_cu * num_cus();
     // the kernel walks super-tiles of ki.u column tiles (never across objects)
     const uint64_t units = ((a.tiles_per_obj + ki.u - 1) / ki.u) * L.count;
     uint64_t grid = units < (uint64_t)grid_cap ? units : (uint64_t)grid_cap;

@@ -1,3 +1,6 @@
+"""Diagnostic: device encode() level 12 (zfec fused into the bao layout) vs the
+oracle for a few object sizes; prints diff runs (stream offsets) when they differ.
+Run on the GPU box from the repo root: python3 tools/pipeline_diff.py"""
 import sys
 sys.path.insert(0, ".")
 import numpy as np

@@ -122,8 +122,8 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {V<2, 3, true, 32, 2, 0, true>(2), VBL<true, 64>(3), VBL<true, 16>(3), VBL<true, 256>(3),
-              VBL<false, 64>(3),                 VBL<true, 64>(2)};
+        vs = {VBL<true, 4>(3), VBL<true, 8>(3), VBL<true, 16>(3), VBL<true, 32>(3),
+              VBL<true, 16>(4)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
