@@ -8,9 +8,11 @@ raise instead of silently running elsewhere.
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libcarbonado_hip.so"
+# CARBONADO_HIP_LIB: another build of the same library (A/B calibration tools only)
+LIB_PATH = Path(os.environ.get("CARBONADO_HIP_LIB") or Path(__file__).resolve().parent / "lib" / "libcarbonado_hip.so")
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)

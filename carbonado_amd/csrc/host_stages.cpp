@@ -29,6 +29,7 @@
 
 #include <immintrin.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
