@@ -59,8 +59,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--verify-all", action="store_true",
-                    help="encode mode: check EVERY object bit-exact (SURVEY 8d): BLAKE3 of each object's "
-                         "shards on the GPU vs the C oracle's zfec + BLAKE3 on 16 host threads")
+                    help="encode / pipeline mode: check EVERY object bit-exact (SURVEY 8d): BLAKE3 of each "
+                         "object's output on the GPU vs the C oracle's zfec (or encode()) + BLAKE3 on 16 host threads")
     ap.add_argument("--no-aliased", action="store_true",
                     help="encode mode: skip the second, in-place (aliased data shards) measurement")
     ap.add_argument("--scatter", action="store_true",
@@ -352,21 +352,30 @@ class Workload:
         from oracle import oracle as O
         t0 = time.perf_counter()
         count, k, m, C = self.count, self.k, self.m, self.C
+        pipeline = self.args.mode == "pipeline"
+        olen = self.blen if pipeline else m * C  # bytes of each object's output
         digests = torch.empty((count, 32), dtype=torch.uint8, device=self.dev)
-        scratch = device.bao_scratch(m * C, count, self.dev)
-        device.bao_encode_batch(self.out, m * C, None, digests, scratch)
+        scratch = device.bao_scratch(olen, count, self.dev)
+        device.bao_encode_batch(self.out, olen, None, digests, scratch)
         torch.cuda.synchronize()
         gpu = digests.cpu().numpy()
+        hashes = self.hashes.cpu().numpy() if pipeline else None
         del scratch
         host_in = self.inp.cpu().numpy()
 
         def check(o):
+            if pipeline:
+                enc, h, _ = O.encode(host_in[o].tobytes(), self.args.level)
+                return O.blake3(enc) == gpu[o].tobytes() and (not self.args.level & 4 or
+                                                              h == hashes[o].tobytes())
             return O.blake3(O.zfec_encode(host_in[o], k, m)[0]) == gpu[o].tobytes()
         with ThreadPoolExecutor(threads) as ex:
             oks = list(ex.map(check, range(count)))
         bad = [o for o, ok in enumerate(oks) if not ok]
         return {"ok": not bad, "objects": count, "mismatched": bad[:16], "seconds": round(time.perf_counter() - t0, 1),
-                "how": f"BLAKE3 of each object's {m} shards on the GPU vs oracle zfec + BLAKE3 on {threads} threads"}
+                "how": (f"BLAKE3 of each object's level-{self.args.level} encoding on the GPU + its bao hash vs the "
+                        f"oracle's encode() + BLAKE3 on {threads} threads" if pipeline else
+                        f"BLAKE3 of each object's {m} shards on the GPU vs oracle zfec + BLAKE3 on {threads} threads")}
 
     def time_aliased(self, steps: int, warmup: int, world: int):
         """the same encode with the data shards aliased (in
@@ -441,7 +450,7 @@ def main():
     if rank == 0 and not args.no_verify and not args.dry_run:
         verified, sample = wl.verify_object0()
     verified_all = None
-    if rank == 0 and args.verify_all and args.mode == "encode" and not args.dry_run:
+    if rank == 0 and args.verify_all and args.mode in ("encode", "pipeline") and not args.dry_run:
         verified_all = wl.verify_all()
     aliased = None
     if args.mode == "encode" and not args.dry_run and not args.no_aliased:
