@@ -272,6 +272,40 @@ hipError_t pipe_streams(PipeStreams **out) {
 }
 }  // namespace
 
+// Two stages over `parts` slices of a batch: stage1 (HBM-bound) of part i+1
+// runs on one stream beside stage2 (VALU-bound) of part i on another;
+// fork/join with events on the caller's stream s.
+template <typename S1, typename S2>
+hipError_t overlap_parts(uint64_t count, uint64_t parts, hipStream_t s, S1 stage1, S2 stage2) {
+    PipeStreams *ps;
+    hipError_t e;
+    if ((e = pipe_streams(&ps)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ps->fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(ps->k1, ps->fork, 0)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(ps->k3, ps->fork, 0)) != hipSuccess) return e;
+    for (uint64_t i = 0, o0 = 0; i < parts; ++i) {
+        const uint64_t o1 = count * (i + 1) / parts, cnt = o1 - o0;
+        if ((e = stage1(o0, cnt, ps->k1)) != hipSuccess) return e;
+        if ((e = hipEventRecord(ps->k1_done, ps->k1)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ps->k3, ps->k1_done, 0)) != hipSuccess) return e;
+        if ((e = stage2(o0, cnt, ps->k3)) != hipSuccess) return e;
+        o0 = o1;
+    }
+    if ((e = hipEventRecord(ps->join1, ps->k1)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ps->join3, ps->k3)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(s, ps->join1, 0)) != hipSuccess) return e;
+    return hipStreamWaitEvent(s, ps->join3, 0);
+}
+
+int pipe_parts_cfg() {
+    static const int p = env_int("CHIP_PIPE_PARTS", 8);
+    return p < 1 ? 1 : p;
+}
+int pipe_wg_cfg() {
+    static const int w = env_int("CHIP_PIPE_K1_WG", 2);
+    return w;
+}
+
 hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
                         uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s) {
     const uint64_t zlen = (uint64_t)CHIP_FEC_M * C;
@@ -280,9 +314,8 @@ hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uin
     if (e != hipSuccess) return e;
     static const std::vector<uint8_t> enc = zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M);
     const GfPlan p = encode_plan(CHIP_FEC_K, CHIP_FEC_M, C, enc);
-    static const int parts_cfg = env_int("CHIP_PIPE_PARTS", 8), k1_wg = env_int("CHIP_PIPE_K1_WG", 2);
     // parts of at least 64 MiB of shards: smaller batches run the two stages back to back
-    const uint64_t parts = std::min<uint64_t>(parts_cfg < 1 ? 1 : parts_cfg, count * zlen / (64ull << 20));
+    const uint64_t parts = std::min<uint64_t>(pipe_parts_cfg(), count * zlen / (64ull << 20));
     if (parts < 2) {
         GfLaunch L{d_in, d_out, in_stride, out_stride, n, C, count};
         L.bao_off = tab;
@@ -290,30 +323,21 @@ hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uin
         if (e != hipSuccess) return e;
         return bao_encode_inplace_dev(d_out, out_stride, zlen, count, d_hash, d_scratch, s);
     }
-    PipeStreams *ps;
-    if ((e = pipe_streams(&ps)) != hipSuccess) return e;
-    if ((e = hipEventRecord(ps->fork, s)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(ps->k1, ps->fork, 0)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(ps->k3, ps->fork, 0)) != hipSuccess) return e;
     uint8_t *scr = static_cast<uint8_t *>(d_scratch);
-    for (uint64_t i = 0, o0 = 0; i < parts; ++i) {
-        const uint64_t o1 = count * (i + 1) / parts, cnt = o1 - o0;
-        GfLaunch L{d_in + o0 * in_stride, d_out + o0 * out_stride, in_stride, out_stride, n, C, cnt};
-        L.bao_off = tab;
-        L.wg_per_cu = k1_wg;
-        if ((e = gf_apply(p, L, ps->k1)) != hipSuccess) return e;
-        if ((e = hipEventRecord(ps->k1_done, ps->k1)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(ps->k3, ps->k1_done, 0)) != hipSuccess) return e;
-        if ((e = bao_encode_inplace_dev(d_out + o0 * out_stride, out_stride, zlen, cnt, d_hash + 32 * o0, scr,
-                                        ps->k3)) != hipSuccess)
-            return e;
-        scr += bao_scratch_len(zlen, cnt);
-        o0 = o1;
-    }
-    if ((e = hipEventRecord(ps->join1, ps->k1)) != hipSuccess) return e;
-    if ((e = hipEventRecord(ps->join3, ps->k3)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(s, ps->join1, 0)) != hipSuccess) return e;
-    return hipStreamWaitEvent(s, ps->join3, 0);
+    return overlap_parts(
+        count, parts, s,
+        [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
+            GfLaunch L{d_in + o0 * in_stride, d_out + o0 * out_stride, in_stride, out_stride, n, C, cnt};
+            L.bao_off = tab;
+            L.wg_per_cu = pipe_wg_cfg();
+            return gf_apply(p, L, st);
+        },
+        [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
+            hipError_t r = bao_encode_inplace_dev(d_out + o0 * out_stride, out_stride, zlen, cnt, d_hash + 32 * o0,
+                                                  scr, st);
+            scr += bao_scratch_len(zlen, cnt);
+            return r;
+        });
 }
 
 // decode plan for k selected shares (slot s holds share sel[s], stored at

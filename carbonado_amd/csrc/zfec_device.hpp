@@ -8,6 +8,7 @@
 #include <cstdint>
 
 #include "chip_internal.hpp"
+#include "layout_store.hpp"
 
 namespace chip {
 namespace zf {
@@ -79,10 +80,6 @@ __device__ __forceinline__ void store8z(uint8_t *p, u32x2 v) {
 template <bool NT>
 __device__ __forceinline__ void put16(uint8_t *ob, uint64_t p, u32x4 v) {
     store16<NT>(ob + p, v);
-}
-
-__device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
 }
 
 // rows[q] = byte q of a0..a3 (4x4 byte transpose, 8 v_perm_b32)
@@ -292,27 +289,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 // BL (bao layout, encode() with Zfec|Bao): zfec 4-of-8 encode whose 8 output
 // shards go straight into their chunk slots of each object's bao stream
-// (shard byte p at bao_off[p >> 10] + (p & 1023)).  Slots are not line-aligned
-// (8 mod 64), and a 128-B memory line written in pieces by several store
-// instructions costs far more than one whole-line store (tools/layout_probe:
-// 13.6 vs 11.1 ms per 1024 x 16 MiB), so every line is written by ONE store
-// instruction wherever the bytes around a chunk are known:
-//  * A unit is one 1 KiB chunk-column (the same 1 KiB of columns of every
-//    shard); a WAVE walks runs of consecutive units on its own (no workgroup
-//    barrier: the 4 waves of a workgroup share only the LDS table), so the
-//    chunk before a chunk, in every shard, is the wave's previous unit.
-//  * Store A: the 8 lines [L0, L0 + 1024), L0 = the line holding the slot
-//    start d; lane l = stream bytes [L0 + 16 l, +16).  Chunk bytes come from a
-//    lane rotation by (d - L0)/16 (ds_bpermute); the bytes before d are the
-//    chunk's parent slots (written as zeros: the bao kernel fills them later)
-//    and, before those, the previous chunk's tail, which the previous unit's
-//    rotation left in the same lanes (kept in registers).
-//  * Store B: the spill line [L0 + 1024, +128) holding the chunk's last d - L0
-//    bytes: written here when the rest of it is parent slots (zeros), else by
-//    the next unit's store A when the wave runs that unit next; only at
-//    shard / object / run borders is a line written in two parts.
-// XCD-grouped runs of CH units per wave (MAP 3 at wave granularity); the
-// next unit's 4 data-shard loads are in flight while a unit is computed.
+// (shard byte p at bao_off[p >> 10] + (p & 1023)), every memory line written
+// whole by one store where its bytes are known (layout_store.hpp).  A unit is
+// one 1 KiB chunk-column (the same 1 KiB of columns of every shard); a WAVE
+// walks runs of consecutive units on its own (no workgroup barrier: the 4
+// waves of a workgroup share only the LDS table), so the chunk before a
+// chunk, in every shard, is the wave's previous unit and its spill bytes are
+// still in registers.  The next unit's 4 data-shard loads are in flight while
+// a unit is computed.
 template <bool NT>
 __global__ __launch_bounds__(TPB) void gf_apply_bl_kernel(ApplyArgs a) {
     constexpr int K = 4, R = replicas_for(4), W = 4, ROWB = K * R * W;
@@ -328,7 +312,6 @@ __global__ __launch_bounds__(TPB) void gf_apply_bl_kernel(ApplyArgs a) {
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int rep = lane % R, grp = (lane & 31) / R;
     uint32_t tb[K];
     uint64_t ioff[K];
@@ -339,19 +322,7 @@ __global__ __launch_bounds__(TPB) void gf_apply_bl_kernel(ApplyArgs a) {
     }
 
     const uint64_t Cc = a.C >> 10;  // units (chunk-columns) per object
-    const uint64_t T = Cc * a.count;
-    const uint64_t CH = a.chunk < 1 ? 1 : a.chunk;
-    const uint64_t G = gridDim.x, b = blockIdx.x;
-    const uint64_t GW = G * 4;
-    // waves of one XCD (b % 8) take consecutive runs
-    uint64_t run = (G & 7) ? b * 4 + w : ((b % 8) * (G / 8) + b / 8) * 4 + w;
-    uint64_t t_in = 0;
-    auto next_unit = [&](uint64_t &t) {
-        if (t_in == CH) { run += GW; t_in = 0; }
-        t = run * CH + t_in;
-        ++t_in;
-        return t < T;
-    };
+    lay::WaveRuns runs(Cc * a.count, a.chunk);
     auto load_unit = [&](uint64_t t, u32x4 (&v)[K]) {
         const uint64_t obj = t / Cc;
         const uint64_t col = (t - obj * Cc) * 1024 + lane * 16;
@@ -359,19 +330,16 @@ __global__ __launch_bounds__(TPB) void gf_apply_bl_kernel(ApplyArgs a) {
 #pragma unroll
         for (int j = 0; j < K; ++j) v[j] = load16_masked(ib, ioff[j] + col, a.valid);
     };
-    typedef const __attribute__((address_space(4))) uint64_t *ctab_t;  // scalar loads
-    const ctab_t tab = (ctab_t)a.bao_off;
-    const u32x2 zero = {0u, 0u};
-
-    u32x2 plo[8], phi[8];  // previous unit's rotated data (its spill line, lanes 0..7), per shard
+    const lay::ctab_t tab = (lay::ctab_t)a.bao_off;
+    lay::Spill spill[8];  // the previous unit's spill lines, per shard
     uint64_t prev_t = ~0ull;
     uint64_t t;
-    bool have = next_unit(t);
+    bool have = runs.next(t);
     u32x4 v[K];
     if (have) load_unit(t, v);
     while (have) {
         uint64_t tn;
-        const bool have_next = next_unit(tn);
+        const bool have_next = runs.next(tn);
         u32x4 vn[K];
         if (have_next) load_unit(tn, vn);
         const uint64_t obj = t / Cc, uc = t - obj * Cc;
@@ -414,50 +382,8 @@ __global__ __launch_bounds__(TPB) void gf_apply_bl_kernel(ApplyArgs a) {
         }
 
 #pragma unroll
-        for (int sh = 0; sh < 8; ++sh) {
-            const uint64_t ci = (uint64_t)sh * Cc + uc;
-            const uint64_t off = tab[ci];
-            uint8_t *d = ob + off;
-            const int r = (int)((uintptr_t)d & 127);
-            uint8_t *L0 = d - r;
-            const bool last = ci + 1 >= a.bao_n;
-            const int pb = ci == 0 ? 0 : (int)(off - tab[ci - 1] - 1024);  // parent bytes before the slot
-            const uint64_t cnext = last ? 0 : (tab[ci + 1] - off - 1024) >> 6;
-            // bytes [L0, d): parent slots only (zeros)?  else, before the parents, the
-            // previous chunk's tail (chunk 0: never touched -- header / another stream)
-            const bool pre_zero = ci != 0 && pb >= r;
-            const bool pred_in = ci != 0 && !pre_zero && prev_ok;
-            const bool post_zero = !last && 64 * cnext >= (uint64_t)(128 - r);
-            const bool succ_takes = !last && !post_zero && next_ok;
-            // rotation: lane l gets chunk bytes [16 l - r, +16) (mod 1024)
-            const int rr = r >> 3;
-            const int src0 = ((2 * lane - rr) >> 1) & 63, src1 = ((2 * lane - rr + 1) >> 1) & 63;
-            const bool up0 = rr & 1;
-            u32x2 lo, hi;
-            lo.x = bperm(src0, up0 ? ov[sh].z : ov[sh].x);
-            lo.y = bperm(src0, up0 ? ov[sh].w : ov[sh].y);
-            hi.x = bperm(src1, up0 ? ov[sh].x : ov[sh].z);
-            hi.y = bperm(src1, up0 ? ov[sh].y : ov[sh].w);
-            const int b0 = 16 * lane - r, b1 = b0 + 8;  // chunk byte of each 8-B half of store A
-            // store A; the previous chunk's spill line == this L0 exactly when the
-            // previous unit left it to us, and its rotation holds those bytes in these lanes
-            u32x2 a0 = lo, a1 = hi;
-            if (b0 < 0) a0 = (pred_in && b0 < -pb) ? plo[sh] : zero;
-            if (b1 < 0) a1 = (pred_in && b1 < -pb) ? phi[sh] : zero;
-            if (b0 >= 0 || pre_zero || pred_in) store16<NT>(L0 + 16 * lane, u32x4{a0.x, a0.y, a1.x, a1.y});
-            else if (b1 >= 0) store8z<NT>(L0 + 16 * lane + 8, a1);
-            // store B: chunk bytes 1024 + b0, 1024 + b1 (< 1024: this chunk's tail)
-            if (r && lane < 8 && !succ_takes) {
-                const bool in0 = b0 < 0, in1 = b1 < 0;
-                uint8_t *q = L0 + 1024 + 16 * lane;
-                if (in1 || post_zero)
-                    store16<NT>(q, u32x4{in0 ? lo.x : 0u, in0 ? lo.y : 0u, in1 ? hi.x : 0u, in1 ? hi.y : 0u});
-                else if (in0)
-                    store8z<NT>(q, lo);
-            }
-            plo[sh] = lo;
-            phi[sh] = hi;
-        }
+        for (int sh = 0; sh < 8; ++sh)
+            lay::put_chunk<NT>(ob, tab, a.bao_n, (uint64_t)sh * Cc + uc, ov[sh], prev_ok, next_ok, spill[sh]);
         prev_t = t;
 #pragma unroll
         for (int j = 0; j < K; ++j) v[j] = vn[j];

@@ -128,3 +128,26 @@ def test_batch_bao_every_line_phase(gpu):
         assert hashes[o].cpu().numpy().tobytes() == oh, o
         assert host[o, :blen].tobytes() == oe, o
         assert (host[o, blen:] == 0xA5).all(), o  # nothing written past the stream
+
+
+def test_batch_bao_ragged_large(gpu):
+    """A 144 MiB batch of 16 MiB + 37 B objects: a short last chunk, an
+    8 mod 16 output stride (the line phase of each stream start differs across
+    objects) and a ragged input stride; nothing written past a stream."""
+    import torch
+    from carbonado_amd import device
+    n, count = (16 << 20) + 37, 9
+    blen = O.lib().orc_bao_encoded_len(n)
+    stride = (blen + 15) // 16 * 16 + 8
+    gen = torch.Generator(device="cuda").manual_seed(91)
+    inp = torch.randint(0, 256, (count, n + 5), dtype=torch.uint8, device="cuda", generator=gen)
+    out = torch.full((count, stride), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+    device.bao_encode_batch(inp, n, out, hashes, device.bao_scratch(n, count))
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    for o in range(count):
+        oe, oh = O.bao_encode(inp[o, :n].cpu().numpy().tobytes())
+        assert hashes[o].cpu().numpy().tobytes() == oh, o
+        assert host[o, :blen].tobytes() == oe, o
+        assert (host[o, blen:] == 0xA5).all(), o
