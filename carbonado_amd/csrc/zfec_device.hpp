@@ -297,7 +297,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // chunk, in every shard, is the wave's previous unit and its spill bytes are
 // still in registers.  The next unit's 4 data-shard loads are in flight while
 // a unit is computed.
-template <bool NT>
+// BL = false: the same wave-private schedule writing the plain shard-major
+// layout (a K1 variant for tools/zfec_tune).
+template <bool NT, bool BL = true>
 __global__ __launch_bounds__(TPB) void gf_apply_bl_kernel(ApplyArgs a) {
     constexpr int K = 4, R = replicas_for(4), W = 4, ROWB = K * R * W;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -381,9 +383,14 @@ __global__ __launch_bounds__(TPB) void gf_apply_bl_kernel(ApplyArgs a) {
             if (dd == 3) { ov[4].w = r0; ov[5].w = r1; ov[6].w = r2; ov[7].w = r3; }
         }
 
+        if constexpr (BL) {
 #pragma unroll
-        for (int sh = 0; sh < 8; ++sh)
-            lay::put_chunk<NT>(ob, tab, a.bao_n, (uint64_t)sh * Cc + uc, ov[sh], prev_ok, next_ok, spill[sh]);
+            for (int sh = 0; sh < 8; ++sh)
+                lay::put_chunk<NT>(ob, tab, a.bao_n, (uint64_t)sh * Cc + uc, ov[sh], prev_ok, next_ok, spill[sh]);
+        } else {
+#pragma unroll
+            for (int sh = 0; sh < 8; ++sh) store16<NT>(ob + (uint64_t)sh * a.C + uc * 1024 + lane * 16, ov[sh]);
+        }
         prev_t = t;
 #pragma unroll
         for (int j = 0; j < K; ++j) v[j] = vn[j];

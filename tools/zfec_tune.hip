@@ -64,11 +64,12 @@ Variant V(int bpc) {
 }
 
 // bao-layout kernel (encode() Zfec|Bao): chunk slots of a bao stream, wave runs of CH 1 KiB units
-template <bool NT, int CH>
+template <bool NT, int CH, bool BL = true>
 Variant VBL(int bpc) {
     char buf[96];
-    snprintf(buf, sizeof buf, "BAO-LAYOUT wave-runs CH%-3d %s bpc%d", CH, NT ? "nt " : "pln", bpc);
-    return Variant{buf, gf_apply_bl_kernel<NT>, bpc, CH, (size_t)256 * 4 * 8 * 4, true};
+    snprintf(buf, sizeof buf, "%s wave-runs CH%-3d %s bpc%d", BL ? "BAO-LAYOUT" : "shard-major", CH, NT ? "nt " : "pln",
+             bpc);
+    return Variant{buf, gf_apply_bl_kernel<NT, BL>, bpc, CH, (size_t)256 * 4 * 8 * 4, BL};
 }
 
 // 8-of-16 variants (K = 8, NG = 2), replica count R
@@ -122,8 +123,8 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {VBL<true, 4>(3), VBL<true, 8>(3), VBL<true, 16>(3), VBL<true, 32>(3),
-              VBL<true, 16>(4)};
+        vs = {V<2, 3, true, 32, 2, 0, true>(2), VBL<true, 32, false>(3), VBL<true, 64, false>(3),
+              VBL<true, 32, false>(2), VBL<false, 32, false>(3), VBL<true, 8, false>(3), VBL<true, 32>(3)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
