@@ -42,61 +42,12 @@ namespace chip {
 namespace host {
 
 // ---------------------------------------------------------------- CRC-32C
-// crc32q has a 3-cycle latency and 1-cycle throughput: one dependency chain
-// runs at a third of the unit's rate.  Long buffers are cut into three
-// segments of CRC3_SEG bytes hashed in one interleaved loop, the segment
-// registers joined with shift(r) = the register after CRC3_SEG zero bytes,
-// a linear map applied as four 256-entry tables (built once from the 32
-// basis vectors).  A full 64 KiB snappy block is one pass + 16 bytes.
-namespace {
-constexpr size_t CRC3_SEG = 21840;  // 3 * 21840 + 16 = 65536
-
-__attribute__((target("sse4.2"))) uint32_t crc_zeros(uint32_t r, size_t n) {
-    uint64_t c = r;
-    for (size_t i = 0; i < n / 8; ++i) c = _mm_crc32_u64(c, 0);
-    return (uint32_t)c;
-}
-
-struct Crc3Tables {
-    uint32_t t[4][256];
-    Crc3Tables() {
-        uint32_t basis[32];
-        for (int i = 0; i < 32; ++i) basis[i] = crc_zeros(1u << i, CRC3_SEG);
-        for (int k = 0; k < 4; ++k)
-            for (int b = 0; b < 256; ++b) {
-                uint32_t v = 0;
-                for (int j = 0; j < 8; ++j)
-                    if (b >> j & 1) v ^= basis[8 * k + j];
-                t[k][b] = v;
-            }
-    }
-    uint32_t shift(uint32_t r) const {
-        return t[0][r & 255] ^ t[1][(r >> 8) & 255] ^ t[2][(r >> 16) & 255] ^ t[3][r >> 24];
-    }
-};
-}  // namespace
-
+// One crc32q chain.  A three-chain version (segments joined by a table shift)
+// ran 3x faster single-threaded (4.3 -> 13.2 GiB/s) but made the level-15
+// decode end to end 25-30 % slower on the GPU box (16 host threads beside the
+// DMA traffic; profiles/r1u_e2ed15_crc_ab.txt), so it was dropped.
 __attribute__((target("sse4.2"))) uint32_t crc32c(const uint8_t *p, size_t n) {
     uint64_t c = 0xFFFFFFFFu;
-    if (n >= 3 * CRC3_SEG) {
-        static const Crc3Tables T;
-        while (n >= 3 * CRC3_SEG) {
-            uint64_t a = c, b = 0, d = 0;
-            const uint8_t *pb = p + CRC3_SEG, *pd = p + 2 * CRC3_SEG;
-            for (size_t i = 0; i < CRC3_SEG; i += 8) {
-                uint64_t x, y, z;
-                std::memcpy(&x, p + i, 8);
-                std::memcpy(&y, pb + i, 8);
-                std::memcpy(&z, pd + i, 8);
-                a = _mm_crc32_u64(a, x);
-                b = _mm_crc32_u64(b, y);
-                d = _mm_crc32_u64(d, z);
-            }
-            c = T.shift(T.shift((uint32_t)a) ^ (uint32_t)b) ^ (uint32_t)d;
-            p += 3 * CRC3_SEG;
-            n -= 3 * CRC3_SEG;
-        }
-    }
     while (n >= 8) {
         uint64_t v;
         std::memcpy(&v, p, 8);

@@ -10,11 +10,13 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -m pytest tests -m gpu -x -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
-timeout -k 10 600 python3 bench.py > $O/bench_encode.log 2>&1
+timeout -k 10 600 python3 bench.py --verify-all > $O/bench_encode.log 2>&1
 timeout -k 10 600 python3 bench.py --mode decode --no-cpu-baseline > $O/bench_decode.log 2>&1
 timeout -k 10 600 python3 bench.py --k 8 --m 16 --no-cpu-baseline > $O/bench_8of16.log 2>&1
-timeout -k 10 600 python3 bench.py --mode bao --objects 512 --object-mib 32 --no-cpu-baseline > $O/bench_bao.log 2>&1
+timeout -k 10 600 python3 bench.py --mode bao --no-cpu-baseline > $O/bench_bao.log 2>&1
+timeout -k 10 600 python3 bench.py --mode pipeline --level 12 --verify-all > $O/bench_pipe12.log 2>&1
 timeout -k 10 600 python3 bench.py --mode e2e --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 > $O/bench_e2e15.log 2>&1
+timeout -k 10 600 python3 bench.py --mode e2e --level 12 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 > $O/bench_e2e12.log 2>&1
 timeout -k 10 600 python3 bench.py --mode e2e-decode --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 > $O/bench_e2ed15.log 2>&1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o stats --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-verify --no-aliased > $O/prof.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o fetch --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-aliased > $O/pmc_fetch.log 2>&1
