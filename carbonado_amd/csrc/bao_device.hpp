@@ -194,13 +194,6 @@ struct ChunkArgs {
     uint32_t *status;      // decode only
 };
 
-// Workgroup barrier that orders only LDS traffic (no wait for global stores).
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 __device__ __forceinline__ void wave_sync() {
     // Every LDS row a wave writes is read only by lanes of the same wave, and
     // a wave's DS instructions execute in order: a compiler-level fence is all
@@ -263,112 +256,6 @@ __device__ __forceinline__ void root_io(const ChunkArgs &a, uint64_t obj, const 
 
 __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
 
-// K3 SP 4 copy wave q of CW: copies the content of hash-wave regions
-// q, q + CW, ... of its workgroup (each region = 64 * CPL consecutive chunks of
-// one object) into their stream slots, chunk after chunk, so every store
-// instruction writes 1 KiB of consecutive stream bytes and a wave's stores run
-// sequentially through the stream (DRAM-friendly, unlike the hash waves' 64
-// scattered 128-B pieces per step).  A chunk is one wave access: lane l loads
-// content bytes [16 l, +16) and, since chunk slots sit at 8 (mod 16) when the
-// object base is 16-B aligned, stores the ALIGNED 16 B [16 l + 8, +16) = its
-// upper half + lane l+1's lower half (DPP wave_shl:1); lane 0 adds the 8-B
-// head, lane 63 the 8-B tail.  UN chunks per batch, the next batch's loads
-// issued before the current batch is stored.  Addresses are wave-uniform
-// (scalar registers); slot offsets advance incrementally (1024 + 64 c(i)).
-struct CopyCursor {
-    uint64_t obj, ci, end, off;
-    int region;
-    bool live;
-};
-
-template <int CPL, int CW>
-__device__ __forceinline__ bool copy_region(const ChunkArgs &a, int region, CopyCursor &c) {
-    const uint64_t span = 64ull * CPL;
-    const uint64_t tpo = (a.N + span - 1) / span;
-    for (; region < K3_WAVES; region += CW) {
-        const uint64_t wt = (uint64_t)blockIdx.x * K3_WAVES + region;
-        if (wt >= a.count * tpo) break;
-        c.obj = wt / tpo;
-        c.ci = (wt - c.obj * tpo) * span;
-        c.end = c.ci + span < a.N ? c.ci + span : a.N;
-        if (c.ci >= c.end) continue;
-        c.off = chunk_stream_off(c.ci, a.N);
-        c.region = region;
-        return c.live = true;
-    }
-    return c.live = false;
-}
-
-template <int CPL, int CW>
-__device__ __forceinline__ void copy_advance(const ChunkArgs &a, CopyCursor &c) {
-    if (++c.ci < c.end) {
-        c.off += 1024 + 64 * (uint64_t)parents_at(c.ci, a.N);
-    } else {
-        copy_region<CPL, CW>(a, c.region + CW, c);
-    }
-}
-
-template <int CPL, int CW, bool NTS>
-__device__ __forceinline__ void copy_wave(const ChunkArgs &a, int q) {
-    constexpr int UN = 8;
-    const int lane = threadIdx.x & 63;
-    if (a.n == 0) return;
-    CopyCursor cur;
-    copy_region<CPL, CW>(a, q, cur);
-    u32x4 v[UN];
-    uint8_t *dst[UN];
-    uint32_t clen[UN];
-    auto load_batch = [&](u32x4 (&vv)[UN], uint8_t *(&dd)[UN], uint32_t (&cl)[UN]) {
-#pragma unroll
-        for (int u = 0; u < UN; ++u) {
-            dd[u] = nullptr;
-            cl[u] = 0;
-            vv[u] = u32x4{0u, 0u, 0u, 0u};
-            if (!cur.live) continue;
-            const uint64_t rem = a.n - cur.ci * 1024;
-            cl[u] = rem < 1024 ? (uint32_t)rem : 1024u;
-            dd[u] = a.out + cur.obj * a.out_stride + cur.off;
-            const uint8_t *src = a.in + cur.obj * a.in_stride + cur.ci * 1024 + 16 * lane;
-            const uint32_t b = 16u * lane;
-            if (b + 16 <= cl[u]) vv[u] = *reinterpret_cast<const u32x4 *>(src);
-            else if (b < cl[u]) vv[u] = load16_partial(src, cl[u] - b);
-            copy_advance<CPL, CW>(a, cur);
-        }
-    };
-    load_batch(v, dst, clen);
-    while (dst[0]) {
-        u32x4 vn[UN];
-        uint8_t *dn[UN];
-        uint32_t cn[UN];
-        load_batch(vn, dn, cn);
-#pragma unroll
-        for (int u = 0; u < UN; ++u) {
-            uint8_t *d = dst[u];
-            if (!d) continue;
-            const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v[u].x, 0x130, 0xF, 0xF, false);  // wave_shl:1
-            const uint32_t ny = __builtin_amdgcn_update_dpp(0u, v[u].y, 0x130, 0xF, 0xF, false);
-            if (clen[u] == 1024) {
-                if (((uintptr_t)d & 15) == 8) {
-                    if (lane < 63) {
-                        const u32x4 o = {v[u].z, v[u].w, nx, ny};
-                        if (NTS) __builtin_nontemporal_store(o, reinterpret_cast<u32x4 *>(d + 16 * lane + 8));
-                        else *reinterpret_cast<u32x4 *>(d + 16 * lane + 8) = o;
-                    }
-                    if (lane == 0) store8<NTS>(d, u32x2{v[u].x, v[u].y});
-                    if (lane == 63) store8<NTS>(d + 1016, u32x2{v[u].z, v[u].w});
-                } else {
-                    store16_a8<NTS>(d + 16 * lane, v[u]);
-                }
-            } else {  // short last chunk of the object
-                const uint32_t b = 16u * lane;
-                if (b < clen[u]) store16_partial(d + b, v[u], clen[u] - b);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UN; ++u) { v[u] = vn[u]; dst[u] = dn[u]; clen[u] = cn[u]; }
-    }
-}
-
 // K3.  MODE 0 = encode (in = content, out = stream), MODE 1 = verify-decode
 // (in = stream, out = content), MODE 2 = per-node check (slices, scrub),
 // MODE 3 = encode in place (in = out = a stream whose chunk slots already
@@ -385,40 +272,24 @@ __device__ __forceinline__ void copy_wave(const ChunkArgs &a, int q) {
 // 3 = rows hold two steps (ping-pong) and every step stores one whole aligned
 //     128-B line of the stream per chunk (plus the head at step 0 and the
 //     tail at step 7), so no line is written in two halves.
-// 4 = copy waves: CW extra waves per workgroup (wave >= K3_WAVES) place the
-//     content of the workgroup's chunks into their stream slots while the
-//     K3_WAVES hash waves only hash and write parents (no global store sits
-//     in a hash wave's instruction stream).  The copy re-reads bytes the hash
-//     waves read moments before (L2 / Infinity Cache hits, not HBM).
-// 5 = store waves: the SP 0 stores, issued by CW extra waves that read the
-//     hash waves' LDS rows; two workgroup barriers per step (rows written ->
-//     stored -> overwritten), so no global store sits in a hash wave.
 // SU: unroll of the SP 3 store loop; SE: issue the SP 3 stores before (1) or
 // after (0) the next step's prefetch loads.
-template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int CW = 0>
-__global__ __launch_bounds__(64 * (K3_WAVES + CW)) void bao_chunk_kernel(ChunkArgs a) {
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0>
+__global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     constexpr int LOG = ilog2(CPL);
     constexpr int NSTEP = 8 * CPL;
     // SP 3: [pad 4 | step-parity-0 data 32 | step-parity-1 data 32] words per row
     // (68/4 = 17 is odd, so the lane-per-row ds_read_b128 stays conflict-free)
     constexpr int RW = SP == 3 ? 68 : ROWW;
-    static_assert(SP != 5 || (MODE == 0 && CW > 0), "SP 5 is the encode store-wave variant");
     __shared__ __attribute__((aligned(16))) uint32_t stage[K3_WAVES][64 * RW];
     auto dofs = [](int step) { return ROW0 + (SP == 3 ? (step & 1) * 32 : 0); };
     __shared__ uint64_t soff[2][K3_WAVES][64];  // stream offset of each lane's current chunk (by parity)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if constexpr (SP == 4) {
-        static_assert(MODE == 0 && CW > 0, "SP 4 is the encode copy-wave variant");
-        if (wave >= K3_WAVES) {
-            copy_wave<CPL, CW, NTS>(a, wave - K3_WAVES);
-            return;
-        }
-    }
     const int lane = threadIdx.x & 63;
     const uint64_t span = 64ull * CPL;
     const uint64_t tpo = (a.N + span - 1) / span;
     const uint64_t wt = (uint64_t)blockIdx.x * K3_WAVES + wave;
-    const bool wave_on = (SP != 5 || wave < K3_WAVES) && wt < a.count * tpo;
+    const bool wave_on = wt < a.count * tpo;
     const uint64_t obj = wave_on ? wt / tpo : 0;
     const uint64_t c0 = wave_on ? (wt - obj * tpo) * span : 0;
     const uint64_t lb = c0 + (uint64_t)lane * CPL;  // my first chunk
@@ -428,7 +299,7 @@ __global__ __launch_bounds__(64 * (K3_WAVES + CW)) void bao_chunk_kernel(ChunkAr
     uint32_t *st = stage[wave];
 
     uint64_t my_off = nmine ? chunk_stream_off(lb, a.N) : 0;  // stream offset of my current chunk
-    if (SP != 5 || wave < K3_WAVES) soff[0][wave][lane] = my_off;
+    soff[0][wave][lane] = my_off;
     if ((MODE == 0 || MODE == 3) && ob && wave_on && c0 == 0 && lane == 0)  // u64 LE content-length header
         *reinterpret_cast<uint64_t *>(ob) = a.n;
     if ((MODE == 1 || MODE == 2) && wave_on && c0 == 0 && lane == 0 && *reinterpret_cast<const uint64_t *>(ib) != a.n && a.status)
@@ -507,8 +378,7 @@ __global__ __launch_bounds__(64 * (K3_WAVES + CW)) void bao_chunk_kernel(ChunkAr
     // [16k-8, 16k+8): the previous step's last 8 bytes live in the row's carry
     // words, so every full piece is one aligned dwordx4 store read from LDS.
     // Chunk head (k = 0) and tail (k = 64) are 8-byte halves.
-    // SP 0: stores of the issuing wave's own rows (w = wave); SP 5: a store
-    // wave issues them for hash wave w.
+    // SP 0: stores of the issuing wave's own rows (wv = wave)
     auto stream_step = [&](int wv, int g) {
         const int j = g >> 3, s = g & 7, gl = lane & 7;
         const uint64_t wt_w = (uint64_t)blockIdx.x * K3_WAVES + wv;
@@ -691,17 +561,6 @@ __global__ __launch_bounds__(64 * (K3_WAVES + CW)) void bao_chunk_kernel(ChunkAr
         }
     };
 
-    if constexpr (SP == 5) {  // store waves: follow the hash waves step by step
-        if (wave >= K3_WAVES) {
-            for (int g = 0; g < NSTEP; ++g) {
-                lds_barrier();  // A(g): rows of step g written
-                for (int wv = wave - K3_WAVES; wv < K3_WAVES; wv += CW) stream_step(wv, g);
-                if (g + 1 < NSTEP) lds_barrier();  // B(g): rows of step g stored
-            }
-            return;
-        }
-    }
-
     uint32_t h[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) h[w] = IV(w);
@@ -712,11 +571,10 @@ __global__ __launch_bounds__(64 * (K3_WAVES + CW)) void bao_chunk_kernel(ChunkAr
     load_step(0, pre);
     for (int g = 0; g < NSTEP; ++g) {
         const int j = g >> 3, s = g & 7;
-        if (SP == 5 && g > 0) lds_barrier();  // B(g-1): the store waves are done with the rows
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             uint32_t *row = st + (t * 8 + (lane >> 3)) * RW;
-            if (MODE == 0 && (SP == 0 || SP == 5) && (lane & 7) == 7)  // carry the previous step's last 8 bytes
+            if (MODE == 0 && SP == 0 && (lane & 7) == 7)  // carry the previous step's last 8 bytes
                 *reinterpret_cast<u32x2 *>(row + 2) = *reinterpret_cast<const u32x2 *>(row + ROW0 + 30);
             *reinterpret_cast<u32x4 *>(row + dofs(s) + (lane & 7) * 4) = pre[t];
         }
@@ -727,8 +585,7 @@ __global__ __launch_bounds__(64 * (K3_WAVES + CW)) void bao_chunk_kernel(ChunkAr
             if ((uint64_t)(j + 1) < nmine) my_off += 1024 + 64 * (uint64_t)parents_at(ni, a.N);
             soff[(j + 1) & 1][wave][lane] = my_off;
         }
-        if (SP == 5) lds_barrier();  // A(g)
-        else wave_sync();
+        wave_sync();
         if (MODE == 0 && ob && SP == 3 && SE) stream_lines(g);
         if (g + 1 < NSTEP) load_step(g + 1, pre);  // in flight during the compressions
         if (MODE == 0 && ob && SP == 0) stream_step(wave, g);
@@ -942,7 +799,7 @@ inline uint64_t bao_scratch_len_t(uint64_t n, uint64_t count) {
 }
 
 // Enqueue K3 then one K4 launch per remaining level.
-template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int CW = 0>
+template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0>
 hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
                    void *d_scratch, hipStream_t stream, size_t pad_lds = 0 /* tuning: occupancy probe */) {
@@ -960,8 +817,8 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
     ca.hash = d_hash; ca.status = d_status;
     const uint64_t waves = count * ((N + 64ull * BAO_CPL - 1) / (64ull * BAO_CPL));
     const uint64_t blocks = (waves + K3_WAVES - 1) / K3_WAVES;
-    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, CW>), dim3((unsigned)blocks),
-                       dim3(64 * (K3_WAVES + CW)), pad_lds,
+    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE>), dim3((unsigned)blocks),
+                       dim3(K3_TPB), pad_lds,
                        stream, ca);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -50,13 +50,12 @@ struct V {
     size_t pad_lds;
 };
 
-template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int CW = 0>
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0>
 V mk(bool stream, size_t pad_lds = 0) {
     char b[96];
-    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d cw%d pad%zu",
-             MODE == 3 ? "in-place" : MODE ? "decode" : "encode", CPL,
-             NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, CW, pad_lds);
-    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE, CW>, CPL, stream, pad_lds};
+    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d pad%zu", MODE == 3 ? "in-place" : MODE ? "decode" : "encode",
+             CPL, NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, pad_lds);
+    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE>, CPL, stream, pad_lds};
 }
 
 int main(int argc, char **argv) {
