@@ -33,7 +33,7 @@ struct Args {
 // MAP 4: object o is processed by the workgroups of XCD o % 8 only, which walk
 // its tiles together (each XCD's write set = 8 sequential streams).
 // ROT: wave w starts its 8 stores at shard (w % 8) (spread instantaneous streams).
-template <int TPB, int MAP, int CH, int STORE, bool LOADNT, bool ROT>
+template <int TPB, int MAP, int CH, int STORE, bool LOADNT, bool ROT, int NW = 8>
 __global__ __launch_bounds__(TPB) void k_mix(Args a) {
     constexpr uint64_t TILE = TPB * 16;
     const uint64_t tpo = a.C / TILE, T = tpo * a.count;
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(TPB) void k_mix(Args a) {
         }
         const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(ob, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
+        for (int jj = 0; jj < NW; ++jj) {
             const int j = ROT ? ((jj + wave) & 7) : jj;
             u32x4 w;
             if (ROT) {
@@ -119,18 +119,16 @@ int main(int argc, char **argv) {
         std::string name;
         void (*fn)(Args);
         int tpb, grid;
+        double bpi;  // bytes moved per input byte
     };
 #define VV(TPB, MAP, CH, ST, LNT, ROT, BPC) \
-    V{#TPB " MAP" #MAP " CH" #CH " st" #ST " lnt" #LNT " rot" #ROT " bpc" #BPC, k_mix<TPB, MAP, CH, ST, LNT, ROT>, TPB, 256 * BPC}
+    V{#TPB " MAP" #MAP " CH" #CH " st" #ST " lnt" #LNT " rot" #ROT " bpc" #BPC, k_mix<TPB, MAP, CH, ST, LNT, ROT>, TPB, 256 * BPC, 3.0}
+#define V4(TPB, MAP, CH, ST, BPC) \
+    V{"4r4w " #TPB " MAP" #MAP " CH" #CH " st" #ST " bpc" #BPC, k_mix<TPB, MAP, CH, ST, false, false, 4>, TPB, 256 * BPC, 2.0}
     std::vector<V> vs = {
-        VV(256, 3, 64, -1, false, false, 4),  // stream_probe's best (product schedule)
-        VV(256, 3, 64, 0, false, false, 4),   VV(256, 3, 64, 16, false, false, 4),
-        VV(256, 3, 64, 17, false, false, 4),  VV(256, 3, 64, 3, false, false, 4),
-        VV(256, 3, 64, 2, false, false, 4),   VV(256, 3, 64, -1, true, false, 4),
-        VV(256, 3, 64, -1, false, true, 4),   VV(64, 3, 256, -1, false, false, 16),
-        VV(64, 3, 256, 0, false, false, 16),  VV(256, 4, 1, -1, false, false, 4),
-        VV(256, 4, 1, 0, false, false, 4),    VV(256, 3, 256, -1, false, false, 4),
-        VV(256, 3, 16, -1, false, false, 8),  VV(512, 3, 32, -1, false, false, 2),
+        VV(256, 3, 64, -1, false, false, 4), VV(512, 3, 32, -1, false, false, 2),
+        V4(256, 3, 64, -1, 4),               V4(256, 3, 64, 0, 4),
+        V4(512, 3, 32, -1, 2),               V4(256, 3, 16, -1, 8),
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -161,7 +159,7 @@ int main(int argc, char **argv) {
         auto t = ms[i];
         std::sort(t.begin(), t.end());
         const char *name = i < vs.size() ? vs[i].name.c_str() : i == vs.size() ? "read-only (input)" : "write-only (output)";
-        const double bytes = i < vs.size() ? 3.0 * count * n : i == vs.size() ? 1.0 * count * n : 2.0 * count * n;
+        const double bytes = i < vs.size() ? vs[i].bpi * count * n : i == vs.size() ? 1.0 * count * n : 2.0 * count * n;
         printf("%-40s median %7.3f ms min %7.3f -> %7.1f GB/s (median) %7.1f (best)\n", name, t[t.size() / 2], t[0],
                bytes / (t[t.size() / 2] * 1e-3) / 1e9, bytes / (t[0] * 1e-3) / 1e9);
     }
