@@ -47,15 +47,21 @@ def parse():
     ap.add_argument("--object-mib", type=float, default=16.0)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=8)
-    ap.add_argument("--mode", choices=["encode", "decode", "bao", "pipeline", "e2e", "e2e-decode"], default="encode",
+    ap.add_argument("--mode", choices=["encode", "decode", "bao", "pipeline", "e2e", "e2e-decode", "scrub", "hasher"],
+                    default="encode",
                     help="pipeline: device-resident encode() at --level (Bao/Zfec bits; 12 = zfec fused into "
-                         "bao); e2e: encode() at --level from pinned HOST memory to host memory (H2D+kernels+D2H)")
+                         "bao); e2e: encode() at --level from pinned HOST memory to host memory (H2D+kernels+D2H); "
+                         "scrub: scrub() of level-12 streams with one corrupted shard (host API, decoding.rs:151-212); "
+                         "hasher: BaoHasher update()+finalize() over the objects in 4 MiB appends (utils.rs:104-137)")
     ap.add_argument("--level", type=int, default=12, help="e2e mode: Format bits (Bao|Zfec = 12)")
     ap.add_argument("--slots", type=int, default=3, help="e2e mode: pipeline slots (streams)")
     ap.add_argument("--host-threads", type=int, default=16,
                     help="e2e mode: host threads for the Snappy/Ecies stages (the GPU box's CPU share is 16)")
     ap.add_argument("--erase", default="1,2", help="decode mode: shards dropped")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of each CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="second CPU baseline with objects in parallel on this many host threads (SURVEY 8d: "
+                         "'all host cores'; the GPU box's CPU share is 16); 0 or 1 = the 1-thread one only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--verify-all", action="store_true",
@@ -70,7 +76,10 @@ def parse():
     ap.add_argument("--traffic-json", default="auto",
                     help="PMC summary (profiles/*_pmc.json, tools/pmc_summary.py) with the measured HBM "
                          "bytes per launch of this kernel; 'auto' = newest matching file, 'none' = null")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.mode in ("scrub", "hasher") and args.objects == ap.get_default("objects"):
+        args.objects = 64  # host-API paths: a bounded host-memory working set
+    return args
 
 
 def setup_dist():
@@ -115,9 +124,11 @@ def measured_traffic(spec: str, kernel_sym: str, alg_bytes: int):
     return None, None
 
 
-def cpu_baseline(args, n: int, sample_obj: bytes | None):
+def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
     """Time the CPU oracle (scalar fec.c-style restatement of zfec-rs / the
-    BLAKE3+bao restatement) on whole objects, 1 thread, ~cpu_seconds of work."""
+    BLAKE3+bao restatement) on whole objects for ~cpu_seconds: 1 thread (the
+    reference crate is single-threaded), or `threads` host threads each
+    working through objects of its own (ctypes releases the GIL)."""
     from oracle import oracle as O
     import numpy as np
     obj = np.frombuffer(sample_obj, np.uint8) if sample_obj is not None else O.fill_object(SEED, 0, n)
@@ -131,15 +142,29 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
         import hashlib
         sk = hashlib.sha256(b"carbonado-amd bench receiver").digest()
         enc_obj, h_obj, inf_obj = O.c_encode_full(obj, args.level, pub, eph if eph else bytes(32), bytes(16))
+    if args.mode == "scrub":
+        enc_obj, h_obj, inf_obj = O.encode(obj, 12)
+        bad = bytearray(enc_obj)
+        bad[scrub_corrupt_offset(len(obj), 0)] ^= 0x40
+        zc, zpad, zC = O.zfec_encode(obj, 4, 8)
     if args.mode == "decode":
         z, pad, C = O.zfec_encode(obj, args.k, args.m)
         keep = [i for i in range(args.m) if str(i) not in args.erase.split(",")]
         shares = [z[i * C:(i + 1) * C] for i in keep]
-    done = 0
-    t0 = time.perf_counter()
-    while True:
+    def one():
         if args.mode == "bao":
             O.bao_encode(obj)
+        elif args.mode == "hasher":
+            O.blake3(obj)
+        elif args.mode == "scrub":
+            # the reference's scrub: bao decode (fails), zfec decode of the
+            # intact shards, re-encode; restated with the C oracle's pieces
+            try:
+                O.bao_decode(bytes(bad), h_obj)
+            except Exception:
+                pass
+            keep_s = [i for i in range(8) if i != 0][:4]
+            O.encode(O.zfec_decode_shares([zc[i * zC:(i + 1) * zC] for i in keep_s], keep_s, zpad), 12)
         elif args.mode == "e2e-decode":
             cur = O.decode(h_obj, enc_obj, inf_obj["padding_len"], args.level & 12) if args.level & 12 else enc_obj
             if args.level & 1:
@@ -155,17 +180,57 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None):
             O.zfec_decode_shares(shares, keep, pad, args.k, args.m)
         else:
             O.zfec_encode(obj, args.k, args.m)
-        done += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or done >= 4096:
-            break
-    what = {"bao": "bao encode", "e2e": f"encode() level {args.level}", "pipeline": f"encode() level {args.level}", "e2e-decode": f"decode() level {args.level}",
+
+    def worker(deadline):
+        c = 0
+        while True:
+            one()
+            c += 1
+            if time.perf_counter() >= deadline or c >= 4096:
+                return c
+    t0 = time.perf_counter()
+    if threads <= 1:
+        done = worker(t0 + args.cpu_seconds)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(threads) as ex:
+            done = sum(ex.map(worker, [t0 + args.cpu_seconds] * threads))
+    el = time.perf_counter() - t0
+    what = {"bao": "bao encode", "e2e": f"encode() level {args.level}", "pipeline": f"encode() level {args.level}",
+            "hasher": "BLAKE3 of the content", "scrub": "scrub() restated: bao decode + zfec decode + encode()", "e2e-decode": f"decode() level {args.level}",
             "decode": f"zfec {args.k}-of-{args.m} decode, erased {args.erase}"}.get(
         args.mode, f"zfec {args.k}-of-{args.m} encode")
-    return {"value": round(done * n / el / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+    return {"value": round(done * n / el / 2**30, 4), "unit": "GiB/s", "cores": max(1, threads), "kind": "port",
             "sample": f"{done} x {n} B objects ({what}) through oracle/carbonado_oracle.c"
                       f"{' + host_oracle.c' if args.mode.startswith('e2e') and args.level & 3 else ''}, scalar "
-                      f"restatement of the reference crates, 1 thread, {el:.1f} s"}
+                      f"restatement of the reference crates, "
+                      f"{'1 thread' if threads <= 1 else f'{threads} threads, objects in parallel'}, {el:.1f} s"}
+
+
+def scrub_corrupt_offset(n: int, o: int) -> int:
+    """Stream offset of a content byte inside data shard o % 4 of a level-12
+    encoding of n bytes (one byte per object is flipped for --mode scrub):
+    chunk i of the bao stream sits at 8 + 1024 i + 64 (P(i) + c(i))."""
+    unit = 1024 * 4
+    C = -(-n // unit) * unit // 4
+    N = 8 * C // 1024
+
+    def clog2(x):
+        return 0 if x <= 1 else (x - 1).bit_length()
+
+    def c_at(s):
+        cl = clog2(N - s)
+        return cl if s == 0 else min((s & -s).bit_length() - 1, cl)
+
+    def p_before(s):
+        total, cnt, L = 0, N, 1
+        while cnt > 1:
+            total += min((s + (1 << L) - 1) >> L, cnt // 2)
+            cnt = (cnt + 1) // 2
+            L += 1
+        return total
+    i = (o % 4) * (C // 1024) + (C // 1024) // 3
+    return 8 + 1024 * i + 64 * (p_before(i) + c_at(i)) + 517
 
 
 class Workload:
@@ -226,6 +291,53 @@ class Workload:
             fused = " (zfec writes the shards into their bao chunk slots; bao hashes in place)" if lv & 12 == 12 else ""
             self.kernel = f"encode() level {lv} on the device: gf_apply_kernel + bao_chunk_kernel + parent levels{fused}"
             self.kernel_sym = "pipeline"
+        elif args.mode == "scrub":
+            import numpy as np
+            import carbonado_amd as ca
+            host = self.inp.cpu().numpy()
+            del self.inp
+            torch.cuda.empty_cache()
+            self.inp = torch.from_numpy(host)
+            self.encs, self.hashes_h, self.infos, self.bads = [], [], [], []
+            for o in range(count):
+                enc, h, info = ca.encode(b"", host[o], 12)
+                bad = np.frombuffer(enc, np.uint8).copy()
+                bad[scrub_corrupt_offset(n, o)] ^= 0x40
+                self.encs.append(enc)
+                self.hashes_h.append(h)
+                self.infos.append(info)
+                self.bads.append(bad)
+            self.fixed = [None] * count
+
+            def step():
+                for o in range(count):
+                    self.fixed[o] = ca.decoding.scrub(self.bads[o], self.hashes_h[o], self.infos[o])
+            self.step = step
+            self.blen = len(self.encs[0])
+            self.alg_bytes = count * 2 * self.blen  # PCIe: the damaged stream up, the repaired stream down
+            self.kernel = ("scrub(): H2D + bao node check + zfec decode of intact shards + fused re-encode + D2H, "
+                           "one call per object (host API)")
+            self.kernel_sym = "scrub"
+        elif args.mode == "hasher":
+            import numpy as np
+            from carbonado_amd.utils import BaoHasher
+            host = self.inp.cpu().numpy().reshape(-1)
+            del self.inp
+            torch.cuda.empty_cache()
+            self.inp = torch.from_numpy(host.reshape(count, n))
+            piece = 4 << 20
+            self.pieces = [host[i:i + piece] for i in range(0, host.size, piece)]
+            self.digest = None
+
+            def step():
+                h = BaoHasher()
+                for p in self.pieces:
+                    h.update(p)
+                self.digest = bytes(h.finalize())
+            self.step = step
+            self.alg_bytes = host.size  # PCIe: the content up (the hash comes back)
+            self.kernel = "BaoHasher: H2D appends into a grow-only HBM buffer + bao kernels at finalize()"
+            self.kernel_sym = "hasher"
         elif args.mode == "e2e-decode":
             import hashlib
             from carbonado_amd.encoding import public_key
@@ -407,6 +519,10 @@ class Workload:
                   self.h_hash[0].numpy().tobytes() == h)
         elif self.args.mode == "decode":
             ok = self.out[0, :self.n].cpu().numpy().tobytes() == sample
+        elif self.args.mode == "scrub":
+            ok = all(self.fixed[o] == self.encs[o] for o in range(self.count))
+        elif self.args.mode == "hasher":
+            ok = self.digest == O.blake3(self.inp.numpy().reshape(-1))
         elif self.args.mode == "pipeline":
             enc, h, _ = O.encode(sample, self.args.level)
             ok = (self.out[0, :self.blen].cpu().numpy().tobytes() == enc and
@@ -468,6 +584,11 @@ def main():
             workload = f"bao encode, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "pipeline":
             workload = f"encode() level {args.level}, {args.objects} x {args.object_mib:g} MiB objects per GPU"
+        elif args.mode == "scrub":
+            workload = (f"scrub() of {args.objects} level-12 streams of {args.object_mib:g} MiB objects, one "
+                        f"corrupted byte each, host buffers")
+        elif args.mode == "hasher":
+            workload = f"BaoHasher over {args.objects} x {args.object_mib:g} MiB in 4 MiB appends, host buffers"
         elif args.mode == "e2e":
             workload = (f"encode() level {args.level} host->HBM->host (pinned), {args.objects} x "
                         f"{args.object_mib:g} MiB objects per GPU")
@@ -478,7 +599,8 @@ def main():
             workload = f"zfec {k}-of-{m} {args.mode}, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         res = {
             "metric": METRIC if args.mode == "encode" and (k, m) == (4, 8) and n == 16 << 20 else
-            (f"GiB/s {workload}" if args.mode.startswith("e2e") else f"GiB/s device-resident {workload}"),
+            (f"GiB/s {workload}" if args.mode.startswith("e2e") or args.mode in ("scrub", "hasher")
+             else f"GiB/s device-resident {workload}"),
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -500,11 +622,12 @@ def main():
                          "min_launch_ms": round(min(launch_ms), 4)},
             "verified_object0": verified,
         }
-        if args.mode.startswith("e2e"):
+        if args.mode.startswith("e2e") or args.mode in ("scrub", "hasher"):
             res["roofline"].update({"bound": "pcie", "peak": 2 * 63.0,
                                     "frac": round(achieved / 126.0, 4),
                                     "note": "PCIe Gen5 x16, 63 GB/s per direction (spec), H2D and D2H overlapped"})
-            res["data"] = "synthetic (uniform random bytes), pinned host buffers"
+            res["data"] = ("synthetic (uniform random bytes), pinned host buffers" if args.mode.startswith("e2e")
+                           else "synthetic (uniform random bytes), pageable host buffers (numpy / bytes)")
         if args.mode == "bao" or (args.mode == "pipeline" and args.level & 4):
             # BLAKE3 compressions: one per 64-B block of content plus one per parent node;
             # 7 rounds x 8 G x 12 VALU lane-ops (a+b+m as one v_add3_u32).
@@ -523,6 +646,12 @@ def main():
                                        "BLAKE3 compression (content blocks + parents)"
                                        + ("; step = zfec kernel (HBM-bound) + bao kernels (VALU-bound), "
                                           "achieved over the whole step" if args.mode == "pipeline" else "")}
+        if args.mode in ("encode", "decode") and k == 4 and not args.dry_run:
+            from carbonado_amd import _lib
+            rows = m if args.mode == "encode" else k  # decode writes the k data shards
+            res["roofline"]["schedule"] = {"k4": _lib.lib().chip_zfec_k4_schedule(rows), "rows": rows,
+                                           "note": "zfec 4-of-8 schedule picked on this box by the first launch "
+                                                   "(0 = 2-tile super-tiles at 2 WG/CU, 1 = 1 tile at 4 WG/CU)"}
         if verified_all is not None:
             res["verified_all_objects"] = verified_all
         if aliased is not None:
@@ -546,6 +675,9 @@ def main():
             res["dry_run"] = True
         elif not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args, n, sample)
+            threads = min(args.cpu_threads, os.cpu_count() or 1)
+            if threads > 1:
+                res["cpu_baseline_all_cores"] = cpu_baseline(args, n, sample, threads)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

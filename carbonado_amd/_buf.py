@@ -28,3 +28,35 @@ def check(status: int) -> None:
             raw = _lib.lib().chip_last_device_error()
             detail = raw.decode() if raw else ""
         raise status_to_error(status, detail)
+
+
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+_BYTES_DATA = bytes.__basicsize__ - 1  # offset of ob_sval in a CPython bytes object
+
+
+class OutBytes:
+    """An output buffer the C-ABI writes into that becomes the returned
+    `bytes` without a copy when the call fills it exactly (the reference
+    returns its Vec<u8> by move; a numpy buffer + tobytes() costs a second
+    pass over every output byte).  The bytes object is private until
+    result() hands it out, so filling it in place is safe.  A shorter result
+    is sliced (one copy, as before).  (No huge-page hint: with THP defrag on
+    "madvise" the kernel compacts memory on the fault path, and a 64-object
+    scrub bench went from 13.5 to 30.7 ms per object with MADV_HUGEPAGE.)"""
+
+    __slots__ = ("cap", "_b")
+
+    def __init__(self, cap: int):
+        self.cap = cap
+        self._b = _new_bytes(None, max(cap, 1))
+
+    def ptr(self) -> ctypes.c_void_p:
+        return ctypes.c_void_p(id(self._b) + _BYTES_DATA)
+
+    def result(self, n: int) -> bytes:
+        b, self._b = self._b, None
+        if n == self.cap and n:
+            return b
+        return b[:n]

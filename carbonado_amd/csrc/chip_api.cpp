@@ -82,13 +82,34 @@ struct Slot {
     DevBuf stage;
 };
 
+// Pinned ring for copies between PAGEABLE host memory and HBM (see h2d/d2h).
+struct Staging {
+    static constexpr int R = 4;
+    static constexpr size_t PIECE = size_t(4) << 20;
+    uint8_t *ring = nullptr;
+    hipEvent_t ev[R] = {};
+    bool armed[R] = {};
+    unsigned next = 0;  // ring slot of the next piece (rotates across calls)
+    void release() {
+        for (int k = 0; k < R; ++k) {
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
+            ev[k] = nullptr;
+            armed[k] = false;
+        }
+        if (ring) (void)hipHostFree(ring);
+        ring = nullptr;
+    }
+};
+
 struct Ctx {
     bool ready = false;
     int dev = -1;  // device the stream and buffers live on
     hipStream_t stream = nullptr;
     DevBuf in, mid, out, scratch, small, x1, x2, flags;
     std::vector<Slot> slots;
+    Staging stage;
     void release() {
+        stage.release();
         // best effort (at process teardown the runtime may already be gone)
         for (DevBuf *b : {&in, &mid, &out, &scratch, &small, &x1, &x2, &flags}) {
             if (b->p) (void)hipFree(b->p);
@@ -199,6 +220,188 @@ int ctx_get(Ctx **out) {
     }
     *out = &c;
     return CHIP_OK;
+}
+
+// ---- host <-> HBM copies of the single-object calls -----------------------
+// The runtime copies PAGEABLE host memory by pinning the caller's range: fast
+// (55 GB/s) once a range is pinned, but pinning a range it has not seen costs
+// ~24 ms per 34 MiB, and every fresh Vec / bytes the crate hands over is such a
+// range.  Pageable buffers therefore go through a pinned 4 x 4 MiB ring, the
+// CPU copy of one piece overlapping the DMA of the next (~1.4 ms per 34 MiB
+// resident, ~6.4 ms into untouched memory, tools/pageable_probe.hip,
+// profiles/r1w_pageable_probe.txt).  Pinned (hipHostMalloc'd / registered)
+// memory and small copies go direct.  CHIP_HOST_COPY=direct|staged forces
+// one path (A/B runs).
+constexpr size_t kStageMin = size_t(256) << 10;
+
+int host_copy_mode() {  // 0 auto, 1 direct, 2 staged
+    static const int m = [] {
+        const char *e = std::getenv("CHIP_HOST_COPY");
+        if (!e) return 0;
+        if (!std::strcmp(e, "direct")) return 1;
+        if (!std::strcmp(e, "staged")) return 2;
+        return 0;
+    }();
+    return m;
+}
+
+bool host_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: not an error for the caller
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+bool staged(const void *host, size_t n) {
+    const int m = host_copy_mode();
+    if (m == 1 || n < kStageMin) return false;
+    return m == 2 || !host_pinned(host);
+}
+
+// memcpy between the ring and pageable memory on a few threads: one thread
+// moves ~20 GB/s, the ring DMA 55 GB/s.  A persistent pool (CHIP_COPY_THREADS
+// total, default 4, 1 = the calling thread only); a caller that finds the
+// pool busy (another thread's copy) copies alone.
+class CopyPool {
+  public:
+    static CopyPool &get() {
+        static CopyPool *p = new CopyPool();  // never destroyed: workers park on the condvar at exit
+        return *p;
+    }
+    void copy(void *dst, const void *src, size_t n) {
+        if (workers_ == 0 || n < (size_t(1) << 20) || !job_.try_lock()) {
+            std::memcpy(dst, src, n);
+            return;
+        }
+        const size_t parts = workers_ + 1;
+        size_t part = (n + parts - 1) / parts;
+        part = (part + 65535) & ~size_t(65535);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            d_ = static_cast<uint8_t *>(dst);
+            s_ = static_cast<const uint8_t *>(src);
+            n_ = n;
+            part_ = part;
+            pending_ = workers_;
+            ++gen_;
+        }
+        cv_.notify_all();
+        std::memcpy(dst, src, std::min(part, n));
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_.wait(lk, [&] { return pending_ == 0; });
+        }
+        job_.unlock();
+    }
+
+  private:
+    CopyPool() {
+        int t = 4;
+        if (const char *e = std::getenv("CHIP_COPY_THREADS")) t = std::max(1, std::min(32, std::atoi(e)));
+        workers_ = t - 1;
+        for (int i = 1; i <= workers_; ++i) std::thread([this, i] { run(i); }).detach();
+    }
+    void run(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint8_t *d;
+            const uint8_t *s;
+            size_t n, part;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                d = d_, s = s_, n = n_, part = part_;
+            }
+            const size_t lo = std::min(n, i * part), hi = std::min(n, lo + part);
+            if (hi > lo) std::memcpy(d + lo, s + lo, hi - lo);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    int workers_ = 0;
+    std::mutex job_, mu_;
+    std::condition_variable cv_, done_;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    uint8_t *d_ = nullptr;
+    const uint8_t *s_ = nullptr;
+    size_t n_ = 0, part_ = 0;
+};
+
+hipError_t stage_slot(Staging &sg, int k) {  // wait until ring slot k is free
+    if (!sg.armed[k]) return hipSuccess;
+    sg.armed[k] = false;
+    return hipEventSynchronize(sg.ev[k]);
+}
+
+hipError_t stage_init(Staging &sg) {
+    if (sg.ring) return hipSuccess;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&sg.ring), Staging::R * Staging::PIECE,
+                                 hipHostMallocDefault);
+    if (e != hipSuccess) {
+        sg.ring = nullptr;
+        return e;
+    }
+    for (int k = 0; k < Staging::R && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&sg.ev[k], hipEventDisableTiming);
+    return e;
+}
+
+// Enqueue host -> HBM on s.  On return `src` may be reused (its bytes are in
+// the ring or already copied); later work on s sees the data.
+hipError_t h2d(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    if (!staged(src, n)) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s);
+    hipError_t e = stage_init(sg);
+    for (size_t off = 0; off < n && e == hipSuccess; off += Staging::PIECE) {
+        const size_t len = std::min(Staging::PIECE, n - off);
+        const int k = sg.next++ % Staging::R;
+        if ((e = stage_slot(sg, k)) != hipSuccess) break;
+        CopyPool::get().copy(sg.ring + k * Staging::PIECE, static_cast<const uint8_t *>(src) + off, len);
+        e = hipMemcpyAsync(static_cast<uint8_t *>(dst) + off, sg.ring + k * Staging::PIECE, len,
+                           hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipEventRecord(sg.ev[k], s);
+        if (e == hipSuccess) sg.armed[k] = true;
+    }
+    return e;
+}
+
+// HBM -> host after the work already on s; returns when `dst` holds the bytes.
+hipError_t d2h(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    if (!staged(dst, n)) {
+        hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
+        return e == hipSuccess ? hipStreamSynchronize(s) : e;
+    }
+    hipError_t e = stage_init(sg);
+    if (e != hipSuccess) return e;
+    const size_t np = (n + Staging::PIECE - 1) / Staging::PIECE;
+    const unsigned base = sg.next;
+    sg.next += (unsigned)np;
+    auto slot = [&](size_t j) { return (int)((base + j) % Staging::R); };
+    auto issue = [&](size_t j) {
+        const int k = slot(j);
+        hipError_t r = stage_slot(sg, k);
+        const size_t off = j * Staging::PIECE;
+        if (r == hipSuccess)
+            r = hipMemcpyAsync(sg.ring + k * Staging::PIECE, static_cast<const uint8_t *>(src) + off,
+                               std::min(Staging::PIECE, n - off), hipMemcpyDeviceToHost, s);
+        if (r == hipSuccess) r = hipEventRecord(sg.ev[k], s);
+        if (r == hipSuccess) sg.armed[k] = true;
+        return r;
+    };
+    for (size_t j = 0; j < np && j < (size_t)Staging::R && e == hipSuccess; ++j) e = issue(j);
+    for (size_t j = 0; j < np && e == hipSuccess; ++j) {
+        const int k = slot(j);
+        if ((e = stage_slot(sg, k)) != hipSuccess) break;
+        const size_t off = j * Staging::PIECE;
+        CopyPool::get().copy(static_cast<uint8_t *>(dst) + off, sg.ring + k * Staging::PIECE,
+                             std::min(Staging::PIECE, n - off));
+        if (j + Staging::R < np) e = issue(j + Staging::R);
+    }
+    return e;
 }
 
 bool valid_km(uint32_t k, uint32_t m) { return k >= 1 && m >= k && m <= 256; }
@@ -678,11 +881,11 @@ int chip_zfec_encode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t n, uint
     if (n) {
         CHIP_HIP(grow(c->in, n));
         CHIP_HIP(grow(c->out, total));
-        CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+        CHIP_HIP(h2d(c->stage, c->in.p, in, n, c->stream));
         GfPlan p = encode_plan(k, m, C, zfec_enc_matrix(k, m));
         GfLaunch L{static_cast<const uint8_t *>(c->in.p), static_cast<uint8_t *>(c->out.p), 0, 0, n, C, 1};
         CHIP_HIP(gf_apply(p, L, c->stream));
-        CHIP_HIP(hipMemcpyAsync(out, c->out.p, total, hipMemcpyDeviceToHost, c->stream));
+        CHIP_HIP(d2h(c->stage, out, c->out.p, total, c->stream));
         CHIP_HIP(hipStreamSynchronize(c->stream));
     }
     *padding = pad;
@@ -727,13 +930,13 @@ int chip_zfec_decode_shares(uint32_t k, uint32_t m, const uint8_t *const *shares
         for (uint32_t s = 0; s < k; ++s) {
             sel[s] = idx[pos[s]];
             slot_off[s] = (uint64_t)s * chunk_len;
-            CHIP_HIP(hipMemcpyAsync(static_cast<uint8_t *>(c->in.p) + slot_off[s], shares[pos[s]],
-                                    chunk_len, hipMemcpyHostToDevice, c->stream));
+            CHIP_HIP(h2d(c->stage, static_cast<uint8_t *>(c->in.p) + slot_off[s], shares[pos[s]], chunk_len,
+                         c->stream));
         }
         st = zfec_decode_device(k, m, static_cast<const uint8_t *>(c->in.p), 0, slot_off, sel, chunk_len,
                                 1, static_cast<uint8_t *>(c->out.p), 0, c->stream);
         if (st != CHIP_OK) return st;
-        if (olen) CHIP_HIP(hipMemcpyAsync(out, c->out.p, olen, hipMemcpyDeviceToHost, c->stream));
+        if (olen) CHIP_HIP(d2h(c->stage, out, c->out.p, olen, c->stream));
         CHIP_HIP(hipStreamSynchronize(c->stream));
     }
     *out_len = olen;
@@ -871,10 +1074,10 @@ int chip_bao_encode(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_ca
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
     CHIP_HIP(grow(c->in, n));
-    if (n) CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+    if (n) CHIP_HIP(h2d(c->stage, c->in.p, in, n, c->stream));
     st = bao_encode_ctx(c, static_cast<const uint8_t *>(c->in.p), n, true, hash);
     if (st != CHIP_OK) return st;
-    CHIP_HIP(hipMemcpyAsync(out, c->out.p, blen, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(d2h(c->stage, out, c->out.p, blen, c->stream));
     CHIP_HIP(hipStreamSynchronize(c->stream));
     *out_len = blen;
     return CHIP_OK;
@@ -886,7 +1089,7 @@ int chip_blake3(const uint8_t *in, uint64_t n, uint8_t hash[CHIP_HASH_LEN]) {
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
     CHIP_HIP(grow(c->in, n));
-    if (n) CHIP_HIP(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+    if (n) CHIP_HIP(h2d(c->stage, c->in.p, in, n, c->stream));
     st = bao_encode_ctx(c, static_cast<const uint8_t *>(c->in.p), n, false, hash);
     if (st != CHIP_OK) return st;
     CHIP_HIP(hipStreamSynchronize(c->stream));
@@ -934,11 +1137,11 @@ int chip_bao_decode(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint6
     const uint64_t blen = bao_encoded_len(n);
     CHIP_HIP(grow(c->in, blen));
     CHIP_HIP(grow(c->out, n));
-    CHIP_HIP(hipMemcpyAsync(c->in.p, enc, blen, hipMemcpyHostToDevice, c->stream));
+    CHIP_HIP(h2d(c->stage, c->in.p, enc, blen, c->stream));
     st = bao_decode_ctx(c, static_cast<const uint8_t *>(c->in.p), blen, n, hash,
                         static_cast<uint8_t *>(c->out.p));
     if (st != CHIP_OK) return st;
-    if (n) CHIP_HIP(hipMemcpyAsync(out, c->out.p, n, hipMemcpyDeviceToHost, c->stream));
+    if (n) CHIP_HIP(d2h(c->stage, out, c->out.p, n, c->stream));
     CHIP_HIP(hipStreamSynchronize(c->stream));
     *out_len = n;
     return CHIP_OK;
@@ -1023,7 +1226,7 @@ int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const uint8_t 
     if (st != CHIP_OK) return st;
     const uint64_t blen = bao_encoded_len(n);
     CHIP_HIP(grow(c->in, blen));
-    CHIP_HIP(hipMemcpyAsync(c->in.p, enc, blen, hipMemcpyHostToDevice, c->stream));
+    CHIP_HIP(h2d(c->stage, c->in.p, enc, blen, c->stream));
     std::vector<uint8_t> cf, pf;
     st = node_check_ctx(c, n, hash, &cf, &pf);
     if (st != CHIP_OK) return st;
@@ -1035,8 +1238,7 @@ int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const uint8_t 
         CHIP_HIP(grow(c->out, (g1 - g0) * 1024));
         CHIP_HIP(bao_gather_content(static_cast<const uint8_t *>(c->in.p), n, g0, g1,
                                     static_cast<uint8_t *>(c->out.p), c->stream));
-        CHIP_HIP(hipMemcpyAsync(out, static_cast<uint8_t *>(c->out.p) + (start - g0 * 1024), olen,
-                                hipMemcpyDeviceToHost, c->stream));
+        CHIP_HIP(d2h(c->stage, out, static_cast<uint8_t *>(c->out.p) + (start - g0 * 1024), olen, c->stream));
         CHIP_HIP(hipStreamSynchronize(c->stream));
     }
     *out_len = olen;
@@ -1055,7 +1257,7 @@ int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t h
     if (st != CHIP_OK) return st;
     const uint64_t blen = bao_encoded_len(n);
     CHIP_HIP(grow(c->in, blen));
-    CHIP_HIP(hipMemcpyAsync(c->in.p, enc, blen, hipMemcpyHostToDevice, c->stream));
+    CHIP_HIP(h2d(c->stage, c->in.p, enc, blen, c->stream));
     std::vector<uint8_t> cf, pf;
     st = node_check_ctx(c, n, hash, &cf, &pf);
     if (st != CHIP_OK) return st;
@@ -1108,7 +1310,7 @@ int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t h
     if (blen2 != len) return CHIP_ERR_SCRUBBED_LENGTH_MISMATCH;  // decoding.rs:198-203
     if (std::memcmp(h2, hash, 32) != 0) return CHIP_ERR_INVALID_SCRUBBED_HASH;  // decoding.rs:205-207
     if (!out || out_cap < blen2) return CHIP_ERR_BUFFER_TOO_SMALL;
-    CHIP_HIP(hipMemcpyAsync(out, c->out.p, blen2, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(d2h(c->stage, out, c->out.p, blen2, c->stream));
     CHIP_HIP(hipStreamSynchronize(c->stream));
     *out_len = blen2;
     return CHIP_OK;
@@ -1148,7 +1350,7 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
         st = ctx_get(&c);
         if (st != CHIP_OK) return st;
         CHIP_HIP(grow(c->in, cur_n));
-        if (cur_n) CHIP_HIP(hipMemcpyAsync(c->in.p, cur, cur_n, hipMemcpyHostToDevice, c->stream));
+        if (cur_n) CHIP_HIP(h2d(c->stage, c->in.p, cur, cur_n, c->stream));
         const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
         if (zfec && bao && cur_len) {  // fused: shards written into the bao stream, hashed in place
             CHIP_HIP(grow(c->out, final_len));
@@ -1158,7 +1360,7 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
             CHIP_HIP(zfec_bao_dev(d_cur, 0, cur_n, 1, inf.chunk_len, static_cast<uint8_t *>(c->out.p), 0, d_hash,
                                   c->scratch.p, c->stream));
             CHIP_HIP(hipMemcpyAsync(hash, d_hash, 32, hipMemcpyDeviceToHost, c->stream));
-            CHIP_HIP(hipMemcpyAsync(out, c->out.p, final_len, hipMemcpyDeviceToHost, c->stream));
+            CHIP_HIP(d2h(c->stage, out, c->out.p, final_len, c->stream));
             CHIP_HIP(hipStreamSynchronize(c->stream));
             *out_len = final_len;
             if (info) *info = inf;
@@ -1174,10 +1376,10 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
         if (bao) {  // encoding.rs:140-142: the zfec output stays on the device
             st = bao_encode_ctx(c, d_cur, cur_len, true, hash);
             if (st != CHIP_OK) return st;
-            CHIP_HIP(hipMemcpyAsync(out, c->out.p, final_len, hipMemcpyDeviceToHost, c->stream));
+            CHIP_HIP(d2h(c->stage, out, c->out.p, final_len, c->stream));
         } else {
             std::memset(hash, 0, 32);  // encoding.rs:145
-            if (final_len) CHIP_HIP(hipMemcpyAsync(out, d_cur, final_len, hipMemcpyDeviceToHost, c->stream));
+            if (final_len) CHIP_HIP(d2h(c->stage, out, d_cur, final_len, c->stream));
         }
         CHIP_HIP(hipStreamSynchronize(c->stream));
     }
@@ -1685,7 +1887,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         if (st != CHIP_OK) return st;
         const uint64_t in_bytes = bao ? bao_encoded_len(blen) : n;
         CHIP_HIP(grow(c->in, in_bytes));
-        if (in_bytes) CHIP_HIP(hipMemcpyAsync(c->in.p, in, in_bytes, hipMemcpyHostToDevice, c->stream));
+        if (in_bytes) CHIP_HIP(h2d(c->stage, c->in.p, in, in_bytes, c->stream));
         const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
         if (bao) {  // decoding.rs:89-93
             CHIP_HIP(grow(c->mid, blen));
@@ -1703,7 +1905,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             if (st != CHIP_OK) return st;
             d_cur = static_cast<const uint8_t *>(c->out.p);
         }
-        if (olen) CHIP_HIP(hipMemcpyAsync(dst, d_cur, olen, hipMemcpyDeviceToHost, c->stream));
+        if (olen) CHIP_HIP(d2h(c->stage, dst, d_cur, olen, c->stream));
         CHIP_HIP(hipStreamSynchronize(c->stream));
         cur = dst;
         cur_n = olen;
@@ -1809,9 +2011,10 @@ int chip_bao_hasher_update(chip_bao_hasher *h, const uint8_t *buf, uint64_t n) {
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
     CHIP_HIP(grow_keep(h->content, h->len + n, h->len, h->stream));
-    CHIP_HIP(hipMemcpyAsync(static_cast<uint8_t *>(h->content.p) + h->len, buf, n, hipMemcpyHostToDevice,
-                            h->stream));
-    CHIP_HIP(hipStreamSynchronize(h->stream));  // the caller may reuse buf on return
+    CHIP_HIP(h2d(c->stage, static_cast<uint8_t *>(h->content.p) + h->len, buf, n, h->stream));
+    // the caller may reuse buf on return: a staged copy is done with it already,
+    // a direct one (pinned buf) is waited for
+    if (!staged(buf, n)) CHIP_HIP(hipStreamSynchronize(h->stream));
     h->len += n;
     return CHIP_OK;
 }
@@ -1855,7 +2058,7 @@ int chip_bao_hasher_read_all(chip_bao_hasher *h, uint8_t *out, uint64_t out_cap,
     Ctx *c;
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    CHIP_HIP(hipMemcpyAsync(out, h->enc.p, h->enc_len, hipMemcpyDeviceToHost, h->stream));
+    CHIP_HIP(d2h(c->stage, out, h->enc.p, h->enc_len, h->stream));
     CHIP_HIP(hipStreamSynchronize(h->stream));
     return CHIP_OK;
 }

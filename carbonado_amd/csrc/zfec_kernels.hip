@@ -23,6 +23,7 @@
 #include "gf256.hpp"
 #include "zfec_device.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -100,9 +101,8 @@ constexpr uint64_t ZF_BL_RUN = 32;  // bao-layout kernel: consecutive 1 KiB unit
 // into registers (K <= 8; K = 16 has no registers to spare).  8 computed
 // rows (NG = 2): plain stores measured +1-3% over nontemporal at 2
 // workgroups/CU (tools/zfec_tune, 8-of-16 sweep in DESIGN.md).
-// The 4-of-8 shape (K = 4, NG = 1): super-tiles of 2 column tiles with the
-// next super-tile prefetched, 2 workgroups/CU: +1.2-1.4% over one tile at
-// occupancy 4, on two boxes.
+// The 4-of-8 shape (K = 4, NG = 1) has two schedules, picked at run time per
+// box (k4_info / k4_tune below).
 struct KernelInfo {
     KernelFn fn;
     size_t lds;
@@ -121,15 +121,10 @@ KernelInfo make_info() {
     ki.bpc_cap = 0;
     if constexpr (K > 4) {
         ki.fn = gf_apply_kernel<K, NG, ZF_U, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
-    } else if constexpr (K == 4 && NG == 1) {
-        static const bool u1 = std::getenv("CHIP_ZFEC_K4_U1") != nullptr;  // A/B tuning switch
-        if (u1) {
-            ki.fn = gf_apply_kernel<4, 1, 1, ZF_MAP, ZF_NT>;
-        } else {
-            ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true>;
-            ki.u = 2;
-            ki.bpc_cap = 2;
-        }
+    } else if constexpr (K == 4 && NG == 1) {  // schedule S0 (k4_info)
+        ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true>;
+        ki.u = 2;
+        ki.bpc_cap = 2;
     } else {
         ki.fn = gf_apply_kernel<K, NG, ZF_U, ZF_MAP, ZF_NT>;
     }
@@ -149,6 +144,19 @@ bool lookup_fast(int k, int ng, KernelInfo &out) {
 #undef CHIP_CASE
 }
 
+// The two 4-of-8 schedules (tools/zfec_tune.hip): S0 = super-tiles of 2
+// column tiles, the next super-tile prefetched, 2 workgroups/CU; S1 = one
+// tile, the next prefetched, 4 workgroups/CU.
+KernelInfo k4_info(int s) {
+    KernelInfo ki = make_info<4, 1>();
+    if (s == 1) {
+        ki.fn = gf_apply_kernel<4, 1, 1, ZF_MAP, ZF_NT, 0, 1, 0, true>;
+        ki.u = 1;
+        ki.bpc_cap = 4;
+    }
+    return ki;
+}
+
 struct DevTable {
     void *ptr = nullptr;
     size_t bytes = 0;
@@ -158,6 +166,33 @@ std::mutex g_mu;
 std::map<std::vector<uint8_t>, DevTable> g_tables;  // key: device, k, ng, coef bytes
 std::map<std::pair<KernelFn, size_t>, int> g_grid;
 std::map<int, uint8_t *> g_multab;                  // per device
+
+// ---- run-time choice of the 4-of-8 schedule ------------------------------
+// S0 and S1 are within a few per cent of each other and which one wins
+// depends on the box (S1 4 % ahead on one box, 0.7 % behind on
+// another).  The first large launch of each (device, output rows) class runs
+// 4 slices of count/8 objects alternately with S0 and S1 between events on
+// its stream, waits for them, keeps the faster one and runs the rest of the
+// batch with it; later launches use the choice.  CHIP_ZFEC_K4_SCHED=0|1 fixes
+// the schedule (A/B runs; CHIP_ZFEC_K4_U1 = 1, the older switch).
+constexpr uint64_t K4_TUNE_MIN = uint64_t(1) << 30;  // input bytes of a launch worth tuning on
+std::map<std::pair<int, int>, int> g_k4;               // (device, output rows) -> schedule
+
+int k4_forced() {
+    static const int f = [] {
+        if (const char *e = std::getenv("CHIP_ZFEC_K4_SCHED")) return std::atoi(e) == 1 ? 1 : 0;
+        return std::getenv("CHIP_ZFEC_K4_U1") ? 1 : -1;
+    }();
+    return f;
+}
+
+int k4_known(int rows) {
+    const int f = k4_forced();
+    if (f >= 0) return f;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_k4.find({selected_device(), rows});
+    return it == g_k4.end() ? -1 : it->second;
+}
 
 int grid_for(const KernelInfo &ki) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -260,11 +295,27 @@ hipError_t apply_generic(const GfPlan &p, const GfLaunch &L, hipStream_t stream)
     return hipFreeAsync(d, stream);
 }
 
+hipError_t k4_tune(const GfPlan &p, const GfLaunch &L, hipStream_t stream, uint32_t row0, uint32_t nrows,
+                   bool copies, int rows);
+
+// sched: the 4-of-8 schedule to use, -1 = the known choice or tune now
 hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
-                                uint32_t row0, uint32_t nrows, bool copies) {
+                         uint32_t row0, uint32_t nrows, bool copies, int sched = -1) {
     const int ng = nrows > 4 ? 2 : 1;
     KernelInfo ki;
     if (!lookup_fast((int)p.k, ng, ki)) return hipErrorInvalidValue;
+    if (p.k == 4 && ng == 1 && !L.bao_off) {
+        int rows = (int)nrows;  // output shards written per column
+        if (copies)
+            for (uint32_t j = 0; j < p.k; ++j) rows += p.copy_off[j] != NO_OUT;
+        if (sched < 0) sched = k4_known(rows);
+        if (sched < 0) {
+            if (L.count >= 8 && L.count * L.valid >= K4_TUNE_MIN)
+                return k4_tune(p, L, stream, row0, nrows, copies, rows);
+            sched = 0;
+        }
+        ki = k4_info(sched);
+    }
     ApplyArgs a;
     std::memset(&a, 0, sizeof a);
     a.in = L.in; a.out = L.out;
@@ -314,6 +365,38 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     return hipGetLastError();
 }
 
+hipError_t k4_tune(const GfPlan &p, const GfLaunch &L, hipStream_t stream, uint32_t row0, uint32_t nrows,
+                   bool copies, int rows) {
+    const uint64_t piece = L.count / 8;
+    auto slice = [&](uint64_t o0, uint64_t cnt) {
+        GfLaunch S = L;
+        S.in = L.in + o0 * L.in_stride;
+        S.out = L.out + o0 * L.out_stride;
+        S.count = cnt;
+        return S;
+    };
+    hipEvent_t ev[5] = {};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
+    if (e == hipSuccess) e = hipEventRecord(ev[0], stream);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) {
+        e = gf_apply_pass(p, slice(i * piece, piece), stream, row0, nrows, copies, i & 1);
+        if (e == hipSuccess) e = hipEventRecord(ev[i + 1], stream);
+    }
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    if (e == hipSuccess) e = hipEventSynchronize(ev[4]);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventElapsedTime(&t[i], ev[i], ev[i + 1]);
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    if (e != hipSuccess) return e;
+    const int s = std::min(t[1], t[3]) < std::min(t[0], t[2]) ? 1 : 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_k4[{selected_device(), rows}] = s;
+    }
+    return gf_apply_pass(p, slice(4 * piece, L.count - 4 * piece), stream, row0, nrows, copies, s);
+}
+
 }  // namespace
 
 hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
@@ -329,3 +412,5 @@ hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
 }
 
 }  // namespace chip
+
+extern "C" int chip_zfec_k4_schedule(uint32_t rows) { return chip::k4_known((int)rows); }

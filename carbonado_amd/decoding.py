@@ -8,7 +8,7 @@ from typing import Sequence
 import numpy as np
 
 from . import _lib
-from ._buf import as_u8, check, ptr
+from ._buf import OutBytes, as_u8, check, ptr
 from .constants import FEC_K, FEC_M, HASH_SIZE, Format
 from .error import HashDecodeError
 
@@ -31,21 +31,21 @@ def zfec_chunks(chunks: Sequence, padding: int, indices: Sequence[int] | None = 
     ptrs = (ctypes.c_void_p * n)(*[x.ctypes.data if x.size else 0 for x in arrs])
     cidx = (ctypes.c_uint32 * n)(*idx)
     olen_max = k * C
-    out = np.empty(max(olen_max, 1), dtype=np.uint8)
+    out = OutBytes(olen_max - padding if 0 <= padding <= olen_max else olen_max)
     olen = ctypes.c_uint64()
-    check(_lib.lib().chip_zfec_decode_shares(k, m, ptrs, cidx, n, C, padding, ptr(out), olen_max,
+    check(_lib.lib().chip_zfec_decode_shares(k, m, ptrs, cidx, n, C, padding, out.ptr(), out.cap,
                                              ctypes.byref(olen)))
-    return out[: olen.value].tobytes()
+    return out.result(olen.value)
 
 
 def zfec(input, padding: int, k: int = FEC_K, m: int = FEC_M) -> bytes:
     """decoding.rs:34-51: m contiguous shards (len % m == 0 else UnevenZfecChunks)."""
     a = as_u8(input)
     cap = (a.size // m) * k if m else 0
-    out = np.empty(max(cap, 1), dtype=np.uint8)
+    out = OutBytes(cap - padding if 0 <= padding <= cap else cap)
     olen = ctypes.c_uint64()
-    check(_lib.lib().chip_zfec_decode(k, m, ptr(a), a.size, padding, ptr(out), cap, ctypes.byref(olen)))
-    return out[: olen.value].tobytes()
+    check(_lib.lib().chip_zfec_decode(k, m, ptr(a), a.size, padding, out.ptr(), out.cap, ctypes.byref(olen)))
+    return out.result(olen.value)
 
 
 def bao(input, hash: bytes) -> bytes:
@@ -55,11 +55,11 @@ def bao(input, hash: bytes) -> bytes:
     a = as_u8(input)
     n = int.from_bytes(a[:8].tobytes(), "little") if a.size >= 8 else 0
     cap = min(n, a.size)
-    out = np.empty(max(cap, 1), dtype=np.uint8)
+    out = OutBytes(cap)
     h = as_u8(hash)
     olen = ctypes.c_uint64()
-    check(_lib.lib().chip_bao_decode(ptr(a), a.size, ptr(h), h.size, ptr(out), cap, ctypes.byref(olen)))
-    return out[: olen.value].tobytes()
+    check(_lib.lib().chip_bao_decode(ptr(a), a.size, ptr(h), h.size, out.ptr(), cap, ctypes.byref(olen)))
+    return out.result(olen.value)
 
 
 def ecies(input, secret_key: bytes) -> bytes:
@@ -78,21 +78,21 @@ def _grow_call(fn, cap: int) -> bytes:
     the library reports (snappy output size is known only after parsing)."""
     from .error import BufferTooSmall
     for _ in range(2):
-        out = np.empty(max(cap, 1), dtype=np.uint8)
+        out = OutBytes(cap)
         olen = ctypes.c_uint64()
-        st = fn(out, cap, olen)
+        st = fn(out.ptr(), cap, olen)
         if st == BufferTooSmall.status and olen.value > cap:
             cap = olen.value
             continue
         check(st)
-        return out[: olen.value].tobytes()
+        return out.result(olen.value)
     check(st)
 
 
 def snap(input) -> bytes:
     """decoding.rs:70-77: snap::read::FrameDecoder::read_to_end."""
     a = as_u8(input)
-    return _grow_call(lambda out, cap, olen: _lib.lib().chip_snap_decompress(ptr(a), a.size, ptr(out), cap,
+    return _grow_call(lambda out, cap, olen: _lib.lib().chip_snap_decompress(ptr(a), a.size, out, cap,
                                                                              ctypes.byref(olen)),
                       2 * a.size + 1024)
 
@@ -104,9 +104,18 @@ def decode(secret_key: bytes, hash: bytes, input, padding: int, format: int) -> 
     h = as_u8(hash)
     sk = as_u8(secret_key)
     fmt = Format(format)
-    cap = a.size * (3 if fmt & Format.Snappy else 1) + 1024
+    if fmt & Format.Snappy:
+        cap = a.size * 3 + 1024
+    else:  # the exact size in the common case: the output becomes the result without a copy
+        cap = a.size
+        if fmt & Format.Bao:
+            cap = min(int.from_bytes(a[:8].tobytes(), "little"), a.size) if a.size >= 8 else 0
+        if fmt & Format.Zfec:
+            cap = max((cap // FEC_M) * FEC_K - padding, 0)
+        if fmt & Format.Ecies:
+            cap = max(cap - 97, 0)
     return _grow_call(lambda out, c, olen: _lib.lib().chip_decode(
-        ptr(sk) if sk.size else None, sk.size, ptr(h), h.size, ptr(a), a.size, padding, int(fmt), ptr(out), c,
+        ptr(sk) if sk.size else None, sk.size, ptr(h), h.size, ptr(a), a.size, padding, int(fmt), out, c,
         ctypes.byref(olen)), cap)
 
 
@@ -119,10 +128,10 @@ def extract_slice(encoded, index: int, slice_len: int = 1024) -> bytes:
     n = int.from_bytes(a[:8].tobytes(), "little") if a.size >= 8 else 0
     L = _lib.lib()
     cap = L.chip_bao_slice_len(n, index * 1024, slice_len) if a.size >= 8 else 0
-    out = np.empty(max(cap, 1), dtype=np.uint8)
+    out = OutBytes(cap)
     olen = ctypes.c_uint64()
-    check(L.chip_bao_extract_slice(ptr(a), a.size, index, slice_len, ptr(out), cap, ctypes.byref(olen)))
-    return out[: olen.value].tobytes()
+    check(L.chip_bao_extract_slice(ptr(a), a.size, index, slice_len, out.ptr(), cap, ctypes.byref(olen)))
+    return out.result(olen.value)
 
 
 def verify_slice(hash: bytes, input, index: int, count: int) -> bytes:
@@ -134,11 +143,11 @@ def verify_slice(hash: bytes, input, index: int, count: int) -> bytes:
     a = as_u8(input)
     h = as_u8(hash)
     cap = count * 1024
-    out = np.empty(max(cap, 1), dtype=np.uint8)
+    out = OutBytes(cap)
     olen = ctypes.c_uint64()
-    check(_lib.lib().chip_bao_verify_slice(ptr(h), h.size, ptr(a), a.size, index, count, ptr(out), cap,
+    check(_lib.lib().chip_bao_verify_slice(ptr(h), h.size, ptr(a), a.size, index, count, out.ptr(), cap,
                                            ctypes.byref(olen)))
-    return out[: olen.value].tobytes()
+    return out.result(olen.value)
 
 
 def scrub(input, hash: bytes, encode_info) -> bytes:
@@ -151,8 +160,8 @@ def scrub(input, hash: bytes, encode_info) -> bytes:
         raise HashDecodeError(HASH_SIZE, len(hash))
     a = as_u8(input)
     h = as_u8(hash)
-    out = np.empty(max(a.size, 1), dtype=np.uint8)
+    out = OutBytes(a.size)
     olen = ctypes.c_uint64()
     check(_lib.lib().chip_scrub(ptr(a), a.size, ptr(h), h.size, encode_info.padding_len, encode_info.chunk_len,
-                                ptr(out), a.size, ctypes.byref(olen)))
-    return out[: olen.value].tobytes()
+                                out.ptr(), a.size, ctypes.byref(olen)))
+    return out.result(olen.value)

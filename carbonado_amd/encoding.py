@@ -8,7 +8,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._buf import as_u8, check, ptr
+from ._buf import OutBytes, as_u8, check, ptr
 from .constants import FEC_K, FEC_M, Format
 from .structs import EncodeInfo, Encoded
 
@@ -66,10 +66,10 @@ def zfec(input, k: int = FEC_K, m: int = FEC_M) -> tuple[bytes, int, int]:
     a = as_u8(input)
     L = _lib.lib()
     total = L.chip_zfec_encoded_len(a.size, k, m)
-    out = np.empty(max(total, 1), dtype=np.uint8)
+    out = OutBytes(total)
     pad, chunk = ctypes.c_uint32(), ctypes.c_uint32()
-    check(L.chip_zfec_encode(k, m, ptr(a), a.size, ptr(out), total, ctypes.byref(pad), ctypes.byref(chunk)))
-    return out[:total].tobytes(), pad.value, chunk.value
+    check(L.chip_zfec_encode(k, m, ptr(a), a.size, out.ptr(), total, ctypes.byref(pad), ctypes.byref(chunk)))
+    return out.result(total), pad.value, chunk.value
 
 
 def bao(input) -> tuple[bytes, bytes]:
@@ -77,11 +77,11 @@ def bao(input) -> tuple[bytes, bytes]:
     a = as_u8(input)
     L = _lib.lib()
     total = L.chip_bao_encoded_len(a.size)
-    out = np.empty(total, dtype=np.uint8)
+    out = OutBytes(total)
     h = np.empty(32, dtype=np.uint8)
     olen = ctypes.c_uint64()
-    check(L.chip_bao_encode(ptr(a), a.size, ptr(out), total, ctypes.byref(olen), ptr(h)))
-    return out[: olen.value].tobytes(), h.tobytes()
+    check(L.chip_bao_encode(ptr(a), a.size, out.ptr(), total, ctypes.byref(olen), ptr(h)))
+    return out.result(olen.value), h.tobytes()
 
 
 def blake3(input) -> bytes:
@@ -102,13 +102,21 @@ def encode(pubkey: bytes, input, format: int, *, ephemeral_sk: bytes | None = No
     a = as_u8(input)
     pk = as_u8(pubkey)
     L = _lib.lib()
-    cap = L.chip_encode_max_len(a.size)
-    out = np.empty(max(cap, 1), dtype=np.uint8)
+    fmt = int(Format(format))
+    if fmt & Format.Snappy:
+        cap = L.chip_encode_max_len(a.size)  # compressed size known only afterwards
+    else:  # exact: the output becomes the returned bytes without a copy
+        cap = a.size + 97 if fmt & Format.Ecies else a.size
+        if fmt & Format.Zfec:
+            cap = L.chip_zfec_encoded_len(cap, FEC_K, FEC_M)
+        if fmt & Format.Bao:
+            cap = L.chip_bao_encoded_len(cap)
+    out = OutBytes(cap)
     h = np.empty(32, dtype=np.uint8)
     olen = ctypes.c_uint64()
     info = _lib.EncodeInfoC()
     inj, _keep = _inject(ephemeral_sk, nonce)
-    check(L.chip_encode(int(Format(format)), ptr(pk) if pk.size else None, pk.size,
-                        ctypes.byref(inj) if inj is not None else None, ptr(a), a.size, ptr(out), cap,
+    check(L.chip_encode(fmt, ptr(pk) if pk.size else None, pk.size,
+                        ctypes.byref(inj) if inj is not None else None, ptr(a), a.size, out.ptr(), cap,
                         ctypes.byref(olen), ptr(h), ctypes.byref(info)))
-    return Encoded(out[: olen.value].tobytes(), h.tobytes(), EncodeInfo.from_c(info))
+    return Encoded(out.result(olen.value), h.tobytes(), EncodeInfo.from_c(info))

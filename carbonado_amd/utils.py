@@ -7,7 +7,7 @@ import threading
 import numpy as np
 
 from . import _lib
-from ._buf import as_u8, check, ptr
+from ._buf import OutBytes, as_u8, check, ptr
 from .constants import FEC_K, HASH_SIZE
 from .error import HashDecodeError
 
@@ -86,10 +86,10 @@ class BaoHasher:
         L = _lib.lib()
         need = ctypes.c_uint64()
         L.chip_bao_hasher_read_all(self._h, None, 0, ctypes.byref(need))  # size query
-        out = np.empty(max(need.value, 1), np.uint8)
+        out = OutBytes(need.value)
         olen = ctypes.c_uint64()
-        check(L.chip_bao_hasher_read_all(self._h, ptr(out), need.value, ctypes.byref(olen)))
-        return out[: olen.value].tobytes()
+        check(L.chip_bao_hasher_read_all(self._h, out.ptr(), need.value, ctypes.byref(olen)))
+        return out.result(olen.value)
 
     def __del__(self):
         h = getattr(self, "_h", None)

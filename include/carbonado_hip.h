@@ -126,6 +126,11 @@ CHIP_API const char *chip_strerror(int status);
 CHIP_API int chip_init(int device);
 /* Last HIP error string seen by this thread (for CHIP_ERR_DEVICE). */
 CHIP_API const char *chip_last_device_error(void);
+/* Diagnostics: the zfec 4-of-8 schedule this process chose on its device for
+ * launches that write `rows` output shards per column (8 = encode with the
+ * data shards, 4 = parity only or a 2-erasure decode): 0 or 1, -1 = not
+ * chosen yet.  The first launch of >= 1 GiB picks it. */
+CHIP_API int chip_zfec_k4_schedule(uint32_t rows);
 
 /* ---- size helpers (host only, no device needed) ----------------------- */
 /* utils.rs:47-58 with FEC_K generalised to k: target = ceil(n/(1024k))*1024k,

@@ -1,0 +1,37 @@
+"""GPU: the run-time choice of the zfec 4-of-8 schedule (zfec_kernels.hip
+k4_tune).  The first launch of >= 1 GiB runs four slices of count/8 objects
+alternately with both schedules, then the rest of the batch with the faster
+one; every object of every slice stays bit-exact."""
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N = 16 << 20
+COUNT = 64  # 1 GiB of input: the smallest batch that tunes
+CHECK = (0, 7, 8, 16, 24, 31, 32, 63)  # slices S0, S1, S0, S1 and the remainder
+
+
+def test_encode_then_decode_tune_and_stay_exact(gpu):
+    import torch
+    from carbonado_amd import _lib, device
+    L = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    inp = torch.randint(0, 256, (COUNT, N), dtype=torch.uint8, device="cuda", generator=g)
+    enc = torch.empty((COUNT, 2 * N), dtype=torch.uint8, device="cuda")
+    device.zfec_encode_batch(inp, N, enc, 4, 8)
+    torch.cuda.synchronize()
+    assert L.chip_zfec_k4_schedule(8) in (0, 1)
+    for o in CHECK:
+        assert enc[o].cpu().numpy().tobytes() == O.zfec_encode(inp[o].cpu().numpy().tobytes())[0], o
+
+    # decode with data shards 1 and 2 lost: 4 output shards per column
+    C = N // 4
+    keep = [0, 3, 4, 5, 6, 7]
+    out = torch.empty((COUNT, N), dtype=torch.uint8, device="cuda")
+    device.zfec_decode_batch(enc, C, keep, out, 4, 8)
+    torch.cuda.synchronize()
+    assert L.chip_zfec_k4_schedule(4) in (0, 1)
+    for o in CHECK:
+        assert torch.equal(out[o], inp[o]), o
