@@ -8,6 +8,7 @@
 // zfec or bao.  The snappy/ECIES stages that the reference runs before zfec
 // (and after it on decode) are host stages by design (host_stages.cpp).
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -271,7 +272,8 @@ class CopyPool {
         return *p;
     }
     void copy(void *dst, const void *src, size_t n) {
-        if (workers_ == 0 || n < (size_t(1) << 20) || !job_.try_lock()) {
+        // (a forked child has no workers: it copies alone)
+        if (workers_ == 0 || n < (size_t(1) << 20) || getpid() != pid_ || !job_.try_lock()) {
             std::memcpy(dst, src, n);
             return;
         }
@@ -301,6 +303,7 @@ class CopyPool {
         int t = 4;
         if (const char *e = std::getenv("CHIP_COPY_THREADS")) t = std::max(1, std::min(32, std::atoi(e)));
         workers_ = t - 1;
+        pid_ = getpid();
         for (int i = 1; i <= workers_; ++i) std::thread([this, i] { run(i); }).detach();
     }
     void run(int i) {
@@ -322,6 +325,7 @@ class CopyPool {
         }
     }
     int workers_ = 0;
+    pid_t pid_ = 0;
     std::mutex job_, mu_;
     std::condition_variable cv_, done_;
     uint64_t gen_ = 0;
