@@ -47,9 +47,11 @@ def parse():
     ap.add_argument("--object-mib", type=float, default=16.0)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=8)
-    ap.add_argument("--mode", choices=["encode", "decode", "bao", "pipeline", "e2e", "e2e-decode", "scrub", "hasher"],
+    ap.add_argument("--mode", choices=["encode", "decode", "bao", "bao-decode", "pipeline", "e2e", "e2e-decode", "scrub",
+                                       "hasher"],
                     default="encode",
-                    help="pipeline: device-resident encode() at --level (Bao/Zfec bits; 12 = zfec fused into "
+                    help="bao-decode: device-resident decoding::bao (verify every node, return the content); "
+                         "pipeline: device-resident encode() at --level (Bao/Zfec bits; 12 = zfec fused into "
                          "bao); e2e: encode() at --level from pinned HOST memory to host memory (H2D+kernels+D2H); "
                          "scrub: scrub() of level-12 streams with one corrupted shard (host API, decoding.rs:151-212); "
                          "hasher: BaoHasher update()+finalize() over the objects in 4 MiB appends (utils.rs:104-137)")
@@ -142,6 +144,8 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
         import hashlib
         sk = hashlib.sha256(b"carbonado-amd bench receiver").digest()
         enc_obj, h_obj, inf_obj = O.c_encode_full(obj, args.level, pub, eph if eph else bytes(32), bytes(16))
+    if args.mode == "bao-decode":
+        bstream, bhash = O.bao_encode(obj)
     if args.mode == "scrub":
         enc_obj, h_obj, inf_obj = O.encode(obj, 12)
         bad = bytearray(enc_obj)
@@ -154,6 +158,8 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
     def one():
         if args.mode == "bao":
             O.bao_encode(obj)
+        elif args.mode == "bao-decode":
+            O.bao_decode(bstream, bhash)
         elif args.mode == "hasher":
             O.blake3(obj)
         elif args.mode == "scrub":
@@ -196,7 +202,7 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
         with ThreadPoolExecutor(threads) as ex:
             done = sum(ex.map(worker, [t0 + args.cpu_seconds] * threads))
     el = time.perf_counter() - t0
-    what = {"bao": "bao encode", "e2e": f"encode() level {args.level}", "pipeline": f"encode() level {args.level}",
+    what = {"bao": "bao encode", "bao-decode": "bao decode (verify + content)", "e2e": f"encode() level {args.level}", "pipeline": f"encode() level {args.level}",
             "hasher": "BLAKE3 of the content", "scrub": "scrub() restated: bao decode + zfec decode + encode()", "e2e-decode": f"decode() level {args.level}",
             "decode": f"zfec {args.k}-of-{args.m} decode, erased {args.erase}"}.get(
         args.mode, f"zfec {args.k}-of-{args.m} encode")
@@ -231,6 +237,11 @@ def scrub_corrupt_offset(n: int, o: int) -> int:
         return total
     i = (o % 4) * (C // 1024) + (C // 1024) // 3
     return 8 + 1024 * i + 64 * (p_before(i) + c_at(i)) + 517
+
+
+def _lib_len(n: int) -> int:
+    from carbonado_amd import _lib
+    return _lib.lib().chip_bao_encoded_len(n)
 
 
 class Workload:
@@ -405,6 +416,18 @@ class Workload:
             host = f"host {stages[:-3]} on {args.host_threads} threads + " if stages else ""
             self.kernel = f"encode() level {lv}: {host}H2D + gf_apply + bao kernels + D2H, {slots} slots"
             self.kernel_sym = "e2e"
+        elif args.mode == "bao-decode":
+            blen = L.chip_bao_encoded_len(n)
+            self.enc = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device=dev)
+            self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
+            self.scratch = device.bao_scratch(n, count, dev)
+            device.bao_encode_batch(self.inp, n, self.enc, self.hashes, self.scratch)
+            self.out = torch.empty((count, n), dtype=torch.uint8, device=dev)
+            self.status = torch.full((count,), -1, dtype=torch.int32, device=dev)
+            self.step = lambda: device.bao_decode_batch(self.enc, n, self.hashes, self.out, self.status, self.scratch)
+            self.alg_bytes = count * (blen + n)  # read the stream, write the content
+            self.kernel = "bao_chunk_kernel<1> (verify + content) + bao_parent_kernel<1> levels"
+            self.kernel_sym = "bao_chunk_kernel"
         else:
             blen = L.chip_bao_encoded_len(n)
             self.out = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device=dev)
@@ -519,6 +542,12 @@ class Workload:
                   self.h_hash[0].numpy().tobytes() == h)
         elif self.args.mode == "decode":
             ok = self.out[0, :self.n].cpu().numpy().tobytes() == sample
+        elif self.args.mode == "bao-decode":
+            # every object verified (status 0) and object 0's content is the input;
+            # the stream itself is checked against the oracle's bao encoding
+            blen = _lib_len(self.n)
+            ok = (bool((self.status == 0).all()) and self.out[0].cpu().numpy().tobytes() == sample and
+                  self.enc[0, :blen].cpu().numpy().tobytes() == O.bao_encode(sample)[0])
         elif self.args.mode == "scrub":
             ok = all(self.fixed[o] == self.encs[o] for o in range(self.count))
         elif self.args.mode == "hasher":
@@ -582,6 +611,8 @@ def main():
         traffic, traffic_src = measured_traffic(args.traffic_json, wl.kernel_sym, wl.alg_bytes)
         if args.mode == "bao":
             workload = f"bao encode, {args.objects} x {args.object_mib:g} MiB objects per GPU"
+        elif args.mode == "bao-decode":
+            workload = f"bao decode (verify + content), {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "pipeline":
             workload = f"encode() level {args.level}, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "scrub":
@@ -628,7 +659,7 @@ def main():
                                     "note": "PCIe Gen5 x16, 63 GB/s per direction (spec), H2D and D2H overlapped"})
             res["data"] = ("synthetic (uniform random bytes), pinned host buffers" if args.mode.startswith("e2e")
                            else "synthetic (uniform random bytes), pageable host buffers (numpy / bytes)")
-        if args.mode == "bao" or (args.mode == "pipeline" and args.level & 4):
+        if args.mode in ("bao", "bao-decode") or (args.mode == "pipeline" and args.level & 4):
             # BLAKE3 compressions: one per 64-B block of content plus one per parent node;
             # 7 rounds x 8 G x 12 VALU lane-ops (a+b+m as one v_add3_u32).
             hashed = wl.zlen if args.mode == "pipeline" else n

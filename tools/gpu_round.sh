@@ -14,6 +14,7 @@ timeout -k 10 600 python3 bench.py --verify-all > $O/bench_encode.log 2>&1
 timeout -k 10 600 python3 bench.py --mode decode --no-cpu-baseline > $O/bench_decode.log 2>&1
 timeout -k 10 600 python3 bench.py --k 8 --m 16 --no-cpu-baseline > $O/bench_8of16.log 2>&1
 timeout -k 10 600 python3 bench.py --mode bao --no-cpu-baseline > $O/bench_bao.log 2>&1
+timeout -k 10 600 python3 bench.py --mode bao-decode --cpu-seconds 8 > $O/bench_bao_decode.log 2>&1
 timeout -k 10 600 python3 bench.py --mode pipeline --level 12 --verify-all > $O/bench_pipe12.log 2>&1
 timeout -k 10 600 python3 bench.py --mode e2e --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 > $O/bench_e2e15.log 2>&1
 timeout -k 10 600 python3 bench.py --mode e2e --level 12 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 > $O/bench_e2e12.log 2>&1
