@@ -9,8 +9,8 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 N = 16 << 20
-COUNT = 64  # 1 GiB of input: the smallest batch that tunes
-CHECK = (0, 7, 8, 16, 24, 31, 32, 63)  # slices S0, S1, S0, S1 and the remainder
+COUNT = 67  # > 1 GiB of input (the smallest batch that tunes), not a multiple of 8
+CHECK = (0, 7, 8, 16, 24, 31, 32, 66)  # slices of 8 objects: S0, S1, S0, S1, then the 35-object remainder
 
 
 def test_encode_then_decode_tune_and_stay_exact(gpu):
