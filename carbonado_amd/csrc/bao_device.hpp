@@ -354,6 +354,16 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     // decode: content is 16-B aligned, store straight from the loaded registers
     auto content_step = [&](int g, const u32x4 (&v)[8]) {
         const int j = g >> 3, s = g & 7;
+        if (full_wave) {  // the loads' fast-path address pattern, in the content buffer
+            uint8_t *b = ob + (c0 + j) * 1024 + s * 128 + lane_off;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                u32x4 *q = reinterpret_cast<u32x4 *>(b + (uint64_t)t * 8 * CPL * 1024);
+                if (NTS) __builtin_nontemporal_store(v[t], q);
+                else *q = v[t];
+            }
+            return;
+        }
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const int cc = t * 8 + (lane >> 3);
