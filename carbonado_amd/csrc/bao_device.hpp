@@ -145,11 +145,10 @@ __device__ __forceinline__ void store16_partial(uint8_t *p, u32x4 v, uint32_t va
 }
 
 // 16 bytes at an 8-byte-aligned address
-__device__ __forceinline__ u32x4 load16_a8(const uint8_t *p) {
-    const u32x2 lo = *reinterpret_cast<const u32x2 *>(p);
-    const u32x2 hi = *reinterpret_cast<const u32x2 *>(p + 8);
-    u32x4 r = {lo.x, lo.y, hi.x, hi.y};
-    return r;
+typedef uint32_t u32x4_a8 __attribute__((ext_vector_type(4), aligned(8)));
+__device__ __forceinline__ u32x4 load16_a8(const uint8_t *p) {  // one dwordx4 load (gfx950: unaligned OK)
+    const u32x4_a8 v = *reinterpret_cast<const u32x4_a8 *>(p);
+    return u32x4{v.x, v.y, v.z, v.w};
 }
 
 
