@@ -57,6 +57,7 @@ def parse():
                          "hasher: BaoHasher update()+finalize() over the objects in 4 MiB appends (utils.rs:104-137)")
     ap.add_argument("--level", type=int, default=12, help="e2e mode: Format bits (Bao|Zfec = 12)")
     ap.add_argument("--slots", type=int, default=3, help="e2e mode: pipeline slots (streams)")
+    ap.add_argument("--slice-mib", type=int, default=256, help="e2e mode: input bytes per pipeline slice")
     ap.add_argument("--host-threads", type=int, default=16,
                     help="e2e mode: host threads for the Snappy/Ecies stages (the GPU box's CPU share is 16)")
     ap.add_argument("--erase", default="1,2", help="decode mode: shards dropped")
@@ -406,6 +407,7 @@ class Workload:
 
             def step():
                 olens, _ = device.encode_host_batch(lv, self.h_in, n, self.h_out, self.h_hash, slots,
+                                                    slice_bytes=args.slice_mib << 20,
                                                     pubkey=self.pub, ephemeral_sk=self.eph, nonce=self.nonce,
                                                     host_threads=args.host_threads)
                 self.final_len = max(olens)
