@@ -8,7 +8,7 @@ R=$PWD
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -m pytest tests -m gpu -x -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 600 python3 bench.py --verify-all > $O/bench_encode.log 2>&1
 timeout -k 10 600 python3 bench.py --mode decode --no-cpu-baseline > $O/bench_decode.log 2>&1
