@@ -271,6 +271,8 @@ __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x
 // 3 = rows hold two steps (ping-pong) and every step stores one whole aligned
 //     128-B line of the stream per chunk (plus the head at step 0 and the
 //     tail at step 7), so no line is written in two halves.
+// SE 2 / 3: diagnostics for tools/bao_tune (LDS reads without the stores /
+// stores without the LDS reads; wrong output).
 // SU: unroll of the SP 3 store loop; SE: issue the SP 3 stores before (1) or
 // after (0) the next step's prefetch loads.
 template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0>
@@ -475,6 +477,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     // The stream lines (128-B aligned in stream space) inside a chunk start at
     // chunk byte d + 128 t, d = (-base) mod 128; at step s the line ending at
     // d + 128 s is complete (its first part is in the other half of the row).
+    uint32_t diag = 0;  // SE 2 diagnostic sink
     uint8_t *lsp[8];  // SP 3 fast path: stream address and line phase of chunk t*8 + lane/8, per round
     uint32_t ldd[8];
     auto stream_lines = [&](int g) {
@@ -497,8 +500,25 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
                 const uint32_t *row = st + (t * 8 + (lane >> 3)) * RW;
                 if (s >= 1) {  // the whole line [d + 128(s-1), d + 128 s)
                     const uint32_t x = d + 128u * (s - 1) + 16u * gl;
+                    if constexpr (SE == 3) {  // diagnostic (tools/bao_tune): the stores without the LDS reads
+                        *reinterpret_cast<u32x4 *>(sp + x) = u32x4{x, d, x, d};
+                        continue;
+                    }
+                    if constexpr (SE == 4) {  // diagnostic: as 3, every wave rewriting the same 8 KiB (L2 hits)
+                        *reinterpret_cast<u32x4 *>(ob + t * 1024 + lane * 16) = u32x4{x, d, x, d};
+                        continue;
+                    }
+                    if constexpr (SE == 5) {  // diagnostic: as 3, half the stores
+                        if (t & 1) continue;
+                        *reinterpret_cast<u32x4 *>(sp + x) = u32x4{x, d, x, d};
+                        continue;
+                    }
                     const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
                     const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+                    if constexpr (SE == 2) {  // diagnostic: the LDS reads without the stores
+                        diag ^= v.x ^ v.w;
+                        continue;
+                    }
                     if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(sp + x));
                     else *reinterpret_cast<u32x4 *>(sp + x) = v;
                 } else {  // head [0, d)
@@ -595,10 +615,10 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
             soff[(j + 1) & 1][wave][lane] = my_off;
         }
         wave_sync();
-        if (MODE == 0 && ob && SP == 3 && SE) stream_lines(g);
+        if (MODE == 0 && ob && SP == 3 && SE == 1) stream_lines(g);
         if (g + 1 < NSTEP) load_step(g + 1, pre);  // in flight during the compressions
         if (MODE == 0 && ob && SP == 0) stream_step(wave, g);
-        if (MODE == 0 && ob && SP == 3 && !SE) stream_lines(g);
+        if (MODE == 0 && ob && SP == 3 && SE != 1) stream_lines(g);
 
         const uint64_t i = lb + j;
         const bool mine = (uint64_t)j < nmine;
@@ -682,6 +702,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         }
     }
     if (MODE == 1 && !ok) flag_mismatch(a.status, obj);
+    if (SE == 2 && diag == 0x9E3779B9u && ob) ob[0] = 0;  // keep the diagnostic's reads alive
 }
 
 struct ParentArgs {

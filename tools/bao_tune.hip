@@ -74,9 +74,10 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&status, count * 4));
     CK(hipMalloc(&scratch, bao_scratch_len_t<1>(n, count)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xB1A3ull);
-    std::vector<V> vs = {mk<0, 2, false, 3>(true),  mk<0, 2, false>(false), mk<0, 4, false>(false),
-                         mk<1, 2, false>(true),     mk<3, 2, false>(true),  mk<3, 4, false>(true),
-                         mk<3, 8, false>(true),     mk<0, 4, false, 3>(true)};
+    // product encode, hash-only, the SE 2-5 store diagnostics, CPL 1, decode CPL 2 / 1
+    std::vector<V> vs = {mk<0, 2, false, 3>(true),       mk<0, 2, false>(false),        mk<0, 2, false, 3, 1, 2>(true),
+                         mk<0, 2, false, 3, 1, 3>(true), mk<0, 2, false, 3, 1, 4>(true), mk<0, 2, false, 3, 1, 5>(true),
+                         mk<0, 1, false, 3>(true),       mk<1, 2, false>(true),         mk<1, 1, false>(true)};
     if (argc > 4) {  // comma-separated subset of variant indices (profiling)
         std::vector<V> keep;
         std::string sel = argv[4];
