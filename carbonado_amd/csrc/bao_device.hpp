@@ -275,7 +275,9 @@ __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x
 // stores without the LDS reads; wrong output).
 // SU: unroll of the SP 3 store loop; SE: issue the SP 3 stores before (1) or
 // after (0) the next step's prefetch loads.
-template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0>
+// XG 1: XCD-grouped block order (block b runs logical block (b % 8) * (B/8) + b/8,
+// so each XCD sweeps one contiguous eighth of the batch; B % 8 == 0 only).
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0>
 __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     constexpr int LOG = ilog2(CPL);
     constexpr int NSTEP = 8 * CPL;
@@ -289,7 +291,9 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     const int lane = threadIdx.x & 63;
     const uint64_t span = 64ull * CPL;
     const uint64_t tpo = (a.N + span - 1) / span;
-    const uint64_t wt = (uint64_t)blockIdx.x * K3_WAVES + wave;
+    uint64_t blk = blockIdx.x;
+    if (XG && (gridDim.x & 7) == 0) blk = (blk & 7) * (gridDim.x >> 3) + (blk >> 3);
+    const uint64_t wt = blk * K3_WAVES + wave;
     const bool wave_on = wt < a.count * tpo;
     const uint64_t obj = wave_on ? wt / tpo : 0;
     const uint64_t c0 = wave_on ? (wt - obj * tpo) * span : 0;
@@ -392,7 +396,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     // SP 0: stores of the issuing wave's own rows (wv = wave)
     auto stream_step = [&](int wv, int g) {
         const int j = g >> 3, s = g & 7, gl = lane & 7;
-        const uint64_t wt_w = (uint64_t)blockIdx.x * K3_WAVES + wv;
+        const uint64_t wt_w = blk * K3_WAVES + wv;
         const bool on_w = wt_w < a.count * tpo;
         const uint64_t obj_w = on_w ? wt_w / tpo : 0;
         const uint64_t c0_w = on_w ? (wt_w - obj_w * tpo) * span : 0;
@@ -829,7 +833,7 @@ inline uint64_t bao_scratch_len_t(uint64_t n, uint64_t count) {
 }
 
 // Enqueue K3 then one K4 launch per remaining level.
-template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0>
+template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0>
 hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
                    void *d_scratch, hipStream_t stream, size_t pad_lds = 0 /* tuning: occupancy probe */) {
@@ -847,7 +851,7 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
     ca.hash = d_hash; ca.status = d_status;
     const uint64_t waves = count * ((N + 64ull * BAO_CPL - 1) / (64ull * BAO_CPL));
     const uint64_t blocks = (waves + K3_WAVES - 1) / K3_WAVES;
-    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG>), dim3((unsigned)blocks),
                        dim3(K3_TPB), pad_lds,
                        stream, ca);
     hipError_t e = hipGetLastError();

@@ -50,12 +50,12 @@ struct V {
     size_t pad_lds;
 };
 
-template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0>
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0>
 V mk(bool stream, size_t pad_lds = 0) {
     char b[96];
-    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d pad%zu", MODE == 3 ? "in-place" : MODE ? "decode" : "encode",
-             CPL, NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, pad_lds);
-    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE>, CPL, stream, pad_lds};
+    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d xg%d pad%zu", MODE == 3 ? "in-place" : MODE ? "decode" : "encode",
+             CPL, NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, XG, pad_lds);
+    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE, XG>, CPL, stream, pad_lds};
 }
 
 int main(int argc, char **argv) {
@@ -74,10 +74,11 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&status, count * 4));
     CK(hipMalloc(&scratch, bao_scratch_len_t<1>(n, count)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xB1A3ull);
-    // product encode, hash-only, the SE 2-5 store diagnostics, CPL 1, decode CPL 2 / 1
-    std::vector<V> vs = {mk<0, 2, false, 3>(true),       mk<0, 2, false>(false),        mk<0, 2, false, 3, 1, 2>(true),
-                         mk<0, 2, false, 3, 1, 3>(true), mk<0, 2, false, 3, 1, 4>(true), mk<0, 2, false, 3, 1, 5>(true),
-                         mk<0, 1, false, 3>(true),       mk<1, 2, false>(true),         mk<1, 1, false>(true)};
+    // product encode / decode / in-place, each with the XCD-grouped block order (XG 1)
+    std::vector<V> vs = {mk<0, 2, false, 3>(true), mk<0, 2, false, 3, 1, 0, 1>(true), mk<1, 2, false>(true),
+                         mk<1, 2, false, 0, 1, 0, 1>(true), mk<3, 8, false>(true), mk<3, 8, false, 0, 1, 0, 1>(true)};
+    // round-1 store diagnostics (profiles/r1x_bao_store_diagnostics.txt): mk<0, 2, false>(false) hash-only,
+    // mk<0, 2, false, 3, 1, SE>(true) for SE 2..5, mk<0, 1, false, 3>(true), mk<1, 1, false>(true)
     if (argc > 4) {  // comma-separated subset of variant indices (profiling)
         std::vector<V> keep;
         std::string sel = argv[4];
