@@ -772,6 +772,66 @@ __global__ __launch_bounds__(256) void bao_parent_kernel(ParentArgs a) {
     }
 }
 
+// K4t: the top of the tree in one launch.  One workgroup per object walks
+// every remaining level (cnt_prev <= K4T_MAX nodes at the first one) with the
+// CVs in LDS, each level exactly as bao_parent_kernel computes it: 13 K4
+// launches per 16 MiB object become 4 + 1.
+constexpr int K4T_MAX = 512;
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void bao_top_kernel(ParentArgs a) {
+    __shared__ uint32_t cvs[2][K4T_MAX][8];
+    const uint64_t obj = blockIdx.x;
+    uint64_t cnt_prev = a.cnt_prev;
+    for (uint64_t i = threadIdx.x; i < cnt_prev; i += 256) {
+        uint32_t c[8];
+        load_cv(a.cv_prev + (obj * a.stride_prev + i) * 32, c);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) cvs[0][i][w] = c[w];
+    }
+    __syncthreads();
+    int cur = 0;
+    bool ok = true;
+    for (int level = a.level; cnt_prev > 1; ++level) {
+        const uint64_t cnt = (cnt_prev + 1) / 2;
+        for (uint64_t q = threadIdx.x; q < cnt; q += 256) {
+            uint32_t l[8], p[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) l[w] = cvs[cur][2 * q][w];
+            if (2 * q + 1 >= cnt_prev) {  // odd last node: promoted unchanged
+#pragma unroll
+                for (int w = 0; w < 8; ++w) cvs[cur ^ 1][q][w] = l[w];
+                continue;
+            }
+            uint32_t r[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) r[w] = cvs[cur][2 * q + 1][w];
+            const bool root = cnt == 1;
+            b3_parent(l, r, root, p);
+            if (a.stream) {
+                uint8_t *node = a.stream + obj * a.stream_stride + parent_stream_off(q << level, level, a.N);
+                ok &= node_io<MODE, NT>(node, l, r);
+            }
+            if (root) {
+                if (MODE == 0) {
+                    store_cv(a.hash + obj * 32, p);
+                } else {
+                    uint32_t e[8];
+                    load_cv(a.hash + obj * 32, e);
+#pragma unroll
+                    for (int w = 0; w < 8; ++w) ok &= e[w] == p[w];
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) cvs[cur ^ 1][q][w] = p[w];
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        cnt_prev = cnt;
+    }
+    if (!ok) flag_mismatch(a.status, obj);
+}
+
 struct CheckArgs {
     const uint8_t *stream;
     uint64_t stream_stride, N, count, nparents;
@@ -867,6 +927,11 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
         pa.cnt_prev = cnt_prev; pa.cnt = (cnt_prev + 1) / 2; pa.level = level;
         pa.N = N; pa.count = count; pa.stream = stream_buf; pa.stream_stride = sstride;
         pa.hash = d_hash; pa.status = d_status;
+        if (cnt_prev <= (uint64_t)K4T_MAX && count <= 0x7fffffffull) {  // the rest of the tree, one launch
+            hipLaunchKernelGGL((bao_top_kernel<MODE == 3 ? 0 : MODE, BAO_NTS>), dim3((unsigned)count), dim3(256), 0,
+                               stream, pa);
+            return hipGetLastError();
+        }
         const uint64_t work = count * pa.cnt;
         hipLaunchKernelGGL((bao_parent_kernel<MODE == 3 ? 0 : MODE, BAO_NTS>), dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
                            stream, pa);
