@@ -504,6 +504,39 @@ hipError_t overlap_parts(uint64_t count, uint64_t parts, hipStream_t s, S1 stage
     return hipStreamWaitEvent(s, ps->join3, 0);
 }
 
+// A batch cut into two halves launched side by side on the two pipeline
+// streams (fork/join with events on s).  Two concurrent launches of the
+// HBM-bound zfec kernel move more bytes per second than one launch of the
+// whole batch.
+template <typename F>
+hipError_t split_pair(uint64_t count, hipStream_t s, F launch) {
+    PipeStreams *ps;
+    hipError_t e;
+    if ((e = pipe_streams(&ps)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ps->fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(ps->k1, ps->fork, 0)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(ps->k3, ps->fork, 0)) != hipSuccess) return e;
+    const uint64_t half = count / 2;
+    if ((e = launch(0, half, ps->k1)) != hipSuccess) return e;
+    if ((e = launch(half, count - half, ps->k3)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ps->join1, ps->k1)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ps->join3, ps->k3)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(s, ps->join1, 0)) != hipSuccess) return e;
+    return hipStreamWaitEvent(s, ps->join3, 0);
+}
+
+// CHIP_ZF_SPLIT: 0 = one launch per batch, 1 = two concurrent halves for
+// batches of >= 2 GiB of input (once the 4-of-8 schedule is chosen)
+int zf_split_cfg() {
+    static const int v = env_int("CHIP_ZF_SPLIT", 0);
+    return v;
+}
+bool zf_split(uint32_t k, uint32_t rows, uint64_t bytes, uint64_t count) {
+    if (!zf_split_cfg() || count < 16 || bytes < (2ull << 30)) return false;
+    // the first large 4-of-8 launch tunes the schedule on slices of its own: not split
+    return !(k == 4 && rows <= 8 && chip_zfec_k4_schedule(rows) < 0);
+}
+
 int pipe_parts_cfg() {
     static const int p = env_int("CHIP_PIPE_PARTS", 8);
     return p < 1 ? 1 : p;
@@ -865,6 +898,13 @@ int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     if (aliased && (uint64_t)k * C > n)  // the zero padding of encoding.rs:53-55 becomes part of shard k-1
         CHIP_HIP(hipMemset2DAsync(d_out + n, out_stride ? out_stride : (uint64_t)m * C, 0, (uint64_t)k * C - n,
                                   count, s));
+    if (zf_split(k, aliased ? m - k : m, count * n, count)) {
+        CHIP_HIP(split_pair(count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
+            GfLaunch L{d_in + o0 * in_stride, d_out + o0 * out_stride, in_stride, out_stride, n, C, cnt};
+            return gf_apply(p, L, st);
+        }));
+        return CHIP_OK;
+    }
     GfLaunch L{d_in, d_out, in_stride, out_stride, n, C, count};
     CHIP_HIP(gf_apply(p, L, s));
     return CHIP_OK;
@@ -977,8 +1017,20 @@ int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
         sel[s] = idx[pos[s]];
         slot_off[s] = (uint64_t)sel[s] * chunk_len;
     }
-    return zfec_decode_device(k, m, d_in, in_stride, slot_off, sel, chunk_len, count, d_out, out_stride,
-                              static_cast<hipStream_t>(stream));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (zf_split(k, k, count * k * chunk_len, count)) {
+        int half_st = CHIP_OK;
+        const hipError_t e = split_pair(count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
+            const int r = zfec_decode_device(k, m, d_in + o0 * in_stride, in_stride, slot_off, sel, chunk_len, cnt,
+                                             d_out + o0 * out_stride, out_stride, st);
+            if (r != CHIP_OK) half_st = r;
+            return r == CHIP_OK ? hipSuccess : hipErrorInvalidValue;
+        });
+        if (half_st != CHIP_OK) return half_st;
+        CHIP_HIP(e);
+        return CHIP_OK;
+    }
+    return zfec_decode_device(k, m, d_in, in_stride, slot_off, sel, chunk_len, count, d_out, out_stride, s);
 }
 
 // ---- bao ---------------------------------------------------------------
