@@ -527,10 +527,7 @@ hipError_t split_pair(uint64_t count, hipStream_t s, F launch) {
 
 // CHIP_ZF_SPLIT: 0 = one launch per batch, 1 = two concurrent halves for
 // batches of >= 2 GiB of input (once the 4-of-8 schedule is chosen)
-int zf_split_cfg() {
-    static const int v = env_int("CHIP_ZF_SPLIT", 0);
-    return v;
-}
+int zf_split_cfg() { return env_int("CHIP_ZF_SPLIT", 0); }  // read per call (tests toggle it)
 bool zf_split(uint32_t k, uint32_t rows, uint64_t bytes, uint64_t count) {
     if (!zf_split_cfg() || count < 16 || bytes < (2ull << 30)) return false;
     // the first large 4-of-8 launch tunes the schedule on slices of its own: not split

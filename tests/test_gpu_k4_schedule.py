@@ -35,3 +35,25 @@ def test_encode_then_decode_tune_and_stay_exact(gpu):
     assert L.chip_zfec_k4_schedule(4) in (0, 1)
     for o in CHECK:
         assert torch.equal(out[o], inp[o]), o
+
+
+def test_two_stream_split_is_exact(gpu, monkeypatch):
+    """CHIP_ZF_SPLIT=1 (opt-in): a >= 2 GiB batch runs as two concurrent halves
+    on two streams; encode and decode stay bit-exact (vs the unsplit launch)."""
+    import torch
+    from carbonado_amd import device
+    count = 160  # 2.5 GiB of input
+    g = torch.Generator(device="cuda").manual_seed(9)
+    inp = torch.randint(0, 256, (count, N), dtype=torch.uint8, device="cuda", generator=g)
+    ref = torch.empty((count, 2 * N), dtype=torch.uint8, device="cuda")
+    device.zfec_encode_batch(inp, N, ref, 4, 8)  # unsplit (and tunes the schedule if needed)
+    monkeypatch.setenv("CHIP_ZF_SPLIT", "1")
+    enc = torch.zeros_like(ref)
+    device.zfec_encode_batch(inp, N, enc, 4, 8)
+    torch.cuda.synchronize()
+    assert torch.equal(enc, ref)
+    out = torch.zeros((count, N), dtype=torch.uint8, device="cuda")
+    device.zfec_decode_batch(enc, N // 4, [0, 3, 4, 5, 6, 7], out, 4, 8)
+    torch.cuda.synchronize()
+    assert torch.equal(out, inp)
+    assert enc[count - 1].cpu().numpy().tobytes() == O.zfec_encode(inp[count - 1].cpu().numpy().tobytes())[0]
