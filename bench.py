@@ -679,12 +679,16 @@ def main():
                                        "BLAKE3 compression (content blocks + parents)"
                                        + ("; step = zfec kernel (HBM-bound) + bao kernels (VALU-bound), "
                                           "achieved over the whole step" if args.mode == "pipeline" else "")}
-        if args.mode in ("encode", "decode") and k == 4 and not args.dry_run:
+        if args.mode in ("encode", "decode") and not args.dry_run:
             from carbonado_amd import _lib
             rows = m if args.mode == "encode" else k  # decode writes the k data shards
-            res["roofline"]["schedule"] = {"k4": _lib.lib().chip_zfec_k4_schedule(rows), "rows": rows,
+            res["roofline"]["schedule"] = {"k4": _lib.lib().chip_zfec_k4_schedule(rows) if k == 4 else None,
+                                           "rows": rows,
+                                           "split": _lib.lib().chip_zfec_split_mode(k, rows),
                                            "note": "zfec 4-of-8 schedule picked on this box by the first launch "
-                                                   "(0 = 2-tile super-tiles at 2 WG/CU, 1 = 1 tile at 4 WG/CU)"}
+                                                   "(0 = 2-tile super-tiles at 2 WG/CU, 1 = 1 tile at 4 WG/CU); "
+                                                   "split: the batch as two concurrent halves (1) or one launch "
+                                                   "(0), picked by timing quarters of the first large batch"}
         if verified_all is not None:
             res["verified_all_objects"] = verified_all
         if aliased is not None:

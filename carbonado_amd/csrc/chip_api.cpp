@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <map>
 #include <memory>
 #include <cstdio>
 #include <cstdlib>
@@ -20,6 +21,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "chip_internal.hpp"
@@ -505,9 +507,7 @@ hipError_t overlap_parts(uint64_t count, uint64_t parts, hipStream_t s, S1 stage
 }
 
 // A batch cut into two halves launched side by side on the two pipeline
-// streams (fork/join with events on s).  Two concurrent launches of the
-// HBM-bound zfec kernel move more bytes per second than one launch of the
-// whole batch.
+// streams (fork/join with events on s).
 template <typename F>
 hipError_t split_pair(uint64_t count, hipStream_t s, F launch) {
     PipeStreams *ps;
@@ -517,6 +517,8 @@ hipError_t split_pair(uint64_t count, hipStream_t s, F launch) {
     if ((e = hipStreamWaitEvent(ps->k1, ps->fork, 0)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(ps->k3, ps->fork, 0)) != hipSuccess) return e;
     const uint64_t half = count / 2;
+    if (const int us = env_int("CHIP_ZF_SPLIT_DELAY_US", 0); us > 0)  // experiment: start the halves out of phase
+        if ((e = delay_on_stream((uint32_t)us, ps->k3)) != hipSuccess) return e;
     if ((e = launch(0, half, ps->k1)) != hipSuccess) return e;
     if ((e = launch(half, count - half, ps->k3)) != hipSuccess) return e;
     if ((e = hipEventRecord(ps->join1, ps->k1)) != hipSuccess) return e;
@@ -525,13 +527,65 @@ hipError_t split_pair(uint64_t count, hipStream_t s, F launch) {
     return hipStreamWaitEvent(s, ps->join3, 0);
 }
 
-// CHIP_ZF_SPLIT: 0 = one launch per batch, 1 = two concurrent halves for
-// batches of >= 2 GiB of input (once the 4-of-8 schedule is chosen)
-int zf_split_cfg() { return env_int("CHIP_ZF_SPLIT", 0); }  // read per call (tests toggle it)
-bool zf_split(uint32_t k, uint32_t rows, uint64_t bytes, uint64_t count) {
-    if (!zf_split_cfg() || count < 16 || bytes < (2ull << 30)) return false;
-    // the first large 4-of-8 launch tunes the schedule on slices of its own: not split
-    return !(k == 4 && rows <= 8 && chip_zfec_k4_schedule(rows) < 0);
+// A zfec batch as one launch or as two concurrent halves.  On some boxes
+// the two halves move 13 % more bytes per second than one launch, on others
+// 1-2.5 % less, so the first eligible batch (>= 2 GiB of
+// input, >= 16 objects) of each (device, k, rows) class times its own
+// quarters both ways — single, split, single, split, events on s — keeps the
+// faster for the rest of that batch and for later ones.  CHIP_ZF_SPLIT=0|1
+// forces one (read per call: tests toggle it).  The first large 4-of-8 batch
+// tunes the kernel schedule (k4_tune) and runs single.
+std::mutex g_split_mu;
+std::map<std::tuple<int, uint32_t, uint32_t>, int> g_split;  // (device, k, rows) -> 0 single, 1 split
+
+template <typename F>  // launch(o0, cnt, stream) -> hipError_t, objects [o0, o0 + cnt)
+hipError_t zf_run(uint32_t k, uint32_t rows, uint64_t in_bytes, uint64_t count, hipStream_t s, F launch) {
+    const char *env = std::getenv("CHIP_ZF_SPLIT");
+    const bool eligible = count >= 16 && in_bytes >= (2ull << 30) &&
+                          !(k == 4 && rows <= 8 && chip_zfec_k4_schedule(rows) < 0);
+    if (!eligible || (env && !std::atoi(env))) return launch(0, count, s);
+    if (env) return split_pair(count, s, launch);
+    const auto key = std::make_tuple(selected_device(), k, rows);
+    int mode = -1;
+    {
+        std::lock_guard<std::mutex> lk(g_split_mu);
+        auto it = g_split.find(key);
+        if (it != g_split.end()) mode = it->second;
+    }
+    if (mode == 0) return launch(0, count, s);
+    if (mode == 1) return split_pair(count, s, launch);
+    hipEvent_t ev[5] = {};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
+    if (e == hipSuccess) e = hipEventRecord(ev[0], s);
+    const uint64_t q = count / 4;
+    uint64_t cnt[4];
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) {
+        const uint64_t o0 = i * q;
+        cnt[i] = i == 3 ? count - 3 * q : q;
+        if (i & 1)
+            e = split_pair(cnt[i], s, [&](uint64_t o, uint64_t c, hipStream_t st) { return launch(o0 + o, c, st); });
+        else
+            e = launch(o0, cnt[i], s);
+        if (e == hipSuccess) e = hipEventRecord(ev[i + 1], s);
+    }
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    if (e == hipSuccess) e = hipEventSynchronize(ev[4]);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventElapsedTime(&t[i], ev[i], ev[i + 1]);
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    if (e != hipSuccess) return e;
+    const double single = std::min(t[0] / cnt[0], t[2] / cnt[2]), split = std::min(t[1] / cnt[1], t[3] / cnt[3]);
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    g_split[key] = split < single ? 1 : 0;
+    return hipSuccess;
+}
+
+int zf_split_known(uint32_t k, uint32_t rows) {
+    if (const char *env = std::getenv("CHIP_ZF_SPLIT")) return std::atoi(env) ? 1 : 0;
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    auto it = g_split.find(std::make_tuple(selected_device(), k, rows));
+    return it == g_split.end() ? -1 : it->second;
 }
 
 int pipe_parts_cfg() {
@@ -895,15 +949,10 @@ int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     if (aliased && (uint64_t)k * C > n)  // the zero padding of encoding.rs:53-55 becomes part of shard k-1
         CHIP_HIP(hipMemset2DAsync(d_out + n, out_stride ? out_stride : (uint64_t)m * C, 0, (uint64_t)k * C - n,
                                   count, s));
-    if (zf_split(k, aliased ? m - k : m, count * n, count)) {
-        CHIP_HIP(split_pair(count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
-            GfLaunch L{d_in + o0 * in_stride, d_out + o0 * out_stride, in_stride, out_stride, n, C, cnt};
-            return gf_apply(p, L, st);
-        }));
-        return CHIP_OK;
-    }
-    GfLaunch L{d_in, d_out, in_stride, out_stride, n, C, count};
-    CHIP_HIP(gf_apply(p, L, s));
+    CHIP_HIP(zf_run(k, aliased ? m - k : m, count * n, count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
+        GfLaunch L{d_in + o0 * in_stride, d_out + o0 * out_stride, in_stride, out_stride, n, C, cnt};
+        return gf_apply(p, L, st);
+    }));
     return CHIP_OK;
 }
 
@@ -1015,22 +1064,21 @@ int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
         slot_off[s] = (uint64_t)sel[s] * chunk_len;
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (zf_split(k, k, count * k * chunk_len, count)) {
-        int half_st = CHIP_OK;
-        const hipError_t e = split_pair(count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
-            const int r = zfec_decode_device(k, m, d_in + o0 * in_stride, in_stride, slot_off, sel, chunk_len, cnt,
-                                             d_out + o0 * out_stride, out_stride, st);
-            if (r != CHIP_OK) half_st = r;
-            return r == CHIP_OK ? hipSuccess : hipErrorInvalidValue;
-        });
-        if (half_st != CHIP_OK) return half_st;
-        CHIP_HIP(e);
-        return CHIP_OK;
-    }
-    return zfec_decode_device(k, m, d_in, in_stride, slot_off, sel, chunk_len, count, d_out, out_stride, s);
+    int part_st = CHIP_OK;
+    const hipError_t e = zf_run(k, k, count * k * chunk_len, count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
+        const int r = zfec_decode_device(k, m, d_in + o0 * in_stride, in_stride, slot_off, sel, chunk_len, cnt,
+                                         d_out + o0 * out_stride, out_stride, st);
+        if (r != CHIP_OK) part_st = r;
+        return r == CHIP_OK ? hipSuccess : hipErrorInvalidValue;
+    });
+    if (part_st != CHIP_OK) return part_st;
+    CHIP_HIP(e);
+    return CHIP_OK;
 }
 
 // ---- bao ---------------------------------------------------------------
+
+int chip_zfec_split_mode(uint32_t k, uint32_t rows) { return zf_split_known(k, rows); }
 
 int chip_bao_encode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                               uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash,

@@ -63,6 +63,8 @@ struct GfLaunch {
 // Plans with more than ZF_MAXP computed rows run in passes of ZF_MAXP rows
 // (copies ride on the first pass); k > ZF_MAXK uses the generic kernel.
 hipError_t gf_apply(const GfPlan &plan, const GfLaunch &L, hipStream_t stream);
+// Delay the work queued behind it on `stream` by `us` microseconds (one spinning wave).
+hipError_t delay_on_stream(uint32_t us, hipStream_t stream);
 
 // ---- bao / BLAKE3 ------------------------------------------------------
 uint64_t bao_encoded_len(uint64_t n);

@@ -108,25 +108,39 @@ __device__ __forceinline__ uint32_t comp(const u32x4 &v, int d) {
 //   3  XCD-grouped chunks: runs of CH consecutive tiles dealt as in 1, each
 //      run walked in order by one workgroup (long sequential streams per
 //      shard; tools/write_probe: HBM writes 5.0 -> 5.9 TB/s)
+//   5  as 3, each workgroup starting its runs at its own rotated tile (a
+//      per-workgroup offset mod CH, wrapping inside the run).  Runs begin at
+//      multiples of CH tiles in every object and shard, so under 3 all
+//      workgroups advance in lockstep at the same offset inside their runs
+//      and every stream in flight shares the same low address bits.
 // Falls back to 0 when G is not a multiple of 8.
 template <int MAP>
 struct TileIter {
     uint64_t T, c, t_in, end, stride, base, CH;
+    uint64_t rot = 0, rl = 0, rotr = 0;  // MAP 5: rotation, current run length, rotation mod rl
     int mode;
+    __device__ void start_run() {
+        rl = c * CH >= T ? 0 : (T - c * CH < CH ? T - c * CH : CH);
+        rotr = rl == CH ? rot : (rl ? rot % rl : 0);
+    }
     __device__ TileIter(uint64_t total, uint64_t ch) : T(total), t_in(0), CH(ch < 1 ? 1 : ch) {
         const uint64_t G = gridDim.x, b = blockIdx.x;
-        mode = ((MAP == 1 || MAP == 3) && (G & 7)) ? 0 : MAP;
+        mode = ((MAP == 1 || MAP == 3 || MAP == 5) && (G & 7)) ? 0 : MAP;
         if (mode == 2) {
             const uint64_t chunk = (T + G - 1) / G;
             c = b * chunk;
             end = c + chunk < T ? c + chunk : T;
             stride = 1;
             base = 0;
-        } else if (mode == 1 || mode == 3) {
+        } else if (mode == 1 || mode == 3 || mode == 5) {
             base = (b % 8) * (G / 8) + b / 8;
             c = base;
             stride = G;
             end = T;
+            if (mode == 5) {
+                rot = (b * 37 + (b >> 3)) % CH;
+                start_run();
+            }
         } else {
             c = b;
             stride = G;
@@ -135,6 +149,19 @@ struct TileIter {
         }
     }
     __device__ bool next(uint64_t &t) {
+        if (mode == 5) {
+            if (t_in == rl) {
+                c += stride;
+                t_in = 0;
+                start_run();
+            }
+            if (rl == 0) return false;
+            uint64_t i = t_in + rotr;
+            if (i >= rl) i -= rl;
+            t = c * CH + i;
+            ++t_in;
+            return true;
+        }
         if (mode == 3) {
             if (t_in == CH) { c += stride; t_in = 0; }
             t = c * CH + t_in;

@@ -399,6 +399,18 @@ hipError_t k4_tune(const GfPlan &p, const GfLaunch &L, hipStream_t stream, uint3
 
 }  // namespace
 
+// One wave spinning on the 100 MHz wall clock for `us` microseconds: delays
+// the work queued behind it on its stream (split experiments, CHIP_ZF_SPLIT_DELAY_US).
+__global__ void delay_kernel(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+}
+
+hipError_t delay_on_stream(uint32_t us, hipStream_t stream) {
+    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, stream, (uint64_t)us * 100);
+    return hipGetLastError();
+}
+
 hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
     if (L.count == 0 || L.C == 0) return hipSuccess;
     if (p.k > (uint32_t)ZF_MAXK) return apply_generic(p, L, stream);

@@ -131,6 +131,11 @@ CHIP_API const char *chip_last_device_error(void);
  * data shards, 4 = parity only or a 2-erasure decode): 0 or 1, -1 = not
  * chosen yet.  The first launch of >= 1 GiB picks it. */
 CHIP_API int chip_zfec_k4_schedule(uint32_t rows);
+/* Diagnostics: whether this process runs large zfec batches of shape
+ * (k, rows) as one launch (0) or as two concurrent halves on two streams (1),
+ * -1 = not decided yet.  The first batch of >= 2 GiB decides by timing its
+ * own quarters both ways; CHIP_ZF_SPLIT=0|1 forces it. */
+CHIP_API int chip_zfec_split_mode(uint32_t k, uint32_t rows);
 
 /* ---- size helpers (host only, no device needed) ----------------------- */
 /* utils.rs:47-58 with FEC_K generalised to k: target = ceil(n/(1024k))*1024k,

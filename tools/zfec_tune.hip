@@ -123,8 +123,8 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {V<2, 3, true, 32, 2, 0, true>(2), V<1, 3, true, 64, 1, 0, true>(4), V<1, 3, true, 64, 1, 0, true>(3),
-              V<2, 3, true, 32, 2, 0, true>(3), V<1, 3, true, 64, 1, 0, false>(4)};
+        vs = {V<2, 3, true, 32, 2, 0, true>(2), V<2, 5, true, 32, 2, 0, true>(2), V<1, 3, true, 64, 1, 0, true>(4),
+              V<1, 5, true, 64, 1, 0, true>(4), V<2, 5, true, 16, 2, 0, true>(2), V<2, 5, true, 64, 2, 0, true>(2)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
