@@ -58,6 +58,12 @@ def parse():
     ap.add_argument("--level", type=int, default=12, help="e2e mode: Format bits (Bao|Zfec = 12)")
     ap.add_argument("--slots", type=int, default=3, help="e2e mode: pipeline slots (streams)")
     ap.add_argument("--slice-mib", type=int, default=256, help="e2e mode: input bytes per pipeline slice")
+    ap.add_argument("--in-pad-kib", type=int, default=0, help="encode/decode: extra bytes per input object row")
+    ap.add_argument("--out-pad-kib", type=int, default=0, help="encode/decode: extra bytes per output object row")
+    ap.add_argument("--prealloc-gib", type=float, default=0, help="allocate (and keep) this much HBM first")
+    ap.add_argument("--alloc", choices=["contiguous", "torch"], default="contiguous",
+                    help="encode/decode batch buffers: physically contiguous HBM through the library's allocator "
+                         "(carbonado_amd.device.empty_batch) or torch's caching allocator")
     ap.add_argument("--host-threads", type=int, default=16,
                     help="e2e mode: host threads for the Snappy/Ecies stages (the GPU box's CPU share is 16)")
     ap.add_argument("--erase", default="1,2", help="decode mode: shards dropped")
@@ -262,26 +268,34 @@ class Workload:
         p32, c32 = ctypes.c_uint32(), ctypes.c_uint32()
         L.chip_calc_padding_len(n, k, ctypes.byref(p32), ctypes.byref(c32))
         self.C = C = c32.value
-        self.inp = torch.empty((count, n), dtype=torch.uint8, device=dev)
+        self.prealloc = (torch.empty(int(args.prealloc_gib * 2**30), dtype=torch.uint8, device=dev)
+                         if args.prealloc_gib else None)
+        def batch_buf(shape):
+            if args.alloc == "contiguous" and args.mode in ("encode", "decode"):
+                return device.empty_batch(shape, dev)
+            return torch.empty(shape, dtype=torch.uint8, device=dev)
+        self.batch_buf = batch_buf
+        self.inp_full = batch_buf((count, n + args.in_pad_kib * 1024))
+        self.inp = self.inp_full[:, :n] if args.in_pad_kib else self.inp_full
         self.scatter_s = None
         rng = object_range(rank, world, world * count)
         if args.scatter and world > 1:
             self.scatter_s = self._scatter_inputs(rank, world)
         else:
-            fill_random(self.inp, SEED + rng.start)
+            fill_random(self.inp_full, SEED + rng.start)
         if args.mode == "encode":
-            self.out = torch.empty((count, m * C), dtype=torch.uint8, device=dev)
-            self.step = lambda: device.zfec_encode_batch(self.inp, n, self.out, k, m)
+            self.out = batch_buf((count, m * C + args.out_pad_kib * 1024))
+            self.step = lambda: device.zfec_encode_batch(self.inp_full, n, self.out, k, m)
             self.alg_bytes = count * (n + m * C)  # read the input + write all m shards
             ng = (m - k + 3) // 4
             self.kernel = f"gf_apply_kernel<{k},{ng}>"
             self.kernel_sym = f"gf_apply_kernel<{k}, {ng},"
         elif args.mode == "decode":
-            self.enc = torch.empty((count, m * C), dtype=torch.uint8, device=dev)
+            self.enc = batch_buf((count, m * C))
             device.zfec_encode_batch(self.inp, n, self.enc, k, m)
             erased = {int(x) for x in args.erase.split(",") if x}
             self.keep = [i for i in range(m) if i not in erased]
-            self.out = torch.empty((count, k * C), dtype=torch.uint8, device=dev)
+            self.out = batch_buf((count, k * C))
             self.step = lambda: device.zfec_decode_batch(self.enc, C, self.keep, self.out, k, m)
             self.alg_bytes = count * (2 * k * C)  # read k shares + write k data shards
             self.kernel = f"gf_apply_kernel<{k},1> (decode, erased {sorted(erased)})"

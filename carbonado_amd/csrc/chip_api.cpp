@@ -1080,6 +1080,47 @@ int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
 
 int chip_zfec_split_mode(uint32_t k, uint32_t rows) { return zf_split_known(k, rows); }
 
+// Batch buffers in physically contiguous HBM (hipDeviceMallocContiguous):
+// large fragments, so address translation covers a whole multi-GiB batch
+// (K1 on the same box: +1.5-4 % and no spread from one process to the next,
+// DESIGN.md §3).  Falls back to hipMalloc when no contiguous range is free.
+int chip_device_alloc(uint64_t bytes, void **ptr) {
+    if (!ptr) return CHIP_ERR_INVALID_ARG;
+    *ptr = nullptr;
+    int st = use_device();
+    if (st != CHIP_OK) return st;
+    void *p = nullptr;
+    const size_t sz = bytes ? bytes : 1;
+    if (hipExtMallocWithFlags(&p, sz, hipDeviceMallocContiguous) != hipSuccess || !p) {
+        (void)hipGetLastError();
+        p = nullptr;
+        CHIP_HIP(hipMalloc(&p, sz));
+    }
+    *ptr = p;
+    return CHIP_OK;
+}
+
+int chip_device_free(void *ptr) {
+    if (!ptr) return CHIP_OK;
+    CHIP_HIP(hipFree(ptr));
+    return CHIP_OK;
+}
+
+// torch.cuda.memory.CUDAPluggableAllocator hooks over chip_device_alloc/free
+void *chip_torch_alloc(ssize_t size, int device, void *stream) {
+    (void)stream;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    void *p = nullptr;
+    return chip_device_alloc(size > 0 ? (uint64_t)size : 0, &p) == CHIP_OK ? p : nullptr;
+}
+
+void chip_torch_free(void *ptr, ssize_t size, int device, void *stream) {
+    (void)size;
+    (void)stream;
+    (void)hipSetDevice(device);
+    (void)chip_device_free(ptr);
+}
+
 int chip_bao_encode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                               uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash,
                               void *d_scratch, void *stream) {

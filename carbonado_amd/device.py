@@ -46,6 +46,28 @@ def zfec_decode_batch(enc: torch.Tensor, chunk_len: int, indices, out: torch.Ten
                                                 enc.shape[0], _p(out), out.shape[1], _stream()))
 
 
+_pools = {}
+
+
+def batch_pool(device=None):
+    """A torch MemPool whose segments come from chip_device_alloc (physically
+    contiguous HBM where available), for multi-GiB batch buffers."""
+    dev = torch.device(device or "cuda")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _pools:
+        alloc = torch.cuda.memory.CUDAPluggableAllocator(str(_lib.LIB_PATH), "chip_torch_alloc", "chip_torch_free")
+        with torch.cuda.device(idx):
+            _pools[idx] = (alloc, torch.cuda.MemPool(alloc.allocator()))
+    return _pools[idx][1]
+
+
+def empty_batch(shape, device=None) -> torch.Tensor:
+    """uint8 tensor for a batch buffer, allocated in batch_pool()."""
+    dev = torch.device(device or "cuda")
+    with torch.cuda.device(dev), torch.cuda.use_mem_pool(batch_pool(dev)):
+        return torch.empty(shape, dtype=torch.uint8, device=dev)
+
+
 def bao_scratch(n: int, count: int, device=None) -> torch.Tensor:
     size = _lib.lib().chip_bao_scratch_len(n, count)
     return torch.empty(size, dtype=torch.uint8, device=device or "cuda")

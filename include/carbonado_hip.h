@@ -47,6 +47,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <sys/types.h> /* ssize_t */
 
 #ifdef __cplusplus
 extern "C" {
@@ -136,6 +137,19 @@ CHIP_API int chip_zfec_k4_schedule(uint32_t rows);
  * -1 = not decided yet.  The first batch of >= 2 GiB decides by timing its
  * own quarters both ways; CHIP_ZF_SPLIT=0|1 forces it. */
 CHIP_API int chip_zfec_split_mode(uint32_t k, uint32_t rows);
+
+/* ---- batch buffers ------------------------------------------------------ */
+/* Device memory for batch buffers, physically contiguous where the device
+ * has such a range free (hipDeviceMallocContiguous; else hipMalloc): the
+ * streaming kernels run faster and steadier over it.
+ * Any 16-B aligned device memory works with the batch entry points. */
+CHIP_API int chip_device_alloc(uint64_t bytes, void **ptr);
+CHIP_API int chip_device_free(void *ptr);
+/* The same, with the signatures torch.cuda.memory.CUDAPluggableAllocator
+ * loads (size, device, stream): a torch MemPool over these hands out
+ * contiguous tensors (carbonado_amd.device.empty_batch). */
+CHIP_API void *chip_torch_alloc(ssize_t size, int device, void *stream);
+CHIP_API void chip_torch_free(void *ptr, ssize_t size, int device, void *stream);
 
 /* ---- size helpers (host only, no device needed) ----------------------- */
 /* utils.rs:47-58 with FEC_K generalised to k: target = ceil(n/(1024k))*1024k,

@@ -87,11 +87,17 @@ int main(int argc, char **argv) {
     const int K = shape == 8 ? 8 : 4, M = 2 * K;
     const uint64_t n = 16ull << 20, C = n / K;
     uint8_t *in, *out;
-    CK(hipMalloc(&in, count * n));
+    // ZT_CONTIG=1: physically contiguous device allocations (hipDeviceMallocContiguous)
+    const bool contig = getenv("ZT_CONTIG") && atoi(getenv("ZT_CONTIG"));
+    auto dmalloc = [&](uint8_t **p, size_t bytes) {
+        if (contig) CK(hipExtMallocWithFlags(reinterpret_cast<void **>(p), bytes, hipDeviceMallocContiguous));
+        else CK(hipMalloc(p, bytes));
+    };
+    dmalloc(&in, count * n);
     // bao layout variants write a whole bao stream per object (8 + 2n + 64 (N - 1) bytes)
     const uint64_t Nch = 2 * n / 1024;
     const uint64_t blen = 8 + 2 * n + 64 * (Nch - 1), bstride = (blen + 255) / 256 * 256;
-    CK(hipMalloc(&out, count * (bstride > 2 * n ? bstride : 2 * n)));
+    dmalloc(&out, count * (bstride > 2 * n ? bstride : 2 * n));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xCA4B0AD0ull);
     CK(hipMemset(out, 0, count * 2 * n));
 
@@ -123,8 +129,7 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {V<2, 3, true, 32, 2, 0, true>(2), V<2, 5, true, 32, 2, 0, true>(2), V<1, 3, true, 64, 1, 0, true>(4),
-              V<1, 5, true, 64, 1, 0, true>(4), V<2, 5, true, 16, 2, 0, true>(2), V<2, 5, true, 64, 2, 0, true>(2)};
+        vs = {V<2, 3, true, 32, 2, 0, true>(2), V<1, 3, true, 64, 1, 0, true>(4), V<2, 5, true, 32, 2, 0, true>(2)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
