@@ -542,7 +542,10 @@ class Workload:
         from carbonado_amd import device
         n, k, m = self.n, self.k, self.m
         self.out[:, :n].copy_(self.inp)
-        el, ms = self.time_steps(steps, warmup, world, lambda: device.zfec_encode_batch(self.out, n, self.out, k, m))
+        step = lambda: device.zfec_encode_batch(self.out, n, self.out, k, m)  # noqa: E731
+        for _ in range(2):  # the library's self-tuning for this shape (4 output shards per column)
+            step()
+        el, ms = self.time_steps(steps, warmup, world, step)
         from oracle import oracle as O
         ok = self.out[0].cpu().numpy().tobytes() == O.zfec_encode(self.inp[0].cpu().numpy().tobytes(), k, m)[0]
         return el, ms, ok
