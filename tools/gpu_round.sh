@@ -21,11 +21,13 @@ timeout -k 10 600 python3 bench.py --mode e2e --level 12 --objects 256 --steps 3
 timeout -k 10 600 python3 bench.py --mode e2e-decode --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 > $O/bench_e2ed15.log 2>&1
 timeout -k 10 600 python3 bench.py --mode scrub --steps 2 --warmup 1 --cpu-seconds 8 > $O/bench_scrub.log 2>&1
 timeout -k 10 600 python3 bench.py --mode hasher --steps 3 --warmup 1 --cpu-seconds 8 > $O/bench_hasher.log 2>&1
-# the profiles run the 4-of-8 schedule the encode line picked on this box, so
-# that every profiled launch is a whole-batch launch of that kernel (the first
-# launch of a process otherwise tunes on count/8-object slices)
+# the profiles run the 4-of-8 schedule and the one-launch/two-halves choice
+# the encode line picked on this box, so that every profiled launch is a
+# whole-batch launch of that kernel (the first large batches of a process
+# otherwise tune on slices of themselves)
 export CHIP_ZFEC_K4_SCHED=$(python3 -c "import json,sys; ls=[l for l in open(sys.argv[1]) if l.startswith('{')]; print(json.loads(ls[-1])['roofline']['schedule']['k4'])" $O/bench_encode.log)
-echo "CHIP_ZFEC_K4_SCHED=$CHIP_ZFEC_K4_SCHED" > $O/schedule.txt
+export CHIP_ZF_SPLIT=$(python3 -c "import json,sys; ls=[l for l in open(sys.argv[1]) if l.startswith('{')]; print(max(0, json.loads(ls[-1])['roofline']['schedule']['split']))" $O/bench_encode.log)
+echo "CHIP_ZFEC_K4_SCHED=$CHIP_ZFEC_K4_SCHED CHIP_ZF_SPLIT=$CHIP_ZF_SPLIT" > $O/schedule.txt
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o stats --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-verify --no-aliased > $O/prof.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o fetch --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-aliased > $O/pmc_fetch.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o write --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-aliased > $O/pmc_write.log 2>&1
