@@ -554,6 +554,8 @@ hipError_t zf_run(uint32_t k, uint32_t rows, uint64_t in_bytes, uint64_t count, 
     }
     if (mode == 0) return launch(0, count, s);
     if (mode == 1) return split_pair(count, s, launch);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;  // tuning waits on events: not while capturing
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return launch(0, count, s);
     hipEvent_t ev[5] = {};
     hipError_t e = hipSuccess;
     for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);

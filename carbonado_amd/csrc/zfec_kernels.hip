@@ -310,7 +310,10 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
             for (uint32_t j = 0; j < p.k; ++j) rows += p.copy_off[j] != NO_OUT;
         if (sched < 0) sched = k4_known(rows);
         if (sched < 0) {
-            if (L.count >= 8 && L.count * L.valid >= K4_TUNE_MIN)
+            // tuning waits on events: not inside a stream capture (hipGraph)
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            const bool capturing = hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+            if (!capturing && L.count >= 8 && L.count * L.valid >= K4_TUNE_MIN)
                 return k4_tune(p, L, stream, row0, nrows, copies, rows);
             sched = 0;
         }
