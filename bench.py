@@ -705,7 +705,7 @@ def main():
         if args.mode in ("encode", "decode") and not args.dry_run:
             from carbonado_amd import _lib
             rows = m if args.mode == "encode" else k  # decode writes the k data shards
-            res["roofline"]["schedule"] = {"k4": _lib.lib().chip_zfec_k4_schedule(rows) if k == 4 else None,
+            res["roofline"]["schedule"] = {"k4": _lib.lib().chip_zfec_schedule(k, rows),
                                            "rows": rows,
                                            "split": _lib.lib().chip_zfec_split_mode(k, rows),
                                            "note": "zfec 4-of-8 schedule picked on this box by the first launch "

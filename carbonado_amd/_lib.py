@@ -51,6 +51,7 @@ SIGNATURES = {
     "chip_init": (ctypes.c_int, [ctypes.c_int]),
     "chip_last_device_error": (ctypes.c_char_p, []),
     "chip_zfec_k4_schedule": (ctypes.c_int, [ctypes.c_uint32]),
+    "chip_zfec_schedule": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32]),
     "chip_zfec_split_mode": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32]),
     "chip_device_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "chip_device_free": (ctypes.c_int, [ctypes.c_void_p]),

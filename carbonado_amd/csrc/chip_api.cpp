@@ -534,7 +534,7 @@ hipError_t split_pair(uint64_t count, hipStream_t s, F launch) {
 // quarters both ways — single, split, single, split, events on s — keeps the
 // faster for the rest of that batch and for later ones.  CHIP_ZF_SPLIT=0|1
 // forces one (read per call: tests toggle it).  The first large 4-of-8 batch
-// tunes the kernel schedule (k4_tune) and runs single.
+// (4-of-8 or 8-of-16) tunes the kernel schedule (k4_tune) and runs single.
 std::mutex g_split_mu;
 std::map<std::tuple<int, uint32_t, uint32_t>, int> g_split;  // (device, k, rows) -> 0 single, 1 split
 
@@ -542,7 +542,7 @@ template <typename F>  // launch(o0, cnt, stream) -> hipError_t, objects [o0, o0
 hipError_t zf_run(uint32_t k, uint32_t rows, uint64_t in_bytes, uint64_t count, hipStream_t s, F launch) {
     const char *env = std::getenv("CHIP_ZF_SPLIT");
     const bool eligible = count >= 16 && in_bytes >= (2ull << 30) &&
-                          !(k == 4 && rows <= 8 && chip_zfec_k4_schedule(rows) < 0);
+                          !((k == 4 || k == 8) && chip_zfec_schedule(k, rows) < 0);
     if (!eligible || (env && !std::atoi(env))) return launch(0, count, s);
     if (env) return split_pair(count, s, launch);
     const auto key = std::make_tuple(selected_device(), k, rows);

@@ -157,6 +157,20 @@ KernelInfo k4_info(int s) {
     return ki;
 }
 
+// The 8-of-16 shape (K = 8, NG = 2): the same kernel at its occupancy of 2
+// workgroups/CU (S0) or at 1 (S1).  Which is faster flips with the process's
+// HBM placement (tools/zfec_tune: 5272 vs 5164 GB/s in one process, 4687 vs
+// 4934 in another).
+KernelInfo k8_info(int s) {
+    KernelInfo ki = make_info<8, 2>();
+    if (s == 1) ki.bpc_cap = 1;
+    return ki;
+}
+
+// shapes with two schedules to pick from at run time
+bool tunable_shape(uint32_t k, int ng) { return (k == 4 && ng == 1) || (k == 8 && ng == 2); }
+KernelInfo tuned_info(uint32_t k, int s) { return k == 4 ? k4_info(s) : k8_info(s); }
+
 struct DevTable {
     void *ptr = nullptr;
     size_t bytes = 0;
@@ -176,7 +190,7 @@ std::map<int, uint8_t *> g_multab;                  // per device
 // batch with it; later launches use the choice.  CHIP_ZFEC_K4_SCHED=0|1 fixes
 // the schedule (A/B runs; CHIP_ZFEC_K4_U1 = 1, the older switch).
 constexpr uint64_t K4_TUNE_MIN = uint64_t(1) << 30;  // input bytes of a launch worth tuning on
-std::map<std::pair<int, int>, int> g_k4;               // (device, output rows) -> schedule
+std::map<std::tuple<int, int, int>, int> g_k4;         // (device, k, output rows) -> schedule
 
 int k4_forced() {
     static const int f = [] {
@@ -186,11 +200,11 @@ int k4_forced() {
     return f;
 }
 
-int k4_known(int rows) {
+int k4_known(int k, int rows) {
     const int f = k4_forced();
     if (f >= 0) return f;
     std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_k4.find({selected_device(), rows});
+    auto it = g_k4.find(std::make_tuple(selected_device(), k, rows));
     return it == g_k4.end() ? -1 : it->second;
 }
 
@@ -205,6 +219,8 @@ int grid_for(const KernelInfo &ki) {
         per_cu < 1)
         per_cu = 1;
     if (ki.bpc_cap > 0 && per_cu > ki.bpc_cap) per_cu = ki.bpc_cap;
+    if (const char *e = std::getenv("CHIP_ZF_GRID_BPC"))  // calibration override (tools)
+        per_cu = std::max(1, std::atoi(e));
     const int g = per_cu * num_cus();
     g_grid[key] = g;
     return g;
@@ -304,11 +320,11 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     const int ng = nrows > 4 ? 2 : 1;
     KernelInfo ki;
     if (!lookup_fast((int)p.k, ng, ki)) return hipErrorInvalidValue;
-    if (p.k == 4 && ng == 1 && !L.bao_off) {
+    if (tunable_shape(p.k, ng) && !L.bao_off) {
         int rows = (int)nrows;  // output shards written per column
         if (copies)
             for (uint32_t j = 0; j < p.k; ++j) rows += p.copy_off[j] != NO_OUT;
-        if (sched < 0) sched = k4_known(rows);
+        if (sched < 0) sched = k4_known((int)p.k, rows);
         if (sched < 0) {
             // tuning waits on events: not inside a stream capture (hipGraph)
             hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -317,7 +333,7 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
                 return k4_tune(p, L, stream, row0, nrows, copies, rows);
             sched = 0;
         }
-        ki = k4_info(sched);
+        ki = tuned_info(p.k, sched);
     }
     ApplyArgs a;
     std::memset(&a, 0, sizeof a);
@@ -395,7 +411,7 @@ hipError_t k4_tune(const GfPlan &p, const GfLaunch &L, hipStream_t stream, uint3
     const int s = std::min(t[1], t[3]) < std::min(t[0], t[2]) ? 1 : 0;
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        g_k4[{selected_device(), rows}] = s;
+        g_k4[std::make_tuple(selected_device(), (int)p.k, rows)] = s;
     }
     return gf_apply_pass(p, slice(4 * piece, L.count - 4 * piece), stream, row0, nrows, copies, s);
 }
@@ -428,4 +444,5 @@ hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
 
 }  // namespace chip
 
-extern "C" int chip_zfec_k4_schedule(uint32_t rows) { return chip::k4_known((int)rows); }
+extern "C" int chip_zfec_k4_schedule(uint32_t rows) { return chip::k4_known(4, (int)rows); }
+extern "C" int chip_zfec_schedule(uint32_t k, uint32_t rows) { return chip::k4_known((int)k, (int)rows); }

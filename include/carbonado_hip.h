@@ -132,6 +132,9 @@ CHIP_API const char *chip_last_device_error(void);
  * data shards, 4 = parity only or a 2-erasure decode): 0 or 1, -1 = not
  * chosen yet.  The first launch of >= 1 GiB picks it. */
 CHIP_API int chip_zfec_k4_schedule(uint32_t rows);
+/* The same for any shape with two schedules (k = 4: as above; k = 8, the
+ * 8-of-16 shape: 0 = 2 workgroups/CU, 1 = 1); -1 for other shapes. */
+CHIP_API int chip_zfec_schedule(uint32_t k, uint32_t rows);
 /* Diagnostics: whether this process runs large zfec batches of shape
  * (k, rows) as one launch (0) or as two concurrent halves on two streams (1),
  * -1 = not decided yet.  The first batch of >= 2 GiB decides by timing its

@@ -134,7 +134,8 @@ int main(int argc, char **argv) {
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
               V16<1, 3, true, 4, 64, 2, 2, true>(2),    V16<1, 3, true, 4, 16, 2, 1, true>(2),
-              V16<1, 3, true, 4, 64, 3, 1>(2),          V16<1, 3, false, 4, 64, 2, 1, true>(2)};
+              V16<1, 3, true, 4, 64, 3, 1>(2),          V16<1, 3, false, 4, 64, 2, 1, true>(2),
+              V16<1, 3, false, 4, 64, 2, 1, true>(1),   V16<1, 3, false, 4, 32, 2, 1, true>(2)};
     unsigned long long *dsum;
     CK(hipMalloc(&dsum, 8));
     std::vector<std::vector<float>> ms(vs.size());
