@@ -709,7 +709,8 @@ def main():
                                            "rows": rows,
                                            "split": _lib.lib().chip_zfec_split_mode(k, rows),
                                            "note": "zfec 4-of-8 schedule picked on this box by the first launch "
-                                                   "(0 = 2-tile super-tiles at 2 WG/CU, 1 = 1 tile at 4 WG/CU); "
+                                                   "(4-of-8: 0 = 2-tile super-tiles at 2 WG/CU, 1 = 1 tile at 4 WG/CU, 2 = super-tiles "
+                                                   "at 1 WG/CU; 8-of-16: 0 = 2 WG/CU, 1 = 1); "
                                                    "split: the batch as two concurrent halves (1) or one launch "
                                                    "(0), picked by timing quarters of the first large batch"}
         if verified_all is not None:

@@ -144,15 +144,19 @@ bool lookup_fast(int k, int ng, KernelInfo &out) {
 #undef CHIP_CASE
 }
 
-// The two 4-of-8 schedules (tools/zfec_tune.hip): S0 = super-tiles of 2
-// column tiles, the next super-tile prefetched, 2 workgroups/CU; S1 = one
-// tile, the next prefetched, 4 workgroups/CU.
+// The 4-of-8 schedules (tools/zfec_tune.hip): S0 = super-tiles of 2 column
+// tiles, the next super-tile prefetched, 2 workgroups/CU; S1 = one tile, the
+// next prefetched, 4 workgroups/CU; S2 = S0 at 1 workgroup/CU.  Each won in
+// some process of the same box (profiles/r1x_k4_schedules.txt: 5446 / 5370 /
+// 5228 GB/s for the winner vs 5240 / 5236 / 5161 for S0).
 KernelInfo k4_info(int s) {
     KernelInfo ki = make_info<4, 1>();
     if (s == 1) {
         ki.fn = gf_apply_kernel<4, 1, 1, ZF_MAP, ZF_NT, 0, 1, 0, true>;
         ki.u = 1;
         ki.bpc_cap = 4;
+    } else if (s == 2) {  // S2: S0's kernel at 1 workgroup/CU
+        ki.bpc_cap = 1;
     }
     return ki;
 }
@@ -169,6 +173,7 @@ KernelInfo k8_info(int s) {
 
 // shapes with two schedules to pick from at run time
 bool tunable_shape(uint32_t k, int ng) { return (k == 4 && ng == 1) || (k == 8 && ng == 2); }
+int tuned_candidates(uint32_t k) { return k == 4 ? 3 : 2; }
 KernelInfo tuned_info(uint32_t k, int s) { return k == 4 ? k4_info(s) : k8_info(s); }
 
 struct DevTable {
@@ -194,7 +199,7 @@ std::map<std::tuple<int, int, int>, int> g_k4;         // (device, k, output row
 
 int k4_forced() {
     static const int f = [] {
-        if (const char *e = std::getenv("CHIP_ZFEC_K4_SCHED")) return std::atoi(e) == 1 ? 1 : 0;
+        if (const char *e = std::getenv("CHIP_ZFEC_K4_SCHED")) return std::max(0, std::min(2, std::atoi(e)));
         return std::getenv("CHIP_ZFEC_K4_U1") ? 1 : -1;
     }();
     return f;
@@ -386,6 +391,8 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
 
 hipError_t k4_tune(const GfPlan &p, const GfLaunch &L, hipStream_t stream, uint32_t row0, uint32_t nrows,
                    bool copies, int rows) {
+    // 2 slices of count/8 objects per candidate, interleaved (S0 S1 [S2] S0 S1 [S2])
+    const int nc = tuned_candidates(p.k), ns = 2 * nc;
     const uint64_t piece = L.count / 8;
     auto slice = [&](uint64_t o0, uint64_t cnt) {
         GfLaunch S = L;
@@ -394,26 +401,32 @@ hipError_t k4_tune(const GfPlan &p, const GfLaunch &L, hipStream_t stream, uint3
         S.count = cnt;
         return S;
     };
-    hipEvent_t ev[5] = {};
+    hipEvent_t ev[7] = {};
     hipError_t e = hipSuccess;
-    for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
+    for (int i = 0; i <= ns && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
     if (e == hipSuccess) e = hipEventRecord(ev[0], stream);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) {
-        e = gf_apply_pass(p, slice(i * piece, piece), stream, row0, nrows, copies, i & 1);
+    for (int i = 0; i < ns && e == hipSuccess; ++i) {
+        e = gf_apply_pass(p, slice(i * piece, piece), stream, row0, nrows, copies, i % nc);
         if (e == hipSuccess) e = hipEventRecord(ev[i + 1], stream);
     }
-    float t[4] = {0.f, 0.f, 0.f, 0.f};
-    if (e == hipSuccess) e = hipEventSynchronize(ev[4]);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventElapsedTime(&t[i], ev[i], ev[i + 1]);
+    float t[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (e == hipSuccess) e = hipEventSynchronize(ev[ns]);
+    for (int i = 0; i < ns && e == hipSuccess; ++i) e = hipEventElapsedTime(&t[i], ev[i], ev[i + 1]);
     for (hipEvent_t x : ev)
         if (x) (void)hipEventDestroy(x);
     if (e != hipSuccess) return e;
-    const int s = std::min(t[1], t[3]) < std::min(t[0], t[2]) ? 1 : 0;
+    int s = 0;
+    float best = std::min(t[0], t[nc]);
+    for (int c = 1; c < nc; ++c)
+        if (std::min(t[c], t[c + nc]) < best) {
+            best = std::min(t[c], t[c + nc]);
+            s = c;
+        }
     {
         std::lock_guard<std::mutex> lk(g_mu);
         g_k4[std::make_tuple(selected_device(), (int)p.k, rows)] = s;
     }
-    return gf_apply_pass(p, slice(4 * piece, L.count - 4 * piece), stream, row0, nrows, copies, s);
+    return gf_apply_pass(p, slice(ns * piece, L.count - ns * piece), stream, row0, nrows, copies, s);
 }
 
 }  // namespace

@@ -129,7 +129,7 @@ CHIP_API int chip_init(int device);
 CHIP_API const char *chip_last_device_error(void);
 /* Diagnostics: the zfec 4-of-8 schedule this process chose on its device for
  * launches that write `rows` output shards per column (8 = encode with the
- * data shards, 4 = parity only or a 2-erasure decode): 0 or 1, -1 = not
+ * data shards, 4 = parity only or a 2-erasure decode): 0, 1 or 2, -1 = not
  * chosen yet.  The first launch of >= 1 GiB picks it. */
 CHIP_API int chip_zfec_k4_schedule(uint32_t rows);
 /* The same for any shape with two schedules (k = 4: as above; k = 8, the
