@@ -186,14 +186,14 @@ std::map<std::vector<uint8_t>, DevTable> g_tables;  // key: device, k, ng, coef 
 std::map<std::pair<KernelFn, size_t>, int> g_grid;
 std::map<int, uint8_t *> g_multab;                  // per device
 
-// ---- run-time choice of the 4-of-8 schedule ------------------------------
-// S0 and S1 are within a few per cent of each other and which one wins
-// depends on the box (S1 4 % ahead on one box, 0.7 % behind on
-// another).  The first large launch of each (device, output rows) class runs
-// 4 slices of count/8 objects alternately with S0 and S1 between events on
-// its stream, waits for them, keeps the faster one and runs the rest of the
-// batch with it; later launches use the choice.  CHIP_ZFEC_K4_SCHED=0|1 fixes
-// the schedule (A/B runs; CHIP_ZFEC_K4_U1 = 1, the older switch).
+// ---- run-time choice of the schedule (4-of-8: S0/S1/S2, 8-of-16: S0/S1) ---
+// The candidates are within a few per cent of each other and which one wins
+// depends on where the process's buffers sit in HBM.  The
+// first large launch of each (device, k, output rows) class runs two slices
+// of count/8 objects per candidate, interleaved, between events on its
+// stream, waits for them, keeps the fastest and runs the rest of the batch
+// with it; later launches use the choice.  CHIP_ZFEC_K4_SCHED=0|1|2 fixes the
+// schedule (A/B runs, profiles; CHIP_ZFEC_K4_U1 = 1, the older switch).
 constexpr uint64_t K4_TUNE_MIN = uint64_t(1) << 30;  // input bytes of a launch worth tuning on
 std::map<std::tuple<int, int, int>, int> g_k4;         // (device, k, output rows) -> schedule
 
