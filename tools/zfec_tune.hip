@@ -129,8 +129,9 @@ int main(int argc, char **argv) {
 
     std::vector<Variant> vs;
     if (K == 4)
-        vs = {V<2, 3, true, 32, 2, 0, true>(2), V<1, 3, true, 64, 1, 0, true>(4), V<2, 3, true, 32, 2, 0, true>(1),
-              V<1, 3, true, 64, 1, 0, true>(2), V<1, 3, true, 64, 1, 0, true>(3)};
+        vs = {V<2, 3, true, 32, 2, 0, true>(2),  V<1, 3, true, 64, 1, 0, true>(4),  V<2, 3, true, 32, 2, 0, true>(1),
+              V<2, 3, false, 32, 2, 0, true>(2), V<1, 3, false, 64, 1, 0, true>(4), V<2, 3, false, 32, 2, 0, true>(1),
+              V<2, 3, true, 16, 2, 0, true>(1),  V<2, 3, true, 64, 2, 0, true>(1)};
     else
         vs = {V16<1, 3, true, 4, 64>(1),                V16<1, 3, true, 4, 64, 2, 1, true>(2),
               V16<1, 3, true, 4, 64, 2, 1, true>(1),    V16<1, 3, true, 4, 64, 1, 0, true>(1),
