@@ -75,8 +75,10 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&scratch, bao_scratch_len_t<1>(n, count)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xB1A3ull);
     // product encode / decode / in-place, each with the XCD-grouped block order (XG 1)
-    std::vector<V> vs = {mk<0, 2, false, 3>(true), mk<0, 2, false, 3, 1, 0, 1>(true), mk<1, 2, false>(true),
-                         mk<1, 2, false, 0, 1, 0, 1>(true), mk<3, 8, false>(true), mk<3, 8, false, 0, 1, 0, 1>(true)};
+    std::vector<V> vs = {mk<0, 2, false, 3, 1, 0, 1>(true), mk<0, 2, false, 3, 2, 0, 1>(true),
+                         mk<0, 2, false, 3, 4, 0, 1>(true), mk<0, 2, false, 3, 8, 0, 1>(true),
+                         mk<0, 2, false, 3, 1, 1, 1>(true)};
+    // earlier: product encode / decode / in-place with XG 0 and 1 (profiles/r1x_ab_bao_xcd_order.txt)
     // round-1 store diagnostics (profiles/r1x_bao_store_diagnostics.txt): mk<0, 2, false>(false) hash-only,
     // mk<0, 2, false, 3, 1, SE>(true) for SE 2..5, mk<0, 1, false, 3>(true), mk<1, 1, false>(true)
     if (argc > 4) {  // comma-separated subset of variant indices (profiling)
