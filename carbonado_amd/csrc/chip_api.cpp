@@ -1811,14 +1811,16 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
             }
             uint64_t got = 0;
             int st = CHIP_OK;
-            if (format & CHIP_FORMAT_ECIES) {
+            if ((format & CHIP_FORMAT_ECIES) && (format & CHIP_FORMAT_SNAPPY)) {
+                st = host::ecies_decrypt_snap(secret_key, sk_len, src, n, dst, out_stride, &got);
+            } else if (format & CHIP_FORMAT_ECIES) {
                 uint8_t *t = tmp.get(n + 1);
                 st = host::ecies_decrypt(secret_key, sk_len, src, n, (format & CHIP_FORMAT_SNAPPY) ? t : dst,
                                          (format & CHIP_FORMAT_SNAPPY) ? n + 1 : out_stride, &got);
                 src = t;
                 n = got;
             }
-            if (st == CHIP_OK && (format & CHIP_FORMAT_SNAPPY)) st = host::snap_decompress(src, n, dst, out_stride, &got);
+            else if (format & CHIP_FORMAT_SNAPPY) st = host::snap_decompress(src, n, dst, out_stride, &got);
             status[o] = st;
             out_len[o] = got;
         }
@@ -1870,6 +1872,11 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
                 uint64_t n = geo[o].olen, got = 0;
                 uint8_t *dst = out + o * out_stride;
                 int r = CHIP_OK;
+                if ((format & CHIP_FORMAT_ECIES) && (format & CHIP_FORMAT_SNAPPY)) {  // one pass, no plaintext buffer
+                    status[o] = host::ecies_decrypt_snap(secret_key, sk_len, src, n, dst, out_stride, &got);
+                    out_len[o] = got;
+                    continue;
+                }
                 if (format & CHIP_FORMAT_ECIES) {
                     const bool snap = format & CHIP_FORMAT_SNAPPY;
                     uint8_t *tb = snap ? tmp.get(n + 1) : nullptr;
@@ -2065,6 +2072,8 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         *out_len = cur_n;
         return CHIP_OK;
     }
+    if (ecies && snap)  // decoding.rs:101-111 in one pass
+        return host::ecies_decrypt_snap(secret_key, sk_len, cur, cur_n, out, out_cap, out_len);
     if (ecies) {  // decoding.rs:101-105
         uint8_t *dst = out;
         uint64_t cap = out_cap;

@@ -578,5 +578,140 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
     return CHIP_OK;
 }
 
+// Ecies|Snappy decode in one pass.  The two-pass form writes the whole
+// plaintext to a scratch buffer and reads it back for the snappy walk: two
+// extra DRAM passes per object, and level-15 decode end to end is bound by
+// the host threads' memory traffic beside the DMA.  Here the
+// plaintext is decrypted into a per-thread window of 256 KiB (L2-resident)
+// and each snappy chunk is decoded from there into `out`.  Status order equals
+// ecies_decrypt + snap_decompress: a bad tag is EciesError whatever the
+// plaintext holds; then framing errors (snap_walk's size pass); then a short
+// `out` (required size in *out_len); then CRC / block errors.  A data chunk
+// longer than the window (never produced by a FrameEncoder) takes the
+// two-pass route.
+int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
+                       uint64_t cap, uint64_t *out_len) {
+    BnPtr k(parse_secret(secret, secret_len));
+    if (!k.p) return CHIP_ERR_ECIES;
+    if (n < ECIES_OVERHEAD) return CHIP_ERR_ECIES;
+    const uint64_t m = n - ECIES_OVERHEAD;
+    PtPtr eph(parse_public(in, 65));
+    if (!eph.p) return CHIP_ERR_ECIES;
+    uint8_t key[32];
+    if (!derive_key(k.p, eph.p, in, key)) return CHIP_ERR_ECIES;
+    const uint8_t *iv = in + 65, *ct = in + 97;
+    uint8_t tagbuf[16];
+    std::memcpy(tagbuf, in + 81, 16);
+    CipherCtx cc;
+    bool dec_ok = cc.c && EVP_DecryptInit_ex(cc.c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+                  EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
+                  EVP_DecryptInit_ex(cc.c, nullptr, nullptr, key, iv) == 1;
+    OPENSSL_cleanse(key, 32);
+    if (!dec_ok) return CHIP_ERR_ECIES;
+
+    constexpr uint64_t W = 256u << 10;
+    static thread_local std::unique_ptr<uint8_t[]> t_win;
+    if (!t_win) t_win.reset(new uint8_t[W]);
+    uint8_t *win = t_win.get();
+    uint64_t wbeg = 0, wend = 0;  // plaintext [wbeg, wend) sits at win[0 .. wend - wbeg)
+    // plaintext [s, s + len) resident in the window; s only moves forward,
+    // len <= W and s + len <= m
+    auto need = [&](uint64_t s, uint64_t len) -> const uint8_t * {
+        if (s + len <= wend) return win + (s - wbeg);
+        uint64_t keep = 0;
+        if (s < wend) {
+            keep = wend - s;
+            std::memmove(win, win + (s - wbeg), keep);
+        }
+        while (wend < s) {  // a skipped chunk: decrypted (for the tag) and dropped
+            const uint64_t step = std::min<uint64_t>(W, s - wend);
+            dec_ok &= gcm_update(cc.c, false, ct + wend, step, win);
+            wend += step;
+        }
+        wbeg = s;
+        wend = s + keep;
+        const uint64_t step = std::min<uint64_t>(W - keep, m - wend);
+        dec_ok &= gcm_update(cc.c, false, ct + wend, step, win + keep);
+        wend += step;
+        return win;
+    };
+
+    uint64_t s = 0, d = 0;
+    bool ident = false, fits = true, two_pass = false;
+    int frame = CHIP_OK, content = CHIP_OK;
+    while (s < m) {  // snap_walk's chunk loop, both passes at once
+        if (m - s < 4) { frame = CHIP_ERR_SNAP; break; }
+        const uint8_t *h = need(s, 4);
+        const uint8_t ty = h[0];
+        const uint64_t clen = (uint64_t)h[1] | ((uint64_t)h[2] << 8) | ((uint64_t)h[3] << 16);
+        s += 4;
+        if (clen > m - s) { frame = CHIP_ERR_SNAP; break; }
+        if (!ident && ty != 0xFF) { frame = CHIP_ERR_SNAP; break; }
+        if (ty >= 0x02 && ty <= 0x7F) { frame = CHIP_ERR_SNAP; break; }
+        if (ty >= 0x80 && ty != 0xFF) { s += clen; continue; }  // skippable
+        if (clen > W) { two_pass = true; break; }
+        const uint8_t *body = need(s, clen);
+        if (ty == 0xFF) {
+            if (clen != 6 || std::memcmp(body, STREAM_ID + 4, 6) != 0) { frame = CHIP_ERR_SNAP; break; }
+            ident = true;
+        } else {
+            if (clen < 4) { frame = CHIP_ERR_SNAP; break; }
+            uint32_t want;
+            std::memcpy(&want, body, 4);
+            const uint8_t *data = body + 4;
+            const uint64_t dl = clen - 4;
+            uint64_t ulen = dl;
+            if (ty == 0x01) {
+                if (dl > MAX_BLOCK) { frame = CHIP_ERR_SNAP; break; }
+            } else {
+                size_t used;
+                if (!get_varint(data, dl, &ulen, &used) || ulen > MAX_BLOCK) { frame = CHIP_ERR_SNAP; break; }
+            }
+            if (fits && ulen > cap - d) fits = false;
+            if (fits && content == CHIP_OK) {
+                if (ty == 0x01) {
+                    if (crc_masked(data, dl) != want) content = CHIP_ERR_SNAP;
+                    else std::memcpy(out + d, data, dl);
+                } else {
+                    size_t got;
+                    if (!decompress_raw(data, dl, out + d, ulen, &got) || got != ulen ||
+                        crc_masked(out + d, ulen) != want)
+                        content = CHIP_ERR_SNAP;
+                }
+            }
+            d += ulen;
+        }
+        s += clen;
+    }
+    if (two_pass) {
+        std::vector<uint8_t> tmp(m + 1);
+        uint64_t got = 0;
+        int st = ecies_decrypt(secret, secret_len, in, n, tmp.data(), tmp.size(), &got);
+        return st != CHIP_OK ? st : snap_decompress(tmp.data(), got, out, cap, out_len);
+    }
+    while (wend < m) {  // the rest of the ciphertext, for the tag
+        const uint64_t step = std::min<uint64_t>(W, m - wend);
+        dec_ok &= gcm_update(cc.c, false, ct + wend, step, win);
+        wend += step;
+    }
+    int fin = 0;
+    uint8_t dummy[16];
+    dec_ok = dec_ok && EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_TAG, 16, tagbuf) == 1 &&
+             EVP_DecryptFinal_ex(cc.c, dummy, &fin) == 1;
+    OPENSSL_cleanse(win, W);
+    if (!dec_ok) {
+        if (d && out) OPENSSL_cleanse(out, std::min(d, cap));  // never hand back unauthenticated plaintext
+        return CHIP_ERR_ECIES;
+    }
+    if (frame != CHIP_OK) return frame;
+    if (!fits || (d && !out)) {
+        *out_len = d;
+        return CHIP_ERR_BUFFER_TOO_SMALL;
+    }
+    if (content != CHIP_OK) return content;
+    *out_len = d;
+    return CHIP_OK;
+}
+
 }  // namespace host
 }  // namespace chip

@@ -32,6 +32,10 @@ int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph
                   const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
 int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
                   uint64_t cap, uint64_t *out_len);
+// ecies_decrypt then snap_decompress (decoding.rs:101-111) in one pass over
+// the ciphertext: same output and status codes, no full-size plaintext buffer.
+int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
+                       uint64_t cap, uint64_t *out_len);
 // Public key (65 B uncompressed) of a 32-byte secret; for tests and tooling.
 int ecies_public_key(const uint8_t *secret, uint8_t out[65]);
 

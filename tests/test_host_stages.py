@@ -189,6 +189,46 @@ def test_ecies_errors(ca):
         ca.encoding.ecies(b"\x02" + bytes(31), b"x")  # wrong length
 
 
+def test_ecies_snap_one_pass_decode(ca):
+    """decode() with Ecies|Snappy (decoding.rs:101-111) decrypts and unsnaps in
+    one pass through a 256 KiB window (host_stages.cpp ecies_decrypt_snap):
+    same bytes and error classes as decoding.ecies followed by decoding.snap."""
+    from carbonado_amd.error import EciesError, SnapError
+    sk = H.sha256(b"one pass receiver")
+    pk = ca.encoding.public_key(sk)
+    rng = np.random.default_rng(11)
+    big = rng.integers(0, 256, 1_000_003, dtype=np.uint8).tobytes()  # raw chunks, 4x the window
+    comp = b"carbonado " * 120_000  # compressed chunks; output > decode()'s first guess
+    for d in [b"", b"x", big, comp]:
+        f = ca.encoding.snap(d)
+        e = ca.encoding.ecies(pk, f)
+        assert ca.decode(sk, b"", e, 0, 3) == d == ca.decoding.snap(ca.decoding.ecies(e, sk))
+        if not f:  # an empty input has an empty stream (no identifier to pad after)
+            continue
+        # skippable padding chunk larger than the window
+        pad = bytes(f[:10]) + b"\xfe" + (300_000).to_bytes(3, "little") + bytes(300_000) + bytes(f[10:])
+        assert ca.decode(sk, b"", ca.encoding.ecies(pk, pad), 0, 3) == d
+    f = ca.encoding.snap(big)
+    bad = bytearray(f)
+    bad[-1] ^= 1  # CRC mismatch in the last chunk, valid tag
+    with pytest.raises(SnapError):
+        ca.decode(sk, b"", ca.encoding.ecies(pk, bytes(bad)), 0, 3)
+    with pytest.raises(SnapError):  # truncated frame
+        ca.decode(sk, b"", ca.encoding.ecies(pk, bytes(f[:-3])), 0, 3)
+    # data chunk longer than the window: the two-pass route, same verdict
+    huge = bytes(f[:10]) + b"\x00" + (300_000).to_bytes(3, "little") + bytes(300_000)
+    with pytest.raises(SnapError):
+        ca.decode(sk, b"", ca.encoding.ecies(pk, huge), 0, 3)
+    e = bytearray(ca.encoding.ecies(pk, bytes(bad)))
+    e[200] ^= 0x40  # bad tag wins over the snap error
+    with pytest.raises(EciesError):
+        ca.decode(sk, b"", bytes(e), 0, 3)
+    e = bytearray(ca.encoding.ecies(pk, f))
+    e[-1] ^= 0x40
+    with pytest.raises(EciesError):
+        ca.decode(sk, b"", bytes(e), 0, 3)
+
+
 # ---------------------------------------------------------------- C restatement
 def test_c_host_oracle_matches_python_oracle(kat):
     """oracle/host_oracle.c (the full-size checker and CPU baseline) agrees
