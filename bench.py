@@ -8,10 +8,15 @@ are independent, so N ranks each encode their own contiguous range of the
 global object set (weak scaling, no data-path collective).  torch.distributed
 (gloo) carries only the control plane: barrier and max-over-ranks time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--objects 1024]
-                    [--object-mib 16] [--k 4 --m 8] [--mode encode|decode|bao]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
+                    [--objects 1024] [--object-mib 16] [--k 4 --m 8]
+                    [--mode encode|decode|bao|...] [--alloc chip|contiguous|torch]
                     [--scatter] [--dry-run]
 
+--gpus N with N > 1 and no WORLD_SIZE in the environment: this process
+starts the N rank processes itself (RANK/LOCAL_RANK/WORLD_SIZE,
+MASTER_ADDR=127.0.0.1) before anything touches the GPU, waits for them and
+exits with their status; under torch.distributed.run WORLD_SIZE must equal N.
 Rank 0 prints one JSON line (metric/value/unit/... + roofline + cpu_baseline).
 """
 from __future__ import annotations
@@ -38,9 +43,22 @@ METRIC = "GiB/s device-resident zfec 4-of-8 encode, 16 MiB objects; % HBM roofli
 SEED = 0xCA4B0AD0
 
 
-def parse():
+# BASELINE.json configs as presets (configs[1..4]; configs[0] is the CPU
+# round trip of tests/test_oracle.py and tests/test_gpu_pipeline.py)
+CONFIGS = {
+    "cfg2": dict(mode="encode", k=4, m=8, objects=1024),                     # zfec 4-of-8 encode, 1024 x 16 MiB
+    "cfg3": dict(mode="decode", k=4, m=8, objects=1024, erase="1,2"),        # decode, 2 shards dropped
+    "cfg4": dict(mode="e2e", k=4, m=8, objects=1024, level=15),              # full encode(), host -> host
+    "cfg5": dict(mode="encode", k=8, m=16, objects=1024),                    # 8-of-16, 1024 per GPU (8192 on 8)
+}
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment bench.py starts them itself")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="BASELINE.json config preset (sets mode, k, m, objects, erase, level)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--objects", type=int, default=1024, help="objects per GPU")
@@ -61,9 +79,10 @@ def parse():
     ap.add_argument("--in-pad-kib", type=int, default=0, help="encode/decode: extra bytes per input object row")
     ap.add_argument("--out-pad-kib", type=int, default=0, help="encode/decode: extra bytes per output object row")
     ap.add_argument("--prealloc-gib", type=float, default=0, help="allocate (and keep) this much HBM first")
-    ap.add_argument("--alloc", choices=["contiguous", "torch"], default="contiguous",
-                    help="encode/decode batch buffers: physically contiguous HBM through the library's allocator "
-                         "(carbonado_amd.device.empty_batch) or torch's caching allocator")
+    ap.add_argument("--alloc", choices=["chip", "contiguous", "torch"], default="chip",
+                    help="device batch buffers: the library's class-balanced allocator (chip_device_alloc via "
+                         "carbonado_amd.device.empty_batch; DESIGN.md §2), physically contiguous HBM "
+                         "(CHIP_ALLOC=contiguous), or torch's caching allocator")
     ap.add_argument("--host-threads", type=int, default=16,
                     help="e2e mode: host threads for the Snappy/Ecies stages (the GPU box's CPU share is 16)")
     ap.add_argument("--erase", default="1,2", help="decode mode: shards dropped")
@@ -74,30 +93,73 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--verify-all", action="store_true",
-                    help="encode / pipeline mode: check EVERY object bit-exact (SURVEY 8d): BLAKE3 of each "
-                         "object's output on the GPU vs the C oracle's zfec (or encode()) + BLAKE3 on 16 host threads")
+                    help="pipeline mode: check EVERY object bit-exact (encode mode does by default): BLAKE3 of "
+                         "each object's output on the GPU vs the C oracle's zfec (or encode()) + BLAKE3 on 16 host "
+                         "threads, outside the timed region")
+    ap.add_argument("--no-verify-all", action="store_true", help="encode mode: check object 0 only")
     ap.add_argument("--no-aliased", action="store_true",
                     help="encode mode: skip the second, in-place (aliased data shards) measurement")
     ap.add_argument("--scatter", action="store_true",
                     help="N>1: rank 0 generates every object and scatters them over RCCL/xGMI (timed "
                          "separately, outside `value`)")
+    ap.add_argument("--scatter-gib", type=float, default=1.0,
+                    help="N>1 without --scatter: GiB per rank that rank 0 scatters over RCCL/xGMI once, timed and "
+                         "reported as `scatter` (the inputs themselves are generated on each rank); 0 = none")
     ap.add_argument("--dry-run", action="store_true", help="no device: exercise the multi-rank control plane")
     ap.add_argument("--traffic-json", default="auto",
                     help="PMC summary (profiles/*_pmc.json, tools/pmc_summary.py) with the measured HBM "
                          "bytes per launch of this kernel; 'auto' = newest matching file, 'none' = null")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.config:
+        explicit = {a.dest for a in ap._actions if any(o in (argv if argv is not None else sys.argv[1:])
+                                                       for o in a.option_strings)}
+        for key, val in CONFIGS[args.config].items():
+            if key not in explicit:
+                setattr(args, key, val)
     if args.mode in ("scrub", "hasher") and args.objects == ap.get_default("objects"):
         args.objects = 64  # host-API paths: a bounded host-memory working set
+    if args.mode != "encode":
+        args.no_verify_all = True
     return args
 
 
-def setup_dist():
+def spawn_ranks(n: int) -> int:
+    """Start the n rank processes of `bench.py --gpus n` (this process never
+    touches the GPU), wait for them, return the worst exit status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    base = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:],
+                              env=dict(base, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {args.gpus}) or leave WORLD_SIZE unset")
     if world > 1:
         dist.init_process_group("gloo")  # control plane only: no bytes of the path cross it
     return world, rank, local
+
+
+def gather_floats(value: float, world: int) -> list:
+    """Every rank's value (gloo control plane), in rank order."""
+    if world == 1:
+        return [float(value)]
+    out = [None] * world
+    dist.all_gather_object(out, float(value))
+    return [float(v) for v in out]
 
 
 def barrier(world):
@@ -270,12 +332,25 @@ class Workload:
         self.C = C = c32.value
         self.prealloc = (torch.empty(int(args.prealloc_gib * 2**30), dtype=torch.uint8, device=dev)
                          if args.prealloc_gib else None)
-        def batch_buf(shape):
-            if args.alloc == "contiguous" and args.mode in ("encode", "decode"):
-                return device.empty_batch(shape, dev)
+        if args.alloc == "contiguous":
+            os.environ["CHIP_ALLOC"] = "contiguous"  # read by chip_device_alloc at each call
+        device_mode = args.mode in ("encode", "decode", "bao", "bao-decode", "pipeline")
+        self.alloc_info = {}
+
+        def batch_buf(shape, name=None):
+            """Device batch buffer: the library's allocator (class-balanced from 1 GiB up) or torch's."""
+            if args.alloc != "torch" and device_mode:
+                t = device.empty_batch(shape, dev)
+                if name:
+                    f, u, sec = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_double()
+                    if L.chip_device_alloc_info(ctypes.c_void_p(t.data_ptr()), ctypes.byref(f), ctypes.byref(u),
+                                                ctypes.byref(sec)) == 0:
+                        self.alloc_info[name] = {"classes_found": f.value, "classes_used": u.value,
+                                                 "alloc_s": round(sec.value, 3)}
+                return t
             return torch.empty(shape, dtype=torch.uint8, device=dev)
         self.batch_buf = batch_buf
-        self.inp_full = batch_buf((count, n + args.in_pad_kib * 1024))
+        self.inp_full = batch_buf((count, n + args.in_pad_kib * 1024), "in")
         self.inp = self.inp_full[:, :n] if args.in_pad_kib else self.inp_full
         self.scatter_s = None
         rng = object_range(rank, world, world * count)
@@ -284,18 +359,18 @@ class Workload:
         else:
             fill_random(self.inp_full, SEED + rng.start)
         if args.mode == "encode":
-            self.out = batch_buf((count, m * C + args.out_pad_kib * 1024))
+            self.out = batch_buf((count, m * C + args.out_pad_kib * 1024), "out")
             self.step = lambda: device.zfec_encode_batch(self.inp_full, n, self.out, k, m)
             self.alg_bytes = count * (n + m * C)  # read the input + write all m shards
             ng = (m - k + 3) // 4
             self.kernel = f"gf_apply_kernel<{k},{ng}>"
             self.kernel_sym = f"gf_apply_kernel<{k}, {ng},"
         elif args.mode == "decode":
-            self.enc = batch_buf((count, m * C))
+            self.enc = batch_buf((count, m * C), "enc")
             device.zfec_encode_batch(self.inp, n, self.enc, k, m)
             erased = {int(x) for x in args.erase.split(",") if x}
             self.keep = [i for i in range(m) if i not in erased]
-            self.out = batch_buf((count, k * C))
+            self.out = batch_buf((count, k * C), "out")
             self.step = lambda: device.zfec_decode_batch(self.enc, C, self.keep, self.out, k, m)
             self.alg_bytes = count * (2 * k * C)  # read k shares + write k data shards
             self.kernel = f"gf_apply_kernel<{k},1> (decode, erased {sorted(erased)})"
@@ -306,7 +381,7 @@ class Workload:
                 raise SystemExit("--mode pipeline runs the device-only levels (Bao/Zfec bits); use --mode e2e")
             zlen = m * C if lv & 8 else n
             self.blen = blen = L.chip_bao_encoded_len(zlen) if lv & 4 else zlen
-            self.out = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device=dev)
+            self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.encode_scratch(lv, n, count, dev)
             self.step = lambda: device.encode_batch(lv, self.inp, n, self.out, self.hashes, self.scratch)
@@ -434,11 +509,11 @@ class Workload:
             self.kernel_sym = "e2e"
         elif args.mode == "bao-decode":
             blen = L.chip_bao_encoded_len(n)
-            self.enc = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device=dev)
+            self.enc = batch_buf((count, (blen + 15) // 16 * 16), "enc")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.bao_scratch(n, count, dev)
             device.bao_encode_batch(self.inp, n, self.enc, self.hashes, self.scratch)
-            self.out = torch.empty((count, n), dtype=torch.uint8, device=dev)
+            self.out = batch_buf((count, n), "out")
             self.status = torch.full((count,), -1, dtype=torch.int32, device=dev)
             self.step = lambda: device.bao_decode_batch(self.enc, n, self.hashes, self.out, self.status, self.scratch)
             self.alg_bytes = count * (blen + n)  # read the stream, write the content
@@ -446,19 +521,13 @@ class Workload:
             self.kernel_sym = "bao_chunk_kernel"
         else:
             blen = L.chip_bao_encoded_len(n)
-            self.out = torch.empty((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device=dev)
+            self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.bao_scratch(n, count, dev)
             self.step = lambda: device.bao_encode_batch(self.inp, n, self.out, self.hashes, self.scratch)
             self.alg_bytes = count * (n + blen)
             self.kernel = "bao_chunk_kernel + bao_parent_kernel levels"
             self.kernel_sym = "bao_chunk_kernel"
-        if args.mode in ("encode", "decode"):
-            # the library tunes itself on its first large batches (the 4-of-8
-            # schedule, then one launch vs two halves): run
-            # those here, before the W warmup steps, whatever W the caller picks
-            for _ in range(2):
-                self.step()
         torch.cuda.synchronize()
 
     def _scatter_inputs(self, rank: int, world: int) -> float:
@@ -478,6 +547,37 @@ class Workload:
         del full, chunks
         torch.cuda.empty_cache()
         return el
+
+    def scatter_sample(self, rank: int, world: int, gib: float) -> dict:
+        """N > 1: rank 0 scatters `gib` GiB to every rank over RCCL (xGMI),
+        once, timed between barriers; the inputs of the timed steps are
+        generated on each rank, so this only shows RCCL seeing N ranks and
+        the per-link rate of the input-staging collective."""
+        grp = dist.new_group(backend="nccl")
+        per = int(gib * 2**30)
+        local = torch.empty(per, dtype=torch.uint8, device=self.dev)
+        chunks = None
+        if rank == 0:
+            full = torch.empty(world * per, dtype=torch.uint8, device=self.dev)
+            full.random_(0, 256)
+            chunks = list(full.chunk(world))
+        dist.scatter(local, chunks, src=0, group=grp)  # warm the communicator
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dist.scatter(local, chunks, src=0, group=grp)
+        torch.cuda.synchronize()
+        el = max_over_ranks(time.perf_counter() - t0)
+        ok = True
+        if rank == 0:
+            ok = bool(torch.equal(local, chunks[0]))
+        del local, chunks
+        torch.cuda.empty_cache()
+        return {"ranks": world, "bytes_per_rank": per, "seconds": round(el, 4),
+                "GiB_per_s_total": round((world - 1) * per / el / 2**30, 2),
+                "GiB_per_s_per_receiver": round(per / el / 2**30, 2), "root_slice_ok": ok,
+                "how": "RCCL scatter (backend nccl) from rank 0 over xGMI, outside the timed region; the timed "
+                       "steps' inputs are generated on each rank"}
 
     def time_steps(self, steps: int, warmup: int, world: int, step=None):
         step = step or self.step
@@ -543,8 +643,6 @@ class Workload:
         n, k, m = self.n, self.k, self.m
         self.out[:, :n].copy_(self.inp)
         step = lambda: device.zfec_encode_batch(self.out, n, self.out, k, m)  # noqa: E731
-        for _ in range(2):  # the library's self-tuning for this shape (4 output shards per column)
-            step()
         el, ms = self.time_steps(steps, warmup, world, step)
         from oracle import oracle as O
         ok = self.out[0].cpu().numpy().tobytes() == O.zfec_encode(self.inp[0].cpu().numpy().tobytes(), k, m)[0]
@@ -610,17 +708,27 @@ class DryRun:
 
 def main():
     args = parse()
-    world, rank, local = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    world, rank, local = setup_dist(args)
     n = int(args.object_mib * (1 << 20))
     wl = DryRun(args, rank) if args.dry_run else Workload(args, rank, local, world)
+    scatter = None
+    if world > 1 and not args.dry_run and not args.scatter and args.scatter_gib > 0:
+        if torch.cuda.device_count() >= world:
+            scatter = wl.scatter_sample(rank, world, args.scatter_gib)
+        else:  # a rehearsal with several ranks on one GPU: RCCL refuses two ranks on one device
+            scatter = {"skipped": f"{world} ranks share {torch.cuda.device_count()} GPU(s); RCCL needs one GPU per rank"}
     elapsed, launch_ms = wl.time_steps(args.steps, args.warmup, world)
     max_elapsed = max_over_ranks(elapsed)
+    rank_avg_ms = gather_floats(sum(launch_ms) / len(launch_ms), world)
 
     verified, sample = None, None
     if rank == 0 and not args.no_verify and not args.dry_run:
         verified, sample = wl.verify_object0()
     verified_all = None
-    if rank == 0 and args.verify_all and args.mode in ("encode", "pipeline") and not args.dry_run:
+    want_all = (args.mode == "encode" and not args.no_verify_all) or (args.mode == "pipeline" and args.verify_all)
+    if rank == 0 and want_all and not args.no_verify and not args.dry_run:
         verified_all = wl.verify_all()
     aliased = None
     if args.mode == "encode" and not args.dry_run and not args.no_aliased:
@@ -702,17 +810,19 @@ def main():
                                        "BLAKE3 compression (content blocks + parents)"
                                        + ("; step = zfec kernel (HBM-bound) + bao kernels (VALU-bound), "
                                           "achieved over the whole step" if args.mode == "pipeline" else "")}
-        if args.mode in ("encode", "decode") and not args.dry_run:
-            from carbonado_amd import _lib
-            rows = m if args.mode == "encode" else k  # decode writes the k data shards
-            res["roofline"]["schedule"] = {"k4": _lib.lib().chip_zfec_schedule(k, rows),
-                                           "rows": rows,
-                                           "split": _lib.lib().chip_zfec_split_mode(k, rows),
-                                           "note": "zfec 4-of-8 schedule picked on this box by the first launch "
-                                                   "(4-of-8: 0 = 2-tile super-tiles at 2 WG/CU, 1 = 1 tile at 4 WG/CU, 2 = super-tiles "
-                                                   "at 1 WG/CU; 8-of-16: 0 = 2 WG/CU, 1 = 1); "
-                                                   "split: the batch as two concurrent halves (1) or one launch "
-                                                   "(0), picked by timing quarters of the first large batch"}
+        if world > 1:
+            fr = [wl.alg_bytes / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS if res["roofline"]["unit"] == "GB/s" else 1)
+                  for ms in rank_avg_ms]
+            res["roofline"]["per_rank_avg_launch_ms"] = [round(x, 4) for x in rank_avg_ms]
+            if res["roofline"]["bound"] == "hbm":
+                res["roofline"]["per_rank_frac_min"] = round(min(fr), 4)
+                res["roofline"]["per_rank_frac_max"] = round(max(fr), 4)
+            res["roofline"]["note_ranks"] = "achieved/frac above: rank 0's launches; per-rank averages listed"
+        if not args.dry_run and args.mode not in ("e2e", "e2e-decode", "scrub", "hasher"):
+            res["alloc"] = {"kind": {"chip": "chip_device_alloc (class-balanced from 1 GiB, DESIGN.md §2)",
+                                     "contiguous": "hipDeviceMallocContiguous (CHIP_ALLOC=contiguous)",
+                                     "torch": "torch caching allocator (hipMalloc)"}[args.alloc],
+                            "buffers": wl.alloc_info}
         if verified_all is not None:
             res["verified_all_objects"] = verified_all
         if aliased is not None:
@@ -728,6 +838,8 @@ def main():
                 "note": ("SURVEY.md 8d: in-place encode, the input already sits in the output slot and only the "
                          "parity shards are written (16 MiB read + 16 MiB written per object); `value` above "
                          "(all 8 shards written, 48 MiB per object) is the graded figure")}
+        if scatter is not None:
+            res["scatter"] = scatter
         if wl.scatter_s is not None:
             res["scatter"] = {"seconds": round(wl.scatter_s, 4),
                               "GiB_per_s": round(world * args.objects * n / wl.scatter_s / 2**30, 2),

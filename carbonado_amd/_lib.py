@@ -50,11 +50,10 @@ SIGNATURES = {
     "chip_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "chip_init": (ctypes.c_int, [ctypes.c_int]),
     "chip_last_device_error": (ctypes.c_char_p, []),
-    "chip_zfec_k4_schedule": (ctypes.c_int, [ctypes.c_uint32]),
-    "chip_zfec_schedule": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32]),
-    "chip_zfec_split_mode": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32]),
     "chip_device_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "chip_device_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "chip_device_alloc_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                              ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double)]),
     "chip_torch_alloc": (ctypes.c_void_p, [ctypes.c_ssize_t, ctypes.c_int, ctypes.c_void_p]),
     "chip_torch_free": (None, [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_int, ctypes.c_void_p]),
     "chip_calc_padding_len": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, c_u32p, c_u32p]),

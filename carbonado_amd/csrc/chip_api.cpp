@@ -506,88 +506,10 @@ hipError_t overlap_parts(uint64_t count, uint64_t parts, hipStream_t s, S1 stage
     return hipStreamWaitEvent(s, ps->join3, 0);
 }
 
-// A batch cut into two halves launched side by side on the two pipeline
-// streams (fork/join with events on s).
-template <typename F>
-hipError_t split_pair(uint64_t count, hipStream_t s, F launch) {
-    PipeStreams *ps;
-    hipError_t e;
-    if ((e = pipe_streams(&ps)) != hipSuccess) return e;
-    if ((e = hipEventRecord(ps->fork, s)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(ps->k1, ps->fork, 0)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(ps->k3, ps->fork, 0)) != hipSuccess) return e;
-    const uint64_t half = count / 2;
-    if (const int us = env_int("CHIP_ZF_SPLIT_DELAY_US", 0); us > 0)  // experiment: start the halves out of phase
-        if ((e = delay_on_stream((uint32_t)us, ps->k3)) != hipSuccess) return e;
-    if ((e = launch(0, half, ps->k1)) != hipSuccess) return e;
-    if ((e = launch(half, count - half, ps->k3)) != hipSuccess) return e;
-    if ((e = hipEventRecord(ps->join1, ps->k1)) != hipSuccess) return e;
-    if ((e = hipEventRecord(ps->join3, ps->k3)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(s, ps->join1, 0)) != hipSuccess) return e;
-    return hipStreamWaitEvent(s, ps->join3, 0);
-}
-
-// A zfec batch as one launch or as two concurrent halves.  On some boxes
-// the two halves move 13 % more bytes per second than one launch, on others
-// 1-2.5 % less, so the first eligible batch (>= 2 GiB of
-// input, >= 16 objects) of each (device, k, rows) class times its own
-// quarters both ways — single, split, single, split, events on s — keeps the
-// faster for the rest of that batch and for later ones.  CHIP_ZF_SPLIT=0|1
-// forces one (read per call: tests toggle it).  The first large 4-of-8 batch
-// (4-of-8 or 8-of-16) tunes the kernel schedule (k4_tune) and runs single.
-std::mutex g_split_mu;
-std::map<std::tuple<int, uint32_t, uint32_t>, int> g_split;  // (device, k, rows) -> 0 single, 1 split
-
+// A zfec batch: one launch (the dynamic run queue balances the XCDs inside it).
 template <typename F>  // launch(o0, cnt, stream) -> hipError_t, objects [o0, o0 + cnt)
-hipError_t zf_run(uint32_t k, uint32_t rows, uint64_t in_bytes, uint64_t count, hipStream_t s, F launch) {
-    const char *env = std::getenv("CHIP_ZF_SPLIT");
-    const bool eligible = count >= 16 && in_bytes >= (2ull << 30) &&
-                          !((k == 4 || k == 8) && chip_zfec_schedule(k, rows) < 0);
-    if (!eligible || (env && !std::atoi(env))) return launch(0, count, s);
-    if (env) return split_pair(count, s, launch);
-    const auto key = std::make_tuple(selected_device(), k, rows);
-    int mode = -1;
-    {
-        std::lock_guard<std::mutex> lk(g_split_mu);
-        auto it = g_split.find(key);
-        if (it != g_split.end()) mode = it->second;
-    }
-    if (mode == 0) return launch(0, count, s);
-    if (mode == 1) return split_pair(count, s, launch);
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;  // tuning waits on events: not while capturing
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return launch(0, count, s);
-    hipEvent_t ev[5] = {};
-    hipError_t e = hipSuccess;
-    for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
-    if (e == hipSuccess) e = hipEventRecord(ev[0], s);
-    const uint64_t q = count / 4;
-    uint64_t cnt[4];
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) {
-        const uint64_t o0 = i * q;
-        cnt[i] = i == 3 ? count - 3 * q : q;
-        if (i & 1)
-            e = split_pair(cnt[i], s, [&](uint64_t o, uint64_t c, hipStream_t st) { return launch(o0 + o, c, st); });
-        else
-            e = launch(o0, cnt[i], s);
-        if (e == hipSuccess) e = hipEventRecord(ev[i + 1], s);
-    }
-    float t[4] = {0.f, 0.f, 0.f, 0.f};
-    if (e == hipSuccess) e = hipEventSynchronize(ev[4]);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventElapsedTime(&t[i], ev[i], ev[i + 1]);
-    for (hipEvent_t x : ev)
-        if (x) (void)hipEventDestroy(x);
-    if (e != hipSuccess) return e;
-    const double single = std::min(t[0] / cnt[0], t[2] / cnt[2]), split = std::min(t[1] / cnt[1], t[3] / cnt[3]);
-    std::lock_guard<std::mutex> lk(g_split_mu);
-    g_split[key] = split < single ? 1 : 0;
-    return hipSuccess;
-}
-
-int zf_split_known(uint32_t k, uint32_t rows) {
-    if (const char *env = std::getenv("CHIP_ZF_SPLIT")) return std::atoi(env) ? 1 : 0;
-    std::lock_guard<std::mutex> lk(g_split_mu);
-    auto it = g_split.find(std::make_tuple(selected_device(), k, rows));
-    return it == g_split.end() ? -1 : it->second;
+hipError_t zf_run(uint64_t count, hipStream_t s, F launch) {
+    return launch(0, count, s);
 }
 
 int pipe_parts_cfg() {
@@ -951,7 +873,7 @@ int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     if (aliased && (uint64_t)k * C > n)  // the zero padding of encoding.rs:53-55 becomes part of shard k-1
         CHIP_HIP(hipMemset2DAsync(d_out + n, out_stride ? out_stride : (uint64_t)m * C, 0, (uint64_t)k * C - n,
                                   count, s));
-    CHIP_HIP(zf_run(k, aliased ? m - k : m, count * n, count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
+    CHIP_HIP(zf_run(count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
         GfLaunch L{d_in + o0 * in_stride, d_out + o0 * out_stride, in_stride, out_stride, n, C, cnt};
         return gf_apply(p, L, st);
     }));
@@ -1067,7 +989,7 @@ int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     int part_st = CHIP_OK;
-    const hipError_t e = zf_run(k, k, count * k * chunk_len, count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
+    const hipError_t e = zf_run(count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
         const int r = zfec_decode_device(k, m, d_in + o0 * in_stride, in_stride, slot_off, sel, chunk_len, cnt,
                                          d_out + o0 * out_stride, out_stride, st);
         if (r != CHIP_OK) part_st = r;
@@ -1080,12 +1002,12 @@ int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
 
 // ---- bao ---------------------------------------------------------------
 
-int chip_zfec_split_mode(uint32_t k, uint32_t rows) { return zf_split_known(k, rows); }
-
-// Batch buffers in physically contiguous HBM (hipDeviceMallocContiguous):
-// large fragments, so address translation covers a whole multi-GiB batch
-// (K1 on the same box: +1.5-4 % and no spread from one process to the next,
-// DESIGN.md §3).  Falls back to hipMalloc when no contiguous range is free.
+// Batch buffers.  From 1 GiB up: class-balanced memory (hbm_alloc.hpp):
+// physical pieces spread over the HBM "classes" and mapped shuffled, so the
+// streaming kernels never write into one class only (DESIGN.md §2, §3 K1:
+// 4-of-8 encode 0.63-0.67 -> 0.77-0.78 of the roofline).  Smaller buffers,
+// or CHIP_ALLOC=contiguous: physically contiguous memory
+// (hipDeviceMallocContiguous), else hipMalloc.
 int chip_device_alloc(uint64_t bytes, void **ptr) {
     if (!ptr) return CHIP_ERR_INVALID_ARG;
     *ptr = nullptr;
@@ -1093,6 +1015,14 @@ int chip_device_alloc(uint64_t bytes, void **ptr) {
     if (st != CHIP_OK) return st;
     void *p = nullptr;
     const size_t sz = bytes ? bytes : 1;
+    const char *mode = std::getenv("CHIP_ALLOC");
+    const bool balanced = !(mode && std::strcmp(mode, "contiguous") == 0);
+    if (balanced && hbm_alloc(sz, &p) == hipSuccess && p) {
+        *ptr = p;
+        return CHIP_OK;
+    }
+    (void)hipGetLastError();
+    p = nullptr;
     if (hipExtMallocWithFlags(&p, sz, hipDeviceMallocContiguous) != hipSuccess || !p) {
         (void)hipGetLastError();
         p = nullptr;
@@ -1104,7 +1034,18 @@ int chip_device_alloc(uint64_t bytes, void **ptr) {
 
 int chip_device_free(void *ptr) {
     if (!ptr) return CHIP_OK;
+    if (hbm_free(ptr)) return CHIP_OK;
     CHIP_HIP(hipFree(ptr));
+    return CHIP_OK;
+}
+
+int chip_device_alloc_info(const void *ptr, uint32_t *classes_found, uint32_t *classes_used, double *seconds) {
+    uint32_t f = 0, u = 0;
+    double t = 0;
+    if (!ptr || !hbm_info(ptr, &f, &u, &t)) return CHIP_ERR_INVALID_ARG;
+    if (classes_found) *classes_found = f;
+    if (classes_used) *classes_used = u;
+    if (seconds) *seconds = t;
     return CHIP_OK;
 }
 

@@ -63,8 +63,6 @@ struct GfLaunch {
 // Plans with more than ZF_MAXP computed rows run in passes of ZF_MAXP rows
 // (copies ride on the first pass); k > ZF_MAXK uses the generic kernel.
 hipError_t gf_apply(const GfPlan &plan, const GfLaunch &L, hipStream_t stream);
-// Delay the work queued behind it on `stream` by `us` microseconds (one spinning wave).
-hipError_t delay_on_stream(uint32_t us, hipStream_t stream);
 
 // ---- bao / BLAKE3 ------------------------------------------------------
 uint64_t bao_encoded_len(uint64_t n);
@@ -98,6 +96,13 @@ hipError_t bao_gather_content(const uint8_t *d_stream, uint64_t n, uint64_t c0, 
 uint64_t bao_chunk_offset(uint64_t i, uint64_t N);
 uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N);
 uint64_t bao_parent_index(uint64_t s, int level, uint64_t N);
+
+// ---- batch buffers (hbm_alloc.hip) --------------------------------------
+// Class-balanced device memory for buffers >= 1 GiB (hbm_alloc.hpp); returns
+// an error for smaller sizes or when the virtual-memory API fails.
+hipError_t hbm_alloc(uint64_t bytes, void **out);
+bool hbm_free(void *p);  // true if p came from hbm_alloc
+bool hbm_info(const void *p, uint32_t *classes_found, uint32_t *classes_used, double *seconds);
 
 // ---- context ------------------------------------------------------------
 int ensure_device();                 // CHIP_OK or CHIP_ERR_NO_DEVICE

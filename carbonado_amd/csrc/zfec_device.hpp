@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "chip_internal.hpp"
 #include "layout_store.hpp"
@@ -32,6 +33,83 @@ struct ApplyArgs {
     uint64_t in_off[ZF_MAXK];
     uint64_t copy_off[ZF_MAXK];
     uint64_t par_off[ZF_MAXP];
+    uint32_t *queue;                   // MAP 6/7: run counters (QueueIter), zero at launch, left zero
+    uint32_t xcd_mask;                 // MAP 6/7: XCDs whose workgroups take runs (0 = all)
+    uint64_t *trace;                   // TR: per-workgroup {start, end, xcc, tiles} (tools only)
+};
+
+// Hardware XCC (XCD) id of the executing workgroup (gfx940+ HW_REG_XCC_ID).
+__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u; }
+
+// Dynamic run queue (MAP 6 and 7).  The tile space is cut into runs of CH
+// consecutive tiles, the runs into 8 shares, one per XCD.  A workgroup takes
+// the next run of its own XCD's share (one device-scope atomic per run, by
+// thread 0, broadcast through LDS) and, once that share is exhausted, runs
+// of the following XCDs' shares: the XCDs that stream faster finish the
+// slower ones' work instead of idling at the end of the launch.
+//   MAP 6: share x = the x-th contiguous eighth of the runs;
+//   MAP 7: MAP 3's interleave (the XCD's G/8 workgroups' runs of each
+//          round of G runs), so all XCDs sweep one window of the batch.
+// q[32 x] = run counter of share x, q[256] = workgroups done; the last
+// workgroup to finish zeroes them, so every launch finds them zero.
+template <int MAP>
+struct QueueIter {
+    uint32_t *q, *slot;
+    uint64_t R, T, CH, g, run = 0, t_in = 0, rl = 0;
+    uint32_t xcc, v = 0, k = 0;
+    __device__ QueueIter(uint64_t total, uint64_t ch, uint32_t *queue, uint32_t *lds_slot, uint32_t mask)
+        : q(queue), slot(lds_slot), T(total), CH(ch < 1 ? 1 : ch) {
+        R = (T + CH - 1) / CH;
+        g = gridDim.x / 8 ? gridDim.x / 8 : 1;
+        xcc = xcc_id();
+        if (mask && !((mask >> xcc) & 1u)) v = 8;  // this XCD sits out: the others take its share
+    }
+    // run index of the i-th run of share x, or ~0 past its end
+    __device__ uint64_t share_run(uint32_t x, uint64_t i) const {
+        if (MAP == 6) {
+            const uint64_t lo = x * R / 8, hi = (x + 1) * R / 8;
+            return lo + i < hi ? lo + i : ~0ull;
+        }
+        const uint64_t r = (i / g) * (8 * g) + x * g + (i % g);
+        return r < R ? r : ~0ull;
+    }
+    __device__ bool grab() {
+        uint32_t *s = slot + (k++ & 1);  // double-buffered: one barrier per grab
+        if (threadIdx.x == 0) {
+            uint32_t got = ~0u;
+            while (v < 8) {
+                const uint32_t x = (xcc + v) & 7u;
+                const uint32_t i = atomicAdd(q + 32 * x, 1u);
+                const uint64_t r = share_run(x, i);
+                if (r != ~0ull) { got = (uint32_t)r; break; }
+                ++v;
+            }
+            *s = got;
+        }
+        __syncthreads();
+        const uint32_t r = *s;
+        if (r == ~0u) return false;
+        run = r;
+        t_in = 0;
+        rl = (run + 1) * CH <= T ? CH : T - run * CH;
+        return true;
+    }
+    __device__ bool next(uint64_t &t) {
+        if (t_in == rl && !grab()) return false;
+        t = run * CH + t_in++;
+        return true;
+    }
+    // every workgroup, after its last next(): the last one resets the counters
+    __device__ void finish() {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(q + 256, 1u) == gridDim.x - 1) {
+                for (int x = 0; x < 8; ++x) atomicExch(q + 32 * x, 0u);
+                atomicExch(q + 256, 0u);
+            }
+        }
+    }
 };
 
 __host__ __device__ constexpr int replicas_for(int k) {
@@ -179,7 +257,7 @@ struct TileIter {
 // super-tile's shards before computing the current one, NTL: nontemporal
 // input loads — tools/zfec_tune.
 template <int K, int NG, int U, int MAP, bool NT, int RO = 0, int WPE = 1, int SB = 0, bool PF = false,
-          bool NTL = false>
+          bool NTL = false, bool TR = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_kernel(ApplyArgs a) {
     constexpr int R = RO ? RO : replicas_for(K);
     using E = typename Entry<NG>::T;
@@ -214,7 +292,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
     // super-tiles of U adjacent column tiles of one object
     const uint64_t spo = (a.tiles_per_obj + U - 1) / U;
-    TileIter<MAP> iter(spo * a.count, a.chunk);
+    uint64_t t_start = 0, n_tiles = 0;
+    if constexpr (TR) t_start = wall_clock64();
+    __shared__ uint32_t q_slot[2];
+    using Iter = typename std::conditional<(MAP >= 6), QueueIter<MAP>, TileIter<MAP>>::type;
+    Iter iter = [&] {
+        if constexpr (MAP >= 6) return Iter(spo * a.count, a.chunk, a.queue, q_slot, a.xcd_mask);
+        else return Iter(spo * a.count, a.chunk);
+    }();
     auto load_tile = [&](uint64_t t, u32x4 (&v)[U][K]) {
         const uint64_t obj = t / spo;
         const uint64_t col0 = (t - obj * spo) * (uint64_t)(U * TILE) + threadIdx.x * VEC;
@@ -311,6 +396,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         st = st_next;
         have = have_next;
+        if constexpr (TR) ++n_tiles;
+    }
+    if constexpr (MAP >= 6) iter.finish();
+    if constexpr (TR) {
+        if (threadIdx.x == 0) {
+            uint64_t *tr = a.trace + 4 * blockIdx.x;
+            tr[0] = t_start;
+            tr[1] = wall_clock64();
+            tr[2] = xcc_id();
+            tr[3] = n_tiles;
+        }
     }
 }
 

@@ -85,14 +85,18 @@ __global__ __launch_bounds__(TPB) void gf_apply_generic_kernel(GenericArgs a) {
 // ---- host side ----------------------------------------------------------
 typedef void (*KernelFn)(ApplyArgs);
 
-// tuned schedule (tools/zfec_tune.hip on MI355X; DESIGN.md "K1 tuning")
-// MI355X sweeps (gpurun_out logs summarised in DESIGN.md): XCD-grouped runs of
-// 64 tiles (256 KiB per shard per workgroup) with nontemporal stores reach
-// ~97% of the bandwidth of the bare 4-read/8-write stream pattern.
-constexpr int ZF_U = 1;
-constexpr int ZF_MAP = 3;
+// Schedule.  Every shape walks its column tiles through the
+// dynamic per-XCD run queue (MAP 6, QueueIter): runs of ZF_CHUNK tiles (256
+// KiB per shard) dealt from 8 contiguous shares of the batch, one per XCD,
+// and once an XCD's share is done it takes runs of the others'.  The XCDs
+// do not stream at the same rate (odd XCDs ~20 % slower on every box
+// measured, tools/zfec_timeline), so the static XCD-grouped order this
+// replaces (MAP 3) ended with half the chip idle for the last ~1 ms of a
+// 10 ms launch; the queue ends every XCD within ~0.1 ms (+2.5-3 % on the
+// headline, and it needs no per-box schedule choice).
+constexpr int ZF_MAP = 6;
 constexpr bool ZF_NT = true;
-constexpr uint64_t ZF_CHUNK = 64;
+constexpr uint64_t ZF_CHUNK = 64;   // tiles per run (U = 1 tiles; U = 2 super-tiles run ZF_CHUNK / 2)
 constexpr uint64_t ZF_BL_RUN = 32;  // bao-layout kernel: consecutive 1 KiB units per wave run
 
 // Wide stripes (K > 4): pin the XOR partial sums every shard (SB = 1) so the
@@ -101,12 +105,11 @@ constexpr uint64_t ZF_BL_RUN = 32;  // bao-layout kernel: consecutive 1 KiB unit
 // into registers (K <= 8; K = 16 has no registers to spare).  8 computed
 // rows (NG = 2): plain stores measured +1-3% over nontemporal at 2
 // workgroups/CU (tools/zfec_tune, 8-of-16 sweep in DESIGN.md).
-// The 4-of-8 shape (K = 4, NG = 1) has two schedules, picked at run time per
-// box (k4_info / k4_tune below).
+// The 4-of-8 shape (K = 4, NG = 1): super-tiles of 2 column tiles, the next
+// one's shards prefetched into registers, 2 workgroups/CU (160 VGPRs).
 struct KernelInfo {
     KernelFn fn;
     size_t lds;
-    int grid;
     int u;        // column tiles per super-tile (the kernel's U)
     int bpc_cap;  // workgroups per CU to launch (0 = occupancy limit)
 };
@@ -116,17 +119,16 @@ KernelInfo make_info() {
     constexpr int R = replicas_for(K);
     KernelInfo ki;
     ki.lds = (size_t)256 * K * R * 4 * NG;
-    ki.grid = 0;
     ki.u = 1;
     ki.bpc_cap = 0;
     if constexpr (K > 4) {
-        ki.fn = gf_apply_kernel<K, NG, ZF_U, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
-    } else if constexpr (K == 4 && NG == 1) {  // schedule S0 (k4_info)
+        ki.fn = gf_apply_kernel<K, NG, 1, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
+    } else if constexpr (K == 4 && NG == 1) {
         ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true>;
         ki.u = 2;
         ki.bpc_cap = 2;
     } else {
-        ki.fn = gf_apply_kernel<K, NG, ZF_U, ZF_MAP, ZF_NT>;
+        ki.fn = gf_apply_kernel<K, NG, 1, ZF_MAP, ZF_NT>;
     }
     return ki;
 }
@@ -144,38 +146,6 @@ bool lookup_fast(int k, int ng, KernelInfo &out) {
 #undef CHIP_CASE
 }
 
-// The 4-of-8 schedules (tools/zfec_tune.hip): S0 = super-tiles of 2 column
-// tiles, the next super-tile prefetched, 2 workgroups/CU; S1 = one tile, the
-// next prefetched, 4 workgroups/CU; S2 = S0 at 1 workgroup/CU.  Each won in
-// some process of the same box (profiles/r1x_k4_schedules.txt: 5446 / 5370 /
-// 5228 GB/s for the winner vs 5240 / 5236 / 5161 for S0).
-KernelInfo k4_info(int s) {
-    KernelInfo ki = make_info<4, 1>();
-    if (s == 1) {
-        ki.fn = gf_apply_kernel<4, 1, 1, ZF_MAP, ZF_NT, 0, 1, 0, true>;
-        ki.u = 1;
-        ki.bpc_cap = 4;
-    } else if (s == 2) {  // S2: S0's kernel at 1 workgroup/CU
-        ki.bpc_cap = 1;
-    }
-    return ki;
-}
-
-// The 8-of-16 shape (K = 8, NG = 2): the same kernel at its occupancy of 2
-// workgroups/CU (S0) or at 1 (S1).  Which is faster flips with the process's
-// HBM placement (tools/zfec_tune: 5272 vs 5164 GB/s in one process, 4687 vs
-// 4934 in another).
-KernelInfo k8_info(int s) {
-    KernelInfo ki = make_info<8, 2>();
-    if (s == 1) ki.bpc_cap = 1;
-    return ki;
-}
-
-// shapes with two schedules to pick from at run time
-bool tunable_shape(uint32_t k, int ng) { return (k == 4 && ng == 1) || (k == 8 && ng == 2); }
-int tuned_candidates(uint32_t k) { return k == 4 ? 3 : 2; }
-KernelInfo tuned_info(uint32_t k, int s) { return k == 4 ? k4_info(s) : k8_info(s); }
-
 struct DevTable {
     void *ptr = nullptr;
     size_t bytes = 0;
@@ -186,31 +156,38 @@ std::map<std::vector<uint8_t>, DevTable> g_tables;  // key: device, k, ng, coef 
 std::map<std::pair<KernelFn, size_t>, int> g_grid;
 std::map<int, uint8_t *> g_multab;                  // per device
 
-// ---- run-time choice of the schedule (4-of-8: S0/S1/S2, 8-of-16: S0/S1) ---
-// The candidates are within a few per cent of each other and which one wins
-// depends on where the process's buffers sit in HBM.  The
-// first large launch of each (device, k, output rows) class runs two slices
-// of count/8 objects per candidate, interleaved, between events on its
-// stream, waits for them, keeps the fastest and runs the rest of the batch
-// with it; later launches use the choice.  CHIP_ZFEC_K4_SCHED=0|1|2 fixes the
-// schedule (A/B runs, profiles; CHIP_ZFEC_K4_U1 = 1, the older switch).
-constexpr uint64_t K4_TUNE_MIN = uint64_t(1) << 30;  // input bytes of a launch worth tuning on
-std::map<std::tuple<int, int, int>, int> g_k4;         // (device, k, output rows) -> schedule
+// Run-queue counters (QueueIter) per stream: launches on one stream run one
+// after another, and each launch leaves its counters zero (its last
+// workgroup resets them), so a stream's launches can share one block.  Blocks
+// come from a per-device pool of QUEUE_SLOTS, handed to streams in order of
+// first use; past QUEUE_SLOTS streams a slot is shared, which is safe unless
+// two of its streams run zfec launches at the same time.
+constexpr int QUEUE_SLOTS = 256;
+constexpr size_t QUEUE_BYTES = 2048;  // 8 counters 128 B apart + the done counter
+std::map<int, uint8_t *> g_queue_pool;                      // per device
+std::map<std::pair<int, hipStream_t>, uint32_t *> g_queue;  // (device, stream) -> counters
 
-int k4_forced() {
-    static const int f = [] {
-        if (const char *e = std::getenv("CHIP_ZFEC_K4_SCHED")) return std::max(0, std::min(2, std::atoi(e)));
-        return std::getenv("CHIP_ZFEC_K4_U1") ? 1 : -1;
-    }();
-    return f;
-}
-
-int k4_known(int k, int rows) {
-    const int f = k4_forced();
-    if (f >= 0) return f;
+hipError_t queue_for(hipStream_t stream, uint32_t **out) {
+    const int dev = selected_device();
     std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_k4.find(std::make_tuple(selected_device(), k, rows));
-    return it == g_k4.end() ? -1 : it->second;
+    auto key = std::make_pair(dev, stream);
+    auto it = g_queue.find(key);
+    if (it != g_queue.end()) { *out = it->second; return hipSuccess; }
+    uint8_t *&pool = g_queue_pool[dev];
+    if (!pool) {
+        uint8_t *d = nullptr;
+        hipError_t e = hipMalloc(&d, QUEUE_SLOTS * QUEUE_BYTES);
+        if (e != hipSuccess) return e;
+        e = hipMemset(d, 0, QUEUE_SLOTS * QUEUE_BYTES);
+        if (e != hipSuccess) { (void)hipFree(d); return e; }
+        pool = d;
+    }
+    size_t used = 0;
+    for (const auto &kv : g_queue) used += kv.first.first == dev;
+    uint32_t *q = reinterpret_cast<uint32_t *>(pool + (used % QUEUE_SLOTS) * QUEUE_BYTES);
+    g_queue[key] = q;
+    *out = q;
+    return hipSuccess;
 }
 
 int grid_for(const KernelInfo &ki) {
@@ -316,30 +293,11 @@ hipError_t apply_generic(const GfPlan &p, const GfLaunch &L, hipStream_t stream)
     return hipFreeAsync(d, stream);
 }
 
-hipError_t k4_tune(const GfPlan &p, const GfLaunch &L, hipStream_t stream, uint32_t row0, uint32_t nrows,
-                   bool copies, int rows);
-
-// sched: the 4-of-8 schedule to use, -1 = the known choice or tune now
 hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
-                         uint32_t row0, uint32_t nrows, bool copies, int sched = -1) {
+                         uint32_t row0, uint32_t nrows, bool copies) {
     const int ng = nrows > 4 ? 2 : 1;
     KernelInfo ki;
     if (!lookup_fast((int)p.k, ng, ki)) return hipErrorInvalidValue;
-    if (tunable_shape(p.k, ng) && !L.bao_off) {
-        int rows = (int)nrows;  // output shards written per column
-        if (copies)
-            for (uint32_t j = 0; j < p.k; ++j) rows += p.copy_off[j] != NO_OUT;
-        if (sched < 0) sched = k4_known((int)p.k, rows);
-        if (sched < 0) {
-            // tuning waits on events: not inside a stream capture (hipGraph)
-            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            const bool capturing = hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
-            if (!capturing && L.count >= 8 && L.count * L.valid >= K4_TUNE_MIN)
-                return k4_tune(p, L, stream, row0, nrows, copies, rows);
-            sched = 0;
-        }
-        ki = tuned_info(p.k, sched);
-    }
     ApplyArgs a;
     std::memset(&a, 0, sizeof a);
     a.in = L.in; a.out = L.out;
@@ -371,6 +329,7 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     sub.coef.assign(p.coef.begin() + (size_t)row0 * p.k, p.coef.begin() + (size_t)(row0 + nrows) * p.k);
     hipError_t e = device_table(sub, ng, &a.table);
     if (e != hipSuccess) return e;
+    if (!bl && (e = queue_for(stream, &a.queue)) != hipSuccess) return e;
     int grid_cap = grid_for(ki);
     if (L.wg_per_cu > 0 && grid_cap > L.wg_per_cu * num_cus()) grid_cap = L.wg_per_cu * num_cus();
     // the kernel walks super-tiles of ki.u column tiles (never across objects)
@@ -389,59 +348,7 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     return hipGetLastError();
 }
 
-hipError_t k4_tune(const GfPlan &p, const GfLaunch &L, hipStream_t stream, uint32_t row0, uint32_t nrows,
-                   bool copies, int rows) {
-    // 2 slices of count/8 objects per candidate, interleaved (S0 S1 [S2] S0 S1 [S2])
-    const int nc = tuned_candidates(p.k), ns = 2 * nc;
-    const uint64_t piece = L.count / 8;
-    auto slice = [&](uint64_t o0, uint64_t cnt) {
-        GfLaunch S = L;
-        S.in = L.in + o0 * L.in_stride;
-        S.out = L.out + o0 * L.out_stride;
-        S.count = cnt;
-        return S;
-    };
-    hipEvent_t ev[7] = {};
-    hipError_t e = hipSuccess;
-    for (int i = 0; i <= ns && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
-    if (e == hipSuccess) e = hipEventRecord(ev[0], stream);
-    for (int i = 0; i < ns && e == hipSuccess; ++i) {
-        e = gf_apply_pass(p, slice(i * piece, piece), stream, row0, nrows, copies, i % nc);
-        if (e == hipSuccess) e = hipEventRecord(ev[i + 1], stream);
-    }
-    float t[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (e == hipSuccess) e = hipEventSynchronize(ev[ns]);
-    for (int i = 0; i < ns && e == hipSuccess; ++i) e = hipEventElapsedTime(&t[i], ev[i], ev[i + 1]);
-    for (hipEvent_t x : ev)
-        if (x) (void)hipEventDestroy(x);
-    if (e != hipSuccess) return e;
-    int s = 0;
-    float best = std::min(t[0], t[nc]);
-    for (int c = 1; c < nc; ++c)
-        if (std::min(t[c], t[c + nc]) < best) {
-            best = std::min(t[c], t[c + nc]);
-            s = c;
-        }
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        g_k4[std::make_tuple(selected_device(), (int)p.k, rows)] = s;
-    }
-    return gf_apply_pass(p, slice(ns * piece, L.count - ns * piece), stream, row0, nrows, copies, s);
-}
-
 }  // namespace
-
-// One wave spinning on the 100 MHz wall clock for `us` microseconds: delays
-// the work queued behind it on its stream (split experiments, CHIP_ZF_SPLIT_DELAY_US).
-__global__ void delay_kernel(uint64_t ticks) {
-    const uint64_t t0 = wall_clock64();
-    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
-}
-
-hipError_t delay_on_stream(uint32_t us, hipStream_t stream) {
-    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, stream, (uint64_t)us * 100);
-    return hipGetLastError();
-}
 
 hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
     if (L.count == 0 || L.C == 0) return hipSuccess;
@@ -457,5 +364,3 @@ hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
 
 }  // namespace chip
 
-extern "C" int chip_zfec_k4_schedule(uint32_t rows) { return chip::k4_known(4, (int)rows); }
-extern "C" int chip_zfec_schedule(uint32_t k, uint32_t rows) { return chip::k4_known((int)k, (int)rows); }

@@ -59,7 +59,7 @@ extern "C" {
 #define CHIP_API
 #endif
 
-#define CHIP_ABI_VERSION 3
+#define CHIP_ABI_VERSION 4
 #define CHIP_HASH_LEN 32   /* bao::HASH_SIZE */
 #define CHIP_SLICE_LEN 1024 /* constants.rs:9 SLICE_LEN */
 #define CHIP_FEC_K 4        /* constants.rs:11 FEC_K */
@@ -127,27 +127,23 @@ CHIP_API const char *chip_strerror(int status);
 CHIP_API int chip_init(int device);
 /* Last HIP error string seen by this thread (for CHIP_ERR_DEVICE). */
 CHIP_API const char *chip_last_device_error(void);
-/* Diagnostics: the zfec 4-of-8 schedule this process chose on its device for
- * launches that write `rows` output shards per column (8 = encode with the
- * data shards, 4 = parity only or a 2-erasure decode): 0, 1 or 2, -1 = not
- * chosen yet.  The first launch of >= 1 GiB picks it. */
-CHIP_API int chip_zfec_k4_schedule(uint32_t rows);
-/* The same for any shape with two schedules (k = 4: as above; k = 8, the
- * 8-of-16 shape: 0 = 2 workgroups/CU, 1 = 1); -1 for other shapes. */
-CHIP_API int chip_zfec_schedule(uint32_t k, uint32_t rows);
-/* Diagnostics: whether this process runs large zfec batches of shape
- * (k, rows) as one launch (0) or as two concurrent halves on two streams (1),
- * -1 = not decided yet.  The first batch of >= 2 GiB decides by timing its
- * own quarters both ways; CHIP_ZF_SPLIT=0|1 forces it. */
-CHIP_API int chip_zfec_split_mode(uint32_t k, uint32_t rows);
 
 /* ---- batch buffers ------------------------------------------------------ */
-/* Device memory for batch buffers, physically contiguous where the device
- * has such a range free (hipDeviceMallocContiguous; else hipMalloc): the
- * streaming kernels run faster and steadier over it.
- * Any 16-B aligned device memory works with the batch entry points. */
+/* Device memory for batch buffers.  From 1 GiB up it is class-balanced:
+ * built from 8 MiB physical pieces chosen across the HBM's write "classes"
+ * (timed at allocation) and mapped in a shuffled order behind one fresh
+ * virtual range, so streaming writes spread over every class (DESIGN.md §2,
+ * §3 K1: 4-of-8 encode at 0.77-0.78 of the roofline vs 0.63-0.67 over one
+ * hipMalloc).  Smaller buffers (or CHIP_ALLOC=contiguous): physically
+ * contiguous memory where free, else hipMalloc.  Any 16-B aligned device
+ * memory works with the batch entry points; this is where they run fastest. */
 CHIP_API int chip_device_alloc(uint64_t bytes, void **ptr);
 CHIP_API int chip_device_free(void *ptr);
+/* For a class-balanced buffer from chip_device_alloc: how many memory
+ * classes the allocation found and used, and the seconds it took.
+ * CHIP_ERR_INVALID_ARG for any other pointer. */
+CHIP_API int chip_device_alloc_info(const void *ptr, uint32_t *classes_found, uint32_t *classes_used,
+                                    double *seconds);
 /* The same, with the signatures torch.cuda.memory.CUDAPluggableAllocator
  * loads (size, device, stream): a torch MemPool over these hands out
  * contiguous tensors (carbonado_amd.device.empty_batch). */

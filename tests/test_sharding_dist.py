@@ -85,3 +85,49 @@ def test_bench_world2_cpu_dry_run(world):
     res = json.loads(lines[0])
     assert res["n_gpus"] == world and res["scaling"] == "weak"
     assert res["config"]["global_objects"] == world * res["config"]["objects_per_gpu"]
+
+
+def test_bench_spawns_its_own_ranks_dry_run():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts the two rank processes
+    itself (the driver's N>1 command line without torch.distributed.run) and
+    rank 0 prints one line with n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                          "--dry-run"], capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_objects"] == 2 * res["config"]["objects_per_gpu"]
+    assert len(res["roofline"]["per_rank_avg_launch_ms"]) == 2
+
+
+def test_bench_refuses_world_size_mismatch():
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=120, cwd=root, env=env)
+    assert out.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in out.stderr
+
+
+def test_bench_config_presets():
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    a = bench.parse(["--config", "cfg5"])
+    assert (a.mode, a.k, a.m, a.objects) == ("encode", 8, 16, 1024)
+    a = bench.parse(["--config", "cfg3", "--objects", "64"])
+    assert (a.mode, a.erase, a.objects) == ("decode", "1,2", 64)
+    a = bench.parse(["--config", "cfg4"])
+    assert (a.mode, a.level) == ("e2e", 15)
+    a = bench.parse([])
+    assert (a.mode, a.k, a.m, a.objects, a.alloc) == ("encode", 4, 8, 1024, "chip")
