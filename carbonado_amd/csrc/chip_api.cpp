@@ -1814,7 +1814,8 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
                 uint8_t *dst = out + o * out_stride;
                 int r = CHIP_OK;
                 if ((format & CHIP_FORMAT_ECIES) && (format & CHIP_FORMAT_SNAPPY)) {  // one pass, no plaintext buffer
-                    status[o] = host::ecies_decrypt_snap(secret_key, sk_len, src, n, dst, out_stride, &got);
+                    status[o] = host::ecies_decrypt_snap(secret_key, sk_len, src, n, dst, out_stride, &got,
+                                                         tmp.get(host::DECRYPT_SNAP_WINDOW));
                     out_len[o] = got;
                     continue;
                 }

@@ -590,7 +590,7 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
 // longer than the window (never produced by a FrameEncoder) takes the
 // two-pass route.
 int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
-                       uint64_t cap, uint64_t *out_len) {
+                       uint64_t cap, uint64_t *out_len, uint8_t *window) {
     BnPtr k(parse_secret(secret, secret_len));
     if (!k.p) return CHIP_ERR_ECIES;
     if (n < ECIES_OVERHEAD) return CHIP_ERR_ECIES;
@@ -609,10 +609,10 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
     OPENSSL_cleanse(key, 32);
     if (!dec_ok) return CHIP_ERR_ECIES;
 
-    constexpr uint64_t W = 256u << 10;
+    constexpr uint64_t W = DECRYPT_SNAP_WINDOW;
     static thread_local std::unique_ptr<uint8_t[]> t_win;
-    if (!t_win) t_win.reset(new uint8_t[W]);
-    uint8_t *win = t_win.get();
+    if (!window && !t_win) t_win.reset(new uint8_t[W]);
+    uint8_t *win = window ? window : t_win.get();
     uint64_t wbeg = 0, wend = 0;  // plaintext [wbeg, wend) sits at win[0 .. wend - wbeg)
     // plaintext [s, s + len) resident in the window; s only moves forward,
     // len <= W and s + len <= m
@@ -637,6 +637,7 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
     };
 
     uint64_t s = 0, d = 0;
+    const uint64_t ecap = out ? cap : 0;  // no buffer: size the output, write nothing
     bool ident = false, fits = true, two_pass = false;
     int frame = CHIP_OK, content = CHIP_OK;
     while (s < m) {  // snap_walk's chunk loop, both passes at once
@@ -667,7 +668,7 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
                 size_t used;
                 if (!get_varint(data, dl, &ulen, &used) || ulen > MAX_BLOCK) { frame = CHIP_ERR_SNAP; break; }
             }
-            if (fits && ulen > cap - d) fits = false;
+            if (fits && ulen > ecap - d) fits = false;
             if (fits && content == CHIP_OK) {
                 if (ty == 0x01) {
                     if (crc_masked(data, dl) != want) content = CHIP_ERR_SNAP;
@@ -684,10 +685,16 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
         s += clen;
     }
     if (two_pass) {
+        // what was written so far is not authenticated yet: wipe it (and the
+        // window) before the two-pass route, whose decrypt checks the tag first
+        if (d && out) OPENSSL_cleanse(out, std::min(d, ecap));
+        OPENSSL_cleanse(win, W);
         std::vector<uint8_t> tmp(m + 1);
         uint64_t got = 0;
         int st = ecies_decrypt(secret, secret_len, in, n, tmp.data(), tmp.size(), &got);
-        return st != CHIP_OK ? st : snap_decompress(tmp.data(), got, out, cap, out_len);
+        if (st == CHIP_OK) st = snap_decompress(tmp.data(), got, out, cap, out_len);
+        OPENSSL_cleanse(tmp.data(), tmp.size());
+        return st;
     }
     while (wend < m) {  // the rest of the ciphertext, for the tag
         const uint64_t step = std::min<uint64_t>(W, m - wend);
@@ -700,7 +707,7 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
              EVP_DecryptFinal_ex(cc.c, dummy, &fin) == 1;
     OPENSSL_cleanse(win, W);
     if (!dec_ok) {
-        if (d && out) OPENSSL_cleanse(out, std::min(d, cap));  // never hand back unauthenticated plaintext
+        if (d && out) OPENSSL_cleanse(out, std::min(d, ecap));  // never hand back unauthenticated plaintext
         return CHIP_ERR_ECIES;
     }
     if (frame != CHIP_OK) return frame;

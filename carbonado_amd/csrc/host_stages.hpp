@@ -34,8 +34,12 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
                   uint64_t cap, uint64_t *out_len);
 // ecies_decrypt then snap_decompress (decoding.rs:101-111) in one pass over
 // the ciphertext: same output and status codes, no full-size plaintext buffer.
+// `window`: DECRYPT_SNAP_WINDOW bytes of caller scratch reused across calls
+// (null: a per-thread buffer).  On a bad tag every byte written to `out` and
+// the window are wiped.
+constexpr uint64_t DECRYPT_SNAP_WINDOW = 256u << 10;
 int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
-                       uint64_t cap, uint64_t *out_len);
+                       uint64_t cap, uint64_t *out_len, uint8_t *window = nullptr);
 // Public key (65 B uncompressed) of a 32-byte secret; for tests and tooling.
 int ecies_public_key(const uint8_t *secret, uint8_t out[65]);
 

@@ -1,0 +1,88 @@
+"""GPU parity at BASELINE.json's own object size (16 MiB), one object per
+config, against the C oracle:
+
+* cfg4: the full level-15 encode() of a 16 MiB random object with the ECIES
+  randomness injected (N = 32776 chunks, padding 1941, C = 4,195,328 — not a
+  multiple of K1's 4 KiB tile), bit-exact against host_oracle.c's
+  orc_encode_full, and decoded back;
+* cfg5 shape: zfec 8-of-16 encode of 16 MiB, then decode with 8 shards
+  dropped (data and parity mixed);
+* cfg3: every one of the 28 two-erasure patterns of 4-of-8 on one 16 MiB
+  object, decoded on the device and compared with the input.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+from oracle import host_oracle as H
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N = 16 << 20
+SK = H.sha256(b"config-size receiver")
+EPH = H.sha256(b"config-size ephemeral")
+NONCE = H.sha256(b"config-size nonce")[:16]
+
+
+@pytest.fixture(scope="module")
+def obj16():
+    return np.random.default_rng(16).integers(0, 256, N, dtype=np.uint8).tobytes()
+
+
+def test_cfg4_level15_16mib_bit_exact(gpu, obj16):
+    import carbonado_amd as ca
+    pub = O.c_public_key(SK)
+    enc, h, info = ca.encode(pub, obj16, 15, ephemeral_sk=EPH, nonce=NONCE)
+    oenc, oh, oinfo = O.c_encode_full(obj16, 15, pub, EPH, NONCE)
+    assert info.padding_len == 1941 and info.chunk_len == 4_195_328
+    assert info.bytes_ecc == 8 * 4_195_328 and info.verifiable_slice_count == 32776
+    assert len(enc) == len(oenc) == info.bytes_verifiable == 35_660_232
+    assert h == oh
+    assert O.blake3(enc) == O.blake3(oenc)
+    assert enc == oenc
+    assert ca.decode(SK, h, enc, info.padding_len, 15) == obj16
+
+
+def test_cfg5_8of16_16mib_encode_and_decode_8_lost(gpu, obj16):
+    import torch
+    from carbonado_amd import device
+    inp = torch.from_numpy(np.frombuffer(obj16, np.uint8).copy()).cuda().reshape(1, N)
+    C = N // 8
+    enc = torch.zeros((1, 16 * C), dtype=torch.uint8, device="cuda")
+    device.zfec_encode_batch(inp, N, enc, 8, 16)
+    torch.cuda.synchronize()
+    ref, pad, oC = O.zfec_encode(obj16, 8, 16)
+    assert pad == 0 and oC == C
+    got = enc[0].cpu().numpy().tobytes()
+    assert got == ref
+    lost = {1, 2, 5, 7, 8, 11, 12, 15}  # 4 data + 4 parity shards
+    keep = [i for i in range(16) if i not in lost]
+    out = torch.zeros((1, N), dtype=torch.uint8, device="cuda")
+    device.zfec_decode_batch(enc, C, keep, out, 8, 16)
+    torch.cuda.synchronize()
+    assert out[0].cpu().numpy().tobytes() == obj16
+    # the C oracle's share-matrix decode agrees
+    shares = [ref[i * C:(i + 1) * C] for i in keep]
+    assert O.zfec_decode_shares(shares, keep, 0, 8, 16) == obj16
+
+
+def test_cfg3_all_28_erasure_pairs_16mib(gpu, obj16):
+    import torch
+    from carbonado_amd import device
+    inp = torch.from_numpy(np.frombuffer(obj16, np.uint8).copy()).cuda().reshape(1, N)
+    C = N // 4
+    enc = torch.zeros((1, 8 * C), dtype=torch.uint8, device="cuda")
+    device.zfec_encode_batch(inp, N, enc, 4, 8)
+    torch.cuda.synchronize()
+    assert enc[0].cpu().numpy().tobytes() == O.zfec_encode(obj16)[0]
+    pairs = list(itertools.combinations(range(8), 2))
+    assert len(pairs) == 28
+    out = torch.zeros((len(pairs), N), dtype=torch.uint8, device="cuda")
+    for i, lost in enumerate(pairs):
+        keep = [s for s in range(8) if s not in lost]
+        device.zfec_decode_batch(enc, C, keep, out[i:i + 1], 4, 8)
+    torch.cuda.synchronize()
+    for i, lost in enumerate(pairs):
+        assert torch.equal(out[i], inp[0]), lost

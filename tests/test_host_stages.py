@@ -264,3 +264,49 @@ def test_c_full_pipeline_golden(golden):
             enc, h, _ = O.c_encode_full(data, level, _x(m["public_key"]), _x(m["ephemeral_sk"]), _x(m["nonce"]))
             g = golden["samples"][name][f"level{level}"]
             assert O.blake3(enc).hex() == g["output_blake3"] and h.hex() == g["hash"], (name, level)
+
+
+def _chip_decode_raw(sk, enc, level, out, cap):
+    """chip_decode straight through the C-ABI with a caller-owned buffer."""
+    import ctypes
+    from carbonado_amd import _lib
+    L = _lib.lib()
+    got = ctypes.c_uint64()
+    e = np.frombuffer(enc, np.uint8)
+    rc = L.chip_decode(sk, len(sk), None, 0, e.ctypes.data, e.size, 0, level,
+                       out.ctypes.data if out is not None else None, cap, ctypes.byref(got))
+    return rc, got.value
+
+
+def test_bad_tag_wipes_written_output(ca):
+    """A bad AES-GCM tag returns EciesError and leaves no plaintext in the
+    caller's buffer, on the one-pass route and on the two-pass route a data
+    chunk longer than the window takes (the fallback used to keep
+    the bytes it had already decoded)."""
+    sk = H.sha256(b"wipe receiver")
+    pk = ca.encoding.public_key(sk)
+    rng = np.random.default_rng(21)
+    head = rng.integers(0, 256, 500_000, dtype=np.uint8).tobytes()
+    f = ca.encoding.snap(head)
+    tail = rng.integers(0, 256, 300_000, dtype=np.uint8).tobytes()
+    two_pass = bytes(f) + b"\x00" + (300_000).to_bytes(3, "little") + tail  # 300 KB data chunk > 256 KiB window
+    for stream in (bytes(f), two_pass):
+        e = bytearray(ca.encoding.ecies(pk, stream))
+        e[-5] ^= 0x40  # ciphertext of the last chunk: the tag check fails at the end
+        out = np.full(2_000_000, 0xAA, np.uint8)
+        rc, _ = _chip_decode_raw(sk, bytes(e), 3, out, out.size)
+        assert rc == 17  # CHIP_ERR_ECIES
+        assert not (out[:len(head)] == np.frombuffer(head, np.uint8)).all()
+        assert set(np.unique(out).tolist()) <= {0x00, 0xAA}
+        assert (out[:len(head)] == 0).all() or (out[:len(head)] == 0xAA).all()
+
+
+def test_null_output_sizes_without_writing(ca):
+    """out == NULL with a nonzero capacity: BUFFER_TOO_SMALL and the required
+    size, nothing written (the one-pass route dereferenced NULL)."""
+    sk = H.sha256(b"null receiver")
+    pk = ca.encoding.public_key(sk)
+    d = b"carbonado " * 5000
+    e = ca.encoding.ecies(pk, ca.encoding.snap(d))
+    rc, need = _chip_decode_raw(sk, e, 3, None, 1 << 20)
+    assert rc == 2 and need == len(d)  # CHIP_ERR_BUFFER_TOO_SMALL
