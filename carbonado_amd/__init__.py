@@ -6,7 +6,7 @@ Mirrors the reference crate's public surface for this path
 functions in `encoding` / `decoding`.  Compute happens only in
 `lib/libcarbonado_hip.so` (HIP kernels); see DESIGN.md.
 """
-from . import constants, decoding, encoding, error, structs, utils
+from . import constants, decoding, encoding, error, file, structs, utils
 from .constants import FEC_K, FEC_M, HASH_SIZE, SLICE_LEN, Format
 from .decoding import decode, extract_slice, scrub, verify_slice
 from .encoding import encode
@@ -16,5 +16,5 @@ from .structs import EncodeInfo, Encoded
 __all__ = [
     "encode", "decode", "extract_slice", "verify_slice", "scrub", "Encoded", "EncodeInfo", "Format", "CarbonadoError",
     "FEC_K", "FEC_M", "SLICE_LEN", "HASH_SIZE",
-    "constants", "decoding", "encoding", "error", "structs", "utils",
+    "constants", "decoding", "encoding", "error", "file", "structs", "utils",
 ]

@@ -44,6 +44,22 @@ class EciesInjectC(ctypes.Structure):
     _fields_ = [("ephemeral_sk", ctypes.c_void_p), ("nonce", ctypes.c_void_p)]
 
 
+class HeaderC(ctypes.Structure):
+    """chip_header == file.rs:24-43 Header, deserialized."""
+
+    _fields_ = [
+        ("pubkey", ctypes.c_uint8 * 33),
+        ("hash", ctypes.c_uint8 * 32),
+        ("signature", ctypes.c_uint8 * 64),
+        ("format", ctypes.c_uint8),
+        ("chunk_index", ctypes.c_uint8),
+        ("encoded_len", ctypes.c_uint32),
+        ("padding_len", ctypes.c_uint32),
+        ("metadata", ctypes.c_uint8 * 8),
+        ("has_metadata", ctypes.c_uint8),
+    ]
+
+
 # name -> (restype, argtypes); mirrors include/carbonado_hip.h exactly
 SIGNATURES = {
     "chip_abi_version": (ctypes.c_int, []),
@@ -52,6 +68,21 @@ SIGNATURES = {
     "chip_last_device_error": (ctypes.c_char_p, []),
     "chip_device_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "chip_device_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "chip_schnorr_sign": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    "chip_schnorr_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "chip_header_new": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint8, ctypes.c_uint8,
+                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.POINTER(HeaderC)]),
+    "chip_header_to_bytes": (ctypes.c_int, [ctypes.POINTER(HeaderC), ctypes.c_void_p]),
+    "chip_header_parse": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(HeaderC)]),
+    "chip_file_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint8, ctypes.c_void_p,
+                                        ctypes.POINTER(EciesInjectC), ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_uint64, c_u64p, ctypes.POINTER(EncodeInfoC)]),
+    "chip_file_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.POINTER(HeaderC), ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
     "chip_device_alloc_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double)]),
     "chip_torch_alloc": (ctypes.c_void_p, [ctypes.c_ssize_t, ctypes.c_int, ctypes.c_void_p]),

@@ -763,6 +763,9 @@ const char *chip_strerror(int st) {
         case CHIP_ERR_INVALID_SCRUBBED_HASH: return "Scrubbed hash is not equal to original hash.";
         case CHIP_ERR_SNAP: return "snappy framing error";
         case CHIP_ERR_ECIES: return "ecies error";
+        case CHIP_ERR_SECP256K1: return "secp256k1 error (key, message or signature)";
+        case CHIP_ERR_INVALID_HEADER_LENGTH: return "Invalid header length calculation";
+        case CHIP_ERR_INVALID_MAGIC: return "File header lacks Carbonado magic number and may not be a proper Carbonado file.";
         case CHIP_ERR_NO_DEVICE: return "no usable gfx950 device";
         case CHIP_ERR_DEVICE: return "HIP runtime error";
         default: return "unknown status";

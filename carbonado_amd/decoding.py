@@ -73,6 +73,21 @@ def ecies(input, secret_key: bytes) -> bytes:
     return out[: olen.value].tobytes()
 
 
+def decoded_cap(a: np.ndarray, padding: int, fmt: Format) -> int:
+    """Output buffer for decode(): the exact size unless Snappy is on (its
+    size is known only after parsing: a first guess, grown on demand)."""
+    if fmt & Format.Snappy:
+        return a.size * 3 + 1024
+    cap = a.size
+    if fmt & Format.Bao:
+        cap = min(int.from_bytes(a[:8].tobytes(), "little"), a.size) if a.size >= 8 else 0
+    if fmt & Format.Zfec:
+        cap = max((cap // FEC_M) * FEC_K - padding, 0)
+    if fmt & Format.Ecies:
+        cap = max(cap - 97, 0)
+    return cap
+
+
 def _grow_call(fn, cap: int) -> bytes:
     """Call fn(out, cap, olen); on BUFFER_TOO_SMALL retry once with the size
     the library reports (snappy output size is known only after parsing)."""
@@ -104,16 +119,7 @@ def decode(secret_key: bytes, hash: bytes, input, padding: int, format: int) -> 
     h = as_u8(hash)
     sk = as_u8(secret_key)
     fmt = Format(format)
-    if fmt & Format.Snappy:
-        cap = a.size * 3 + 1024
-    else:  # the exact size in the common case: the output becomes the result without a copy
-        cap = a.size
-        if fmt & Format.Bao:
-            cap = min(int.from_bytes(a[:8].tobytes(), "little"), a.size) if a.size >= 8 else 0
-        if fmt & Format.Zfec:
-            cap = max((cap // FEC_M) * FEC_K - padding, 0)
-        if fmt & Format.Ecies:
-            cap = max(cap - 97, 0)
+    cap = decoded_cap(a, padding, fmt)
     return _grow_call(lambda out, c, olen: _lib.lib().chip_decode(
         ptr(sk) if sk.size else None, sk.size, ptr(h), h.size, ptr(a), a.size, padding, int(fmt), out, c,
         ctypes.byref(olen)), cap)

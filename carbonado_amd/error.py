@@ -73,6 +73,23 @@ class EciesError(CarbonadoError):
     status = 17
 
 
+class Secp256k1Error(CarbonadoError):
+    """error.rs:55 NostrSecp256k1Error(secp256k1::Error): bad key, message or
+    Schnorr signature (Header::new / Header::try_from, file.rs:263-289, :116-154)."""
+    status = 18
+
+
+class InvalidHeaderLength(CarbonadoError):
+    """error.rs:113-115 (also a header slice too short to parse, where the
+    reference panics, file.rs:126)"""
+    status = 19
+
+
+class InvalidMagicNumber(CarbonadoError):
+    """error.rs:97-99"""
+    status = 20
+
+
 class UnnecessaryScrub(CarbonadoError):
     """error.rs:65-67"""
     status = 12
@@ -132,6 +149,12 @@ def status_to_error(status: int, detail: str = "") -> CarbonadoError:
         return SnapError("snappy framing error")
     if status == 17:
         return EciesError("ecies error")
+    if status == 18:
+        return Secp256k1Error("secp256k1 error (key, message or signature)")
+    if status == 19:
+        return InvalidHeaderLength("Invalid header length calculation")
+    if status == 20:
+        return InvalidMagicNumber("File header lacks Carbonado magic number and may not be a proper Carbonado file.")
     if status == 12:
         return UnnecessaryScrub()
     if status == 13:

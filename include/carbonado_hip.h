@@ -64,6 +64,7 @@ extern "C" {
 #define CHIP_SLICE_LEN 1024 /* constants.rs:9 SLICE_LEN */
 #define CHIP_FEC_K 4        /* constants.rs:11 FEC_K */
 #define CHIP_FEC_M 8        /* constants.rs:13 FEC_M */
+#define CHIP_HEADER_LEN 160  /* file.rs:257-259 Header::len() */
 
 /* constants.rs:49-56 (bitmask_enum, declaration order) */
 #define CHIP_FORMAT_ECIES 1u
@@ -90,6 +91,9 @@ typedef enum chip_status {
     CHIP_ERR_INVALID_SCRUBBED_HASH = 15,     /* InvalidScrubbedHash             error.rs:81-83 */
     CHIP_ERR_SNAP = 16,              /* snappy framing error: StdIoError / SnapError error.rs:7,35 */
     CHIP_ERR_ECIES = 17,             /* CarbonadoError::EciesError (bad key, bad tag) error.rs:43 */
+    CHIP_ERR_SECP256K1 = 18,         /* secp256k1::Error (bad key / message / signature), error.rs:55 */
+    CHIP_ERR_INVALID_HEADER_LENGTH = 19, /* CarbonadoError::InvalidHeaderLength  error.rs:113-115 */
+    CHIP_ERR_INVALID_MAGIC = 20,     /* CarbonadoError::InvalidMagicNumber    error.rs:97-99 */
     CHIP_ERR_NO_DEVICE = 100,        /* new variant: no usable gfx950 device     */
     CHIP_ERR_DEVICE = 101            /* new variant: HIP runtime error            */
 } chip_status;
@@ -127,6 +131,52 @@ CHIP_API const char *chip_strerror(int status);
 CHIP_API int chip_init(int device);
 /* Last HIP error string seen by this thread (for CHIP_ERR_DEVICE). */
 CHIP_API const char *chip_last_device_error(void);
+
+/* ---- flat-file container (file.rs) -------------------------------------- */
+/* file.rs:24-43 Header, deserialized.  `has_metadata` = Option::Some (the
+ * reference reads eight zero bytes as None, file.rs:379-384). */
+typedef struct chip_header {
+    uint8_t pubkey[33];     /* compressed secp256k1 point */
+    uint8_t hash[32];       /* bao hash */
+    uint8_t signature[64];  /* BIP-340 Schnorr signature over `hash` */
+    uint8_t format;
+    uint8_t chunk_index;
+    uint32_t encoded_len;
+    uint32_t padding_len;
+    uint8_t metadata[8];
+    uint8_t has_metadata;
+} chip_header;
+/* BIP-340 over secp256k1 (secp256k1 0.28 Keypair::sign_schnorr, used by
+ * Header::new file.rs:269-271).  aux = 32 bytes of auxiliary randomness, or
+ * NULL for fresh random bytes (the reference draws them from thread_rng). */
+CHIP_API int chip_schnorr_sign(const uint8_t *sk, uint64_t sk_len, const uint8_t *msg32, const uint8_t *aux32,
+                               uint8_t *sig64);
+/* pubkey: 32-byte x-only, 33-byte compressed or 65-byte uncompressed. */
+CHIP_API int chip_schnorr_verify(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *msg32,
+                                 const uint8_t *sig64);
+/* Header::new (file.rs:263-289): signs `hash` with `sk`, stores `pk` (33 or
+ * 65 bytes; kept compressed).  metadata: 8 bytes or NULL (None). */
+CHIP_API int chip_header_new(const uint8_t *sk, uint64_t sk_len, const uint8_t *pk, uint64_t pk_len,
+                             const uint8_t *hash, uint64_t hash_len, uint8_t format, uint8_t chunk_index,
+                             uint32_t encoded_len, uint32_t padding_len, const uint8_t *metadata8,
+                             const uint8_t *aux32, chip_header *out);
+/* Header::try_to_vec (file.rs:292-335): CHIP_HEADER_LEN bytes. */
+CHIP_API int chip_header_to_bytes(const chip_header *h, uint8_t *out160);
+/* Header::try_from(&[u8]) (file.rs:116-154): magic, pubkey, signature check.
+ * A slice shorter than the parsed 159 bytes is CHIP_ERR_INVALID_HEADER_LENGTH
+ * (the reference panics, file.rs:126). */
+CHIP_API int chip_header_parse(const uint8_t *bytes, uint64_t len, chip_header *out);
+/* file::encode (file.rs:409-440): header || encode(pubkey, input, level);
+ * pk NULL/0 = derived from sk.  Randomness: `inject` (ECIES) and `aux32`
+ * (signature) or NULL for fresh values.  Needs CHIP_HEADER_LEN +
+ * chip_encode_max_len(n) bytes (a short buffer reports that in *out_len). */
+CHIP_API int chip_file_encode(const uint8_t *sk, uint64_t sk_len, const uint8_t *pk, uint64_t pk_len,
+                              const uint8_t *in, uint64_t n, uint8_t level, const uint8_t *metadata8,
+                              const chip_ecies_inject *inject, const uint8_t *aux32, uint8_t *out, uint64_t out_cap,
+                              uint64_t *out_len, chip_encode_info *info);
+/* file::decode (file.rs:395-407): parse + verify the header, then decode(). */
+CHIP_API int chip_file_decode(const uint8_t *sk, uint64_t sk_len, const uint8_t *in, uint64_t n, chip_header *hdr,
+                              uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 
 /* ---- batch buffers ------------------------------------------------------ */
 /* Device memory for batch buffers.  From 1 GiB up it is class-balanced:

@@ -550,3 +550,93 @@ def host_decode(data: bytes, fmt: int, secret: bytes | None = None) -> bytes:
     if fmt & 2:
         cur = snap_decompress(cur)
     return cur
+
+
+# ---------------------------------------------------------------- BIP-340 + header
+# The flat-file container (reference src/file.rs): Header::new signs the bao
+# hash with secp256k1 0.28's Keypair::sign_schnorr (file.rs:263-289), i.e.
+# BIP-340 with 32 bytes of auxiliary randomness from thread_rng; parsing
+# verifies it against the x-only key of the stored pubkey (file.rs:129-131).
+# Restated from the BIP-340 specification (tagged hashes, even-y keys and
+# nonces), pinned by its published test vectors in tests/golden/host_kat.json.
+MAGICNO = b"CARBONADO01\n"  # constants.rs:4
+HEADER_LEN = 160            # file.rs:257-259
+
+
+def tagged_hash(tag: str, msg: bytes) -> bytes:
+    th = sha256(tag.encode())
+    return sha256(th + th + msg)
+
+
+def _lift_x(x: int):
+    if x >= P:
+        return None
+    c = (pow(x, 3, P) + 7) % P
+    y = pow(c, (P + 1) // 4, P)
+    if y * y % P != c:
+        return None
+    return x, (y if y % 2 == 0 else P - y)
+
+
+def schnorr_sign(sk: bytes, msg: bytes, aux: bytes) -> bytes:
+    d0 = int.from_bytes(sk, "big")
+    if len(sk) != 32 or not 0 < d0 < N or len(aux) != 32:
+        raise ValueError("bad secret key")
+    pub = point_mul(d0)
+    d = d0 if pub[1] % 2 == 0 else N - d0
+    t = bytes(a ^ b for a, b in zip(d.to_bytes(32, "big"), tagged_hash("BIP0340/aux", aux)))
+    px = pub[0].to_bytes(32, "big")
+    k0 = int.from_bytes(tagged_hash("BIP0340/nonce", t + px + msg), "big") % N
+    if k0 == 0:
+        raise ValueError("nonce is zero")
+    r = point_mul(k0)
+    k = k0 if r[1] % 2 == 0 else N - k0
+    rx = r[0].to_bytes(32, "big")
+    e = int.from_bytes(tagged_hash("BIP0340/challenge", rx + px + msg), "big") % N
+    return rx + ((k + e * d) % N).to_bytes(32, "big")
+
+
+def schnorr_verify(pkx: bytes, msg: bytes, sig: bytes) -> bool:
+    pt = _lift_x(int.from_bytes(pkx, "big"))
+    if pt is None or len(sig) != 64:
+        return False
+    r, s = int.from_bytes(sig[:32], "big"), int.from_bytes(sig[32:], "big")
+    if r >= P or s >= N:
+        return False
+    e = int.from_bytes(tagged_hash("BIP0340/challenge", sig[:32] + pkx + msg), "big") % N
+    big_r = _add(point_mul(s), point_mul(N - e, pt) if e else None)
+    return big_r is not None and big_r[1] % 2 == 0 and big_r[0] == r
+
+
+def ser_compressed(pt) -> bytes:
+    return bytes([2 + (pt[1] & 1)]) + pt[0].to_bytes(32, "big")
+
+
+def header_bytes(sk: bytes, pk: bytes, hash32: bytes, fmt: int, chunk_index: int, encoded_len: int,
+                 padding_len: int, metadata: bytes | None, aux: bytes) -> bytes:
+    """Header::new + Header::try_to_vec (file.rs:263-335)."""
+    if len(hash32) != 32:
+        raise ValueError("message must be 32 bytes")
+    pub = parse_pubkey(pk)
+    sig = schnorr_sign(sk, hash32, aux)
+    out = (MAGICNO + ser_compressed(pub) + hash32 + sig + bytes([fmt, chunk_index]) +
+           encoded_len.to_bytes(4, "little") + padding_len.to_bytes(4, "little") +
+           (metadata if metadata is not None else bytes(8)) + b"\x00")
+    assert len(out) == HEADER_LEN
+    return out
+
+
+def header_parse(b: bytes) -> dict:
+    """Header::try_from(&[u8]) (file.rs:116-154): magic, pubkey, signature."""
+    if len(b) < HEADER_LEN - 1:
+        raise ValueError("InvalidHeaderLength")
+    if b[:12] != MAGICNO:
+        raise ValueError("InvalidMagicNumber")
+    pub = parse_pubkey(b[12:45])
+    h, sig = b[45:77], b[77:141]
+    if not schnorr_verify(pub[0].to_bytes(32, "big"), h, sig):
+        raise ValueError("signature")
+    meta = b[151:159]
+    return {"pubkey": b[12:45], "hash": h, "signature": sig, "format": b[141], "chunk_index": b[142],
+            "encoded_len": int.from_bytes(b[143:147], "little"), "padding_len": int.from_bytes(b[147:151], "little"),
+            "metadata": meta if any(meta) else None}

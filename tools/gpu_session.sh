@@ -1,0 +1,35 @@
+#!/bin/bash
+# A GPU session of named steps, each under its own time limit, stopping at
+# the first failure.  bash tools/gpu_session.sh TAG step...
+#   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 e2e15 e2e15full
+#          e2e12 e2ed15 scrub hasher file15 file12 prof
+set -e -o pipefail
+TAG=$1; shift
+O=$PWD/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+run() { local name=$1 lim=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; }
+for s in "$@"; do
+  case $s in
+    tests) run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    encode) run bench_encode 600 python3 bench.py ;;
+    decode) run bench_decode 600 python3 bench.py --config cfg3 --no-cpu-baseline ;;
+    8of16) run bench_8of16 600 python3 bench.py --config cfg5 --no-cpu-baseline ;;
+    2rank) run bench_2rank_one_gpu 600 python3 bench.py --gpus 2 --objects 256 --no-cpu-baseline ;;
+    bao) run bench_bao 600 python3 bench.py --mode bao --no-cpu-baseline ;;
+    baodec) run bench_bao_decode 600 python3 bench.py --mode bao-decode --cpu-seconds 8 ;;
+    pipe12) run bench_pipe12 600 python3 bench.py --mode pipeline --level 12 --verify-all ;;
+    e2e15) run bench_e2e15 600 python3 bench.py --mode e2e --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    e2e15full) run bench_e2e15_full 900 python3 bench.py --config cfg4 --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    e2e12) run bench_e2e12 600 python3 bench.py --mode e2e --level 12 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    e2ed15) run bench_e2ed15 600 python3 bench.py --mode e2e-decode --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    scrub) run bench_scrub 600 python3 bench.py --mode scrub --steps 2 --warmup 1 --cpu-seconds 8 ;;
+    hasher) run bench_hasher 600 python3 bench.py --mode hasher --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    file15) run bench_file15 600 python3 bench.py --mode file --level 15 --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    file12) run bench_file12 600 python3 bench.py --mode file --level 12 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    prof) bash tools/gpu_prof.sh $TAG ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done > $O/done
