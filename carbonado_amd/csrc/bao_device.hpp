@@ -843,7 +843,7 @@ struct CheckArgs {
 // the copy in its own parent (the root: with the hash).  Independent per node,
 // so one launch checks the whole tree; flags are indexed in stream order,
 // pidx = P(s) + c(s) - level.
-__global__ __launch_bounds__(256) void bao_parent_check_kernel(CheckArgs a) {
+static __global__ __launch_bounds__(256) void bao_parent_check_kernel(CheckArgs a) {
     const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (gid >= a.count * a.nparents) return;
     const uint64_t obj = gid / a.nparents;
@@ -892,6 +892,39 @@ inline uint64_t bao_scratch_len_t(uint64_t n, uint64_t count) {
     return count * 32 * (N0 + (N0 + 1) / 2);
 }
 
+// The tree above a level of node CVs: K4 per level, then K4t for the top
+// once a level has <= K4T_MAX nodes.  cv_prev [count][stride_prev] holds the
+// cnt_prev nodes of level `level - 1`; cv_next (stride_next >= ceil(cnt_prev/2))
+// is the ping-pong buffer.  Parents are written into (MODE 0) or checked
+// against (MODE 1) the streams, the root into / against d_hash.
+template <int MODE, bool BAO_NTS>
+hipError_t run_parent_levels(uint8_t *cv_prev, uint64_t stride_prev, uint64_t cnt_prev, int level, uint8_t *cv_next,
+                             uint64_t stride_next, uint64_t N, uint64_t count, uint8_t *stream_buf, uint64_t sstride,
+                             uint8_t *d_hash, uint32_t *d_status, hipStream_t stream) {
+    uint8_t *prev = cv_prev, *next = cv_next;
+    uint64_t sp = stride_prev, sn = stride_next;
+    for (; cnt_prev > 1; ++level) {
+        ParentArgs pa;
+        pa.cv_prev = prev; pa.cv_next = next; pa.stride_prev = sp; pa.stride_next = sn;
+        pa.cnt_prev = cnt_prev; pa.cnt = (cnt_prev + 1) / 2; pa.level = level;
+        pa.N = N; pa.count = count; pa.stream = stream_buf; pa.stream_stride = sstride;
+        pa.hash = d_hash; pa.status = d_status;
+        if (cnt_prev <= (uint64_t)K4T_MAX && count <= 0x7fffffffull) {  // the rest of the tree, one launch
+            hipLaunchKernelGGL((bao_top_kernel<MODE, BAO_NTS>), dim3((unsigned)count), dim3(256), 0, stream, pa);
+            return hipGetLastError();
+        }
+        const uint64_t work = count * pa.cnt;
+        hipLaunchKernelGGL((bao_parent_kernel<MODE, BAO_NTS>), dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                           stream, pa);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        cnt_prev = pa.cnt;
+        std::swap(prev, next);
+        std::swap(sp, sn);
+    }
+    return hipSuccess;
+}
+
 // Enqueue K3 then one K4 launch per remaining level.
 template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0>
 hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
@@ -919,34 +952,13 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
 
     uint8_t *stream_buf = (MODE == 0 || MODE == 3) ? d_out : const_cast<uint8_t *>(d_in);
     const uint64_t sstride = (MODE == 0 || MODE == 3) ? out_stride : in_stride;
-    uint8_t *prev = bufA, *next = bufB;
-    uint64_t sp = strideA, sn = strideB, cnt_prev = N0;
-    for (int level = LOG + 1; cnt_prev > 1; ++level) {
-        ParentArgs pa;
-        pa.cv_prev = prev; pa.cv_next = next; pa.stride_prev = sp; pa.stride_next = sn;
-        pa.cnt_prev = cnt_prev; pa.cnt = (cnt_prev + 1) / 2; pa.level = level;
-        pa.N = N; pa.count = count; pa.stream = stream_buf; pa.stream_stride = sstride;
-        pa.hash = d_hash; pa.status = d_status;
-        if (cnt_prev <= (uint64_t)K4T_MAX && count <= 0x7fffffffull) {  // the rest of the tree, one launch
-            hipLaunchKernelGGL((bao_top_kernel<MODE == 3 ? 0 : MODE, BAO_NTS>), dim3((unsigned)count), dim3(256), 0,
-                               stream, pa);
-            return hipGetLastError();
-        }
-        const uint64_t work = count * pa.cnt;
-        hipLaunchKernelGGL((bao_parent_kernel<MODE == 3 ? 0 : MODE, BAO_NTS>), dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
-                           stream, pa);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        cnt_prev = pa.cnt;
-        std::swap(prev, next);
-        std::swap(sp, sn);
-    }
-    return hipSuccess;
+    return run_parent_levels<MODE == 3 ? 0 : MODE, BAO_NTS>(bufA, strideA, N0, LOG + 1, bufB, strideB, N, count,
+                                                           stream_buf, sstride, d_hash, d_status, stream);
 }
 
 // Gather the content of chunks [c0, c1) of one stream into a contiguous buffer
 // (the inverse of the layout: strips the interleaved parent nodes).
-__global__ __launch_bounds__(256) void bao_gather_kernel(const uint8_t *stream, uint64_t n, uint64_t N,
+static __global__ __launch_bounds__(256) void bao_gather_kernel(const uint8_t *stream, uint64_t n, uint64_t N,
                                                          uint64_t c0, uint64_t c1, uint8_t *out) {
     const uint64_t bytes = (c1 * 1024 < n ? c1 * 1024 : n) - c0 * 1024;
     for (uint64_t b = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; b < bytes;

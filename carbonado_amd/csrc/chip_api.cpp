@@ -521,9 +521,18 @@ int pipe_wg_cfg() {
     return w;
 }
 
+// K13 (fused_device.hpp) by default: the shards are hashed while they are on
+// chip instead of read back from HBM; CHIP_FUSED=0 runs the two-kernel
+// overlapped pipeline below (A/B runs).  Scratch: zfec_bao_scratch_len.
+bool fused_on() {
+    static const bool on = env_int("CHIP_FUSED", 1) != 0;
+    return on;
+}
+
 hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
                         uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s) {
     const uint64_t zlen = (uint64_t)CHIP_FEC_M * C;
+    if (fused_on()) return zfec_bao_fused_dev(d_in, in_stride, n, count, C, d_out, out_stride, d_hash, d_scratch, s);
     const uint64_t *tab = nullptr;
     hipError_t e = bao_chunk_table(zlen / 1024, &tab);
     if (e != hipSuccess) return e;
@@ -1094,6 +1103,8 @@ uint64_t chip_encode_scratch_len(uint8_t format, uint64_t n, uint64_t count) {
     chip_encode_info inf;
     uint64_t zlen, fl;
     if (encode_info_for(format, n, n, 0, 0, &inf, &zlen, &fl) != CHIP_OK) return 16;
+    if ((format & CHIP_FORMAT_BAO) && (format & CHIP_FORMAT_ZFEC))  // fused K13: level-0 CVs of every chunk
+        return std::max(zfec_bao_scratch_len(zlen, count), bao_scratch_len(zlen, count)) + 16;
     return (format & CHIP_FORMAT_BAO) ? bao_scratch_len(zlen, count) + 16 : 16;
 }
 
@@ -1442,7 +1453,7 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
         const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
         if (zfec && bao && cur_len) {  // fused: shards written into the bao stream, hashed in place
             CHIP_HIP(grow(c->out, final_len));
-            CHIP_HIP(grow(c->scratch, bao_scratch_len(cur_len, 1)));
+            CHIP_HIP(grow(c->scratch, std::max(zfec_bao_scratch_len(cur_len, 1), bao_scratch_len(cur_len, 1))));
             CHIP_HIP(grow(c->small, 64));
             uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
             CHIP_HIP(zfec_bao_dev(d_cur, 0, cur_n, 1, inf.chunk_len, static_cast<uint8_t *>(c->out.p), 0, d_hash,
@@ -1581,7 +1592,8 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             if (zfec && !bao) CHIP_HIP(grow(sl.mid, S * ((zlen_max + 15) / 16 * 16)));  // Zfec|Bao: fused
             if (bao) {
                 CHIP_HIP(grow(sl.out, S * ((final_max + 15) / 16 * 16)));
-                CHIP_HIP(grow(sl.scratch, bao_scratch_len(zlen_max, S)));
+                CHIP_HIP(grow(sl.scratch, zfec ? std::max(zfec_bao_scratch_len(zlen_max, S), bao_scratch_len(zlen_max, S))
+                                                : bao_scratch_len(zlen_max, S)));
             }
             CHIP_HIP(grow(sl.hash, S * 32));
             if (hs) CHIP_HIP(grow_pinned(sl.stage, S * h_al));

@@ -63,6 +63,18 @@ struct GfLaunch {
 // Plans with more than ZF_MAXP computed rows run in passes of ZF_MAXP rows
 // (copies ride on the first pass); k > ZF_MAXK uses the generic kernel.
 hipError_t gf_apply(const GfPlan &plan, const GfLaunch &L, hipStream_t stream);
+// Device copy of the packed parity table of a k-of-m encode (m - k <= 4):
+// [k][256] dwords, byte r of entry [s][x] = E[k + r][s] * x (cached).
+hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out);
+
+// ---- K13: encode() at Zfec|Bao in one pass (fused_kernels.hip) ----------
+// `count` objects of n bytes (zero padded to 4C) -> bao streams of their
+// 4-of-8 zfec outputs (8C bytes each) + root hashes; scratch of
+// zfec_bao_scratch_len(8C, count) bytes (level-0 CVs + one tree level).
+uint64_t zfec_bao_scratch_len(uint64_t zlen, uint64_t count);
+hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
+                              uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,
+                              hipStream_t stream);
 
 // ---- bao / BLAKE3 ------------------------------------------------------
 uint64_t bao_encoded_len(uint64_t n);

@@ -1,0 +1,238 @@
+// fused_device.hpp — K13: encode() at Zfec|Bao in one pass (gfx950).
+//
+// encode() level 12 (encoding.rs:121-147) is zfec 4-of-8 of the object
+// followed by bao over the zfec output.  Done as two kernels (K1-BL writes
+// the shards into their chunk slots, K3 reads them back and hashes them) the
+// 32 MiB of shards per 16 MiB object cross HBM twice.  Here one wave
+// computes the shards of 8 consecutive chunk-columns and hashes the 64
+// resulting chunks while they are still on chip:
+//
+//  * a wave's block = chunk-columns [ub, ub + 8) of one object = chunks
+//    (shard sh, column u) for 8 shards x 8 columns.  The 8 steps of a block
+//    each cover 128 B of every chunk.
+//  * GF role (per step): lane (cu = lane/8, g = lane%8) loads 16 B of each of
+//    the 4 data shards at column ub + cu, bytes 128 s + 16 g (coalesced: 8
+//    lanes = one 128-B line), computes the 4 parity 16-B pieces with the
+//    packed LDS table (one ds_read_b32 per input byte gives all 4 parity
+//    products, as K1) and writes the 8 pieces into the LDS rows of chunks
+//    (sh, cu) at word 4 g of the step's half-row.  The next step's loads are
+//    issued before the hashing (the next block's first step at the last step).
+//  * store role: the 8 lanes of group cu store the stream lines of chunks
+//    (t, cu), t = 0..7, whole 128-B memory lines read back from the rows (the
+//    rows hold two steps, so the line ending at chunk byte d + 128 s is
+//    complete at step s; bao K3 SP 3's path).
+//  * hash role: lane L hashes row L = chunk (L/8, ub + L%8), two BLAKE3
+//    compressions per step; after 8 steps its chunk CV goes to the level-0
+//    CV buffer, from which the parent kernels (K4, K4t) build the tree and
+//    write the parent nodes into the stream.
+//
+// HBM traffic per 16 MiB object: 16 MiB read + 32 MiB of chunk lines + the
+// parents (2 MiB) and the 1 MiB of level-0 CVs written and read once — about
+// 52 MiB against 84 MiB for K1-BL + K3.  The kernel is VALU-bound: 16
+// compressions per chunk (672 lane-ops each) plus ~250 lane-ops of GF work
+// per step.
+#pragma once
+
+#include "bao_device.hpp"
+#include "zfec_device.hpp"
+
+namespace chip {
+namespace fused {
+
+using bao::u32x2;
+using bao::u32x4;
+
+constexpr int FW = 8;               // waves per workgroup
+constexpr int FTPB = 64 * FW;
+constexpr int FR = 4;               // replicas of the GF table (4 data shards x FR dwords per byte value)
+constexpr int RW = 68;              // LDS words per chunk row: [pad 4 | even step 32 | odd step 32]
+constexpr size_t TAB_BYTES = 256 * 4 * FR * 4;
+constexpr size_t LDS_BYTES = TAB_BYTES + (size_t)FW * 64 * RW * 4;  // 16 KiB + 136 KiB
+
+struct FusedArgs {
+    const uint8_t *in;
+    uint64_t in_stride, valid, C;   // objects, bytes of data per object (zero beyond), shard length
+    uint8_t *out;
+    uint64_t out_stride;            // bao streams of the 8C-byte zfec outputs
+    uint64_t count, N, cols, bpo;   // objects, chunks per stream, chunk-columns per shard, blocks per object
+    const uint32_t *table;          // [4][256] packed parity products (4 parity rows per dword)
+    const uint64_t *coff;           // [N] stream offset of each chunk (bao_chunk_table)
+    uint8_t *cv;                    // [count][N] level-0 chunk CVs, 32 B each
+};
+
+__device__ __forceinline__ int dofs(int step) { return 4 + (step & 1) * 32; }
+
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
+    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    else *reinterpret_cast<u32x4 *>(p) = v;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    {  // table: lds[x][s][r] = T_s[x], FR replicas
+        uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
+        for (int i = threadIdx.x; i < 256 * 4 * FR; i += FTPB) {
+            const int x = i / (4 * FR);
+            const int s = (i - x * (4 * FR)) / FR;
+            dst[i] = a.table[s * 256 + x];
+        }
+    }
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    uint32_t *rows = reinterpret_cast<uint32_t *>(lds + TAB_BYTES) + wave * 64 * RW;
+    constexpr int ROWB = 4 * FR * 4;  // table bytes per byte value
+    const int rep = lane % FR, grp = (lane & 31) / FR;
+    uint32_t tb[4];
+    uint64_t ioff[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // lane group grp walks the data shards in the rotated order (j + grp) mod 4
+        tb[j] = (uint32_t)((((j + grp) & 3) * FR + rep) * 4);
+        ioff[j] = (uint64_t)((j + grp) & 3) * a.C;
+    }
+    const int gl = lane & 7, cu = lane >> 3;
+    const uint64_t total = a.count * a.bpo;
+    const uint64_t GW = (uint64_t)gridDim.x * FW;
+
+    auto load_step = [&](uint64_t blk, int s, u32x4 (&v)[4]) {
+        const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * 8;
+        const bool col = ub + cu < a.cols;
+        const uint8_t *ib = a.in + obj * a.in_stride;
+        const uint64_t off = (ub + cu) * 1024 + 128 * (uint64_t)s + 16 * gl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = col ? zf::load16_masked(ib, ioff[j] + off, a.valid) : u32x4{0u, 0u, 0u, 0u};
+    };
+
+    uint64_t blk = (uint64_t)blockIdx.x * FW + wave;
+    u32x4 v[4];
+    if (blk < total) load_step(blk, 0, v);
+    for (; blk < total; blk += GW) {
+        const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * 8;
+        uint8_t *ob = a.out + obj * a.out_stride;
+        if (ub == 0 && lane == 0) *reinterpret_cast<uint64_t *>(ob) = 8 * a.C;  // u64 LE content length
+        const bool gcol = ub + cu < a.cols;                 // store role: chunks (t, ub + cu)
+        const uint64_t hu = ub + (lane & 7);                // hash role: chunk (lane / 8, hu)
+        const bool mine = hu < a.cols;
+        const uint64_t ci = (uint64_t)(lane >> 3) * a.cols + hu;
+        uint8_t *lsp[8];
+        uint32_t ldd[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            lsp[t] = gcol ? ob + a.coff[(uint64_t)t * a.cols + ub + cu] : ob;
+            ldd[t] = (uint32_t)(-(uintptr_t)lsp[t]) & 127u;
+        }
+        uint32_t h[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) h[w] = bao::IV(w);
+
+        for (int s = 0; s < 8; ++s) {
+            // ---- GF role: 8 pieces of 16 B into the rows of chunks (sh, cu) ----
+            uint32_t acc[16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t x = zf::comp(v[j], d);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const uint32_t e =
+                            *reinterpret_cast<const uint32_t *>(lds + ((x >> (8 * b)) & 0xFFu) * ROWB + tb[j]);
+                        if (j == 0) acc[d * 4 + b] = e;
+                        else acc[d * 4 + b] ^= e;
+                    }
+                }
+            }
+            const int wo = dofs(s) + 4 * gl;
+#pragma unroll
+            for (int sh = 0; sh < 4; ++sh) {  // data shard sh sits in v[(sh - grp) mod 4]
+                const int jj = (sh - grp) & 3;
+                u32x4 x = v[0];
+#pragma unroll
+                for (int j = 1; j < 4; ++j)
+                    if (jj == j) x = v[j];
+                *reinterpret_cast<u32x4 *>(rows + (sh * 8 + cu) * RW + wo) = x;
+            }
+            {
+                u32x4 p[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    uint32_t r0, r1, r2, r3;
+                    zf::transpose4(acc[d * 4 + 0], acc[d * 4 + 1], acc[d * 4 + 2], acc[d * 4 + 3], r0, r1, r2, r3);
+                    if (d == 0) { p[0].x = r0; p[1].x = r1; p[2].x = r2; p[3].x = r3; }
+                    if (d == 1) { p[0].y = r0; p[1].y = r1; p[2].y = r2; p[3].y = r3; }
+                    if (d == 2) { p[0].z = r0; p[1].z = r1; p[2].z = r2; p[3].z = r3; }
+                    if (d == 3) { p[0].w = r0; p[1].w = r1; p[2].w = r2; p[3].w = r3; }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) *reinterpret_cast<u32x4 *>(rows + ((4 + q) * 8 + cu) * RW + wo) = p[q];
+            }
+            // next loads in flight during the stores and the compressions
+            if (s < 7) load_step(blk, s + 1, v);
+            else if (blk + GW < total) load_step(blk + GW, 0, v);
+            bao::wave_sync();
+
+            // ---- store role: whole 128-B memory lines of chunks (t, cu) ----
+            if (gcol) {
+                auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x
+                    return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
+                };
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    uint8_t *sp = lsp[t];
+                    const uint32_t d = ldd[t];
+                    const uint32_t *row = rows + (t * 8 + cu) * RW;
+                    if (s >= 1) {  // the whole line [d + 128 (s-1), d + 128 s)
+                        const uint32_t x = d + 128u * (s - 1) + 16u * gl;
+                        const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                        st16<NT>(sp + x, u32x4{lo.x, lo.y, hi.x, hi.y});
+                    } else {  // head [0, d)
+                        const uint32_t hd = d & 8u;
+                        if (hd && gl == 0) *reinterpret_cast<u32x2 *>(sp) = piece(row, 0);
+                        const uint32_t x = 16u * gl + hd;
+                        if (x + 16 <= d) {
+                            const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                            *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                        }
+                    }
+                    if (s == 7) {  // tail [896 + d, 1024)
+                        const uint32_t x = 896u + d + 16u * gl;
+                        if (x + 16 <= 1024) {
+                            const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                            *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                        } else if (x + 8 == 1024) {
+                            *reinterpret_cast<u32x2 *>(sp + x) = piece(row, x);
+                        }
+                    }
+                }
+            }
+
+            // ---- hash role: blocks 2s, 2s+1 of my chunk ----
+            if (mine) {
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    uint32_t m[16];
+                    const u32x4 *r = reinterpret_cast<const u32x4 *>(rows + lane * RW + dofs(s) + hh * 16);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const u32x4 x = r[q];
+                        m[4 * q] = x.x; m[4 * q + 1] = x.y; m[4 * q + 2] = x.z; m[4 * q + 3] = x.w;
+                    }
+                    const int b = 2 * s + hh;
+                    const uint32_t flags = (b == 0 ? bao::F_CHUNK_START : 0u) | (b == 15 ? bao::F_CHUNK_END : 0u);
+                    bao::b3_compress(h, m, ci, 64, flags);
+                }
+            }
+            bao::wave_sync();
+        }
+        if (mine) {
+            u32x4 *cvp = reinterpret_cast<u32x4 *>(a.cv + (obj * a.N + ci) * 32);
+            cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
+            cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
+        }
+    }
+}
+
+}  // namespace fused
+}  // namespace chip

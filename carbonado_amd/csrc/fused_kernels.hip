@@ -1,0 +1,51 @@
+// fused_kernels.hip — host side of K13 (fused_device.hpp): encode() at
+// Zfec|Bao as one zfec+hash pass, then the parent levels (K4 / K4t).
+#include "chip_internal.hpp"
+#include "fused_device.hpp"
+
+namespace chip {
+
+uint64_t zfec_bao_scratch_len(uint64_t zlen, uint64_t count) {
+    const uint64_t N = bao::n_chunks(zlen);
+    return count * 32 * (N + (N + 1) / 2);
+}
+
+hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
+                              uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,
+                              hipStream_t stream) {
+    if (count == 0) return hipSuccess;
+    if (C == 0 || C % 1024) return hipErrorInvalidValue;
+    using namespace fused;
+    FusedArgs a;
+    a.in = d_in; a.in_stride = in_stride; a.valid = n; a.C = C;
+    a.out = d_out; a.out_stride = out_stride;
+    a.count = count;
+    a.cols = C / 1024;
+    a.N = 8 * a.cols;
+    a.bpo = (a.cols + 7) / 8;
+    const void *tab = nullptr;
+    hipError_t e = zfec_parity_table(4, 8, &tab);
+    if (e != hipSuccess) return e;
+    a.table = static_cast<const uint32_t *>(tab);
+    const uint64_t *coff = nullptr;
+    if ((e = bao_chunk_table(a.N, &coff)) != hipSuccess) return e;
+    a.coff = coff;
+    a.cv = static_cast<uint8_t *>(d_scratch);
+    static bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES) == hipSuccess;
+    }();
+    (void)attr;
+    (void)hipGetLastError();
+    const uint64_t blocks = count * a.bpo;
+    uint64_t grid = (blocks + FW - 1) / FW;
+    const uint64_t cap = (uint64_t)num_cus();  // one workgroup (8 waves) per CU fits the LDS
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(zfec_bao_fused_kernel<false>, dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint8_t *next = a.cv + count * a.N * 32;
+    return bao::run_parent_levels<0, false>(a.cv, a.N, a.N, 1, next, (a.N + 1) / 2, a.N, count, d_out, out_stride,
+                                            d_hash, nullptr, stream);
+}
+
+}  // namespace chip

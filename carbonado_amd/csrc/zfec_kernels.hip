@@ -350,6 +350,16 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
 
 }  // namespace
 
+hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out) {
+    if (k == 0 || m <= k || m - k > 4) return hipErrorInvalidValue;
+    const std::vector<uint8_t> enc = zfec_enc_matrix(k, m);
+    GfPlan p;
+    p.k = k;
+    p.np = m - k;
+    p.coef.assign(enc.begin() + (size_t)k * k, enc.end());
+    return device_table(p, 1, out);
+}
+
 hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
     if (L.count == 0 || L.C == 0) return hipSuccess;
     if (p.k > (uint32_t)ZF_MAXK) return apply_generic(p, L, stream);

@@ -20,6 +20,7 @@ for s in "$@"; do
     bao) run bench_bao 600 python3 bench.py --mode bao --no-cpu-baseline ;;
     baodec) run bench_bao_decode 600 python3 bench.py --mode bao-decode --cpu-seconds 8 ;;
     pipe12) run bench_pipe12 600 python3 bench.py --mode pipeline --level 12 --verify-all ;;
+    pipe12old) CHIP_FUSED=0 run bench_pipe12_twokernel 600 python3 bench.py --mode pipeline --level 12 --no-cpu-baseline ;;
     e2e15) run bench_e2e15 600 python3 bench.py --mode e2e --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     e2e15full) run bench_e2e15_full 900 python3 bench.py --config cfg4 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     e2e12) run bench_e2e12 600 python3 bench.py --mode e2e --level 12 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 ;;
