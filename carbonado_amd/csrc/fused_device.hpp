@@ -16,7 +16,8 @@
 //    packed LDS table (one ds_read_b32 per input byte gives all 4 parity
 //    products, as K1) and writes the 8 pieces into the LDS rows of chunks
 //    (sh, cu) at word 4 g of the step's half-row.  The next step's loads are
-//    issued before the hashing (the next block's first step at the last step).
+//    issued after the stores, before the hashing (the next block's first
+//    step at the last step), so they land while the lane compresses.
 //  * store role: the 8 lanes of group cu store the stream lines of chunks
 //    (t, cu), t = 0..7, whole 128-B memory lines read back from the rows (the
 //    rows hold two steps, so the line ending at chunk byte d + 128 s is
@@ -68,7 +69,11 @@ __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
     else *reinterpret_cast<u32x4 *>(p) = v;
 }
 
-template <bool NT>
+// DG: diagnostics for tools/fused_tune (wrong output): 1 = no line stores,
+// 2 = no hashing, 3 = no GF (rows get the data shards only), 4 = neither
+// stores nor hashing, 5 = every chunk's lines 128-B aligned (no partial
+// lines), 6 = 5 without hashing.
+template <bool NT, int DG = 0>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     {  // table: lds[x][s][r] = T_s[x], FR replicas
@@ -96,13 +101,24 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     const uint64_t total = a.count * a.bpo;
     const uint64_t GW = (uint64_t)gridDim.x * FW;
 
+    // Loads of a step.  A block whose input columns all lie below `valid`
+    // (every block of an object without zfec padding) takes plain loads whose
+    // wait the compiler can defer to the first use; the masked form (a branch
+    // and an immediate wait per load) only runs in an object's last blocks.
     auto load_step = [&](uint64_t blk, int s, u32x4 (&v)[4]) {
         const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * 8;
-        const bool col = ub + cu < a.cols;
         const uint8_t *ib = a.in + obj * a.in_stride;
         const uint64_t off = (ub + cu) * 1024 + 128 * (uint64_t)s + 16 * gl;
+        const bool full = ub + 8 <= a.cols && 3 * a.C + (ub + 8) * 1024 <= a.valid;  // wave-uniform
+        if (full) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = col ? zf::load16_masked(ib, ioff[j] + off, a.valid) : u32x4{0u, 0u, 0u, 0u};
+            for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const u32x4 *>(ib + ioff[j] + off);
+        } else {
+            const bool col = ub + cu < a.cols;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                v[j] = col ? zf::load16_masked(ib, ioff[j] + off, a.valid) : u32x4{0u, 0u, 0u, 0u};
+        }
     };
 
     uint64_t blk = (uint64_t)blockIdx.x * FW + wave;
@@ -118,10 +134,17 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         const uint64_t ci = (uint64_t)(lane >> 3) * a.cols + hu;
         uint8_t *lsp[8];
         uint32_t ldd[8];
+        {
+            uint64_t co[8];  // all 8 offset loads in flight together
+            const uint64_t c0 = gcol ? ub + cu : 0;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            lsp[t] = gcol ? ob + a.coff[(uint64_t)t * a.cols + ub + cu] : ob;
-            ldd[t] = (uint32_t)(-(uintptr_t)lsp[t]) & 127u;
+            for (int t = 0; t < 8; ++t) co[t] = a.coff[(uint64_t)t * a.cols + c0];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                lsp[t] = ob + co[t];
+                if (DG == 5 || DG == 6) lsp[t] = reinterpret_cast<uint8_t *>((uintptr_t)lsp[t] & ~(uintptr_t)127);
+                ldd[t] = (DG == 5 || DG == 6) ? 0u : (uint32_t)(-(uintptr_t)lsp[t]) & 127u;
+            }
         }
         uint32_t h[8];
 #pragma unroll
@@ -130,6 +153,10 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         for (int s = 0; s < 8; ++s) {
             // ---- GF role: 8 pieces of 16 B into the rows of chunks (sh, cu) ----
             uint32_t acc[16];
+            if (DG == 3) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) acc[c] = zf::comp(v[c & 3], c >> 2);
+            } else
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -146,14 +173,8 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             }
             const int wo = dofs(s) + 4 * gl;
 #pragma unroll
-            for (int sh = 0; sh < 4; ++sh) {  // data shard sh sits in v[(sh - grp) mod 4]
-                const int jj = (sh - grp) & 3;
-                u32x4 x = v[0];
-#pragma unroll
-                for (int j = 1; j < 4; ++j)
-                    if (jj == j) x = v[j];
-                *reinterpret_cast<u32x4 *>(rows + (sh * 8 + cu) * RW + wo) = x;
-            }
+            for (int j = 0; j < 4; ++j)  // v[j] is data shard (j + grp) mod 4
+                *reinterpret_cast<u32x4 *>(rows + (((j + grp) & 3) * 8 + cu) * RW + wo) = v[j];
             {
                 u32x4 p[4];
 #pragma unroll
@@ -168,48 +189,63 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) *reinterpret_cast<u32x4 *>(rows + ((4 + q) * 8 + cu) * RW + wo) = p[q];
             }
-            // next loads in flight during the stores and the compressions
-            if (s < 7) load_step(blk, s + 1, v);
-            else if (blk + GW < total) load_step(blk + GW, 0, v);
             bao::wave_sync();
 
             // ---- store role: whole 128-B memory lines of chunks (t, cu) ----
-            if (gcol) {
+            // (all 16 piece reads issued before the 8 stores of a step)
+            if (DG != 1 && DG != 4) {
                 auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x
                     return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
                 };
+                if (s >= 1) {  // the whole line [d + 128 (s-1), d + 128 s) of every chunk
+                    u32x4 q[8];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    uint8_t *sp = lsp[t];
-                    const uint32_t d = ldd[t];
-                    const uint32_t *row = rows + (t * 8 + cu) * RW;
-                    if (s >= 1) {  // the whole line [d + 128 (s-1), d + 128 s)
-                        const uint32_t x = d + 128u * (s - 1) + 16u * gl;
+                    for (int t = 0; t < 8; ++t) {
+                        const uint32_t x = ldd[t] + 128u * (s - 1) + 16u * gl;
+                        const uint32_t *row = rows + (t * 8 + cu) * RW;
                         const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                        st16<NT>(sp + x, u32x4{lo.x, lo.y, hi.x, hi.y});
-                    } else {  // head [0, d)
-                        const uint32_t hd = d & 8u;
-                        if (hd && gl == 0) *reinterpret_cast<u32x2 *>(sp) = piece(row, 0);
-                        const uint32_t x = 16u * gl + hd;
-                        if (x + 16 <= d) {
-                            const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                            *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
-                        }
+                        q[t] = u32x4{lo.x, lo.y, hi.x, hi.y};
                     }
-                    if (s == 7) {  // tail [896 + d, 1024)
-                        const uint32_t x = 896u + d + 16u * gl;
-                        if (x + 16 <= 1024) {
-                            const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                            *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
-                        } else if (x + 8 == 1024) {
-                            *reinterpret_cast<u32x2 *>(sp + x) = piece(row, x);
+                    if (gcol) {
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) st16<NT>(lsp[t] + ldd[t] + 128u * (s - 1) + 16u * gl, q[t]);
+                    }
+                }
+                if ((s == 0 || s == 7) && gcol) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        uint8_t *sp = lsp[t];
+                        const uint32_t d = ldd[t];
+                        const uint32_t *row = rows + (t * 8 + cu) * RW;
+                        if (s == 0) {  // head [0, d)
+                            const uint32_t hd = d & 8u;
+                            if (hd && gl == 0) *reinterpret_cast<u32x2 *>(sp) = piece(row, 0);
+                            const uint32_t x = 16u * gl + hd;
+                            if (x + 16 <= d) {
+                                const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                                *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                            }
+                        } else {  // tail [896 + d, 1024)
+                            const uint32_t x = 896u + d + 16u * gl;
+                            if (x + 16 <= 1024) {
+                                const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                                *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                            } else if (x + 8 == 1024) {
+                                *reinterpret_cast<u32x2 *>(sp + x) = piece(row, x);
+                            }
                         }
                     }
                 }
             }
 
+            // next loads, after this step's stores, in flight during the compressions
+            if (s < 7) load_step(blk, s + 1, v);
+            else if (blk + GW < total) load_step(blk + GW, 0, v);
+
             // ---- hash role: blocks 2s, 2s+1 of my chunk ----
-            if (mine) {
+            if (DG == 2 || DG == 4 || DG == 6) {  // keep the rows' reads alive
+                h[0] ^= rows[lane * RW + dofs(s)];
+            } else if (mine) {
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
                     uint32_t m[16];

@@ -32,7 +32,7 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     a.coff = coff;
     a.cv = static_cast<uint8_t *>(d_scratch);
     static bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<false>),
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<true>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES) == hipSuccess;
     }();
     (void)attr;
@@ -41,7 +41,7 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     uint64_t grid = (blocks + FW - 1) / FW;
     const uint64_t cap = (uint64_t)num_cus();  // one workgroup (8 waves) per CU fits the LDS
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(zfec_bao_fused_kernel<false>, dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
+    hipLaunchKernelGGL(zfec_bao_fused_kernel<true>, dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     uint8_t *next = a.cv + count * a.N * 32;
     return bao::run_parent_levels<0, false>(a.cv, a.N, a.N, 1, next, (a.N + 1) / 2, a.N, count, d_out, out_stride,

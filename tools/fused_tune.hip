@@ -1,0 +1,109 @@
+// fused_tune.hip — K13 (carbonado_amd/csrc/fused_device.hpp) variants and
+// diagnostics on 256 x 16 MiB objects, interleaved in one process.  Times
+// the fused kernel alone (the parent levels are not run).  Calibration tool.
+//   fused_tune [objects=256] [rounds=3]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../carbonado_amd/csrc/fused_device.hpp"
+#include "../carbonado_amd/csrc/gf256.hpp"
+#include "../carbonado_amd/csrc/hbm_alloc.hpp"
+
+using namespace chip;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t e = (x);                                                                   \
+        if (e != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));          \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+namespace chip {
+int num_cus() { return 256; }
+}
+
+__global__ void fill_kernel(uint64_t *p, size_t n, uint64_t seed) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+struct Variant {
+    std::string name;
+    void (*fn)(fused::FusedArgs);
+};
+
+int main(int argc, char **argv) {
+    const uint64_t count = argc > 1 ? atoll(argv[1]) : 256;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 3;
+    const uint64_t n = 16ull << 20, C = n / 4, N = 8 * C / 1024;
+    const uint64_t blen = 8 + 8 * C + 64 * (N - 1), bstride = (blen + 255) / 256 * 256;
+    uint8_t *in, *out, *cv;
+    CK(hbm::Allocator::get().alloc(count * n, reinterpret_cast<void **>(&in)));
+    CK(hbm::Allocator::get().alloc(count * bstride, reinterpret_cast<void **>(&out)));
+    CK(hipMalloc(&cv, count * N * 32));
+    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xCA4B0AD0ull);
+    std::vector<uint8_t> enc = zfec_enc_matrix(4, 8);
+    const Gf256 &gf = Gf256::get();
+    std::vector<uint32_t> tab(4 * 256, 0);
+    for (int s = 0; s < 4; ++s)
+        for (int x = 0; x < 256; ++x)
+            for (int r = 0; r < 4; ++r) tab[s * 256 + x] |= (uint32_t)gf.mul(enc[(4 + r) * 4 + s], (uint8_t)x) << (8 * r);
+    uint32_t *dtab;
+    uint64_t *dcoff;
+    CK(hipMalloc(&dtab, tab.size() * 4));
+    CK(hipMemcpy(dtab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+    std::vector<uint64_t> coff(N);
+    for (uint64_t i = 0; i < N; ++i) coff[i] = bao::chunk_stream_off(i, N);
+    CK(hipMalloc(&dcoff, N * 8));
+    CK(hipMemcpy(dcoff, coff.data(), N * 8, hipMemcpyHostToDevice));
+    fused::FusedArgs a{};
+    a.in = in; a.in_stride = n; a.valid = n; a.C = C; a.out = out; a.out_stride = bstride;
+    a.count = count; a.N = N; a.cols = C / 1024; a.bpo = (a.cols + 7) / 8; a.table = dtab; a.coff = dcoff; a.cv = cv;
+    std::vector<Variant> vs = {{"product (nt)", fused::zfec_bao_fused_kernel<true, 0>},
+                               {"DG1 no line stores", fused::zfec_bao_fused_kernel<true, 1>},
+                               {"DG2 no hashing", fused::zfec_bao_fused_kernel<true, 2>},
+                               {"DG5 aligned lines", fused::zfec_bao_fused_kernel<true, 5>},
+                               {"DG6 aligned, no hashing", fused::zfec_bao_fused_kernel<true, 6>},
+                               {"cached stores", fused::zfec_bao_fused_kernel<false, 0>}};
+    for (auto &v : vs)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(v.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)fused::LDS_BYTES);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<std::vector<float>> ms(vs.size());
+    const uint64_t blocks = count * a.bpo;
+    const unsigned grid = (unsigned)std::min<uint64_t>(256, (blocks + fused::FW - 1) / fused::FW);
+    for (int rd = 0; rd < rounds; ++rd)
+        for (size_t v = 0; v < vs.size(); ++v) {
+            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            ms[v].push_back(t);
+        }
+    // 672 lane-ops per compression, 16 per chunk, N chunks per object
+    const double ops = (double)count * N * 16 * 672;
+    for (size_t v = 0; v < vs.size(); ++v) {
+        auto t = ms[v];
+        std::sort(t.begin(), t.end());
+        printf("%-22s median %7.3f ms  -> %6.1f GiB/s input, %.3f of VALU (compressions only)\n", vs[v].name.c_str(),
+               t[t.size() / 2], count * n / (t[t.size() / 2] * 1e-3) / 1073741824.0,
+               ops / (t[t.size() / 2] * 1e-3) / 39.3e12);
+    }
+    return 0;
+}
