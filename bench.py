@@ -391,12 +391,22 @@ class Workload:
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.encode_scratch(lv, n, count, dev)
             self.step = lambda: device.encode_batch(lv, self.inp, n, self.out, self.hashes, self.scratch)
-            # HBM bytes of the fused level-12 path: K1 reads n and writes the m shards into
-            # their chunk slots; K3/K4 read them back and write the header and parents
-            self.alg_bytes = count * (n + zlen + zlen + (blen - zlen)) if lv & 12 == 12 else count * (n + blen)
+            # HBM bytes: the object read once, its stream written once.  At Zfec|Bao the fused
+            # kernel (K13) hashes the shards on chip; CHIP_FUSED=0 runs K1-BL + K3, which
+            # read the 8C bytes of shards back (counted then)
+            two = lv & 12 == 12 and os.environ.get("CHIP_FUSED", "1") == "0"
+            self.alg_bytes = count * (n + zlen + zlen + (blen - zlen)) if two else count * (n + blen)
             self.zlen = zlen
-            fused = " (zfec writes the shards into their bao chunk slots; bao hashes in place)" if lv & 12 == 12 else ""
-            self.kernel = f"encode() level {lv} on the device: gf_apply_kernel + bao_chunk_kernel + parent levels{fused}"
+            if lv & 12 == 12 and not two:
+                self.kernel = (f"encode() level {lv} on the device: zfec_bao_fused_kernel (zfec 4-of-8 + chunk "
+                               "hashing + tree levels 1-3 in one pass) + parent levels from level 4")
+            elif two:
+                self.kernel = (f"encode() level {lv} on the device: gf_apply_kernel + bao_chunk_kernel + parent "
+                               "levels (zfec writes the shards into their bao chunk slots; bao hashes in place)")
+            elif lv & 4:
+                self.kernel = f"encode() level {lv} on the device: bao_chunk_kernel + parent levels"
+            else:
+                self.kernel = f"encode() level {lv} on the device: gf_apply_kernel"
             self.kernel_sym = "pipeline"
         elif args.mode == "scrub":
             import numpy as np
@@ -866,8 +876,8 @@ def main():
                                "avg_launch_ms": hbm["avg_launch_ms"], "min_launch_ms": hbm["min_launch_ms"],
                                "note": "int32 VALU peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; ops = 672 per "
                                        "BLAKE3 compression (content blocks + parents)"
-                                       + ("; step = zfec kernel (HBM-bound) + bao kernels (VALU-bound), "
-                                          "achieved over the whole step" if args.mode == "pipeline" else "")}
+                                       + ("; achieved over the whole step (every kernel of the level)"
+                                          if args.mode == "pipeline" else "")}
         if world > 1:
             fr = [wl.alg_bytes / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS if res["roofline"]["unit"] == "GB/s" else 1)
                   for ms in rank_avg_ms]

@@ -58,7 +58,7 @@ struct FusedArgs {
     uint64_t count, N, cols, bpo;   // objects, chunks per stream, chunk-columns per shard, blocks per object
     const uint32_t *table;          // [4][256] packed parity products (4 parity rows per dword)
     const uint64_t *coff;           // [N] stream offset of each chunk (bao_chunk_table)
-    uint8_t *cv;                    // [count][N] level-0 chunk CVs, 32 B each
+    uint8_t *cv;                    // level-0 CVs [count][N], or level-3 CVs [count][N/8] (FULL)
 };
 
 __device__ __forceinline__ int dofs(int step) { return 4 + (step & 1) * 32; }
@@ -69,11 +69,76 @@ __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
     else *reinterpret_cast<u32x4 *>(p) = v;
 }
 
+// Levels 1-3 of the tree inside the wave, pipelined over blocks.  With
+// cols % 8 == 0 the 8 lanes 8j..8j+7 of a block hold the CVs of 8 aligned
+// chunks of one shard: a complete subtree that is not the root (N >= 64).
+// Its 7 parents need three dependent compressions; instead of three
+// compression times per block (32, 16, 8 lanes busy) one step per block
+// computes level 1 of this block (even lanes), level 2 of the previous block
+// (lanes 4j+1, from the level-1 CVs lanes 4j and 4j+2 kept) and level 3 of
+// the block before (lanes 8j+3, from lanes 8j+1 and 8j+5): 56 lanes, one
+// compression.  Each parent node (l || r) is written at its stream slot —
+// the node with leftmost chunk s at level k sits 64 k bytes before chunk s —
+// and the level-3 CVs go to `cv` [count][N/8] for the parent kernels.
+template <bool NT>
+struct Tree {
+    uint32_t pr[8];   // my last parent CV (roles 1 and 2)
+    uint8_t *node;    // ... its node slot
+    uint64_t cvi;     // ... global index (obj N + chunk) of its leftmost chunk
+    bool ok = false;  // ... valid
+    int lane;
+    uint8_t *cv;
+    __device__ Tree(int l, uint8_t *c) : node(nullptr), cvi(0), lane(l), cv(c) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) pr[w] = 0u;
+    }
+    // h: my chunk CV; nd: the level-1 node slot of my chunk (even lanes);
+    // gi: obj N + chunk; cur: this block has chunks (false when draining)
+    __device__ __forceinline__ void step(const uint32_t (&h)[8], uint8_t *nd, uint64_t gi, bool cur) {
+        const bool r1 = !(lane & 1), r2 = (lane & 3) == 1, r3 = (lane & 7) == 3;
+        const int sl = r2 ? lane - 1 : lane - 2, sr = r2 ? lane + 1 : lane + 2;
+        uint32_t l[8], r[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const uint32_t hr = (uint32_t)__shfl_xor((int)h[w], 1);
+            const uint32_t pl = (uint32_t)__shfl((int)pr[w], sl);
+            const uint32_t pq = (uint32_t)__shfl((int)pr[w], sr);
+            l[w] = r1 ? h[w] : pl;
+            r[w] = r1 ? hr : pq;
+        }
+        const uint64_t tn = (uint64_t)__shfl((long long)(uintptr_t)node, sl);
+        const uint64_t tc = (uint64_t)__shfl((long long)cvi, sl);
+        const bool tok = __shfl((int)ok, sl) != 0;
+        uint8_t *my = r1 ? nd : reinterpret_cast<uint8_t *>(tn) - 64;
+        const uint64_t mc = r1 ? gi : tc;
+        const bool act = r1 ? cur : ((r2 || r3) && tok);
+        if (act) {
+            uint32_t p[8];
+            bao::b3_parent(l, r, false, p);
+            bao::node_io<0, NT>(my, l, r);
+            if (r3) {
+                bao::store_cv(cv + (mc / 8) * 32, p);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) pr[w] = p[w];
+            }
+        }
+        node = my;
+        cvi = mc;
+        ok = act && !r3;
+    }
+};
+
 // DG: diagnostics for tools/fused_tune (wrong output): 1 = no line stores,
 // 2 = no hashing, 3 = no GF (rows get the data shards only), 4 = neither
 // stores nor hashing, 5 = every chunk's lines 128-B aligned (no partial
 // lines), 6 = 5 without hashing.
-template <bool NT, int DG = 0>
+// FULL: cols % 8 == 0 and no zfec padding (valid >= 4 C): every block is 8
+// whole columns of plain loads, levels 1-3 run in the wave (Tree) and `cv`
+// receives level-3 CVs; otherwise lanes are predicated and `cv` receives the
+// level-0 CVs.  ORD 1 places the line stores between the step's two
+// compressions (their LDS reads issued before the first).
+template <bool NT, bool FULL, int ORD = 1, int DG = 0>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     {  // table: lds[x][s][r] = T_s[x], FR replicas
@@ -109,7 +174,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * 8;
         const uint8_t *ib = a.in + obj * a.in_stride;
         const uint64_t off = (ub + cu) * 1024 + 128 * (uint64_t)s + 16 * gl;
-        const bool full = ub + 8 <= a.cols && 3 * a.C + (ub + 8) * 1024 <= a.valid;  // wave-uniform
+        const bool full = FULL || (ub + 8 <= a.cols && 3 * a.C + (ub + 8) * 1024 <= a.valid);  // wave-uniform
         if (full) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const u32x4 *>(ib + ioff[j] + off);
@@ -121,6 +186,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         }
     };
 
+    Tree<NT> tree(lane, a.cv);
     uint64_t blk = (uint64_t)blockIdx.x * FW + wave;
     u32x4 v[4];
     if (blk < total) load_step(blk, 0, v);
@@ -128,10 +194,11 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * 8;
         uint8_t *ob = a.out + obj * a.out_stride;
         if (ub == 0 && lane == 0) *reinterpret_cast<uint64_t *>(ob) = 8 * a.C;  // u64 LE content length
-        const bool gcol = ub + cu < a.cols;                 // store role: chunks (t, ub + cu)
+        const bool gcol = FULL || ub + cu < a.cols;         // store role: chunks (t, ub + cu)
         const uint64_t hu = ub + (lane & 7);                // hash role: chunk (lane / 8, hu)
-        const bool mine = hu < a.cols;
+        const bool mine = FULL || hu < a.cols;
         const uint64_t ci = (uint64_t)(lane >> 3) * a.cols + hu;
+        const uint64_t hco = FULL ? a.coff[ci] : 0;          // tree role: my chunk's stream offset
         uint8_t *lsp[8];
         uint32_t ldd[8];
         {
@@ -192,26 +259,26 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             bao::wave_sync();
 
             // ---- store role: whole 128-B memory lines of chunks (t, cu) ----
-            // (all 16 piece reads issued before the 8 stores of a step)
-            if (DG != 1 && DG != 4) {
-                auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x
-                    return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
-                };
-                if (s >= 1) {  // the whole line [d + 128 (s-1), d + 128 s) of every chunk
-                    u32x4 q[8];
+            auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x
+                return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
+            };
+            constexpr bool ST = DG != 1 && DG != 4;
+            u32x4 q[8];
+            if (ST && s >= 1) {  // the whole line [d + 128 (s-1), d + 128 s) of every chunk
 #pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        const uint32_t x = ldd[t] + 128u * (s - 1) + 16u * gl;
-                        const uint32_t *row = rows + (t * 8 + cu) * RW;
-                        const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                        q[t] = u32x4{lo.x, lo.y, hi.x, hi.y};
-                    }
-                    if (gcol) {
-#pragma unroll
-                        for (int t = 0; t < 8; ++t) st16<NT>(lsp[t] + ldd[t] + 128u * (s - 1) + 16u * gl, q[t]);
-                    }
+                for (int t = 0; t < 8; ++t) {
+                    const uint32_t x = ldd[t] + 128u * (s - 1) + 16u * gl;
+                    const uint32_t *row = rows + (t * 8 + cu) * RW;
+                    const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                    q[t] = u32x4{lo.x, lo.y, hi.x, hi.y};
                 }
-                if ((s == 0 || s == 7) && gcol) {
+            }
+            auto line_stores = [&]() {
+                if (ST && s >= 1 && gcol) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) st16<NT>(lsp[t] + ldd[t] + 128u * (s - 1) + 16u * gl, q[t]);
+                }
+                if (ST && (s == 0 || s == 7) && gcol) {
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {
                         uint8_t *sp = lsp[t];
@@ -236,37 +303,51 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                         }
                     }
                 }
-            }
-
-            // next loads, after this step's stores, in flight during the compressions
-            if (s < 7) load_step(blk, s + 1, v);
-            else if (blk + GW < total) load_step(blk + GW, 0, v);
+                // next loads, after this step's stores, in flight during the compressions
+                if (s < 7) load_step(blk, s + 1, v);
+                else if (blk + GW < total) load_step(blk + GW, 0, v);
+            };
 
             // ---- hash role: blocks 2s, 2s+1 of my chunk ----
-            if (DG == 2 || DG == 4 || DG == 6) {  // keep the rows' reads alive
-                h[0] ^= rows[lane * RW + dofs(s)];
-            } else if (mine) {
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
+            auto hash = [&](int hh) {
+                if (DG == 2 || DG == 4 || DG == 6) {  // keep the rows' reads alive
+                    h[hh] ^= rows[lane * RW + dofs(s) + hh];
+                } else if (mine) {
                     uint32_t m[16];
                     const u32x4 *r = reinterpret_cast<const u32x4 *>(rows + lane * RW + dofs(s) + hh * 16);
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const u32x4 x = r[q];
-                        m[4 * q] = x.x; m[4 * q + 1] = x.y; m[4 * q + 2] = x.z; m[4 * q + 3] = x.w;
+                    for (int q4 = 0; q4 < 4; ++q4) {
+                        const u32x4 x = r[q4];
+                        m[4 * q4] = x.x; m[4 * q4 + 1] = x.y; m[4 * q4 + 2] = x.z; m[4 * q4 + 3] = x.w;
                     }
                     const int b = 2 * s + hh;
                     const uint32_t flags = (b == 0 ? bao::F_CHUNK_START : 0u) | (b == 15 ? bao::F_CHUNK_END : 0u);
                     bao::b3_compress(h, m, ci, 64, flags);
                 }
+            };
+            if (ORD == 1) {
+                hash(0);
+                line_stores();
+                hash(1);
+            } else {
+                line_stores();
+                hash(0);
+                hash(1);
             }
             bao::wave_sync();
         }
-        if (mine) {
+        if (FULL) {
+            tree.step(h, ob + hco - 64, obj * a.N + ci, true);
+        } else if (mine) {
             u32x4 *cvp = reinterpret_cast<u32x4 *>(a.cv + (obj * a.N + ci) * 32);
             cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
             cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
         }
+    }
+    if (FULL) {  // drain: level 2 of the last block, level 3 of the last two
+        uint32_t z[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        tree.step(z, nullptr, 0, false);
+        tree.step(z, nullptr, 0, false);
     }
 }
 

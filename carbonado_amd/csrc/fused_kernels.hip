@@ -31,8 +31,11 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     if ((e = bao_chunk_table(a.N, &coff)) != hipSuccess) return e;
     a.coff = coff;
     a.cv = static_cast<uint8_t *>(d_scratch);
+    const bool full = a.cols % 8 == 0 && n >= 4 * C;  // levels 1-3 in the kernel (N >= 64, 8 subtrees a block)
     static bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<true>),
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<true, true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<true, false>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES) == hipSuccess;
     }();
     (void)attr;
@@ -41,11 +44,15 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     uint64_t grid = (blocks + FW - 1) / FW;
     const uint64_t cap = (uint64_t)num_cus();  // one workgroup (8 waves) per CU fits the LDS
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(zfec_bao_fused_kernel<true>, dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
+    if (full)
+        hipLaunchKernelGGL((zfec_bao_fused_kernel<true, true>), dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
+    else
+        hipLaunchKernelGGL((zfec_bao_fused_kernel<true, false>), dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    uint8_t *next = a.cv + count * a.N * 32;
-    return bao::run_parent_levels<0, false>(a.cv, a.N, a.N, 1, next, (a.N + 1) / 2, a.N, count, d_out, out_stride,
-                                            d_hash, nullptr, stream);
+    const uint64_t n0 = full ? a.N / 8 : a.N;  // nodes per object in `cv`
+    uint8_t *next = a.cv + count * n0 * 32;
+    return bao::run_parent_levels<0, false>(a.cv, n0, n0, full ? 4 : 1, next, (n0 + 1) / 2, a.N, count, d_out,
+                                            out_stride, d_hash, nullptr, stream);
 }
 
 }  // namespace chip

@@ -8,7 +8,10 @@ config, against the C oracle:
 * cfg5 shape: zfec 8-of-16 encode of 16 MiB, then decode with 8 shards
   dropped (data and parity mixed);
 * cfg3: every one of the 28 two-erasure patterns of 4-of-8 on one 16 MiB
-  object, decoded on the device and compared with the input.
+  object, decoded on the device and compared with the input;
+* the level-12 device pipeline at 16 MiB (the fused zfec + bao kernel with
+  tree levels 1-3 in the wave, its full-block path), streams and hashes
+  bit-exact for several objects and stream placements.
 """
 import itertools
 
@@ -86,3 +89,29 @@ def test_cfg3_all_28_erasure_pairs_16mib(gpu, obj16):
     torch.cuda.synchronize()
     for i, lost in enumerate(pairs):
         assert torch.equal(out[i], inp[0]), lost
+
+
+@pytest.mark.parametrize("shift", [0, 112])
+def test_level12_16mib_fused_full_path(gpu, obj16, shift):
+    """encode_batch at Zfec|Bao on 3 x 16 MiB objects (C = 4 MiB: 4096 chunk
+    columns, no zfec padding: the fused kernel's FULL path) against the
+    oracle's encode(); shift 112 moves every chunk to another phase of the
+    128-B memory lines (the line stores' head and tail pieces)."""
+    import torch
+    from carbonado_amd import device
+    objs = [obj16, bytes(reversed(obj16)), np.random.default_rng(12).integers(0, 256, N, np.uint8).tobytes()]
+    oenc = [O.encode(o, 12) for o in objs]
+    blen = len(oenc[0][0])
+    stride = (blen + shift + 255) // 256 * 256
+    inp = torch.from_numpy(np.frombuffer(b"".join(objs), np.uint8).copy()).cuda().reshape(3, N)
+    raw = torch.full((3 * stride + 256,), 0xA5, dtype=torch.uint8, device="cuda")
+    out = raw[shift:shift + 3 * stride].view(3, stride)
+    hashes = torch.zeros((3, 32), dtype=torch.uint8, device="cuda")
+    olen, info = device.encode_batch(12, inp, N, out, hashes, device.encode_scratch(12, N, 3))
+    torch.cuda.synchronize()
+    assert olen == blen and info.padding_len == 0
+    got, gh = out.cpu().numpy(), hashes.cpu().numpy()
+    for o, (enc, h, _) in enumerate(oenc):
+        assert got[o, :blen].tobytes() == enc, o
+        assert gh[o].tobytes() == h
+        assert (got[o, blen:] == 0xA5).all()

@@ -41,6 +41,7 @@ __global__ void fill_kernel(uint64_t *p, size_t n, uint64_t seed) {
 struct Variant {
     std::string name;
     void (*fn)(fused::FusedArgs);
+    int shift;  // stream base offset in bytes (56: the u64 prefix ends on a 64-B boundary)
 };
 
 int main(int argc, char **argv) {
@@ -70,12 +71,13 @@ int main(int argc, char **argv) {
     fused::FusedArgs a{};
     a.in = in; a.in_stride = n; a.valid = n; a.C = C; a.out = out; a.out_stride = bstride;
     a.count = count; a.N = N; a.cols = C / 1024; a.bpo = (a.cols + 7) / 8; a.table = dtab; a.coff = dcoff; a.cv = cv;
-    std::vector<Variant> vs = {{"product (nt)", fused::zfec_bao_fused_kernel<true, 0>},
-                               {"DG1 no line stores", fused::zfec_bao_fused_kernel<true, 1>},
-                               {"DG2 no hashing", fused::zfec_bao_fused_kernel<true, 2>},
-                               {"DG5 aligned lines", fused::zfec_bao_fused_kernel<true, 5>},
-                               {"DG6 aligned, no hashing", fused::zfec_bao_fused_kernel<true, 6>},
-                               {"cached stores", fused::zfec_bao_fused_kernel<false, 0>}};
+    std::vector<Variant> vs = {{"FULL ORD1 (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0>, 0},
+                               {"FULL ORD1 base+56", fused::zfec_bao_fused_kernel<true, true, 1, 0>, 56},
+                               {"FULL ORD1 cached base+56", fused::zfec_bao_fused_kernel<false, true, 1, 0>, 56},
+                               {"general ORD1", fused::zfec_bao_fused_kernel<true, false, 1, 0>, 0},
+                               {"general ORD1 base+56", fused::zfec_bao_fused_kernel<true, false, 1, 0>, 56},
+                               {"FULL ORD1 DG1 no stores", fused::zfec_bao_fused_kernel<true, true, 1, 1>, 0},
+                               {"FULL ORD1 DG5 aligned", fused::zfec_bao_fused_kernel<true, true, 1, 5>, 0}};
     for (auto &v : vs)
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(v.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)fused::LDS_BYTES);
@@ -87,6 +89,7 @@ int main(int argc, char **argv) {
     const unsigned grid = (unsigned)std::min<uint64_t>(256, (blocks + fused::FW - 1) / fused::FW);
     for (int rd = 0; rd < rounds; ++rd)
         for (size_t v = 0; v < vs.size(); ++v) {
+            a.out = out + vs[v].shift;
             hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
@@ -101,7 +104,7 @@ int main(int argc, char **argv) {
     for (size_t v = 0; v < vs.size(); ++v) {
         auto t = ms[v];
         std::sort(t.begin(), t.end());
-        printf("%-22s median %7.3f ms  -> %6.1f GiB/s input, %.3f of VALU (compressions only)\n", vs[v].name.c_str(),
+        printf("%-24s median %7.3f ms  -> %6.1f GiB/s input, %.3f of VALU (compressions only)\n", vs[v].name.c_str(),
                t[t.size() / 2], count * n / (t[t.size() / 2] * 1e-3) / 1073741824.0,
                ops / (t[t.size() / 2] * 1e-3) / 39.3e12);
     }
