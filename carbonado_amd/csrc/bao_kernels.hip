@@ -69,6 +69,8 @@ uint64_t bao_scratch_len(uint64_t n, uint64_t count) { return bao_scratch_len_t<
 hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                           uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,
                           hipStream_t stream) {
+    if (d_out && fused_on() && bao_fused_ok(d_in, in_stride, n, count))  // K13 KIND 1 (fused_kernels.hip)
+        return bao_fused_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_scratch, stream);
     return run_bao<0>(d_in, in_stride, n, count, d_out, out_stride, d_hash, nullptr, d_scratch, stream);
 }
 

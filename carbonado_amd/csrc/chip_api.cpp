@@ -524,10 +524,6 @@ int pipe_wg_cfg() {
 // K13 (fused_device.hpp) by default: the shards are hashed while they are on
 // chip instead of read back from HBM; CHIP_FUSED=0 runs the two-kernel
 // overlapped pipeline below (A/B runs).  Scratch: zfec_bao_scratch_len.
-bool fused_on() {
-    static const bool on = env_int("CHIP_FUSED", 1) != 0;
-    return on;
-}
 
 hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
                         uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s) {

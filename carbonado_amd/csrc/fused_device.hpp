@@ -137,11 +137,21 @@ struct Tree {
 // whole columns of plain loads, levels 1-3 run in the wave (Tree) and `cv`
 // receives level-3 CVs; otherwise lanes are predicated and `cv` receives the
 // level-0 CVs.  ORD 1 places the line stores between the step's two
-// compressions (their LDS reads issued before the first).
-template <bool NT, bool FULL, int ORD = 1, int DG = 0>
+// compressions (their LDS reads issued before the first) and the next step's
+// loads after them; ORD 2 issues those loads first, as soon as the step's
+// rows are written.
+// KIND 0: encode() Zfec|Bao (zfec 4-of-8, then bao of the 8 shards); KIND 1:
+// bao of the content itself (encode() level 8, FULL only: 64 | N, every chunk
+// whole).  KIND 1's block is 64 consecutive chunks (row / hash lane
+// L = chunk ub + L), loaded 8 x 16 B per lane per step instead of computed.
+template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
+    static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    {  // table: lds[x][s][r] = T_s[x], FR replicas
+    constexpr int NV = KIND ? 8 : 4;         // 16-B loads per lane per step
+    constexpr uint64_t BW = KIND ? 64 : 8;   // chunks (KIND 1) / columns (KIND 0) per block
+    const uint64_t TS = KIND ? 8 : a.cols;   // chunk index step between the 8 lane groups
+    if (KIND == 0) {  // table: lds[x][s][r] = T_s[x], FR replicas
         uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
         for (int i = threadIdx.x; i < 256 * 4 * FR; i += FTPB) {
             const int x = i / (4 * FR);
@@ -170,15 +180,21 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     // (every block of an object without zfec padding) takes plain loads whose
     // wait the compiler can defer to the first use; the masked form (a branch
     // and an immediate wait per load) only runs in an object's last blocks.
-    auto load_step = [&](uint64_t blk, int s, u32x4 (&v)[4]) {
-        const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * 8;
+    auto load_step = [&](uint64_t blk, int s, u32x4 (&v)[NV]) {
+        const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * BW;
         const uint8_t *ib = a.in + obj * a.in_stride;
+        if (KIND == 1) {  // chunk ub + 8 t + cu, bytes 128 s + 16 gl
+            const uint8_t *b = ib + (ub + cu) * 1024 + 128 * (uint64_t)s + 16 * gl;
+#pragma unroll
+            for (int t = 0; t < NV; ++t) v[t] = *reinterpret_cast<const u32x4 *>(b + (uint64_t)t * 8192);
+            return;
+        }
         const uint64_t off = (ub + cu) * 1024 + 128 * (uint64_t)s + 16 * gl;
         const bool full = FULL || (ub + 8 <= a.cols && 3 * a.C + (ub + 8) * 1024 <= a.valid);  // wave-uniform
         if (full) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const u32x4 *>(ib + ioff[j] + off);
-        } else {
+        } else if (KIND == 0) {
             const bool col = ub + cu < a.cols;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -188,16 +204,17 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
 
     Tree<NT> tree(lane, a.cv);
     uint64_t blk = (uint64_t)blockIdx.x * FW + wave;
-    u32x4 v[4];
+    u32x4 v[NV];
     if (blk < total) load_step(blk, 0, v);
     for (; blk < total; blk += GW) {
-        const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * 8;
+        const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * BW;
         uint8_t *ob = a.out + obj * a.out_stride;
-        if (ub == 0 && lane == 0) *reinterpret_cast<uint64_t *>(ob) = 8 * a.C;  // u64 LE content length
+        if (ub == 0 && lane == 0)  // u64 LE content length
+            *reinterpret_cast<uint64_t *>(ob) = KIND ? a.valid : 8 * a.C;
         const bool gcol = FULL || ub + cu < a.cols;         // store role: chunks (t, ub + cu)
         const uint64_t hu = ub + (lane & 7);                // hash role: chunk (lane / 8, hu)
         const bool mine = FULL || hu < a.cols;
-        const uint64_t ci = (uint64_t)(lane >> 3) * a.cols + hu;
+        const uint64_t ci = (uint64_t)(lane >> 3) * TS + hu;
         const uint64_t hco = FULL ? a.coff[ci] : 0;          // tree role: my chunk's stream offset
         uint8_t *lsp[8];
         uint32_t ldd[8];
@@ -205,7 +222,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             uint64_t co[8];  // all 8 offset loads in flight together
             const uint64_t c0 = gcol ? ub + cu : 0;
 #pragma unroll
-            for (int t = 0; t < 8; ++t) co[t] = a.coff[(uint64_t)t * a.cols + c0];
+            for (int t = 0; t < 8; ++t) co[t] = a.coff[(uint64_t)t * TS + c0];
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 lsp[t] = ob + co[t];
@@ -219,6 +236,11 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
 
         for (int s = 0; s < 8; ++s) {
             // ---- GF role: 8 pieces of 16 B into the rows of chunks (sh, cu) ----
+            if (KIND == 1) {  // content: the 8 loaded pieces are the rows' bytes
+                const int wo = dofs(s) + 4 * gl;
+#pragma unroll
+                for (int t = 0; t < NV; ++t) *reinterpret_cast<u32x4 *>(rows + (t * 8 + cu) * RW + wo) = v[t];
+            } else {
             uint32_t acc[16];
             if (DG == 3) {
 #pragma unroll
@@ -256,7 +278,14 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) *reinterpret_cast<u32x4 *>(rows + ((4 + q) * 8 + cu) * RW + wo) = p[q];
             }
+            }
             bao::wave_sync();
+
+            auto next_loads = [&]() {
+                if (s < 7) load_step(blk, s + 1, v);
+                else if (blk + GW < total) load_step(blk + GW, 0, v);
+            };
+            if (ORD == 2) next_loads();  // as soon as v is free: two compressions of cover
 
             // ---- store role: whole 128-B memory lines of chunks (t, cu) ----
             auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x
@@ -304,8 +333,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                     }
                 }
                 // next loads, after this step's stores, in flight during the compressions
-                if (s < 7) load_step(blk, s + 1, v);
-                else if (blk + GW < total) load_step(blk + GW, 0, v);
+                if (ORD != 2) next_loads();
             };
 
             // ---- hash role: blocks 2s, 2s+1 of my chunk ----
@@ -325,7 +353,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                     bao::b3_compress(h, m, ci, 64, flags);
                 }
             };
-            if (ORD == 1) {
+            if (ORD >= 1) {
                 hash(0);
                 line_stores();
                 hash(1);

@@ -3,6 +3,8 @@
 #include "chip_internal.hpp"
 #include "fused_device.hpp"
 
+#include <cstdlib>
+
 namespace chip {
 
 uint64_t zfec_bao_scratch_len(uint64_t zlen, uint64_t count) {
@@ -53,6 +55,56 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     uint8_t *next = a.cv + count * n0 * 32;
     return bao::run_parent_levels<0, false>(a.cv, n0, n0, full ? 4 : 1, next, (n0 + 1) / 2, a.N, count, d_out,
                                             out_stride, d_hash, nullptr, stream);
+}
+
+bool fused_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_FUSED");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    return on;
+}
+
+bool bao_fused_ok(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count) {
+    return n >= 65536 && n % 65536 == 0 && (reinterpret_cast<uintptr_t>(d_in) & 15) == 0 &&
+           (count <= 1 || in_stride % 16 == 0);
+}
+
+hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint8_t *d_out,
+                         uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t stream) {
+    if (count == 0) return hipSuccess;
+    if (!bao_fused_ok(d_in, in_stride, n, count)) return hipErrorInvalidValue;
+    using namespace fused;
+    FusedArgs a{};
+    a.in = d_in; a.in_stride = in_stride; a.valid = n; a.C = 0;
+    a.out = d_out; a.out_stride = out_stride;
+    a.count = count;
+    a.N = n / 1024;
+    a.cols = 0;
+    a.bpo = a.N / 64;
+    a.table = nullptr;
+    const uint64_t *coff = nullptr;
+    hipError_t e = bao_chunk_table(a.N, &coff);
+    if (e != hipSuccess) return e;
+    a.coff = coff;
+    a.cv = static_cast<uint8_t *>(d_scratch);
+    constexpr auto K = zfec_bao_fused_kernel<true, true, 1, 0, 1>;
+    static bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(K), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)LDS_BYTES) == hipSuccess;
+    }();
+    (void)attr;
+    (void)hipGetLastError();
+    const uint64_t blocks = count * a.bpo;
+    uint64_t grid = (blocks + FW - 1) / FW;
+    const uint64_t cap = (uint64_t)num_cus();
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(K, dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint64_t n3 = a.N / 8;  // level-3 CVs per object
+    uint8_t *next = a.cv + count * n3 * 32;
+    return bao::run_parent_levels<0, false>(a.cv, n3, n3, 4, next, (n3 + 1) / 2, a.N, count, d_out, out_stride,
+                                            d_hash, nullptr, stream);
 }
 
 }  // namespace chip

@@ -1,12 +1,13 @@
 // fused_tune.hip — K13 (carbonado_amd/csrc/fused_device.hpp) variants and
 // diagnostics on 256 x 16 MiB objects, interleaved in one process.  Times
 // the fused kernel alone (the parent levels are not run).  Calibration tool.
-//   fused_tune [objects=256] [rounds=3]
+//   fused_tune [objects=256] [rounds=3] [variant-name filter]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -41,18 +42,19 @@ __global__ void fill_kernel(uint64_t *p, size_t n, uint64_t seed) {
 struct Variant {
     std::string name;
     void (*fn)(fused::FusedArgs);
-    int shift;  // stream base offset in bytes (56: the u64 prefix ends on a 64-B boundary)
+    int kind;  // 0: zfec 4-of-8 + bao of the shards, 1: bao of the content
 };
 
 int main(int argc, char **argv) {
     const uint64_t count = argc > 1 ? atoll(argv[1]) : 256;
     const int rounds = argc > 2 ? atoi(argv[2]) : 3;
-    const uint64_t n = 16ull << 20, C = n / 4, N = 8 * C / 1024;
-    const uint64_t blen = 8 + 8 * C + 64 * (N - 1), bstride = (blen + 255) / 256 * 256;
+    const uint64_t n = 16ull << 20, C = n / 4;
+    const uint64_t N0 = 8 * C / 1024, N1 = n / 1024;  // chunks per stream: KIND 0 (zfec output), KIND 1 (content)
+    const uint64_t blen0 = 8 + 8 * C + 64 * (N0 - 1), bstride = (blen0 + 255) / 256 * 256;
     uint8_t *in, *out, *cv;
     CK(hbm::Allocator::get().alloc(count * n, reinterpret_cast<void **>(&in)));
     CK(hbm::Allocator::get().alloc(count * bstride, reinterpret_cast<void **>(&out)));
-    CK(hipMalloc(&cv, count * N * 32));
+    CK(hipMalloc(&cv, count * N0 * 32));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xCA4B0AD0ull);
     std::vector<uint8_t> enc = zfec_enc_matrix(4, 8);
     const Gf256 &gf = Gf256::get();
@@ -61,23 +63,38 @@ int main(int argc, char **argv) {
         for (int x = 0; x < 256; ++x)
             for (int r = 0; r < 4; ++r) tab[s * 256 + x] |= (uint32_t)gf.mul(enc[(4 + r) * 4 + s], (uint8_t)x) << (8 * r);
     uint32_t *dtab;
-    uint64_t *dcoff;
     CK(hipMalloc(&dtab, tab.size() * 4));
     CK(hipMemcpy(dtab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
-    std::vector<uint64_t> coff(N);
-    for (uint64_t i = 0; i < N; ++i) coff[i] = bao::chunk_stream_off(i, N);
-    CK(hipMalloc(&dcoff, N * 8));
-    CK(hipMemcpy(dcoff, coff.data(), N * 8, hipMemcpyHostToDevice));
-    fused::FusedArgs a{};
-    a.in = in; a.in_stride = n; a.valid = n; a.C = C; a.out = out; a.out_stride = bstride;
-    a.count = count; a.N = N; a.cols = C / 1024; a.bpo = (a.cols + 7) / 8; a.table = dtab; a.coff = dcoff; a.cv = cv;
-    std::vector<Variant> vs = {{"FULL ORD1 (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0>, 0},
-                               {"FULL ORD1 base+56", fused::zfec_bao_fused_kernel<true, true, 1, 0>, 56},
-                               {"FULL ORD1 cached base+56", fused::zfec_bao_fused_kernel<false, true, 1, 0>, 56},
-                               {"general ORD1", fused::zfec_bao_fused_kernel<true, false, 1, 0>, 0},
-                               {"general ORD1 base+56", fused::zfec_bao_fused_kernel<true, false, 1, 0>, 56},
-                               {"FULL ORD1 DG1 no stores", fused::zfec_bao_fused_kernel<true, true, 1, 1>, 0},
-                               {"FULL ORD1 DG5 aligned", fused::zfec_bao_fused_kernel<true, true, 1, 5>, 0}};
+    uint64_t *dcoff[2];
+    for (int k = 0; k < 2; ++k) {
+        const uint64_t N = k ? N1 : N0;
+        std::vector<uint64_t> coff(N);
+        for (uint64_t i = 0; i < N; ++i) coff[i] = bao::chunk_stream_off(i, N);
+        CK(hipMalloc(&dcoff[k], N * 8));
+        CK(hipMemcpy(dcoff[k], coff.data(), N * 8, hipMemcpyHostToDevice));
+    }
+    fused::FusedArgs A[2];
+    for (int k = 0; k < 2; ++k) {
+        fused::FusedArgs &a = A[k];
+        a = fused::FusedArgs{};
+        a.in = in; a.in_stride = n; a.valid = n; a.C = k ? 0 : C; a.out = out; a.out_stride = bstride;
+        a.count = count; a.N = k ? N1 : N0; a.cols = k ? 0 : C / 1024; a.bpo = k ? N1 / 64 : (C / 1024 + 7) / 8;
+        a.table = dtab; a.coff = dcoff[k]; a.cv = cv;
+    }
+    const char *which = argc > 3 ? argv[3] : "all";
+    std::vector<Variant> all = {
+        {"K0 FULL ORD1 (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
+        {"K0 FULL ORD2", fused::zfec_bao_fused_kernel<true, true, 2, 0, 0>, 0},
+        {"K0 FULL ORD0", fused::zfec_bao_fused_kernel<true, true, 0, 0, 0>, 0},
+        {"K1 ORD1 (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1>, 1},
+        {"K1 ORD2", fused::zfec_bao_fused_kernel<true, true, 2, 0, 1>, 1},
+        {"K1 ORD0", fused::zfec_bao_fused_kernel<true, true, 0, 0, 1>, 1},
+        {"K1 ORD1 cached stores", fused::zfec_bao_fused_kernel<false, true, 1, 0, 1>, 1},
+        {"K1 ORD1 DG1 no stores", fused::zfec_bao_fused_kernel<true, true, 1, 1, 1>, 1},
+        {"K1 ORD1 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 1>, 1}};
+    std::vector<Variant> vs;
+    for (auto &v : all)
+        if (!strcmp(which, "all") || strstr(v.name.c_str(), which)) vs.push_back(v);
     for (auto &v : vs)
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(v.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)fused::LDS_BYTES);
@@ -85,11 +102,11 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<std::vector<float>> ms(vs.size());
-    const uint64_t blocks = count * a.bpo;
-    const unsigned grid = (unsigned)std::min<uint64_t>(256, (blocks + fused::FW - 1) / fused::FW);
     for (int rd = 0; rd < rounds; ++rd)
         for (size_t v = 0; v < vs.size(); ++v) {
-            a.out = out + vs[v].shift;
+            const fused::FusedArgs &a = A[vs[v].kind];
+            const uint64_t blocks = count * a.bpo;
+            const unsigned grid = (unsigned)std::min<uint64_t>(256, (blocks + fused::FW - 1) / fused::FW);
             hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
@@ -99,14 +116,14 @@ int main(int argc, char **argv) {
             CK(hipEventElapsedTime(&t, e0, e1));
             ms[v].push_back(t);
         }
-    // 672 lane-ops per compression, 16 per chunk, N chunks per object
-    const double ops = (double)count * N * 16 * 672;
     for (size_t v = 0; v < vs.size(); ++v) {
         auto t = ms[v];
         std::sort(t.begin(), t.end());
-        printf("%-24s median %7.3f ms  -> %6.1f GiB/s input, %.3f of VALU (compressions only)\n", vs[v].name.c_str(),
-               t[t.size() / 2], count * n / (t[t.size() / 2] * 1e-3) / 1073741824.0,
-               ops / (t[t.size() / 2] * 1e-3) / 39.3e12);
+        const double m = t[t.size() / 2];
+        // 672 lane-ops per compression, 16 per chunk
+        const double ops = (double)count * A[vs[v].kind].N * 16 * 672;
+        printf("%-26s median %7.3f ms  -> %6.1f GiB/s input, %.3f of VALU (chunk compressions only)\n",
+               vs[v].name.c_str(), m, count * n / (m * 1e-3) / 1073741824.0, ops / (m * 1e-3) / 39.3e12);
     }
     return 0;
 }
