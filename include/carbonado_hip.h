@@ -334,8 +334,9 @@ CHIP_API int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, 
  * encoding (*out_len bytes, the same for every object) at d_out +
  * o*out_stride, its hash at d_hash + 32*o (zeros without Bao,
  * encoding.rs:145), *info = its EncodeInfo (may be NULL).  Zfec|Bao runs
- * fused: the zfec kernel writes the 8 shards straight into their chunk slots
- * of the bao stream, which is then hashed in place (no zfec buffer).
+ * fused: one kernel computes the 8 shards, hashes them on chip and writes
+ * them straight into their chunk slots of the bao stream (no zfec buffer,
+ * the shards cross HBM once; CHIP_FUSED=0 selects the two-kernel path).
  * d_scratch: chip_encode_scratch_len(format, n, count) bytes.  Pointers and
  * strides must be multiples of 16; enqueued on `stream`, not synchronised.
  * Replaces, for these levels, encode() = zfec (encoding.rs:121-138) -> bao
