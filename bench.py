@@ -65,7 +65,7 @@ def parse(argv=None):
     ap.add_argument("--object-mib", type=float, default=16.0)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=8)
-    ap.add_argument("--mode", choices=["encode", "decode", "bao", "bao-decode", "pipeline", "e2e", "e2e-decode", "scrub",
+    ap.add_argument("--mode", choices=["encode", "decode", "bao", "bao-decode", "pipeline", "pipeline-decode", "e2e", "e2e-decode", "scrub",
                                        "hasher", "file"],
                     default="encode",
                     help="bao-decode: device-resident decoding::bao (verify every node, return the content); "
@@ -220,6 +220,8 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
         enc_obj, h_obj, inf_obj = O.c_encode_full(obj, args.level, pub, eph if eph else bytes(32), bytes(16))
     if args.mode == "bao-decode":
         bstream, bhash = O.bao_encode(obj)
+    if args.mode == "pipeline-decode":
+        enc_obj, h_obj, inf_obj = O.encode(obj, args.level)
     if args.mode == "scrub":
         enc_obj, h_obj, inf_obj = O.encode(obj, 12)
         bad = bytearray(enc_obj)
@@ -245,6 +247,8 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
                 pass
             keep_s = [i for i in range(8) if i != 0][:4]
             O.encode(O.zfec_decode_shares([zc[i * zC:(i + 1) * zC] for i in keep_s], keep_s, zpad), 12)
+        elif args.mode == "pipeline-decode":
+            O.decode(h_obj, enc_obj, inf_obj["padding_len"], args.level)
         elif args.mode == "e2e-decode":
             cur = O.decode(h_obj, enc_obj, inf_obj["padding_len"], args.level & 12) if args.level & 12 else enc_obj
             if args.level & 1:
@@ -279,6 +283,7 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
     what = {"bao": "bao encode", "bao-decode": "bao decode (verify + content)", "e2e": f"encode() level {args.level}", "pipeline": f"encode() level {args.level}",
             "file": f"encode() level {args.level} (in memory, no file I/O, no header)",
             "hasher": "BLAKE3 of the content", "scrub": "scrub() restated: bao decode + zfec decode + encode()", "e2e-decode": f"decode() level {args.level}",
+            "pipeline-decode": f"decode() level {args.level}",
             "decode": f"zfec {args.k}-of-{args.m} decode, erased {args.erase}"}.get(
         args.mode, f"zfec {args.k}-of-{args.m} encode")
     return {"value": round(done * n / el / 2**30, 4), "unit": "GiB/s", "cores": max(1, threads), "kind": "port",
@@ -340,7 +345,7 @@ class Workload:
                          if args.prealloc_gib else None)
         if args.alloc == "contiguous":
             os.environ["CHIP_ALLOC"] = "contiguous"  # read by chip_device_alloc at each call
-        device_mode = args.mode in ("encode", "decode", "bao", "bao-decode", "pipeline")
+        device_mode = args.mode in ("encode", "decode", "bao", "bao-decode", "pipeline", "pipeline-decode")
         self.alloc_info = {}
 
         def batch_buf(shape, name=None):
@@ -407,6 +412,36 @@ class Workload:
                 self.kernel = f"encode() level {lv} on the device: bao_chunk_kernel + parent levels"
             else:
                 self.kernel = f"encode() level {lv} on the device: gf_apply_kernel"
+            self.kernel_sym = "pipeline"
+        elif args.mode == "pipeline-decode":
+            lv = args.level
+            if lv & 3:
+                raise SystemExit("--mode pipeline-decode runs the device-only levels (Bao/Zfec bits); use --mode "
+                                 "e2e-decode")
+            zlen = m * C if lv & 8 else n
+            self.blen = blen = L.chip_bao_encoded_len(zlen) if lv & 4 else zlen
+            self.zlen = zlen
+            self.enc = batch_buf((count, (blen + 15) // 16 * 16), "enc")
+            self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
+            esc = device.encode_scratch(lv, n, count, dev)
+            _, info = device.encode_batch(lv, self.inp, n, self.enc, self.hashes, esc)
+            torch.cuda.synchronize()
+            del esc
+            self.pad = info.padding_len
+            self.out = batch_buf((count, (n + 15) // 16 * 16), "out")
+            self.status = torch.full((count,), -1, dtype=torch.int32, device=dev)
+            self.scratch = device.decode_scratch(lv, blen, count, dev)
+            self.step = lambda: device.decode_batch(lv, self.enc, blen, self.hashes, self.pad, self.out, self.status,
+                                                    self.scratch)
+            # read each encoding once (every byte verified) and write the decoded object once;
+            # without Bao only the primaries' bytes are read
+            self.alg_bytes = count * (blen + n) if lv & 4 else count * 2 * n
+            if lv & 4:
+                self.kernel = (f"decode() level {lv} on the device: bao_chunk_kernel MODE 1 (every chunk and "
+                               f"parent verified{', only the 4 data shards written' if lv & 8 else ''}) + parent "
+                               "check levels")
+            else:
+                self.kernel = f"decode() level {lv} on the device: primaries' bytes copied"
             self.kernel_sym = "pipeline"
         elif args.mode == "scrub":
             import numpy as np
@@ -739,6 +774,12 @@ class Workload:
                   (self.hashes[0].cpu().numpy().tobytes() == h if self.args.level & 4 else True))
         elif self.args.mode == "e2e-decode":
             ok = self.h_out[0, :self.n].numpy().tobytes() == sample
+        elif self.args.mode == "pipeline-decode":
+            # every object: status 0 and the decoded bytes equal the input (on the device);
+            # object 0's encoding is the oracle's encode()
+            enc, h, _ = O.encode(sample, self.args.level)
+            ok = (bool((self.status == 0).all()) and torch.equal(self.out[:, :self.n], self.inp[:, :self.n]) and
+                  self.enc[0, :self.blen].cpu().numpy().tobytes() == enc)
         elif self.args.mode == "file":
             from carbonado_amd import file as cfile
             path, info = self.results[0]
@@ -811,6 +852,8 @@ def main():
             workload = f"bao decode (verify + content), {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "pipeline":
             workload = f"encode() level {args.level}, {args.objects} x {args.object_mib:g} MiB objects per GPU"
+        elif args.mode == "pipeline-decode":
+            workload = f"decode() level {args.level}, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "scrub":
             workload = (f"scrub() of {args.objects} level-12 streams of {args.object_mib:g} MiB objects, one "
                         f"corrupted byte each, host buffers")
@@ -860,10 +903,11 @@ def main():
                            else "synthetic (uniform random bytes) in files on the box's local disk, read and "
                                 "written through the page cache" if args.mode == "file"
                            else "synthetic (uniform random bytes), pageable host buffers (numpy / bytes)")
-        if args.mode in ("bao", "bao-decode") or (args.mode == "pipeline" and args.level & 4):
+        pipe = args.mode in ("pipeline", "pipeline-decode")
+        if args.mode in ("bao", "bao-decode") or (pipe and args.level & 4):
             # BLAKE3 compressions: one per 64-B block of content plus one per parent node;
             # 7 rounds x 8 G x 12 VALU lane-ops (a+b+m as one v_add3_u32).
-            hashed = wl.zlen if args.mode == "pipeline" else n
+            hashed = getattr(wl, "zlen", n) if pipe else n
             chunks = max(1, -(-hashed // 1024))
             comps = args.objects * (max(1, -(-hashed // 64)) + (chunks - 1))
             ops = comps * 7 * 8 * 12
@@ -877,7 +921,7 @@ def main():
                                "note": "int32 VALU peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; ops = 672 per "
                                        "BLAKE3 compression (content blocks + parents)"
                                        + ("; achieved over the whole step (every kernel of the level)"
-                                          if args.mode == "pipeline" else "")}
+                                          if pipe else "")}
         if world > 1:
             fr = [wl.alg_bytes / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS if res["roofline"]["unit"] == "GB/s" else 1)
                   for ms in rank_avg_ms]

@@ -141,6 +141,11 @@ SIGNATURES = {
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p,
                                              ctypes.c_void_p, ctypes.POINTER(EncodeInfoC), ctypes.c_void_p,
                                              ctypes.c_void_p]),
+    "chip_decode_scratch_len": (ctypes.c_uint64, [ctypes.c_uint8, ctypes.c_uint64, ctypes.c_uint64]),
+    "chip_decode_batch_dev": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                             ctypes.c_uint64, c_u64p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
     "chip_bao_slice_len": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
     "chip_bao_extract_slice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                               ctypes.c_void_p, ctypes.c_uint64, c_u64p]),

@@ -191,6 +191,7 @@ struct ChunkArgs {
     uint64_t cv_stride;
     uint8_t *hash;         // encode: root hash out (when the root is formed here); decode: expected
     uint32_t *status;      // decode only
+    uint64_t out_limit = ~0ull;  // decode: content bytes at or past it are verified, not written
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     // decode: content is 16-B aligned, store straight from the loaded registers
     auto content_step = [&](int g, const u32x4 (&v)[8]) {
         const int j = g >> 3, s = g & 7;
-        if (full_wave) {  // the loads' fast-path address pattern, in the content buffer
+        if (full_wave && (c0 + span) * 1024 <= a.out_limit) {  // the loads' fast-path address pattern, in the content buffer
             uint8_t *b = ob + (c0 + j) * 1024 + s * 128 + lane_off;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
@@ -374,8 +375,8 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
             const int cc = t * 8 + (lane >> 3);
             const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
             const uint32_t byte = (uint32_t)(s * 128 + (lane & 7) * 16);
-            if (!(wave_on && ci < a.N)) continue;
-            const uint64_t rem = a.n - ci * 1024;
+            if (!(wave_on && ci < a.N) || ci * 1024 >= a.out_limit) continue;
+            const uint64_t rem = (a.n < a.out_limit ? a.n : a.out_limit) - ci * 1024;
             const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
             if (byte >= clen) continue;
             const uint32_t valid = clen - byte;
@@ -929,7 +930,8 @@ hipError_t run_parent_levels(uint8_t *cv_prev, uint64_t stride_prev, uint64_t cn
 template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0>
 hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
-                   void *d_scratch, hipStream_t stream, size_t pad_lds = 0 /* tuning: occupancy probe */) {
+                   void *d_scratch, hipStream_t stream, size_t pad_lds = 0 /* tuning: occupancy probe */,
+                   uint64_t out_limit = ~0ull /* decode: content prefix written */) {
     if (count == 0) return hipSuccess;
     const uint64_t N = n_chunks(n);
     constexpr int LOG = ilog2(BAO_CPL);
@@ -942,6 +944,7 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
     ca.in = d_in; ca.out = d_out; ca.in_stride = in_stride; ca.out_stride = out_stride;
     ca.n = n; ca.N = N; ca.count = count; ca.cv = bufA; ca.cv_stride = strideA;
     ca.hash = d_hash; ca.status = d_status;
+    ca.out_limit = out_limit;
     const uint64_t waves = count * ((N + 64ull * BAO_CPL - 1) / (64ull * BAO_CPL));
     const uint64_t blocks = (waves + K3_WAVES - 1) / K3_WAVES;
     hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG>), dim3((unsigned)blocks),

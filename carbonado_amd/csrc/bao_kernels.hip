@@ -81,6 +81,14 @@ hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
                       d_status, d_scratch, stream);
 }
 
+hipError_t bao_decode_prefix_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                                 const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
+                                 uint32_t *d_status, void *d_scratch, hipStream_t stream) {
+    return run_bao_t<1, BAO_CPL, BAO_NTS, 0, 1, 0, BAO_XG>(d_in, in_stride, n, count, d_out, out_stride,
+                                                          const_cast<uint8_t *>(d_hash), d_status, d_scratch, stream,
+                                                          0, out_limit);
+}
+
 hipError_t bao_node_check(const uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count,
                           const uint8_t *d_hash, uint8_t *chunk_flags, uint8_t *parent_flags, hipStream_t stream) {
     return run_node_check(d_stream, stride, n, count, d_hash, chunk_flags, parent_flags, stream);

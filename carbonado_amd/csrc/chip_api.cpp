@@ -1139,9 +1139,63 @@ int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_strid
     } else if (bao) {
         CHIP_HIP(bao_encode_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_scratch, s));
     } else {  // no device stage: the encoding is the input
-        if (n) CHIP_HIP(hipMemcpy2DAsync(d_out, count > 1 ? out_stride : n, d_in, count > 1 ? in_stride : n, n, count,
-                                         hipMemcpyDeviceToDevice, s));
+        if (n) CHIP_HIP(copy_rows_dev(d_out, count > 1 ? out_stride : n, d_in, count > 1 ? in_stride : n, n, count, s));
         CHIP_HIP(hipMemsetAsync(d_hash, 0, 32 * count, s));
+    }
+    return CHIP_OK;
+}
+
+// The content length n of a bao stream of `len` bytes (bao_encoded_len is
+// strictly increasing): false when no n gives exactly `len`.
+static bool bao_content_len(uint64_t len, uint64_t *n) {
+    if (len < 8) return false;
+    uint64_t lo = 0, hi = len - 8;
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (bao_encoded_len(mid) < len) lo = mid + 1;
+        else hi = mid;
+    }
+    *n = lo;
+    return bao_encoded_len(lo) == len;
+}
+
+uint64_t chip_decode_scratch_len(uint8_t format, uint64_t in_len, uint64_t count) {
+    uint64_t n = 0;
+    if (!(format & CHIP_FORMAT_BAO) || !bao_content_len(in_len, &n)) return 16;
+    return bao_scratch_len(n, count) + 16;
+}
+
+int chip_decode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_stride, uint64_t in_len, uint64_t count,
+                          const uint8_t *d_hash, uint32_t padding, uint8_t *d_out, uint64_t out_stride,
+                          uint64_t *out_len, uint32_t *d_status, void *d_scratch, void *stream) {
+    if (has_host_stages(format) || format > 15 || !out_len) return CHIP_ERR_INVALID_ARG;
+    const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
+    if ((!d_in && in_len) || (count && !d_status) || (in_stride % 16) || (out_stride % 16) || misaligned16(d_in) ||
+        misaligned16(d_out))
+        return CHIP_ERR_INVALID_ARG;
+    if (bao && (!d_hash || !d_scratch)) return bao && !d_hash ? CHIP_ERR_HASH_DECODE : CHIP_ERR_INVALID_ARG;
+    uint64_t blen = in_len;  // bytes entering zfec (decoding.rs:90-99)
+    if (bao && !bao_content_len(in_len, &blen)) return CHIP_ERR_BAO_TRUNCATED;
+    uint64_t olen = blen;
+    if (zfec) {
+        if (blen % CHIP_FEC_M) return CHIP_ERR_UNEVEN_ZFEC_CHUNKS;  // decoding.rs:39-41
+        const uint64_t C = blen / CHIP_FEC_M;
+        if (padding > CHIP_FEC_K * C) return CHIP_ERR_ZFEC;
+        olen = CHIP_FEC_K * C - padding;  // positional shards: the primaries' bytes (decoding.rs:24-29)
+    }
+    *out_len = olen;
+    if (count == 0) return CHIP_OK;
+    if ((olen && !d_out) || (count > 1 && out_stride < olen)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    int st = use_device();
+    if (st != CHIP_OK) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    CHIP_HIP(hipMemsetAsync(d_status, 0, count * sizeof(uint32_t), s));
+    if (bao) {  // every node verified; only content bytes [0, olen) written
+        CHIP_HIP(bao_decode_prefix_dev(d_in, in_stride, blen, count, d_hash, d_out, out_stride, olen, d_status,
+                                       d_scratch, s));
+    } else if (olen) {
+        CHIP_HIP(copy_rows_dev(d_out, count > 1 ? out_stride : olen, d_in, count > 1 ? in_stride : olen, olen, count,
+                               s));
     }
     return CHIP_OK;
 }

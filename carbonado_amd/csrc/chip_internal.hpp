@@ -84,6 +84,9 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
                          uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t stream);
 // CHIP_FUSED (default 1): 0 keeps the two-kernel / K3 paths (A/B runs).
 bool fused_on();
+// `rows` rows of `width` bytes, device to device (16-B aligned pointers/pitches).
+hipError_t copy_rows_dev(uint8_t *dst, uint64_t dpitch, const uint8_t *src, uint64_t spitch, uint64_t width,
+                         uint64_t rows, hipStream_t stream);
 
 // ---- bao / BLAKE3 ------------------------------------------------------
 uint64_t bao_encoded_len(uint64_t n);
@@ -96,6 +99,11 @@ hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
 hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                           const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                           uint32_t *d_status, void *d_scratch, hipStream_t stream);
+// The same, writing only content bytes [0, out_limit) of each object (every
+// byte is still verified): decode() at Bao|Zfec keeps the data shards only.
+hipError_t bao_decode_prefix_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                                 const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
+                                 uint32_t *d_status, void *d_scratch, hipStream_t stream);
 
 // bao encode in place: the stream's chunk slots already hold the content
 // (written there by gf_apply with GfLaunch::bao_off); writes the header, the

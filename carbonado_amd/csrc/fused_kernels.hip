@@ -57,6 +57,38 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
                                             out_stride, d_hash, nullptr, stream);
 }
 
+// Row copy for the device-only levels without a kernel stage (decode at
+// Zfec only, encode at level 0): hipMemcpy2DAsync refuses device-to-device
+// copies of many-GiB batches ("invalid argument"), so a plain grid-stride
+// copy, 16 B per lane (pointers and pitches are multiples of 16 by the
+// C-ABI's rules), bytes for a ragged row end.
+static __global__ __launch_bounds__(256) void copy_rows_kernel(uint8_t *dst, uint64_t dpitch, const uint8_t *src,
+                                                               uint64_t spitch, uint64_t width, uint64_t rows) {
+    const uint64_t vec = width / 16, per_row = vec + (width % 16 ? 1 : 0), total = per_row * rows;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t r = i / per_row, c = i - r * per_row;
+        const uint8_t *s = src + r * spitch;
+        uint8_t *d = dst + r * dpitch;
+        if (c < vec) {
+            *reinterpret_cast<uint4 *>(d + 16 * c) = *reinterpret_cast<const uint4 *>(s + 16 * c);
+        } else {
+            for (uint64_t b = 16 * vec; b < width; ++b) d[b] = s[b];
+        }
+    }
+}
+
+hipError_t copy_rows_dev(uint8_t *dst, uint64_t dpitch, const uint8_t *src, uint64_t spitch, uint64_t width,
+                         uint64_t rows, hipStream_t stream) {
+    if (!width || !rows) return hipSuccess;
+    const uint64_t work = ((width + 15) / 16) * rows;
+    uint64_t grid = (work + 255) / 256;
+    const uint64_t cap = (uint64_t)num_cus() * 8;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(copy_rows_kernel, dim3((unsigned)grid), dim3(256), 0, stream, dst, dpitch, src, spitch, width,
+                       rows);
+    return hipGetLastError();
+}
+
 bool fused_on() {
     static const bool on = [] {
         const char *v = std::getenv("CHIP_FUSED");

@@ -92,7 +92,7 @@ def encode_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes:
     """encode() of device-resident objects at a level without host stages
     (Bao and/or Zfec bits): inp uint8 [count, in_stride] (first n bytes of each
     row), out uint8 [count, >= encoded length], hashes uint8 [count, 32].
-    Zfec|Bao runs fused (shards written straight into the bao streams).
+    Zfec|Bao runs fused (shards hashed on chip, written into their bao slots).
     Returns (encoded length, EncodeInfoC)."""
     assert inp.is_cuda and out.is_cuda and inp.is_contiguous() and out.is_contiguous()
     assert inp.shape[0] == out.shape[0] == hashes.shape[0] and inp.shape[1] >= n
@@ -103,6 +103,26 @@ def encode_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes:
                                            _stream()))
     assert olen.value <= out.shape[1]
     return olen.value, info
+
+
+def decode_scratch(fmt: int, in_len: int, count: int, device=None) -> torch.Tensor:
+    size = _lib.lib().chip_decode_scratch_len(fmt, in_len, count)
+    return torch.empty(size, dtype=torch.uint8, device=device or "cuda")
+
+
+def decode_batch(fmt: int, enc: torch.Tensor, in_len: int, hashes: torch.Tensor, padding: int, out: torch.Tensor,
+                 status: torch.Tensor, scratch: torch.Tensor) -> int:
+    """decode() of device-resident encodings at a level without host stages:
+    enc uint8 [count, in_stride] (first in_len bytes of each row), hashes uint8
+    [count, 32], out uint8 [count, >= decoded length], status int32 [count]
+    (0, or the chip_status of that object).  Returns the decoded length."""
+    assert enc.is_cuda and out.is_cuda and enc.is_contiguous() and out.is_contiguous()
+    assert enc.shape[0] == out.shape[0] == status.shape[0] and enc.shape[1] >= in_len
+    olen = ctypes.c_uint64()
+    check(_lib.lib().chip_decode_batch_dev(fmt, _p(enc), enc.shape[1], in_len, enc.shape[0], _p(hashes), padding,
+                                           _p(out), out.shape[1], ctypes.byref(olen), _p(status), _p(scratch),
+                                           _stream()))
+    return olen.value
 
 
 def bao_decode_batch(enc: torch.Tensor, n: int, hashes: torch.Tensor, out: torch.Tensor,

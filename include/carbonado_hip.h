@@ -346,6 +346,24 @@ CHIP_API int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t
                                    uint64_t count, uint8_t *d_out, uint64_t out_stride, uint64_t *out_len,
                                    uint8_t *d_hash, chip_encode_info *info, void *d_scratch, void *stream);
 
+/* decode() (decoding.rs:80-114) of `count` DEVICE-resident encodings of the
+ * device-only formats (Bao and/or Zfec bits; Snappy/Ecies bits give
+ * CHIP_ERR_INVALID_ARG).  Object o: the in_len-byte encoding at d_in +
+ * o*in_stride, its bao hash at d_hash + 32*o (device), all with the zfec
+ * `padding` of one chip_encode_batch_dev; decoded bytes (*out_len, the same
+ * for every object) at d_out + o*out_stride, status (0 or a chip_status:
+ * CHIP_ERR_BAO_HASH_MISMATCH for a corrupted stream or a header that
+ * disagrees with in_len) at d_status[o].  At Bao|Zfec every node of the
+ * stream is verified and only the primaries' bytes are written (the shards
+ * are indexed by position, decoding.rs:95-99: decode = the 4 data shards,
+ * padding dropped).  d_scratch: chip_decode_scratch_len(format, in_len,
+ * count) bytes.  Pointers and strides multiples of 16; enqueued on `stream`. */
+CHIP_API uint64_t chip_decode_scratch_len(uint8_t format, uint64_t in_len, uint64_t count);
+CHIP_API int chip_decode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_stride, uint64_t in_len,
+                                   uint64_t count, const uint8_t *d_hash, uint32_t padding, uint8_t *d_out,
+                                   uint64_t out_stride, uint64_t *out_len, uint32_t *d_status, void *d_scratch,
+                                   void *stream);
+
 /* ---- slices and scrub (decoding.rs:116-212) ----------------------------- */
 /* Chunk range of a bao slice request [start, start+len) over n content bytes,
  * bao's rules: at least one chunk; a start at/after the end selects the last

@@ -309,3 +309,72 @@ def test_chip_init_selects_the_process_device(gpu):
     enc, h, _ = ca.encode(b"", d, 12)
     assert (enc, h) == O.encode(d, 12)[:2]
     assert L.chip_init(0) == 0
+
+
+@pytest.mark.parametrize("n", [0, 1, 4096, 70_001, (1 << 20) + 1, 3 << 20])
+@pytest.mark.parametrize("level", [0, 4, 8, 12])
+def test_decode_batch_dev_roundtrip(gpu, level, n):
+    """chip_decode_batch_dev (device-resident decode(), decoding.rs:80-114)
+    inverts chip_encode_batch_dev at every device-only level; at Bao|Zfec only
+    the data shards are written, every node still verified.  A flipped byte
+    in one object's stream fails that object alone (status 5); its
+    neighbours decode."""
+    import torch
+    from carbonado_amd import device
+    count = 4
+    rng = np.random.default_rng(7000 + 10 * level + n % 991)
+    stride = (n + 16 + 15) // 16 * 16
+    host = rng.integers(0, 256, (count, stride), dtype=np.uint8)
+    inp = torch.from_numpy(host).cuda()
+    cap = device._lib.lib().chip_encode_max_len(n)
+    enc = torch.zeros((count, (cap + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    olen, info = device.encode_batch(level, inp, n, enc, hashes, device.encode_scratch(level, n, count))
+    out = torch.full((count, stride), 0xA5, dtype=torch.uint8, device="cuda")
+    status = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    scratch = device.decode_scratch(level, olen, count)
+    dlen = device.decode_batch(level, enc, olen, hashes, info.padding_len, out, status, scratch)
+    torch.cuda.synchronize()
+    assert dlen == n
+    assert status.cpu().tolist() == [0] * count
+    got = out.cpu().numpy()
+    for o in range(count):
+        assert got[o, :n].tobytes() == host[o, :n].tobytes(), o
+        assert (got[o, n:] == 0xA5).all(), "bytes past the decoded length were written"
+    if level & 4 and n > 0:
+        enc[1, olen // 2] ^= 1
+        out.fill_(0)
+        device.decode_batch(level, enc, olen, hashes, info.padding_len, out, status, scratch)
+        torch.cuda.synchronize()
+        assert status.cpu().tolist() == [0, 5, 0, 0]
+        for o in (0, 2, 3):
+            assert out[o, :n].cpu().numpy().tobytes() == host[o, :n].tobytes()
+
+
+def test_decode_batch_dev_errors(gpu):
+    import torch
+    from carbonado_amd import device
+    from carbonado_amd.error import BaoDecodeError, CarbonadoError, UnevenZfecChunks
+    n, count = 50_000, 2
+    inp = torch.randint(0, 256, (count, (n + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    enc = torch.zeros((count, 1 << 18), dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    olen, info = device.encode_batch(12, inp, n, enc, hashes, device.encode_scratch(12, n, count))
+    out = torch.zeros((count, 1 << 17), dtype=torch.uint8, device="cuda")
+    status = torch.zeros((count,), dtype=torch.int32, device="cuda")
+    scratch = device.decode_scratch(12, olen, count)
+    with pytest.raises(BaoDecodeError):  # no bao stream has this length (1 KiB: 1032 B, 1025 B: 1097 B)
+        device.decode_batch(12, enc, 1040, hashes, info.padding_len, out, status, scratch)
+    with pytest.raises(UnevenZfecChunks):  # a bao stream, but of zlen - 1 content bytes
+        device.decode_batch(12, enc, olen - 1, hashes, info.padding_len, out, status, scratch)
+    with pytest.raises(UnevenZfecChunks):  # zfec-only input that is not 8 shards
+        device.decode_batch(8, enc, 8 * 1024 + 3, hashes, 0, out, status, scratch)
+    with pytest.raises(CarbonadoError):  # host stages (Snappy/Ecies bits)
+        device.decode_batch(15, enc, olen, hashes, info.padding_len, out, status, scratch)
+    # a header that disagrees with in_len: the stream of a shorter object, same length
+    hdr = enc[0, :8].clone()
+    enc[0, :8] = torch.tensor(list((123).to_bytes(8, "little")), dtype=torch.uint8)
+    device.decode_batch(12, enc, olen, hashes, info.padding_len, out, status, scratch)
+    torch.cuda.synchronize()
+    assert status.cpu().tolist() == [5, 0]
+    enc[0, :8] = hdr

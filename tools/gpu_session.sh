@@ -1,7 +1,7 @@
 #!/bin/bash
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
-#   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 e2e15 e2e15full
+#   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
 #          e2e12 e2ed15 scrub hasher file15 file12 prof
 set -e -o pipefail
 TAG=$1; shift
@@ -20,6 +20,9 @@ for s in "$@"; do
     bao) run bench_bao 600 python3 bench.py --mode bao --no-cpu-baseline ;;
     baodec) run bench_bao_decode 600 python3 bench.py --mode bao-decode --cpu-seconds 8 ;;
     pipe12) run bench_pipe12 600 python3 bench.py --mode pipeline --level 12 --verify-all ;;
+    pdec12) run bench_pdec12 600 python3 bench.py --mode pipeline-decode --level 12 ;;
+    pdec4) run bench_pdec4 600 python3 bench.py --mode pipeline-decode --level 4 ;;
+    pdec8) run bench_pdec8 600 python3 bench.py --mode pipeline-decode --level 8 ;;
     pipe12old) CHIP_FUSED=0 run bench_pipe12_twokernel 600 python3 bench.py --mode pipeline --level 12 --no-cpu-baseline ;;
     e2e15) run bench_e2e15 600 python3 bench.py --mode e2e --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     e2e15full) run bench_e2e15_full 900 python3 bench.py --config cfg4 --steps 3 --warmup 1 --cpu-seconds 8 ;;
