@@ -66,6 +66,9 @@ hipError_t gf_apply(const GfPlan &plan, const GfLaunch &L, hipStream_t stream);
 // Device copy of the packed parity table of a k-of-m encode (m - k <= 4):
 // [k][256] dwords, byte r of entry [s][x] = E[k + r][s] * x (cached).
 hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out);
+// Per-stream block of zeroed run-queue counters (2 KiB) shared by the
+// persistent kernels launched on that stream.
+hipError_t stream_queue(hipStream_t stream, uint32_t **out);
 
 // ---- K13: encode() at Zfec|Bao in one pass (fused_kernels.hip) ----------
 // `count` objects of n bytes (zero padded to 4C) -> bao streams of their

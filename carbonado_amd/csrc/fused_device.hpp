@@ -59,6 +59,7 @@ struct FusedArgs {
     const uint32_t *table;          // [4][256] packed parity products (4 parity rows per dword)
     const uint64_t *coff;           // [N] stream offset of each chunk (bao_chunk_table)
     uint8_t *cv;                    // level-0 CVs [count][N], or level-3 CVs [count][N/8] (FULL)
+    uint32_t *queue;                // block queue (DQ): [0] next block, [32] waves done; zero at launch
 };
 
 __device__ __forceinline__ int dofs(int step) { return 4 + (step & 1) * 32; }
@@ -144,7 +145,7 @@ struct Tree {
 // bao of the content itself (encode() level 8, FULL only: 64 | N, every chunk
 // whole).  KIND 1's block is 64 consecutive chunks (row / hash lane
 // L = chunk ub + L), loaded 8 x 16 B per lane per step instead of computed.
-template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0>
+template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -203,10 +204,20 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     };
 
     Tree<NT> tree(lane, a.cv);
-    uint64_t blk = (uint64_t)blockIdx.x * FW + wave;
+    // Blocks: DQ takes them from a queue (one atomic per block and wave, lane
+    // 0, vector memory), so waves on slower XCDs simply take fewer; otherwise
+    // a static stride of GW.  The next block is known before the current one
+    // starts, for its first loads at step 7.
+    auto grab = [&]() -> uint64_t {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(a.queue, 1u);
+        return (uint64_t)__builtin_amdgcn_readfirstlane(b);
+    };
+    uint64_t blk = DQ ? grab() : (uint64_t)blockIdx.x * FW + wave;
     u32x4 v[NV];
     if (blk < total) load_step(blk, 0, v);
-    for (; blk < total; blk += GW) {
+    for (uint64_t nxt; blk < total; blk = nxt) {
+        nxt = DQ ? grab() : blk + GW;
         const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * BW;
         uint8_t *ob = a.out + obj * a.out_stride;
         if (ub == 0 && lane == 0)  // u64 LE content length
@@ -283,7 +294,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
 
             auto next_loads = [&]() {
                 if (s < 7) load_step(blk, s + 1, v);
-                else if (blk + GW < total) load_step(blk + GW, 0, v);
+                else if (nxt < total) load_step(nxt, 0, v);
             };
             if (ORD == 2) next_loads();  // as soon as v is free: two compressions of cover
 
@@ -376,6 +387,13 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         uint32_t z[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
         tree.step(z, nullptr, 0, false);
         tree.step(z, nullptr, 0, false);
+    }
+    if (DQ && lane == 0) {  // the last wave out leaves the queue zero for the next launch
+        const uint32_t done = atomicAdd(a.queue + 32, 1u);
+        if (done + 1 == gridDim.x * (uint32_t)FW) {
+            a.queue[0] = 0u;
+            a.queue[32] = 0u;
+        }
     }
 }
 

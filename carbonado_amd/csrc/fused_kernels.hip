@@ -3,6 +3,7 @@
 #include "chip_internal.hpp"
 #include "fused_device.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace chip {
@@ -12,13 +13,41 @@ uint64_t zfec_bao_scratch_len(uint64_t zlen, uint64_t count) {
     return count * 32 * (N + (N + 1) / 2);
 }
 
+namespace {
+
+// One launch per part of the batch small enough for the kernel's 32-bit block
+// queue (< 2^31 blocks; a part is whole objects).  cv_nodes: CVs per object
+// the kernel writes into a.cv.
+hipError_t launch_parts(const fused::FusedArgs &a, uint64_t cv_nodes, void (*kern)(fused::FusedArgs),
+                        hipStream_t stream) {
+    using namespace fused;
+    const uint64_t per = std::max<uint64_t>(1, (1ull << 31) / std::max<uint64_t>(1, a.bpo));
+    for (uint64_t o0 = 0; o0 < a.count; o0 += per) {
+        FusedArgs p = a;
+        p.count = std::min(per, a.count - o0);
+        p.in = a.in + o0 * a.in_stride;
+        p.out = a.out + o0 * a.out_stride;
+        p.cv = a.cv + o0 * cv_nodes * 32;
+        const uint64_t blocks = p.count * p.bpo;
+        uint64_t grid = (blocks + FW - 1) / FW;
+        const uint64_t cap = (uint64_t)num_cus();  // one workgroup (8 waves) per CU fits the LDS
+        if (grid > cap) grid = cap;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, p);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
 hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
                               uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,
                               hipStream_t stream) {
     if (count == 0) return hipSuccess;
     if (C == 0 || C % 1024) return hipErrorInvalidValue;
     using namespace fused;
-    FusedArgs a;
+    FusedArgs a{};
     a.in = d_in; a.in_stride = in_stride; a.valid = n; a.C = C;
     a.out = d_out; a.out_stride = out_stride;
     a.count = count;
@@ -33,6 +62,9 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     if ((e = bao_chunk_table(a.N, &coff)) != hipSuccess) return e;
     a.coff = coff;
     a.cv = static_cast<uint8_t *>(d_scratch);
+    uint32_t *q = nullptr;
+    if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
+    a.queue = q + 512;
     const bool full = a.cols % 8 == 0 && n >= 4 * C;  // levels 1-3 in the kernel (N >= 64, 8 subtrees a block)
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<true, true>),
@@ -42,16 +74,10 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     }();
     (void)attr;
     (void)hipGetLastError();
-    const uint64_t blocks = count * a.bpo;
-    uint64_t grid = (blocks + FW - 1) / FW;
-    const uint64_t cap = (uint64_t)num_cus();  // one workgroup (8 waves) per CU fits the LDS
-    if (grid > cap) grid = cap;
-    if (full)
-        hipLaunchKernelGGL((zfec_bao_fused_kernel<true, true>), dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
-    else
-        hipLaunchKernelGGL((zfec_bao_fused_kernel<true, false>), dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint64_t n0 = full ? a.N / 8 : a.N;  // nodes per object in `cv`
+    if ((e = launch_parts(a, n0, full ? zfec_bao_fused_kernel<true, true> : zfec_bao_fused_kernel<true, false>,
+                          stream)) != hipSuccess)
+        return e;
     uint8_t *next = a.cv + count * n0 * 32;
     return bao::run_parent_levels<0, false>(a.cv, n0, n0, full ? 4 : 1, next, (n0 + 1) / 2, a.N, count, d_out,
                                             out_stride, d_hash, nullptr, stream);
@@ -120,6 +146,9 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     if (e != hipSuccess) return e;
     a.coff = coff;
     a.cv = static_cast<uint8_t *>(d_scratch);
+    uint32_t *q = nullptr;
+    if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
+    a.queue = q + 512;
     constexpr auto K = zfec_bao_fused_kernel<true, true, 1, 0, 1>;
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(K), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -127,13 +156,8 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     }();
     (void)attr;
     (void)hipGetLastError();
-    const uint64_t blocks = count * a.bpo;
-    uint64_t grid = (blocks + FW - 1) / FW;
-    const uint64_t cap = (uint64_t)num_cus();
-    if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(K, dim3((unsigned)grid), dim3(FTPB), LDS_BYTES, stream, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint64_t n3 = a.N / 8;  // level-3 CVs per object
+    if ((e = launch_parts(a, n3, K, stream)) != hipSuccess) return e;
     uint8_t *next = a.cv + count * n3 * 32;
     return bao::run_parent_levels<0, false>(a.cv, n3, n3, 4, next, (n3 + 1) / 2, a.N, count, d_out, out_stride,
                                             d_hash, nullptr, stream);

@@ -350,6 +350,10 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
 
 }  // namespace
 
+// The stream's run-queue block for other persistent kernels (K13 uses words
+// 512 and 544, clear of K1's counters; each launch leaves its words zero).
+hipError_t stream_queue(hipStream_t stream, uint32_t **out) { return queue_for(stream, out); }
+
 hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out) {
     if (k == 0 || m <= k || m - k > 4) return hipErrorInvalidValue;
     const std::vector<uint8_t> enc = zfec_enc_matrix(k, m);

@@ -73,20 +73,27 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&dcoff[k], N * 8));
         CK(hipMemcpy(dcoff[k], coff.data(), N * 8, hipMemcpyHostToDevice));
     }
+    uint32_t *dq;
+    CK(hipMalloc(&dq, 4096));
+    CK(hipMemset(dq, 0, 4096));
     fused::FusedArgs A[2];
     for (int k = 0; k < 2; ++k) {
         fused::FusedArgs &a = A[k];
         a = fused::FusedArgs{};
         a.in = in; a.in_stride = n; a.valid = n; a.C = k ? 0 : C; a.out = out; a.out_stride = bstride;
         a.count = count; a.N = k ? N1 : N0; a.cols = k ? 0 : C / 1024; a.bpo = k ? N1 / 64 : (C / 1024 + 7) / 8;
-        a.table = dtab; a.coff = dcoff[k]; a.cv = cv;
+        a.table = dtab; a.coff = dcoff[k]; a.cv = cv; a.queue = dq;
     }
     const char *which = argc > 3 ? argv[3] : "all";
     std::vector<Variant> all = {
         {"K0 FULL (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
+        {"K0 FULL static blocks", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, false>, 0},
         {"K0 general", fused::zfec_bao_fused_kernel<true, false, 1, 0, 0>, 0},
+        {"K0 general static blocks", fused::zfec_bao_fused_kernel<true, false, 1, 0, 0, false>, 0},
         {"K1 (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1>, 1},
-        {"K1 ORD2", fused::zfec_bao_fused_kernel<true, true, 2, 0, 1>, 1},
+        {"K1 static blocks", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1, false>, 1},
+        {"K0 DG1 no stores", fused::zfec_bao_fused_kernel<true, true, 1, 1, 0>, 0},
+        {"K0 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 0>, 0},
         {"K1 DG1 no stores", fused::zfec_bao_fused_kernel<true, true, 1, 1, 1>, 1},
         {"K1 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 1>, 1}};
     std::vector<Variant> vs;
