@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <utility>
 
@@ -192,6 +193,7 @@ struct ChunkArgs {
     uint8_t *hash;         // encode: root hash out (when the root is formed here); decode: expected
     uint32_t *status;      // decode only
     uint64_t out_limit = ~0ull;  // decode: content bytes at or past it are verified, not written
+    uint32_t *queue = nullptr;   // DQ: [0] next wave task, [32] waves done
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -278,7 +280,8 @@ __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x
 // after (0) the next step's prefetch loads.
 // XG 1: XCD-grouped block order (block b runs logical block (b % 8) * (B/8) + b/8,
 // so each XCD sweeps one contiguous eighth of the batch; B % 8 == 0 only).
-template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0>
+// DQ: persistent grid, wave tasks from the run queue a.queue (zero at launch).
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0, bool DQ = false>
 __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     constexpr int LOG = ilog2(CPL);
     constexpr int NSTEP = 8 * CPL;
@@ -293,240 +296,297 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
     const uint64_t span = 64ull * CPL;
     const uint64_t tpo = (a.N + span - 1) / span;
     uint64_t blk = blockIdx.x;
-    if (XG && (gridDim.x & 7) == 0) blk = (blk & 7) * (gridDim.x >> 3) + (blk >> 3);
-    const uint64_t wt = blk * K3_WAVES + wave;
-    const bool wave_on = wt < a.count * tpo;
-    const uint64_t obj = wave_on ? wt / tpo : 0;
-    const uint64_t c0 = wave_on ? (wt - obj * tpo) * span : 0;
-    const uint64_t lb = c0 + (uint64_t)lane * CPL;  // my first chunk
-    const uint64_t nmine = (wave_on && lb < a.N) ? ((a.N - lb) < (uint64_t)CPL ? (a.N - lb) : (uint64_t)CPL) : 0;
-    const uint8_t *ib = a.in + obj * a.in_stride;
-    uint8_t *ob = a.out ? a.out + obj * a.out_stride : nullptr;
-    uint32_t *st = stage[wave];
+    if (!DQ && XG && (gridDim.x & 7) == 0) blk = (blk & 7) * (gridDim.x >> 3) + (blk >> 3);
+    // DQ: wave tasks from a run queue (one atomic per task, lane 0; vector
+    // memory), persistent grid: the slower XCDs take fewer tasks.  Otherwise
+    // one task per wave of the grid.
+    const uint64_t ntasks = a.count * tpo;
+    auto grab = [&]() -> uint64_t {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(a.queue, 1u);
+        return (uint64_t)__builtin_amdgcn_readfirstlane(b);
+    };
+    for (uint64_t wt = DQ ? grab() : blk * K3_WAVES + wave;; wt = grab()) {
+        if (DQ && wt >= ntasks) break;
+        const bool wave_on = wt < a.count * tpo;
+        const uint64_t obj = wave_on ? wt / tpo : 0;
+        const uint64_t c0 = wave_on ? (wt - obj * tpo) * span : 0;
+        const uint64_t lb = c0 + (uint64_t)lane * CPL;  // my first chunk
+        const uint64_t nmine = (wave_on && lb < a.N) ? ((a.N - lb) < (uint64_t)CPL ? (a.N - lb) : (uint64_t)CPL) : 0;
+        const uint8_t *ib = a.in + obj * a.in_stride;
+        uint8_t *ob = a.out ? a.out + obj * a.out_stride : nullptr;
+        uint32_t *st = stage[wave];
 
-    uint64_t my_off = nmine ? chunk_stream_off(lb, a.N) : 0;  // stream offset of my current chunk
-    soff[0][wave][lane] = my_off;
-    if ((MODE == 0 || MODE == 3) && ob && wave_on && c0 == 0 && lane == 0)  // u64 LE content-length header
-        *reinterpret_cast<uint64_t *>(ob) = a.n;
-    if ((MODE == 1 || MODE == 2) && wave_on && c0 == 0 && lane == 0 && *reinterpret_cast<const uint64_t *>(ib) != a.n && a.status)
-        flag_mismatch(a.status, obj);  // header disagrees with the batch's content length
-    wave_sync();
+        uint64_t my_off = nmine ? chunk_stream_off(lb, a.N) : 0;  // stream offset of my current chunk
+        soff[0][wave][lane] = my_off;
+        if ((MODE == 0 || MODE == 3) && ob && wave_on && c0 == 0 && lane == 0)  // u64 LE content-length header
+            *reinterpret_cast<uint64_t *>(ob) = a.n;
+        if ((MODE == 1 || MODE == 2) && wave_on && c0 == 0 && lane == 0 && *reinterpret_cast<const uint64_t *>(ib) != a.n && a.status)
+            flag_mismatch(a.status, obj);  // header disagrees with the batch's content length
+        wave_sync();
 
-    // Fast path: every chunk of this wave is a full 1 KiB chunk of the object
-    // (all but the last wave of an object), so no per-load bounds logic: the
-    // content address is a wave-uniform base + a per-lane constant + t*8*CPL KiB,
-    // and stream-mode chunk offsets are fetched from LDS once per chunk round.
-    const bool full_wave = wave_on && c0 + span <= a.n / 1024;
-    const uint32_t lane_off = (uint32_t)((lane & 7) * 16 + (lane >> 3) * CPL * 1024);
-    uint64_t soff_t[8];  // MODE != 0: stream offset of chunk t*8 + lane/8 of the current round
-    // loader view: step g covers chunk j = g/8 of every lane, bytes [128*(g%8), +128)
-    auto load_step = [&](int g, u32x4 (&v)[8]) {
-        const int j = g >> 3, s = g & 7;
-        if (full_wave) {
-            if (MODE == 0) {
-                const uint8_t *b = ib + (c0 + j) * 1024 + s * 128 + lane_off;
-#pragma unroll
-                for (int t = 0; t < 8; ++t)
-                    v[t] = *reinterpret_cast<const u32x4 *>(b + (uint64_t)t * 8 * CPL * 1024);
-            } else {
-                if (s == 0) {
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) soff_t[t] = soff[j & 1][wave][t * 8 + (lane >> 3)];
+        // Fast path: every chunk of this wave is a full 1 KiB chunk of the object
+        // (all but the last wave of an object), so no per-load bounds logic: the
+        // content address is a wave-uniform base + a per-lane constant + t*8*CPL KiB,
+        // and stream-mode chunk offsets are fetched from LDS once per chunk round.
+        const bool full_wave = wave_on && c0 + span <= a.n / 1024;
+        const uint32_t lane_off = (uint32_t)((lane & 7) * 16 + (lane >> 3) * CPL * 1024);
+        uint64_t soff_t[8];  // MODE != 0: stream offset of chunk t*8 + lane/8 of the current round
+        // loader view: step g covers chunk j = g/8 of every lane, bytes [128*(g%8), +128)
+        auto load_step = [&](int g, u32x4 (&v)[8]) {
+            const int j = g >> 3, s = g & 7;
+            if (full_wave) {
+                if (MODE == 0) {
+                    const uint8_t *b = ib + (c0 + j) * 1024 + s * 128 + lane_off;
+    #pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        v[t] = *reinterpret_cast<const u32x4 *>(b + (uint64_t)t * 8 * CPL * 1024);
+                } else {
+                    if (s == 0) {
+    #pragma unroll
+                        for (int t = 0; t < 8; ++t) soff_t[t] = soff[j & 1][wave][t * 8 + (lane >> 3)];
+                    }
+                    const uint8_t *b = ib + s * 128 + (lane & 7) * 16;
+    #pragma unroll
+                    for (int t = 0; t < 8; ++t) v[t] = load16_a8(b + soff_t[t]);
                 }
-                const uint8_t *b = ib + s * 128 + (lane & 7) * 16;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) v[t] = load16_a8(b + soff_t[t]);
+                return;
             }
-            return;
-        }
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int cc = t * 8 + (lane >> 3);
-            const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
-            const uint32_t byte = (uint32_t)(s * 128 + (lane & 7) * 16);
-            v[t] = u32x4{0u, 0u, 0u, 0u};
-            if (wave_on && ci < a.N) {
+    #pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int cc = t * 8 + (lane >> 3);
+                const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
+                const uint32_t byte = (uint32_t)(s * 128 + (lane & 7) * 16);
+                v[t] = u32x4{0u, 0u, 0u, 0u};
+                if (wave_on && ci < a.N) {
+                    const uint64_t rem = a.n - ci * 1024;
+                    const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+                    if (byte < clen) {
+                        const uint32_t valid = clen - byte;
+                        const uint8_t *src = MODE == 0 ? ib + ci * 1024 + byte : ib + soff[j & 1][wave][cc] + byte;  // 1, 2: stream
+                        if (valid >= 16) v[t] = MODE == 0 ? *reinterpret_cast<const u32x4 *>(src) : load16_a8(src);
+                        else v[t] = load16_partial(src, valid);
+                    }
+                }
+            }
+        };
+        // decode: content is 16-B aligned, store straight from the loaded registers
+        auto content_step = [&](int g, const u32x4 (&v)[8]) {
+            const int j = g >> 3, s = g & 7;
+            if (full_wave && (c0 + span) * 1024 <= a.out_limit) {  // the loads' fast-path address pattern, in the content buffer
+                uint8_t *b = ob + (c0 + j) * 1024 + s * 128 + lane_off;
+    #pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    u32x4 *q = reinterpret_cast<u32x4 *>(b + (uint64_t)t * 8 * CPL * 1024);
+                    if (NTS) __builtin_nontemporal_store(v[t], q);
+                    else *q = v[t];
+                }
+                return;
+            }
+    #pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int cc = t * 8 + (lane >> 3);
+                const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
+                const uint32_t byte = (uint32_t)(s * 128 + (lane & 7) * 16);
+                if (!(wave_on && ci < a.N) || ci * 1024 >= a.out_limit) continue;
+                const uint64_t rem = (a.n < a.out_limit ? a.n : a.out_limit) - ci * 1024;
+                const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+                if (byte >= clen) continue;
+                const uint32_t valid = clen - byte;
+                uint8_t *dst = ob + ci * 1024 + byte;
+                if (valid >= 16) {
+                    if (NTS) __builtin_nontemporal_store(v[t], reinterpret_cast<u32x4 *>(dst));
+                    else *reinterpret_cast<u32x4 *>(dst) = v[t];
+                } else {
+                    store16_partial(dst, v[t], valid);
+                }
+            }
+        };
+        // encode: chunks sit at stream offsets = 8 (mod 16), so lane g of a chunk's
+        // 8-lane group emits the 16-B ALIGNED piece k = 8s+g covering chunk bytes
+        // [16k-8, 16k+8): the previous step's last 8 bytes live in the row's carry
+        // words, so every full piece is one aligned dwordx4 store read from LDS.
+        // Chunk head (k = 0) and tail (k = 64) are 8-byte halves.
+        // SP 0: stores of the issuing wave's own rows (wv = wave)
+        auto stream_step = [&](int wv, int g) {
+            const int j = g >> 3, s = g & 7, gl = lane & 7;
+            const uint64_t wt_w = blk * K3_WAVES + wv;
+            const bool on_w = wt_w < a.count * tpo;
+            const uint64_t obj_w = on_w ? wt_w / tpo : 0;
+            const uint64_t c0_w = on_w ? (wt_w - obj_w * tpo) * span : 0;
+            uint8_t *ob_w = a.out + obj_w * a.out_stride;
+            const uint32_t *st_w = stage[wv];
+    #pragma unroll 1
+            for (int t = 0; t < 8; ++t) {
+                const int cc = t * 8 + (lane >> 3);
+                const uint64_t ci = c0_w + (uint64_t)cc * CPL + j;
+                if (!(on_w && ci < a.N)) continue;
                 const uint64_t rem = a.n - ci * 1024;
                 const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
-                if (byte < clen) {
-                    const uint32_t valid = clen - byte;
-                    const uint8_t *src = MODE == 0 ? ib + ci * 1024 + byte : ib + soff[j & 1][wave][cc] + byte;  // 1, 2: stream
-                    if (valid >= 16) v[t] = MODE == 0 ? *reinterpret_cast<const u32x4 *>(src) : load16_a8(src);
-                    else v[t] = load16_partial(src, valid);
+                uint8_t *base = ob_w + soff[j & 1][wv][cc];
+                const uint32_t *w = st_w + cc * RW + 2 + 4 * gl;  // carry/previous half, then this piece
+                const int lo = 16 * (8 * s + gl) - 8;             // chunk byte of the piece's first half
+                if (clen == 1024) {
+                    if (lo >= 0) {
+                        const u32x2 x = *reinterpret_cast<const u32x2 *>(w);
+                        const u32x2 y = *reinterpret_cast<const u32x2 *>(w + 2);
+                        const u32x4 v = {x.x, x.y, y.x, y.y};
+                        if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(base + lo));
+                        else *reinterpret_cast<u32x4 *>(base + lo) = v;
+                    } else {  // head: chunk bytes [0, 8)
+                        store8<NTS>(base, *reinterpret_cast<const u32x2 *>(w + 2));
+                    }
+                    if (s == 7 && gl == 7)  // tail: chunk bytes [1016, 1024)
+                        store8<NTS>(base + 1016, *reinterpret_cast<const u32x2 *>(w + 4));
+                } else {  // short last chunk of the object: byte stores
+                    for (int q = 0; q < 16; ++q) {
+                        const int cb = lo + q;
+                        if (cb >= 0 && (uint32_t)cb < clen)
+                            base[cb] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+                    }
+                    if (s == 7 && gl == 7)
+                        for (int q = 0; q < 8; ++q)
+                            if (1016u + q < clen) base[1016 + q] = (uint8_t)(w[4 + (q >> 2)] >> (8 * (q & 3)));
                 }
             }
-        }
-    };
-    // decode: content is 16-B aligned, store straight from the loaded registers
-    auto content_step = [&](int g, const u32x4 (&v)[8]) {
-        const int j = g >> 3, s = g & 7;
-        if (full_wave && (c0 + span) * 1024 <= a.out_limit) {  // the loads' fast-path address pattern, in the content buffer
-            uint8_t *b = ob + (c0 + j) * 1024 + s * 128 + lane_off;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                u32x4 *q = reinterpret_cast<u32x4 *>(b + (uint64_t)t * 8 * CPL * 1024);
-                if (NTS) __builtin_nontemporal_store(v[t], q);
-                else *q = v[t];
-            }
-            return;
-        }
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int cc = t * 8 + (lane >> 3);
-            const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
-            const uint32_t byte = (uint32_t)(s * 128 + (lane & 7) * 16);
-            if (!(wave_on && ci < a.N) || ci * 1024 >= a.out_limit) continue;
-            const uint64_t rem = (a.n < a.out_limit ? a.n : a.out_limit) - ci * 1024;
-            const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
-            if (byte >= clen) continue;
-            const uint32_t valid = clen - byte;
-            uint8_t *dst = ob + ci * 1024 + byte;
-            if (valid >= 16) {
-                if (NTS) __builtin_nontemporal_store(v[t], reinterpret_cast<u32x4 *>(dst));
-                else *reinterpret_cast<u32x4 *>(dst) = v[t];
-            } else {
-                store16_partial(dst, v[t], valid);
-            }
-        }
-    };
-    // encode: chunks sit at stream offsets = 8 (mod 16), so lane g of a chunk's
-    // 8-lane group emits the 16-B ALIGNED piece k = 8s+g covering chunk bytes
-    // [16k-8, 16k+8): the previous step's last 8 bytes live in the row's carry
-    // words, so every full piece is one aligned dwordx4 store read from LDS.
-    // Chunk head (k = 0) and tail (k = 64) are 8-byte halves.
-    // SP 0: stores of the issuing wave's own rows (wv = wave)
-    auto stream_step = [&](int wv, int g) {
-        const int j = g >> 3, s = g & 7, gl = lane & 7;
-        const uint64_t wt_w = blk * K3_WAVES + wv;
-        const bool on_w = wt_w < a.count * tpo;
-        const uint64_t obj_w = on_w ? wt_w / tpo : 0;
-        const uint64_t c0_w = on_w ? (wt_w - obj_w * tpo) * span : 0;
-        uint8_t *ob_w = a.out + obj_w * a.out_stride;
-        const uint32_t *st_w = stage[wv];
-#pragma unroll 1
-        for (int t = 0; t < 8; ++t) {
-            const int cc = t * 8 + (lane >> 3);
-            const uint64_t ci = c0_w + (uint64_t)cc * CPL + j;
-            if (!(on_w && ci < a.N)) continue;
-            const uint64_t rem = a.n - ci * 1024;
-            const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
-            uint8_t *base = ob_w + soff[j & 1][wv][cc];
-            const uint32_t *w = st_w + cc * RW + 2 + 4 * gl;  // carry/previous half, then this piece
-            const int lo = 16 * (8 * s + gl) - 8;             // chunk byte of the piece's first half
-            if (clen == 1024) {
-                if (lo >= 0) {
-                    const u32x2 x = *reinterpret_cast<const u32x2 *>(w);
-                    const u32x2 y = *reinterpret_cast<const u32x2 *>(w + 2);
-                    const u32x4 v = {x.x, x.y, y.x, y.y};
-                    if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(base + lo));
-                    else *reinterpret_cast<u32x4 *>(base + lo) = v;
-                } else {  // head: chunk bytes [0, 8)
-                    store8<NTS>(base, *reinterpret_cast<const u32x2 *>(w + 2));
-                }
-                if (s == 7 && gl == 7)  // tail: chunk bytes [1016, 1024)
-                    store8<NTS>(base + 1016, *reinterpret_cast<const u32x2 *>(w + 4));
-            } else {  // short last chunk of the object: byte stores
-                for (int q = 0; q < 16; ++q) {
-                    const int cb = lo + q;
-                    if (cb >= 0 && (uint32_t)cb < clen)
-                        base[cb] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
-                }
-                if (s == 7 && gl == 7)
-                    for (int q = 0; q < 8; ++q)
-                        if (1016u + q < clen) base[1016 + q] = (uint8_t)(w[4 + (q >> 2)] >> (8 * (q & 3)));
-            }
-        }
-    };
-
-    // encode, SP 1: straight from the loaded registers.  Lane g of a chunk's
-    // 8-lane group holds chunk bytes [128s+16g, +16) at stream offset 8 (mod 16);
-    // it stores the ALIGNED 16 B [128s+16g+8, +16) = its upper half + the next
-    // lane's lower half (DPP row_shl:1), lane 0 adds the 8-B head of the step
-    // and lane 7 the 8-B tail, so a step needs no bytes of its neighbours.
-    auto stream_regs = [&](int g, const u32x4 (&v)[8]) {
-        const int j = g >> 3, s = g & 7, gl = lane & 7;
-        uint64_t bo[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) bo[t] = soff[j & 1][wave][t * 8 + (lane >> 3)];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v[t].x, 0x101, 0xF, 0xF, false);
-            const uint32_t ny = __builtin_amdgcn_update_dpp(0u, v[t].y, 0x101, 0xF, 0xF, false);
-            const int cc = t * 8 + (lane >> 3);
-            const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
-            if (!(wave_on && ci < a.N)) continue;
-            const uint64_t rem = a.n - ci * 1024;
-            const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
-            if (SP == 2) {
-                uint8_t *q = ob + (bo[t] & ~127ull) + 128 * s + 16 * gl;
-                if (clen == 1024) *reinterpret_cast<u32x4 *>(q) = v[t];
-                continue;
-            }
-            uint8_t *p = ob + bo[t] + 128 * s + 16 * gl;
-            if (clen == 1024) {
-                if (gl < 7) {
-                    const u32x4 o = {v[t].z, v[t].w, nx, ny};
-                    if (NTS) __builtin_nontemporal_store(o, reinterpret_cast<u32x4 *>(p + 8));
-                    else *reinterpret_cast<u32x4 *>(p + 8) = o;
-                }
-                if (gl == 0 || gl == 7)
-                    store8<NTS>(gl == 0 ? p : p + 8, gl == 0 ? u32x2{v[t].x, v[t].y} : u32x2{v[t].z, v[t].w});
-            } else {  // short last chunk of the object
-                const uint32_t cb = 128u * s + 16u * gl;
-                if (cb < clen) store16_partial(p, v[t], clen - cb);
-            }
-        }
-    };
-
-    // encode, SP 3: chunk bytes x live in the row at word dofs(x >> 7) + (x & 127) / 4.
-    // The stream lines (128-B aligned in stream space) inside a chunk start at
-    // chunk byte d + 128 t, d = (-base) mod 128; at step s the line ending at
-    // d + 128 s is complete (its first part is in the other half of the row).
-    uint32_t diag = 0;  // SE 2 diagnostic sink
-    uint8_t *lsp[8];  // SP 3 fast path: stream address and line phase of chunk t*8 + lane/8, per round
-    uint32_t ldd[8];
-    auto stream_lines = [&](int g) {
-        const int j = g >> 3, s = g & 7, gl = lane & 7;
-        auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x (8-aligned)
-            return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
         };
-        if (full_wave) {  // all chunks full: per-chunk values computed once per round
-            if (s == 0) {
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    lsp[t] = ob + soff[j & 1][wave][t * 8 + (lane >> 3)];
-                    ldd[t] = (uint32_t)(-(uintptr_t)lsp[t]) & 127u;
+
+        // encode, SP 1: straight from the loaded registers.  Lane g of a chunk's
+        // 8-lane group holds chunk bytes [128s+16g, +16) at stream offset 8 (mod 16);
+        // it stores the ALIGNED 16 B [128s+16g+8, +16) = its upper half + the next
+        // lane's lower half (DPP row_shl:1), lane 0 adds the 8-B head of the step
+        // and lane 7 the 8-B tail, so a step needs no bytes of its neighbours.
+        auto stream_regs = [&](int g, const u32x4 (&v)[8]) {
+            const int j = g >> 3, s = g & 7, gl = lane & 7;
+            uint64_t bo[8];
+    #pragma unroll
+            for (int t = 0; t < 8; ++t) bo[t] = soff[j & 1][wave][t * 8 + (lane >> 3)];
+    #pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v[t].x, 0x101, 0xF, 0xF, false);
+                const uint32_t ny = __builtin_amdgcn_update_dpp(0u, v[t].y, 0x101, 0xF, 0xF, false);
+                const int cc = t * 8 + (lane >> 3);
+                const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
+                if (!(wave_on && ci < a.N)) continue;
+                const uint64_t rem = a.n - ci * 1024;
+                const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+                if (SP == 2) {
+                    uint8_t *q = ob + (bo[t] & ~127ull) + 128 * s + 16 * gl;
+                    if (clen == 1024) *reinterpret_cast<u32x4 *>(q) = v[t];
+                    continue;
+                }
+                uint8_t *p = ob + bo[t] + 128 * s + 16 * gl;
+                if (clen == 1024) {
+                    if (gl < 7) {
+                        const u32x4 o = {v[t].z, v[t].w, nx, ny};
+                        if (NTS) __builtin_nontemporal_store(o, reinterpret_cast<u32x4 *>(p + 8));
+                        else *reinterpret_cast<u32x4 *>(p + 8) = o;
+                    }
+                    if (gl == 0 || gl == 7)
+                        store8<NTS>(gl == 0 ? p : p + 8, gl == 0 ? u32x2{v[t].x, v[t].y} : u32x2{v[t].z, v[t].w});
+                } else {  // short last chunk of the object
+                    const uint32_t cb = 128u * s + 16u * gl;
+                    if (cb < clen) store16_partial(p, v[t], clen - cb);
                 }
             }
-#pragma unroll SU
+        };
+
+        // encode, SP 3: chunk bytes x live in the row at word dofs(x >> 7) + (x & 127) / 4.
+        // The stream lines (128-B aligned in stream space) inside a chunk start at
+        // chunk byte d + 128 t, d = (-base) mod 128; at step s the line ending at
+        // d + 128 s is complete (its first part is in the other half of the row).
+        uint32_t diag = 0;  // SE 2 diagnostic sink
+        uint8_t *lsp[8];  // SP 3 fast path: stream address and line phase of chunk t*8 + lane/8, per round
+        uint32_t ldd[8];
+        auto stream_lines = [&](int g) {
+            const int j = g >> 3, s = g & 7, gl = lane & 7;
+            auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x (8-aligned)
+                return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
+            };
+            if (full_wave) {  // all chunks full: per-chunk values computed once per round
+                if (s == 0) {
+    #pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        lsp[t] = ob + soff[j & 1][wave][t * 8 + (lane >> 3)];
+                        ldd[t] = (uint32_t)(-(uintptr_t)lsp[t]) & 127u;
+                    }
+                }
+    #pragma unroll SU
+                for (int t = 0; t < 8; ++t) {
+                    uint8_t *sp = lsp[t];
+                    const uint32_t d = ldd[t];
+                    const uint32_t *row = st + (t * 8 + (lane >> 3)) * RW;
+                    if (s >= 1) {  // the whole line [d + 128(s-1), d + 128 s)
+                        const uint32_t x = d + 128u * (s - 1) + 16u * gl;
+                        if constexpr (SE == 3) {  // diagnostic (tools/bao_tune): the stores without the LDS reads
+                            *reinterpret_cast<u32x4 *>(sp + x) = u32x4{x, d, x, d};
+                            continue;
+                        }
+                        if constexpr (SE == 4) {  // diagnostic: as 3, every wave rewriting the same 8 KiB (L2 hits)
+                            *reinterpret_cast<u32x4 *>(ob + t * 1024 + lane * 16) = u32x4{x, d, x, d};
+                            continue;
+                        }
+                        if constexpr (SE == 5) {  // diagnostic: as 3, half the stores
+                            if (t & 1) continue;
+                            *reinterpret_cast<u32x4 *>(sp + x) = u32x4{x, d, x, d};
+                            continue;
+                        }
+                        const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                        const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+                        if constexpr (SE == 2) {  // diagnostic: the LDS reads without the stores
+                            diag ^= v.x ^ v.w;
+                            continue;
+                        }
+                        if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(sp + x));
+                        else *reinterpret_cast<u32x4 *>(sp + x) = v;
+                    } else {  // head [0, d)
+                        const uint32_t h = d & 8u;
+                        if (h && gl == 0) store8<NTS>(sp, piece(row, 0));
+                        const uint32_t x = 16u * gl + h;
+                        if (x + 16 <= d) {
+                            const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                            *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                        }
+                    }
+                    if (s == 7) {  // tail [896 + d, 1024)
+                        const uint32_t x = 896u + d + 16u * gl;
+                        if (x + 16 <= 1024) {
+                            const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
+                            *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                        } else if (x + 8 == 1024) {
+                            store8<NTS>(sp + x, piece(row, x));
+                        }
+                    }
+                }
+                return;
+            }
+    #pragma unroll SU
             for (int t = 0; t < 8; ++t) {
-                uint8_t *sp = lsp[t];
-                const uint32_t d = ldd[t];
-                const uint32_t *row = st + (t * 8 + (lane >> 3)) * RW;
+                const int cc = t * 8 + (lane >> 3);
+                const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
+                if (!(wave_on && ci < a.N)) continue;
+                const uint64_t rem = a.n - ci * 1024;
+                const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+                const uint64_t base = soff[j & 1][wave][cc];
+                uint8_t *sp = ob + base;
+                const uint32_t *row = st + cc * RW;
+                if (clen < 1024) {  // short last chunk of the object: this step's bytes, byte stores
+                    const uint32_t *w = row + dofs(s) + 4 * gl;
+                    for (int q = 0; q < 16; ++q) {
+                        const uint32_t cb = 128u * s + 16u * gl + q;
+                        if (cb < clen) sp[cb] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+                    }
+                    continue;
+                }
+                // lines are aligned in memory, not in the stream: any 8-aligned object base
+                const uint32_t d = (uint32_t)(-(uintptr_t)sp) & 127u;
                 if (s >= 1) {  // the whole line [d + 128(s-1), d + 128 s)
                     const uint32_t x = d + 128u * (s - 1) + 16u * gl;
-                    if constexpr (SE == 3) {  // diagnostic (tools/bao_tune): the stores without the LDS reads
-                        *reinterpret_cast<u32x4 *>(sp + x) = u32x4{x, d, x, d};
-                        continue;
-                    }
-                    if constexpr (SE == 4) {  // diagnostic: as 3, every wave rewriting the same 8 KiB (L2 hits)
-                        *reinterpret_cast<u32x4 *>(ob + t * 1024 + lane * 16) = u32x4{x, d, x, d};
-                        continue;
-                    }
-                    if constexpr (SE == 5) {  // diagnostic: as 3, half the stores
-                        if (t & 1) continue;
-                        *reinterpret_cast<u32x4 *>(sp + x) = u32x4{x, d, x, d};
-                        continue;
-                    }
                     const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
                     const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
-                    if constexpr (SE == 2) {  // diagnostic: the LDS reads without the stores
-                        diag ^= v.x ^ v.w;
-                        continue;
-                    }
                     if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(sp + x));
                     else *reinterpret_cast<u32x4 *>(sp + x) = v;
-                } else {  // head [0, d)
+                } else {  // head [0, d): 8 B at 0 when d is 8 mod 16, then aligned 16-B pieces
                     const uint32_t h = d & 8u;
                     if (h && gl == 0) store8<NTS>(sp, piece(row, 0));
                     const uint32_t x = 16u * gl + h;
@@ -535,179 +595,141 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
                         *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
                     }
                 }
-                if (s == 7) {  // tail [896 + d, 1024)
+                if (s == 7) {  // tail [896 + d, 1024): aligned pieces, 8 B at the end
                     const uint32_t x = 896u + d + 16u * gl;
                     if (x + 16 <= 1024) {
                         const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                        *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                        const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+                        *reinterpret_cast<u32x4 *>(sp + x) = v;
                     } else if (x + 8 == 1024) {
                         store8<NTS>(sp + x, piece(row, x));
                     }
                 }
             }
-            return;
-        }
-#pragma unroll SU
-        for (int t = 0; t < 8; ++t) {
-            const int cc = t * 8 + (lane >> 3);
-            const uint64_t ci = c0 + (uint64_t)cc * CPL + j;
-            if (!(wave_on && ci < a.N)) continue;
-            const uint64_t rem = a.n - ci * 1024;
-            const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
-            const uint64_t base = soff[j & 1][wave][cc];
-            uint8_t *sp = ob + base;
-            const uint32_t *row = st + cc * RW;
-            if (clen < 1024) {  // short last chunk of the object: this step's bytes, byte stores
-                const uint32_t *w = row + dofs(s) + 4 * gl;
-                for (int q = 0; q < 16; ++q) {
-                    const uint32_t cb = 128u * s + 16u * gl + q;
-                    if (cb < clen) sp[cb] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
-                }
-                continue;
-            }
-            // lines are aligned in memory, not in the stream: any 8-aligned object base
-            const uint32_t d = (uint32_t)(-(uintptr_t)sp) & 127u;
-            if (s >= 1) {  // the whole line [d + 128(s-1), d + 128 s)
-                const uint32_t x = d + 128u * (s - 1) + 16u * gl;
-                const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
-                if (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(sp + x));
-                else *reinterpret_cast<u32x4 *>(sp + x) = v;
-            } else {  // head [0, d): 8 B at 0 when d is 8 mod 16, then aligned 16-B pieces
-                const uint32_t h = d & 8u;
-                if (h && gl == 0) store8<NTS>(sp, piece(row, 0));
-                const uint32_t x = 16u * gl + h;
-                if (x + 16 <= d) {
-                    const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                    *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
-                }
-            }
-            if (s == 7) {  // tail [896 + d, 1024): aligned pieces, 8 B at the end
-                const uint32_t x = 896u + d + 16u * gl;
-                if (x + 16 <= 1024) {
-                    const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                    const u32x4 v = {lo.x, lo.y, hi.x, hi.y};
-                    *reinterpret_cast<u32x4 *>(sp + x) = v;
-                } else if (x + 8 == 1024) {
-                    store8<NTS>(sp + x, piece(row, x));
-                }
-            }
-        }
-    };
+        };
 
-    uint32_t h[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) h[w] = IV(w);
-    uint32_t L[LOG + 1][8];  // pending left nodes per level (CV stack)
-    bool ok = true;
+        uint32_t h[8];
+    #pragma unroll
+        for (int w = 0; w < 8; ++w) h[w] = IV(w);
+        uint32_t L[LOG + 1][8];  // pending left nodes per level (CV stack)
+        bool ok = true;
 
-    u32x4 pre[8];
-    load_step(0, pre);
-    for (int g = 0; g < NSTEP; ++g) {
-        const int j = g >> 3, s = g & 7;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            uint32_t *row = st + (t * 8 + (lane >> 3)) * RW;
-            if (MODE == 0 && SP == 0 && (lane & 7) == 7)  // carry the previous step's last 8 bytes
-                *reinterpret_cast<u32x2 *>(row + 2) = *reinterpret_cast<const u32x2 *>(row + ROW0 + 30);
-            *reinterpret_cast<u32x4 *>(row + dofs(s) + (lane & 7) * 4) = pre[t];
-        }
-        if (MODE == 1 && ob) content_step(g, pre);
-        if (MODE == 0 && ob && (SP == 1 || SP == 2)) stream_regs(g, pre);
-        if (s == 7 && j + 1 < CPL) {  // stream offset of my next chunk, for the loads issued below
-            const uint64_t ni = lb + j + 1;
-            if ((uint64_t)(j + 1) < nmine) my_off += 1024 + 64 * (uint64_t)parents_at(ni, a.N);
-            soff[(j + 1) & 1][wave][lane] = my_off;
-        }
-        wave_sync();
-        if (MODE == 0 && ob && SP == 3 && SE == 1) stream_lines(g);
-        if (g + 1 < NSTEP) load_step(g + 1, pre);  // in flight during the compressions
-        if (MODE == 0 && ob && SP == 0) stream_step(wave, g);
-        if (MODE == 0 && ob && SP == 3 && SE != 1) stream_lines(g);
-
-        const uint64_t i = lb + j;
-        const bool mine = (uint64_t)j < nmine;
-        const uint32_t len = mine ? (uint32_t)((a.n - i * 1024) < 1024 ? (a.n - i * 1024) : 1024) : 0u;
-        const uint32_t nb = len == 0 ? 1 : (len + 63) / 64;
-        for (int hh = 0; hh < 2; ++hh) {
-            const uint32_t b = (uint32_t)(2 * s + hh);
-            if (mine && b < nb) {
-                uint32_t m[16];
-                const u32x4 *row = reinterpret_cast<const u32x4 *>(st + lane * RW + dofs(s) + hh * 16);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const u32x4 x = row[q];
-                    m[4 * q] = x.x; m[4 * q + 1] = x.y; m[4 * q + 2] = x.z; m[4 * q + 3] = x.w;
-                }
-                const bool last = b + 1 == nb;
-                const uint32_t blen = last ? len - 64 * b : 64u;
-                const uint32_t flags = (b == 0 ? F_CHUNK_START : 0u) |
-                                       (last ? (F_CHUNK_END | (a.N == 1 ? F_ROOT : 0u)) : 0u);
-                b3_compress(h, m, i, blen, flags);
+        u32x4 pre[8];
+        load_step(0, pre);
+        for (int g = 0; g < NSTEP; ++g) {
+            const int j = g >> 3, s = g & 7;
+    #pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                uint32_t *row = st + (t * 8 + (lane >> 3)) * RW;
+                if (MODE == 0 && SP == 0 && (lane & 7) == 7)  // carry the previous step's last 8 bytes
+                    *reinterpret_cast<u32x2 *>(row + 2) = *reinterpret_cast<const u32x2 *>(row + ROW0 + 30);
+                *reinterpret_cast<u32x4 *>(row + dofs(s) + (lane & 7) * 4) = pre[t];
             }
-        }
-        wave_sync();
-
-        if (MODE == 2 && s == 7) {  // node check: chunk CV vs its stored slot (or the hash)
-            if (mine) {
-                bool cok;
-                if (a.N == 1) {
-                    const u32x4 *hp = reinterpret_cast<const u32x4 *>(a.hash + obj * 32);
-                    const u32x4 e0 = hp[0], e1 = hp[1];
-                    cok = e0.x == h[0] && e0.y == h[1] && e0.z == h[2] && e0.w == h[3] && e1.x == h[4] &&
-                          e1.y == h[5] && e1.z == h[6] && e1.w == h[7];
-                } else {
-                    cok = stored_slot_matches(ib, i, 0, a.N, h);
-                }
-                a.cv[obj * a.cv_stride + i] = cok ? 1 : 0;
+            if (MODE == 1 && ob) content_step(g, pre);
+            if (MODE == 0 && ob && (SP == 1 || SP == 2)) stream_regs(g, pre);
+            if (s == 7 && j + 1 < CPL) {  // stream offset of my next chunk, for the loads issued below
+                const uint64_t ni = lb + j + 1;
+                if ((uint64_t)(j + 1) < nmine) my_off += 1024 + 64 * (uint64_t)parents_at(ni, a.N);
+                soff[(j + 1) & 1][wave][lane] = my_off;
             }
-#pragma unroll
-            for (int w = 0; w < 8; ++w) h[w] = IV(w);
-        } else if (s == 7) {  // chunk j of every lane is complete
-            if (mine) {
-                const bool final = (uint64_t)j + 1 == nmine;
-                // CV stack: merge while the chunk count below this point is odd;
-                // on the lane's last chunk merge everything pending (promotions
-                // of a short tail follow the global tree)
-                bool done = false;
-#pragma unroll
-                for (int lv = 0; lv < LOG; ++lv) {
-                    if (done) continue;
-                    const bool bit = (j >> lv) & 1;
-                    if (bit) {
-                        const uint64_t sl = lb + ((uint64_t)(j >> (lv + 1)) << (lv + 1));
-                        const bool root = a.N <= (2ull << lv);
-                        if (ob || MODE == 1) {
-                            uint8_t *node = (MODE == 0 ? ob : const_cast<uint8_t *>(ib)) +
-                                            parent_stream_off(sl, lv + 1, a.N);
-                            ok &= node_io<MODE == 3 ? 0 : MODE, NTS>(node, L[lv], h);
-                        }
-                        uint32_t p[8];
-                        b3_parent(L[lv], h, root, p);
-#pragma unroll
-                        for (int w = 0; w < 8; ++w) h[w] = p[w];
-                    } else if (!final) {
-#pragma unroll
-                        for (int w = 0; w < 8; ++w) L[lv][w] = h[w];
-                        done = true;
+            wave_sync();
+            if (MODE == 0 && ob && SP == 3 && SE == 1) stream_lines(g);
+            if (g + 1 < NSTEP) load_step(g + 1, pre);  // in flight during the compressions
+            if (MODE == 0 && ob && SP == 0) stream_step(wave, g);
+            if (MODE == 0 && ob && SP == 3 && SE != 1) stream_lines(g);
+
+            const uint64_t i = lb + j;
+            const bool mine = (uint64_t)j < nmine;
+            const uint32_t len = mine ? (uint32_t)((a.n - i * 1024) < 1024 ? (a.n - i * 1024) : 1024) : 0u;
+            const uint32_t nb = len == 0 ? 1 : (len + 63) / 64;
+            for (int hh = 0; hh < 2; ++hh) {
+                const uint32_t b = (uint32_t)(2 * s + hh);
+                if (mine && b < nb) {
+                    uint32_t m[16];
+                    const u32x4 *row = reinterpret_cast<const u32x4 *>(st + lane * RW + dofs(s) + hh * 16);
+    #pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const u32x4 x = row[q];
+                        m[4 * q] = x.x; m[4 * q + 1] = x.y; m[4 * q + 2] = x.z; m[4 * q + 3] = x.w;
                     }
+                    const bool last = b + 1 == nb;
+                    const uint32_t blen = last ? len - 64 * b : 64u;
+                    const uint32_t flags = (b == 0 ? F_CHUNK_START : 0u) |
+                                           (last ? (F_CHUNK_END | (a.N == 1 ? F_ROOT : 0u)) : 0u);
+                    b3_compress(h, m, i, blen, flags);
                 }
-                if (!done) {  // h is my level-LOG node (or the root)
-                    if (a.N <= (uint64_t)CPL) {
-                        root_io<MODE == 3 ? 0 : MODE>(a, obj, h);
+            }
+            wave_sync();
+
+            if (MODE == 2 && s == 7) {  // node check: chunk CV vs its stored slot (or the hash)
+                if (mine) {
+                    bool cok;
+                    if (a.N == 1) {
+                        const u32x4 *hp = reinterpret_cast<const u32x4 *>(a.hash + obj * 32);
+                        const u32x4 e0 = hp[0], e1 = hp[1];
+                        cok = e0.x == h[0] && e0.y == h[1] && e0.z == h[2] && e0.w == h[3] && e1.x == h[4] &&
+                              e1.y == h[5] && e1.z == h[6] && e1.w == h[7];
                     } else {
-                        u32x4 *cvp = reinterpret_cast<u32x4 *>(a.cv + (obj * a.cv_stride + lb / CPL) * 32);
-                        cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
-                        cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
+                        cok = stored_slot_matches(ib, i, 0, a.N, h);
+                    }
+                    a.cv[obj * a.cv_stride + i] = cok ? 1 : 0;
+                }
+    #pragma unroll
+                for (int w = 0; w < 8; ++w) h[w] = IV(w);
+            } else if (s == 7) {  // chunk j of every lane is complete
+                if (mine) {
+                    const bool final = (uint64_t)j + 1 == nmine;
+                    // CV stack: merge while the chunk count below this point is odd;
+                    // on the lane's last chunk merge everything pending (promotions
+                    // of a short tail follow the global tree)
+                    bool done = false;
+    #pragma unroll
+                    for (int lv = 0; lv < LOG; ++lv) {
+                        if (done) continue;
+                        const bool bit = (j >> lv) & 1;
+                        if (bit) {
+                            const uint64_t sl = lb + ((uint64_t)(j >> (lv + 1)) << (lv + 1));
+                            const bool root = a.N <= (2ull << lv);
+                            if (ob || MODE == 1) {
+                                uint8_t *node = (MODE == 0 ? ob : const_cast<uint8_t *>(ib)) +
+                                                parent_stream_off(sl, lv + 1, a.N);
+                                ok &= node_io<MODE == 3 ? 0 : MODE, NTS>(node, L[lv], h);
+                            }
+                            uint32_t p[8];
+                            b3_parent(L[lv], h, root, p);
+    #pragma unroll
+                            for (int w = 0; w < 8; ++w) h[w] = p[w];
+                        } else if (!final) {
+    #pragma unroll
+                            for (int w = 0; w < 8; ++w) L[lv][w] = h[w];
+                            done = true;
+                        }
+                    }
+                    if (!done) {  // h is my level-LOG node (or the root)
+                        if (a.N <= (uint64_t)CPL) {
+                            root_io<MODE == 3 ? 0 : MODE>(a, obj, h);
+                        } else {
+                            u32x4 *cvp = reinterpret_cast<u32x4 *>(a.cv + (obj * a.cv_stride + lb / CPL) * 32);
+                            cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
+                            cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
+                        }
                     }
                 }
+    #pragma unroll
+                for (int w = 0; w < 8; ++w) h[w] = IV(w);
             }
-#pragma unroll
-            for (int w = 0; w < 8; ++w) h[w] = IV(w);
+        }
+        if (MODE == 1 && !ok) flag_mismatch(a.status, obj);
+        if (SE == 2 && diag == 0x9E3779B9u && ob) ob[0] = 0;  // keep the diagnostic's reads alive
+        if (!DQ) break;
+    }
+    if (DQ && lane == 0) {  // the last wave out leaves the queue zero for the next launch
+        const uint32_t done = atomicAdd(a.queue + 32, 1u);
+        if (done + 1 == gridDim.x * (uint32_t)K3_WAVES) {
+            a.queue[0] = 0u;
+            a.queue[32] = 0u;
         }
     }
-    if (MODE == 1 && !ok) flag_mismatch(a.status, obj);
-    if (SE == 2 && diag == 0x9E3779B9u && ob) ob[0] = 0;  // keep the diagnostic's reads alive
 }
 
 struct ParentArgs {
@@ -927,7 +949,7 @@ hipError_t run_parent_levels(uint8_t *cv_prev, uint64_t stride_prev, uint64_t cn
 }
 
 // Enqueue K3 then one K4 launch per remaining level.
-template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0>
+template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0, bool DQ = false>
 hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
                    void *d_scratch, hipStream_t stream, size_t pad_lds = 0 /* tuning: occupancy probe */,
@@ -947,10 +969,26 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
     ca.out_limit = out_limit;
     const uint64_t waves = count * ((N + 64ull * BAO_CPL - 1) / (64ull * BAO_CPL));
     const uint64_t blocks = (waves + K3_WAVES - 1) / K3_WAVES;
-    hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG>), dim3((unsigned)blocks),
-                       dim3(K3_TPB), pad_lds,
-                       stream, ca);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipSuccess;
+    bool dq = DQ && waves < (1ull << 31);
+    if (dq) {  // persistent grid of resident workgroups, wave tasks from the stream's run queue
+        uint32_t *q = nullptr;
+        int per_cu = 0;
+        const void *fn = reinterpret_cast<const void *>(bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG, true>);
+        dq = stream_queue(stream, &q) == hipSuccess &&
+             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, K3_TPB, pad_lds) == hipSuccess && per_cu > 0;
+        (void)hipGetLastError();
+        if (dq) {
+            ca.queue = q + 640;
+            const uint64_t grid = std::min<uint64_t>(blocks, (uint64_t)per_cu * (uint64_t)num_cus());
+            hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG, true>), dim3((unsigned)grid),
+                               dim3(K3_TPB), pad_lds, stream, ca);
+        }
+    }
+    if (!dq)
+        hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG>), dim3((unsigned)blocks),
+                           dim3(K3_TPB), pad_lds, stream, ca);
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
 
     uint8_t *stream_buf = (MODE == 0 || MODE == 3) ? d_out : const_cast<uint8_t *>(d_in);

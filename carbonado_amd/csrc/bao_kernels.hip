@@ -51,12 +51,16 @@ constexpr int BAO_SP = 3;
 constexpr int BAO_XG = 1;
 // SP 3 store loop fully unrolled over the 8 chunk groups: +0.6-0.9 % (tools/bao_tune, r1x)
 constexpr int BAO_SU = 8;
+// Persistent grid with wave tasks from the stream's run queue: the XCDs do
+// not stream at one rate, and a static grid ends on the slowest (K13 measured
+// +5.6-7.8 % from the same change, tools/fused_tune r2l).
+constexpr bool BAO_DQ = true;
 
 template <int MODE>
 hipError_t run_bao(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
                    void *d_scratch, hipStream_t stream) {
-    return run_bao_t<MODE, BAO_CPL, BAO_NTS, MODE == 0 ? BAO_SP : 0, MODE == 0 ? BAO_SU : 1, 0, BAO_XG>(
+    return run_bao_t<MODE, BAO_CPL, BAO_NTS, MODE == 0 ? BAO_SP : 0, MODE == 0 ? BAO_SU : 1, 0, BAO_XG, BAO_DQ>(
         d_in, in_stride, n, count, d_out, out_stride, d_hash, d_status, d_scratch, stream);
 }
 
@@ -84,7 +88,7 @@ hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
 hipError_t bao_decode_prefix_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                                  const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
                                  uint32_t *d_status, void *d_scratch, hipStream_t stream) {
-    return run_bao_t<1, BAO_CPL, BAO_NTS, 0, 1, 0, BAO_XG>(d_in, in_stride, n, count, d_out, out_stride,
+    return run_bao_t<1, BAO_CPL, BAO_NTS, 0, 1, 0, BAO_XG, BAO_DQ>(d_in, in_stride, n, count, d_out, out_stride,
                                                           const_cast<uint8_t *>(d_hash), d_status, d_scratch, stream,
                                                           0, out_limit);
 }
@@ -112,8 +116,8 @@ hipError_t bao_encode_inplace_dev(uint8_t *d_stream, uint64_t stride, uint64_t n
     // three tree levels fold in registers (tools/bao_tune: 3.15 vs 3.39 ms
     // for CPL 2 on 256 x 32 MiB; fewer K4 launches).  Scratch sized for
     // BAO_CPL covers it (N/8 <= N/2 level nodes).
-    return run_bao_t<3, 8, BAO_NTS, 0, 1, 0, BAO_XG>(d_stream, stride, n, count, d_stream, stride, d_hash, nullptr,
-                                                     d_scratch, stream);
+    return run_bao_t<3, 8, BAO_NTS, 0, 1, 0, BAO_XG, BAO_DQ>(d_stream, stride, n, count, d_stream, stride, d_hash,
+                                                             nullptr, d_scratch, stream);
 }
 
 namespace {
