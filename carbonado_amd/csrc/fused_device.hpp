@@ -214,8 +214,11 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         return (uint64_t)__builtin_amdgcn_readfirstlane(b);
     };
     uint64_t blk = DQ ? grab() : (uint64_t)blockIdx.x * FW + wave;
-    u32x4 v[NV];
-    if (blk < total) load_step(blk, 0, v);
+    u32x4 v[NV], v2[NV];  // this step's loads; ORD 3: the next step's too
+    if (blk < total) {
+        load_step(blk, 0, v);
+        if (ORD == 3) load_step(blk, 1, v2);
+    }
     for (uint64_t nxt; blk < total; blk = nxt) {
         nxt = DQ ? grab() : blk + GW;
         const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * BW;
@@ -297,6 +300,12 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                 else if (nxt < total) load_step(nxt, 0, v);
             };
             if (ORD == 2) next_loads();  // as soon as v is free: two compressions of cover
+            if (ORD == 3) {  // two steps ahead: v takes the next step's data, v2 loads the one after
+#pragma unroll
+                for (int t = 0; t < NV; ++t) v[t] = v2[t];
+                if (s < 6) load_step(blk, s + 2, v2);
+                else if (nxt < total) load_step(nxt, s - 6, v2);
+            }
 
             // ---- store role: whole 128-B memory lines of chunks (t, cu) ----
             auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x
@@ -344,7 +353,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                     }
                 }
                 // next loads, after this step's stores, in flight during the compressions
-                if (ORD != 2) next_loads();
+                if (ORD <= 1) next_loads();
             };
 
             // ---- hash role: blocks 2s, 2s+1 of my chunk ----
