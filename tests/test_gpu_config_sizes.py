@@ -115,3 +115,25 @@ def test_level12_16mib_fused_full_path(gpu, obj16, shift):
         assert got[o, :blen].tobytes() == enc, o
         assert gh[o].tobytes() == h
         assert (got[o, blen:] == 0xA5).all()
+
+
+def test_zfec_linearity_16mib_batch(gpu):
+    """A size-independent property at the config size: zfec encode is linear
+    over GF(2^8), so the shards of A xor B are the xor of the shards of A and
+    of B (8 objects of 16 MiB, 4-of-8 and 8-of-16), and the data shards are
+    the input itself (systematic code)."""
+    import torch
+    from carbonado_amd import device
+    g = torch.Generator(device="cuda").manual_seed(1616)
+    a = torch.randint(0, 256, (8, N), dtype=torch.uint8, device="cuda", generator=g)
+    b = torch.randint(0, 256, (8, N), dtype=torch.uint8, device="cuda", generator=g)
+    for k, m in ((4, 8), (8, 16)):
+        C = N // k
+        outs = []
+        for x in (a, b, a ^ b):
+            o = torch.empty((8, m * C), dtype=torch.uint8, device="cuda")
+            device.zfec_encode_batch(x, N, o, k, m)
+            outs.append(o)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[2], outs[0] ^ outs[1])
+        assert torch.equal(outs[0][:, :N], a)
