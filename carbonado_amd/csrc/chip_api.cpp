@@ -1173,7 +1173,8 @@ int chip_decode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_strid
     if ((!d_in && in_len) || (count && !d_status) || (in_stride % 16) || (out_stride % 16) || misaligned16(d_in) ||
         misaligned16(d_out))
         return CHIP_ERR_INVALID_ARG;
-    if (bao && (!d_hash || !d_scratch)) return bao && !d_hash ? CHIP_ERR_HASH_DECODE : CHIP_ERR_INVALID_ARG;
+    if (bao && !d_hash) return CHIP_ERR_HASH_DECODE;
+    if (bao && !d_scratch) return CHIP_ERR_INVALID_ARG;
     uint64_t blen = in_len;  // bytes entering zfec (decoding.rs:90-99)
     if (bao && !bao_content_len(in_len, &blen)) return CHIP_ERR_BAO_TRUNCATED;
     uint64_t olen = blen;
