@@ -187,8 +187,8 @@ def measured_traffic(spec: str, kernel_sym: str, alg_bytes: int):
     kernel and workload (profiles/<tag>_pmc.json), else (None, None)."""
     if spec == "none":
         return None, None
-    files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=lambda p: p.stat().st_mtime) if spec == "auto" \
-        else [Path(spec)]
+    # newest round/session tag last (r1…, r2a … r2z sort in the order they were taken)
+    files = sorted((ROOT / "profiles").glob("*_pmc.json")) if spec == "auto" else [Path(spec)]
     for f in reversed(files):
         try:
             tj = json.loads(f.read_text())
@@ -405,6 +405,7 @@ class Workload:
             if lv & 12 == 12 and not two:
                 self.kernel = (f"encode() level {lv} on the device: zfec_bao_fused_kernel (zfec 4-of-8 + chunk "
                                "hashing + tree levels 1-3 in one pass) + parent levels from level 4")
+                self.kernel_sym = "zfec_bao_fused_kernel"
             elif two:
                 self.kernel = (f"encode() level {lv} on the device: gf_apply_kernel + bao_chunk_kernel + parent "
                                "levels (zfec writes the shards into their bao chunk slots; bao hashes in place)")
@@ -412,7 +413,8 @@ class Workload:
                 self.kernel = f"encode() level {lv} on the device: bao_chunk_kernel + parent levels"
             else:
                 self.kernel = f"encode() level {lv} on the device: gf_apply_kernel"
-            self.kernel_sym = "pipeline"
+            if not (lv & 12 == 12 and not two):
+                self.kernel_sym = "pipeline"
         elif args.mode == "pipeline-decode":
             lv = args.level
             if lv & 3:
@@ -619,8 +621,11 @@ class Workload:
             self.scratch = device.bao_scratch(n, count, dev)
             self.step = lambda: device.bao_encode_batch(self.inp, n, self.out, self.hashes, self.scratch)
             self.alg_bytes = count * (n + blen)
-            self.kernel = "bao_chunk_kernel + bao_parent_kernel levels"
-            self.kernel_sym = "bao_chunk_kernel"
+            fused = n >= 65536 and n % 65536 == 0 and os.environ.get("CHIP_FUSED", "1") != "0"
+            self.kernel = ("zfec_bao_fused_kernel content mode (chunk hashing + tree levels 1-3, 64 consecutive "
+                           "chunks per wave) + bao_parent_kernel levels from level 4" if fused else
+                           "bao_chunk_kernel + bao_parent_kernel levels")
+            self.kernel_sym = "zfec_bao_fused_kernel" if fused else "bao_chunk_kernel"
         torch.cuda.synchronize()
 
     def _scatter_inputs(self, rank: int, world: int) -> float:
