@@ -613,7 +613,7 @@ class Workload:
             self.step = lambda: device.bao_decode_batch(self.enc, n, self.hashes, self.out, self.status, self.scratch)
             self.alg_bytes = count * (blen + n)  # read the stream, write the content
             self.kernel = "bao_chunk_kernel<1> (verify + content) + bao_parent_kernel<1> levels"
-            self.kernel_sym = "bao_chunk_kernel"
+            self.kernel_sym = "bao_chunk_kernel<1,"
         else:
             blen = L.chip_bao_encoded_len(n)
             self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
@@ -625,7 +625,7 @@ class Workload:
             self.kernel = ("zfec_bao_fused_kernel content mode (chunk hashing + tree levels 1-3, 64 consecutive "
                            "chunks per wave) + bao_parent_kernel levels from level 4" if fused else
                            "bao_chunk_kernel + bao_parent_kernel levels")
-            self.kernel_sym = "zfec_bao_fused_kernel" if fused else "bao_chunk_kernel"
+            self.kernel_sym = "zfec_bao_fused_kernel" if fused else "bao_chunk_kernel<0,"
         torch.cuda.synchronize()
 
     def _scatter_inputs(self, rank: int, world: int) -> float:
