@@ -46,6 +46,14 @@ namespace {
 // decode CPL 2 1.88 vs CPL 8 1.77.
 constexpr int BAO_CPL = 2;
 constexpr bool BAO_NTS = false;
+// Verify-decode writes the content in whole 128-B lines it never reads back:
+// nontemporal, or the L2 fetches every destination line first (PMC: reads
+// 1.59x the stream with plain stores, r2q_baodec_pmc.json; tools/fetch_calib
+// pins FETCH_SIZE at 1/2 of the bytes for these loads).
+#ifndef BAO_DEC_NTS_DEF
+#define BAO_DEC_NTS_DEF true
+#endif
+constexpr bool BAO_DEC_NTS = BAO_DEC_NTS_DEF;
 constexpr int BAO_SP = 3;
 // XCD-grouped block order: +0.9-1.8 % on encode / decode / in-place (tools/bao_tune, r1x)
 constexpr int BAO_XG = 1;
@@ -60,7 +68,8 @@ template <int MODE>
 hipError_t run_bao(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
                    void *d_scratch, hipStream_t stream) {
-    return run_bao_t<MODE, BAO_CPL, BAO_NTS, MODE == 0 ? BAO_SP : 0, MODE == 0 ? BAO_SU : 1, 0, BAO_XG, BAO_DQ>(
+    return run_bao_t<MODE, BAO_CPL, MODE == 1 ? BAO_DEC_NTS : BAO_NTS, MODE == 0 ? BAO_SP : 0, MODE == 0 ? BAO_SU : 1, 0,
+                     BAO_XG, BAO_DQ>(
         d_in, in_stride, n, count, d_out, out_stride, d_hash, d_status, d_scratch, stream);
 }
 
@@ -88,7 +97,7 @@ hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
 hipError_t bao_decode_prefix_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                                  const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
                                  uint32_t *d_status, void *d_scratch, hipStream_t stream) {
-    return run_bao_t<1, BAO_CPL, BAO_NTS, 0, 1, 0, BAO_XG, BAO_DQ>(d_in, in_stride, n, count, d_out, out_stride,
+    return run_bao_t<1, BAO_CPL, BAO_DEC_NTS, 0, 1, 0, BAO_XG, BAO_DQ>(d_in, in_stride, n, count, d_out, out_stride,
                                                           const_cast<uint8_t *>(d_hash), d_status, d_scratch, stream,
                                                           0, out_limit);
 }
