@@ -133,7 +133,8 @@ struct Tree {
 // DG: diagnostics for tools/fused_tune (wrong output): 1 = no line stores,
 // 2 = no hashing, 3 = no GF (rows get the data shards only), 4 = neither
 // stores nor hashing, 5 = every chunk's lines 128-B aligned (no partial
-// lines), 6 = 5 without hashing.
+// lines), 6 = 5 without hashing, 7 = the line stores' LDS reads without the
+// stores.
 // FULL: cols % 8 == 0 and no zfec padding (valid >= 4 C): every block is 8
 // whole columns of plain loads, levels 1-3 run in the wave (Tree) and `cv`
 // receives level-3 CVs; otherwise lanes are predicated and `cv` receives the
@@ -324,8 +325,13 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             }
             auto line_stores = [&]() {
                 if (ST && s >= 1 && gcol) {
+                    if (DG == 7) {  // diagnostic: the piece reads without the line stores
 #pragma unroll
-                    for (int t = 0; t < 8; ++t) st16<NT>(lsp[t] + ldd[t] + 128u * (s - 1) + 16u * gl, q[t]);
+                        for (int t = 0; t < 8; ++t) h[7] ^= q[t].x ^ q[t].w;
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) st16<NT>(lsp[t] + ldd[t] + 128u * (s - 1) + 16u * gl, q[t]);
+                    }
                 }
                 if (ST && (s == 0 || s == 7) && gcol) {
 #pragma unroll

@@ -87,14 +87,14 @@ int main(int argc, char **argv) {
     const char *which = argc > 3 ? argv[3] : "all";
     std::vector<Variant> all = {
         {"K0 FULL (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
-        {"K0 FULL ORD3 (2 ahead)", fused::zfec_bao_fused_kernel<true, true, 3, 0, 0>, 0},
-        {"K0 FULL ORD2", fused::zfec_bao_fused_kernel<true, true, 2, 0, 0>, 0},
         {"K0 general", fused::zfec_bao_fused_kernel<true, false, 1, 0, 0>, 0},
-        {"K0 general ORD3", fused::zfec_bao_fused_kernel<true, false, 3, 0, 0>, 0},
         {"K1 (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1>, 1},
-        {"K0 DG1 no stores", fused::zfec_bao_fused_kernel<true, true, 1, 1, 0>, 0},
+        {"K0 DG1 no line stores/reads", fused::zfec_bao_fused_kernel<true, true, 1, 1, 0>, 0},
+        {"K0 DG7 piece reads, no stores", fused::zfec_bao_fused_kernel<true, true, 1, 7, 0>, 0},
         {"K0 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 0>, 0},
-        {"K0 DG4 GF+loads", fused::zfec_bao_fused_kernel<true, true, 1, 4, 0>, 0}};
+        {"K1 DG1 no line stores/reads", fused::zfec_bao_fused_kernel<true, true, 1, 1, 1>, 1},
+        {"K1 DG7 piece reads, no stores", fused::zfec_bao_fused_kernel<true, true, 1, 7, 1>, 1},
+        {"K1 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 1>, 1}};
     std::vector<Variant> vs;
     for (auto &v : all)
         if (!strcmp(which, "all") || strstr(v.name.c_str(), which)) vs.push_back(v);
