@@ -309,8 +309,11 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             }
 
             // ---- store role: whole 128-B memory lines of chunks (t, cu) ----
-            auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x
-                return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
+            // 8 B at chunk byte x (x % 8 == 0): the row's two step halves are one
+            // 256-B ring after the 16-B pad, so byte x sits at pad + x mod 256
+            // (= dofs(x >> 7) + (x & 127) / 4 words, in two VALU ops)
+            auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {
+                return *reinterpret_cast<const u32x2 *>(reinterpret_cast<const uint8_t *>(row) + 16 + (x & 255u));
             };
             constexpr bool ST = DG != 1 && DG != 4;
             u32x4 q[8];
