@@ -500,8 +500,11 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         uint32_t ldd[8];
         auto stream_lines = [&](int g) {
             const int j = g >> 3, s = g & 7, gl = lane & 7;
-            auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {  // 8 B at chunk byte x (8-aligned)
-                return *reinterpret_cast<const u32x2 *>(row + dofs((int)(x >> 7)) + ((x & 127u) >> 2));
+            // 8 B at chunk byte x (8-aligned): the two step halves after the 16-B
+            // pad are one 256-B ring (SP 3's only layout), byte x at pad + x mod 256
+            auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {
+                static_assert(SP != 3 || RW == 68, "ring layout");
+                return *reinterpret_cast<const u32x2 *>(reinterpret_cast<const uint8_t *>(row) + 4 * ROW0 + (x & 255u));
             };
             if (full_wave) {  // all chunks full: per-chunk values computed once per round
                 if (s == 0) {
