@@ -111,7 +111,12 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true", help="no device: exercise the multi-rank control plane")
     ap.add_argument("--traffic-json", default="auto",
                     help="PMC summary (profiles/*_pmc.json, tools/pmc_summary.py) with the measured HBM "
-                         "bytes per launch of this kernel; 'auto' = newest matching file, 'none' = null")
+                         "bytes per launch of this kernel; 'auto' = newest matching file, 'none' = null; used "
+                         "when the live PMC passes are off or fail")
+    ap.add_argument("--live-pmc", choices=["auto", "on", "off"], default="auto",
+                    help="measure roofline.traffic in this run: two child processes of the same workload under "
+                         "`rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (one pass each) before this process "
+                         "touches the GPU; auto = on for encode/decode at N=1")
     args = ap.parse_args(argv)
     if args.config:
         explicit = {a.dest for a in ap._actions if any(o in (argv if argv is not None else sys.argv[1:])
@@ -198,6 +203,72 @@ def measured_traffic(spec: str, kernel_sym: str, alg_bytes: int):
         if hb and kernel_sym in (tj.get("kernel") or "") and abs(hb - alg_bytes) < 0.25 * alg_bytes:
             return round(hb), str(f.relative_to(ROOT))
     return None, None
+
+
+def pmc_kernel_sym(args) -> str | None:
+    """Substring of the rocprofv3 kernel name of the mode's dominant kernel
+    (the Workload's kernel_sym), for the HBM-bound modes the live PMC covers."""
+    if args.mode == "encode":
+        return f"gf_apply_kernel<{args.k}, {(args.m - args.k + 3) // 4},"
+    if args.mode == "decode":
+        return f"gf_apply_kernel<{args.k}, 1,"
+    return None
+
+
+def live_traffic(args, argv: list, timeout_s: float = 240.0) -> dict:
+    """roofline.traffic measured in this run: the same workload in two child
+    processes under rocprofv3, one counter pass each (FETCH_SIZE uses 3 TCC
+    counters and WRITE_SIZE 2, so they cannot share a pass), then the
+    MI355X_MICROARCH.md HBM recipe: bytes = 2 x FETCH_SIZE (gfx950 reports
+    half of a wide streaming read; tools/fetch_calib pins the factor for this
+    access shape) + WRITE_SIZE, both KiB, averaged over the timed launches
+    (the last `steps` dispatches of the kernel: decode's child also runs the
+    encode that builds its shares).  Runs before this process initialises the
+    GPU; every child runs in its own process group and is killed (SIGKILL) at
+    the time limit.  Returns {"bytes": ...} or {"error": ...}."""
+    import csv
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    sym = pmc_kernel_sym(args)
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if sym is None or not Path(prof).exists():
+        return {"error": "no rocprofv3" if sym else f"no live PMC for mode {args.mode}"}
+    steps = 2
+    child = [sys.executable, str(Path(__file__).resolve())] + list(argv) + [
+        "--steps", str(steps), "--warmup", "1", "--live-pmc", "off", "--no-cpu-baseline", "--no-verify",
+        "--no-verify-all", "--no-aliased", "--traffic-json", "none"]
+    tmp = Path(tempfile.mkdtemp(prefix="chip_pmc_", dir="/tmp"))
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals, name = {}, None
+    t0 = time.perf_counter()
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        tag = ctr.split("_")[0].lower()
+        cmd = [prof, "--pmc", ctr, "-d", str(tmp / tag), "-o", tag, "--output-format", "csv", "--"] + child
+        with open(tmp / f"{tag}.log", "wb") as log:
+            p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT,
+                                 start_new_session=True)
+            try:
+                rc = p.wait(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return {"error": f"{ctr} pass killed after {timeout_s:.0f} s"}
+        if rc != 0:
+            return {"error": f"{ctr} pass exit status {rc}"}
+        rows = []
+        for f in sorted((tmp / tag).rglob("*counter_collection.csv")):
+            rows += [r for r in csv.DictReader(open(f)) if sym in r.get("Kernel_Name", "")]
+        rows.sort(key=lambda r: int(r.get("Dispatch_Id", 0) or 0))
+        if len(rows) < steps:
+            return {"error": f"{ctr} pass: {len(rows)} dispatches of {sym!r}"}
+        name = rows[-1]["Kernel_Name"]
+        vals[ctr] = sum(float(r["Counter_Value"]) for r in rows[-steps:]) / steps
+    shutil.rmtree(tmp, ignore_errors=True)
+    return {"bytes": round(2 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024),
+            "FETCH_SIZE_KiB": vals["FETCH_SIZE"], "WRITE_SIZE_KiB": vals["WRITE_SIZE"], "kernel": name,
+            "seconds": round(time.perf_counter() - t0, 1)}
 
 
 def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
@@ -821,6 +892,10 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     world, rank, local = setup_dist(args)
     n = int(args.object_mib * (1 << 20))
+    live = None
+    if (not args.dry_run and world == 1 and
+            (args.live_pmc == "on" or (args.live_pmc == "auto" and pmc_kernel_sym(args) is not None))):
+        live = live_traffic(args, sys.argv[1:])  # before this process touches the GPU
     wl = DryRun(args, rank) if args.dry_run else Workload(args, rank, local, world)
     scatter = None
     if world > 1 and not args.dry_run and not args.scatter and args.scatter_gib > 0:
@@ -850,7 +925,15 @@ def main():
         value = total_units / max_elapsed / 2**30
         avg_ms = sum(launch_ms) / len(launch_ms)
         achieved = wl.alg_bytes / (avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = measured_traffic(args.traffic_json, wl.kernel_sym, wl.alg_bytes)
+        traffic, traffic_src = None, None
+        if live and "bytes" in live:
+            traffic = live["bytes"]
+            traffic_src = (f"live: this run's rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same workload "
+                           f"(2 x FETCH_SIZE + WRITE_SIZE per launch, {live['seconds']} s)")
+        else:
+            traffic, traffic_src = measured_traffic(args.traffic_json, wl.kernel_sym, wl.alg_bytes)
+            if live:
+                traffic_src = f"{traffic_src or 'none'} (live PMC failed: {live['error']})"
         if args.mode == "bao":
             workload = f"bao encode, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "bao-decode":
@@ -900,6 +983,11 @@ def main():
                          "min_launch_ms": round(min(launch_ms), 4)},
             "verified_object0": verified,
         }
+        if live and "bytes" in live:
+            res["roofline"].update({"traffic_ratio": round(live["bytes"] / wl.alg_bytes, 4),
+                                    "pmc_KiB_per_launch": {"FETCH_SIZE": live["FETCH_SIZE_KiB"],
+                                                           "WRITE_SIZE": live["WRITE_SIZE_KiB"]},
+                                    "pmc_kernel": live["kernel"]})
         if args.mode.startswith("e2e") or args.mode in ("scrub", "hasher", "file"):
             res["roofline"].update({"bound": "pcie", "peak": 2 * 63.0,
                                     "frac": round(achieved / 126.0, 4),

@@ -24,3 +24,39 @@ def test_scrub_corrupt_offset_lands_in_a_chunk(n):
         off = bench.scrub_corrupt_offset(n, o)
         i = o * (C // 1024) + (C // 1024) // 3  # the chunk the helper aims at
         assert enc[off - 517:off - 517 + 1024] == z[1024 * i:1024 * (i + 1)]
+
+
+FAKE_ROCPROF = r'''#!/usr/bin/env python3
+# stand-in for rocprofv3 --pmc CTR -d DIR -o TAG --output-format csv -- cmd...
+import sys
+from pathlib import Path
+a = sys.argv[1:]
+ctr, d, tag = a[a.index("--pmc") + 1], Path(a[a.index("-d") + 1]), a[a.index("-o") + 1]
+cmd = a[a.index("--") + 1:]
+assert "--live-pmc" in cmd and cmd[cmd.index("--live-pmc") + 1] == "off", cmd
+d.mkdir(parents=True, exist_ok=True)
+val = {"FETCH_SIZE": [999.0, 100.0, 200.0], "WRITE_SIZE": [5.0, 300.0, 500.0]}[ctr]
+with open(d / f"{tag}_counter_collection.csv", "w") as f:
+    f.write("Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n")
+    f.write("1,at::fill_kernel,%s,1\n" % ctr)
+    for i, v in enumerate(val):
+        f.write('%d,"chip::zf::gf_apply_kernel<4, 1, 2, 6, true>(chip::zf::ApplyArgs)",%s,%s\n' % (i + 2, ctr, v))
+'''
+
+
+def test_live_traffic_two_passes(tmp_path, monkeypatch):
+    """bench.live_traffic: one rocprofv3 pass per counter, the kernel's last
+    `steps` dispatches averaged, bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB)."""
+    import shutil
+    import bench
+    fake = tmp_path / "rocprofv3"
+    fake.write_text(FAKE_ROCPROF)
+    fake.chmod(0o755)
+    monkeypatch.setattr(shutil, "which", lambda name: str(fake))
+    args = bench.parse([])
+    r = bench.live_traffic(args, [], timeout_s=60)
+    assert r["FETCH_SIZE_KiB"] == 150.0 and r["WRITE_SIZE_KiB"] == 400.0, r
+    assert r["bytes"] == (2 * 150 + 400) * 1024
+    assert "gf_apply_kernel<4, 1," in r["kernel"]
+    # a mode without an HBM-bound kernel gets no passes
+    assert "error" in bench.live_traffic(bench.parse(["--mode", "bao"]), [])
