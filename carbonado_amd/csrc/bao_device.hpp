@@ -204,10 +204,20 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// A generic pointer as a global-memory one.  Stores through a pointer whose
+// address space the compiler cannot trace (one passed through __shfl, or
+// picked from a per-lane array) compile to flat_store; flat instructions
+// count in LGKM_CNT as well as VM_CNT and complete out of order, so the next
+// LDS read's s_waitcnt lgkmcnt(0) would wait for every such store in flight.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T *glb(T *p) {
+    return (__attribute__((address_space(1))) T *)p;
+}
+
 template <bool NT>
 __device__ __forceinline__ void store8(uint8_t *p, u32x2 v) {
-    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x2 *>(p));
-    else *reinterpret_cast<u32x2 *>(p) = v;
+    if (NT) __builtin_nontemporal_store(v, glb(reinterpret_cast<u32x2 *>(p)));
+    else *glb(reinterpret_cast<u32x2 *>(p)) = v;
 }
 
 template <bool NT>
@@ -755,8 +765,8 @@ __device__ __forceinline__ void load_cv(const uint8_t *p, uint32_t (&c)[8]) {
 }
 
 __device__ __forceinline__ void store_cv(uint8_t *p, const uint32_t (&c)[8]) {
-    reinterpret_cast<u32x4 *>(p)[0] = u32x4{c[0], c[1], c[2], c[3]};
-    reinterpret_cast<u32x4 *>(p)[1] = u32x4{c[4], c[5], c[6], c[7]};
+    glb(reinterpret_cast<u32x4 *>(p))[0] = u32x4{c[0], c[1], c[2], c[3]};
+    glb(reinterpret_cast<u32x4 *>(p))[1] = u32x4{c[4], c[5], c[6], c[7]};
 }
 
 // K4: one lane = one node of `level` (parent of two level-1 nodes, or the

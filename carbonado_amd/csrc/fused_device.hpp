@@ -66,8 +66,8 @@ __device__ __forceinline__ int dofs(int step) { return 4 + (step & 1) * 32; }
 
 template <bool NT>
 __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
-    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
-    else *reinterpret_cast<u32x4 *>(p) = v;
+    if (NT) __builtin_nontemporal_store(v, bao::glb(reinterpret_cast<u32x4 *>(p)));
+    else *bao::glb(reinterpret_cast<u32x4 *>(p)) = v;
 }
 
 // Levels 1-3 of the tree inside the wave, pipelined over blocks.  With
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * BW;
         uint8_t *ob = a.out + obj * a.out_stride;
         if (ub == 0 && lane == 0)  // u64 LE content length
-            *reinterpret_cast<uint64_t *>(ob) = KIND ? a.valid : 8 * a.C;
+            *bao::glb(reinterpret_cast<uint64_t *>(ob)) = KIND ? a.valid : 8 * a.C;
         const bool gcol = FULL || ub + cu < a.cols;         // store role: chunks (t, ub + cu)
         const uint64_t hu = ub + (lane & 7);                // hash role: chunk (lane / 8, hu)
         const bool mine = FULL || hu < a.cols;
@@ -245,6 +245,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                 ldd[t] = (DG == 5 || DG == 6) ? 0u : (uint32_t)(-(uintptr_t)lsp[t]) & 127u;
             }
         }
+        auto lat = [&](int t, uint32_t x) -> uint8_t * { return lsp[t] + x; };
         uint32_t h[8];
 #pragma unroll
         for (int w = 0; w < 8; ++w) h[w] = bao::IV(w);
@@ -260,18 +261,22 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             if (DG == 3) {
 #pragma unroll
                 for (int c = 0; c < 16; ++c) acc[c] = zf::comp(v[c & 3], c >> 2);
-            } else
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            } else {
+                // per output word, the 4 shards' lookups together: independent
+                // LDS reads the compiler can keep in flight (shard-outer order
+                // left it one register for them, an lgkmcnt(0) per lookup)
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
-                    const uint32_t x = zf::comp(v[j], d);
+                    uint32_t x[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) x[j] = zf::comp(v[j], d);
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
-                        const uint32_t e =
-                            *reinterpret_cast<const uint32_t *>(lds + ((x >> (8 * b)) & 0xFFu) * ROWB + tb[j]);
-                        if (j == 0) acc[d * 4 + b] = e;
-                        else acc[d * 4 + b] ^= e;
+                        uint32_t e[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            e[j] = *reinterpret_cast<const uint32_t *>(lds + ((x[j] >> (8 * b)) & 0xFFu) * ROWB + tb[j]);
+                        acc[d * 4 + b] = (e[0] ^ e[1]) ^ (e[2] ^ e[3]);
                     }
                 }
             }
@@ -333,30 +338,29 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                         for (int t = 0; t < 8; ++t) h[7] ^= q[t].x ^ q[t].w;
                     } else {
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) st16<NT>(lsp[t] + ldd[t] + 128u * (s - 1) + 16u * gl, q[t]);
+                        for (int t = 0; t < 8; ++t) st16<NT>(lat(t, ldd[t] + 128u * (s - 1) + 16u * gl), q[t]);
                     }
                 }
                 if (ST && (s == 0 || s == 7) && gcol) {
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {
-                        uint8_t *sp = lsp[t];
                         const uint32_t d = ldd[t];
                         const uint32_t *row = rows + (t * 8 + cu) * RW;
                         if (s == 0) {  // head [0, d)
                             const uint32_t hd = d & 8u;
-                            if (hd && gl == 0) *reinterpret_cast<u32x2 *>(sp) = piece(row, 0);
+                            if (hd && gl == 0) *bao::glb(reinterpret_cast<u32x2 *>(lat(t, 0))) = piece(row, 0);
                             const uint32_t x = 16u * gl + hd;
                             if (x + 16 <= d) {
                                 const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                                *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                                *bao::glb(reinterpret_cast<u32x4 *>(lat(t, x))) = u32x4{lo.x, lo.y, hi.x, hi.y};
                             }
                         } else {  // tail [896 + d, 1024)
                             const uint32_t x = 896u + d + 16u * gl;
                             if (x + 16 <= 1024) {
                                 const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                                *reinterpret_cast<u32x4 *>(sp + x) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                                *bao::glb(reinterpret_cast<u32x4 *>(lat(t, x))) = u32x4{lo.x, lo.y, hi.x, hi.y};
                             } else if (x + 8 == 1024) {
-                                *reinterpret_cast<u32x2 *>(sp + x) = piece(row, x);
+                                *bao::glb(reinterpret_cast<u32x2 *>(lat(t, x))) = piece(row, x);
                             }
                         }
                     }
@@ -396,7 +400,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         if (FULL) {
             tree.step(h, ob + hco - 64, obj * a.N + ci, true);
         } else if (mine) {
-            u32x4 *cvp = reinterpret_cast<u32x4 *>(a.cv + (obj * a.N + ci) * 32);
+            auto *cvp = bao::glb(reinterpret_cast<u32x4 *>(a.cv + (obj * a.N + ci) * 32));
             cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
             cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
         }
