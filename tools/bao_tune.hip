@@ -40,7 +40,7 @@ __global__ void checksum_kernel(const uint64_t *p, size_t n, unsigned long long 
 }
 
 typedef hipError_t (*RunFn)(const uint8_t *, uint64_t, uint64_t, uint64_t, uint8_t *, uint64_t, uint8_t *,
-                            uint32_t *, void *, hipStream_t, size_t);
+                            uint32_t *, void *, hipStream_t, size_t, uint64_t);
 
 struct V {
     std::string name;
@@ -50,13 +50,28 @@ struct V {
     size_t pad_lds;
 };
 
-template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0>
+template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0, bool DQ = false>
 V mk(bool stream, size_t pad_lds = 0) {
     char b[96];
-    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d xg%d pad%zu", MODE == 3 ? "in-place" : MODE ? "decode" : "encode",
-             CPL, NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, XG, pad_lds);
-    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE, XG>, CPL, stream, pad_lds};
+    snprintf(b, sizeof b, "%s CPL%d %s %s sp%d su%d se%d xg%d dq%d pad%zu", MODE == 3 ? "in-place" : MODE ? "decode" : "encode",
+             CPL, NTS ? "nt " : "pln", stream ? "stream" : "hash-only", SP, SU, SE, XG, (int)DQ, pad_lds);
+    return V{b, run_bao_t<MODE, CPL, NTS, SP, SU, SE, XG, DQ>, CPL, stream, pad_lds};
 }
+
+namespace chip {
+int num_cus() { return 256; }
+// run-queue counters for the DQ (persistent) variants: one zeroed block, as the library's per-stream one
+hipError_t stream_queue(hipStream_t, uint32_t **out) {
+    static uint32_t *q = nullptr;
+    if (!q) {
+        hipError_t e = hipMalloc(&q, 4096);
+        if (e != hipSuccess) return e;
+        if ((e = hipMemset(q, 0, 4096)) != hipSuccess) return e;
+    }
+    *out = q;
+    return hipSuccess;
+}
+}  // namespace chip
 
 int main(int argc, char **argv) {
     const uint64_t count = argc > 1 ? atoll(argv[1]) : 256;
@@ -75,9 +90,11 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&scratch, bao_scratch_len_t<1>(n, count)));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xB1A3ull);
     // product encode / decode / in-place, each with the XCD-grouped block order (XG 1)
-    std::vector<V> vs = {mk<0, 2, false, 3, 1, 0, 1>(true), mk<0, 2, false, 3, 2, 0, 1>(true),
-                         mk<0, 2, false, 3, 4, 0, 1>(true), mk<0, 2, false, 3, 8, 0, 1>(true),
-                         mk<0, 2, false, 3, 1, 1, 1>(true)};
+    // encode with the stream (SP 3, the non-64-KiB-multiple path), decode (product: CPL 2, nt content
+    // stores, XG 1, DQ), hash-only encode for the VALU ceiling.  A decode variant issuing the content
+    // stores after the next step's loads (read back from the rows) measured the same (r2x_bao_tune.txt)
+    std::vector<V> vs = {mk<0, 2, false, 3, 8, 0, 1, true>(true), mk<1, 2, true, 0, 1, 0, 1, true>(true),
+                         mk<0, 2, false, 0, 1, 0, 1, true>(false)};
     // earlier: product encode / decode / in-place with XG 0 and 1 (profiles/r1x_ab_bao_xcd_order.txt)
     // round-1 store diagnostics (profiles/r1x_bao_store_diagnostics.txt): mk<0, 2, false>(false) hash-only,
     // mk<0, 2, false, 3, 1, SE>(true) for SE 2..5, mk<0, 1, false, 3>(true), mk<1, 1, false>(true)
@@ -109,13 +126,13 @@ int main(int argc, char **argv) {
             const bool inplace = vs[v].name[0] == 'i';
             auto launch = [&] {
                 if (inplace) {
-                    CK(vs[v].fn(out, ostride, n, count, out, ostride, hash, nullptr, scratch, 0, vs[v].pad_lds));
+                    CK(vs[v].fn(out, ostride, n, count, out, ostride, hash, nullptr, scratch, 0, vs[v].pad_lds, ~0ull));
                 } else if (dec_mode) {
                     CK(hipMemsetAsync(status, 0, count * 4, 0));
-                    CK(vs[v].fn(out, ostride, n, count, dec, n, hash, status, scratch, 0, vs[v].pad_lds));
+                    CK(vs[v].fn(out, ostride, n, count, dec, n, hash, status, scratch, 0, vs[v].pad_lds, ~0ull));
                 } else {
                     CK(vs[v].fn(in, n, n, count, vs[v].stream ? out : nullptr, ostride, hash, nullptr, scratch, 0,
-                                vs[v].pad_lds));
+                                vs[v].pad_lds, ~0ull));
                 }
             };
             launch();

@@ -106,6 +106,11 @@ int main(int argc, char **argv) {
     const char *which = argc > 3 ? argv[3] : "all";
     std::vector<Variant> all = {
         {"K0 FULL (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
+        {"K0 FULL ORD0", fused::zfec_bao_fused_kernel<true, true, 0, 0, 0>, 0},
+        {"K0 FULL ORD2", fused::zfec_bao_fused_kernel<true, true, 2, 0, 0>, 0},
+        {"K0 FULL ORD3", fused::zfec_bao_fused_kernel<true, true, 3, 0, 0>, 0},
+        {"K1 ORD2", fused::zfec_bao_fused_kernel<true, true, 2, 0, 1>, 1},
+        {"K1 ORD3", fused::zfec_bao_fused_kernel<true, true, 3, 0, 1>, 1},
         {"K0 general", fused::zfec_bao_fused_kernel<true, false, 1, 0, 0>, 0},
         {"K1 (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1>, 1},
         {"K0 DG1 no line stores/reads", fused::zfec_bao_fused_kernel<true, true, 1, 1, 0>, 0},
