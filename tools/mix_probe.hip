@@ -2,7 +2,7 @@
 // object, 16 B per lane per stream, no GF maths) under store cache policies,
 // wave counts, object-to-XCD placements and store orders that stream_probe /
 // write_probe did not cover.  Calibration tool (not product code).
-//   mix_probe [objects=1024] [rounds=5]
+//   mix_probe [objects=1024] [rounds=5] [alloc: hip | bal]  (bal = the library's class-balanced allocator)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -10,6 +10,10 @@
 #include <cstdlib>
 #include <string>
 #include <vector>
+
+#include <cstring>
+
+#include "../carbonado_amd/csrc/hbm_alloc.hpp"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -101,6 +105,10 @@ __global__ __launch_bounds__(256) void k_read(const u32x4 *in, size_t n, u32x4 *
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) acc ^= in[i];
     if ((acc.x & acc.y & acc.z & acc.w) == 0xFFFFFFFFu) sink[0] = acc;
 }
+__global__ __launch_bounds__(256) void k_copy(const u32x4 *in, u32x4 *out, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        __builtin_nontemporal_store(in[i], out + i);
+}
 __global__ __launch_bounds__(256) void k_write(u32x4 *out, size_t n) {
     const u32x4 v = {1, 2, 3, (uint32_t)blockIdx.x};
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) out[i] = v;
@@ -111,8 +119,15 @@ int main(int argc, char **argv) {
     const int rounds = argc > 2 ? atoi(argv[2]) : 5;
     const uint64_t n = 16ull << 20, C = n / 4;
     uint8_t *in, *out;
-    CK(hipMalloc(&in, count * n));
-    CK(hipMalloc(&out, count * 2 * n));
+    const bool bal = argc > 3 && !strcmp(argv[3], "bal");
+    if (bal) {
+        CK(chip::hbm::Allocator::get().alloc(count * n, reinterpret_cast<void **>(&in)));
+        CK(chip::hbm::Allocator::get().alloc(count * 2 * n, reinterpret_cast<void **>(&out)));
+    } else {
+        CK(hipMalloc(&in, count * n));
+        CK(hipMalloc(&out, count * 2 * n));
+    }
+    printf("buffers: %s\n", bal ? "class-balanced (hbm_alloc.hpp)" : "hipMalloc");
     CK(hipMemset(in, 7, count * n));
     CK(hipMemset(out, 0, count * 2 * n));
     struct V {
@@ -143,7 +158,7 @@ int main(int argc, char **argv) {
         CK(hipEventElapsedTime(&t, e0, e1));
         return t;
     };
-    std::vector<std::vector<float>> ms(vs.size() + 2);
+    std::vector<std::vector<float>> ms(vs.size() + 3);
     for (int rd = 0; rd < rounds; ++rd) {
         for (size_t i = 0; i < vs.size(); ++i) {
             Args a{in, out, C, count};
@@ -154,12 +169,19 @@ int main(int argc, char **argv) {
         }));
         ms[vs.size() + 1].push_back(
             timed([&] { hipLaunchKernelGGL(k_write, dim3(4096), dim3(256), 0, 0, (u32x4 *)out, count * 2 * n / 16); }));
+        ms[vs.size() + 2].push_back(timed([&] {
+            hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, 0, (const u32x4 *)in, (u32x4 *)out, count * n / 16);
+        }));
     }
     for (size_t i = 0; i < ms.size(); ++i) {
         auto t = ms[i];
         std::sort(t.begin(), t.end());
-        const char *name = i < vs.size() ? vs[i].name.c_str() : i == vs.size() ? "read-only (input)" : "write-only (output)";
-        const double bytes = i < vs.size() ? vs[i].bpi * count * n : i == vs.size() ? 1.0 * count * n : 2.0 * count * n;
+        const size_t x = i - vs.size();
+        const char *name = i < vs.size() ? vs[i].name.c_str()
+                           : x == 0      ? "read-only (input)"
+                           : x == 1      ? "write-only (output)"
+                                         : "copy 1:1 (input -> output, nt stores)";
+        const double bytes = i < vs.size() ? vs[i].bpi * count * n : x == 0 ? 1.0 * count * n : 2.0 * count * n;
         printf("%-40s median %7.3f ms min %7.3f -> %7.1f GB/s (median) %7.1f (best)\n", name, t[t.size() / 2], t[0],
                bytes / (t[t.size() / 2] * 1e-3) / 1e9, bytes / (t[0] * 1e-3) / 1e9);
     }
