@@ -900,7 +900,12 @@ def main():
     scatter = None
     if world > 1 and not args.dry_run and not args.scatter and args.scatter_gib > 0:
         if torch.cuda.device_count() >= world:
-            scatter = wl.scatter_sample(rank, world, args.scatter_gib)
+            try:  # outside the metric: an RCCL failure is reported, not fatal to the measurement
+                scatter = wl.scatter_sample(rank, world, args.scatter_gib)
+            except (RuntimeError, ValueError) as e:
+                scatter = {"error": f"{type(e).__name__}: {e}"[:300]}
+                torch.cuda.synchronize()
+                barrier(world)
         else:  # a rehearsal with several ranks on one GPU: RCCL refuses two ranks on one device
             scatter = {"skipped": f"{world} ranks share {torch.cuda.device_count()} GPU(s); RCCL needs one GPU per rank"}
     elapsed, launch_ms = wl.time_steps(args.steps, args.warmup, world)
