@@ -432,8 +432,10 @@ class Workload:
                 return t
             return torch.empty(shape, dtype=torch.uint8, device=dev)
         self.batch_buf = batch_buf
-        self.inp_full = batch_buf((count, n + args.in_pad_kib * 1024), "in")
-        self.inp = self.inp_full[:, :n] if args.in_pad_kib else self.inp_full
+        # bao mode: 16-B aligned object rows for any n (the content mode's rule), handed over whole
+        row = ((n + 15) // 16 * 16 if args.mode == "bao" else n) + args.in_pad_kib * 1024
+        self.inp_full = batch_buf((count, row), "in")
+        self.inp = self.inp_full[:, :n] if row != n else self.inp_full
         self.scatter_s = None
         rng = object_range(rank, world, world * count)
         if args.scatter and world > 1:
@@ -690,11 +692,12 @@ class Workload:
             self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.bao_scratch(n, count, dev)
-            self.step = lambda: device.bao_encode_batch(self.inp, n, self.out, self.hashes, self.scratch)
+            self.step = lambda: device.bao_encode_batch(self.inp_full, n, self.out, self.hashes, self.scratch)
             self.alg_bytes = count * (n + blen)
-            fused = n >= 65536 and n % 65536 == 0 and os.environ.get("CHIP_FUSED", "1") != "0"
+            fused = n >= 65536 and os.environ.get("CHIP_FUSED", "1") != "0"
             self.kernel = ("zfec_bao_fused_kernel content mode (chunk hashing + tree levels 1-3, 64 consecutive "
-                           "chunks per wave) + bao_parent_kernel levels from level 4" if fused else
+                           "chunks per wave) + bao_parent_kernel levels from level 4"
+                           + ("" if n % 65536 == 0 else " + bao_tail_kernel (the last < 64 chunks)") if fused else
                            "bao_chunk_kernel + bao_parent_kernel levels")
             self.kernel_sym = "zfec_bao_fused_kernel" if fused else "bao_chunk_kernel<0,"
         torch.cuda.synchronize()

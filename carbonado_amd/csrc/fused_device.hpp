@@ -58,8 +58,9 @@ struct FusedArgs {
     uint64_t count, N, cols, bpo;   // objects, chunks per stream, chunk-columns per shard, blocks per object
     const uint32_t *table;          // [4][256] packed parity products (4 parity rows per dword)
     const uint64_t *coff;           // [N] stream offset of each chunk (bao_chunk_table)
-    uint8_t *cv;                    // level-0 CVs [count][N], or level-3 CVs [count][N/8] (FULL)
+    uint8_t *cv;                    // level-0 CVs [count][N], or level-3 CVs [count][cvs] (FULL)
     uint32_t *queue;                // block queue (DQ): [0] next block, [32] waves done; zero at launch
+    uint64_t cvs;                   // FULL: level-3 CVs per object = ceil(N / 8)
 };
 
 __device__ __forceinline__ int dofs(int step) { return 4 + (step & 1) * 32; }
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             bao::wave_sync();
         }
         if (FULL) {
-            tree.step(h, ob + hco - 64, obj * a.N + ci, true);
+            tree.step(h, ob + hco - 64, obj * 8 * a.cvs + ci, true);
         } else if (mine) {
             auto *cvp = bao::glb(reinterpret_cast<u32x4 *>(a.cv + (obj * a.N + ci) * 32));
             cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
@@ -417,6 +418,75 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             a.queue[32] = 0u;
         }
     }
+}
+
+// The last chunks of a content-mode bao encode (encode() level 4/8, bao of the
+// content) whose chunk count is not a multiple of 64: KIND 1 covers the whole
+// 64-chunk blocks [0, Nf) of every object, this kernel the rest [Nf, N), at
+// most 64 chunks including a short last chunk: one wave per object, one lane
+// per chunk, content read and copied into the chunk's slot straight from
+// memory (a few KiB per object), levels 1-3 of the tail's aligned 8-chunk
+// groups merged through lane shuffles with bao's promotion rule (a node
+// without a right child is its left child), nodes written at their slots and
+// the level-3 CVs stored beside KIND 1's for the parent kernels (from level
+// 4).  N > 64, so none of these nodes is the root.
+struct TailArgs {
+    const uint8_t *in;
+    uint64_t in_stride, n;
+    uint8_t *out;
+    uint64_t out_stride;
+    uint64_t count, N, Nf, cvs;
+    const uint64_t *coff;  // [N] stream offset of each chunk
+    uint8_t *cv;           // level-3 CVs [count][cvs]
+};
+
+__global__ __launch_bounds__(64) void bao_tail_kernel(TailArgs a) {
+    const uint64_t obj = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint64_t ci = a.Nf + (uint64_t)lane;
+    const bool on = obj < a.count && ci < a.N;
+    const uint8_t *src = a.in + obj * a.in_stride + ci * 1024;
+    uint8_t *ob = a.out + obj * a.out_stride;
+    uint32_t h[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) h[w] = bao::IV(w);
+    if (on) {
+        const uint64_t rem = a.n - ci * 1024;
+        const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;  // >= 1: ci < N = ceil(n / 1024)
+        const uint32_t nb = (clen + 63) / 64;
+        uint8_t *dst = ob + a.coff[ci];  // 8-B aligned slot
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t blen = clen - 64 * b < 64 ? clen - 64 * b : 64u;
+            uint32_t m[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t off = 64 * b + 16 * q;
+                const uint32_t valid = off < clen ? clen - off : 0u;
+                const u32x4 x = valid >= 16 ? *reinterpret_cast<const u32x4 *>(src + off)
+                                            : bao::load16_partial(src + off, valid);
+                m[4 * q] = x.x; m[4 * q + 1] = x.y; m[4 * q + 2] = x.z; m[4 * q + 3] = x.w;
+                if (valid >= 16) bao::store16_a8<false>(dst + off, x);
+                else if (valid) bao::store16_partial(dst + off, x, valid);
+            }
+            const uint32_t flags = (b == 0 ? bao::F_CHUNK_START : 0u) | (b + 1 == nb ? bao::F_CHUNK_END : 0u);
+            bao::b3_compress(h, m, ci, blen, flags);
+        }
+    }
+#pragma unroll
+    for (int L = 1; L <= 3; ++L) {
+        const int d = 1 << (L - 1);
+        uint32_t r[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) r[w] = (uint32_t)__shfl((int)h[w], (lane + d) & 63);
+        if (on && (lane & (2 * d - 1)) == 0 && ci + d < a.N) {  // a real node: both children exist
+            uint32_t p[8];
+            bao::node_io<0, false>(ob + bao::parent_stream_off(ci, L, a.N), h, r);
+            bao::b3_parent(h, r, false, p);
+#pragma unroll
+            for (int w = 0; w < 8; ++w) h[w] = p[w];
+        }
+    }
+    if (on && (lane & 7) == 0) bao::store_cv(a.cv + (obj * a.cvs + ci / 8) * 32, h);
 }
 
 }  // namespace fused

@@ -54,6 +54,7 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     a.cols = C / 1024;
     a.N = 8 * a.cols;
     a.bpo = (a.cols + 7) / 8;
+    a.cvs = a.N / 8;
     const void *tab = nullptr;
     hipError_t e = zfec_parity_table(4, 8, &tab);
     if (e != hipSuccess) return e;
@@ -123,9 +124,12 @@ bool fused_on() {
     return on;
 }
 
+// Content mode: objects of at least one 64-chunk block; whole blocks run in
+// KIND 1, the last < 64 chunks (when 64 KiB does not divide n) in the tail
+// kernel.
 bool bao_fused_ok(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count) {
-    return n >= 65536 && n % 65536 == 0 && (reinterpret_cast<uintptr_t>(d_in) & 15) == 0 &&
-           (count <= 1 || in_stride % 16 == 0);
+    return n >= 65536 && (reinterpret_cast<uintptr_t>(d_in) & 15) == 0 && (count <= 1 || in_stride % 16 == 0) &&
+           count < (1ull << 31);
 }
 
 hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint8_t *d_out,
@@ -137,9 +141,11 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     a.in = d_in; a.in_stride = in_stride; a.valid = n; a.C = 0;
     a.out = d_out; a.out_stride = out_stride;
     a.count = count;
-    a.N = n / 1024;
+    a.N = bao::n_chunks(n);
     a.cols = 0;
-    a.bpo = a.N / 64;
+    a.bpo = n / 65536;                 // whole 64-chunk blocks (every chunk 1 KiB)
+    a.cvs = (a.N + 7) / 8;             // level-3 CVs per object
+    const uint64_t Nf = 64 * a.bpo;    // chunks [Nf, N): the tail kernel
     a.table = nullptr;
     const uint64_t *coff = nullptr;
     hipError_t e = bao_chunk_table(a.N, &coff);
@@ -156,8 +162,17 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     }();
     (void)attr;
     (void)hipGetLastError();
-    const uint64_t n3 = a.N / 8;  // level-3 CVs per object
+    const uint64_t n3 = a.cvs;
     if ((e = launch_parts(a, n3, K, stream)) != hipSuccess) return e;
+    if (Nf < a.N) {
+        TailArgs t{};
+        t.in = d_in; t.in_stride = in_stride; t.n = n;
+        t.out = d_out; t.out_stride = out_stride;
+        t.count = count; t.N = a.N; t.Nf = Nf; t.cvs = n3;
+        t.coff = coff; t.cv = a.cv;
+        hipLaunchKernelGGL(bao_tail_kernel, dim3((unsigned)count), dim3(64), 0, stream, t);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     uint8_t *next = a.cv + count * n3 * 32;
     return bao::run_parent_levels<0, false>(a.cv, n3, n3, 4, next, (n3 + 1) / 2, a.N, count, d_out, out_stride,
                                             d_hash, nullptr, stream);

@@ -76,6 +76,7 @@ def bao_scratch(n: int, count: int, device=None) -> torch.Tensor:
 def bao_encode_batch(inp: torch.Tensor, n: int, out: torch.Tensor | None, hashes: torch.Tensor,
                      scratch: torch.Tensor) -> None:
     """out: uint8 [count, >= bao_len(n)] or None (hash only); hashes: uint8 [count, 32]."""
+    assert inp.is_contiguous() and inp.shape[1] >= n  # the row stride is inp.shape[1]
     count = inp.shape[0]
     check(_lib.lib().chip_bao_encode_batch_dev(
         _p(inp), inp.shape[1], n, count, _p(out) if out is not None else ctypes.c_void_p(0),

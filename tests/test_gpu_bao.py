@@ -8,8 +8,11 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 2049, 3073, 8192, 8193, 65 * 1024 + 7,
-         (1 << 20) + 3, 3 * (1 << 20) + 1024 * 5]
+# from 64 KiB up, encode runs the content mode (K13 KIND 1) on the whole 64-chunk
+# blocks and the tail kernel on the rest: tails of 1 byte, 2 chunks, 9 whole
+# chunks, 64 chunks with a short last one
+SIZES = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 2049, 3073, 8192, 8193, 65536, 65536 + 1, 65 * 1024 + 7,
+         131072 - 5, 4 * 65536 + 9 * 1024, (1 << 20) + 3, 3 * (1 << 20) + 1024 * 5]
 
 
 def rnd(n, seed):
@@ -141,6 +144,32 @@ def test_batch_bao_ragged_large(gpu):
     stride = (blen + 15) // 16 * 16 + 8
     gen = torch.Generator(device="cuda").manual_seed(91)
     inp = torch.randint(0, 256, (count, n + 5), dtype=torch.uint8, device="cuda", generator=gen)
+    out = torch.full((count, stride), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+    device.bao_encode_batch(inp, n, out, hashes, device.bao_scratch(n, count))
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    for o in range(count):
+        oe, oh = O.bao_encode(inp[o, :n].cpu().numpy().tobytes())
+        assert hashes[o].cpu().numpy().tobytes() == oh, o
+        assert host[o, :blen].tobytes() == oe, o
+        assert (host[o, blen:] == 0xA5).all(), o
+
+
+@pytest.mark.parametrize("n", [65536 + 1, 131072 - 5, 40 * 65536 + 17 * 1024 + 999, (16 << 20) + 37])
+def test_batch_bao_content_mode_tail(gpu, n):
+    """Content-mode bao encode of sizes 64 KiB does not divide: K13 KIND 1 on
+    the whole 64-chunk blocks, the tail kernel on the last < 64 chunks (their
+    levels 1-3 and level-3 CVs), the parent kernels from level 4.  Output
+    bases at every 8-B phase of a 128-B line, nothing written past a stream."""
+    import torch
+    from carbonado_amd import device
+    count = 16 if n < (1 << 20) else 3
+    blen = O.lib().orc_bao_encoded_len(n)
+    stride = (blen + 15) // 16 * 16 + 8
+    istride = (n + 15) // 16 * 16
+    gen = torch.Generator(device="cuda").manual_seed(n % 9973)
+    inp = torch.randint(0, 256, (count, istride), dtype=torch.uint8, device="cuda", generator=gen)
     out = torch.full((count, stride), 0xA5, dtype=torch.uint8, device="cuda")
     hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
     device.bao_encode_batch(inp, n, out, hashes, device.bao_scratch(n, count))
