@@ -79,9 +79,10 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
                               uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,
                               hipStream_t stream);
 
-// The same kernel for bao of the content itself (encode() level 8) when every
-// chunk is whole and 64 | N (n % 64 KiB == 0, 16-B aligned rows); bao_encode_dev
-// takes it then.  Scratch: bao_scratch_len covers it.
+// The same kernel for bao of the content itself (encoding::bao, encode() at
+// the Bao bit, level 4) for n >= 64 KiB with 16-B aligned rows: the whole
+// 64-chunk blocks in KIND 1, the rest in bao_tail_kernel; bao_encode_dev takes
+// it then.  Scratch: bao_scratch_len covers it.
 bool bao_fused_ok(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count);
 hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint8_t *d_out,
                          uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t stream);

@@ -144,8 +144,8 @@ struct Tree {
 // loads after them; ORD 2 issues those loads first, as soon as the step's
 // rows are written.
 // KIND 0: encode() Zfec|Bao (zfec 4-of-8, then bao of the 8 shards); KIND 1:
-// bao of the content itself (encode() level 8, FULL only: 64 | N, every chunk
-// whole).  KIND 1's block is 64 consecutive chunks (row / hash lane
+// bao of the content itself (encoding::bao, encode() level 4; FULL only: the
+// launch covers the whole 64-chunk blocks, bao_tail_kernel the rest).  KIND 1's block is 64 consecutive chunks (row / hash lane
 // L = chunk ub + L), loaded 8 x 16 B per lane per step instead of computed.
 template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     }
 }
 
-// The last chunks of a content-mode bao encode (encode() level 4/8, bao of the
+// The last chunks of a content-mode bao encode (encode() level 4, bao of the
 // content) whose chunk count is not a multiple of 64: KIND 1 covers the whole
 // 64-chunk blocks [0, Nf) of every object, this kernel the rest [Nf, N), at
 // most 64 chunks including a short last chunk: one wave per object, one lane
