@@ -102,6 +102,7 @@ int main(int argc, char **argv) {
         a.in = in; a.in_stride = n; a.valid = n; a.C = k ? 0 : C; a.out = out; a.out_stride = bstride;
         a.count = count; a.N = k ? N1 : N0; a.cols = k ? 0 : C / 1024; a.bpo = k ? N1 / 64 : (C / 1024 + 7) / 8;
         a.table = dtab; a.coff = dcoff[k]; a.cv = cv; a.queue = dq;
+        a.cvs = a.N / 8;  // level-3 CVs per object (FULL)
     }
     const char *which = argc > 3 ? argv[3] : "all";
     std::vector<Variant> all = {
@@ -116,6 +117,8 @@ int main(int argc, char **argv) {
         {"K0 DG1 no line stores/reads", fused::zfec_bao_fused_kernel<true, true, 1, 1, 0>, 0},
         {"K0 DG7 piece reads, no stores", fused::zfec_bao_fused_kernel<true, true, 1, 7, 0>, 0},
         {"K0 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 0>, 0},
+        {"K0 DG5 aligned lines", fused::zfec_bao_fused_kernel<true, true, 1, 5, 0>, 0},
+        {"K1 DG5 aligned lines", fused::zfec_bao_fused_kernel<true, true, 1, 5, 1>, 1},
         {"K1 DG1 no line stores/reads", fused::zfec_bao_fused_kernel<true, true, 1, 1, 1>, 1},
         {"K1 DG7 piece reads, no stores", fused::zfec_bao_fused_kernel<true, true, 1, 7, 1>, 1},
         {"K1 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 1>, 1}};
