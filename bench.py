@@ -76,6 +76,7 @@ def parse(argv=None):
                          "file: file::encode of flat files on disk to .c<level> files (file.rs:409-440)")
     ap.add_argument("--file-dir", default=None, help="file mode: working directory (default $TMPDIR/carbonado_files)")
     ap.add_argument("--fsync", action="store_true", help="file mode: fsync every output file")
+    ap.add_argument("--file-slice", type=int, default=64, help="file mode: files per pipeline slice")
     ap.add_argument("--level", type=int, default=12, help="e2e mode: Format bits (Bao|Zfec = 12)")
     ap.add_argument("--slots", type=int, default=3, help="e2e mode: pipeline slots (streams)")
     ap.add_argument("--slice-mib", type=int, default=256, help="e2e mode: input bytes per pipeline slice")
@@ -597,7 +598,7 @@ class Workload:
                 d.mkdir(exist_ok=True)
                 self.file_step += 1
                 self.file_stats = {}
-                self.results = cfile.encode_files(self.paths, d, self.sk, lv,
+                self.results = cfile.encode_files(self.paths, d, self.sk, lv, slice_objects=args.file_slice,
                                                   host_threads=args.host_threads, fsync=args.fsync,
                                                   stats=self.file_stats)
             self.step = step
