@@ -117,7 +117,7 @@ def parse(argv=None):
     ap.add_argument("--live-pmc", choices=["auto", "on", "off"], default="auto",
                     help="measure roofline.traffic in this run: two child processes of the same workload under "
                          "`rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (one pass each) before this process "
-                         "touches the GPU; auto = on for encode/decode at N=1")
+                         "touches the GPU; auto = on at N=1 for the device-resident modes with one dominant kernel")
     args = ap.parse_args(argv)
     if args.config:
         explicit = {a.dest for a in ap._actions if any(o in (argv if argv is not None else sys.argv[1:])
@@ -208,11 +208,18 @@ def measured_traffic(spec: str, kernel_sym: str, alg_bytes: int):
 
 def pmc_kernel_sym(args) -> str | None:
     """Substring of the rocprofv3 kernel name of the mode's dominant kernel
-    (the Workload's kernel_sym), for the HBM-bound modes the live PMC covers."""
+    (the Workload's kernel_sym) for the device-resident modes the live PMC
+    covers: one launch of it per step."""
+    fused = os.environ.get("CHIP_FUSED", "1") != "0"
+    n = int(args.object_mib * (1 << 20))
     if args.mode == "encode":
         return f"gf_apply_kernel<{args.k}, {(args.m - args.k + 3) // 4},"
     if args.mode == "decode":
         return f"gf_apply_kernel<{args.k}, 1,"
+    if fused and ((args.mode == "bao" and n >= 65536) or (args.mode == "pipeline" and args.level & 12 == 12)):
+        return "zfec_bao_fused_kernel"
+    if args.mode == "bao-decode" or (args.mode == "pipeline-decode" and args.level & 4):
+        return "bao_chunk_kernel<1,"
     return None
 
 
@@ -1024,6 +1031,12 @@ def main():
                                        "BLAKE3 compression (content blocks + parents)"
                                        + ("; achieved over the whole step (every kernel of the level)"
                                           if pipe else "")}
+            for key in ("traffic_ratio", "pmc_KiB_per_launch", "pmc_kernel", "alg_bytes_per_launch"):
+                if key in hbm:
+                    res["roofline"][key] = hbm[key]
+            if pipe and "pmc_kernel" in hbm:
+                res["roofline"]["note_traffic"] = ("traffic: the one dominant kernel's launch (the parent-level "
+                                                   "kernels after it move a few % more); alg bytes: the whole step")
         if world > 1:
             fr = [wl.alg_bytes / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS if res["roofline"]["unit"] == "GB/s" else 1)
                   for ms in rank_avg_ms]
