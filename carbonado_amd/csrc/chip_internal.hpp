@@ -61,7 +61,8 @@ struct GfLaunch {
 
 // Enqueue the matrix apply.  Tables are cached device-side per plan key.
 // Plans with more than ZF_MAXP computed rows run in passes of ZF_MAXP rows
-// (copies ride on the first pass); k > ZF_MAXK uses the generic kernel.
+// (copies ride on the first pass); k outside the fast kernel's instances (1..8,
+// 16) uses the generic kernel.
 hipError_t gf_apply(const GfPlan &plan, const GfLaunch &L, hipStream_t stream);
 // Device copy of the packed parity table of a k-of-m encode (m - k <= 4):
 // [k][256] dwords, byte r of entry [s][x] = E[k + r][s] * x (cached).

@@ -366,7 +366,11 @@ hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out) {
 
 hipError_t gf_apply(const GfPlan &p, const GfLaunch &L, hipStream_t stream) {
     if (L.count == 0 || L.C == 0) return hipSuccess;
-    if (p.k > (uint32_t)ZF_MAXK) return apply_generic(p, L, stream);
+    KernelInfo fast;  // the fast kernel is instantiated for k in 1..8 and 16; other k take the generic one
+    if (p.k > (uint32_t)ZF_MAXK || !lookup_fast((int)p.k, 1, fast)) {
+        if (L.bao_off) return hipErrorInvalidValue;  // the bao-layout store exists for 4-of-8 only
+        return apply_generic(p, L, stream);
+    }
     if (p.np == 0) return gf_apply_pass(p, L, stream, 0, 0, true);
     for (uint32_t row0 = 0; row0 < p.np; row0 += ZF_MAXP) {
         const uint32_t nrows = p.np - row0 < (uint32_t)ZF_MAXP ? p.np - row0 : (uint32_t)ZF_MAXP;

@@ -1,0 +1,101 @@
+"""Seeded randomized parity: the device batch paths against the C oracle over
+sizes drawn around the boundaries the kernels branch on (1 KiB chunks, 4 KiB
+zfec tiles, 8 KiB column groups, 64 KiB content-mode blocks, 32 KiB level-12
+full blocks), random batch counts, row strides and output line phases, and
+random zfec shapes with random erasure sets.  Every case is bit-exact or the
+test fails; the seeds are fixed, so a failure reproduces."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+BOUNDARIES = [1024, 4096, 8192, 32768, 65536, 131072, 1 << 20]
+
+
+def draw_size(rng) -> int:
+    base = int(rng.choice(BOUNDARIES)) * int(rng.integers(1, 4))
+    return max(1, base + int(rng.integers(-70, 71)))
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_encode_decode_batch_dev_random(gpu, case):
+    """chip_encode_batch_dev then chip_decode_batch_dev at a random device-only
+    level: every object's encoding equals the oracle's encode(), every object
+    decodes back (status 0), nothing is written past an encoding."""
+    import torch
+    from carbonado_amd import device
+    rng = np.random.default_rng(0xF022 + case)
+    level = int(rng.choice([4, 8, 12]))
+    n = draw_size(rng)
+    count = int(rng.integers(1, 5))
+    stride = (n + int(rng.integers(0, 64)) + 15) // 16 * 16
+    host = rng.integers(0, 256, (count, stride), dtype=np.uint8)
+    inp = torch.from_numpy(host).cuda()
+    cap = device._lib.lib().chip_encode_max_len(n)
+    ostride = (cap + 15) // 16 * 16 + 16 * int(rng.integers(0, 8))
+    out = torch.full((count, ostride), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    olen, info = device.encode_batch(level, inp, n, out, hashes, device.encode_scratch(level, n, count))
+    torch.cuda.synchronize()
+    got, gh = out.cpu().numpy(), hashes.cpu().numpy()
+    for o in range(count):
+        enc, h, oinfo = O.encode(host[o, :n].tobytes(), level)
+        assert olen == len(enc), (level, n)
+        assert got[o, :olen].tobytes() == enc, (level, n, o)
+        assert (got[o, olen:] == 0xA5).all(), (level, n, o)
+        if level & 4:
+            assert gh[o].tobytes() == h, (level, n, o)
+    dec = torch.full((count, stride), 0x5A, dtype=torch.uint8, device="cuda")
+    status = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    dlen = device.decode_batch(level, out, olen, hashes, info.padding_len, dec, status,
+                               device.decode_scratch(level, olen, count))
+    torch.cuda.synchronize()
+    assert dlen == n and status.cpu().tolist() == [0] * count
+    assert np.array_equal(dec.cpu().numpy()[:, :n], host[:, :n])
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_bao_batch_random_line_phase(gpu, case):
+    """bao encode of a random batch (content mode from 64 KiB, K3 below) with
+    an output stride of 8 mod 16, so object bases take varying 8-B phases of
+    a 128-B line."""
+    import torch
+    from carbonado_amd import device
+    rng = np.random.default_rng(0xBA0 + case)
+    n = draw_size(rng)
+    count = int(rng.integers(2, 6))
+    blen = O.lib().orc_bao_encoded_len(n)
+    stride = (blen + 15) // 16 * 16 + 8 + 16 * int(rng.integers(0, 8))
+    istride = (n + 15) // 16 * 16
+    host = rng.integers(0, 256, (count, istride), dtype=np.uint8)
+    out = torch.full((count, stride), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+    device.bao_encode_batch(torch.from_numpy(host).cuda(), n, out, hashes, device.bao_scratch(n, count))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for o in range(count):
+        oe, oh = O.bao_encode(host[o, :n].tobytes())
+        assert hashes[o].cpu().numpy().tobytes() == oh, (n, o)
+        assert got[o, :blen].tobytes() == oe, (n, o)
+        assert (got[o, blen:] == 0xA5).all(), (n, o)
+
+
+@pytest.mark.parametrize("case", range(20))
+def test_zfec_random_shape_and_erasures(gpu, case):
+    """zfec k-of-m encode of a random size and shape (k up to 20, m up to
+    k + 12), then decode from a random k-subset of the shares given with
+    their true indices; the shards equal the oracle's."""
+    from carbonado_amd import decoding, encoding
+    rng = np.random.default_rng(0x2FEC + case)
+    k = int(rng.integers(1, 21))
+    m = k + int(rng.integers(1, 13))
+    n = draw_size(rng) // 4 + 1
+    d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    z, pad, C = encoding.zfec(d, k, m)
+    oz, opad, oC = O.zfec_encode(d, k, m)
+    assert (pad, C) == (opad, oC) and z == oz, (k, m, n)
+    keep = sorted(rng.choice(m, size=k, replace=False).tolist())
+    shares = [z[i * C:(i + 1) * C] for i in keep]
+    assert decoding.zfec_chunks(shares, pad, indices=keep, k=k, m=m) == d, (k, m, n, keep)

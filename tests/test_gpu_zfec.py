@@ -29,7 +29,7 @@ def test_encode_4of8_matches_oracle(gpu, n):
     assert encoding.zfec(d) == O.zfec_encode(d)
 
 
-@pytest.mark.parametrize("k,m", [(8, 16), (3, 10), (2, 5), (1, 3), (5, 7), (16, 20), (4, 20), (17, 21), (6, 6)])
+@pytest.mark.parametrize("k,m", [(8, 16), (3, 10), (2, 5), (1, 3), (5, 7), (16, 20), (4, 20), (17, 21), (6, 6), (9, 12), (14, 22)])
 @pytest.mark.parametrize("n", [1, 5000, 100_003])
 def test_encode_other_shapes(gpu, k, m, n):
     from carbonado_amd import encoding
