@@ -2,7 +2,8 @@
 sizes drawn around the boundaries the kernels branch on (1 KiB chunks, 4 KiB
 zfec tiles, 8 KiB column groups, 64 KiB content-mode blocks, 32 KiB level-12
 full blocks), random batch counts, row strides and output line phases, and
-random zfec shapes with random erasure sets.  Every case is bit-exact or the
+random zfec shapes with random erasure sets, and every format level over
+compressible data (the host Snappy stage's copy and literal paths).  Every case is bit-exact or the
 test fails; the seeds are fixed, so a failure reproduces."""
 import numpy as np
 import pytest
@@ -19,7 +20,7 @@ def draw_size(rng) -> int:
     return max(1, base + int(rng.integers(-70, 71)))
 
 
-@pytest.mark.parametrize("case", range(24))
+@pytest.mark.parametrize("case", range(40))
 def test_encode_decode_batch_dev_random(gpu, case):
     """chip_encode_batch_dev then chip_decode_batch_dev at a random device-only
     level: every object's encoding equals the oracle's encode(), every object
@@ -56,7 +57,7 @@ def test_encode_decode_batch_dev_random(gpu, case):
     assert np.array_equal(dec.cpu().numpy()[:, :n], host[:, :n])
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", range(24))
 def test_bao_batch_random_line_phase(gpu, case):
     """bao encode of a random batch (content mode from 64 KiB, K3 below) with
     an output stride of 8 mod 16, so object bases take varying 8-B phases of
@@ -82,7 +83,7 @@ def test_bao_batch_random_line_phase(gpu, case):
         assert (got[o, blen:] == 0xA5).all(), (n, o)
 
 
-@pytest.mark.parametrize("case", range(20))
+@pytest.mark.parametrize("case", range(32))
 def test_zfec_random_shape_and_erasures(gpu, case):
     """zfec k-of-m encode of a random size and shape (k up to 20, m up to
     k + 12), then decode from a random k-subset of the shares given with
@@ -99,3 +100,44 @@ def test_zfec_random_shape_and_erasures(gpu, case):
     keep = sorted(rng.choice(m, size=k, replace=False).tolist())
     shares = [z[i * C:(i + 1) * C] for i in keep]
     assert decoding.zfec_chunks(shares, pad, indices=keep, k=k, m=m) == d, (k, m, n, keep)
+
+
+def compressible(rng, n: int) -> bytes:
+    """Bytes snappy compresses in every way it can: runs, back-references at
+    random distances and lengths (short and long copies, overlapping ones),
+    and literal stretches."""
+    out = bytearray()
+    while len(out) < n:
+        kind = int(rng.integers(0, 4))
+        if kind == 0 or len(out) < 8:
+            out += rng.integers(0, 256, int(rng.integers(1, 200)), dtype=np.uint8).tobytes()
+        elif kind == 1:
+            out += bytes([int(rng.integers(0, 256))]) * int(rng.integers(4, 3000))
+        else:
+            dist = int(rng.integers(1, min(len(out), 70_000) + 1))
+            ln = int(rng.integers(4, 300))
+            start = len(out) - dist
+            for i in range(ln):
+                out.append(out[start + i])
+    return bytes(out[:n])
+
+
+@pytest.mark.parametrize("case", range(32))
+def test_every_level_compressible_random(gpu, case):
+    """encode() at a random level of compressible data with the ECIES
+    randomness injected == the C oracle's full pipeline; decode() inverts it."""
+    import carbonado_amd as ca
+    from oracle import host_oracle as H
+    rng = np.random.default_rng(0xC0DE + case)
+    level = int(rng.integers(0, 16))
+    n = int(rng.choice([int(rng.integers(0, 5000)), draw_size(rng), int(rng.integers(300_000, 1_500_000))]))
+    d = compressible(rng, n)
+    sk = H.sha256(b"fuzz receiver %d" % case)
+    pub = H.public_key(sk)
+    eph = H.sha256(b"fuzz eph %d" % case)
+    nonce = H.sha256(b"fuzz nonce %d" % case)[:16]
+    enc, h, info = ca.encode(pub, d, level, ephemeral_sk=eph, nonce=nonce)
+    oenc, oh, oinfo = O.c_encode_full(d, level, pub, eph, nonce)
+    assert enc == oenc and h == oh, (level, n)
+    assert info.padding_len == oinfo["padding_len"], (level, n)
+    assert ca.decode(sk, h, enc, info.padding_len, level) == d, (level, n)
