@@ -141,3 +141,47 @@ def test_every_level_compressible_random(gpu, case):
     assert enc == oenc and h == oh, (level, n)
     assert info.padding_len == oinfo["padding_len"], (level, n)
     assert ca.decode(sk, h, enc, info.padding_len, level) == d, (level, n)
+
+
+def chunk_off(i: int, N: int) -> int:
+    """Stream offset of chunk i of an N-chunk bao stream: 8 + 1024 i + 64 (P(i) + c(i))."""
+    def clog2(x):
+        return 0 if x <= 1 else (x - 1).bit_length()
+    cl = clog2(N - i)
+    c = cl if i == 0 else min((i & -i).bit_length() - 1, cl)
+    total, cnt, L = 0, N, 1
+    while cnt > 1:
+        total += min((i + (1 << L) - 1) >> L, cnt // 2)
+        cnt = (cnt + 1) // 2
+        L += 1
+    return 8 + 1024 * i + 64 * (total + c)
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_scrub_random_shard_corruption(gpu, case):
+    """scrub() (decoding.rs:159-212) of a level-12 stream with content bytes
+    flipped inside a random set of shards: up to m - k = 4 damaged shards are
+    repaired bit-exactly (true share indices), 5 or more fail with a zfec
+    error, an intact stream is UnnecessaryScrub."""
+    import carbonado_amd as ca
+    from carbonado_amd.error import UnnecessaryScrub, ZfecError
+    rng = np.random.default_rng(0x5C2B + case)
+    n = draw_size(rng) // 2 + 1
+    d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    enc, h, info = ca.encode(b"", d, 12)
+    cols = info.chunk_len // 1024
+    N = 8 * cols
+    with pytest.raises(UnnecessaryScrub):
+        ca.scrub(enc, h, info)
+    nbad = int(rng.integers(1, 7))
+    shards = sorted(rng.choice(8, size=nbad, replace=False).tolist())
+    bad = bytearray(enc)
+    for s in shards:  # distinct content bytes of the shard, so no flip undoes another
+        for pos in rng.choice(cols * 1024, size=int(rng.integers(1, 4)), replace=False).tolist():
+            i = s * cols + pos // 1024
+            bad[chunk_off(i, N) + pos % 1024] ^= 1 << int(rng.integers(0, 8))
+    if nbad <= 4:
+        assert ca.scrub(bytes(bad), h, info) == enc, (n, shards)
+    else:
+        with pytest.raises(ZfecError):
+            ca.scrub(bytes(bad), h, info)
