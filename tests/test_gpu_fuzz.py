@@ -185,3 +185,50 @@ def test_scrub_random_shard_corruption(gpu, case):
     else:
         with pytest.raises(ZfecError):
             ca.scrub(bytes(bad), h, info)
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_decode_malformed_inputs_random(gpu, case):
+    """decode() of damaged encodings: a CarbonadoError, never a crash, and
+    never a wrong answer where the format can tell (a flipped byte at a level
+    with Bao or Ecies, a truncated encoding, random bytes of a random
+    length)."""
+    import carbonado_amd as ca
+    from carbonado_amd.error import CarbonadoError
+    from oracle import host_oracle as H
+    rng = np.random.default_rng(0xDEAD + case)
+    level = int(rng.integers(0, 16))
+    n = int(rng.choice([int(rng.integers(1, 3000)), draw_size(rng) // 4 + 1]))
+    d = compressible(rng, n) if case % 2 else rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    sk = H.sha256(b"malformed %d" % case)
+    enc, h, info = ca.encode(H.public_key(sk), d, level)
+    assert ca.decode(sk, h, enc, info.padding_len, level) == d
+    # Bao verifies every byte of the encoding; the AES-GCM tag every byte that
+    # decryption reads (without Bao, zfec decode reads the data shards only, so
+    # a flip in a parity shard or the padding is harmless and goes unnoticed,
+    # as in the reference); levels 0, 2, 8, 10 have no integrity check at all
+    detects = bool(level & 4) or bool(level & 1)
+
+    def outcome(buf):
+        try:
+            return ca.decode(sk, h, buf, info.padding_len, level)
+        except CarbonadoError:
+            return None
+    flipped = bytearray(enc)
+    flipped[int(rng.integers(0, len(enc)))] ^= 1 << int(rng.integers(0, 8))
+    got = outcome(bytes(flipped))
+    if level & 4:
+        assert got is None, (level, n)
+    elif level & 1:
+        assert got is None or got == d, (level, n)
+    if len(enc) > 1:
+        got = outcome(enc[:int(rng.integers(0, len(enc)))])
+        if detects:
+            assert got is None, (level, n)
+    junk = rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8).tobytes()
+    try:
+        out = ca.decode(sk, h, junk, info.padding_len, level)
+        assert not detects, "random bytes decoded at a level that verifies its input"
+        assert isinstance(out, bytes)
+    except CarbonadoError:
+        pass
