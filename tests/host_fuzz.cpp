@@ -1,0 +1,182 @@
+// host_fuzz.cpp — test infrastructure (tests/test_host_asan.py builds it with
+// AddressSanitizer + UndefinedBehaviorSanitizer and runs it).  Drives the
+// library's HOST code — snappy framing, ECIES, the one-pass decrypt+unsnap,
+// the 160-byte file header parser — with valid inputs and seeded mutations of
+// them (bit flips, truncations, random chunk headers, random bytes), checking
+// that every call either fails with a status or returns exactly the original
+// bytes, and letting the sanitizers catch any out-of-bounds access.
+//   host_fuzz SECONDS SEED
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../carbonado_amd/csrc/host_stages.hpp"
+#include "../include/carbonado_hip.h"
+
+// file_container.cpp's file::encode/decode call the device pipeline, which is
+// not linked here; the fuzzer never calls them.
+extern "C" {
+uint64_t chip_encode_max_len(uint64_t) { std::abort(); }
+int chip_encode(uint8_t, const uint8_t *, uint64_t, const chip_ecies_inject *, const uint8_t *, uint64_t, uint8_t *,
+                uint64_t, uint64_t *, uint8_t *, chip_encode_info *) {
+    std::abort();
+}
+int chip_decode(const uint8_t *, uint64_t, const uint8_t *, uint64_t, const uint8_t *, uint64_t, uint32_t, uint8_t,
+                uint8_t *, uint64_t, uint64_t *) {
+    std::abort();
+}
+}
+
+using namespace chip::host;
+using Bytes = std::vector<uint8_t>;
+
+static std::mt19937_64 rng;
+static uint64_t rnd(uint64_t n) { return n ? rng() % n : 0; }
+
+static Bytes compressible(size_t n) {
+    Bytes out;
+    while (out.size() < n) {
+        const int kind = (int)rnd(4);
+        if (kind == 0 || out.size() < 8) {
+            for (uint64_t i = 0, k = 1 + rnd(200); i < k; ++i) out.push_back((uint8_t)rng());
+        } else if (kind == 1) {
+            out.insert(out.end(), 4 + rnd(3000), (uint8_t)rng());
+        } else {
+            const size_t dist = 1 + rnd(std::min<size_t>(out.size(), 70000));
+            const size_t start = out.size() - dist;
+            for (uint64_t i = 0, k = 4 + rnd(300); i < k; ++i) out.push_back(out[start + i]);
+        }
+    }
+    out.resize(n);
+    return out;
+}
+
+static Bytes mutate(const Bytes &in) {
+    Bytes b = in;
+    switch (rnd(4)) {
+        case 0:  // bit flips
+            for (uint64_t i = 0, k = 1 + rnd(4); i < k && !b.empty(); ++i) b[rnd(b.size())] ^= (uint8_t)(1u << rnd(8));
+            break;
+        case 1:  // truncation
+            b.resize(rnd(b.size() + 1));
+            break;
+        case 2: {  // a random chunk header (type, 24-bit length) somewhere
+            if (b.size() >= 4) {
+                const size_t p = rnd(b.size() - 3);
+                b[p] = (uint8_t)rng();
+                b[p + 1] = (uint8_t)rng();
+                b[p + 2] = (uint8_t)rng();
+                b[p + 3] = (uint8_t)rnd(4);
+            }
+            break;
+        }
+        default:  // random bytes appended
+            for (uint64_t i = 0, k = 1 + rnd(64); i < k; ++i) b.push_back((uint8_t)rng());
+    }
+    return b;
+}
+
+// memcmp with an empty range may see null pointers (std::vector::data() of an empty vector)
+static bool same(const uint8_t *a, const uint8_t *b, size_t n) { return n == 0 || !std::memcmp(a, b, n); }
+
+static int fails = 0;
+#define EXPECT(c, ...)                             \
+    do {                                           \
+        if (!(c)) {                                \
+            std::fprintf(stderr, "FAIL %s: ", #c); \
+            std::fprintf(stderr, __VA_ARGS__);     \
+            std::fprintf(stderr, "\n");            \
+            ++fails;                               \
+        }                                          \
+    } while (0)
+
+// decompress with an exact-size buffer: an error, or exactly `orig`
+static void snap_check(const Bytes &frame, const Bytes &orig, bool must_match) {
+    uint64_t len = 0;
+    const int sl = snap_decompressed_len(frame.data(), frame.size(), &len);
+    Bytes out(sl == 0 ? len : orig.size());
+    uint64_t got = 0;
+    const int st = snap_decompress(frame.data(), frame.size(), out.data(), out.size(), &got);
+    if (must_match) {
+        EXPECT(st == 0 && got == orig.size() && same(out.data(), orig.data(), got), "valid frame, n=%zu",
+               orig.size());
+    } else if (st == 0) {
+        // a mutation that still decodes passed every chunk's CRC: the original,
+        // or a prefix of it (the frame cut at a chunk boundary: the framing
+        // format has no end marker, so snap's FrameDecoder accepts it too)
+        EXPECT(got <= orig.size() && same(out.data(), orig.data(), got), "mutated frame decoded to other bytes");
+    }
+    if (len > 0 && sl == 0) {  // a buffer one byte short: never written past
+        Bytes small(len - 1);
+        uint64_t g2 = 0;
+        (void)snap_decompress(frame.data(), frame.size(), small.data(), small.size(), &g2);
+    }
+}
+
+int main(int argc, char **argv) {
+    const double seconds = argc > 1 ? std::atof(argv[1]) : 10.0;
+    rng.seed(argc > 2 ? std::strtoull(argv[2], nullptr, 0) : 0xF022ull);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto elapsed = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+    uint8_t sk[32], pub[65];
+    for (auto &x : sk) x = (uint8_t)rng();
+    sk[0] &= 0x7f;
+    EXPECT(ecies_public_key(sk, pub) == 0, "public key");
+    long iters = 0;
+    while (elapsed() < seconds) {
+        ++iters;
+        const size_t n = rnd(4) == 0 ? rnd(300000) : rnd(5000);
+        const Bytes d = rnd(2) ? compressible(n) : [&] { Bytes r(n); for (auto &x : r) x = (uint8_t)rng(); return r; }();
+        // snappy framing
+        Bytes frame(snap_max_len(n));
+        uint64_t fl = 0;
+        EXPECT(snap_compress(d.data(), n, frame.data(), frame.size(), &fl) == 0, "compress n=%zu", n);
+        frame.resize(fl);
+        snap_check(frame, d, true);
+        for (int k = 0; k < 4; ++k) snap_check(mutate(frame), d, false);
+        // ECIES, and the one-pass decrypt + unsnap of a snappy frame
+        const Bytes &pt = rnd(2) ? frame : d;
+        Bytes ct(pt.size() + ECIES_OVERHEAD);
+        uint64_t cl = 0;
+        EXPECT(ecies_encrypt(pub, 65, nullptr, nullptr, pt.data(), pt.size(), ct.data(), ct.size(), &cl) == 0, "enc");
+        ct.resize(cl);
+        for (int k = 0; k < 3; ++k) {
+            const Bytes bad = k == 0 ? ct : mutate(ct);
+            Bytes out(pt.size() + 16);
+            uint64_t ol = 0;
+            const int st = ecies_decrypt(sk, 32, bad.data(), bad.size(), out.data(), out.size(), &ol);
+            if (k == 0) EXPECT(st == 0 && ol == pt.size() && same(out.data(), pt.data(), ol), "dec");
+            else if (st == 0) EXPECT(ol == pt.size() && same(out.data(), pt.data(), ol), "mutated ct decrypted");
+            if (&pt == &frame) {
+                Bytes o2(n + 16);
+                uint64_t l2 = 0;
+                const int s2 = ecies_decrypt_snap(sk, 32, bad.data(), bad.size(), o2.data(), o2.size(), &l2);
+                if (k == 0) EXPECT(s2 == 0 && l2 == n && same(o2.data(), d.data(), n), "dec+unsnap");
+                else if (s2 == 0) EXPECT(l2 == n && same(o2.data(), d.data(), n), "mutated dec+unsnap");
+            }
+        }
+        // the 160-byte file header
+        chip_header h{};
+        uint8_t hash[32], meta[8], aux[32], bytes[CHIP_HEADER_LEN];
+        for (auto &x : hash) x = (uint8_t)rng();
+        for (auto &x : meta) x = (uint8_t)rng();
+        for (auto &x : aux) x = (uint8_t)rng();
+        EXPECT(chip_header_new(sk, 32, pub, 65, hash, 32, (uint8_t)rnd(16), (uint8_t)rng(), (uint32_t)rng(),
+                               (uint32_t)rng(), rnd(2) ? meta : nullptr, aux, &h) == 0, "header new");
+        EXPECT(chip_header_to_bytes(&h, bytes) == 0, "header bytes");
+        chip_header back{};
+        EXPECT(chip_header_parse(bytes, CHIP_HEADER_LEN, &back) == 0 && !std::memcmp(&back.hash, &h.hash, 32),
+               "header parse");
+        const Bytes good(bytes, bytes + CHIP_HEADER_LEN);
+        for (int k = 0; k < 4; ++k) {
+            const Bytes bad = mutate(good);
+            chip_header x{};
+            (void)chip_header_parse(bad.data(), bad.size(), &x);
+        }
+    }
+    std::printf("host_fuzz: %ld iterations in %.1f s, %d failures\n", iters, elapsed(), fails);
+    return fails ? 1 : 0;
+}
