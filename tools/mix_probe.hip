@@ -99,6 +99,29 @@ __global__ __launch_bounds__(TPB) void k_mix(Args a) {
     }
 }
 
+// the zfec 8-of-16 pattern: 8 read + 16 write streams per object (object =
+// 8 shards of C2 bytes in, 16 out), XCD-grouped runs of CH tiles, nt stores
+template <int TPB, int CH>
+__global__ __launch_bounds__(TPB) void k_mix816(Args a) {
+    constexpr uint64_t TILE = TPB * 16;
+    const uint64_t C2 = a.C / 2, tpo = C2 / TILE, T = tpo * a.count, G = gridDim.x, b = blockIdx.x;
+    uint64_t c = (b % 8) * (G / 8) + b / 8, tin = 0;
+    for (;;) {
+        if (tin == CH) { c += G; tin = 0; }
+        const uint64_t t = c * CH + tin++;
+        if (t >= T) break;
+        const uint64_t obj = t / tpo, col = (t - obj * tpo) * TILE + threadIdx.x * 16;
+        const uint8_t *ib = a.in + obj * 4 * a.C;
+        uint8_t *ob = a.out + obj * 8 * a.C;
+        u32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = *(const u32x4 *)(ib + j * C2 + col);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            __builtin_nontemporal_store(j < 8 ? v[j] : (v[j - 8] ^ 0x01020304u), (u32x4 *)(ob + j * C2 + col));
+    }
+}
+
 // copy (1:1) and pure read / pure write references on the same buffers
 __global__ __launch_bounds__(256) void k_read(const u32x4 *in, size_t n, u32x4 *sink) {
     u32x4 acc = {0, 0, 0, 0};
@@ -144,6 +167,9 @@ int main(int argc, char **argv) {
         VV(256, 3, 64, -1, false, false, 4), VV(512, 3, 32, -1, false, false, 2),
         V4(256, 3, 64, -1, 4),               V4(256, 3, 64, 0, 4),
         V4(512, 3, 32, -1, 2),               V4(256, 3, 16, -1, 8),
+        V{"8r16w 256 MAP3 CH32 st-1 bpc2", k_mix816<256, 32>, 256, 512, 3.0},
+        V{"8r16w 256 MAP3 CH32 st-1 bpc4", k_mix816<256, 32>, 256, 1024, 3.0},
+        V{"8r16w 512 MAP3 CH16 st-1 bpc2", k_mix816<512, 16>, 512, 512, 3.0},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
