@@ -928,8 +928,18 @@ def main():
         verified, sample = wl.verify_object0()
     verified_all = None
     want_all = (args.mode == "encode" and not args.no_verify_all) or (args.mode == "pipeline" and args.verify_all)
-    if rank == 0 and want_all and not args.no_verify and not args.dry_run:
-        verified_all = wl.verify_all()
+    if want_all and not args.no_verify and not args.dry_run:
+        # every rank checks its own objects (N > 1: the whole global set), rank 0 reports
+        mine = wl.verify_all(threads=16)
+        if world > 1:
+            every = [None] * world
+            dist.all_gather_object(every, mine)
+            verified_all = {"ok": all(v["ok"] for v in every), "objects": sum(v["objects"] for v in every),
+                            "ranks": world, "mismatched_by_rank": {r: v["mismatched"] for r, v in enumerate(every)
+                                                                   if v["mismatched"]},
+                            "seconds_max": max(v["seconds"] for v in every), "how": mine["how"] + ", on every rank"}
+        else:
+            verified_all = mine
     aliased = None
     if args.mode == "encode" and not args.dry_run and not args.no_aliased:
         a_el, a_ms, a_ok = wl.time_aliased(args.steps, args.warmup, world)
