@@ -65,6 +65,19 @@ struct FusedArgs {
 
 __device__ __forceinline__ int dofs(int step) { return 4 + (step & 1) * 32; }
 
+// LDS address of T[byte b of x] for table slot tb: byte * 64 + tb in two VALU
+// ops for every b.  Written plainly, byte 0 compiles to shift, mask and add;
+// the mask is kept opaque so that the shift and add fuse (v_lshl_add_u32).
+__device__ __forceinline__ uint32_t gf_addr(uint32_t x, int b, uint32_t tb) {
+    constexpr uint32_t ROWB = 4 * FR * 4;
+    if (b == 0) {
+        uint32_t t;
+        asm("v_and_b32 %0, 0xff, %1" : "=v"(t) : "v"(x));
+        return t * ROWB + tb;
+    }
+    return ((x >> (8 * b)) & 0xFFu) * ROWB + tb;
+}
+
 template <bool NT>
 __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
     if (NT) __builtin_nontemporal_store(v, bao::glb(reinterpret_cast<u32x4 *>(p)));
@@ -166,7 +179,6 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     uint32_t *rows = reinterpret_cast<uint32_t *>(lds + TAB_BYTES) + wave * 64 * RW;
-    constexpr int ROWB = 4 * FR * 4;  // table bytes per byte value
     const int rep = lane % FR, grp = (lane & 31) / FR;
     uint32_t tb[4];
     uint64_t ioff[4];
@@ -276,8 +288,9 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                         uint32_t e[4];
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
-                            e[j] = *reinterpret_cast<const uint32_t *>(lds + ((x[j] >> (8 * b)) & 0xFFu) * ROWB + tb[j]);
-                        acc[d * 4 + b] = (e[0] ^ e[1]) ^ (e[2] ^ e[3]);
+                            e[j] = *reinterpret_cast<const uint32_t *>(lds + gf_addr(x[j], b, tb[j]));
+                        // v_bitop3 (gfx950): three of the four terms in one instruction
+                        acc[d * 4 + b] = __builtin_amdgcn_bitop3_b32(e[0], e[1], e[2], 0x96) ^ e[3];
                     }
                 }
             }
