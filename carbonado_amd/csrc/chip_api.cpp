@@ -111,8 +111,22 @@ struct Ctx {
     DevBuf in, mid, out, scratch, small, x1, x2, flags;
     std::vector<Slot> slots;
     Staging stage;
+    // pinned arena for the few-byte copies of a call (hashes, status words,
+    // node flags): see small_h2d / small_d2h / small_sync
+    DevBuf hs;
+    size_t hs_used = 0;
+    struct HsOut {
+        void *dst;
+        const uint8_t *src;
+        size_t n;
+    };
+    std::vector<HsOut> hs_out;
     void release() {
         stage.release();
+        if (hs.p) (void)hipHostFree(hs.p);
+        hs = DevBuf{};
+        hs_used = 0;
+        hs_out.clear();
         // best effort (at process teardown the runtime may already be gone)
         for (DevBuf *b : {&in, &mid, &out, &scratch, &small, &x1, &x2, &flags}) {
             if (b->p) (void)hipFree(b->p);
@@ -221,8 +235,64 @@ int ctx_get(Ctx **out) {
         c.dev = dev;
         c.ready = true;
     }
+    if (c.hs_used) {  // an earlier call returned early: let its copies land, drop its outputs
+        c.hs_out.clear();
+        c.hs_used = 0;
+        CHIP_HIP(hipStreamSynchronize(c.stream));
+    }
     *out = &c;
     return CHIP_OK;
+}
+
+// ---- few-byte copies of a single-object call ------------------------------
+// hipMemcpyAsync on pageable memory costs ~22 us of API time per call, even
+// for 4 bytes (profiles/r4c: the runtime stages and waits), which dominated
+// small objects' latency.  Hashes, status words and node flags therefore go
+// through a pinned per-context arena: small_h2d copies the bytes in at once,
+// small_d2h lands them there and small_sync (the call's stream
+// synchronisation) hands them to their destinations.
+constexpr size_t kHostSmall = size_t(64) << 10;
+
+hipError_t small_h2d(Ctx *c, void *ddst, const void *src, size_t n) {
+    if (!n) return hipSuccess;
+    const size_t need = (n + 15) & ~size_t(15);
+    if (!c->hs.p) {
+        hipError_t e = grow_pinned(c->hs, kHostSmall);
+        if (e != hipSuccess) return e;
+    }
+    if (c->hs_used + need > c->hs.cap) return hipMemcpyAsync(ddst, src, n, hipMemcpyHostToDevice, c->stream);
+    uint8_t *p = static_cast<uint8_t *>(c->hs.p) + c->hs_used;
+    c->hs_used += need;
+    std::memcpy(p, src, n);
+    return hipMemcpyAsync(ddst, p, n, hipMemcpyHostToDevice, c->stream);
+}
+
+// `dst` receives the n bytes at the next small_sync (or d2h_sync)
+hipError_t small_d2h(Ctx *c, void *dst, const void *dsrc, size_t n) {
+    if (!n) return hipSuccess;
+    const size_t need = (n + 15) & ~size_t(15);
+    if (!c->hs.p) {
+        hipError_t e = grow_pinned(c->hs, kHostSmall);
+        if (e != hipSuccess) return e;
+    }
+    if (c->hs_used + need > c->hs.cap) return hipMemcpyAsync(dst, dsrc, n, hipMemcpyDeviceToHost, c->stream);
+    uint8_t *p = static_cast<uint8_t *>(c->hs.p) + c->hs_used;
+    c->hs_used += need;
+    c->hs_out.push_back({dst, p, n});
+    return hipMemcpyAsync(p, dsrc, n, hipMemcpyDeviceToHost, c->stream);
+}
+
+void small_deliver(Ctx *c) {
+    for (const Ctx::HsOut &o : c->hs_out) std::memcpy(o.dst, o.src, o.n);
+    c->hs_out.clear();
+    c->hs_used = 0;
+}
+
+// the call's stream work is done and its small outputs delivered
+hipError_t small_sync(Ctx *c) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) small_deliver(c);
+    return e;
 }
 
 // ---- host <-> HBM copies of the single-object calls -----------------------
@@ -232,10 +302,10 @@ int ctx_get(Ctx **out) {
 // range.  Pageable buffers therefore go through a pinned 4 x 4 MiB ring, the
 // CPU copy of one piece overlapping the DMA of the next (~1.4 ms per 34 MiB
 // resident, ~6.4 ms into untouched memory, tools/pageable_probe.hip,
-// profiles/r1w_pageable_probe.txt).  Pinned (hipHostMalloc'd / registered)
-// memory and small copies go direct.  CHIP_HOST_COPY=direct|staged forces
-// one path (A/B runs).
-constexpr size_t kStageMin = size_t(256) << 10;
+// profiles/r1w_pageable_probe.txt).  Small pageable copies take the ring
+// too: direct, each costs ~22 us of API time whatever its size (r4c).
+// Pinned (hipHostMalloc'd / registered) memory goes direct.
+// CHIP_HOST_COPY=direct|staged forces one path (A/B runs).
 
 int host_copy_mode() {  // 0 auto, 1 direct, 2 staged
     static const int m = [] {
@@ -259,7 +329,7 @@ bool host_pinned(const void *p) {
 
 bool staged(const void *host, size_t n) {
     const int m = host_copy_mode();
-    if (m == 1 || n < kStageMin) return false;
+    if (m == 1 || !n) return false;
     return m == 2 || !host_pinned(host);
 }
 
@@ -908,7 +978,7 @@ int chip_zfec_encode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t n, uint
         GfLaunch L{static_cast<const uint8_t *>(c->in.p), static_cast<uint8_t *>(c->out.p), 0, 0, n, C, 1};
         CHIP_HIP(gf_apply(p, L, c->stream));
         CHIP_HIP(d2h(c->stage, out, c->out.p, total, c->stream));
-        CHIP_HIP(hipStreamSynchronize(c->stream));
+        CHIP_HIP(small_sync(c));
     }
     *padding = pad;
     *chunk_len = (uint32_t)C;
@@ -959,7 +1029,7 @@ int chip_zfec_decode_shares(uint32_t k, uint32_t m, const uint8_t *const *shares
                                 1, static_cast<uint8_t *>(c->out.p), 0, c->stream);
         if (st != CHIP_OK) return st;
         if (olen) CHIP_HIP(d2h(c->stage, out, c->out.p, olen, c->stream));
-        CHIP_HIP(hipStreamSynchronize(c->stream));
+        CHIP_HIP(small_sync(c));
     }
     *out_len = olen;
     return CHIP_OK;
@@ -1211,7 +1281,7 @@ static int bao_encode_ctx(Ctx *c, const uint8_t *d_in, uint64_t n, bool want_str
     uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
     CHIP_HIP(bao_encode_dev(d_in, 0, n, 1, want_stream ? static_cast<uint8_t *>(c->out.p) : nullptr, 0,
                             d_hash, c->scratch.p, c->stream));
-    CHIP_HIP(hipMemcpyAsync(hash, d_hash, 32, hipMemcpyDeviceToHost, c->stream));
+    CHIP_HIP(small_d2h(c, hash, d_hash, 32));
     return CHIP_OK;
 }
 
@@ -1228,7 +1298,7 @@ int chip_bao_encode(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_ca
     st = bao_encode_ctx(c, static_cast<const uint8_t *>(c->in.p), n, true, hash);
     if (st != CHIP_OK) return st;
     CHIP_HIP(d2h(c->stage, out, c->out.p, blen, c->stream));
-    CHIP_HIP(hipStreamSynchronize(c->stream));
+    CHIP_HIP(small_sync(c));
     *out_len = blen;
     return CHIP_OK;
 }
@@ -1242,7 +1312,7 @@ int chip_blake3(const uint8_t *in, uint64_t n, uint8_t hash[CHIP_HASH_LEN]) {
     if (n) CHIP_HIP(h2d(c->stage, c->in.p, in, n, c->stream));
     st = bao_encode_ctx(c, static_cast<const uint8_t *>(c->in.p), n, false, hash);
     if (st != CHIP_OK) return st;
-    CHIP_HIP(hipStreamSynchronize(c->stream));
+    CHIP_HIP(small_sync(c));
     return CHIP_OK;
 }
 
@@ -1254,12 +1324,13 @@ static int bao_decode_ctx(Ctx *c, const uint8_t *d_enc, uint64_t len, uint64_t n
     CHIP_HIP(grow(c->small, 64));
     uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
     uint32_t *d_status = reinterpret_cast<uint32_t *>(d_hash + 32);
-    CHIP_HIP(hipMemcpyAsync(d_hash, hash, 32, hipMemcpyHostToDevice, c->stream));
-    CHIP_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
+    uint8_t hs[36] = {};  // the hash and a zero status word, one copy
+    std::memcpy(hs, hash, 32);
+    CHIP_HIP(small_h2d(c, d_hash, hs, sizeof hs));
     CHIP_HIP(bao_decode_dev(d_enc, 0, n, 1, d_hash, d_dst, 0, d_status, c->scratch.p, c->stream));
     uint32_t status = 0;
-    CHIP_HIP(hipMemcpyAsync(&status, d_status, 4, hipMemcpyDeviceToHost, c->stream));
-    CHIP_HIP(hipStreamSynchronize(c->stream));
+    CHIP_HIP(small_d2h(c, &status, d_status, 4));
+    CHIP_HIP(small_sync(c));
     return status ? (int)status : CHIP_OK;
 }
 
@@ -1292,7 +1363,7 @@ int chip_bao_decode(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint6
                         static_cast<uint8_t *>(c->out.p));
     if (st != CHIP_OK) return st;
     if (n) CHIP_HIP(d2h(c->stage, out, c->out.p, n, c->stream));
-    CHIP_HIP(hipStreamSynchronize(c->stream));
+    CHIP_HIP(small_sync(c));
     *out_len = n;
     return CHIP_OK;
 }
@@ -1307,13 +1378,13 @@ static int node_check_ctx(Ctx *c, uint64_t n, const uint8_t *hash, std::vector<u
     CHIP_HIP(grow(c->flags, 2 * N + 16));
     uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
     uint8_t *d_cf = static_cast<uint8_t *>(c->flags.p), *d_pf = d_cf + N;
-    CHIP_HIP(hipMemcpyAsync(d_hash, hash, 32, hipMemcpyHostToDevice, c->stream));
+    CHIP_HIP(small_h2d(c, d_hash, hash, 32));
     CHIP_HIP(bao_node_check(static_cast<const uint8_t *>(c->in.p), 0, n, 1, d_hash, d_cf, d_pf, c->stream));
     cf->resize(N);
     pf->resize(N - 1);
-    CHIP_HIP(hipMemcpyAsync(cf->data(), d_cf, N, hipMemcpyDeviceToHost, c->stream));
-    if (N > 1) CHIP_HIP(hipMemcpyAsync(pf->data(), d_pf, N - 1, hipMemcpyDeviceToHost, c->stream));
-    CHIP_HIP(hipStreamSynchronize(c->stream));
+    CHIP_HIP(small_d2h(c, cf->data(), d_cf, N));
+    if (N > 1) CHIP_HIP(small_d2h(c, pf->data(), d_pf, N - 1));
+    CHIP_HIP(small_sync(c));
     return CHIP_OK;
 }
 
@@ -1389,7 +1460,7 @@ int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const uint8_t 
         CHIP_HIP(bao_gather_content(static_cast<const uint8_t *>(c->in.p), n, g0, g1,
                                     static_cast<uint8_t *>(c->out.p), c->stream));
         CHIP_HIP(d2h(c->stage, out, static_cast<uint8_t *>(c->out.p) + (start - g0 * 1024), olen, c->stream));
-        CHIP_HIP(hipStreamSynchronize(c->stream));
+        CHIP_HIP(small_sync(c));
     }
     *out_len = olen;
     return CHIP_OK;
@@ -1455,13 +1526,13 @@ int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t h
     uint8_t h2[32];
     st = bao_encode_ctx(c, d_z2, CHIP_FEC_M * C2, true, h2);
     if (st != CHIP_OK) return st;
-    CHIP_HIP(hipStreamSynchronize(c->stream));
+    CHIP_HIP(small_sync(c));
     const uint64_t blen2 = bao_encoded_len(CHIP_FEC_M * C2);
     if (blen2 != len) return CHIP_ERR_SCRUBBED_LENGTH_MISMATCH;  // decoding.rs:198-203
     if (std::memcmp(h2, hash, 32) != 0) return CHIP_ERR_INVALID_SCRUBBED_HASH;  // decoding.rs:205-207
     if (!out || out_cap < blen2) return CHIP_ERR_BUFFER_TOO_SMALL;
     CHIP_HIP(d2h(c->stage, out, c->out.p, blen2, c->stream));
-    CHIP_HIP(hipStreamSynchronize(c->stream));
+    CHIP_HIP(small_sync(c));
     *out_len = blen2;
     return CHIP_OK;
 }
@@ -1509,9 +1580,9 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
             uint8_t *d_hash = static_cast<uint8_t *>(c->small.p);
             CHIP_HIP(zfec_bao_dev(d_cur, 0, cur_n, 1, inf.chunk_len, static_cast<uint8_t *>(c->out.p), 0, d_hash,
                                   c->scratch.p, c->stream));
-            CHIP_HIP(hipMemcpyAsync(hash, d_hash, 32, hipMemcpyDeviceToHost, c->stream));
+            CHIP_HIP(small_d2h(c, hash, d_hash, 32));
             CHIP_HIP(d2h(c->stage, out, c->out.p, final_len, c->stream));
-            CHIP_HIP(hipStreamSynchronize(c->stream));
+            CHIP_HIP(small_sync(c));
             *out_len = final_len;
             if (info) *info = inf;
             return CHIP_OK;
@@ -1531,7 +1602,7 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
             std::memset(hash, 0, 32);  // encoding.rs:145
             if (final_len) CHIP_HIP(d2h(c->stage, out, d_cur, final_len, c->stream));
         }
-        CHIP_HIP(hipStreamSynchronize(c->stream));
+        CHIP_HIP(small_sync(c));
     }
     *out_len = final_len;
     if (info) *info = inf;
@@ -2065,7 +2136,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             d_cur = static_cast<const uint8_t *>(c->out.p);
         }
         if (olen) CHIP_HIP(d2h(c->stage, dst, d_cur, olen, c->stream));
-        CHIP_HIP(hipStreamSynchronize(c->stream));
+        CHIP_HIP(small_sync(c));
         cur = dst;
         cur_n = olen;
     }
