@@ -3,6 +3,9 @@
 // (bao_kernels.hip) and tools/bao_tune.hip.  Design notes: bao_kernels.hip.
 #pragma once
 
+#include <map>
+#include <mutex>
+
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -986,10 +989,24 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
     bool dq = DQ && waves < (1ull << 31);
     if (dq) {  // persistent grid of resident workgroups, wave tasks from the stream's run queue
         uint32_t *q = nullptr;
-        int per_cu = 0;
         const void *fn = reinterpret_cast<const void *>(bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG, true>);
-        dq = stream_queue(stream, &q) == hipSuccess &&
-             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, K3_TPB, pad_lds) == hipSuccess && per_cu > 0;
+        // per instance and LDS pad, asked once: the query costs ~6 us of API
+        // time, which single small objects paid on every call (profiles/r4c)
+        static std::mutex occ_mu;
+        static std::map<size_t, int> occ;
+        int per_cu = 0;
+        {
+            std::lock_guard<std::mutex> lk(occ_mu);
+            auto it = occ.find(pad_lds);
+            if (it != occ.end()) {
+                per_cu = it->second;
+            } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, K3_TPB, pad_lds) == hipSuccess) {
+                occ[pad_lds] = per_cu;
+            } else {
+                per_cu = 0;
+            }
+        }
+        dq = per_cu > 0 && stream_queue(stream, &q) == hipSuccess;
         (void)hipGetLastError();
         if (dq) {
             ca.queue = q + 640;

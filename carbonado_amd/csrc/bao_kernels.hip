@@ -29,6 +29,7 @@
 // K5 (verify-decode) = the same kernels in MODE 1: every stored parent node is
 // compared with the recomputed children, the root with the expected hash.
 #include "bao_device.hpp"
+#include "chip_internal.hpp"
 
 #include <algorithm>
 #include <map>
@@ -82,6 +83,7 @@ uint64_t bao_scratch_len(uint64_t n, uint64_t count) { return bao_scratch_len_t<
 hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                           uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,
                           hipStream_t stream) {
+    if (small_ok(n, count)) return small_bao_encode_dev(d_in, n, d_out, d_hash, stream);
     if (d_out && fused_on() && bao_fused_ok(d_in, in_stride, n, count))  // K13 KIND 1 (fused_kernels.hip)
         return bao_fused_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_scratch, stream);
     return run_bao<0>(d_in, in_stride, n, count, d_out, out_stride, d_hash, nullptr, d_scratch, stream);
@@ -90,6 +92,7 @@ hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
 hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                           const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                           uint32_t *d_status, void *d_scratch, hipStream_t stream) {
+    if (small_ok(n, count)) return small_bao_decode_dev(d_in, n, d_hash, d_out, d_out ? n : 0, d_status, stream);
     return run_bao<1>(d_in, in_stride, n, count, d_out, out_stride, const_cast<uint8_t *>(d_hash),
                       d_status, d_scratch, stream);
 }
@@ -97,6 +100,8 @@ hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
 hipError_t bao_decode_prefix_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                                  const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
                                  uint32_t *d_status, void *d_scratch, hipStream_t stream) {
+    if (small_ok(n, count))
+        return small_bao_decode_dev(d_in, n, d_hash, d_out, d_out ? std::min(out_limit, n) : 0, d_status, stream);
     return run_bao_t<1, BAO_CPL, BAO_DEC_NTS, 0, 1, 0, BAO_XG, BAO_DQ>(d_in, in_stride, n, count, d_out, out_stride,
                                                           const_cast<uint8_t *>(d_hash), d_status, d_scratch, stream,
                                                           0, out_limit);

@@ -598,6 +598,7 @@ int pipe_wg_cfg() {
 hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
                         uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s) {
     const uint64_t zlen = (uint64_t)CHIP_FEC_M * C;
+    if (small_ok(zlen, count)) return small_zfec_bao_dev(d_in, n, C, d_out, d_hash, s);
     if (fused_on()) return zfec_bao_fused_dev(d_in, in_stride, n, count, C, d_out, out_stride, d_hash, d_scratch, s);
     const uint64_t *tab = nullptr;
     hipError_t e = bao_chunk_table(zlen / 1024, &tab);
@@ -1318,7 +1319,7 @@ int chip_blake3(const uint8_t *in, uint64_t n, uint8_t hash[CHIP_HASH_LEN]) {
 
 // verify-decode a device-resident stream of `len` bytes; content -> dst (device)
 static int bao_decode_ctx(Ctx *c, const uint8_t *d_enc, uint64_t len, uint64_t n, const uint8_t *hash,
-                          uint8_t *d_dst) {
+                          uint8_t *d_dst, uint64_t out_limit = ~0ull) {
     (void)len;
     CHIP_HIP(grow(c->scratch, bao_scratch_len(n, 1)));
     CHIP_HIP(grow(c->small, 64));
@@ -1327,7 +1328,11 @@ static int bao_decode_ctx(Ctx *c, const uint8_t *d_enc, uint64_t len, uint64_t n
     uint8_t hs[36] = {};  // the hash and a zero status word, one copy
     std::memcpy(hs, hash, 32);
     CHIP_HIP(small_h2d(c, d_hash, hs, sizeof hs));
-    CHIP_HIP(bao_decode_dev(d_enc, 0, n, 1, d_hash, d_dst, 0, d_status, c->scratch.p, c->stream));
+    if (out_limit < n)  // only content bytes [0, out_limit) written (every byte verified)
+        CHIP_HIP(bao_decode_prefix_dev(d_enc, 0, n, 1, d_hash, d_dst, 0, out_limit, d_status, c->scratch.p,
+                                       c->stream));
+    else
+        CHIP_HIP(bao_decode_dev(d_enc, 0, n, 1, d_hash, d_dst, 0, d_status, c->scratch.p, c->stream));
     uint32_t status = 0;
     CHIP_HIP(small_d2h(c, &status, d_status, 4));
     CHIP_HIP(small_sync(c));
@@ -2119,13 +2124,19 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         CHIP_HIP(grow(c->in, in_bytes));
         if (in_bytes) CHIP_HIP(h2d(c->stage, c->in.p, in, in_bytes, c->stream));
         const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
-        if (bao) {  // decoding.rs:89-93
+        if (bao && zfec) {  // decoding.rs:89-99: the positional shares' primaries are the content's
+            // first 4 C bytes, so zfec's decode is the prefix: verify all, write olen bytes
+            CHIP_HIP(grow(c->mid, olen));
+            st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p), olen);
+            if (st != CHIP_OK) return st;
+            d_cur = static_cast<const uint8_t *>(c->mid.p);
+        } else if (bao) {  // decoding.rs:89-93
             CHIP_HIP(grow(c->mid, blen));
             st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p));
             if (st != CHIP_OK) return st;
             d_cur = static_cast<const uint8_t *>(c->mid.p);
         }
-        if (zfec && C) {  // decoding.rs:95-99: shards by position, primaries present
+        if (zfec && !bao && C) {  // decoding.rs:95-99: shards by position, primaries present
             CHIP_HIP(grow(c->out, CHIP_FEC_K * C));
             std::vector<uint32_t> sel(CHIP_FEC_K);
             std::vector<uint64_t> slot_off(CHIP_FEC_K);

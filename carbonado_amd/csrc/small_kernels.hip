@@ -1,0 +1,331 @@
+// small_kernels.hip — KS: one workgroup encodes or verify-decodes one small
+// object (bao stream of N <= 512 chunks) in one launch (gfx950).
+//
+// The batch kernels (K13, K3 + K4/K4t) are built for throughput: one lane
+// hashes a whole 1 KiB chunk (16 dependent BLAKE3 compressions of ~700 VALU
+// instructions each, ~19 us for one wave), and a call runs two or more
+// launches.  A single small object through them costs 40-50 us of kernel
+// time for one chunk (profiles/r4c).  KS is built for latency instead:
+//
+//  * four lanes share one compression: lane q of a quad holds column q of the
+//    BLAKE3 state (a, b, c, d) and runs that column's G; the diagonal step
+//    rotates b, c, d across the quad with DPP quad permutes and back.  7 rounds
+//    of 2 G (12 ops each) and 6 DPP moves: ~220 VALU per compression per
+//    lane instead of ~700, so a chunk's 16 compressions take about a third of
+//    the time.  The message words a lane needs in round r are
+//    m[SCHED(r, 2q)], m[SCHED(r, 2q + 1)] (column) and m[SCHED(r, 8 + 2q)],
+//    m[SCHED(r, 9 + 2q)] (diagonal): read from the quad's 64-B LDS slot at
+//    per-lane offsets fixed at kernel start.
+//  * one launch does everything: (encode) the header, the zfec shards or the
+//    content into their chunk slots, the chunk CVs, every parent level (K4t's
+//    level walk, CVs in LDS, each parent also on four lanes) and the root
+//    hash; (decode) the content prefix out, every chunk and parent recomputed
+//    and compared with the stored node, the root with the expected hash.
+//
+// Used for single-object calls (count == 1) of bao encode / decode and
+// encode() at Zfec|Bao with N <= KS_MAX_N; CHIP_SMALL=0 turns it off (A/B
+// runs and tests compare the two paths byte for byte).
+#include "bao_device.hpp"
+#include "chip_internal.hpp"
+#include "zfec_device.hpp"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace chip {
+
+using namespace bao;
+
+namespace small {
+
+constexpr int TPB = 512;         // 8 waves = 128 quads
+constexpr int QUADS = TPB / 4;
+
+struct SmallArgs {
+    const uint8_t *in;      // encode: content (C == 0) or zfec input; decode: stream
+    uint8_t *out;           // encode: stream (may be null when C == 0: hash only); decode: content
+    uint64_t in_stride, out_stride;
+    uint64_t n;             // bao content bytes (encode with zfec: 8 C)
+    uint64_t N;             // chunks of the bao content
+    uint64_t valid;         // encode with zfec: input bytes (zero beyond)
+    uint64_t C;             // encode: zfec 4-of-8 shard length, 0 = bao of the content
+    uint64_t out_limit;     // decode: content bytes written
+    uint64_t count;
+    const uint32_t *table;  // zfec parity table [4][256]
+    uint8_t *hash;          // encode: root hashes out; decode: expected
+    uint32_t *status;       // decode: per object, 0 or CHIP_ERR_BAO_HASH_MISMATCH
+};
+
+// value of x held by lane (q + K) & 3 of my quad
+template <int K>
+__device__ __forceinline__ uint32_t qrot(uint32_t x) {
+    constexpr int ctrl = K == 1 ? 0x39 : K == 2 ? 0x4E : 0x93;  // quad_perm [1,2,3,0] / [2,3,0,1] / [3,0,1,2]
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, false);
+}
+
+// Per-lane LDS byte offsets of the message words of each round (within the
+// quad's slot): [r][0..1] column G, [r][2..3] diagonal G.
+struct MsgIdx {
+    uint32_t o[28];
+    __device__ explicit MsgIdx(int q, uint32_t slot) {
+#pragma unroll
+        for (int r = 0; r < 7; ++r) {
+            uint32_t c0 = 0, c1 = 0, d0 = 0, d1 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (q == k) {
+                    c0 = SCHED(r, 2 * k); c1 = SCHED(r, 2 * k + 1);
+                    d0 = SCHED(r, 8 + 2 * k); d1 = SCHED(r, 9 + 2 * k);
+                }
+            o[4 * r] = slot + 4 * c0; o[4 * r + 1] = slot + 4 * c1;
+            o[4 * r + 2] = slot + 4 * d0; o[4 * r + 3] = slot + 4 * d1;
+        }
+    }
+};
+
+__device__ __forceinline__ uint32_t lds_word(const uint8_t *lds, uint32_t off) {
+    return *reinterpret_cast<const uint32_t *>(lds + off);
+}
+
+// (h0, h1) = words q and 4 + q of the CV, updated to compress(h, m, ctr,
+// blen, flags) with the message in the quad's LDS slot.
+__device__ __forceinline__ void compress4(uint32_t &h0, uint32_t &h1, const uint8_t *lds, const MsgIdx &mi,
+                                          int q, uint32_t ivq, uint64_t ctr, uint32_t blen, uint32_t flags) {
+    uint32_t m[28];
+#pragma unroll
+    for (int i = 0; i < 28; ++i) m[i] = lds_word(lds, mi.o[i]);
+    uint32_t a = h0, b = h1, c = ivq;
+    uint32_t d = q == 0 ? (uint32_t)ctr : q == 1 ? (uint32_t)(ctr >> 32) : q == 2 ? blen : flags;
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+        B3G(a, b, c, d, m[4 * r], m[4 * r + 1]);
+        b = qrot<1>(b); c = qrot<2>(c); d = qrot<3>(d);
+        B3G(a, b, c, d, m[4 * r + 2], m[4 * r + 3]);
+        b = qrot<3>(b); c = qrot<2>(c); d = qrot<1>(d);
+    }
+    h0 = a ^ c;
+    h1 = b ^ d;
+}
+
+__device__ __forceinline__ u32x4 load16_bytes(const uint8_t *p, uint32_t valid) {  // valid < 16: byte loads
+    return valid == 0 ? u32x4{0u, 0u, 0u, 0u} : load16_partial(p, valid);
+}
+
+// MODE 0: encode, MODE 1: verify-decode.  One workgroup per object.
+template <int MODE>
+__global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[4 * 256];        // zfec parity products
+    __shared__ __attribute__((aligned(16))) uint32_t cvs[2][K4T_MAX][8];  // one tree level and the next
+    __shared__ __attribute__((aligned(16))) uint32_t msg[QUADS][16];  // each quad's message block
+    const uint64_t obj = blockIdx.x;
+    const int t = threadIdx.x, q = t & 3, g = t >> 2;
+    const uint64_t N = a.N, n = a.n;
+    const uint8_t *src = a.in + obj * a.in_stride;
+    uint8_t *dst = a.out ? a.out + obj * a.out_stride : nullptr;
+    const uint8_t *stream = MODE == 0 ? dst : src;
+    bool ok = true;
+
+    // ---- phase 1: header; zfec shards or content into their slots / content out
+    if (MODE == 0) {
+        if (dst && t == 0) *glb(reinterpret_cast<uint64_t *>(dst)) = n;
+        if (a.C) {
+            for (int i = t; i < 4 * 256; i += TPB) tab[i] = a.table[i];
+            __syncthreads();
+            const uint64_t cols = a.C / 1024;
+            for (uint64_t o = 16 * (uint64_t)t; o < a.C; o += 16 * TPB) {  // 16 B of every shard at shard byte o
+                u32x4 v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = zf::load16_masked(src, j * a.C + o, a.valid);
+                uint32_t acc[16];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) x ^= tab[j * 256 + ((zf::comp(v[j], d) >> (8 * b)) & 0xFFu)];
+                        acc[d * 4 + b] = x;
+                    }
+                }
+                u32x4 p[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    uint32_t r0, r1, r2, r3;
+                    zf::transpose4(acc[d * 4], acc[d * 4 + 1], acc[d * 4 + 2], acc[d * 4 + 3], r0, r1, r2, r3);
+                    if (d == 0) { p[0].x = r0; p[1].x = r1; p[2].x = r2; p[3].x = r3; }
+                    if (d == 1) { p[0].y = r0; p[1].y = r1; p[2].y = r2; p[3].y = r3; }
+                    if (d == 2) { p[0].z = r0; p[1].z = r1; p[2].z = r2; p[3].z = r3; }
+                    if (d == 3) { p[0].w = r0; p[1].w = r1; p[2].w = r2; p[3].w = r3; }
+                }
+                const uint64_t u = o / 1024, w = o % 1024;
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    store16_a8<false>(dst + chunk_stream_off(s * cols + u, N) + w, s < 4 ? v[s] : p[s - 4]);
+            }
+        } else if (dst) {
+            for (uint64_t o = 16 * (uint64_t)t; o < n; o += 16 * TPB) {
+                const u32x4 v = zf::load16_masked(src, o, n);
+                uint8_t *p = dst + chunk_stream_off(o / 1024, N) + o % 1024;
+                if (o + 16 <= n) store16_a8<false>(p, v);
+                else store16_partial(p, v, (uint32_t)(n - o));
+            }
+        }
+    } else {
+        if (t == 0 && *reinterpret_cast<const uint64_t *>(src) != n) ok = false;
+        for (uint64_t o = 16 * (uint64_t)t; o < a.out_limit; o += 16 * TPB) {
+            const uint8_t *p = src + chunk_stream_off(o / 1024, N) + o % 1024;
+            const uint64_t left = a.out_limit - o;
+            if (left >= 16) {
+                *glb(reinterpret_cast<u32x4 *>(dst + o)) = load16_a8(p);
+            } else {
+                store16_partial(dst + o, load16_bytes(p, (uint32_t)left), (uint32_t)left);
+            }
+        }
+    }
+    __syncthreads();  // (encode) the slots written above are read back below
+
+    // ---- phase 2: chunk CVs, one quad per chunk
+    const uint32_t slot = (uint32_t)(reinterpret_cast<uintptr_t>(&msg[g][0]) - reinterpret_cast<uintptr_t>(&msg[0][0]));
+    const uint8_t *mbase = reinterpret_cast<const uint8_t *>(&msg[0][0]);
+    const MsgIdx mi(q, slot);
+    const uint32_t iv0 = q == 0 ? IV(0) : q == 1 ? IV(1) : q == 2 ? IV(2) : IV(3);
+    const uint32_t iv1 = q == 0 ? IV(4) : q == 1 ? IV(5) : q == 2 ? IV(6) : IV(7);
+    const bool content_in = MODE == 0 && a.C == 0;  // encode of the content: read it where it is
+    for (uint64_t c = g; c < N; c += QUADS) {
+        const uint64_t rem = n - c * 1024;
+        const uint32_t clen = n == 0 ? 0u : (rem < 1024 ? (uint32_t)rem : 1024u);
+        const uint32_t nb = clen == 0 ? 1u : (clen + 63) / 64;
+        const uint8_t *cp = content_in ? src + c * 1024 : stream + chunk_stream_off(c, N);
+        u32x4 pc[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {  // my 16 B of every block of the chunk, all loads in flight
+            const uint32_t off = 64 * b + 16 * q;
+            if (off >= clen) pc[b] = u32x4{0u, 0u, 0u, 0u};
+            else if (content_in) pc[b] = zf::load16_masked(src, c * 1024 + off, n);
+            else pc[b] = off + 16 <= clen ? load16_a8(cp + off) : load16_bytes(cp + off, clen - off);
+        }
+        uint32_t h0 = iv0, h1 = iv1;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            if ((uint32_t)b < nb) {
+                *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = pc[b];
+                wave_sync();
+                const bool last = (uint32_t)b + 1 == nb;
+                const uint32_t flags = (b == 0 ? F_CHUNK_START : 0u) | (last ? F_CHUNK_END : 0u) |
+                                       (last && N == 1 ? F_ROOT : 0u);
+                compress4(h0, h1, mbase, mi, q, iv0, c, last ? clen - 64 * b : 64u, flags);
+                wave_sync();
+            }
+        }
+        if (N == 1) {  // the chunk is the root
+            uint32_t *hp = reinterpret_cast<uint32_t *>(a.hash + obj * 32);
+            if (MODE == 0) {
+                hp[q] = h0;
+                hp[4 + q] = h1;
+            } else {
+                ok &= hp[q] == h0 && hp[4 + q] == h1;
+            }
+        } else {
+            cvs[0][c][q] = h0;
+            cvs[0][c][4 + q] = h1;
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 3: the parent levels (bao_top_kernel's walk), one quad per parent
+    int cur = 0;
+    uint64_t cnt_prev = N;
+    for (int level = 1; cnt_prev > 1; ++level) {
+        const uint64_t cnt = (cnt_prev + 1) / 2;
+        for (uint64_t p = g; p < cnt; p += QUADS) {
+            if (2 * p + 1 >= cnt_prev) {  // odd last node: promoted unchanged
+                cvs[cur ^ 1][p][q] = cvs[cur][2 * p][q];
+                cvs[cur ^ 1][p][4 + q] = cvs[cur][2 * p][4 + q];
+                continue;
+            }
+            // message = left CV || right CV: my 16 B are words 4q..4q+3
+            const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cvs[cur][2 * p + (q >> 1)][4 * (q & 1)]);
+            *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = mw;
+            wave_sync();
+            const bool root = cnt == 1;
+            uint32_t h0 = iv0, h1 = iv1;
+            compress4(h0, h1, mbase, mi, q, iv0, 0, 64, F_PARENT | (root ? F_ROOT : 0u));
+            wave_sync();
+            uint8_t *node = const_cast<uint8_t *>(stream) + parent_stream_off(p << level, level, N) + 16 * q;
+            if (MODE == 0) {
+                if (dst) store16_a8<false>(node, mw);
+            } else {
+                const u32x4 s = load16_a8(node);
+                ok &= s.x == mw.x && s.y == mw.y && s.z == mw.z && s.w == mw.w;
+            }
+            if (root) {
+                uint32_t *hp = reinterpret_cast<uint32_t *>(a.hash + obj * 32);
+                if (MODE == 0) {
+                    hp[q] = h0;
+                    hp[4 + q] = h1;
+                } else {
+                    ok &= hp[q] == h0 && hp[4 + q] == h1;
+                }
+            } else {
+                cvs[cur ^ 1][p][q] = h0;
+                cvs[cur ^ 1][p][4 + q] = h1;
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        cnt_prev = cnt;
+    }
+    if (MODE == 1 && !ok) flag_mismatch(a.status, obj);
+}
+
+bool enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("CHIP_SMALL");
+        return !(e && !std::strcmp(e, "0"));
+    }();
+    return on;
+}
+
+hipError_t launch(int mode, const SmallArgs &a, hipStream_t stream) {
+    if (mode == 0) hipLaunchKernelGGL(small_kernel<0>, dim3((unsigned)a.count), dim3(TPB), 0, stream, a);
+    else hipLaunchKernelGGL(small_kernel<1>, dim3((unsigned)a.count), dim3(TPB), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace small
+
+bool small_ok(uint64_t bao_n, uint64_t count) {
+    return small::enabled() && count == 1 && n_chunks(bao_n) <= (uint64_t)KS_MAX_N;
+}
+
+hipError_t small_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_out, uint8_t *d_hash,
+                                hipStream_t stream) {
+    small::SmallArgs a{};
+    a.in = d_in; a.out = d_out; a.n = n; a.N = n_chunks(n); a.valid = n; a.count = 1;
+    a.hash = d_hash;
+    return small::launch(0, a, stream);
+}
+
+hipError_t small_zfec_bao_dev(const uint8_t *d_in, uint64_t n, uint64_t C, uint8_t *d_out, uint8_t *d_hash,
+                              hipStream_t stream) {
+    if (C == 0 || C % 1024) return hipErrorInvalidValue;
+    const void *tab = nullptr;
+    hipError_t e = zfec_parity_table(4, 8, &tab);
+    if (e != hipSuccess) return e;
+    small::SmallArgs a{};
+    a.in = d_in; a.out = d_out; a.n = 8 * C; a.N = n_chunks(8 * C); a.valid = n; a.C = C; a.count = 1;
+    a.table = static_cast<const uint32_t *>(tab);
+    a.hash = d_hash;
+    return small::launch(0, a, stream);
+}
+
+hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t n, const uint8_t *d_hash, uint8_t *d_out,
+                                uint64_t out_limit, uint32_t *d_status, hipStream_t stream) {
+    small::SmallArgs a{};
+    a.in = d_stream; a.out = d_out; a.n = n; a.N = n_chunks(n); a.out_limit = out_limit; a.count = 1;
+    a.hash = const_cast<uint8_t *>(d_hash);
+    a.status = d_status;
+    return small::launch(1, a, stream);
+}
+
+}  // namespace chip

@@ -1,0 +1,104 @@
+"""GPU parity of KS, the single-launch path for single small objects
+(carbonado_amd/csrc/small_kernels.hip: bao streams of N <= 512 chunks, four
+lanes per BLAKE3 compression).  Every size class around its limits — empty
+input, partial chunks and blocks, N = 1 (the chunk is the root), N = 2,
+odd and power-of-two chunk counts, the N = 512 / 513 border with the batch
+kernels — bit-exact against the C oracle; decode rejects a flipped byte in
+the header, a chunk, a parent node and the hash (the same cases
+test_gpu_bao.py holds for the batch kernels)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+BAO_SIZES = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 3 * 1024 + 7, 8192, 65536 - 5, 100_000,
+             511 * 1024 + 1, 512 * 1024, 512 * 1024 + 1]
+# encode() level 12: N = 8 C / 1024, C = ceil(n / 4096) * 1024: N = 8 .. 512 and 520
+ZFEC_SIZES = [0, 1, 4095, 4096, 4097, 10_000, 65536, 64 * 4096 - 3, 64 * 4096, 64 * 4096 + 1]
+
+
+def _data(n, seed=0):
+    return np.random.default_rng(n * 7 + seed).integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+@pytest.mark.parametrize("n", BAO_SIZES)
+def test_small_bao_encode_decode(gpu, n):
+    import carbonado_amd as ca
+    d = _data(n)
+    enc, h = ca.encoding.bao(d)
+    oenc, oh = O.bao_encode(d)
+    assert h == oh and enc == oenc
+    assert ca.encoding.blake3(d) == oh  # hash-only call (no stream buffer)
+    assert ca.decoding.bao(enc, h) == d
+
+
+@pytest.mark.parametrize("n", ZFEC_SIZES)
+@pytest.mark.parametrize("level", [4, 12])
+def test_small_encode_levels(gpu, n, level):
+    import carbonado_amd as ca
+    d = _data(n, level)
+    enc, h, info = ca.encode(b"", d, level)
+    oenc, oh, _ = O.encode(d, level)
+    assert h == oh and enc == oenc
+    assert ca.decode(b"", h, enc, info.padding_len, level) == d
+
+
+@pytest.mark.parametrize("n", [1, 1024, 3000, 70_000])
+def test_small_decode_rejects_tampering(gpu, n):
+    import carbonado_amd as ca
+    from carbonado_amd.error import BaoDecodeError
+    d = _data(n, 3)
+    enc, h = ca.encoding.bao(d)
+    N = max(1, (n + 1023) // 1024)
+    spots = [8, len(enc) - 1]  # first content (or parent) byte, last byte
+    if N > 1:
+        spots.append(8 + 64 + 5)  # inside the first chunk (after the root's node)
+    for pos in spots:
+        bad = bytearray(enc)
+        bad[pos] ^= 0x10
+        with pytest.raises(BaoDecodeError):
+            ca.decoding.bao(bytes(bad), h)
+    bad_h = bytearray(h)
+    bad_h[31] ^= 1
+    with pytest.raises(BaoDecodeError):
+        ca.decoding.bao(enc, bytes(bad_h))
+
+
+def test_small_level12_decode_rejects_parent_flip(gpu):
+    """A parent node of the Zfec|Bao stream (not only content) is checked."""
+    import carbonado_amd as ca
+    from carbonado_amd.error import BaoDecodeError
+    d = _data(20_000, 5)
+    enc, h, info = ca.encode(b"", d, 12)
+    bad = bytearray(enc)
+    bad[8 + 3] ^= 0x80  # the root's node (left CV)
+    with pytest.raises(BaoDecodeError):
+        ca.decode(b"", h, bytes(bad), info.padding_len, 12)
+    assert ca.decode(b"", h, enc, info.padding_len, 12) == d
+
+
+def test_small_matches_batch_kernels(gpu):
+    """The same objects through KS (one object per call) and the batch
+    kernels (a device batch of several objects): identical streams and hashes."""
+    import torch
+    import carbonado_amd as ca
+    from carbonado_amd import device as D
+    n, count = 37_000, 3
+    objs = [_data(n, s) for s in range(count)]
+    stride = (n + 15) // 16 * 16
+    inp = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    for i, o in enumerate(objs):
+        inp[i, :n] = torch.frombuffer(bytearray(o), dtype=torch.uint8).cuda()
+    for level in (4, 12):
+        single = [ca.encode(b"", o, level) for o in objs]
+        olen = len(single[0][0])
+        ostride = (olen + 15) // 16 * 16
+        out = torch.zeros((count, ostride), dtype=torch.uint8, device="cuda")
+        hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+        D.encode_batch(level, inp, n, out, hashes, D.encode_scratch(level, n, count))
+        torch.cuda.synchronize()
+        for i in range(count):
+            assert bytes(out[i, :olen].cpu().numpy()) == single[i][0]
+            assert bytes(hashes[i].cpu().numpy()) == single[i][1]
