@@ -66,12 +66,14 @@ def parse(argv=None):
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=8)
     ap.add_argument("--mode", choices=["encode", "decode", "bao", "bao-decode", "pipeline", "pipeline-decode", "e2e", "e2e-decode", "scrub",
-                                       "hasher", "file"],
+                                       "scrub-batch", "hasher", "file"],
                     default="encode",
                     help="bao-decode: device-resident decoding::bao (verify every node, return the content); "
                          "pipeline: device-resident encode() at --level (Bao/Zfec bits; 12 = zfec fused into "
                          "bao); e2e: encode() at --level from pinned HOST memory to host memory (H2D+kernels+D2H); "
                          "scrub: scrub() of level-12 streams with one corrupted shard (host API, decoding.rs:151-212); "
+                         "scrub-batch: scrub() of device-resident level-12 streams, every --scrub-every-th one damaged "
+                         "(chip_scrub_batch_dev); "
                          "hasher: BaoHasher update()+finalize() over the objects in 4 MiB appends (utils.rs:104-137); "
                          "file: file::encode of flat files on disk to .c<level> files (file.rs:409-440)")
     ap.add_argument("--file-dir", default=None, help="file mode: working directory (default $TMPDIR/carbonado_files)")
@@ -90,6 +92,8 @@ def parse(argv=None):
     ap.add_argument("--host-threads", type=int, default=16,
                     help="e2e mode: host threads for the Snappy/Ecies stages (the GPU box's CPU share is 16)")
     ap.add_argument("--erase", default="1,2", help="decode mode: shards dropped")
+    ap.add_argument("--scrub-every", type=int, default=64,
+                    help="scrub-batch mode: one object in this many has a corrupted byte in a data shard")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of each CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="second CPU baseline with objects in parallel on this many host threads (SURVEY 8d: "
@@ -301,6 +305,8 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
         bstream, bhash = O.bao_encode(obj)
     if args.mode == "pipeline-decode":
         enc_obj, h_obj, inf_obj = O.encode(obj, args.level)
+    if args.mode == "scrub-batch":
+        enc_obj, h_obj, inf_obj = O.encode(obj, 12)
     if args.mode == "scrub":
         enc_obj, h_obj, inf_obj = O.encode(obj, 12)
         bad = bytearray(enc_obj)
@@ -328,6 +334,8 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
             O.encode(O.zfec_decode_shares([zc[i * zC:(i + 1) * zC] for i in keep_s], keep_s, zpad), 12)
         elif args.mode == "pipeline-decode":
             O.decode(h_obj, enc_obj, inf_obj["padding_len"], args.level)
+        elif args.mode == "scrub-batch":  # an intact stream: scrub()'s bao_decode succeeds
+            O.bao_decode(enc_obj, h_obj)
         elif args.mode == "e2e-decode":
             cur = O.decode(h_obj, enc_obj, inf_obj["padding_len"], args.level & 12) if args.level & 12 else enc_obj
             if args.level & 1:
@@ -363,6 +371,7 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
             "file": f"encode() level {args.level} (in memory, no file I/O, no header)",
             "hasher": "BLAKE3 of the content", "scrub": "scrub() restated: bao decode + zfec decode + encode()", "e2e-decode": f"decode() level {args.level}",
             "pipeline-decode": f"decode() level {args.level}",
+            "scrub-batch": "scrub() of an intact level-12 stream: bao decode of the stream",
             "decode": f"zfec {args.k}-of-{args.m} decode, erased {args.erase}"}.get(
         args.mode, f"zfec {args.k}-of-{args.m} encode")
     return {"value": round(done * n / el / 2**30, 4), "unit": "GiB/s", "cores": max(1, threads), "kind": "port",
@@ -424,7 +433,8 @@ class Workload:
                          if args.prealloc_gib else None)
         if args.alloc == "contiguous":
             os.environ["CHIP_ALLOC"] = "contiguous"  # read by chip_device_alloc at each call
-        device_mode = args.mode in ("encode", "decode", "bao", "bao-decode", "pipeline", "pipeline-decode")
+        device_mode = args.mode in ("encode", "decode", "bao", "bao-decode", "pipeline", "pipeline-decode",
+                                    "scrub-batch")
         self.alloc_info = {}
 
         def batch_buf(shape, name=None):
@@ -553,6 +563,43 @@ class Workload:
             self.kernel = ("scrub(): H2D + bao node check + zfec decode of intact shards + fused re-encode + D2H, "
                            "one call per object (host API)")
             self.kernel_sym = "scrub"
+        elif args.mode == "scrub-batch":
+            zlen = m * C
+            self.zlen = zlen
+            self.blen = blen = L.chip_bao_encoded_len(zlen)
+            row = (blen + 15) // 16 * 16
+            self.enc = batch_buf((count, row), "enc")
+            self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
+            esc = device.encode_scratch(12, n, count, dev)
+            _, info = device.encode_batch(12, self.inp, n, self.enc, self.hashes, esc)
+            torch.cuda.synchronize()
+            del esc
+            self.pad = info.padding_len
+            self.sample0 = self.inp[0].cpu().numpy().tobytes()
+            self.inp = self.inp[:1]  # only object 0's input is kept (the oracle check)
+            torch.cuda.empty_cache()
+            every = max(1, args.scrub_every)
+            self.damaged = list(range(every // 2 % count, count, every))
+            self.orig = {o: self.enc[o, :blen].clone() for o in self.damaged}
+            for o in self.damaged:  # one byte of a data shard's chunk
+                off = scrub_corrupt_offset(n, o)
+                self.enc[o, off] ^= 0x40
+            self.out = batch_buf((count, row), "out")
+            self.scratch = device.scrub_scratch(blen, count, dev)
+            self.scrub_status = None
+
+            def step():
+                self.scrub_status = device.scrub_batch(self.enc, blen, self.hashes, self.pad, C, self.out,
+                                                       self.scratch)
+            self.step = step
+            # VALU: every chunk and parent of every stream re-hashed (node check), plus the
+            # damaged streams' re-encode (zfec + bao); HBM bytes: the streams read once
+            self.scrub_comps = (count + len(self.damaged)) * (zlen // 64 + zlen // 1024 - 1)
+            self.alg_bytes = count * blen + len(self.damaged) * (2 * blen + zlen)
+            self.kernel = (f"scrub() of {count} device-resident level-12 streams, {len(self.damaged)} damaged: "
+                           "bao_chunk_kernel MODE 2 + bao_parent_check_kernel (every node), scrub_mask_kernel, "
+                           "then per damaged stream gather + zfec decode + fused re-encode")
+            self.kernel_sym = "scrub-batch"
         elif args.mode == "hasher":
             import numpy as np
             from carbonado_amd.utils import BaoHasher
@@ -853,6 +900,15 @@ class Workload:
                   self.enc[0, :blen].cpu().numpy().tobytes() == O.bao_encode(sample)[0])
         elif self.args.mode == "scrub":
             ok = all(self.fixed[o] == self.encs[o] for o in range(self.count))
+        elif self.args.mode == "scrub-batch":
+            # intact streams: UnnecessaryScrub (12); damaged: repaired (0) to the original stream;
+            # object 0's stream is the oracle's encode()
+            sample = self.sample0
+            st = self.scrub_status
+            want = [0 if o in self.orig else 12 for o in range(self.count)]
+            ok = (st is not None and list(st) == want and
+                  all(torch.equal(self.out[o, :self.blen], self.orig[o]) for o in self.orig) and
+                  self.enc[0, :self.blen].cpu().numpy().tobytes() == O.encode(sample, 12)[0])
         elif self.args.mode == "hasher":
             ok = self.digest == O.blake3(self.inp.numpy().reshape(-1))
         elif self.args.mode == "pipeline":
@@ -971,6 +1027,9 @@ def main():
         elif args.mode == "scrub":
             workload = (f"scrub() of {args.objects} level-12 streams of {args.object_mib:g} MiB objects, one "
                         f"corrupted byte each, host buffers")
+        elif args.mode == "scrub-batch":
+            workload = (f"scrub() of {args.objects} device-resident level-12 streams of {args.object_mib:g} MiB "
+                        f"objects per GPU, 1 in {args.scrub_every} damaged")
         elif args.mode == "hasher":
             workload = f"BaoHasher over {args.objects} x {args.object_mib:g} MiB in 4 MiB appends, host buffers"
         elif args.mode == "e2e":
@@ -1022,13 +1081,14 @@ def main():
                            else "synthetic (uniform random bytes) in files on the box's local disk, read and "
                                 "written through the page cache" if args.mode == "file"
                            else "synthetic (uniform random bytes), pageable host buffers (numpy / bytes)")
-        pipe = args.mode in ("pipeline", "pipeline-decode")
-        if args.mode in ("bao", "bao-decode") or (pipe and args.level & 4):
+        pipe = args.mode in ("pipeline", "pipeline-decode", "scrub-batch")
+        if args.mode in ("bao", "bao-decode", "scrub-batch") or (pipe and args.level & 4):
             # BLAKE3 compressions: one per 64-B block of content plus one per parent node;
             # 7 rounds x 8 G x 12 VALU lane-ops (a+b+m as one v_add3_u32).
             hashed = getattr(wl, "zlen", n) if pipe else n
             chunks = max(1, -(-hashed // 1024))
-            comps = args.objects * (max(1, -(-hashed // 64)) + (chunks - 1))
+            comps = (wl.scrub_comps if args.mode == "scrub-batch" else
+                     args.objects * (max(1, -(-hashed // 64)) + (chunks - 1)))
             ops = comps * 7 * 8 * 12
             tops = ops / (avg_ms * 1e-3) / 1e12
             hbm = res["roofline"]

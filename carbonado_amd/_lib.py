@@ -154,6 +154,10 @@ SIGNATURES = {
                                              c_u64p]),
     "chip_scrub": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
+    "chip_scrub_scratch_len": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+    "chip_scrub_batch_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "chip_bao_hasher_new": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "chip_bao_hasher_update": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "chip_bao_hasher_finalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

@@ -1009,7 +1009,7 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
         dq = per_cu > 0 && stream_queue(stream, &q) == hipSuccess;
         (void)hipGetLastError();
         if (dq) {
-            ca.queue = q + 640;
+            ca.queue = q + QUEUE_K3;
             const uint64_t grid = std::min<uint64_t>(blocks, (uint64_t)per_cu * (uint64_t)num_cus());
             hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG, true>), dim3((unsigned)grid),
                                dim3(K3_TPB), pad_lds, stream, ca);

@@ -160,6 +160,58 @@ hipError_t bao_chunk_table(uint64_t N, const uint64_t **out) {
     return hipSuccess;
 }
 
+namespace {
+
+// Which of the 8 zfec shards of a Bao|Zfec stream scrub() may use
+// (decoding.rs:172-183: verify_slice of each shard's chunk range), from the
+// per-node flags of bao_node_check: shard i is authentic iff every chunk in
+// its range and every parent whose subtree meets the range verified (the
+// nodes bao's slice decoder walks; a parent node is checked against the CV
+// stored in its own parent, the root against the hash).  One workgroup per
+// object; mask bit i = shard i authentic, 0 for a stream whose header does not
+// hold n.
+__global__ __launch_bounds__(256) void scrub_mask_kernel(const uint8_t *stream, uint64_t stride, uint64_t n,
+                                                         uint64_t N, uint64_t spc, const uint8_t *cflags,
+                                                         const uint8_t *pflags, uint8_t *masks) {
+    __shared__ uint32_t bad;
+    const uint64_t obj = blockIdx.x;
+    if (threadIdx.x == 0) bad = *reinterpret_cast<const uint64_t *>(stream + obj * stride) != n ? 0xFFu : 0u;
+    __syncthreads();
+    uint32_t mine = 0;
+    const uint8_t *cf = cflags + obj * N, *pf = pflags + obj * (N - 1);
+    for (uint64_t c = threadIdx.x; c < N; c += 256)
+        if (!cf[c]) mine |= 1u << (c / spc);
+    for (uint64_t r0 = threadIdx.x; r0 + 1 < N; r0 += 256) {  // the r0-th real parent in level order
+        uint64_t r = r0, cnt = N;
+        int level = 1;
+        for (;; ++level) {
+            const uint64_t np = cnt / 2;
+            if (r < np) break;
+            r -= np;
+            cnt = (cnt + 1) / 2;
+        }
+        const uint64_t sx = r << level;
+        if (pf[parents_before(sx, N) + parents_at(sx, N) - level]) continue;
+        const uint64_t end = sx + (1ull << level) < N ? sx + (1ull << level) : N;
+        for (uint64_t sh = sx / spc; sh <= (end - 1) / spc; ++sh) mine |= 1u << sh;
+    }
+    if (mine) atomicOr(&bad, mine);
+    __syncthreads();
+    if (threadIdx.x == 0) masks[obj] = (uint8_t)(~bad & 0xFFu);
+}
+
+}  // namespace
+
+hipError_t scrub_masks(const uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count, uint64_t spc,
+                       const uint8_t *chunk_flags, const uint8_t *parent_flags, uint8_t *masks, hipStream_t stream) {
+    const uint64_t N = n_chunks(n);
+    if (count == 0) return hipSuccess;
+    if (N < 2 || spc == 0 || N != 8 * spc) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(scrub_mask_kernel, dim3((unsigned)count), dim3(256), 0, stream, d_stream, stride, n, N, spc,
+                       chunk_flags, parent_flags, masks);
+    return hipGetLastError();
+}
+
 uint64_t bao_chunk_offset(uint64_t i, uint64_t N) { return chunk_stream_off(i, N); }
 uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N) { return parent_stream_off(s, level, N); }
 uint64_t bao_parent_index(uint64_t s, int level, uint64_t N) {

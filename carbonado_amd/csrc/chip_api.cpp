@@ -1471,6 +1471,53 @@ int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const uint8_t 
     return CHIP_OK;
 }
 
+}  // extern "C"
+
+// scrub()'s repair (decoding.rs:172-209) of one device-resident Bao|Zfec
+// stream (content n = 8 C bytes) whose authentic shards are `good`, enqueued
+// on the context's stream: zfec decode from them by TRUE index
+// (decoding.rs:187), then encode() at Zfec|Bao of the result (the fused
+// kernel: shards hashed on chip) into d_dst, its hash to d_h2 (device).  The
+// host-side verdicts (too few shares, padding and length mismatch) come back
+// at once; the caller compares d_h2 with the expected hash after a sync.  The
+// length check is made before the stream is written (the reference makes it
+// after encoding; the verdict is the same), so d_dst never receives more
+// than `len` bytes.
+static int scrub_repair_enqueue(Ctx *c, const uint8_t *d_stream, uint64_t n, uint64_t len,
+                                const std::vector<uint32_t> &good, uint32_t padding, uint64_t C, uint8_t *d_dst,
+                                uint8_t *d_h2) {
+    if (good.size() < CHIP_FEC_K) return CHIP_ERR_ZFEC;
+    const uint64_t kc = (uint64_t)CHIP_FEC_K * C;
+    if (padding > kc) return CHIP_ERR_ZFEC;
+    const uint64_t dl = kc - padding;
+    uint32_t pad2;
+    uint64_t C2;
+    calc_pad(dl, CHIP_FEC_K, &pad2, &C2);
+    if (pad2 != padding) return CHIP_ERR_SCRUBBED_PADDING_MISMATCH;  // decoding.rs:192-194
+    const uint64_t z2 = (uint64_t)CHIP_FEC_M * C2;
+    if (bao_encoded_len(z2) != len) return CHIP_ERR_SCRUBBED_LENGTH_MISMATCH;  // decoding.rs:198-203
+    std::vector<uint32_t> pos;
+    int st = select_shares(CHIP_FEC_K, CHIP_FEC_M, good.data(), (uint32_t)good.size(), &pos);
+    if (st != CHIP_OK) return st;
+    // content of all shards, parents stripped
+    CHIP_HIP(grow(c->mid, n));
+    uint8_t *d_z = static_cast<uint8_t *>(c->mid.p);
+    CHIP_HIP(bao_gather_content(d_stream, n, 0, n_chunks_of(n), d_z, c->stream));
+    std::vector<uint32_t> sel(CHIP_FEC_K);
+    std::vector<uint64_t> slot_off(CHIP_FEC_K);
+    for (uint32_t s2 = 0; s2 < CHIP_FEC_K; ++s2) { sel[s2] = good[pos[s2]]; slot_off[s2] = sel[s2] * C; }
+    CHIP_HIP(grow(c->x1, kc));
+    uint8_t *d_dec = static_cast<uint8_t *>(c->x1.p);
+    st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_z, 0, slot_off, sel, C, 1, d_dec, 0, c->stream);
+    if (st != CHIP_OK) return st;
+    // re-encode: encoding::zfec then encoding::bao (decoding.rs:191-196), one fused pass
+    CHIP_HIP(grow(c->scratch, std::max(zfec_bao_scratch_len(z2, 1), bao_scratch_len(z2, 1))));
+    CHIP_HIP(zfec_bao_dev(d_dec, 0, dl, 1, C2, d_dst, 0, d_h2, c->scratch.p, c->stream));
+    return CHIP_OK;
+}
+
+extern "C" {
+
 int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t hash_len, uint32_t padding,
                uint32_t chunk_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
     if (!out_len || (!enc && len)) return CHIP_ERR_INVALID_ARG;
@@ -1497,48 +1544,83 @@ int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t h
     std::vector<uint32_t> good;
     for (uint32_t i = 0; i < CHIP_FEC_M; ++i)  // decoding.rs:173-183
         if (slice_ok(n, i * spc, (i + 1) * spc, cf, pf)) good.push_back(i);
-    if (good.size() < CHIP_FEC_K) return CHIP_ERR_ZFEC;
-    const uint64_t kc = (uint64_t)CHIP_FEC_K * C;
-    if (padding > kc) return CHIP_ERR_ZFEC;
-    // content of all shards, parents stripped
-    CHIP_HIP(grow(c->mid, n));
-    uint8_t *d_z = static_cast<uint8_t *>(c->mid.p);
-    CHIP_HIP(bao_gather_content(static_cast<const uint8_t *>(c->in.p), n, 0, n_chunks_of(n), d_z, c->stream));
-    // zfec decode from the good shards, TRUE indices (decoding.rs:187)
-    std::vector<uint32_t> pos;
-    st = select_shares(CHIP_FEC_K, CHIP_FEC_M, good.data(), (uint32_t)good.size(), &pos);
+    CHIP_HIP(grow(c->out, len));
+    CHIP_HIP(grow(c->small, 64));
+    uint8_t *d_h2 = static_cast<uint8_t *>(c->small.p);
+    st = scrub_repair_enqueue(c, static_cast<const uint8_t *>(c->in.p), n, len, good, padding, C,
+                              static_cast<uint8_t *>(c->out.p), d_h2);
     if (st != CHIP_OK) return st;
-    std::vector<uint32_t> sel(CHIP_FEC_K);
-    std::vector<uint64_t> slot_off(CHIP_FEC_K);
-    for (uint32_t s2 = 0; s2 < CHIP_FEC_K; ++s2) { sel[s2] = good[pos[s2]]; slot_off[s2] = sel[s2] * C; }
-    CHIP_HIP(grow(c->x1, kc));
-    uint8_t *d_dec = static_cast<uint8_t *>(c->x1.p);
-    st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_z, 0, slot_off, sel, C, 1, d_dec, 0, c->stream);
-    if (st != CHIP_OK) return st;
-    const uint64_t dl = kc - padding;
-    // re-encode: encoding::zfec then encoding::bao (decoding.rs:191-196)
-    uint32_t pad2;
-    uint64_t C2;
-    calc_pad(dl, CHIP_FEC_K, &pad2, &C2);
-    if (pad2 != padding) return CHIP_ERR_SCRUBBED_PADDING_MISMATCH;  // decoding.rs:192-194
-    CHIP_HIP(grow(c->x2, CHIP_FEC_M * C2));
-    uint8_t *d_z2 = static_cast<uint8_t *>(c->x2.p);
-    {
-        GfPlan p = encode_plan(CHIP_FEC_K, CHIP_FEC_M, C2, zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M));
-        GfLaunch L{d_dec, d_z2, 0, 0, dl, C2, 1};
-        CHIP_HIP(gf_apply(p, L, c->stream));
-    }
     uint8_t h2[32];
-    st = bao_encode_ctx(c, d_z2, CHIP_FEC_M * C2, true, h2);
-    if (st != CHIP_OK) return st;
+    CHIP_HIP(small_d2h(c, h2, d_h2, 32));
     CHIP_HIP(small_sync(c));
-    const uint64_t blen2 = bao_encoded_len(CHIP_FEC_M * C2);
-    if (blen2 != len) return CHIP_ERR_SCRUBBED_LENGTH_MISMATCH;  // decoding.rs:198-203
     if (std::memcmp(h2, hash, 32) != 0) return CHIP_ERR_INVALID_SCRUBBED_HASH;  // decoding.rs:205-207
-    if (!out || out_cap < blen2) return CHIP_ERR_BUFFER_TOO_SMALL;
-    CHIP_HIP(d2h(c->stage, out, c->out.p, blen2, c->stream));
+    if (!out || out_cap < len) return CHIP_ERR_BUFFER_TOO_SMALL;
+    CHIP_HIP(d2h(c->stage, out, c->out.p, len, c->stream));
     CHIP_HIP(small_sync(c));
-    *out_len = blen2;
+    *out_len = len;
+    return CHIP_OK;
+}
+
+uint64_t chip_scrub_scratch_len(uint64_t len, uint64_t count) {
+    uint64_t n = 0;
+    if (!bao_content_len(len, &n)) return 16;
+    const uint64_t N = n_chunks_of(n);
+    return ((count * (2 * N - 1) + count + 15) & ~uint64_t(15)) + 16;
+}
+
+int chip_scrub_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t len, uint64_t count,
+                         const uint8_t *d_hash, uint32_t padding, uint32_t chunk_len, uint8_t *d_out,
+                         uint64_t out_stride, int32_t *status, void *d_scratch, void *stream) {
+    if (count == 0) return CHIP_OK;
+    if (!d_in || !d_hash || !d_out || !status || !d_scratch) return CHIP_ERR_INVALID_ARG;
+    uint64_t n = 0;
+    if (!bao_content_len(len, &n) || in_stride < len || out_stride < len) return CHIP_ERR_INVALID_ARG;
+    if (misaligned16(d_in) || misaligned16(d_out) || in_stride % 16 || out_stride % 16) return CHIP_ERR_INVALID_ARG;
+    const uint64_t C = chunk_len;
+    if (C == 0 || C % 1024 || n != (uint64_t)CHIP_FEC_M * C) return CHIP_ERR_ZFEC;
+    int st = use_device();
+    if (st != CHIP_OK) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t N = n_chunks_of(n);
+    uint8_t *cf = static_cast<uint8_t *>(d_scratch), *pf = cf + count * N, *masks = pf + count * (N - 1);
+    // every node of every stream, then each stream's authentic shards (decoding.rs:168-183)
+    CHIP_HIP(bao_node_check(d_in, in_stride, n, count, d_hash, cf, pf, s));
+    CHIP_HIP(scrub_masks(d_in, in_stride, n, count, C / 1024, cf, pf, masks, s));
+    std::vector<uint8_t> m(count), want(32 * count);
+    CHIP_HIP(hipMemcpyAsync(m.data(), masks, count, hipMemcpyDeviceToHost, s));
+    CHIP_HIP(hipMemcpyAsync(want.data(), d_hash, 32 * count, hipMemcpyDeviceToHost, s));
+    CHIP_HIP(hipStreamSynchronize(s));
+    std::vector<uint64_t> repair;
+    for (uint64_t o = 0; o < count; ++o) {
+        const int good = __builtin_popcount(m[o]);
+        if (good == CHIP_FEC_M) status[o] = CHIP_ERR_UNNECESSARY_SCRUB;  // decoding.rs:169-170
+        else if (good < CHIP_FEC_K) status[o] = CHIP_ERR_ZFEC;          // zfec_chunks: too few shares
+        else repair.push_back(o);
+    }
+    if (repair.empty()) return CHIP_OK;
+    // the damaged streams, one after another on the thread's stream (the
+    // buffers are reused in stream order); one synchronisation for all
+    Ctx *c;
+    st = ctx_get(&c);
+    if (st != CHIP_OK) return st;
+    CHIP_HIP(grow(c->flags, 32 * repair.size()));
+    uint8_t *d_h2 = static_cast<uint8_t *>(c->flags.p);
+    std::vector<uint64_t> queued;
+    for (uint64_t o : repair) {
+        std::vector<uint32_t> good;
+        for (uint32_t i = 0; i < CHIP_FEC_M; ++i)
+            if (m[o] >> i & 1) good.push_back(i);
+        status[o] = scrub_repair_enqueue(c, d_in + o * in_stride, n, len, good, padding, C, d_out + o * out_stride,
+                                         d_h2 + 32 * queued.size());
+        if (status[o] == CHIP_ERR_DEVICE) return CHIP_ERR_DEVICE;
+        if (status[o] == CHIP_OK) queued.push_back(o);
+    }
+    std::vector<uint8_t> h2(32 * queued.size());
+    if (!queued.empty()) CHIP_HIP(small_d2h(c, h2.data(), d_h2, h2.size()));
+    CHIP_HIP(small_sync(c));
+    for (size_t j = 0; j < queued.size(); ++j)  // decoding.rs:205-207
+        if (std::memcmp(h2.data() + 32 * j, want.data() + 32 * queued[j], 32) != 0)
+            status[queued[j]] = CHIP_ERR_INVALID_SCRUBBED_HASH;
     return CHIP_OK;
 }
 

@@ -67,8 +67,11 @@ hipError_t gf_apply(const GfPlan &plan, const GfLaunch &L, hipStream_t stream);
 // Device copy of the packed parity table of a k-of-m encode (m - k <= 4):
 // [k][256] dwords, byte r of entry [s][x] = E[k + r][s] * x (cached).
 hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out);
-// Per-stream block of zeroed run-queue counters (2 KiB) shared by the
-// persistent kernels launched on that stream.
+// Per-stream block of zeroed run-queue counters (4 KiB) shared by the
+// persistent kernels launched on that stream: K1 words 0-256, K13 from word
+// QUEUE_K13, K3 from word QUEUE_K3 (two counters 32 words apart each).
+constexpr int QUEUE_K13 = 512;
+constexpr int QUEUE_K3 = 640;
 hipError_t stream_queue(hipStream_t stream, uint32_t **out);
 
 // ---- K13: encode() at Zfec|Bao in one pass (fused_kernels.hip) ----------
@@ -123,6 +126,10 @@ hipError_t bao_chunk_table(uint64_t N, const uint64_t **out);
 // parent (the root: the hash).
 hipError_t bao_node_check(const uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count,
                           const uint8_t *d_hash, uint8_t *chunk_flags, uint8_t *parent_flags, hipStream_t stream);
+// scrub(): per-object mask of authentic zfec shards (bit i = shard i) of
+// Bao|Zfec streams from bao_node_check's flags; spc = chunks per shard.
+hipError_t scrub_masks(const uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count, uint64_t spc,
+                       const uint8_t *chunk_flags, const uint8_t *parent_flags, uint8_t *masks, hipStream_t stream);
 // Content of chunks [c0, c1) of one stream, parents stripped, to d_out.
 hipError_t bao_gather_content(const uint8_t *d_stream, uint64_t n, uint64_t c0, uint64_t c1, uint8_t *d_out,
                               hipStream_t stream);

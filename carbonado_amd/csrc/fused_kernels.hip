@@ -65,7 +65,7 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     a.cv = static_cast<uint8_t *>(d_scratch);
     uint32_t *q = nullptr;
     if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
-    a.queue = q + 512;
+    a.queue = q + QUEUE_K13;
     const bool full = a.cols % 8 == 0 && n >= 4 * C;  // levels 1-3 in the kernel (N >= 64, 8 subtrees a block)
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<true, true>),
@@ -154,7 +154,7 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     a.cv = static_cast<uint8_t *>(d_scratch);
     uint32_t *q = nullptr;
     if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
-    a.queue = q + 512;
+    a.queue = q + QUEUE_K13;
     constexpr auto K = zfec_bao_fused_kernel<true, true, 1, 0, 1>;
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(K), hipFuncAttributeMaxDynamicSharedMemorySize,

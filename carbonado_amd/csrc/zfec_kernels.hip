@@ -161,9 +161,16 @@ std::map<int, uint8_t *> g_multab;                  // per device
 // workgroup resets them), so a stream's launches can share one block.  Blocks
 // come from a per-device pool of QUEUE_SLOTS, handed to streams in order of
 // first use; past QUEUE_SLOTS streams a slot is shared, which is safe unless
-// two of its streams run zfec launches at the same time.
+// two of its streams run persistent launches at the same time.  Block layout
+// (uint32 words): K1 0-256 (8 counters 32 apart + the done counter), K13
+// QUEUE_K13 + {0, 32}, K3 QUEUE_K3 + {0, 32}.  (The block was 2 KiB while K13
+// and K3 already used words 512-672, i.e. the NEXT stream's K1 counters: a K1
+// launch on one thread's stream beside a K13 / K3 launch on the neighbouring
+// stream could lose or repeat column tiles.)
 constexpr int QUEUE_SLOTS = 256;
-constexpr size_t QUEUE_BYTES = 2048;  // 8 counters 128 B apart + the done counter
+constexpr size_t QUEUE_BYTES = 4096;
+static_assert(QUEUE_K3 + 33 <= (int)(QUEUE_BYTES / 4) && QUEUE_K13 + 33 <= QUEUE_K3 && 257 <= QUEUE_K13,
+              "run-queue block layout");
 std::map<int, uint8_t *> g_queue_pool;                      // per device
 std::map<std::pair<int, hipStream_t>, uint32_t *> g_queue;  // (device, stream) -> counters
 

@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
+
 import torch
 
 from . import _lib
@@ -132,6 +134,27 @@ def bao_decode_batch(enc: torch.Tensor, n: int, hashes: torch.Tensor, out: torch
     count = enc.shape[0]
     check(_lib.lib().chip_bao_decode_batch_dev(_p(enc), enc.shape[1], n, count, _p(hashes), _p(out),
                                                out.shape[1], _p(status), _p(scratch), _stream()))
+
+
+def scrub_scratch(length: int, count: int, device=None) -> torch.Tensor:
+    size = _lib.lib().chip_scrub_scratch_len(length, count)
+    return torch.empty(size, dtype=torch.uint8, device=device or "cuda")
+
+
+def scrub_batch(enc: torch.Tensor, length: int, hashes: torch.Tensor, padding: int, chunk_len: int,
+                out: torch.Tensor, scratch: torch.Tensor) -> np.ndarray:
+    """scrub() (decoding.rs:159-212) of device-resident Bao|Zfec streams
+    enc uint8 [count, >= length] with one EncodeInfo; repaired streams go to
+    the rows of `out`.  Returns the per-object statuses (int32 numpy):
+    0 = repaired, CHIP_ERR_UNNECESSARY_SCRUB = intact, else scrub's error."""
+    assert enc.is_cuda and out.is_cuda and enc.is_contiguous() and out.is_contiguous()
+    count = enc.shape[0]
+    assert out.shape[0] == count and hashes.shape[0] == count
+    status = np.zeros(count, dtype=np.int32)
+    check(_lib.lib().chip_scrub_batch_dev(_p(enc), enc.shape[1], length, count, _p(hashes), padding, chunk_len,
+                                          _p(out), out.shape[1], status.ctypes.data_as(ctypes.c_void_p),
+                                          _p(scratch), _stream()))
+    return status
 
 
 def encode_host_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes: torch.Tensor,

@@ -390,6 +390,22 @@ CHIP_API int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const
  * out must hold `len` bytes. */
 CHIP_API int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t hash_len,
                         uint32_t padding, uint32_t chunk_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+/* scrub (decoding.rs:151-212) of `count` DEVICE-resident Bao|Zfec streams of
+ * `len` bytes each (stream o at d_in + o*in_stride, its expected hash at
+ * d_hash + 32*o, device), all with one EncodeInfo (padding, chunk_len; the
+ * content is 8*chunk_len bytes, else CHIP_ERR_ZFEC for the call).  Every
+ * node of every stream is verified on the device in one pass, then each
+ * stream's shards (the slices decoding.rs:173-183 verifies): status[o]
+ * (host) = CHIP_ERR_UNNECESSARY_SCRUB for an intact stream, CHIP_ERR_ZFEC
+ * with fewer than 4 authentic shards, else the repaired stream is written to
+ * d_out + o*out_stride and status[o] = CHIP_OK or the reference's scrub error
+ * (padding / length mismatch, invalid scrubbed hash).  d_scratch:
+ * chip_scrub_scratch_len(len, count) bytes.  Pointers and strides multiples
+ * of 16.  Synchronous: returns when every status is final. */
+CHIP_API uint64_t chip_scrub_scratch_len(uint64_t len, uint64_t count);
+CHIP_API int chip_scrub_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t len, uint64_t count,
+                                  const uint8_t *d_hash, uint32_t padding, uint32_t chunk_len, uint8_t *d_out,
+                                  uint64_t out_stride, int32_t *status, void *d_scratch, void *stream);
 
 /* ---- streaming bao hasher (utils.rs:104-137 BaoHasher) ------------------ */
 /* A thread-safe append-only hasher (one mutex per hasher, as the reference's

@@ -90,3 +90,53 @@ def test_scrub_multi_shard_and_unrecoverable(gpu):
     assert ca.scrub(corrupt([1, 2, 3, 4]), h, info) == enc
     with pytest.raises(ZfecError):
         ca.scrub(corrupt([0, 1, 2, 3, 4]), h, info)
+
+
+def test_scrub_batch_matches_single(gpu):
+    """chip_scrub_batch_dev over device-resident streams gives, object by
+    object, the status and the repaired stream of the single-object scrub():
+    intact, one / two / four damaged shards (the last repaired from the parity
+    shards alone), five damaged shards and a damaged root node (too few
+    authentic shards)."""
+    import torch
+    import carbonado_amd as ca
+    from carbonado_amd import device as D
+    from carbonado_amd.error import CarbonadoError
+    n = 50_000
+    damage = [[], [2], [1, 6], [0, 1, 2, 3], [0, 1, 2, 3, 4], "root"]
+    objs = [_rnd(n, 100 + i) for i in range(len(damage))]
+    encs = [ca.encode(b"", d, 12) for d in objs]
+    info = encs[0][2]
+    spc = info.chunk_slice_count
+    L = len(encs[0][0])
+    bad = []
+    for (enc, h, _), d, dmg in zip(encs, objs, damage):
+        content = O.zfec_encode(d)[0]
+        b = bytearray(enc)
+        if dmg == "root":
+            b[8 + 3] ^= 0x04
+        else:
+            for sh in dmg:
+                chunk = content[sh * spc * 1024:(sh * spc + 1) * 1024]
+                b[enc.index(chunk) + 100 + sh] ^= 0x21
+        bad.append(bytes(b))
+    count = len(bad)
+    stride = (L + 15) // 16 * 16
+    inp = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    for o in range(count):
+        inp[o, :L] = torch.frombuffer(bytearray(bad[o]), dtype=torch.uint8).cuda()
+        hashes[o] = torch.frombuffer(bytearray(encs[o][1]), dtype=torch.uint8).cuda()
+    out = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    status = D.scrub_batch(inp, L, hashes, info.padding_len, info.chunk_len, out, D.scrub_scratch(L, count))
+    expect = [12, 0, 0, 0, 7, 7]
+    assert list(status) == expect
+    for o in range(count):
+        try:
+            single, st = ca.scrub(bad[o], encs[o][1], info), 0
+        except CarbonadoError as e:
+            single, st = None, e.status
+        assert st == status[o], o
+        if st == 0:
+            assert single == encs[o][0]
+            assert bytes(out[o, :L].cpu().numpy()) == encs[o][0]

@@ -99,3 +99,74 @@ def test_8of16_queue_exact(gpu):
     torch.cuda.synchronize()
     for o in (0, 9, 19):
         assert enc[o].cpu().numpy().tobytes() == O.zfec_encode(inp[o].cpu().numpy().tobytes(), 8, 16)[0], o
+
+
+def test_concurrent_kernel_families_on_neighbouring_streams(gpu):
+    """Two host threads (each with its own stream and run-queue block)
+    alternate K1 zfec encodes, K13 content-mode bao encodes and K3 verify-
+    decodes, so persistent launches of different families overlap on
+    neighbouring streams; every result stays bit-exact.  (The queue blocks
+    were once 2 KiB while K13 / K3 kept their counters at words 512-672,
+    i.e. in the next stream's K1 counters.)"""
+    import threading
+    import numpy as np
+    import carbonado_amd as ca
+    rng = np.random.default_rng(11)
+    zd = rng.integers(0, 256, 6 << 20, dtype=np.uint8).tobytes()
+    bd = rng.integers(0, 256, (2 << 20) + 4096, dtype=np.uint8).tobytes()
+    z_want = O.zfec_encode(zd)[0]
+    b_want, b_hash = O.bao_encode(bd)
+    errors = []
+
+    def work(tid):
+        try:
+            for i in range(24):
+                op = (i + tid) % 3
+                if op == 0:
+                    assert ca.encoding.zfec(zd)[0] == z_want
+                elif op == 1:
+                    assert ca.encoding.bao(bd) == (b_want, b_hash)
+                else:
+                    assert ca.decoding.bao(b_want, b_hash) == bd
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((tid, repr(e)[:200]))
+    ts = [threading.Thread(target=work, args=(t,)) for t in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
+def test_concurrent_streams_k13_beside_k1(gpu):
+    """Back-to-back batches on two streams registered one after the other:
+    K13 content-mode bao encodes on the first, K1 zfec encodes on the second,
+    so the two persistent kernels run side by side with neighbouring run-queue
+    blocks.  Every round bit-exact (round 0 against the oracle, the others
+    against round 0)."""
+    import torch
+    from carbonado_amd import _lib, device
+    L = _lib.lib()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    nb, cb, nz, cz, R = 4 << 20, 16, 16 << 20, 8, 6
+    bin_ = _rand((cb, nb), 21)
+    zin = _rand((cz, nz), 22)
+    bstride = (L.chip_bao_encoded_len(nb) + 15) // 16 * 16
+    bouts = [torch.zeros((cb, bstride), dtype=torch.uint8, device="cuda") for _ in range(R)]
+    bh = [torch.zeros((cb, 32), dtype=torch.uint8, device="cuda") for _ in range(R)]
+    zouts = [torch.zeros((cz, 2 * nz), dtype=torch.uint8, device="cuda") for _ in range(R)]
+    bscr = device.bao_scratch(nb, cb)
+    torch.cuda.synchronize()
+    for r in range(R):  # stream sa first: its queue block precedes sb's
+        with torch.cuda.stream(sa):
+            device.bao_encode_batch(bin_, nb, bouts[r], bh[r], bscr)
+        with torch.cuda.stream(sb):
+            device.zfec_encode_batch(zin, nz, zouts[r], 4, 8)
+    torch.cuda.synchronize()
+    blen = L.chip_bao_encoded_len(nb)
+    enc0, h0 = O.bao_encode(bin_[3].cpu().numpy().tobytes())
+    assert bouts[0][3, :blen].cpu().numpy().tobytes() == enc0 and bh[0][3].cpu().numpy().tobytes() == h0
+    assert zouts[0][5].cpu().numpy().tobytes() == O.zfec_encode(zin[5].cpu().numpy().tobytes())[0]
+    for r in range(1, R):
+        assert torch.equal(bouts[r], bouts[0]) and torch.equal(bh[r], bh[0]), r
+        assert torch.equal(zouts[r], zouts[0]), r

@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 scrub hasher file15 file12 prof
+#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -29,6 +29,7 @@ for s in "$@"; do
     e2e12) run bench_e2e12 600 python3 bench.py --mode e2e --level 12 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     e2ed15) run bench_e2ed15 600 python3 bench.py --mode e2e-decode --level 15 --objects 256 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     scrub) run bench_scrub 600 python3 bench.py --mode scrub --steps 2 --warmup 1 --cpu-seconds 8 ;;
+    scrubb) run bench_scrub_batch 600 python3 bench.py --mode scrub-batch --steps 5 --warmup 1 --cpu-seconds 8 ;;
     hasher) run bench_hasher 600 python3 bench.py --mode hasher --steps 3 --warmup 1 --cpu-seconds 8 ;;
     file15) run bench_file15 600 python3 bench.py --mode file --level 15 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     file12) run bench_file12 600 python3 bench.py --mode file --level 12 --steps 3 --warmup 1 --no-cpu-baseline ;;
