@@ -964,32 +964,17 @@ hipError_t run_parent_levels(uint8_t *cv_prev, uint64_t stride_prev, uint64_t cn
     return hipSuccess;
 }
 
-// Enqueue K3 then one K4 launch per remaining level.
-template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0, bool DQ = false>
-hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
-                   uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
-                   void *d_scratch, hipStream_t stream, size_t pad_lds = 0 /* tuning: occupancy probe */,
-                   uint64_t out_limit = ~0ull /* decode: content prefix written */) {
-    if (count == 0) return hipSuccess;
-    const uint64_t N = n_chunks(n);
-    constexpr int LOG = ilog2(BAO_CPL);
-    const uint64_t N0 = (N + BAO_CPL - 1) / BAO_CPL;  // nodes at level LOG
-    uint8_t *bufA = static_cast<uint8_t *>(d_scratch);
-    uint8_t *bufB = bufA + count * N0 * 32;
-    const uint64_t strideA = N0, strideB = (N0 + 1) / 2;
-
-    ChunkArgs ca;
-    ca.in = d_in; ca.out = d_out; ca.in_stride = in_stride; ca.out_stride = out_stride;
-    ca.n = n; ca.N = N; ca.count = count; ca.cv = bufA; ca.cv_stride = strideA;
-    ca.hash = d_hash; ca.status = d_status;
-    ca.out_limit = out_limit;
-    const uint64_t waves = count * ((N + 64ull * BAO_CPL - 1) / (64ull * BAO_CPL));
+// Enqueue K3 over `waves` wave tasks: with DQ a persistent grid of resident
+// workgroups taking wave tasks from the stream's run queue, else one wave per
+// task.
+template <int MODE, int CPL, bool NTS, int SP, int SU, int SE, int XG, bool DQ>
+hipError_t launch_chunk_kernel(ChunkArgs ca, hipStream_t stream, size_t pad_lds) {
+    const uint64_t waves = ca.count * ((ca.N + 64ull * CPL - 1) / (64ull * CPL));
     const uint64_t blocks = (waves + K3_WAVES - 1) / K3_WAVES;
-    hipError_t e = hipSuccess;
     bool dq = DQ && waves < (1ull << 31);
     if (dq) {  // persistent grid of resident workgroups, wave tasks from the stream's run queue
         uint32_t *q = nullptr;
-        const void *fn = reinterpret_cast<const void *>(bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG, true>);
+        const void *fn = reinterpret_cast<const void *>(bao_chunk_kernel<MODE, CPL, NTS, SP, SU, SE, XG, true>);
         // per instance and LDS pad, asked once: the query costs ~6 us of API
         // time, which single small objects paid on every call (profiles/r4c)
         static std::mutex occ_mu;
@@ -1011,14 +996,36 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
         if (dq) {
             ca.queue = q + QUEUE_K3;
             const uint64_t grid = std::min<uint64_t>(blocks, (uint64_t)per_cu * (uint64_t)num_cus());
-            hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG, true>), dim3((unsigned)grid),
+            hipLaunchKernelGGL((bao_chunk_kernel<MODE, CPL, NTS, SP, SU, SE, XG, true>), dim3((unsigned)grid),
                                dim3(K3_TPB), pad_lds, stream, ca);
         }
     }
     if (!dq)
-        hipLaunchKernelGGL((bao_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG>), dim3((unsigned)blocks),
+        hipLaunchKernelGGL((bao_chunk_kernel<MODE, CPL, NTS, SP, SU, SE, XG>), dim3((unsigned)blocks),
                            dim3(K3_TPB), pad_lds, stream, ca);
-    e = hipGetLastError();
+    return hipGetLastError();
+}
+
+// Enqueue K3 then one K4 launch per remaining level.
+template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0, bool DQ = false>
+hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                   uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
+                   void *d_scratch, hipStream_t stream, size_t pad_lds = 0 /* tuning: occupancy probe */,
+                   uint64_t out_limit = ~0ull /* decode: content prefix written */) {
+    if (count == 0) return hipSuccess;
+    const uint64_t N = n_chunks(n);
+    constexpr int LOG = ilog2(BAO_CPL);
+    const uint64_t N0 = (N + BAO_CPL - 1) / BAO_CPL;  // nodes at level LOG
+    uint8_t *bufA = static_cast<uint8_t *>(d_scratch);
+    uint8_t *bufB = bufA + count * N0 * 32;
+    const uint64_t strideA = N0, strideB = (N0 + 1) / 2;
+
+    ChunkArgs ca;
+    ca.in = d_in; ca.out = d_out; ca.in_stride = in_stride; ca.out_stride = out_stride;
+    ca.n = n; ca.N = N; ca.count = count; ca.cv = bufA; ca.cv_stride = strideA;
+    ca.hash = d_hash; ca.status = d_status;
+    ca.out_limit = out_limit;
+    hipError_t e = launch_chunk_kernel<MODE, BAO_CPL, BAO_NTS, SP, SU, SE, XG, DQ>(ca, stream, pad_lds);
     if (e != hipSuccess) return e;
 
     uint8_t *stream_buf = (MODE == 0 || MODE == 3) ? d_out : const_cast<uint8_t *>(d_in);
@@ -1054,10 +1061,8 @@ hipError_t run_node_check(const uint8_t *d_stream, uint64_t stride, uint64_t n, 
     ca.in = d_stream; ca.out = nullptr; ca.in_stride = stride; ca.out_stride = 0;
     ca.n = n; ca.N = N; ca.count = count; ca.cv = chunk_flags; ca.cv_stride = N;
     ca.hash = const_cast<uint8_t *>(d_hash); ca.status = nullptr;
-    const uint64_t waves = count * ((N + 63) / 64);
-    hipLaunchKernelGGL((bao_chunk_kernel<2, 1, false>), dim3((unsigned)((waves + K3_WAVES - 1) / K3_WAVES)),
-                       dim3(K3_TPB), 0, stream, ca);
-    hipError_t e = hipGetLastError();
+    // persistent grid, wave tasks from the run queue (as decode); scrub's batch check
+    hipError_t e = launch_chunk_kernel<2, 1, false, 0, 1, 0, 1, true>(ca, stream, 0);
     if (e != hipSuccess || N < 2) return e;
     CheckArgs pa{d_stream, stride, N, count, N - 1, d_hash, parent_flags};
     const uint64_t work = count * (N - 1);

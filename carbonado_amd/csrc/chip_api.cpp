@@ -1561,6 +1561,9 @@ int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t h
     return CHIP_OK;
 }
 
+// damaged streams repaired per batch (scratch: ~5 x the stream per object)
+constexpr size_t kScrubGroup = 64;
+
 uint64_t chip_scrub_scratch_len(uint64_t len, uint64_t count) {
     uint64_t n = 0;
     if (!bao_content_len(len, &n)) return 16;
@@ -1598,29 +1601,73 @@ int chip_scrub_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t len, 
         else repair.push_back(o);
     }
     if (repair.empty()) return CHIP_OK;
-    // the damaged streams, one after another on the thread's stream (the
-    // buffers are reused in stream order); one synchronisation for all
+    // the damaged streams in groups of up to kScrubGroup, as batches: gather
+    // each stream's content, zfec decode per share pattern (the group sorted
+    // by pattern), one fused re-encode of the group, rows copied to d_out;
+    // one synchronisation per group.  (One object at a time, each launch ran
+    // nearly empty: ~0.19 ms per 16 MiB object.)
     Ctx *c;
     st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    CHIP_HIP(grow(c->flags, 32 * repair.size()));
-    uint8_t *d_h2 = static_cast<uint8_t *>(c->flags.p);
-    std::vector<uint64_t> queued;
-    for (uint64_t o : repair) {
-        std::vector<uint32_t> good;
+    const uint64_t kc = (uint64_t)CHIP_FEC_K * C;
+    struct Rep { uint64_t o; std::vector<uint32_t> sel; };
+    std::vector<Rep> reps;
+    uint32_t pad2 = 0;
+    uint64_t C2 = 0;
+    const bool pad_ok = padding <= kc;
+    if (pad_ok) calc_pad(kc - padding, CHIP_FEC_K, &pad2, &C2);
+    for (uint64_t o : repair) {  // the host-side verdicts, as scrub_repair_enqueue's order
+        std::vector<uint32_t> good, pos;
         for (uint32_t i = 0; i < CHIP_FEC_M; ++i)
             if (m[o] >> i & 1) good.push_back(i);
-        status[o] = scrub_repair_enqueue(c, d_in + o * in_stride, n, len, good, padding, C, d_out + o * out_stride,
-                                         d_h2 + 32 * queued.size());
-        if (status[o] == CHIP_ERR_DEVICE) return CHIP_ERR_DEVICE;
-        if (status[o] == CHIP_OK) queued.push_back(o);
+        if (!pad_ok) { status[o] = CHIP_ERR_ZFEC; continue; }
+        if (pad2 != padding) { status[o] = CHIP_ERR_SCRUBBED_PADDING_MISMATCH; continue; }
+        if (bao_encoded_len((uint64_t)CHIP_FEC_M * C2) != len) { status[o] = CHIP_ERR_SCRUBBED_LENGTH_MISMATCH; continue; }
+        if (select_shares(CHIP_FEC_K, CHIP_FEC_M, good.data(), (uint32_t)good.size(), &pos) != CHIP_OK) {
+            status[o] = CHIP_ERR_ZFEC;
+            continue;
+        }
+        Rep r{o, {}};
+        for (uint32_t p : pos) r.sel.push_back(good[p]);
+        reps.push_back(std::move(r));
     }
-    std::vector<uint8_t> h2(32 * queued.size());
-    if (!queued.empty()) CHIP_HIP(small_d2h(c, h2.data(), d_h2, h2.size()));
-    CHIP_HIP(small_sync(c));
-    for (size_t j = 0; j < queued.size(); ++j)  // decoding.rs:205-207
-        if (std::memcmp(h2.data() + 32 * j, want.data() + 32 * queued[j], 32) != 0)
-            status[queued[j]] = CHIP_ERR_INVALID_SCRUBBED_HASH;
+    std::stable_sort(reps.begin(), reps.end(), [](const Rep &a, const Rep &b) { return a.sel < b.sel; });
+    const uint64_t z2 = (uint64_t)CHIP_FEC_M * C2, lstride = (len + 15) & ~uint64_t(15);
+    for (size_t g0 = 0; g0 < reps.size(); g0 += kScrubGroup) {
+        const size_t R = std::min(kScrubGroup, reps.size() - g0);
+        CHIP_HIP(grow(c->mid, R * n));
+        CHIP_HIP(grow(c->x1, R * kc));
+        CHIP_HIP(grow(c->x2, R * lstride));
+        CHIP_HIP(grow(c->flags, 32 * R));
+        CHIP_HIP(grow(c->scratch, std::max(zfec_bao_scratch_len(z2, R), bao_scratch_len(z2, R))));
+        uint8_t *d_z = static_cast<uint8_t *>(c->mid.p), *d_dec = static_cast<uint8_t *>(c->x1.p);
+        uint8_t *d_enc = static_cast<uint8_t *>(c->x2.p), *d_h2 = static_cast<uint8_t *>(c->flags.p);
+        for (size_t j = 0; j < R; ++j)
+            CHIP_HIP(bao_gather_content(d_in + reps[g0 + j].o * in_stride, n, 0, N, d_z + j * n, c->stream));
+        for (size_t j = 0; j < R;) {  // zfec decode from the authentic shares, TRUE indices (decoding.rs:187)
+            size_t e2 = j + 1;
+            while (e2 < R && reps[g0 + e2].sel == reps[g0 + j].sel) ++e2;
+            std::vector<uint64_t> slot_off(CHIP_FEC_K);
+            for (uint32_t k2 = 0; k2 < CHIP_FEC_K; ++k2) slot_off[k2] = reps[g0 + j].sel[k2] * C;
+            st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_z + j * n, n, slot_off, reps[g0 + j].sel, C, e2 - j,
+                                    d_dec + j * kc, kc, c->stream);
+            if (st != CHIP_OK) return st;
+            j = e2;
+        }
+        // re-encode (decoding.rs:191-196): encode() at Zfec|Bao of every decoded object, one fused pass
+        CHIP_HIP(zfec_bao_dev(d_dec, kc, kc - padding, R, C2, d_enc, lstride, d_h2, c->scratch.p, c->stream));
+        for (size_t j = 0; j < R; ++j)
+            CHIP_HIP(hipMemcpyAsync(d_out + reps[g0 + j].o * out_stride, d_enc + j * lstride, len,
+                                    hipMemcpyDeviceToDevice, c->stream));
+        std::vector<uint8_t> h2(32 * R);
+        CHIP_HIP(small_d2h(c, h2.data(), d_h2, h2.size()));
+        CHIP_HIP(small_sync(c));
+        for (size_t j = 0; j < R; ++j) {  // decoding.rs:205-207
+            const uint64_t o = reps[g0 + j].o;
+            status[o] = std::memcmp(h2.data() + 32 * j, want.data() + 32 * o, 32) ? CHIP_ERR_INVALID_SCRUBBED_HASH
+                                                                                 : CHIP_OK;
+        }
+    }
     return CHIP_OK;
 }
 
