@@ -132,13 +132,21 @@ struct Ctx {
             if (b->p) (void)hipFree(b->p);
             *b = DevBuf{};
         }
-        if (stream) (void)hipStreamDestroy(stream);
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            stream_queue_release(stream);
+            (void)hipStreamDestroy(stream);
+        }
         stream = nullptr;
         for (Slot &sl : slots) {
             for (DevBuf *b : {&sl.in, &sl.mid, &sl.out, &sl.hash, &sl.scratch})
                 if (b->p) (void)hipFree(b->p);
             if (sl.stage.p) (void)hipHostFree(sl.stage.p);
-            if (sl.stream) (void)hipStreamDestroy(sl.stream);
+            if (sl.stream) {
+                (void)hipStreamSynchronize(sl.stream);
+                stream_queue_release(sl.stream);
+                (void)hipStreamDestroy(sl.stream);
+            }
         }
         slots.clear();
         ready = false;
@@ -2441,7 +2449,11 @@ void chip_bao_hasher_free(chip_bao_hasher *h) {
         std::lock_guard<std::mutex> lk(h->mu);
         for (DevBuf *b : {&h->content, &h->enc, &h->scratch, &h->hash})
             if (b->p) (void)hipFree(b->p);
-        if (h->stream) (void)hipStreamDestroy(h->stream);
+        if (h->stream) {
+            (void)hipStreamSynchronize(h->stream);
+            stream_queue_release(h->stream);
+            (void)hipStreamDestroy(h->stream);
+        }
     }
     delete h;
 }

@@ -73,6 +73,9 @@ hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out);
 constexpr int QUEUE_K13 = 512;
 constexpr int QUEUE_K3 = 640;
 hipError_t stream_queue(hipStream_t stream, uint32_t **out);
+// Return a stream's block to the pool; call once the stream's work is done,
+// before the stream is destroyed (a later stream may get the same handle).
+void stream_queue_release(hipStream_t stream);
 
 // ---- K13: encode() at Zfec|Bao in one pass (fused_kernels.hip) ----------
 // `count` objects of n bytes (zero padded to 4C) -> bao streams of their

@@ -173,6 +173,8 @@ static_assert(QUEUE_K3 + 33 <= (int)(QUEUE_BYTES / 4) && QUEUE_K13 + 33 <= QUEUE
               "run-queue block layout");
 std::map<int, uint8_t *> g_queue_pool;                      // per device
 std::map<std::pair<int, hipStream_t>, uint32_t *> g_queue;  // (device, stream) -> counters
+std::map<int, std::vector<uint32_t *>> g_queue_free;        // per device: blocks of destroyed streams
+std::map<int, size_t> g_queue_next;                          // per device: next never-used block
 
 hipError_t queue_for(hipStream_t stream, uint32_t **out) {
     const int dev = selected_device();
@@ -189,9 +191,18 @@ hipError_t queue_for(hipStream_t stream, uint32_t **out) {
         if (e != hipSuccess) { (void)hipFree(d); return e; }
         pool = d;
     }
-    size_t used = 0;
-    for (const auto &kv : g_queue) used += kv.first.first == dev;
-    uint32_t *q = reinterpret_cast<uint32_t *>(pool + (used % QUEUE_SLOTS) * QUEUE_BYTES);
+    // a destroyed stream's block first (its launches left it zero), then a
+    // fresh one; blocks are shared only once QUEUE_SLOTS streams are alive
+    uint32_t *q;
+    std::vector<uint32_t *> &fl = g_queue_free[dev];
+    if (!fl.empty()) {
+        q = fl.back();
+        fl.pop_back();
+    } else {
+        size_t &nx = g_queue_next[dev];
+        q = reinterpret_cast<uint32_t *>(pool + (nx % QUEUE_SLOTS) * QUEUE_BYTES);
+        ++nx;
+    }
     g_queue[key] = q;
     *out = q;
     return hipSuccess;
@@ -360,6 +371,15 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
 // The stream's run-queue block for other persistent kernels (K13 uses words
 // 512 and 544, clear of K1's counters; each launch leaves its words zero).
 hipError_t stream_queue(hipStream_t stream, uint32_t **out) { return queue_for(stream, out); }
+
+void stream_queue_release(hipStream_t stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int dev = selected_device();
+    auto it = g_queue.find(std::make_pair(dev, stream));
+    if (it == g_queue.end()) return;
+    g_queue_free[dev].push_back(it->second);
+    g_queue.erase(it);
+}
 
 hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out) {
     if (k == 0 || m <= k || m - k > 4) return hipErrorInvalidValue;

@@ -81,3 +81,26 @@ def test_hasher_state_errors(gpu):
     h.finalize()
     with pytest.raises(InvalidArgument):
         h.update(b"more")  # bao's Encoder cannot take bytes after finalize
+
+
+def test_hasher_churn_recycles_queue_blocks(gpu):
+    """Hundreds of hashers, each with its own stream and (once it runs a
+    persistent kernel) its own run-queue block, created and freed one after
+    another past the 256-block pool: blocks of freed streams are reused, and
+    every digest stays exact while a long-lived stream (this thread's K1
+    encodes) keeps its own block."""
+    import gc
+    import carbonado_amd as ca
+    from carbonado_amd.utils import BaoHasher
+    data = np.random.default_rng(9).integers(0, 256, (1 << 20) + 5, dtype=np.uint8).tobytes()
+    want = O.blake3(data)
+    zd = data[: 3 << 20] if len(data) >= 3 << 20 else data * 3
+    z_want = O.zfec_encode(zd)[0]
+    for i in range(300):
+        h = BaoHasher.new()
+        h.update(data)
+        assert h.finalize() == want, i
+        del h
+        if i % 50 == 0:
+            gc.collect()
+            assert ca.encoding.zfec(zd)[0] == z_want
