@@ -83,8 +83,12 @@ uint64_t bao_scratch_len(uint64_t n, uint64_t count) { return bao_scratch_len_t<
 hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                           uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch,
                           hipStream_t stream) {
-    if (small_ok(n, count)) return small_bao_encode_dev(d_in, n, d_out, d_hash, stream);
-    if (d_out && fused_on() && bao_fused_ok(d_in, in_stride, n, count))  // K13 KIND 1 (fused_kernels.hip)
+    // batches: KS below 64 KiB, where K13's content mode cannot take whole 64-chunk blocks
+    // (r4q: 32 KiB objects 1032 vs 528 GiB/s; 64 KiB: K13 1477 vs KS 1046)
+    const bool k13 = d_out && fused_on() && bao_fused_ok(d_in, in_stride, n, count);
+    if (small_ok(n, count, k13 ? 0 : KS_TINY_N))
+        return small_bao_encode_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, stream);
+    if (k13)  // K13 KIND 1 (fused_kernels.hip)
         return bao_fused_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_scratch, stream);
     return run_bao<0>(d_in, in_stride, n, count, d_out, out_stride, d_hash, nullptr, d_scratch, stream);
 }
@@ -92,7 +96,8 @@ hipError_t bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, u
 hipError_t bao_decode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                           const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                           uint32_t *d_status, void *d_scratch, hipStream_t stream) {
-    if (small_ok(n, count)) return small_bao_decode_dev(d_in, n, d_hash, d_out, d_out ? n : 0, d_status, stream);
+    if (small_ok(n, count))
+        return small_bao_decode_dev(d_in, in_stride, n, count, d_hash, d_out, out_stride, n, d_status, stream);
     return run_bao<1>(d_in, in_stride, n, count, d_out, out_stride, const_cast<uint8_t *>(d_hash),
                       d_status, d_scratch, stream);
 }
@@ -101,7 +106,8 @@ hipError_t bao_decode_prefix_dev(const uint8_t *d_in, uint64_t in_stride, uint64
                                  const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
                                  uint32_t *d_status, void *d_scratch, hipStream_t stream) {
     if (small_ok(n, count))
-        return small_bao_decode_dev(d_in, n, d_hash, d_out, d_out ? std::min(out_limit, n) : 0, d_status, stream);
+        return small_bao_decode_dev(d_in, in_stride, n, count, d_hash, d_out, out_stride, std::min(out_limit, n),
+                                    d_status, stream);
     return run_bao_t<1, BAO_CPL, BAO_DEC_NTS, 0, 1, 0, BAO_XG, BAO_DQ>(d_in, in_stride, n, count, d_out, out_stride,
                                                           const_cast<uint8_t *>(d_hash), d_status, d_scratch, stream,
                                                           0, out_limit);

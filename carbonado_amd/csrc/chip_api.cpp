@@ -606,7 +606,10 @@ int pipe_wg_cfg() {
 hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
                         uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s) {
     const uint64_t zlen = (uint64_t)CHIP_FEC_M * C;
-    if (small_ok(zlen, count)) return small_zfec_bao_dev(d_in, n, C, d_out, d_hash, s);
+    // batches: KS while K13's 8-column blocks are not full (N < 64; r4q: 16 KiB objects 618 vs 393
+    // GiB/s, 32 KiB = N 64: K13 737 vs KS 608)
+    if (small_ok(zlen, count, KS_TINY_N - 1))
+        return small_zfec_bao_dev(d_in, in_stride, n, count, C, d_out, out_stride, d_hash, s);
     if (fused_on()) return zfec_bao_fused_dev(d_in, in_stride, n, count, C, d_out, out_stride, d_hash, d_scratch, s);
     const uint64_t *tab = nullptr;
     hipError_t e = bao_chunk_table(zlen / 1024, &tab);

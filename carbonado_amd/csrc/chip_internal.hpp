@@ -141,18 +141,23 @@ uint64_t bao_chunk_offset(uint64_t i, uint64_t N);
 uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N);
 uint64_t bao_parent_index(uint64_t s, int level, uint64_t N);
 
-// ---- KS: single small objects in one launch (small_kernels.hip) ---------
-// Latency path for count == 1 and a bao stream of at most KS_MAX_N chunks
-// (CHIP_SMALL=0 turns it off); the batch entry points above take it
+// ---- KS: small objects, one workgroup per object (small_kernels.hip) ----
+// Latency path for count == 1 and a bao stream of at most KS_MAX_N chunks,
+// and the batch path for tiny objects (at most KS_TINY_N chunks, one wave
+// each); CHIP_SMALL=0 turns both off.  The batch entry points take them
 // themselves when small_ok() holds.
+// tiny_max: the largest N for which the caller's batch kernel loses to KS
+// (measured per path, DESIGN.md §3 KS; at most KS_TINY_N).
 constexpr uint64_t KS_MAX_N = 512;
-bool small_ok(uint64_t bao_n, uint64_t count);
-hipError_t small_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_out, uint8_t *d_hash,
-                                hipStream_t stream);
-hipError_t small_zfec_bao_dev(const uint8_t *d_in, uint64_t n, uint64_t C, uint8_t *d_out, uint8_t *d_hash,
-                              hipStream_t stream);
-hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t n, const uint8_t *d_hash, uint8_t *d_out,
-                                uint64_t out_limit, uint32_t *d_status, hipStream_t stream);
+constexpr uint64_t KS_TINY_N = 64;
+bool small_ok(uint64_t bao_n, uint64_t count, uint64_t tiny_max = KS_TINY_N);
+hipError_t small_bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                                uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, hipStream_t stream);
+hipError_t small_zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
+                              uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, hipStream_t stream);
+hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t in_stride, uint64_t n, uint64_t count,
+                                const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
+                                uint32_t *d_status, hipStream_t stream);
 
 // ---- batch buffers (hbm_alloc.hip) --------------------------------------
 // Class-balanced device memory for buffers >= 1 GiB (hbm_alloc.hpp); returns

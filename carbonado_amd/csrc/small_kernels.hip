@@ -22,9 +22,10 @@
 //    hash; (decode) the content prefix out, every chunk and parent recomputed
 //    and compared with the stored node, the root with the expected hash.
 //
-// Used for single-object calls (count == 1) of bao encode / decode and
-// encode() at Zfec|Bao with N <= KS_MAX_N; CHIP_SMALL=0 turns it off (A/B
-// runs and tests compare the two paths byte for byte).
+// Used for single-object calls (count == 1, N <= KS_MAX_N) and for batches
+// of tiny objects (N <= KS_TINY_N) of bao encode / decode and encode() at
+// Zfec|Bao; CHIP_SMALL=0 turns it off (A/B runs and tests compare the paths
+// byte for byte).
 #include "bao_device.hpp"
 #include "chip_internal.hpp"
 #include "zfec_device.hpp"
@@ -38,8 +39,13 @@ using namespace bao;
 
 namespace small {
 
-constexpr int TPB = 512;         // 8 waves = 128 quads
-constexpr int QUADS = TPB / 4;
+// Two shapes: one object per call (512 threads = 128 quads, N <= 512: one
+// chunk round for up to 128 chunks) and batches of tiny objects (64 threads =
+// 16 quads, N <= 64: one wave per object, so a CU holds many objects at once
+// where the batch kernels would run 1-8 of a wave's 64 lanes).
+constexpr int BIG_TPB = 512, BIG_N = 512;
+constexpr int TINY_TPB = 64, TINY_N = 64;
+static_assert(BIG_N <= K4T_MAX, "tree walk bound");
 
 struct SmallArgs {
     const uint8_t *in;      // encode: content (C == 0) or zfec input; decode: stream
@@ -111,11 +117,12 @@ __device__ __forceinline__ u32x4 load16_bytes(const uint8_t *p, uint32_t valid) 
     return valid == 0 ? u32x4{0u, 0u, 0u, 0u} : load16_partial(p, valid);
 }
 
-// MODE 0: encode, MODE 1: verify-decode.  One workgroup per object.
-template <int MODE>
+// MODE 0: encode, MODE 1: verify-decode.  One workgroup per object, N <= MAXN.
+template <int MODE, int TPB, int MAXN>
 __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t tab[4 * 256];        // zfec parity products
-    __shared__ __attribute__((aligned(16))) uint32_t cvs[2][K4T_MAX][8];  // one tree level and the next
+    constexpr int QUADS = TPB / 4;
+    __shared__ __attribute__((aligned(16))) uint32_t tab[4 * 256];     // zfec parity products
+    __shared__ __attribute__((aligned(16))) uint32_t cvs[2][MAXN][8];  // one tree level and the next
     __shared__ __attribute__((aligned(16))) uint32_t msg[QUADS][16];  // each quad's message block
     const uint64_t obj = blockIdx.x;
     const int t = threadIdx.x, q = t & 3, g = t >> 2;
@@ -287,42 +294,57 @@ bool enabled() {
 }
 
 hipError_t launch(int mode, const SmallArgs &a, hipStream_t stream) {
-    if (mode == 0) hipLaunchKernelGGL(small_kernel<0>, dim3((unsigned)a.count), dim3(TPB), 0, stream, a);
-    else hipLaunchKernelGGL(small_kernel<1>, dim3((unsigned)a.count), dim3(TPB), 0, stream, a);
+    if (a.count == 0) return hipSuccess;
+    if (a.count > 0x7fffffffull) return hipErrorInvalidValue;
+    const bool tiny = a.N <= (uint64_t)TINY_N && a.count > 1;
+    const dim3 grid((unsigned)a.count);
+    if (tiny) {
+        if (mode == 0) hipLaunchKernelGGL((small_kernel<0, TINY_TPB, TINY_N>), grid, dim3(TINY_TPB), 0, stream, a);
+        else hipLaunchKernelGGL((small_kernel<1, TINY_TPB, TINY_N>), grid, dim3(TINY_TPB), 0, stream, a);
+    } else {
+        if (mode == 0) hipLaunchKernelGGL((small_kernel<0, BIG_TPB, BIG_N>), grid, dim3(BIG_TPB), 0, stream, a);
+        else hipLaunchKernelGGL((small_kernel<1, BIG_TPB, BIG_N>), grid, dim3(BIG_TPB), 0, stream, a);
+    }
     return hipGetLastError();
 }
 
 }  // namespace small
 
-bool small_ok(uint64_t bao_n, uint64_t count) {
-    return small::enabled() && count == 1 && n_chunks(bao_n) <= (uint64_t)KS_MAX_N;
+bool small_ok(uint64_t bao_n, uint64_t count, uint64_t tiny_max) {
+    if (!small::enabled() || count == 0) return false;
+    const uint64_t N = n_chunks(bao_n);
+    return count == 1 ? N <= (uint64_t)KS_MAX_N : N <= tiny_max && count <= 0x7fffffffull;
 }
 
-hipError_t small_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_out, uint8_t *d_hash,
-                                hipStream_t stream) {
+hipError_t small_bao_encode_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
+                                uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, hipStream_t stream) {
     small::SmallArgs a{};
-    a.in = d_in; a.out = d_out; a.n = n; a.N = n_chunks(n); a.valid = n; a.count = 1;
+    a.in = d_in; a.in_stride = in_stride; a.out = d_out; a.out_stride = out_stride;
+    a.n = n; a.N = n_chunks(n); a.valid = n; a.count = count;
     a.hash = d_hash;
     return small::launch(0, a, stream);
 }
 
-hipError_t small_zfec_bao_dev(const uint8_t *d_in, uint64_t n, uint64_t C, uint8_t *d_out, uint8_t *d_hash,
-                              hipStream_t stream) {
-    if (C == 0 || C % 1024) return hipErrorInvalidValue;
+hipError_t small_zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
+                              uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, hipStream_t stream) {
+    if (C == 0 || C % 1024 || !d_out) return hipErrorInvalidValue;
     const void *tab = nullptr;
     hipError_t e = zfec_parity_table(4, 8, &tab);
     if (e != hipSuccess) return e;
     small::SmallArgs a{};
-    a.in = d_in; a.out = d_out; a.n = 8 * C; a.N = n_chunks(8 * C); a.valid = n; a.C = C; a.count = 1;
+    a.in = d_in; a.in_stride = in_stride; a.out = d_out; a.out_stride = out_stride;
+    a.n = 8 * C; a.N = n_chunks(8 * C); a.valid = n; a.C = C; a.count = count;
     a.table = static_cast<const uint32_t *>(tab);
     a.hash = d_hash;
     return small::launch(0, a, stream);
 }
 
-hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t n, const uint8_t *d_hash, uint8_t *d_out,
-                                uint64_t out_limit, uint32_t *d_status, hipStream_t stream) {
+hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t in_stride, uint64_t n, uint64_t count,
+                                const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
+                                uint32_t *d_status, hipStream_t stream) {
     small::SmallArgs a{};
-    a.in = d_stream; a.out = d_out; a.n = n; a.N = n_chunks(n); a.out_limit = out_limit; a.count = 1;
+    a.in = d_stream; a.in_stride = in_stride; a.out = d_out; a.out_stride = out_stride;
+    a.n = n; a.N = n_chunks(n); a.out_limit = d_out ? out_limit : 0; a.count = count;
     a.hash = const_cast<uint8_t *>(d_hash);
     a.status = d_status;
     return small::launch(1, a, stream);

@@ -102,3 +102,50 @@ def test_small_matches_batch_kernels(gpu):
         for i in range(count):
             assert bytes(out[i, :olen].cpu().numpy()) == single[i][0]
             assert bytes(hashes[i].cpu().numpy()) == single[i][1]
+
+
+# batches of tiny objects (bao stream of at most 64 chunks): one 64-thread
+# workgroup per object; n values give N = 1, 2, 7, 63, 64 (and 65 / 72: the
+# batch kernels) at level 4, N = 8, 16, 64 (and 72) at level 12
+TINY = [(4, 0), (4, 1), (4, 1025), (4, 6 * 1024 + 1), (4, 63 * 1024), (4, 64 * 1024), (4, 64 * 1024 + 1),
+        (12, 1), (12, 4097), (12, 32768), (12, 32769)]
+
+
+@pytest.mark.parametrize("level,n", TINY)
+def test_tiny_batches(gpu, level, n):
+    import torch
+    from carbonado_amd import device as D
+    count = 9
+    objs = [_data(n, 40 + s) for s in range(count)]
+    stride = max(16, (n + 15) // 16 * 16)
+    inp = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    for i, o in enumerate(objs):
+        if n:
+            inp[i, :n] = torch.frombuffer(bytearray(o), dtype=torch.uint8).cuda()
+    oenc, oh, oinfo = O.encode(objs[0], level)
+    olen = len(oenc)
+    ostride = (olen + 15) // 16 * 16
+    out = torch.zeros((count, ostride), dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    got_len, info = D.encode_batch(level, inp, n, out, hashes, D.encode_scratch(level, n, count))
+    torch.cuda.synchronize()
+    assert got_len == olen
+    encs = []
+    for i in range(count):
+        e, h, _ = O.encode(objs[i], level)
+        assert bytes(out[i, :olen].cpu().numpy()) == e, i
+        assert bytes(hashes[i].cpu().numpy()) == h, i
+        encs.append(e)
+    # decode the batch back; object 4's stream has one flipped byte
+    bad = out.clone()
+    bad[4, olen - 1] ^= 1
+    dec = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    status = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    D.decode_batch(level, bad, olen, hashes, info.padding_len, dec, status,
+                   D.decode_scratch(level, olen, count))
+    torch.cuda.synchronize()
+    st = status.cpu().tolist()
+    assert st[4] == 5 and all(s == 0 for i, s in enumerate(st) if i != 4), st
+    for i in range(count):
+        if i != 4:
+            assert bytes(dec[i, :n].cpu().numpy()) == objs[i], i
