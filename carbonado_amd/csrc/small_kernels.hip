@@ -57,6 +57,7 @@ struct SmallArgs {
     uint64_t C;             // encode: zfec 4-of-8 shard length, 0 = bao of the content
     uint64_t out_limit;     // decode: content bytes written
     uint64_t count;
+    uint32_t per;           // objects per workgroup (a power of two; per * N <= QUADS when > 1)
     const uint32_t *table;  // zfec parity table [4][256]
     uint8_t *hash;          // encode: root hashes out; decode: expected
     uint32_t *status;       // decode: per object, 0 or CHIP_ERR_BAO_HASH_MISMATCH
@@ -117,29 +118,34 @@ __device__ __forceinline__ u32x4 load16_bytes(const uint8_t *p, uint32_t valid) 
     return valid == 0 ? u32x4{0u, 0u, 0u, 0u} : load16_partial(p, valid);
 }
 
-// MODE 0: encode, MODE 1: verify-decode.  One workgroup per object, N <= MAXN.
+// MODE 0: encode, MODE 1: verify-decode.  A workgroup holds a.per objects
+// (1 unless N is small enough for several to share the quads), N <= MAXN / per.
 template <int MODE, int TPB, int MAXN>
 __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
     constexpr int QUADS = TPB / 4;
     __shared__ __attribute__((aligned(16))) uint32_t tab[4 * 256];     // zfec parity products
     __shared__ __attribute__((aligned(16))) uint32_t cvs[2][MAXN][8];  // one tree level and the next
     __shared__ __attribute__((aligned(16))) uint32_t msg[QUADS][16];  // each quad's message block
-    const uint64_t obj = blockIdx.x;
     const int t = threadIdx.x, q = t & 3, g = t >> 2;
+    const int GT = TPB / (int)a.per, GQ = GT / 4;  // threads and quads of one object
+    const int ol = t / GT, tl = t - ol * GT, gl = tl >> 2;
+    const uint64_t obj = (uint64_t)blockIdx.x * a.per + ol;
+    const bool live = obj < a.count;
+    const uint32_t cb = (uint32_t)ol * (MAXN / a.per);  // my object's CV rows
     const uint64_t N = a.N, n = a.n;
-    const uint8_t *src = a.in + obj * a.in_stride;
-    uint8_t *dst = a.out ? a.out + obj * a.out_stride : nullptr;
+    const uint8_t *src = a.in + (live ? obj : 0) * a.in_stride;
+    uint8_t *dst = a.out ? a.out + (live ? obj : 0) * a.out_stride : nullptr;
     const uint8_t *stream = MODE == 0 ? dst : src;
     bool ok = true;
 
     // ---- phase 1: header; zfec shards or content into their slots / content out
     if (MODE == 0) {
-        if (dst && t == 0) *glb(reinterpret_cast<uint64_t *>(dst)) = n;
+        if (live && dst && tl == 0) *glb(reinterpret_cast<uint64_t *>(dst)) = n;
         if (a.C) {
             for (int i = t; i < 4 * 256; i += TPB) tab[i] = a.table[i];
             __syncthreads();
             const uint64_t cols = a.C / 1024;
-            for (uint64_t o = 16 * (uint64_t)t; o < a.C; o += 16 * TPB) {  // 16 B of every shard at shard byte o
+            for (uint64_t o = 16 * (uint64_t)tl; live && o < a.C; o += 16 * GT) {  // 16 B of every shard at byte o
                 u32x4 v[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = zf::load16_masked(src, j * a.C + o, a.valid);
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
                     store16_a8<false>(dst + chunk_stream_off(s * cols + u, N) + w, s < 4 ? v[s] : p[s - 4]);
             }
         } else if (dst) {
-            for (uint64_t o = 16 * (uint64_t)t; o < n; o += 16 * TPB) {
+            for (uint64_t o = 16 * (uint64_t)tl; live && o < n; o += 16 * GT) {
                 const u32x4 v = zf::load16_masked(src, o, n);
                 uint8_t *p = dst + chunk_stream_off(o / 1024, N) + o % 1024;
                 if (o + 16 <= n) store16_a8<false>(p, v);
@@ -178,8 +184,8 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
             }
         }
     } else {
-        if (t == 0 && *reinterpret_cast<const uint64_t *>(src) != n) ok = false;
-        for (uint64_t o = 16 * (uint64_t)t; o < a.out_limit; o += 16 * TPB) {
+        if (live && tl == 0 && *reinterpret_cast<const uint64_t *>(src) != n) ok = false;
+        for (uint64_t o = 16 * (uint64_t)tl; live && o < a.out_limit; o += 16 * GT) {
             const uint8_t *p = src + chunk_stream_off(o / 1024, N) + o % 1024;
             const uint64_t left = a.out_limit - o;
             if (left >= 16) {
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
     const uint32_t iv0 = q == 0 ? IV(0) : q == 1 ? IV(1) : q == 2 ? IV(2) : IV(3);
     const uint32_t iv1 = q == 0 ? IV(4) : q == 1 ? IV(5) : q == 2 ? IV(6) : IV(7);
     const bool content_in = MODE == 0 && a.C == 0;  // encode of the content: read it where it is
-    for (uint64_t c = g; c < N; c += QUADS) {
+    for (uint64_t c = gl; live && c < N; c += GQ) {
         const uint64_t rem = n - c * 1024;
         const uint32_t clen = n == 0 ? 0u : (rem < 1024 ? (uint32_t)rem : 1024u);
         const uint32_t nb = clen == 0 ? 1u : (clen + 63) / 64;
@@ -233,8 +239,8 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
                 ok &= hp[q] == h0 && hp[4 + q] == h1;
             }
         } else {
-            cvs[0][c][q] = h0;
-            cvs[0][c][4 + q] = h1;
+            cvs[0][cb + c][q] = h0;
+            cvs[0][cb + c][4 + q] = h1;
         }
     }
     __syncthreads();
@@ -244,14 +250,14 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
     uint64_t cnt_prev = N;
     for (int level = 1; cnt_prev > 1; ++level) {
         const uint64_t cnt = (cnt_prev + 1) / 2;
-        for (uint64_t p = g; p < cnt; p += QUADS) {
+        for (uint64_t p = gl; live && p < cnt; p += GQ) {
             if (2 * p + 1 >= cnt_prev) {  // odd last node: promoted unchanged
-                cvs[cur ^ 1][p][q] = cvs[cur][2 * p][q];
-                cvs[cur ^ 1][p][4 + q] = cvs[cur][2 * p][4 + q];
+                cvs[cur ^ 1][cb + p][q] = cvs[cur][cb + 2 * p][q];
+                cvs[cur ^ 1][cb + p][4 + q] = cvs[cur][cb + 2 * p][4 + q];
                 continue;
             }
             // message = left CV || right CV: my 16 B are words 4q..4q+3
-            const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cvs[cur][2 * p + (q >> 1)][4 * (q & 1)]);
+            const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cvs[cur][cb + 2 * p + (q >> 1)][4 * (q & 1)]);
             *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = mw;
             wave_sync();
             const bool root = cnt == 1;
@@ -274,15 +280,15 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
                     ok &= hp[q] == h0 && hp[4 + q] == h1;
                 }
             } else {
-                cvs[cur ^ 1][p][q] = h0;
-                cvs[cur ^ 1][p][4 + q] = h1;
+                cvs[cur ^ 1][cb + p][q] = h0;
+                cvs[cur ^ 1][cb + p][4 + q] = h1;
             }
         }
         __syncthreads();
         cur ^= 1;
         cnt_prev = cnt;
     }
-    if (MODE == 1 && !ok) flag_mismatch(a.status, obj);
+    if (MODE == 1 && live && !ok) flag_mismatch(a.status, obj);
 }
 
 bool enabled() {
@@ -293,11 +299,13 @@ bool enabled() {
     return on;
 }
 
-hipError_t launch(int mode, const SmallArgs &a, hipStream_t stream) {
+hipError_t launch(int mode, SmallArgs a, hipStream_t stream) {
     if (a.count == 0) return hipSuccess;
     if (a.count > 0x7fffffffull) return hipErrorInvalidValue;
     const bool tiny = a.N <= (uint64_t)TINY_N && a.count > 1;
-    const dim3 grid((unsigned)a.count);
+    a.per = 1;  // tiny objects: as many per workgroup as fill its 16 quads
+    while (tiny && a.per * 2 * a.N <= (uint64_t)(TINY_TPB / 4) && a.per * 2 <= a.count) a.per *= 2;
+    const dim3 grid((unsigned)((a.count + a.per - 1) / a.per));
     if (tiny) {
         if (mode == 0) hipLaunchKernelGGL((small_kernel<0, TINY_TPB, TINY_N>), grid, dim3(TINY_TPB), 0, stream, a);
         else hipLaunchKernelGGL((small_kernel<1, TINY_TPB, TINY_N>), grid, dim3(TINY_TPB), 0, stream, a);
