@@ -20,6 +20,7 @@
 // (AES-NI/VAES GCM, EC arithmetic); both values the reference draws from its
 // RNG can be injected for bit-exact tests.
 #include "host_stages.hpp"
+#include "secp256k1_host.hpp"
 
 #include <openssl/ec.h>
 #include <openssl/evp.h>
@@ -444,10 +445,6 @@ EC_POINT *parse_public(const uint8_t *pk, uint64_t len) {
     return pt;
 }
 
-bool point65(const EC_POINT *pt, uint8_t out[65]) {
-    return EC_POINT_point2oct(ec().g, pt, POINT_CONVERSION_UNCOMPRESSED, out, 65, ec().bn) == 65;
-}
-
 // HKDF-SHA256 (RFC 5869) with no salt and no info, 32-byte output: one HMAC
 // for the extract step, one for T(1).
 bool hkdf_sha256_32(const uint8_t *ikm, size_t n, uint8_t out[32]) {
@@ -463,14 +460,29 @@ bool hkdf_sha256_32(const uint8_t *ikm, size_t n, uint8_t out[32]) {
     return true;
 }
 
-// encapsulate / decapsulate: key = HKDF(eph_pub65 || (peer * secret)65)
+// k * G as 0x04 || x || y (secp256k1_host.hpp: constant time, ~25x OpenSSL's
+// generic ladder for this curve)
+bool mul_g65(const BIGNUM *k, uint8_t out[65]) {
+    uint8_t kb[32];
+    if (BN_bn2binpad(k, kb, 32) != 32) return false;
+    const bool ok = k1::to65(k1::mul_g(kb), out);
+    OPENSSL_cleanse(kb, sizeof kb);
+    return ok;
+}
+
+// encapsulate / decapsulate: key = HKDF(eph_pub65 || (peer * secret)65).  The
+// peer was parsed and checked to lie on the curve by OpenSSL (parse_public).
 bool derive_key(const BIGNUM *secret, const EC_POINT *peer, const uint8_t eph_pub[65], uint8_t key[32]) {
-    PtPtr shared(EC_POINT_new(ec().g));
-    if (!shared.p || EC_POINT_mul(ec().g, shared.p, nullptr, peer, secret, ec().bn) != 1) return false;
+    uint8_t kb[32], xb[32], yb[32];
+    BnPtr x(BN_new()), y(BN_new());
+    if (!x.p || !y.p || EC_POINT_get_affine_coordinates(ec().g, peer, x.p, y.p, ec().bn) != 1 ||
+        BN_bn2binpad(x.p, xb, 32) != 32 || BN_bn2binpad(y.p, yb, 32) != 32 || BN_bn2binpad(secret, kb, 32) != 32)
+        return false;
     uint8_t master[130];
     std::memcpy(master, eph_pub, 65);
-    if (!point65(shared.p, master + 65)) return false;
-    const bool ok = hkdf_sha256_32(master, 130, key);
+    bool ok = k1::to65(k1::mul(kb, k1::fe_from_be(xb), k1::fe_from_be(yb)), master + 65);
+    OPENSSL_cleanse(kb, sizeof kb);
+    ok = ok && hkdf_sha256_32(master, 130, key);
     OPENSSL_cleanse(master, sizeof master);
     return ok;
 }
@@ -498,9 +510,7 @@ bool gcm_update(EVP_CIPHER_CTX *c, bool enc, const uint8_t *in, uint64_t n, uint
 int ecies_public_key(const uint8_t *secret, uint8_t out[65]) {
     BnPtr k(parse_secret(secret, 32));
     if (!k.p) return CHIP_ERR_ECIES;
-    PtPtr pub(EC_POINT_new(ec().g));
-    if (!pub.p || EC_POINT_mul(ec().g, pub.p, k.p, nullptr, nullptr, ec().bn) != 1 || !point65(pub.p, out))
-        return CHIP_ERR_ECIES;
+    if (!mul_g65(k.p, out)) return CHIP_ERR_ECIES;
     return CHIP_OK;
 }
 
@@ -522,9 +532,7 @@ int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph
     BnPtr k(parse_secret(sk, 32));
     OPENSSL_cleanse(sk, 32);
     if (!k.p) return CHIP_ERR_ECIES;
-    PtPtr eph(EC_POINT_new(ec().g));
-    if (!eph.p || EC_POINT_mul(ec().g, eph.p, k.p, nullptr, nullptr, ec().bn) != 1 || !point65(eph.p, out))
-        return CHIP_ERR_ECIES;
+    if (!mul_g65(k.p, out)) return CHIP_ERR_ECIES;
     uint8_t key[32];
     if (!derive_key(k.p, peer.p, out, key)) return CHIP_ERR_ECIES;
 

@@ -310,3 +310,30 @@ def test_null_output_sizes_without_writing(ca):
     e = ca.encoding.ecies(pk, ca.encoding.snap(d))
     rc, need = _chip_decode_raw(sk, e, 3, None, 1 << 20)
     assert rc == 2 and need == len(d)  # CHIP_ERR_BUFFER_TOO_SMALL
+
+
+def test_secp256k1_scalar_mult_matches_oracles(ca):
+    """The ECIES stage's constant-time secp256k1 (csrc/secp256k1_host.hpp):
+    k*G (public_key) and k*P (the ECDH inside encrypt/decrypt) against the
+    C oracle's Jacobian code and the Python restatement, for edge scalars and
+    random ones."""
+    from oracle import oracle as O
+    n = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+    edge = [1, 2, 3, 15, 16, 17, 255, 256, 2**128, 2**255, n - 1, n - 2, n // 2]
+    rng = np.random.default_rng(77)
+    rand = [int.from_bytes(rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), "big") % (n - 1) + 1
+            for _ in range(60)]
+    for k in edge + rand:
+        sk = k.to_bytes(32, "big")
+        assert ca.encoding.public_key(sk) == O.c_public_key(sk), hex(k)
+    for k in edge[:6] + rand[:4]:
+        assert ca.encoding.public_key(k.to_bytes(32, "big")) == H.public_key(k.to_bytes(32, "big"))
+    # k * P through ECIES: random receivers and ephemeral keys, against the C oracle's envelope
+    for i in range(12):
+        sk = rand[i].to_bytes(32, "big")
+        eph = (edge[i] if i < len(edge) else rand[-i]).to_bytes(32, "big")
+        pub = O.c_public_key(sk)
+        nonce = bytes(range(16))
+        e = ca.encoding.ecies(pub, b"m" * i, ephemeral_sk=eph, nonce=nonce)
+        assert e == O.c_ecies_encrypt(pub, b"m" * i, eph, nonce)
+        assert ca.decoding.ecies(e, sk) == b"m" * i
