@@ -23,6 +23,7 @@
 #include <cstring>
 #include <vector>
 
+#include "secp256k1_host.hpp"
 #include "../../include/carbonado_hip.h"
 
 namespace {
@@ -103,6 +104,19 @@ bool xy(const EC_POINT *pt, uint8_t x32[32], bool *even) {
     return bn32(x.v, x32);
 }
 
+// k * G (secp256k1_host.hpp: constant time; OpenSSL's generic-curve ladder
+// was ~5x slower): affine x and whether y is even
+bool mul_g_xy(const BIGNUM *k, uint8_t x32[32], bool *even) {
+    uint8_t kb[32], o[65];
+    if (!bn32(k, kb)) return false;
+    const bool ok = chip::k1::to65(chip::k1::mul_g(kb), o);
+    OPENSSL_cleanse(kb, sizeof kb);
+    if (!ok) return false;
+    std::memcpy(x32, o + 1, 32);
+    *even = !(o[64] & 1);
+    return true;
+}
+
 // a secret key as the reference accepts it (SecretKey::from_slice): 32 bytes, 0 < d < n
 bool parse_secret(const uint8_t *sk, uint64_t len, Bn &d) {
     if (!sk || len != 32) return false;
@@ -134,11 +148,9 @@ int schnorr_sign(const uint8_t sk[32], const uint8_t msg[32], const uint8_t *aux
     uint8_t aux[32];
     if (aux_in) std::memcpy(aux, aux_in, 32);
     else if (RAND_bytes(aux, 32) != 1) return CHIP_ERR_SECP256K1;
-    Pt P;
     uint8_t px[32], dd[32], t[32], rnd[32], rx[32], e32[32];
     bool even = false;
-    if (EC_POINT_mul(ctx().g, P.v, d0.v, nullptr, nullptr, ctx().bn) != 1 || !xy(P.v, px, &even))
-        return CHIP_ERR_SECP256K1;
+    if (!mul_g_xy(d0.v, px, &even)) return CHIP_ERR_SECP256K1;
     Bn d;
     if (even) BN_copy(d.v, d0.v);
     else BN_sub(d.v, order(), d0.v);
@@ -148,10 +160,8 @@ int schnorr_sign(const uint8_t sk[32], const uint8_t msg[32], const uint8_t *aux
     Bn k0(rnd), k, e, s;
     BN_mod(k0.v, k0.v, order(), ctx().bn);
     if (BN_is_zero(k0.v)) return CHIP_ERR_SECP256K1;
-    Pt R;
     bool reven = false;
-    if (EC_POINT_mul(ctx().g, R.v, k0.v, nullptr, nullptr, ctx().bn) != 1 || !xy(R.v, rx, &reven))
-        return CHIP_ERR_SECP256K1;
+    if (!mul_g_xy(k0.v, rx, &reven)) return CHIP_ERR_SECP256K1;
     if (reven) BN_copy(k.v, k0.v);
     else BN_sub(k.v, order(), k0.v);
     if (!tagged("BIP0340/challenge", rx, 32, px, 32, msg, 32, e32)) return CHIP_ERR_SECP256K1;
@@ -178,14 +188,22 @@ int schnorr_verify_x(const uint8_t x32[32], const uint8_t msg[32], const uint8_t
     if (!tagged("BIP0340/challenge", sig, 32, x32, 32, msg, 32, e32)) return CHIP_ERR_SECP256K1;
     BN_bin2bn(e32, 32, e.v);
     BN_mod(e.v, e.v, order(), ctx().bn);
-    // R = s G - e P
+    // R = s G - e P = s G + (n - e) P (public values); R must not be infinity,
+    // must have an even y and x = r
     Bn ne;
     BN_sub(ne.v, order(), e.v);
-    Pt R;
+    uint8_t sb[32], nb[32], xb[32], yb[32], o[65];
     bool even = false;
-    if (EC_POINT_mul(ctx().g, R.v, s.v, P.v, ne.v, ctx().bn) != 1 || EC_POINT_is_at_infinity(ctx().g, R.v) ||
-        !xy(R.v, rx, &even) || !even || std::memcmp(rx, sig, 32) != 0)
-        return CHIP_ERR_SECP256K1;
+    if (!bn32(s.v, sb) || !bn32(ne.v, nb) || !xy(P.v, xb, &even)) return CHIP_ERR_SECP256K1;
+    {
+        Bn x, y;
+        if (EC_POINT_get_affine_coordinates(ctx().g, P.v, x.v, y.v, ctx().bn) != 1 || !bn32(y.v, yb))
+            return CHIP_ERR_SECP256K1;
+    }
+    namespace k1 = chip::k1;
+    const k1::Pt R = k1::pt_add(k1::mul_g(sb), k1::mul(nb, k1::fe_from_be(xb), k1::fe_from_be(yb)));
+    if (!k1::to65(R, o) || (o[64] & 1) || std::memcmp(o + 1, sig, 32) != 0) return CHIP_ERR_SECP256K1;
+    (void)rx;
     return CHIP_OK;
 }
 
@@ -309,10 +327,9 @@ int chip_file_encode(const uint8_t *sk, uint64_t sk_len, const uint8_t *pk, uint
         if (!parse_public(pk, pk_len, P) || !compressed(P.v, pub)) return CHIP_ERR_SECP256K1;
     } else {
         Bn d;
-        Pt P;
-        if (!parse_secret(sk, sk_len, d) || EC_POINT_mul(ctx().g, P.v, d.v, nullptr, nullptr, ctx().bn) != 1 ||
-            !compressed(P.v, pub))
-            return CHIP_ERR_SECP256K1;
+        bool even = false;
+        if (!parse_secret(sk, sk_len, d) || !mul_g_xy(d.v, pub + 1, &even)) return CHIP_ERR_SECP256K1;
+        pub[0] = even ? 0x02 : 0x03;
     }
     uint64_t max = chip_encode_max_len(n);
     if (!out || cap < CHIP_HEADER_LEN) {
