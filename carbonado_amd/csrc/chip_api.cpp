@@ -1329,8 +1329,11 @@ int chip_blake3(const uint8_t *in, uint64_t n, uint8_t hash[CHIP_HASH_LEN]) {
 }
 
 // verify-decode a device-resident stream of `len` bytes; content -> dst (device)
+// `deferred` non-null: the status word lands there at the caller's next
+// small_sync (one synchronisation for the verdict and the content copy; the
+// caller wipes what it copied out if the verdict is a mismatch)
 static int bao_decode_ctx(Ctx *c, const uint8_t *d_enc, uint64_t len, uint64_t n, const uint8_t *hash,
-                          uint8_t *d_dst, uint64_t out_limit = ~0ull) {
+                          uint8_t *d_dst, uint64_t out_limit = ~0ull, uint32_t *deferred = nullptr) {
     (void)len;
     CHIP_HIP(grow(c->scratch, bao_scratch_len(n, 1)));
     CHIP_HIP(grow(c->small, 64));
@@ -1344,6 +1347,11 @@ static int bao_decode_ctx(Ctx *c, const uint8_t *d_enc, uint64_t len, uint64_t n
                                        c->stream));
     else
         CHIP_HIP(bao_decode_dev(d_enc, 0, n, 1, d_hash, d_dst, 0, d_status, c->scratch.p, c->stream));
+    if (deferred) {
+        *deferred = 0;
+        CHIP_HIP(small_d2h(c, deferred, d_status, 4));
+        return CHIP_OK;
+    }
     uint32_t status = 0;
     CHIP_HIP(small_d2h(c, &status, d_status, 4));
     CHIP_HIP(small_sync(c));
@@ -1375,11 +1383,16 @@ int chip_bao_decode(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint6
     CHIP_HIP(grow(c->in, blen));
     CHIP_HIP(grow(c->out, n));
     CHIP_HIP(h2d(c->stage, c->in.p, enc, blen, c->stream));
+    uint32_t verdict = 0;
     st = bao_decode_ctx(c, static_cast<const uint8_t *>(c->in.p), blen, n, hash,
-                        static_cast<uint8_t *>(c->out.p));
+                        static_cast<uint8_t *>(c->out.p), ~0ull, &verdict);
     if (st != CHIP_OK) return st;
     if (n) CHIP_HIP(d2h(c->stage, out, c->out.p, n, c->stream));
     CHIP_HIP(small_sync(c));
+    if (verdict) {  // never hand back unverified content
+        if (n) std::memset(out, 0, n);
+        return (int)verdict;
+    }
     *out_len = n;
     return CHIP_OK;
 }
@@ -2264,15 +2277,16 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         CHIP_HIP(grow(c->in, in_bytes));
         if (in_bytes) CHIP_HIP(h2d(c->stage, c->in.p, in, in_bytes, c->stream));
         const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
+        uint32_t verdict = 0;  // bao's, read at the synchronisation below
         if (bao && zfec) {  // decoding.rs:89-99: the positional shares' primaries are the content's
             // first 4 C bytes, so zfec's decode is the prefix: verify all, write olen bytes
             CHIP_HIP(grow(c->mid, olen));
-            st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p), olen);
+            st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p), olen, &verdict);
             if (st != CHIP_OK) return st;
             d_cur = static_cast<const uint8_t *>(c->mid.p);
         } else if (bao) {  // decoding.rs:89-93
             CHIP_HIP(grow(c->mid, blen));
-            st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p));
+            st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p), ~0ull, &verdict);
             if (st != CHIP_OK) return st;
             d_cur = static_cast<const uint8_t *>(c->mid.p);
         }
@@ -2288,6 +2302,10 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         }
         if (olen) CHIP_HIP(d2h(c->stage, dst, d_cur, olen, c->stream));
         CHIP_HIP(small_sync(c));
+        if (verdict) {  // never hand back unverified content
+            if (olen) std::memset(dst, 0, olen);
+            return (int)verdict;
+        }
         cur = dst;
         cur_n = olen;
     }

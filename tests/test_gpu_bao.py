@@ -180,3 +180,29 @@ def test_batch_bao_content_mode_tail(gpu, n):
         assert hashes[o].cpu().numpy().tobytes() == oh, o
         assert host[o, :blen].tobytes() == oe, o
         assert (host[o, blen:] == 0xA5).all(), o
+
+
+@pytest.mark.parametrize("n", [3000, 200_000])
+def test_bao_decode_mismatch_leaves_no_content(gpu, n):
+    """chip_bao_decode reads the verdict and copies the content out behind one
+    synchronisation; on a mismatch the caller's buffer is wiped, never left
+    holding unverified bytes (KS for 3000 B, the batch kernels for 200 KB)."""
+    import ctypes
+    import numpy as np
+    from carbonado_amd import _lib
+    L = _lib.lib()
+    d = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+    enc, h = O.bao_encode(d)
+    bad = bytearray(enc)
+    bad[-3] ^= 0x20
+    bad = np.frombuffer(bytes(bad), np.uint8)
+    out = np.full(n, 0xAA, np.uint8)
+    hh = np.frombuffer(h, np.uint8)
+    olen = ctypes.c_uint64()
+    rc = L.chip_bao_decode(bad.ctypes.data, bad.size, hh.ctypes.data, 32, out.ctypes.data, out.size,
+                           ctypes.byref(olen))
+    assert rc == 5 and not out.any()
+    good = np.frombuffer(enc, np.uint8)
+    rc = L.chip_bao_decode(good.ctypes.data, good.size, hh.ctypes.data, 32, out.ctypes.data, out.size,
+                           ctypes.byref(olen))
+    assert rc == 0 and olen.value == n and out.tobytes() == d
