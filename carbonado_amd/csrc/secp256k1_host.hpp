@@ -32,7 +32,6 @@
 
 #include <cstdint>
 #include <cstring>
-#include <mutex>
 
 namespace chip {
 namespace k1 {
@@ -50,7 +49,7 @@ constexpr uint64_t P0 = 0xFFFFFFFEFFFFFC2Full, P1 = ~0ull, P2 = ~0ull, P3 = ~0ul
 // x86-64 add/sub-with-carry intrinsics (plain __int128 shifts compiled to a
 // slow serial chain: 41 ns per addition).
 inline void fe_reduce5(const uint64_t r[4], uint64_t hi, Fe &out) {
-    unsigned long long a0, a1, a2, a3, lo;
+    unsigned long long a0, a1, a2, a3;
     const u128 m = (u128)hi * RC;
     unsigned char c = _addcarry_u64(0, r[0], (uint64_t)m, &a0);
     c = _addcarry_u64(c, r[1], (uint64_t)(m >> 64), &a1);
@@ -72,7 +71,6 @@ inline void fe_reduce5(const uint64_t r[4], uint64_t hi, Fe &out) {
     out.v[1] = (a1 & keep) | (s1 & ~keep);
     out.v[2] = (a2 & keep) | (s2 & ~keep);
     out.v[3] = (a3 & keep) | (s3 & ~keep);
-    (void)lo;
 }
 
 inline Fe fe_mul(const Fe &a, const Fe &b) {
