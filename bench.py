@@ -22,6 +22,7 @@ Rank 0 prints one JSON line (metric/value/unit/... + roofline + cpu_baseline).
 from __future__ import annotations
 
 import argparse
+import datetime
 import ctypes
 import json
 import os
@@ -759,7 +760,7 @@ class Workload:
 
     def _scatter_inputs(self, rank: int, world: int) -> float:
         """Rank 0 generates all world*count objects and scatters them (RCCL)."""
-        grp = dist.new_group(backend="nccl")
+        grp = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))  # a stuck collective ends the run, not the node's slot
         full = None
         if rank == 0:
             full = torch.empty((world * self.count, self.n), dtype=torch.uint8, device=self.dev)
@@ -780,7 +781,7 @@ class Workload:
         once, timed between barriers; the inputs of the timed steps are
         generated on each rank, so this only shows RCCL seeing N ranks and
         the per-link rate of the input-staging collective."""
-        grp = dist.new_group(backend="nccl")
+        grp = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))  # a stuck collective ends the run, not the node's slot
         per = int(gib * 2**30)
         local = torch.empty(per, dtype=torch.uint8, device=self.dev)
         chunks = None
