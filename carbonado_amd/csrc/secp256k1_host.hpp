@@ -161,15 +161,29 @@ inline Fe fe_mul21(const Fe &a) {  // b3 = 3 * 7
     return out;
 }
 
-// a^(p-2) (a != 0): the exponent is public, so its bits may steer the loop
+inline Fe fe_sqr_n(Fe a, int n) {
+    for (int i = 0; i < n; ++i) a = fe_sqr(a);
+    return a;
+}
+
+// a^(p-2) (a != 0) by the addition chain over the blocks of ones of p - 2
+// (lengths 1, 2, 22 and 223): 255 squarings and 15 multiplications
 inline Fe fe_inv(const Fe &a) {
-    const uint64_t e[4] = {P0 - 2, P1, P2, P3};
-    Fe r = {{1, 0, 0, 0}};
-    for (int i = 255; i >= 0; --i) {
-        r = fe_sqr(r);
-        if ((e[i / 64] >> (i % 64)) & 1) r = fe_mul(r, a);
-    }
-    return r;
+    const Fe x2 = fe_mul(fe_sqr(a), a);
+    const Fe x3 = fe_mul(fe_sqr(x2), a);
+    const Fe x6 = fe_mul(fe_sqr_n(x3, 3), x3);
+    const Fe x9 = fe_mul(fe_sqr_n(x6, 3), x3);
+    const Fe x11 = fe_mul(fe_sqr_n(x9, 2), x2);
+    const Fe x22 = fe_mul(fe_sqr_n(x11, 11), x11);
+    const Fe x44 = fe_mul(fe_sqr_n(x22, 22), x22);
+    const Fe x88 = fe_mul(fe_sqr_n(x44, 44), x44);
+    const Fe x176 = fe_mul(fe_sqr_n(x88, 88), x88);
+    const Fe x220 = fe_mul(fe_sqr_n(x176, 44), x44);
+    const Fe x223 = fe_mul(fe_sqr_n(x220, 3), x3);
+    Fe t = fe_mul(fe_sqr_n(x223, 23), x22);
+    t = fe_mul(fe_sqr_n(t, 5), a);
+    t = fe_mul(fe_sqr_n(t, 3), x2);
+    return fe_mul(fe_sqr_n(t, 2), a);
 }
 
 inline Fe fe_from_be(const uint8_t b[32]) {
