@@ -149,3 +149,46 @@ def test_tiny_batches(gpu, level, n):
     for i in range(count):
         if i != 4:
             assert bytes(dec[i, :n].cpu().numpy()) == objs[i], i
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_tiny_batches_randomized(gpu, seed):
+    """Seeded random batches for the tiny-object path (several objects per
+    workgroup when N <= 8, one per workgroup up to N = 64, the batch kernels
+    above): random sizes, counts, levels and a random set of tampered
+    objects; every object's encoding against the oracle, every decode status
+    and the intact objects' bytes."""
+    import torch
+    from carbonado_amd import device as D
+    rng = np.random.default_rng(1000 + seed)
+    level = int(rng.choice([4, 12]))
+    n = int(rng.integers(0, (66 if level == 4 else 34) * 1024))
+    count = int(rng.integers(2, 41))
+    objs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for _ in range(count)]
+    stride = max(16, (n + 15) // 16 * 16)
+    inp = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    for i, o in enumerate(objs):
+        if n:
+            inp[i, :n] = torch.frombuffer(bytearray(o), dtype=torch.uint8).cuda()
+    oenc0 = O.encode(objs[0], level)[0]
+    olen = len(oenc0)
+    out = torch.zeros((count, (olen + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    _, info = D.encode_batch(level, inp, n, out, hashes, D.encode_scratch(level, n, count))
+    torch.cuda.synchronize()
+    for i in sorted({0, count - 1, int(rng.integers(0, count))}):
+        e, h, _ = O.encode(objs[i], level)
+        assert bytes(out[i, :olen].cpu().numpy()) == e and bytes(hashes[i].cpu().numpy()) == h, (n, count, i)
+    bad = out.clone()
+    hit = sorted(set(rng.integers(0, count, int(rng.integers(0, 4))).tolist()))
+    for i in hit:
+        bad[i, int(rng.integers(0, olen))] ^= int(rng.integers(1, 256))
+    dec = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    status = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    D.decode_batch(level, bad, olen, hashes, info.padding_len, dec, status, D.decode_scratch(level, olen, count))
+    torch.cuda.synchronize()
+    st = status.cpu().tolist()
+    for i in range(count):
+        assert st[i] == (5 if i in hit else 0), (n, count, i, st[i])
+        if i not in hit:
+            assert bytes(dec[i, :n].cpu().numpy()) == objs[i], (n, count, i)
