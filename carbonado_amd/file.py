@@ -137,6 +137,13 @@ def decode(secret_key: bytes, encoded) -> tuple[Header, bytes]:
     return Header._from_c(hdr), body
 
 
+def _host_buffer(shape):
+    """Pinned host memory for the PCIe stages (page-locked only where a device
+    exists; without one the device stage fails anyway)."""
+    import torch
+    return torch.empty(shape, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+
+
 def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None = None,
                  metadata: bytes | None = None, slice_objects: int = 64, host_threads: int = 16,
                  nslots: int = 3, io_threads: int = 8, fsync: bool = False, stats: dict | None = None) -> list:
@@ -177,9 +184,9 @@ def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None =
     cap = L.chip_encode_max_len(n)
     S = max(1, min(slice_objects, len(in_paths)))
     nbuf = 2
-    h_in = [torch.empty((S, max(n, 1)), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
-    h_out = [torch.empty((S, cap), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
-    h_hash = [torch.empty((S, 32), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
+    h_in = [_host_buffer((S, max(n, 1))) for _ in range(nbuf)]
+    h_out = [_host_buffer((S, cap)) for _ in range(nbuf)]
+    h_hash = [_host_buffer((S, 32)) for _ in range(nbuf)]
     slices = [list(range(i, min(i + S, len(in_paths)))) for i in range(0, len(in_paths), S)]
     results: list = [None] * len(in_paths)
     free_in, ready_in = queue.Queue(), queue.Queue()
@@ -188,6 +195,22 @@ def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None =
         free_in.put(b)
         free_out.put(b)
     errors = []
+    # Any stage that fails sets `stop`; every wait below is a timed get that
+    # gives up once `stop` is set, so no stage can wait forever on a buffer a
+    # failed stage will never hand back.
+    stop = threading.Event()
+
+    def fail(e):
+        errors.append(e)
+        stop.set()
+
+    def get(q):
+        while True:
+            try:
+                return q.get(timeout=0.05)
+            except queue.Empty:
+                if stop.is_set():
+                    return None
 
     rpool, wpool = ThreadPoolExecutor(io_threads), ThreadPoolExecutor(io_threads)
     busy = {"read_s": 0.0, "device_s": 0.0, "write_s": 0.0}
@@ -216,7 +239,9 @@ def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None =
     def reader():
         try:
             for sl in slices:
-                b = free_in.get()
+                b = get(free_in)
+                if b is None:
+                    return
                 t0 = time.perf_counter()
                 buf = h_in[b].numpy()
                 for fut in [rpool.submit(read_one, buf, j, o) for j, o in enumerate(sl)]:
@@ -224,48 +249,58 @@ def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None =
                 busy["read_s"] += time.perf_counter() - t0
                 ready_in.put((b, sl))
         except BaseException as e:  # noqa: BLE001
-            errors.append(e)
+            fail(e)
+        finally:
             ready_in.put(None)
 
     def writer():
-        try:
-            while True:
-                item = ready_out.get()
-                if item is None:
-                    return
-                b, sl, olens, infos = item
-                t0 = time.perf_counter()
-                out, hashes = h_out[b].numpy(), h_hash[b].numpy()
-                for fut in [wpool.submit(write_one, out, hashes, olens, infos, j, o) for j, o in enumerate(sl)]:
-                    fut.result()
-                busy["write_s"] += time.perf_counter() - t0
-                free_out.put(b)
-        except BaseException as e:  # noqa: BLE001
-            errors.append(e)
-            while ready_out.get() is not None:
-                pass
+        while True:
+            item = get(ready_out)
+            if item is None:  # end of the batch, or a stage failed
+                return
+            b, sl, olens, infos = item
+            try:
+                if not stop.is_set():
+                    t0 = time.perf_counter()
+                    out, hashes = h_out[b].numpy(), h_hash[b].numpy()
+                    for fut in [wpool.submit(write_one, out, hashes, olens, infos, j, o) for j, o in enumerate(sl)]:
+                        fut.result()
+                    busy["write_s"] += time.perf_counter() - t0
+            except BaseException as e:  # noqa: BLE001
+                fail(e)
+            finally:
+                free_out.put(b)  # always returned, also while draining after a failure
 
     tr, tw = threading.Thread(target=reader), threading.Thread(target=writer)
     tr.start()
     tw.start()
     try:
         for _ in slices:
-            item = ready_in.get()
+            item = None if stop.is_set() else get(ready_in)
             if item is None:
                 break
             b, sl = item
-            ob = free_out.get()
+            ob = get(free_out)
+            if ob is None:
+                break
             cnt = len(sl)
             t0 = time.perf_counter()
-            olens, infos = device.encode_host_batch(level, h_in[b][:cnt], n, h_out[ob][:cnt], h_hash[ob][:cnt],
-                                                    nslots, pubkey=pk, host_threads=host_threads)
+            try:
+                olens, infos = device.encode_host_batch(level, h_in[b][:cnt], n, h_out[ob][:cnt], h_hash[ob][:cnt],
+                                                        nslots, pubkey=pk, host_threads=host_threads)
+            except BaseException as e:  # noqa: BLE001
+                fail(e)
+                break
             busy["device_s"] += time.perf_counter() - t0
             free_in.put(b)
             ready_out.put((ob, sl, olens, infos))
     finally:
         ready_out.put(None)
-        tr.join()
+        if errors:
+            stop.set()
         tw.join()
+        stop.set()  # the writer has finished: release a reader still waiting for a buffer
+        tr.join()
         rpool.shutdown()
         wpool.shutdown()
     if errors:

@@ -143,3 +143,98 @@ def test_file_encode_given_pubkey_and_metadata(ca):
     out, _ = file.encode(sk, H.public_key(other_sk), b"Hello world!", 3)
     with pytest.raises(Secp256k1Error):
         file.decode(other_sk, out)
+
+
+def _fake_device(fail_at=None):
+    """Stand-in for device.encode_host_batch (no GPU here): copies each input
+    into its output row; raises on slice number `fail_at`."""
+    from carbonado_amd.structs import EncodeInfo
+    calls = []
+
+    def f(level, inp, n, out, hashes, nslots, pubkey=b"", host_threads=0):
+        calls.append(inp.shape[0])
+        if fail_at is not None and len(calls) - 1 == fail_at:
+            raise RuntimeError("device stage failed")
+        cnt = inp.shape[0]
+        out[:, :n] = inp[:, :n]
+        hashes.zero_()
+        hashes[:, 0] = len(calls)
+        hashes[:, 1] = __import__("torch").arange(cnt, dtype=__import__("torch").uint8)
+        infos = [EncodeInfo(n, n, 0, 0.0, 0, 0, 0, 0.0, 0, 0, 0, 0) for _ in range(cnt)]
+        return [n] * cnt, infos
+    return f, calls
+
+
+def _files(tmp_path, count, n=4096):
+    d = tmp_path / "in"
+    d.mkdir()
+    paths = []
+    for i in range(count):
+        p = d / f"f{i}"
+        p.write_bytes(bytes([i & 255]) * n)
+        paths.append(p)
+    return paths
+
+
+def test_encode_files_pipeline_ok(ca, tmp_path, monkeypatch):
+    """encode_files' three stages end to end with a stand-in device stage."""
+    from carbonado_amd import device, file
+    f, calls = _fake_device()
+    monkeypatch.setattr(device, "encode_host_batch", f)
+    paths = _files(tmp_path, 7)
+    out = tmp_path / "out"
+    out.mkdir()
+    sk = H.sha256(b"writer")
+    res = file.encode_files(paths, out, sk, 12, slice_objects=2, io_threads=2)
+    assert calls == [2, 2, 2, 1]
+    assert len(res) == 7 and all(r is not None for r in res)
+    for i, (p, info) in enumerate(res):
+        body = p.read_bytes()
+        assert body[file.HEADER_LEN:] == bytes([i & 255]) * 4096
+
+
+@pytest.mark.timeout(60)
+def test_encode_files_writer_error_raises(ca, tmp_path, monkeypatch):
+    """A failing write stage (out_dir is a file) with 3+ slices raises instead
+    of hanging (the writer never returned its buffers)."""
+    from carbonado_amd import device, file
+    f, _ = _fake_device()
+    monkeypatch.setattr(device, "encode_host_batch", f)
+    paths = _files(tmp_path, 9)
+    not_a_dir = tmp_path / "plainfile"
+    not_a_dir.write_bytes(b"x")
+    with pytest.raises(OSError):
+        file.encode_files(paths, not_a_dir, H.sha256(b"w"), 12, slice_objects=2, io_threads=2)
+
+
+@pytest.mark.timeout(60)
+@pytest.mark.parametrize("fail_at", [0, 2])
+def test_encode_files_device_error_raises(ca, tmp_path, monkeypatch, fail_at):
+    """A device stage that raises (first or a later slice) propagates, with
+    the reader and writer threads released (the reader blocked on a
+    buffer the main loop never returned)."""
+    from carbonado_amd import device, file
+    f, _ = _fake_device(fail_at)
+    monkeypatch.setattr(device, "encode_host_batch", f)
+    paths = _files(tmp_path, 9)
+    out = tmp_path / "out"
+    out.mkdir()
+    with pytest.raises(RuntimeError, match="device stage failed"):
+        file.encode_files(paths, out, H.sha256(b"w"), 12, slice_objects=2, io_threads=2)
+
+
+@pytest.mark.timeout(60)
+def test_encode_files_reader_error_raises(ca, tmp_path, monkeypatch):
+    """A short read (a file shrinks after the size check) raises."""
+    from carbonado_amd import device, file
+    f, _ = _fake_device()
+    monkeypatch.setattr(device, "encode_host_batch", f)
+    paths = _files(tmp_path, 9)
+    import pathlib
+    orig = pathlib.Path.stat
+    out = tmp_path / "out"
+    out.mkdir()
+    paths[5].write_bytes(b"")
+    monkeypatch.setattr(pathlib.Path, "stat", lambda self, *a, **k: orig(paths[0]) if self == paths[5] else orig(self, *a, **k))
+    with pytest.raises(IOError):
+        file.encode_files(paths, out, H.sha256(b"w"), 12, slice_objects=2, io_threads=2)
