@@ -105,7 +105,8 @@ def parse(argv=None):
                     help="pipeline mode: check EVERY object bit-exact (encode mode does by default): BLAKE3 of "
                          "each object's output on the GPU vs the C oracle's zfec (or encode()) + BLAKE3 on 16 host "
                          "threads, outside the timed region")
-    ap.add_argument("--no-verify-all", action="store_true", help="encode mode: check object 0 only")
+    ap.add_argument("--no-verify-all", action="store_true",
+                    help="encode / decode / e2e modes (which check every object by default): object 0 only")
     ap.add_argument("--no-aliased", action="store_true",
                     help="encode mode: skip the second, in-place (aliased data shards) measurement")
     ap.add_argument("--scatter", action="store_true",
@@ -134,7 +135,7 @@ def parse(argv=None):
         args.objects = 64  # host-API paths: a bounded host-memory working set
     if args.mode == "file" and args.objects == ap.get_default("objects"):
         args.objects = 128  # 2 GiB of input files + 2.1 GiB of output files on the box's disk
-    if args.mode != "encode":
+    if args.mode not in ("encode", "decode", "e2e"):
         args.no_verify_all = True
     return args
 
@@ -176,6 +177,13 @@ def gather_floats(value: float, world: int) -> list:
     out = [None] * world
     dist.all_gather_object(out, float(value))
     return [float(v) for v in out]
+
+
+def verify_threads(world: int) -> int:
+    """Host threads each rank may use for its checks: the ranks share the
+    host's CPUs (os.cpu_count() // world), at most 16 each (a GPU's share of
+    the box)."""
+    return max(1, min(16, (os.cpu_count() or 1) // max(1, world)))
 
 
 def barrier(world):
@@ -724,6 +732,7 @@ class Workload:
                                                     pubkey=self.pub, ephemeral_sk=self.eph, nonce=self.nonce,
                                                     host_threads=args.host_threads)
                 self.final_len = max(olens)
+                self.olens = olens
             self.step = step
             step()
             self.alg_bytes = count * (n + self.final_len)  # PCIe bytes: H2D input + D2H encoding
@@ -831,7 +840,14 @@ class Workload:
         BLAKE3 digests of the m shards (computed on the device by the bao
         kernels, hash-only) against oracle/carbonado_oracle.c's zfec + BLAKE3
         of the same inputs (ctypes releases the GIL: the checks run in
-        parallel on `threads` host threads)."""
+        parallel on `threads` host threads).  cfg3 (decode): every decoded
+        object equals its resident input, compared on the device.  cfg4
+        (e2e): every object's encoding in host memory equals the C oracle's
+        encode() (orc_encode_full with the same injected ECIES values)."""
+        if self.args.mode == "decode":
+            return self._verify_all_decode()
+        if self.args.mode == "e2e":
+            return self._verify_all_e2e(threads)
         from concurrent.futures import ThreadPoolExecutor
         from carbonado_amd import device
         from oracle import oracle as O
@@ -861,6 +877,50 @@ class Workload:
                 "how": (f"BLAKE3 of each object's level-{self.args.level} encoding on the GPU + its bao hash vs the "
                         f"oracle's encode() + BLAKE3 on {threads} threads" if pipeline else
                         f"BLAKE3 of each object's {m} shards on the GPU vs oracle zfec + BLAKE3 on {threads} threads")}
+
+    def _verify_all_decode(self):
+        """decoding::zfec of every object (decoding.rs:21-51): the k data
+        shards' first n bytes equal the object's input, both resident in HBM
+        (compared 64 objects at a time)."""
+        t0 = time.perf_counter()
+        n, bad = self.n, []
+        for o0 in range(0, self.count, 64):
+            o1 = min(self.count, o0 + 64)
+            diff = (self.out[o0:o1, :n] != self.inp[o0:o1, :n]).any(dim=1)
+            bad += [o0 + int(i) for i in torch.nonzero(diff).flatten().tolist()]
+        torch.cuda.synchronize()
+        return {"ok": not bad, "objects": self.count, "mismatched": bad[:16],
+                "seconds": round(time.perf_counter() - t0, 1),
+                "how": "every decoded object's n bytes vs its resident input, compared on the device"}
+
+    def _verify_all_e2e(self, threads: int):
+        """encode() of every object (encoding.rs:86-172) against the C oracle
+        on `threads` host threads: at levels with host stages
+        orc_encode_full with the object's injected ephemeral key and nonce
+        (host_oracle.c), else the device-stage oracle; bytes and hash."""
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import oracle as O
+        t0 = time.perf_counter()
+        lv, host_in = self.args.level, self.h_in.numpy()
+        out, hashes = self.h_out.numpy(), self.h_hash.numpy()
+
+        def check(o):
+            if lv & 3:
+                eph = self.eph[o].tobytes() if self.eph is not None else bytes(32)
+                nonce = self.nonce[o].tobytes() if self.nonce is not None else bytes(16)
+                enc, h, _ = O.c_encode_full(host_in[o].tobytes(), lv, self.pub, eph, nonce)
+            else:
+                enc, h, _ = O.encode(host_in[o].tobytes(), lv)
+            return (self.olens[o] == len(enc) and out[o, :len(enc)].tobytes() == enc and
+                    (not lv & 4 or hashes[o].tobytes() == h))
+        with ThreadPoolExecutor(threads) as ex:
+            oks = list(ex.map(check, range(self.count)))
+        bad = [o for o, ok in enumerate(oks) if not ok]
+        return {"ok": not bad, "objects": self.count, "mismatched": bad[:16],
+                "seconds": round(time.perf_counter() - t0, 1),
+                "how": (f"every object's level-{lv} encoding (host memory) and hash vs the C oracle's "
+                        f"{'orc_encode_full (same injected ECIES values)' if lv & 3 else 'encode()'} on "
+                        f"{threads} threads")}
 
     def time_aliased(self, steps: int, warmup: int, world: int):
         """the same encode with the data shards aliased (in
@@ -944,6 +1004,7 @@ class DryRun:
         self.kernel = self.kernel_sym = "dry-run"
         self.C = n // args.k
         self.scatter_s = None
+        self.alloc_info = {"in": {"classes_found": 0, "classes_used": 0, "alloc_s": 0.0, "rank": rank}}
 
     def time_steps(self, steps: int, warmup: int, world: int):
         barrier(world)
@@ -979,15 +1040,21 @@ def main():
     elapsed, launch_ms = wl.time_steps(args.steps, args.warmup, world)
     max_elapsed = max_over_ranks(elapsed)
     rank_avg_ms = gather_floats(sum(launch_ms) / len(launch_ms), world)
+    rank_alloc = [getattr(wl, "alloc_info", {})]
+    if world > 1:  # each rank's buffers' memory classes (placement differs per GPU)
+        rank_alloc = [None] * world
+        dist.all_gather_object(rank_alloc, getattr(wl, "alloc_info", {}))
 
     verified, sample = None, None
     if rank == 0 and not args.no_verify and not args.dry_run:
         verified, sample = wl.verify_object0()
     verified_all = None
-    want_all = (args.mode == "encode" and not args.no_verify_all) or (args.mode == "pipeline" and args.verify_all)
+    want_all = ((args.mode in ("encode", "decode", "e2e") and not args.no_verify_all) or
+                (args.mode == "pipeline" and args.verify_all))
     if want_all and not args.no_verify and not args.dry_run:
-        # every rank checks its own objects (N > 1: the whole global set), rank 0 reports
-        mine = wl.verify_all(threads=16)
+        # every rank checks its own objects (N > 1: the whole global set), rank 0 reports;
+        # the host threads are split over the ranks (16 per GPU is the box's CPU share)
+        mine = wl.verify_all(threads=verify_threads(world))
         if world > 1:
             every = [None] * world
             dist.all_gather_object(every, mine)
@@ -1017,6 +1084,9 @@ def main():
             traffic, traffic_src = measured_traffic(args.traffic_json, wl.kernel_sym, wl.alg_bytes)
             if live:
                 traffic_src = f"{traffic_src or 'none'} (live PMC failed: {live['error']})"
+            elif world > 1 and traffic_src:
+                traffic_src = (f"committed fallback {traffic_src}: the live PMC passes run at N=1 only (one "
+                               "profiled child per GPU would need every rank's GPU twice more)")
         if args.mode == "bao":
             workload = f"bao encode, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "bao-decode":
@@ -1121,6 +1191,10 @@ def main():
                                      "contiguous": "hipDeviceMallocContiguous (CHIP_ALLOC=contiguous)",
                                      "torch": "torch caching allocator (hipMalloc)"}[args.alloc],
                             "buffers": wl.alloc_info}
+            if world > 1:
+                res["alloc"]["buffers_by_rank"] = rank_alloc
+        if world > 1:
+            res["verify_threads_per_rank"] = verify_threads(world)
         if verified_all is not None:
             res["verified_all_objects"] = verified_all
         if aliased is not None:

@@ -956,6 +956,7 @@ int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     uint64_t C;
     calc_pad(n, k, &pad, &C);
     if (count > 1 && out_stride < (uint64_t)m * C) return CHIP_ERR_INVALID_ARG;
+    if (count > 1 && d_in != d_out && in_stride < n) return CHIP_ERR_INVALID_ARG;  // rows would overlap
     // in place (SURVEY 8d "aliased"): data shards are the input bytes themselves
     const bool aliased = d_in == d_out && n;
     if (aliased && count > 1 && in_stride != out_stride) return CHIP_ERR_INVALID_ARG;
@@ -1074,10 +1075,14 @@ int chip_zfec_decode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     if (st != CHIP_OK) return st;
     std::vector<uint32_t> sel(k);
     std::vector<uint64_t> slot_off(k);
+    uint64_t row_in = 0;
     for (uint32_t s = 0; s < k; ++s) {
         sel[s] = idx[pos[s]];
         slot_off[s] = (uint64_t)sel[s] * chunk_len;
+        row_in = std::max(row_in, slot_off[s] + chunk_len);
     }
+    // rows would overlap
+    if (count > 1 && (in_stride < row_in || out_stride < (uint64_t)k * chunk_len)) return CHIP_ERR_INVALID_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     int part_st = CHIP_OK;
     const hipError_t e = zf_run(count, s, [&](uint64_t o0, uint64_t cnt, hipStream_t st) {
@@ -1140,6 +1145,23 @@ int chip_device_alloc_info(const void *ptr, uint32_t *classes_found, uint32_t *c
     return CHIP_OK;
 }
 
+int chip_stream_queue_block(void *stream, uint64_t *addr) {
+    if (!addr) return CHIP_ERR_INVALID_ARG;
+    int st = use_device();
+    if (st != CHIP_OK) return st;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!s) {
+        Ctx *c = nullptr;
+        st = ctx_get(&c);
+        if (st != CHIP_OK) return st;
+        s = c->stream;
+    }
+    uint32_t *q = nullptr;
+    CHIP_HIP(chip::stream_queue(s, &q));
+    *addr = (uint64_t)(uintptr_t)q;
+    return CHIP_OK;
+}
+
 // torch.cuda.memory.CUDAPluggableAllocator hooks over chip_device_alloc/free
 void *chip_torch_alloc(ssize_t size, int device, void *stream) {
     (void)stream;
@@ -1159,6 +1181,7 @@ int chip_bao_encode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
                               uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash,
                               void *d_scratch, void *stream) {
     if ((!d_in && n) || !d_hash || !d_scratch) return CHIP_ERR_INVALID_ARG;
+    if (count > 1 && (in_stride < n || (d_out && out_stride < bao_encoded_len(n)))) return CHIP_ERR_INVALID_ARG;
     int st = use_device();
     if (st != CHIP_OK) return st;
     CHIP_HIP(bao_encode_dev(d_in, in_stride, n, count, d_out, out_stride, d_hash, d_scratch,
@@ -1170,6 +1193,7 @@ int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
                               const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride,
                               uint32_t *d_status, void *d_scratch, void *stream) {
     if (!d_in || !d_hash || !d_status || !d_scratch || (!d_out && n)) return CHIP_ERR_INVALID_ARG;
+    if (count > 1 && (in_stride < bao_encoded_len(n) || out_stride < n)) return CHIP_ERR_INVALID_ARG;
     int st = use_device();
     if (st != CHIP_OK) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1199,6 +1223,7 @@ int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_strid
     int st = encode_info_for(format, n, n, 0, 0, &inf, &zlen, &fl);
     if (st != CHIP_OK) return st;
     if ((fl && !d_out) || (count > 1 && out_stride < fl)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (count > 1 && in_stride < n) return CHIP_ERR_INVALID_ARG;  // rows would overlap
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
     if (bao && !d_scratch) return CHIP_ERR_INVALID_ARG;
     *out_len = fl;
@@ -1270,6 +1295,7 @@ int chip_decode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_strid
     *out_len = olen;
     if (count == 0) return CHIP_OK;
     if ((olen && !d_out) || (count > 1 && out_stride < olen)) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (count > 1 && in_stride < in_len) return CHIP_ERR_INVALID_ARG;  // rows would overlap
     int st = use_device();
     if (st != CHIP_OK) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1681,18 +1707,22 @@ int chip_scrub_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t len, 
         }
         // re-encode (decoding.rs:191-196): encode() at Zfec|Bao of every decoded object, one fused pass
         CHIP_HIP(zfec_bao_dev(d_dec, kc, kc - padding, R, C2, d_enc, lstride, d_h2, c->scratch.p, c->stream));
-        for (size_t j = 0; j < R; ++j)
-            CHIP_HIP(hipMemcpyAsync(d_out + reps[g0 + j].o * out_stride, d_enc + j * lstride, len,
-                                    hipMemcpyDeviceToDevice, c->stream));
         std::vector<uint8_t> h2(32 * R);
         CHIP_HIP(small_d2h(c, h2.data(), d_h2, h2.size()));
         CHIP_HIP(small_sync(c));
         for (size_t j = 0; j < R; ++j) {  // decoding.rs:205-207
             const uint64_t o = reps[g0 + j].o;
-            status[o] = std::memcmp(h2.data() + 32 * j, want.data() + 32 * o, 32) ? CHIP_ERR_INVALID_SCRUBBED_HASH
-                                                                                 : CHIP_OK;
+            const bool ok = std::memcmp(h2.data() + 32 * j, want.data() + 32 * o, 32) == 0;
+            status[o] = ok ? CHIP_OK : CHIP_ERR_INVALID_SCRUBBED_HASH;
+            // only a repaired stream whose hash matches is handed out, as
+            // chip_scrub (the next group's work is behind these copies on the
+            // same stream)
+            if (ok)
+                CHIP_HIP(hipMemcpyAsync(d_out + o * out_stride, d_enc + j * lstride, len, hipMemcpyDeviceToDevice,
+                                        c->stream));
         }
     }
+    CHIP_HIP(hipStreamSynchronize(c->stream));
     return CHIP_OK;
 }
 

@@ -211,15 +211,23 @@ class Allocator {
         return hipSuccess;
     }
 
-    // true if p came from alloc(); unmaps and releases it (its VA is retired)
+    // true if p came from alloc(); unmaps and releases it (its VA is retired).
+    // Like hipFree it first waits for the device (work in flight may still
+    // use the buffer), but outside the allocator's mutex: other threads'
+    // allocations and frees are not held up behind that wait.
     bool free(void *p) {
-        std::lock_guard<std::mutex> lk(mu_);
-        auto it = live_.find(static_cast<uint8_t *>(p));
-        if (it == live_.end()) return false;
+        Allocation A;
+        uint8_t *va = static_cast<uint8_t *>(p);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto it = live_.find(va);
+            if (it == live_.end()) return false;
+            A = std::move(it->second);
+            live_.erase(it);
+        }
         (void)hipDeviceSynchronize();
-        for (size_t i = 0; i < it->second.h.size(); ++i) (void)hipMemUnmap(it->first + i * PIECE, PIECE);
-        for (auto x : it->second.h) (void)hipMemRelease(x);
-        live_.erase(it);
+        for (size_t i = 0; i < A.h.size(); ++i) (void)hipMemUnmap(va + i * PIECE, PIECE);
+        for (auto x : A.h) (void)hipMemRelease(x);
         return true;
     }
 

@@ -158,23 +158,26 @@ std::map<int, uint8_t *> g_multab;                  // per device
 
 // Run-queue counters (QueueIter) per stream: launches on one stream run one
 // after another, and each launch leaves its counters zero (its last
-// workgroup resets them), so a stream's launches can share one block.  Blocks
-// come from a per-device pool of QUEUE_SLOTS, handed to streams in order of
-// first use; past QUEUE_SLOTS streams a slot is shared, which is safe unless
-// two of its streams run persistent launches at the same time.  Block layout
-// (uint32 words): K1 0-256 (8 counters 32 apart + the done counter), K13
-// QUEUE_K13 + {0, 32}, K3 QUEUE_K3 + {0, 32}.  (The block was 2 KiB while K13
-// and K3 already used words 512-672, i.e. the NEXT stream's K1 counters: a K1
-// launch on one thread's stream beside a K13 / K3 launch on the neighbouring
-// stream could lose or repeat column tiles.)
+// workgroup resets them), so a stream's launches can share one block.  Every
+// stream gets a block of its own: a destroyed stream's block first, else a
+// never-used one, and when a pool of QUEUE_SLOTS blocks is used up another
+// pool is allocated.  No two live streams ever share a block (two persistent
+// launches on one block lose or repeat tiles).  Streams the library does not
+// own (torch's, a Rust caller's) keep their block for the process lifetime:
+// 4 KiB per distinct stream.  Block layout (uint32 words): K1 0-256 (8
+// counters 32 apart + the done counter), K13 QUEUE_K13 + {0, 32}, K3
+// QUEUE_K3 + {0, 32}.  (The block was 2 KiB while K13 and K3 already used
+// words 512-672, i.e. the NEXT stream's K1 counters: a K1 launch on one
+// thread's stream beside a K13 / K3 launch on the neighbouring stream could
+// lose or repeat column tiles.)
 constexpr int QUEUE_SLOTS = 256;
 constexpr size_t QUEUE_BYTES = 4096;
 static_assert(QUEUE_K3 + 33 <= (int)(QUEUE_BYTES / 4) && QUEUE_K13 + 33 <= QUEUE_K3 && 257 <= QUEUE_K13,
               "run-queue block layout");
-std::map<int, uint8_t *> g_queue_pool;                      // per device
+std::map<int, std::vector<uint8_t *>> g_queue_pools;        // per device: pools of QUEUE_SLOTS blocks
 std::map<std::pair<int, hipStream_t>, uint32_t *> g_queue;  // (device, stream) -> counters
 std::map<int, std::vector<uint32_t *>> g_queue_free;        // per device: blocks of destroyed streams
-std::map<int, size_t> g_queue_next;                          // per device: next never-used block
+std::map<int, size_t> g_queue_next;                          // per device: next never-used block of the last pool
 
 hipError_t queue_for(hipStream_t stream, uint32_t **out) {
     const int dev = selected_device();
@@ -182,30 +185,44 @@ hipError_t queue_for(hipStream_t stream, uint32_t **out) {
     auto key = std::make_pair(dev, stream);
     auto it = g_queue.find(key);
     if (it != g_queue.end()) { *out = it->second; return hipSuccess; }
-    uint8_t *&pool = g_queue_pool[dev];
-    if (!pool) {
-        uint8_t *d = nullptr;
-        hipError_t e = hipMalloc(&d, QUEUE_SLOTS * QUEUE_BYTES);
-        if (e != hipSuccess) return e;
-        e = hipMemset(d, 0, QUEUE_SLOTS * QUEUE_BYTES);
-        if (e != hipSuccess) { (void)hipFree(d); return e; }
-        pool = d;
-    }
-    // a destroyed stream's block first (its launches left it zero), then a
-    // fresh one; blocks are shared only once QUEUE_SLOTS streams are alive
     uint32_t *q;
     std::vector<uint32_t *> &fl = g_queue_free[dev];
-    if (!fl.empty()) {
+    if (!fl.empty()) {  // a destroyed stream's block (its launches left it zero)
         q = fl.back();
         fl.pop_back();
     } else {
+        std::vector<uint8_t *> &pools = g_queue_pools[dev];
         size_t &nx = g_queue_next[dev];
-        q = reinterpret_cast<uint32_t *>(pool + (nx % QUEUE_SLOTS) * QUEUE_BYTES);
+        if (pools.empty() || nx == (size_t)QUEUE_SLOTS) {
+            uint8_t *d = nullptr;
+            hipError_t e = hipMalloc(&d, QUEUE_SLOTS * QUEUE_BYTES);
+            if (e != hipSuccess) return e;
+            // zeroed on a private stream and waited for, so the pool is zero
+            // before any stream's launch reads it, whatever that stream's flags
+            hipStream_t zs = nullptr;
+            e = hipStreamCreateWithFlags(&zs, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipMemsetAsync(d, 0, QUEUE_SLOTS * QUEUE_BYTES, zs);
+            if (e == hipSuccess) e = hipStreamSynchronize(zs);
+            if (zs) (void)hipStreamDestroy(zs);
+            if (e != hipSuccess) { (void)hipFree(d); return e; }
+            pools.push_back(d);
+            nx = 0;
+        }
+        q = reinterpret_cast<uint32_t *>(pools.back() + nx * QUEUE_BYTES);
         ++nx;
     }
     g_queue[key] = q;
     *out = q;
     return hipSuccess;
+}
+
+size_t queue_blocks_in_use() {
+    const int dev = selected_device();
+    std::lock_guard<std::mutex> lk(g_mu);
+    size_t n = 0;
+    for (const auto &kv : g_queue)
+        if (kv.first.first == dev) ++n;
+    return n;
 }
 
 int grid_for(const KernelInfo &ki) {

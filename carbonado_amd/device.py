@@ -146,7 +146,9 @@ def scrub_batch(enc: torch.Tensor, length: int, hashes: torch.Tensor, padding: i
     """scrub() (decoding.rs:159-212) of device-resident Bao|Zfec streams
     enc uint8 [count, >= length] with one EncodeInfo; repaired streams go to
     the rows of `out`.  Returns the per-object statuses (int32 numpy):
-    0 = repaired, CHIP_ERR_UNNECESSARY_SCRUB = intact, else scrub's error."""
+    0 = repaired, CHIP_ERR_UNNECESSARY_SCRUB = intact, else scrub's error.
+    A row of `out` is written only where the status is 0 (its repaired
+    stream's hash matched); every other row is left untouched."""
     assert enc.is_cuda and out.is_cuda and enc.is_contiguous() and out.is_contiguous()
     count = enc.shape[0]
     assert out.shape[0] == count and hashes.shape[0] == count

@@ -200,6 +200,12 @@ CHIP_API int chip_device_alloc_info(const void *ptr, uint32_t *classes_found, ui
 CHIP_API void *chip_torch_alloc(ssize_t size, int device, void *stream);
 CHIP_API void chip_torch_free(void *ptr, ssize_t size, int device, void *stream);
 
+/* Diagnostic: the device address of the run-queue counter block the batch
+ * kernels use on `stream` (NULL = the calling thread's own stream), assigning
+ * one if the stream has none yet.  Every live stream has a block of its own
+ * (DESIGN.md §3 K1 "Counter blocks"). */
+CHIP_API int chip_stream_queue_block(void *stream, uint64_t *addr);
+
 /* ---- size helpers (host only, no device needed) ----------------------- */
 /* utils.rs:47-58 with FEC_K generalised to k: target = ceil(n/(1024k))*1024k,
  * padding = target - n, chunk_len = target / k (integer maths; the reference's
@@ -297,7 +303,9 @@ CHIP_API int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8
  * (bytes beyond n inside the padded object read as zero, exactly as
  * encoding.rs:53-55 pads), its m*chunk_len-byte output at d_out + o*out_stride.
  * d_in, d_out, in_stride and out_stride must be multiples of 16
- * (CHIP_ERR_INVALID_ARG otherwise).
+ * (CHIP_ERR_INVALID_ARG otherwise).  Every batch entry point below refuses
+ * (CHIP_ERR_INVALID_ARG) strides under the row length when count > 1: rows
+ * would overlap.
  * In place: d_out == d_in (and out_stride == in_stride) means each object's
  * first n bytes already are its data shards; only the m-k parity shards are
  * written and the padding bytes [n, k*chunk_len) are zeroed (SURVEY.md 8d

@@ -131,3 +131,26 @@ def test_bench_config_presets():
     assert (a.mode, a.level) == ("e2e", 15)
     a = bench.parse([])
     assert (a.mode, a.k, a.m, a.objects, a.alloc) == ("encode", 4, 8, 1024, "chip")
+
+
+def test_bench_cfg5_eight_ranks_dry_run():
+    """The driver's SCALE command shape for cfg5 (8192 x 16 MiB objects over 8
+    GPUs), rehearsed with 8 gloo ranks on CPU: one line, per-rank arrays 8
+    long, 8192 global objects, verify threads split over the ranks."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, str(root / "bench.py"), "--config", "cfg5", "--gpus", "8", "--steps", "2",
+                          "--warmup", "1", "--dry-run"], capture_output=True, text=True, timeout=600, cwd=root,
+                         env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 8 and res["config"]["global_objects"] == 8192
+    assert (res["config"]["k"], res["config"]["m"]) == (8, 16)
+    assert len(res["roofline"]["per_rank_avg_launch_ms"]) == 8
+    assert 1 <= res["verify_threads_per_rank"] <= 16
