@@ -38,7 +38,15 @@ sys.path.insert(0, str(ROOT))
 
 from carbonado_amd.sharding import max_over_ranks, object_range  # noqa: E402
 
-VALU_PEAK_TOPS = 39.3  # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz, one int32 op per lane-cycle
+# BLAKE3 ceiling, measured (tools/valu_probe.hip, profiles/r6b_valu_probe.txt): the product's b3_compress
+# in a register-only loop at 8 waves/SIMD runs 5.685e10 compressions/s = 38.2 T "672-op" lane-ops/s.
+# gfx950 issues the VOP2 int ops (v_add_u32, v_xor_b32) and v_bitop3_b32 at the full SIMD-32 rate
+# (~69 T lane-ops/s measured, 78.6 nominal) but v_add3_u32, v_alignbit_b32, v_perm_b32, v_lshl_add_u32
+# and SDWA forms at half rate (~38 T); half of a compression's instructions are of the second kind.
+VALU_PEAK_TOPS = 38.2
+VALU_PEAK_SRC = ("measured BLAKE3 ceiling: b3_compress register loop, 8 waves/SIMD, 5.685e10 compressions/s x 672 "
+                 "(tools/valu_probe.hip, profiles/r6b_valu_probe.txt); VOP2 add/xor run at ~69 T lane-ops/s, the "
+                 "VOP3 add3/alignbit at ~38 T")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "GiB/s device-resident zfec 4-of-8 encode, 16 MiB objects; % HBM roofline"
 SEED = 0xCA4B0AD0
@@ -620,14 +628,20 @@ class Workload:
             self.pieces = [host[i:i + piece] for i in range(0, host.size, piece)]
             self.digest = None
 
+            self.finalize_ms = []
+
             def step():
                 h = BaoHasher()
                 for p in self.pieces:
                     h.update(p)
+                t0 = time.perf_counter()
                 self.digest = bytes(h.finalize())
+                self.finalize_ms.append((time.perf_counter() - t0) * 1e3)
             self.step = step
             self.alg_bytes = host.size  # PCIe: the content up (the hash comes back)
-            self.kernel = "BaoHasher: H2D appends into a grow-only HBM buffer + bao kernels at finalize()"
+            self.kernel = ("BaoHasher: H2D appends into a grow-only HBM buffer, chunk CVs hashed during update() "
+                           "(64-chunk units with bytes past them), finalize(): last chunks + slot layout + parent "
+                           "levels")
             self.kernel_sym = "hasher"
         elif args.mode == "file":
             import hashlib
@@ -1168,8 +1182,9 @@ def main():
                                "traffic_source": hbm["traffic_source"], "kernel": wl.kernel,
                                "alg_ops_per_launch": ops, "hbm_achieved_GBps": hbm["achieved"],
                                "avg_launch_ms": hbm["avg_launch_ms"], "min_launch_ms": hbm["min_launch_ms"],
-                               "note": "int32 VALU peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; ops = 672 per "
-                                       "BLAKE3 compression (content blocks + parents)"
+                               "peak_source": VALU_PEAK_SRC,
+                               "note": "ops = 672 per BLAKE3 compression (content blocks + parents); peak = the "
+                                       "measured compression ceiling x 672"
                                        + ("; achieved over the whole step (every kernel of the level)"
                                           if pipe else "")}
             for key in ("traffic_ratio", "pmc_KiB_per_launch", "pmc_kernel", "alg_bytes_per_launch"):
@@ -1212,6 +1227,11 @@ def main():
                          "(all 8 shards written, 48 MiB per object) is the graded figure")}
         if scatter is not None:
             res["scatter"] = scatter
+        if args.mode == "hasher" and not args.dry_run:
+            fm = sorted(wl.finalize_ms[-args.steps:])
+            res["finalize_ms"] = {"median": round(fm[len(fm) // 2], 3), "max": round(fm[-1], 3),
+                                  "how": "host wall time of finalize() after the last update() of each timed step "
+                                         f"({args.objects * args.object_mib:g} MiB in 4 MiB appends)"}
         if args.mode == "file" and not args.dry_run:
             res["file_stages_last_step"] = dict(wl.file_stats, note="busy seconds of each overlapped stage")
         if wl.scatter_s is not None:

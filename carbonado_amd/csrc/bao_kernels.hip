@@ -218,6 +218,87 @@ hipError_t scrub_masks(const uint8_t *d_stream, uint64_t stride, uint64_t n, uin
     return hipGetLastError();
 }
 
+// ---- incremental BaoHasher (utils.rs:104-137) ------------------------------
+//
+// bao's Encoder takes the content in appends; the chunk CVs of a chunk do not
+// depend on what follows it (counter = chunk index, CHUNK_START / CHUNK_END
+// on its first / last block, ROOT only when N == 1).  So chunk_update hashes
+// chunks as soon as bytes past them have arrived (they are full and not the
+// root), and finalize only hashes the last < 64 + 1 chunks, lays the content
+// out in its chunk slots and builds the parent levels from the chunk CVs (the
+// slot offsets depend on the final N, so the layout waits for it).
+
+namespace {
+
+// chunk CVs of chunks [c0, c1) of a content buffer of n bytes (N > 1: none is
+// the root), one lane per chunk
+__global__ __launch_bounds__(64) void hasher_chunk_kernel(const uint8_t *content, uint64_t n, uint64_t c0,
+                                                          uint64_t c1, uint8_t *cv) {
+    const uint64_t ci = c0 + (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (ci >= c1) return;
+    const uint8_t *src = content + ci * 1024;
+    const uint64_t rem = n - ci * 1024;
+    const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+    const uint32_t nb = clen ? (clen + 63) / 64 : 1;
+    uint32_t h[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) h[w] = IV(w);
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint32_t blen = clen - 64 * b < 64 ? clen - 64 * b : 64u;
+        uint32_t m[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t off = 64 * b + 16 * q;
+            const uint32_t valid = off < clen ? clen - off : 0u;
+            const u32x4 x = valid >= 16 ? *reinterpret_cast<const u32x4 *>(src + off) : load16_partial(src + off, valid);
+            m[4 * q] = x.x; m[4 * q + 1] = x.y; m[4 * q + 2] = x.z; m[4 * q + 3] = x.w;
+        }
+        const uint32_t flags = (b == 0 ? F_CHUNK_START : 0u) | (b + 1 == nb ? F_CHUNK_END : 0u);
+        b3_compress(h, m, ci, blen, flags);
+    }
+    store_cv(cv + ci * 32, h);
+}
+
+// the stream's header and every chunk's content at its slot (one wave per
+// chunk, 16 B per lane; slots are 8-B aligned)
+__global__ __launch_bounds__(256) void hasher_layout_kernel(const uint8_t *content, uint64_t n, uint64_t N,
+                                                            uint8_t *out) {
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *glb(reinterpret_cast<uint64_t *>(out)) = n;
+    for (uint64_t ci = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); ci < N; ci += (uint64_t)gridDim.x * 4) {
+        const uint64_t off = chunk_stream_off(ci, N);
+        const uint64_t b = ci * 1024 + 16 * (uint64_t)lane;
+        if (b + 16 <= n) {
+            store16_a8<false>(out + off + 16 * lane, *reinterpret_cast<const u32x4 *>(content + b));
+        } else if (b < n) {
+            store16_partial(out + off + 16 * lane, load16_partial(content + b, (uint32_t)(n - b)), (uint32_t)(n - b));
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t hasher_chunks_dev(const uint8_t *content, uint64_t n, uint64_t c0, uint64_t c1, uint8_t *cv0,
+                             hipStream_t stream) {
+    if (c1 <= c0) return hipSuccess;
+    const uint64_t blocks = (c1 - c0 + 63) / 64;
+    hipLaunchKernelGGL(hasher_chunk_kernel, dim3((unsigned)blocks), dim3(64), 0, stream, content, n, c0, c1, cv0);
+    return hipGetLastError();
+}
+
+hipError_t hasher_finish_dev(const uint8_t *content, uint64_t n, uint64_t c_done, uint8_t *cv0, uint8_t *cv1,
+                             uint8_t *d_out, uint8_t *d_hash, hipStream_t stream) {
+    const uint64_t N = n_chunks(n);
+    if (N < 2) return hipErrorInvalidValue;  // the single chunk is the root: the batch path
+    hipError_t e = hasher_chunks_dev(content, n, c_done, N, cv0, stream);
+    if (e != hipSuccess) return e;
+    const uint64_t blocks = std::min<uint64_t>((N + 3) / 4, 65536);
+    hipLaunchKernelGGL(hasher_layout_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, content, n, N, d_out);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return run_parent_levels<0, false>(cv0, N, N, 1, cv1, (N + 1) / 2, N, 1, d_out, 0, d_hash, nullptr, stream);
+}
+
 uint64_t bao_chunk_offset(uint64_t i, uint64_t N) { return chunk_stream_off(i, N); }
 uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N) { return parent_stream_off(s, level, N); }
 uint64_t bao_parent_index(uint64_t s, int level, uint64_t N) {

@@ -2381,11 +2381,19 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
 
 }  // extern "C"
 
+// Incremental (utils.rs:104-137 streams into bao's Encoder): update() appends
+// to a grow-only HBM buffer and, asynchronously on the hasher's stream, hashes
+// every chunk that bytes have arrived past (whole 64-chunk units, so each
+// launch fills a wave per unit); finalize() hashes the last chunks, lays the
+// content out in its slots and builds the parent levels from the chunk CVs.
 struct chip_bao_hasher {
     std::mutex mu;
-    hipStream_t stream = nullptr;
-    DevBuf content, enc, scratch, hash;
+    hipStream_t stream = nullptr;   // copies (and finalize)
+    hipStream_t hstream = nullptr;  // update()'s chunk hashing, behind the copies through `copied`
+    hipEvent_t copied = nullptr;
+    DevBuf content, enc, scratch, hash, cv0, cv1;
     uint64_t len = 0, enc_len = 0;
+    uint64_t units = 0;  // 64-chunk units whose chunk CVs are in cv0
     bool finalized = false;
     uint8_t h[32] = {0};
 };
@@ -2425,7 +2433,12 @@ int chip_bao_hasher_new(chip_bao_hasher **out) {
     if (st != CHIP_OK) return st;
     auto *h = new chip_bao_hasher();
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->hstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->copied, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (h->copied) (void)hipEventDestroy(h->copied);
+        if (h->hstream) (void)hipStreamDestroy(h->hstream);
+        if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
         set_device_error(e);
         return CHIP_ERR_DEVICE;
@@ -2442,12 +2455,27 @@ int chip_bao_hasher_update(chip_bao_hasher *h, const uint8_t *buf, uint64_t n) {
     Ctx *c;
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
+    if (h->content.cap < h->len + n) CHIP_HIP(hipStreamSynchronize(h->hstream));  // hashing reads the old buffer
     CHIP_HIP(grow_keep(h->content, h->len + n, h->len, h->stream));
     CHIP_HIP(h2d(c->stage, static_cast<uint8_t *>(h->content.p) + h->len, buf, n, h->stream));
+    h->len += n;
+    // units u with bytes past them ((u + 1) * 64 KiB < len): full chunks, none of them the last;
+    // hashed on the second stream once their bytes have landed, so the copies never wait for it
+    const uint64_t ready = (h->len - 1) / 65536;
+    if (ready > h->units) {
+        if (h->cv0.cap < ready * 64 * 32) {
+            CHIP_HIP(hipStreamSynchronize(h->hstream));
+            CHIP_HIP(grow_keep(h->cv0, std::max<uint64_t>(ready * 64 * 32, 1 << 20), h->units * 64 * 32, h->hstream));
+        }
+        CHIP_HIP(hipEventRecord(h->copied, h->stream));
+        CHIP_HIP(hipStreamWaitEvent(h->hstream, h->copied, 0));
+        CHIP_HIP(hasher_chunks_dev(static_cast<const uint8_t *>(h->content.p), h->len, h->units * 64, ready * 64,
+                                   static_cast<uint8_t *>(h->cv0.p), h->hstream));
+        h->units = ready;
+    }
     // the caller may reuse buf on return: a staged copy is done with it already,
     // a direct one (pinned buf) is waited for
     if (!staged(buf, n)) CHIP_HIP(hipStreamSynchronize(h->stream));
-    h->len += n;
     return CHIP_OK;
 }
 
@@ -2462,11 +2490,22 @@ int chip_bao_hasher_finalize(chip_bao_hasher *h, uint8_t hash[CHIP_HASH_LEN]) {
         h->enc_len = bao_encoded_len(n);
         CHIP_HIP(grow_keep(h->content, 16, h->len, h->stream));
         CHIP_HIP(grow(h->enc, h->enc_len));
-        CHIP_HIP(grow(h->scratch, bao_scratch_len(n, 1)));
         CHIP_HIP(grow(h->hash, 32));
-        CHIP_HIP(bao_encode_dev(static_cast<const uint8_t *>(h->content.p), 0, n, 1,
-                                static_cast<uint8_t *>(h->enc.p), 0, static_cast<uint8_t *>(h->hash.p),
-                                h->scratch.p, h->stream));
+        if (h->units == 0) {  // under 64 KiB + 1 byte in all: the batch path in one go
+            CHIP_HIP(grow(h->scratch, bao_scratch_len(n, 1)));
+            CHIP_HIP(bao_encode_dev(static_cast<const uint8_t *>(h->content.p), 0, n, 1,
+                                    static_cast<uint8_t *>(h->enc.p), 0, static_cast<uint8_t *>(h->hash.p),
+                                    h->scratch.p, h->stream));
+        } else {  // only the last chunks are hashed here
+            const uint64_t N = (n + 1023) / 1024;
+            CHIP_HIP(hipStreamSynchronize(h->hstream));  // update()'s chunk CVs are in cv0
+            CHIP_HIP(grow_keep(h->cv0, N * 32, h->units * 64 * 32, h->stream));
+            CHIP_HIP(grow(h->cv1, (N + 1) / 2 * 32));
+            CHIP_HIP(hasher_finish_dev(static_cast<const uint8_t *>(h->content.p), n, h->units * 64,
+                                       static_cast<uint8_t *>(h->cv0.p), static_cast<uint8_t *>(h->cv1.p),
+                                       static_cast<uint8_t *>(h->enc.p), static_cast<uint8_t *>(h->hash.p),
+                                       h->stream));
+        }
         CHIP_HIP(hipMemcpyAsync(h->h, h->hash.p, 32, hipMemcpyDeviceToHost, h->stream));
         CHIP_HIP(hipStreamSynchronize(h->stream));
         h->finalized = true;
@@ -2499,13 +2538,16 @@ void chip_bao_hasher_free(chip_bao_hasher *h) {
     if (!h) return;
     {
         std::lock_guard<std::mutex> lk(h->mu);
-        for (DevBuf *b : {&h->content, &h->enc, &h->scratch, &h->hash})
+        if (h->hstream) (void)hipStreamSynchronize(h->hstream);
+        if (h->stream) (void)hipStreamSynchronize(h->stream);
+        for (DevBuf *b : {&h->content, &h->enc, &h->scratch, &h->hash, &h->cv0, &h->cv1})
             if (b->p) (void)hipFree(b->p);
+        if (h->hstream) (void)hipStreamDestroy(h->hstream);
         if (h->stream) {
-            (void)hipStreamSynchronize(h->stream);
             stream_queue_release(h->stream);
             (void)hipStreamDestroy(h->stream);
         }
+        if (h->copied) (void)hipEventDestroy(h->copied);
     }
     delete h;
 }

@@ -136,6 +136,15 @@ hipError_t scrub_masks(const uint8_t *d_stream, uint64_t stride, uint64_t n, uin
 // Content of chunks [c0, c1) of one stream, parents stripped, to d_out.
 hipError_t bao_gather_content(const uint8_t *d_stream, uint64_t n, uint64_t c0, uint64_t c1, uint8_t *d_out,
                               hipStream_t stream);
+// Incremental BaoHasher: chunk CVs of full, non-final chunks [c0, c1) of a
+// contiguous content buffer (cv0[i] = chunk i's CV, 32 B); at finalize the
+// remaining chunks [c_done, N), the content laid out in the stream d_out,
+// the parent levels (cv0 and cv1 ((N+1)/2 CVs) as ping-pong buffers, cv0
+// overwritten) and the root hash.  N = n_chunks(n) must be >= 2.
+hipError_t hasher_chunks_dev(const uint8_t *content, uint64_t n, uint64_t c0, uint64_t c1, uint8_t *cv0,
+                             hipStream_t stream);
+hipError_t hasher_finish_dev(const uint8_t *content, uint64_t n, uint64_t c_done, uint8_t *cv0, uint8_t *cv1,
+                             uint8_t *d_out, uint8_t *d_hash, hipStream_t stream);
 // Stream layout (host side, same formulas as the kernels).
 uint64_t bao_chunk_offset(uint64_t i, uint64_t N);
 uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N);

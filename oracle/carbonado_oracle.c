@@ -46,6 +46,10 @@ static void gf_table_init(void) {
     gf_table_ready = 1;
 }
 
+/* built once at load time, before any thread runs (the checkers call the
+   oracle from many threads) */
+__attribute__((constructor)) static void gf_tables_at_load(void) { gf_table_init(); }
+
 /* fec.c addmul(dst, src, c, sz): dst[i] ^= c * src[i] by table lookup */
 static void addmul(uint8_t *dst, const uint8_t *src, uint8_t c, uint64_t sz) {
     const uint8_t *row = gf_mul_table[c];

@@ -84,7 +84,7 @@ static uint64_t snap_block(uint8_t *d, const uint8_t *s, uint64_t n) {
     unsigned shift = 24;
     uint64_t ts = 256;
     while (ts < 16384 && ts < n) { --shift; ts <<= 1; }
-    static uint16_t table[16384];
+    uint16_t table[16384]; /* per call: the oracle runs on many threads at once */
     memset(table, 0, ts * sizeof(uint16_t));
 #define HSH(u) ((uint32_t)((uint32_t)(u) * 0x1E35A7BDu) >> shift)
     const uint64_t lim = n - 15;
@@ -312,6 +312,13 @@ static void aes_init(void) {
         TE[0][i] = t; TE[1][i] = rr(t, 8); TE[2][i] = rr(t, 16); TE[3][i] = rr(t, 24);
     }
     aes_ready = 1;
+}
+
+/* the lazily built tables are built once at load time, before any thread
+   runs (the checkers call the oracle from many threads) */
+__attribute__((constructor)) static void host_oracle_tables(void) {
+    crc_init();
+    aes_init();
 }
 
 typedef struct { uint32_t rk[60]; } aes256;

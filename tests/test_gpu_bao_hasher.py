@@ -25,7 +25,8 @@ def _pieces(total, seed):
     return data, parts
 
 
-@pytest.mark.parametrize("total", [0, 1, 1023, 1024, 1025, 8191, 70_000, (3 << 20) + 17])
+@pytest.mark.parametrize("total", [0, 1, 1023, 1024, 1025, 8191, 65536, 65537, 70_000, 131072, 131073,
+                                   (64 << 10) * 65, (3 << 20) + 17])
 def test_hasher_matches_oneshot(gpu, total):
     from carbonado_amd.utils import BaoHasher
     data, parts = _pieces(total, total)
@@ -104,3 +105,37 @@ def test_hasher_churn_recycles_queue_blocks(gpu):
         if i % 50 == 0:
             gc.collect()
             assert ca.encoding.zfec(zd)[0] == z_want
+
+
+@pytest.mark.parametrize("piece,total", [(4 << 20, (16 << 20) + 5), (65536, (2 << 20)), (65537, (2 << 20) + 999),
+                                         (1000, 300_000), (1 << 20, 64 << 20)])
+def test_hasher_incremental_appends(gpu, piece, total):
+    """Appends of fixed size at chunk- and unit-misaligned boundaries: the
+    chunks hashed during update() (64-chunk units with bytes past them) plus
+    the ones finalize() hashes give the one-shot stream and hash."""
+    from carbonado_amd.utils import BaoHasher
+    rng = np.random.default_rng(piece ^ total)
+    data = rng.integers(0, 256, total, dtype=np.uint8).tobytes()
+    h = BaoHasher()
+    for off in range(0, total, piece):
+        h.update(data[off:off + piece])
+    enc, oh = O.bao_encode(data)
+    assert h.finalize() == oh
+    assert h.read_all() == enc
+
+
+def test_hasher_incremental_pinned_appends(gpu):
+    """Pinned (direct-copy) appends of a torch buffer, 4 MiB each, unit
+    boundaries inside appends; then the same hasher's stream vs the oracle."""
+    import torch
+    from carbonado_amd.utils import BaoHasher
+    total = (12 << 20) + 4097
+    src = torch.randint(0, 256, (total,), dtype=torch.uint8).pin_memory()
+    h = BaoHasher()
+    piece = (4 << 20) - 3
+    for off in range(0, total, piece):
+        h.update(src[off:off + piece].numpy())
+    data = src.numpy().tobytes()
+    enc, oh = O.bao_encode(data)
+    assert h.finalize() == oh
+    assert h.read_all() == enc

@@ -173,7 +173,8 @@ def test_concurrent_streams_k13_beside_k1(gpu):
 
 
 def test_queue_blocks_never_shared_past_pool(gpu):
-    """300 distinct caller streams (more than one pool of 256 blocks) each get
+    """300 distinct caller streams (more than one pool of 256 blocks; created
+    with hipStreamCreate: torch.cuda.Stream() hands out a pool of 32) each get
     a run-queue block of their own; then K13 content-mode bao batches on
     stream 1 run concurrently with K1 zfec batches on stream 257, the pair a
     wrapping pool (nx % 256) used to give the same block.  Bit-exact against
@@ -182,38 +183,51 @@ def test_queue_blocks_never_shared_past_pool(gpu):
     import torch
     from carbonado_amd import _lib, device
     L = _lib.lib()
-    streams = [torch.cuda.Stream() for _ in range(300)]
-    blocks = []
-    for s in streams:
-        a = ctypes.c_uint64()
-        assert L.chip_stream_queue_block(ctypes.c_void_p(s.cuda_stream), ctypes.byref(a)) == 0
-        blocks.append(a.value)
-    own = ctypes.c_uint64()
-    assert L.chip_stream_queue_block(None, ctypes.byref(own)) == 0
-    assert len(set(blocks + [own.value])) == 301
-    again = ctypes.c_uint64()  # stable per stream
-    L.chip_stream_queue_block(ctypes.c_void_p(streams[7].cuda_stream), ctypes.byref(again))
-    assert again.value == blocks[7]
-    sa, sb = streams[1], streams[257]
-    nb, cb, nz, cz, R = 4 << 20, 16, 16 << 20, 8, 4
-    bin_ = _rand((cb, nb), 41)
-    zin = _rand((cz, nz), 42)
-    bstride = (L.chip_bao_encoded_len(nb) + 15) // 16 * 16
-    bouts = [torch.zeros((cb, bstride), dtype=torch.uint8, device="cuda") for _ in range(R)]
-    bh = [torch.zeros((cb, 32), dtype=torch.uint8, device="cuda") for _ in range(R)]
-    zouts = [torch.zeros((cz, 2 * nz), dtype=torch.uint8, device="cuda") for _ in range(R)]
-    bscr = device.bao_scratch(nb, cb)
-    torch.cuda.synchronize()
-    for r in range(R):
-        with torch.cuda.stream(sa):
-            device.bao_encode_batch(bin_, nb, bouts[r], bh[r], bscr)
-        with torch.cuda.stream(sb):
-            device.zfec_encode_batch(zin, nz, zouts[r], 4, 8)
-    torch.cuda.synchronize()
-    blen = L.chip_bao_encoded_len(nb)
-    enc0, h0 = O.bao_encode(bin_[9].cpu().numpy().tobytes())
-    assert bouts[0][9, :blen].cpu().numpy().tobytes() == enc0 and bh[0][9].cpu().numpy().tobytes() == h0
-    assert zouts[0][2].cpu().numpy().tobytes() == O.zfec_encode(zin[2].cpu().numpy().tobytes())[0]
-    for r in range(1, R):
-        assert torch.equal(bouts[r], bouts[0]) and torch.equal(bh[r], bh[0]), r
-        assert torch.equal(zouts[r], zouts[0]), r
+    hip = ctypes.CDLL("libamdhip64.so")
+    raw = []
+    for _ in range(300):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        raw.append(s)
+    try:
+        blocks = []
+        for s in raw:
+            a = ctypes.c_uint64()
+            assert L.chip_stream_queue_block(s, ctypes.byref(a)) == 0
+            blocks.append(a.value)
+        own = ctypes.c_uint64()
+        assert L.chip_stream_queue_block(None, ctypes.byref(own)) == 0
+        assert len(set(blocks + [own.value])) == 301
+        again = ctypes.c_uint64()  # stable per stream
+        L.chip_stream_queue_block(raw[7], ctypes.byref(again))
+        assert again.value == blocks[7]
+        sa, sb = torch.cuda.ExternalStream(raw[1].value), torch.cuda.ExternalStream(raw[257].value)
+        nb, cb, nz, cz, R = 4 << 20, 16, 16 << 20, 8, 4
+        bin_ = _rand((cb, nb), 41)
+        zin = _rand((cz, nz), 42)
+        bstride = (L.chip_bao_encoded_len(nb) + 15) // 16 * 16
+        bouts = [torch.zeros((cb, bstride), dtype=torch.uint8, device="cuda") for _ in range(R)]
+        bh = [torch.zeros((cb, 32), dtype=torch.uint8, device="cuda") for _ in range(R)]
+        zouts = [torch.zeros((cz, 2 * nz), dtype=torch.uint8, device="cuda") for _ in range(R)]
+        bscr = device.bao_scratch(nb, cb)
+        torch.cuda.synchronize()
+        for r in range(R):
+            with torch.cuda.stream(sa):
+                device.bao_encode_batch(bin_, nb, bouts[r], bh[r], bscr)
+            with torch.cuda.stream(sb):
+                device.zfec_encode_batch(zin, nz, zouts[r], 4, 8)
+        sa.synchronize()
+        sb.synchronize()
+        torch.cuda.synchronize()
+        blen = L.chip_bao_encoded_len(nb)
+        enc0, h0 = O.bao_encode(bin_[9].cpu().numpy().tobytes())
+        assert bouts[0][9, :blen].cpu().numpy().tobytes() == enc0 and bh[0][9].cpu().numpy().tobytes() == h0
+        assert zouts[0][2].cpu().numpy().tobytes() == O.zfec_encode(zin[2].cpu().numpy().tobytes())[0]
+        for r in range(1, R):
+            assert torch.equal(bouts[r], bouts[0]) and torch.equal(bh[r], bh[0]), r
+            assert torch.equal(zouts[r], zouts[0]), r
+    finally:
+        torch.cuda.synchronize()
+        for s in raw:
+            hip.hipStreamSynchronize(s)
+            hip.hipStreamDestroy(s)

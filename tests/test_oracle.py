@@ -154,3 +154,25 @@ def test_level8_scrub_style_recovery():
     # lose data shard 0 and 1 (the case the reference mislabels)
     keep = [2, 3, 4, 5, 6, 7]
     assert O.zfec_decode_shares([shards[i] for i in keep], keep, pad) == d
+
+
+def test_c_oracle_thread_safe():
+    """bench.py checks every object with the C oracle on 16 threads at once:
+    threaded results equal serial ones (the snappy hash table was once a
+    function-level static shared by all threads)."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    rng = np.random.default_rng(77)
+    objs = [rng.integers(0, 256, (2 << 20) + 31 * i, dtype=np.uint8).tobytes() for i in range(16)]
+    objs[3] = bytes(2 << 20)  # compressible objects too
+    objs[7] = b"carbonado " * 200_000
+    pub = O.c_public_key(hashlib.sha256(b"thread safety").digest())
+    eph = [hashlib.sha256(b"e%d" % i).digest() for i in range(16)]
+
+    def one(i):
+        return O.c_encode_full(objs[i], 15, pub, eph[i], bytes(16))[0]
+    serial = [one(i) for i in range(16)]
+    with ThreadPoolExecutor(16) as ex:
+        for _ in range(2):
+            assert list(ex.map(one, range(16))) == serial

@@ -32,9 +32,10 @@
         }                                                                                     \
     } while (0)
 
-enum Op { ADD = 0, ADD3, XOR, BITOP3, ALIGNBIT, FMA, PERM, LSHLADD, NOPS };
+enum Op { ADD = 0, ADD3, XOR, BITOP3, ALIGNBIT, FMA, PERM, LSHLADD, XORSDWA, MIX, NOPS };
 static const char *op_name[NOPS] = {"v_add_u32", "v_add3_u32", "v_xor_b32", "v_bitop3_b32",
-                                    "v_alignbit_b32", "v_fma_f32", "v_perm_b32", "v_lshl_add_u32"};
+                                    "v_alignbit_b32", "v_fma_f32", "v_perm_b32", "v_lshl_add_u32",
+                                    "v_xor_b32_sdwa", "mix4"};
 
 template <int OP>
 __device__ __forceinline__ void one(uint32_t &x, uint32_t a, uint32_t b) {
@@ -46,6 +47,16 @@ __device__ __forceinline__ void one(uint32_t &x, uint32_t a, uint32_t b) {
     if constexpr (OP == FMA) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
     if constexpr (OP == PERM) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
     if constexpr (OP == LSHLADD) asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(x) : "v"(a));
+    if constexpr (OP == XORSDWA)
+        asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
+                     : "+v"(x) : "v"(a));
+    // one of each class on the chain in BLAKE3's G order: counted as 4 instructions
+    if constexpr (OP == MIX) {
+        asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(a));
+        asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(x));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(x) : "v"(a));
+        asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
+    }
 }
 
 struct Stamp { uint64_t t0, t1, r0, r1; };
@@ -101,6 +112,81 @@ __global__ __launch_bounds__(256) void b3_kernel(uint32_t *out, Stamp *st, int i
     for (int q = 0; q < NS; ++q)
 #pragma unroll
         for (int i = 0; i < 8; ++i) s ^= h[q][i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+    if ((threadIdx.x & 63) == 0) {
+        Stamp v{t0, t1, r0, r1};
+        st[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = v;
+    }
+}
+
+__device__ __forceinline__ uint32_t xor_rot16(uint32_t d, uint32_t a) {
+    uint32_t r;
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1"
+                 : "=v"(r) : "v"(d), "v"(a));
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
+                 : "+v"(r) : "v"(d), "v"(a));
+    return r;
+}
+__device__ __forceinline__ uint32_t add2(uint32_t a, uint32_t b, uint32_t m) {
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %2\n\tv_add_u32 %0, %0, %3" : "=&v"(r) : "v"(a), "v"(b), "v"(m));
+    return r;
+}
+template <int VAR>
+__device__ __forceinline__ void gv(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t x, uint32_t y) {
+    a = VAR == 2 ? add2(a, b, x) : a + b + x;
+    d = VAR >= 1 ? xor_rot16(d, a) : chip::bao::rotr(d ^ a, 16);
+    c = c + d;
+    b = chip::bao::rotr(b ^ c, 12);
+    a = VAR == 2 ? add2(a, b, y) : a + b + y;
+    d = chip::bao::rotr(d ^ a, 8);
+    c = c + d;
+    b = chip::bao::rotr(b ^ c, 7);
+}
+template <int VAR, int R>
+__device__ __forceinline__ void rv(uint32_t (&v)[16], const uint32_t (&m)[16]) {
+    using chip::bao::SCHED;
+    gv<VAR>(v[0], v[4], v[8], v[12], m[SCHED(R, 0)], m[SCHED(R, 1)]);
+    gv<VAR>(v[1], v[5], v[9], v[13], m[SCHED(R, 2)], m[SCHED(R, 3)]);
+    gv<VAR>(v[2], v[6], v[10], v[14], m[SCHED(R, 4)], m[SCHED(R, 5)]);
+    gv<VAR>(v[3], v[7], v[11], v[15], m[SCHED(R, 6)], m[SCHED(R, 7)]);
+    gv<VAR>(v[0], v[5], v[10], v[15], m[SCHED(R, 8)], m[SCHED(R, 9)]);
+    gv<VAR>(v[1], v[6], v[11], v[12], m[SCHED(R, 10)], m[SCHED(R, 11)]);
+    gv<VAR>(v[2], v[7], v[8], v[13], m[SCHED(R, 12)], m[SCHED(R, 13)]);
+    gv<VAR>(v[3], v[4], v[9], v[14], m[SCHED(R, 14)], m[SCHED(R, 15)]);
+}
+template <int VAR>
+__device__ __forceinline__ void cv_compress(uint32_t (&h)[8], const uint32_t (&m)[16], uint64_t ctr, uint32_t blen,
+                                            uint32_t flags) {
+    using chip::bao::IV;
+    uint32_t v[16] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], IV(0), IV(1), IV(2), IV(3),
+                      (uint32_t)ctr, (uint32_t)(ctr >> 32), blen, flags};
+    rv<VAR, 0>(v, m); rv<VAR, 1>(v, m); rv<VAR, 2>(v, m); rv<VAR, 3>(v, m);
+    rv<VAR, 4>(v, m); rv<VAR, 5>(v, m); rv<VAR, 6>(v, m);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = v[i] ^ v[i + 8];
+}
+// BLAKE3 variants: VAR 1 = rot16 fused into its xor as two SDWA xors, VAR 2 =
+// VAR 1 + a+b+m as two v_add_u32 instead of v_add3_u32.  out[] of every
+// variant must equal VAR 0's (checked on the host).
+template <int VAR>
+__global__ __launch_bounds__(256) void b3v_kernel(uint32_t *out, Stamp *st, int iters, uint32_t seed) {
+    uint32_t h[8], m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = seed * (i + 1) + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = chip::bao::IV(i) + threadIdx.x;
+    const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; ++it) {
+        cv_compress<VAR>(h, m, (uint64_t)it, 64, 0);
+        m[it & 15] ^= h[it & 7];
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s ^= h[i] * (i + 1);
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
     if ((threadIdx.x & 63) == 0) {
         Stamp v{t0, t1, r0, r1};
@@ -175,6 +261,30 @@ static void probe_op(int iters) {
     fflush(stdout);
 }
 
+template <int VAR>
+static void probe_b3v(int iters, std::vector<uint32_t> *ref) {
+    for (int W : {2, 4, 8}) {
+        Result r = run([&](int blocks, uint32_t *o, Stamp *s) {
+            b3v_kernel<VAR><<<blocks, 256>>>(o, s, iters, 12345u);
+        }, W, 672.0 * iters, 3);
+        printf("blake3 VAR %d W=%d  %8.3f ms  %7.2f T lane-op/s (672/compress)  %.3e compress/s  clk %.2f GHz\n", VAR,
+               W, r.ms, r.lane_ops_t, r.lane_ops_t * 1e12 / 672.0, r.clock_ghz);
+    }
+    // correctness of the variant: one W=1 launch's outputs against VAR 0's
+    uint32_t *d = nullptr;
+    Stamp *st = nullptr;
+    CK(hipMalloc(&d, 256 * 256 * 4));
+    CK(hipMalloc(&st, 256 * 4 * sizeof(Stamp)));
+    b3v_kernel<VAR><<<256, 256>>>(d, st, 50, 777u);
+    std::vector<uint32_t> h(256 * 256);
+    CK(hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+    if (ref->empty()) *ref = h;
+    printf("blake3 VAR %d output %s VAR 0\n", VAR, h == *ref ? "==" : "!=");
+    CK(hipFree(d));
+    CK(hipFree(st));
+    fflush(stdout);
+}
+
 template <int NS>
 static void probe_b3(int iters) {
     for (int W : {1, 2, 3, 4, 8}) {
@@ -204,7 +314,13 @@ int main(int argc, char **argv) {
     probe_op<FMA>(iters);
     probe_op<PERM>(iters);
     probe_op<LSHLADD>(iters);
+    probe_op<XORSDWA>(iters);
+    probe_op<MIX>(iters / 4);
     probe_b3<1>(iters / 64);
     probe_b3<2>(iters / 128);
+    std::vector<uint32_t> ref;
+    probe_b3v<0>(iters / 64, &ref);
+    probe_b3v<1>(iters / 64, &ref);
+    probe_b3v<2>(iters / 64, &ref);
     return 0;
 }
