@@ -142,40 +142,49 @@ bool lift_x(const uint8_t x32[32], Pt &pt) {
     return EC_POINT_set_compressed_coordinates(ctx().g, pt.v, x.v, 0, ctx().bn) == 1;
 }
 
+// BIP-340 signing.  The key and nonce scalars stay in secp256k1_host.hpp's
+// constant-time arithmetic: k * G there, d / n - d and k / n - k chosen with
+// masks, s = k + e d mod n with fixed limb loops.
 int schnorr_sign(const uint8_t sk[32], const uint8_t msg[32], const uint8_t *aux_in, uint8_t sig[64]) {
-    Bn d0;
-    if (!parse_secret(sk, 32, d0)) return CHIP_ERR_SECP256K1;
+    namespace k1 = chip::k1;
+    {
+        Bn d0;
+        if (!parse_secret(sk, 32, d0)) return CHIP_ERR_SECP256K1;  // 0 < d < n (public check)
+    }
     uint8_t aux[32];
     if (aux_in) std::memcpy(aux, aux_in, 32);
     else if (RAND_bytes(aux, 32) != 1) return CHIP_ERR_SECP256K1;
-    uint8_t px[32], dd[32], t[32], rnd[32], rx[32], e32[32];
-    bool even = false;
-    if (!mul_g_xy(d0.v, px, &even)) return CHIP_ERR_SECP256K1;
-    Bn d;
-    if (even) BN_copy(d.v, d0.v);
-    else BN_sub(d.v, order(), d0.v);
-    if (!bn32(d.v, dd) || !tagged("BIP0340/aux", aux, 32, nullptr, 0, nullptr, 0, t)) return CHIP_ERR_SECP256K1;
+    uint8_t px[32], dd[32], t[32], rnd[32], rx[32], e32[32], o[65];
+    if (!k1::to65(k1::mul_g(sk), o)) return CHIP_ERR_SECP256K1;
+    std::memcpy(px, o + 1, 32);
+    k1::Sc d = k1::sc_cond_neg(k1::sc_from_be(sk), o[64] & 1);  // the key with an even y
+    k1::sc_to_be(d, dd);
+    if (!tagged("BIP0340/aux", aux, 32, nullptr, 0, nullptr, 0, t)) return CHIP_ERR_SECP256K1;
     for (int i = 0; i < 32; ++i) t[i] ^= dd[i];
     if (!tagged("BIP0340/nonce", t, 32, px, 32, msg, 32, rnd)) return CHIP_ERR_SECP256K1;
-    Bn k0(rnd), k, e, s;
-    BN_mod(k0.v, k0.v, order(), ctx().bn);
-    if (BN_is_zero(k0.v)) return CHIP_ERR_SECP256K1;
-    bool reven = false;
-    if (!mul_g_xy(k0.v, rx, &reven)) return CHIP_ERR_SECP256K1;
-    if (reven) BN_copy(k.v, k0.v);
-    else BN_sub(k.v, order(), k0.v);
-    if (!tagged("BIP0340/challenge", rx, 32, px, 32, msg, 32, e32)) return CHIP_ERR_SECP256K1;
-    BN_bin2bn(e32, 32, e.v);
-    BN_mod(e.v, e.v, order(), ctx().bn);
-    // s = (k + e d) mod n
-    if (BN_mod_mul(s.v, e.v, d.v, order(), ctx().bn) != 1 || BN_mod_add(s.v, s.v, k.v, order(), ctx().bn) != 1)
-        return CHIP_ERR_SECP256K1;
-    std::memcpy(sig, rx, 32);
-    if (!bn32(s.v, sig + 32)) return CHIP_ERR_SECP256K1;
+    k1::Sc k = k1::sc_from_be(rnd);
+    int st = CHIP_OK;
+    if (k1::sc_is_zero(k)) st = CHIP_ERR_SECP256K1;  // probability ~2^-256
+    uint8_t kb[32];
+    k1::sc_to_be(k, kb);
+    if (st == CHIP_OK && !k1::to65(k1::mul_g(kb), o)) st = CHIP_ERR_SECP256K1;
+    if (st == CHIP_OK) {
+        std::memcpy(rx, o + 1, 32);
+        k = k1::sc_cond_neg(k, o[64] & 1);  // the nonce with an even y
+        if (!tagged("BIP0340/challenge", rx, 32, px, 32, msg, 32, e32)) st = CHIP_ERR_SECP256K1;
+    }
+    if (st == CHIP_OK) {
+        const k1::Sc s = k1::sc_add(k, k1::sc_mul(k1::sc_from_be(e32), d));  // s = (k + e d) mod n
+        std::memcpy(sig, rx, 32);
+        k1::sc_to_be(s, sig + 32);
+    }
+    k1::sc_clear(d);
+    k1::sc_clear(k);
     OPENSSL_cleanse(dd, 32);
     OPENSSL_cleanse(t, 32);
     OPENSSL_cleanse(rnd, 32);
-    return CHIP_OK;
+    OPENSSL_cleanse(kb, 32);
+    return st;
 }
 
 // BIP-340 verify against the x-only key x32

@@ -348,5 +348,115 @@ inline bool to65(const Pt &p, uint8_t out[65]) {
     return true;
 }
 
+// ---- scalars mod n (BIP-340 signing: s = k + e d, d or n - d) ------------
+// Fixed limb counts and loops, results chosen with masks: the same
+// instructions run whatever the key or nonce (OpenSSL's BIGNUM arithmetic
+// branches on the values).  Reduction mod n as libsecp256k1's: with
+// C = 2^256 - n (129 bits), x = hi 2^256 + lo = hi C + lo (mod n), folded
+// three times, then one conditional subtraction.
+struct Sc {
+    uint64_t v[4];  // little-endian limbs, < n
+};
+
+constexpr uint64_t N0 = 0xBFD25E8CD0364141ull, N1 = 0xBAAEDCE6AF48A03Bull, N2 = 0xFFFFFFFFFFFFFFFEull,
+                   N3 = 0xFFFFFFFFFFFFFFFFull;
+constexpr uint64_t NC[3] = {0x402DA1732FC9BEBFull, 0x4551231950B75FC4ull, 1ull};  // 2^256 - n
+
+// out += a * b (AL x BL limbs); carries run to the end of out (OL limbs)
+template <int AL, int BL, int OL>
+inline void sc_mac(uint64_t (&out)[OL], const uint64_t *a, const uint64_t *b) {
+    for (int i = 0; i < AL; ++i) {
+        uint64_t carry = 0;
+        for (int j = 0; j < BL; ++j) {
+            const u128 acc = (u128)a[i] * b[j] + out[i + j] + carry;
+            out[i + j] = (uint64_t)acc;
+            carry = (uint64_t)(acc >> 64);
+        }
+        for (int k = i + BL; k < OL; ++k) {
+            const u128 acc = (u128)out[k] + carry;
+            out[k] = (uint64_t)acc;
+            carry = (uint64_t)(acc >> 64);
+        }
+    }
+}
+
+// x (5 limbs, < 2n) -> x mod n
+inline Sc sc_reduce_once(const uint64_t (&x)[5]) {
+    unsigned long long s0, s1, s2, s3, s4;
+    unsigned char b = _subborrow_u64(0, x[0], N0, &s0);
+    b = _subborrow_u64(b, x[1], N1, &s1);
+    b = _subborrow_u64(b, x[2], N2, &s2);
+    b = _subborrow_u64(b, x[3], N3, &s3);
+    b = _subborrow_u64(b, x[4], 0, &s4);
+    const uint64_t keep = 0 - (uint64_t)b;  // all ones: x < n
+    Sc r;
+    r.v[0] = (x[0] & keep) | (s0 & ~keep);
+    r.v[1] = (x[1] & keep) | (s1 & ~keep);
+    r.v[2] = (x[2] & keep) | (s2 & ~keep);
+    r.v[3] = (x[3] & keep) | (s3 & ~keep);
+    return r;
+}
+
+// 32 big-endian bytes (any value < 2^256 < 2n) -> value mod n
+inline Sc sc_from_be(const uint8_t b[32]) {
+    uint64_t x[5] = {0, 0, 0, 0, 0};
+    for (int i = 0; i < 32; ++i) x[3 - i / 8] |= (uint64_t)b[i] << (8 * (7 - i % 8));
+    return sc_reduce_once(x);
+}
+
+inline void sc_to_be(const Sc &a, uint8_t b[32]) {
+    for (int i = 0; i < 32; ++i) b[i] = (uint8_t)(a.v[3 - i / 8] >> (8 * (7 - i % 8)));
+}
+
+inline Sc sc_add(const Sc &a, const Sc &b) {
+    uint64_t x[5];
+    unsigned long long t;
+    unsigned char c = _addcarry_u64(0, a.v[0], b.v[0], &t);
+    x[0] = t;
+    c = _addcarry_u64(c, a.v[1], b.v[1], &t);
+    x[1] = t;
+    c = _addcarry_u64(c, a.v[2], b.v[2], &t);
+    x[2] = t;
+    c = _addcarry_u64(c, a.v[3], b.v[3], &t);
+    x[3] = t;
+    x[4] = c;
+    return sc_reduce_once(x);
+}
+
+// neg ? n - a : a, for 0 < a < n
+inline Sc sc_cond_neg(const Sc &a, bool neg) {
+    unsigned long long m0, m1, m2, m3;
+    unsigned char b = _subborrow_u64(0, N0, a.v[0], &m0);
+    b = _subborrow_u64(b, N1, a.v[1], &m1);
+    b = _subborrow_u64(b, N2, a.v[2], &m2);
+    (void)_subborrow_u64(b, N3, a.v[3], &m3);
+    const uint64_t sel = 0 - (uint64_t)neg;
+    Sc r;
+    r.v[0] = (m0 & sel) | (a.v[0] & ~sel);
+    r.v[1] = (m1 & sel) | (a.v[1] & ~sel);
+    r.v[2] = (m2 & sel) | (a.v[2] & ~sel);
+    r.v[3] = (m3 & sel) | (a.v[3] & ~sel);
+    return r;
+}
+
+inline Sc sc_mul(const Sc &a, const Sc &b) {
+    uint64_t l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    sc_mac<4, 4, 8>(l, a.v, b.v);                               // < n^2 < 2^512
+    uint64_t m[7] = {l[0], l[1], l[2], l[3], 0, 0, 0};
+    sc_mac<4, 3, 7>(m, l + 4, NC);                              // < 2^256 + 2^385
+    uint64_t p[5] = {m[0], m[1], m[2], m[3], 0};
+    sc_mac<3, 3, 5>(p, m + 4, NC);                              // m >> 256 < 2^130: < 2^260
+    uint64_t r[5] = {p[0], p[1], p[2], p[3], 0};
+    sc_mac<1, 3, 5>(r, p + 4, NC);                              // p >> 256 < 2^4: < 2^256 + 2^133 < 2n
+    return sc_reduce_once(r);
+}
+
+inline bool sc_is_zero(const Sc &a) { return (a.v[0] | a.v[1] | a.v[2] | a.v[3]) == 0; }
+
+inline void sc_clear(Sc &a) {
+    volatile uint64_t *p = a.v;
+    for (int i = 0; i < 4; ++i) p[i] = 0;
+}
+
 }  // namespace k1
 }  // namespace chip

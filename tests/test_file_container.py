@@ -238,3 +238,24 @@ def test_encode_files_reader_error_raises(ca, tmp_path, monkeypatch):
     monkeypatch.setattr(pathlib.Path, "stat", lambda self, *a, **k: orig(paths[0]) if self == paths[5] else orig(self, *a, **k))
     with pytest.raises(IOError):
         file.encode_files(paths, out, H.sha256(b"w"), 12, slice_objects=2, io_threads=2)
+
+
+def test_sign_scalar_edge_cases_match_oracle(ca):
+    """The constant-time scalar arithmetic mod n (secp256k1_host.hpp sc_*):
+    keys and messages at the edges of the reductions (d = 1, 2, n - 1, n - 2,
+    2^255, all-ones-ish limbs) and random ones, signatures equal to the
+    independent Python restatement's."""
+    from carbonado_amd import _lib
+    L = _lib.lib()
+    n = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+    keys = [1, 2, 3, n - 1, n - 2, 1 << 255, (1 << 255) - 1, n >> 1, (n >> 1) + 1,
+            0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFE00000000000000000000000000000000]
+    keys += [int.from_bytes(H.sha256(b"edge%d" % i), "big") % (n - 1) + 1 for i in range(20)]
+    msgs = [bytes(32), b"\xff" * 32, H.sha256(b"m")]
+    for i, d in enumerate(keys):
+        sk = d.to_bytes(32, "big")
+        msg = msgs[i % 3]
+        aux = H.sha256(b"aux-edge%d" % i) if i % 2 else b"\xff" * 32
+        rc, sig = _sign(L, sk, msg, aux)
+        assert rc == 0 and sig == H.schnorr_sign(sk, msg, aux), i
+    assert _sign(L, n.to_bytes(32, "big"), msgs[0], bytes(32))[0] == 18  # d = n: not a key
