@@ -72,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--objects", type=int, default=1024, help="objects per GPU")
     ap.add_argument("--object-mib", type=float, default=16.0)
+    ap.add_argument("--object-bytes", type=int, default=0,
+                    help="object size in bytes (overrides --object-mib), e.g. 16779371: a 16 MiB object after "
+                         "level 15's snap + ECIES stages, zfec shards of 4,195,328 B")
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=8)
     ap.add_argument("--mode", choices=["encode", "decode", "bao", "bao-decode", "pipeline", "pipeline-decode", "e2e", "e2e-decode", "scrub",
@@ -133,6 +136,8 @@ def parse(argv=None):
                          "`rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (one pass each) before this process "
                          "touches the GPU; auto = on at N=1 for the device-resident modes with one dominant kernel")
     args = ap.parse_args(argv)
+    if args.object_bytes:
+        args.object_mib = args.object_bytes / 2**20  # exact: an integer over a power of two
     if args.config:
         explicit = {a.dest for a in ap._actions if any(o in (argv if argv is not None else sys.argv[1:])
                                                        for o in a.option_strings)}
@@ -468,7 +473,9 @@ class Workload:
             return torch.empty(shape, dtype=torch.uint8, device=dev)
         self.batch_buf = batch_buf
         # bao mode: 16-B aligned object rows for any n (the content mode's rule), handed over whole
-        row = ((n + 15) // 16 * 16 if args.mode == "bao" else n) + args.in_pad_kib * 1024
+        # (bao, pipeline modes: 16-B aligned object rows for any n, the batch entry points' rule)
+        row = ((n + 15) // 16 * 16 if args.mode in ("bao", "pipeline", "pipeline-decode", "bao-decode") else n) + \
+            args.in_pad_kib * 1024
         self.inp_full = batch_buf((count, row), "in")
         self.inp = self.inp_full[:, :n] if row != n else self.inp_full
         self.scatter_s = None
@@ -503,7 +510,7 @@ class Workload:
             self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.encode_scratch(lv, n, count, dev)
-            self.step = lambda: device.encode_batch(lv, self.inp, n, self.out, self.hashes, self.scratch)
+            self.step = lambda: device.encode_batch(lv, self.inp_full, n, self.out, self.hashes, self.scratch)
             # HBM bytes: the object read once, its stream written once.  At Zfec|Bao the fused
             # kernel (K13) hashes the shards on chip; CHIP_FUSED=0 runs K1-BL + K3, which
             # read the 8C bytes of shards back (counted then)
@@ -534,7 +541,7 @@ class Workload:
             self.enc = batch_buf((count, (blen + 15) // 16 * 16), "enc")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             esc = device.encode_scratch(lv, n, count, dev)
-            _, info = device.encode_batch(lv, self.inp, n, self.enc, self.hashes, esc)
+            _, info = device.encode_batch(lv, self.inp_full, n, self.enc, self.hashes, esc)
             torch.cuda.synchronize()
             del esc
             self.pad = info.padding_len
@@ -759,7 +766,7 @@ class Workload:
             self.enc = batch_buf((count, (blen + 15) // 16 * 16), "enc")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.bao_scratch(n, count, dev)
-            device.bao_encode_batch(self.inp, n, self.enc, self.hashes, self.scratch)
+            device.bao_encode_batch(self.inp_full, n, self.enc, self.hashes, self.scratch)
             self.out = batch_buf((count, n), "out")
             self.status = torch.full((count,), -1, dtype=torch.int32, device=dev)
             self.step = lambda: device.bao_decode_batch(self.enc, n, self.hashes, self.out, self.status, self.scratch)
@@ -1036,7 +1043,9 @@ def main():
     world, rank, local = setup_dist(args)
     n = int(args.object_mib * (1 << 20))
     live = None
-    if (not args.dry_run and world == 1 and
+    under_profiler = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ) or \
+        "rocprofiler" in os.environ.get("LD_PRELOAD", "")
+    if (not args.dry_run and world == 1 and not under_profiler and
             (args.live_pmc == "on" or (args.live_pmc == "auto" and pmc_kernel_sym(args) is not None))):
         live = live_traffic(args, sys.argv[1:])  # before this process touches the GPU
     wl = DryRun(args, rank) if args.dry_run else Workload(args, rank, local, world)

@@ -80,6 +80,20 @@ __device__ __forceinline__ void b3_compress(uint32_t (&h)[8], const uint32_t (&m
     for (int i = 0; i < 8; ++i) h[i] = v[i] ^ v[i + 8];
 }
 
+// The same with f(r) called after round r (fused_tune: instructions placed
+// between the rounds, e.g. stores spread over a compression).
+template <class F>
+__device__ __forceinline__ void b3_compress_cb(uint32_t (&h)[8], const uint32_t (&m)[16], uint64_t ctr,
+                                               uint32_t blen, uint32_t flags, F &&f) {
+    uint32_t v[16] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7],
+                      IV(0), IV(1), IV(2), IV(3),
+                      (uint32_t)ctr, (uint32_t)(ctr >> 32), blen, flags};
+    b3_round<0>(v, m); f(0); b3_round<1>(v, m); f(1); b3_round<2>(v, m); f(2); b3_round<3>(v, m); f(3);
+    b3_round<4>(v, m); f(4); b3_round<5>(v, m); f(5); b3_round<6>(v, m); f(6);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = v[i] ^ v[i + 8];
+}
+
 __device__ __forceinline__ void b3_parent(const uint32_t (&l)[8], const uint32_t (&r)[8], bool root,
                                           uint32_t (&out)[8]) {
     uint32_t m[16];

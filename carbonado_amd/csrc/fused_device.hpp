@@ -148,7 +148,7 @@ struct Tree {
 // 2 = no hashing, 3 = no GF (rows get the data shards only), 4 = neither
 // stores nor hashing, 5 = every chunk's lines 128-B aligned (no partial
 // lines), 6 = 5 without hashing, 7 = the line stores' LDS reads without the
-// stores.
+// stores, 8 = the whole-line stores aimed at 8 KiB per wave (L2 hits).
 // FULL: cols % 8 == 0 and no zfec padding (valid >= 4 C): every block is 8
 // whole columns of plain loads, levels 1-3 run in the wave (Tree) and `cv`
 // receives level-3 CVs; otherwise lanes are predicated and `cv` receives the
@@ -160,7 +160,14 @@ struct Tree {
 // bao of the content itself (encoding::bao, encode() level 4; FULL only: the
 // launch covers the whole 64-chunk blocks, bao_tail_kernel the rest).  KIND 1's block is 64 consecutive chunks (row / hash lane
 // L = chunk ub + L), loaded 8 x 16 B per lane per step instead of computed.
-template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true>
+// MP 1: both compressions' message words of a step are read from the rows at
+// once, before the store role's piece reads, so the second compression's LDS
+// reads land while the first one runs (MP 0: each read right before its
+// compression, its latency exposed).
+// SS 1: the step's 8 whole-line stores issued two after each of the first
+// four rounds of the first compression (scheduling barriers around them)
+// instead of as one burst between the compressions.
+template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -334,6 +341,20 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             auto piece = [&](const uint32_t *row, uint32_t x) -> u32x2 {
                 return *reinterpret_cast<const u32x2 *>(reinterpret_cast<const uint8_t *>(row) + 16 + (x & 255u));
             };
+            auto read_msg = [&](int hh, uint32_t (&m)[16]) {
+                const u32x4 *r = reinterpret_cast<const u32x4 *>(rows + lane * RW + dofs(s) + hh * 16);
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const u32x4 x = r[q4];
+                    m[4 * q4] = x.x; m[4 * q4 + 1] = x.y; m[4 * q4 + 2] = x.z; m[4 * q4 + 3] = x.w;
+                }
+            };
+            constexpr bool HS = DG != 2 && DG != 4 && DG != 6;  // hashing on
+            uint32_t mA[16], mB[16];
+            if (MP && HS && mine) {
+                read_msg(0, mA);
+                read_msg(1, mB);
+            }
             constexpr bool ST = DG != 1 && DG != 4;
             u32x4 q[8];
             if (ST && s >= 1) {  // the whole line [d + 128 (s-1), d + 128 s) of every chunk
@@ -345,14 +366,20 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                     q[t] = u32x4{lo.x, lo.y, hi.x, hi.y};
                 }
             }
+            auto one_line = [&](int t) {
+                if (DG == 8)  // diagnostic: the same stores into 8 KiB per wave (L2-resident)
+                    st16<NT>(a.out + ((uint64_t)(blockIdx.x * FW + wave) * 8192 + t * 1024 + lane * 16), q[t]);
+                else
+                    st16<NT>(lat(t, ldd[t] + 128u * (s - 1) + 16u * gl), q[t]);
+            };
             auto line_stores = [&]() {
-                if (ST && s >= 1 && gcol) {
+                if (ST && s >= 1 && gcol && !SS) {
                     if (DG == 7) {  // diagnostic: the piece reads without the line stores
 #pragma unroll
                         for (int t = 0; t < 8; ++t) h[7] ^= q[t].x ^ q[t].w;
                     } else {
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) st16<NT>(lat(t, ldd[t] + 128u * (s - 1) + 16u * gl), q[t]);
+                        for (int t = 0; t < 8; ++t) one_line(t);
                     }
                 }
                 if (ST && (s == 0 || s == 7) && gcol) {
@@ -385,19 +412,35 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
 
             // ---- hash role: blocks 2s, 2s+1 of my chunk ----
             auto hash = [&](int hh) {
-                if (DG == 2 || DG == 4 || DG == 6) {  // keep the rows' reads alive
+                if (!HS) {  // keep the rows' reads alive
                     h[hh] ^= rows[lane * RW + dofs(s) + hh];
                 } else if (mine) {
-                    uint32_t m[16];
-                    const u32x4 *r = reinterpret_cast<const u32x4 *>(rows + lane * RW + dofs(s) + hh * 16);
-#pragma unroll
-                    for (int q4 = 0; q4 < 4; ++q4) {
-                        const u32x4 x = r[q4];
-                        m[4 * q4] = x.x; m[4 * q4 + 1] = x.y; m[4 * q4 + 2] = x.z; m[4 * q4 + 3] = x.w;
-                    }
                     const int b = 2 * s + hh;
                     const uint32_t flags = (b == 0 ? bao::F_CHUNK_START : 0u) | (b == 15 ? bao::F_CHUNK_END : 0u);
-                    bao::b3_compress(h, m, ci, 64, flags);
+                    if (SS && hh == 0) {
+                        uint32_t m[16];
+                        if (MP) {
+#pragma unroll
+                            for (int w = 0; w < 16; ++w) m[w] = mA[w];
+                        } else {
+                            read_msg(0, m);
+                        }
+                        const bool do_st = ST && s >= 1 && gcol && DG != 7;
+                        bao::b3_compress_cb(h, m, ci, 64, flags, [&](int r) {
+                            if (r < 4 && do_st) {
+                                __builtin_amdgcn_sched_barrier(0);
+                                one_line(2 * r);
+                                one_line(2 * r + 1);
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                        });
+                    } else if (MP) {
+                        bao::b3_compress(h, hh ? mB : mA, ci, 64, flags);
+                    } else {
+                        uint32_t m[16];
+                        read_msg(hh, m);
+                        bao::b3_compress(h, m, ci, 64, flags);
+                    }
                 }
             };
             if (ORD >= 1) {
@@ -500,6 +543,128 @@ __global__ __launch_bounds__(64) void bao_tail_kernel(TailArgs a) {
         }
     }
     if (on && (lane & 7) == 0) bao::store_cv(a.cv + (obj * a.cvs + ci / 8) * 32, h);
+}
+
+// Levels 1-3 of the tree from the chunk CVs, for the streams the kernel's
+// FULL path does not cover (8 does not divide the shard's chunk count, e.g.
+// level 15's 4097-chunk shards, or zfec padding): one lane per aligned group
+// of 8 chunks [8g, 8g + 8), its up to 7 parents computed one after another
+// with bao's promotion rule (a node without a right child is its left child),
+// each real node written at its slot (64 l bytes before its leftmost chunk),
+// the level-3 CV stored for the parent kernels, which start at level 4.
+// N > 8, so none of these nodes is the root.  (Three K4 launches with a CV
+// round trip per level did this before: ~2.1 ms per 1024 x 16 MiB step.)
+// NW: how the nodes are written (tools/fused_tune A/B): 1 = eight 8-B stores,
+// 2 = four 16-B stores (8-B aligned), 0 = not at all (diagnostic).
+template <int NW = 1>
+__global__ __launch_bounds__(256) void bao_levels123_kernel(const uint8_t *cv0, uint64_t N, uint64_t count,
+                                                            const uint64_t *coff, uint8_t *out, uint64_t out_stride,
+                                                            uint8_t *cv3, uint64_t n3) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= count * n3) return;
+    const uint64_t obj = gid / n3, g = gid - obj * n3, s0 = 8 * g;
+    const uint32_t cnt = N - s0 < 8 ? (uint32_t)(N - s0) : 8u;
+    uint32_t c[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if ((uint32_t)i < cnt) {
+            bao::load_cv(cv0 + (obj * N + s0 + i) * 32, c[i]);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) c[i][w] = 0u;
+        }
+    }
+    uint8_t *ob = out + obj * out_stride;
+#pragma unroll
+    for (int l = 1; l <= 3; ++l) {
+        const uint32_t span = 1u << l, half = span >> 1;  // chunks per node at level l, and per child
+#pragma unroll
+        for (int q = 0; q < (8 >> l); ++q) {
+            const uint32_t left = q * span;       // first chunk of node q (group-relative)
+            const int li = q * 2, ri = q * 2 + 1;  // child slots at level l - 1
+            if (left + half < cnt) {  // a real node: both children exist
+                uint8_t *node = ob + coff[s0 + left] - 64 * l;
+                if (NW == 1) bao::node_io<0, false>(node, c[li], c[ri]);
+                if (NW == 2) {
+                    auto *q4 = (__attribute__((address_space(1))) bao::u32x4_a8 *)node;
+                    q4[0] = bao::u32x4_a8{c[li][0], c[li][1], c[li][2], c[li][3]};
+                    q4[1] = bao::u32x4_a8{c[li][4], c[li][5], c[li][6], c[li][7]};
+                    q4[2] = bao::u32x4_a8{c[ri][0], c[ri][1], c[ri][2], c[ri][3]};
+                    q4[3] = bao::u32x4_a8{c[ri][4], c[ri][5], c[ri][6], c[ri][7]};
+                }
+                uint32_t p[8];
+                bao::b3_parent(c[li], c[ri], false, p);
+#pragma unroll
+                for (int w = 0; w < 8; ++w) c[q][w] = p[w];
+            } else {  // promoted (or empty): the left child
+#pragma unroll
+                for (int w = 0; w < 8; ++w) c[q][w] = c[li][w];
+            }
+        }
+    }
+    bao::store_cv(cv3 + (obj * n3 + g) * 32, c[0]);
+}
+
+// The same with the node stores coalesced (NW 3): one wave per block; each
+// level's nodes go to LDS first, then the wave writes them four lanes per
+// node, 16 nodes (64 contiguous bytes each) per store instruction instead of
+// 64 lanes at 64 places 8 KiB apart.
+__global__ __launch_bounds__(64) void bao_levels123_lds_kernel(const uint8_t *cv0, uint64_t N, uint64_t count,
+                                                               const uint64_t *coff, uint8_t *out,
+                                                               uint64_t out_stride, uint8_t *cv3, uint64_t n3) {
+    __shared__ bao::u32x4 buf[64 * 4 * 4];  // [lane][node][16-B unit] of the current level
+    __shared__ uint64_t naddr[64 * 4];      // [lane][node]: its slot (0: not a real node)
+    const int lane = threadIdx.x;
+    const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
+    const bool on = gid < count * n3;
+    const uint64_t obj = on ? gid / n3 : 0, g = on ? gid - obj * n3 : 0, s0 = 8 * g;
+    const uint32_t cnt = !on ? 0u : (N - s0 < 8 ? (uint32_t)(N - s0) : 8u);
+    uint32_t c[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if ((uint32_t)i < cnt) {
+            bao::load_cv(cv0 + (obj * N + s0 + i) * 32, c[i]);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) c[i][w] = 0u;
+        }
+    }
+    uint8_t *ob = out + obj * out_stride;
+#pragma unroll
+    for (int l = 1; l <= 3; ++l) {
+        const int nq = 8 >> l;
+        const uint32_t span = 1u << l, half = span >> 1;
+#pragma unroll
+        for (int q = 0; q < (8 >> l); ++q) {
+            const uint32_t left = q * span;
+            const int li = q * 2, ri = q * 2 + 1;
+            const bool real = left + half < cnt;
+            bao::u32x4 *b = buf + (lane * nq + q) * 4;
+            b[0] = bao::u32x4{c[li][0], c[li][1], c[li][2], c[li][3]};
+            b[1] = bao::u32x4{c[li][4], c[li][5], c[li][6], c[li][7]};
+            b[2] = bao::u32x4{c[ri][0], c[ri][1], c[ri][2], c[ri][3]};
+            b[3] = bao::u32x4{c[ri][4], c[ri][5], c[ri][6], c[ri][7]};
+            naddr[lane * nq + q] = real ? (uint64_t)(uintptr_t)(ob + coff[s0 + left] - 64 * l) : 0ull;
+            if (real) {
+                uint32_t p[8];
+                bao::b3_parent(c[li], c[ri], false, p);
+#pragma unroll
+                for (int w = 0; w < 8; ++w) c[q][w] = p[w];
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) c[q][w] = c[li][w];
+            }
+        }
+        bao::wave_sync();
+        for (int i = 0; i < nq * 4; ++i) {  // unit k = i * 64 + lane: node k / 4, 16-B unit k % 4
+            const int k = i * 64 + lane;
+            const uint64_t a = naddr[k >> 2];
+            if (a) *(__attribute__((address_space(1))) bao::u32x4_a8 *)(uintptr_t)(a + 16 * (k & 3)) =
+                bao::u32x4_a8{buf[k].x, buf[k].y, buf[k].z, buf[k].w};
+        }
+        bao::wave_sync();
+    }
+    if (on) bao::store_cv(cv3 + (obj * n3 + g) * 32, c[0]);
 }
 
 }  // namespace fused

@@ -15,6 +15,15 @@ uint64_t zfec_bao_scratch_len(uint64_t zlen, uint64_t count) {
 
 namespace {
 
+// CHIP_L123=0 keeps the K4-per-level path from level 1 for non-FULL streams (A/B)
+bool l123_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_L123");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    return on;
+}
+
 // One launch per part of the batch small enough for the kernel's 32-bit block
 // queue (< 2^31 blocks; a part is whole objects).  cv_nodes: CVs per object
 // the kernel writes into a.cv.
@@ -67,19 +76,29 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
     a.queue = q + QUEUE_K13;
     const bool full = a.cols % 8 == 0 && n >= 4 * C;  // levels 1-3 in the kernel (N >= 64, 8 subtrees a block)
+    // general path: both compressions' message words read at once (MP 1): -1.5 % kernel time
+    // (tools/fused_tune, profiles/r6f/r6h/r6i); the FULL path measured no gain from it
+    constexpr auto KF = zfec_bao_fused_kernel<true, true>;
+    constexpr auto KG = zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1>;
     static bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<true, true>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void *>(zfec_bao_fused_kernel<true, false>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES) == hipSuccess;
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(KF), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)LDS_BYTES) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(KG), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)LDS_BYTES) == hipSuccess;
     }();
     (void)attr;
     (void)hipGetLastError();
     const uint64_t n0 = full ? a.N / 8 : a.N;  // nodes per object in `cv`
-    if ((e = launch_parts(a, n0, full ? zfec_bao_fused_kernel<true, true> : zfec_bao_fused_kernel<true, false>,
-                          stream)) != hipSuccess)
-        return e;
+    if ((e = launch_parts(a, n0, full ? KF : KG, stream)) != hipSuccess) return e;
     uint8_t *next = a.cv + count * n0 * 32;
+    if (!full && a.N > 8 && l123_on()) {  // levels 1-3 in one pass, then from level 4
+        const uint64_t n3 = (a.N + 7) / 8, work = count * n3;
+        hipLaunchKernelGGL(fused::bao_levels123_lds_kernel, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, stream,
+                           a.cv, a.N, count, coff, d_out, out_stride, next, n3);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return bao::run_parent_levels<0, false>(next, n3, n3, 4, a.cv, (n3 + 1) / 2, a.N, count, d_out, out_stride,
+                                                d_hash, nullptr, stream);
+    }
     return bao::run_parent_levels<0, false>(a.cv, n0, n0, full ? 4 : 1, next, (n0 + 1) / 2, a.N, count, d_out,
                                             out_stride, d_hash, nullptr, stream);
 }

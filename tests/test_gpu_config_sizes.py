@@ -137,3 +137,34 @@ def test_zfec_linearity_16mib_batch(gpu):
         torch.cuda.synchronize()
         assert torch.equal(outs[2], outs[0] ^ outs[1])
         assert torch.equal(outs[0][:, :N], a)
+
+
+def test_level15_shape_batch_level12_bit_exact(gpu):
+    """The zfec + bao device batch at the shard length level 15 produces for a
+    16 MiB object (16,779,371 B after snap + ECIES: 4097-chunk shards, 8 does
+    not divide the column count, padding 1941): the fused kernel's general
+    path, then tree levels 1-3 in one pass (bao_levels123_kernel) and the
+    parent kernels from level 4.  Every stream and hash against the oracle."""
+    import torch
+    from carbonado_amd import _lib, device
+    L = _lib.lib()
+    n, count = 16_779_371, 3
+    rng = np.random.default_rng(1515)
+    host = rng.integers(0, 256, (count, n), dtype=np.uint8)
+    row = (n + 15) // 16 * 16
+    inp = torch.zeros((count, row), dtype=torch.uint8)
+    inp[:, :n] = torch.from_numpy(host)
+    inp = inp.cuda()
+    zlen = 8 * 4_195_328
+    blen = L.chip_bao_encoded_len(zlen)
+    out = torch.zeros((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    scratch = device.encode_scratch(12, n, count)
+    _, info = device.encode_batch(12, inp, n, out, hashes, scratch)
+    torch.cuda.synchronize()
+    assert info.padding_len == 1941 and info.chunk_len == 4_195_328
+    for o in range(count):
+        enc, h, _ = O.encode(host[o].tobytes(), 12)
+        assert len(enc) == blen
+        assert out[o, :blen].cpu().numpy().tobytes() == enc, o
+        assert hashes[o].cpu().numpy().tobytes() == h, o

@@ -107,6 +107,14 @@ int main(int argc, char **argv) {
     const char *which = argc > 3 ? argv[3] : "all";
     std::vector<Variant> all = {
         {"K0 FULL (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
+        {"K0 FULL MP1", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 1>, 0},
+        {"K0 FULL ORD2 MP1", fused::zfec_bao_fused_kernel<true, true, 2, 0, 0, true, 1>, 0},
+        {"K1 MP1", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 1>, 1},
+        {"K0 general MP1", fused::zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1>, 0},
+        {"K0 general ORD2", fused::zfec_bao_fused_kernel<true, false, 2, 0, 0, true, 0>, 0},
+        {"K0 general ORD2 MP1", fused::zfec_bao_fused_kernel<true, false, 2, 0, 0, true, 1>, 0},
+        {"K0 FULL ORD2 NT0", fused::zfec_bao_fused_kernel<false, true, 2, 0, 0>, 0},
+        {"K0 general ORD2 NT0", fused::zfec_bao_fused_kernel<false, false, 2, 0, 0>, 0},
         {"K0 FULL ORD0", fused::zfec_bao_fused_kernel<true, true, 0, 0, 0>, 0},
         {"K0 FULL ORD2", fused::zfec_bao_fused_kernel<true, true, 2, 0, 0>, 0},
         {"K0 FULL ORD3", fused::zfec_bao_fused_kernel<true, true, 3, 0, 0>, 0},
@@ -117,11 +125,18 @@ int main(int argc, char **argv) {
         {"K0 DG1 no line stores/reads", fused::zfec_bao_fused_kernel<true, true, 1, 1, 0>, 0},
         {"K0 DG7 piece reads, no stores", fused::zfec_bao_fused_kernel<true, true, 1, 7, 0>, 0},
         {"K0 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 0>, 0},
+        {"K0 DG8 line stores to L2", fused::zfec_bao_fused_kernel<true, true, 1, 8, 0>, 0},
+        {"K0 FULL SS1", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 1>, 0},
+        {"K0 FULL SS1 ORD2", fused::zfec_bao_fused_kernel<true, true, 2, 0, 0, true, 0, 1>, 0},
+        {"K0 general SS1 MP1", fused::zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 1>, 0},
+        {"K1 SS1", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 0, 1>, 1},
+        {"K0 DG8 ORD2 line stores to L2", fused::zfec_bao_fused_kernel<true, true, 2, 8, 0>, 0},
         {"K0 DG5 aligned lines", fused::zfec_bao_fused_kernel<true, true, 1, 5, 0>, 0},
         {"K1 DG5 aligned lines", fused::zfec_bao_fused_kernel<true, true, 1, 5, 1>, 1},
         {"K1 DG1 no line stores/reads", fused::zfec_bao_fused_kernel<true, true, 1, 1, 1>, 1},
         {"K1 DG7 piece reads, no stores", fused::zfec_bao_fused_kernel<true, true, 1, 7, 1>, 1},
-        {"K1 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 1>, 1}};
+        {"K1 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 1>, 1},
+        {"K0 FULL (product, again)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0}};
     std::vector<Variant> vs;
     for (auto &v : all)
         if (!strcmp(which, "all") || strstr(v.name.c_str(), which)) vs.push_back(v);
@@ -154,6 +169,39 @@ int main(int argc, char **argv) {
                 sums[v] = checksum(out, count * bstride) ^ (checksum(cv, count * N0 * 32) * 3);
             }
         }
+    {  // levels 1-3 from level-0 CVs (what the general path adds): bao_levels123_kernel, node-store variants
+        const uint64_t N = N0, n3 = N / 8, work = count * n3;
+        uint8_t *cv3;
+        CK(hipMalloc(&cv3, count * n3 * 32));
+        void (*kv[4])(const uint8_t *, uint64_t, uint64_t, const uint64_t *, uint8_t *, uint64_t, uint8_t *, uint64_t) = {
+            fused::bao_levels123_kernel<1>, fused::bao_levels123_kernel<2>, fused::bao_levels123_kernel<0>,
+            fused::bao_levels123_lds_kernel};
+        const char *kn[4] = {"8-B node stores (product)", "16-B node stores", "no node stores (diagnostic)",
+                             "LDS-staged node stores, 4 lanes per node"};
+        std::vector<float> t3[4];
+        unsigned long long sum3[4] = {0, 0, 0, 0};
+        for (int rd = 0; rd < rounds + 1; ++rd)
+            for (int k = 0; k < 4; ++k) {
+                const int tpb = k == 3 ? 64 : 256;
+                CK(hipEventRecord(e0));
+                hipLaunchKernelGGL(kv[k], dim3((unsigned)((work + tpb - 1) / tpb)), dim3(tpb), 0, 0, cv, N, count,
+                                   dcoff[0], out, bstride, cv3, n3);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float t;
+                CK(hipEventElapsedTime(&t, e0, e1));
+                if (rd) t3[k].push_back(t);
+                if (rd == 0) sum3[k] = checksum(out, count * bstride) ^ (checksum(cv3, count * n3 * 32) * 3);
+            }
+        printf("levels 1-3 outputs: LDS-staged %s 8-B stores; 16-B %s\n", sum3[3] == sum3[0] ? "==" : "!=",
+               sum3[1] == sum3[0] ? "==" : "!=");
+        for (int k = 0; k < 4; ++k) {
+            std::sort(t3[k].begin(), t3[k].end());
+            printf("levels 1-3 from chunk CVs (bao_levels123_kernel), %s, %llu objects: median %.3f ms\n", kn[k],
+                   (unsigned long long)count, t3[k][t3[k].size() / 2]);
+        }
+        CK(hipFree(cv3));
+    }
     for (size_t v = 0; v < vs.size(); ++v) {
         auto t = ms[v];
         std::sort(t.begin(), t.end());
