@@ -25,6 +25,12 @@ constexpr int K3_WAVES = 4;
 constexpr int K3_TPB = 64 * K3_WAVES;
 constexpr int ROWW = 36;  // LDS words per staged chunk row: [_, _, carry w30, w31 | 32 data words]
 constexpr int ROW0 = 4;   // first data word (16-B aligned; stride 36 keeps b128 reads conflict-free)
+// verify-decode reads each chunk pair's level-1 node with the pair's first
+// loads (K3 MODE 1, CPL 2); -DBAO_DEC_PREFETCH_DEF=0 builds the old order (A/B)
+#ifndef BAO_DEC_PREFETCH_DEF
+#define BAO_DEC_PREFETCH_DEF 1
+#endif
+constexpr bool BAO_DEC_PREFETCH = BAO_DEC_PREFETCH_DEF;
 
 __host__ __device__ constexpr uint32_t IV(int i) {
     return i == 0 ? 0x6A09E667u : i == 1 ? 0xBB67AE85u : i == 2 ? 0x3C6EF372u
@@ -643,6 +649,18 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
         for (int w = 0; w < 8; ++w) h[w] = IV(w);
         uint32_t L[LOG + 1][8];  // pending left nodes per level (CV stack)
         bool ok = true;
+        // Verify-decode (CPL 2): the stored level-1 node of the lane's chunk
+        // pair sits in the 64 bytes just before its first chunk, in lines the
+        // step-0 loads fetch anyway.  Read it now, with them, instead of at
+        // the pair's end (step 15), when those lines have long left L2 and
+        // are fetched again (decode read 1.18x its stream).
+        constexpr bool PN = MODE == 1 && CPL == 2 && BAO_DEC_PREFETCH;
+        u32x4 pnode[4];
+        if (PN && nmine == 2) {
+            const uint8_t *np = ib + my_off - 64;
+    #pragma unroll
+            for (int q = 0; q < 4; ++q) pnode[q] = load16_a8(np + 16 * q);
+        }
 
         u32x4 pre[8];
         load_step(0, pre);
@@ -720,7 +738,15 @@ __global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
                         if (bit) {
                             const uint64_t sl = lb + ((uint64_t)(j >> (lv + 1)) << (lv + 1));
                             const bool root = a.N <= (2ull << lv);
-                            if (ob || MODE == 1) {
+                            if (PN && lv == 0) {  // the level-1 node read at step 0
+                                const uint32_t *l = L[0];
+                                ok &= pnode[0].x == l[0] && pnode[0].y == l[1] && pnode[0].z == l[2] &&
+                                      pnode[0].w == l[3] && pnode[1].x == l[4] && pnode[1].y == l[5] &&
+                                      pnode[1].z == l[6] && pnode[1].w == l[7] && pnode[2].x == h[0] &&
+                                      pnode[2].y == h[1] && pnode[2].z == h[2] && pnode[2].w == h[3] &&
+                                      pnode[3].x == h[4] && pnode[3].y == h[5] && pnode[3].z == h[6] &&
+                                      pnode[3].w == h[7];
+                            } else if (ob || MODE == 1) {
                                 uint8_t *node = (MODE == 0 ? ob : const_cast<uint8_t *>(ib)) +
                                                 parent_stream_off(sl, lv + 1, a.N);
                                 ok &= node_io<MODE == 3 ? 0 : MODE, NTS>(node, L[lv], h);
