@@ -87,6 +87,37 @@ __global__ __launch_bounds__(256) void chain_kernel(uint32_t *out, Stamp *st, in
     }
 }
 
+// The mix4 instructions grouped by class: 16 chains, each class applied to
+// all 16 before the next class (64 instructions per loop iteration, the same
+// multiset as mix4's).
+__global__ __launch_bounds__(256) void mixg_kernel(uint32_t *out, Stamp *st, int iters, uint32_t a, uint32_t b) {
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = threadIdx.x * 7u + i;
+    const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(x[i]));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[i]) : "v"(a), "v"(b));
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s ^= x[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+    if ((threadIdx.x & 63) == 0) {
+        Stamp v{t0, t1, r0, r1};
+        st[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = v;
+    }
+}
+
 // NS independent BLAKE3 compressions per lane per iteration (the product's
 // b3_compress: 7 rounds x 8 G, 12 VALU per G = 672 per compression).
 template <int NS>
@@ -143,9 +174,40 @@ __device__ __forceinline__ void gv(uint32_t &a, uint32_t &b, uint32_t &c, uint32
     c = c + d;
     b = chip::bao::rotr(b ^ c, 7);
 }
+#define ADD3(d, x, y) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(d) : "v"(x), "v"(y))
+#define XOR(d, x) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(d) : "v"(x))
+#define ROT(d, n) asm volatile("v_alignbit_b32 %0, %0, %0, " #n : "+v"(d))
+#define ADD(d, x) asm volatile("v_add_u32 %0, %0, %1" : "+v"(d) : "v"(x))
+// four G's at once, each step applied to the four before the next step
+__device__ __forceinline__ void g4(uint32_t &a0, uint32_t &b0, uint32_t &c0, uint32_t &d0, uint32_t &a1, uint32_t &b1,
+                                   uint32_t &c1, uint32_t &d1, uint32_t &a2, uint32_t &b2, uint32_t &c2, uint32_t &d2,
+                                   uint32_t &a3, uint32_t &b3, uint32_t &c3, uint32_t &d3, uint32_t x0, uint32_t y0,
+                                   uint32_t x1, uint32_t y1, uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) {
+    ADD3(a0, b0, x0); ADD3(a1, b1, x1); ADD3(a2, b2, x2); ADD3(a3, b3, x3);
+    XOR(d0, a0); XOR(d1, a1); XOR(d2, a2); XOR(d3, a3);
+    ROT(d0, 16); ROT(d1, 16); ROT(d2, 16); ROT(d3, 16);
+    ADD(c0, d0); ADD(c1, d1); ADD(c2, d2); ADD(c3, d3);
+    XOR(b0, c0); XOR(b1, c1); XOR(b2, c2); XOR(b3, c3);
+    ROT(b0, 12); ROT(b1, 12); ROT(b2, 12); ROT(b3, 12);
+    ADD3(a0, b0, y0); ADD3(a1, b1, y1); ADD3(a2, b2, y2); ADD3(a3, b3, y3);
+    XOR(d0, a0); XOR(d1, a1); XOR(d2, a2); XOR(d3, a3);
+    ROT(d0, 8); ROT(d1, 8); ROT(d2, 8); ROT(d3, 8);
+    ADD(c0, d0); ADD(c1, d1); ADD(c2, d2); ADD(c3, d3);
+    XOR(b0, c0); XOR(b1, c1); XOR(b2, c2); XOR(b3, c3);
+    ROT(b0, 7); ROT(b1, 7); ROT(b2, 7); ROT(b3, 7);
+}
 template <int VAR, int R>
 __device__ __forceinline__ void rv(uint32_t (&v)[16], const uint32_t (&m)[16]) {
     using chip::bao::SCHED;
+    if constexpr (VAR == 3) {
+        g4(v[0], v[4], v[8], v[12], v[1], v[5], v[9], v[13], v[2], v[6], v[10], v[14], v[3], v[7], v[11], v[15],
+           m[SCHED(R, 0)], m[SCHED(R, 1)], m[SCHED(R, 2)], m[SCHED(R, 3)], m[SCHED(R, 4)], m[SCHED(R, 5)],
+           m[SCHED(R, 6)], m[SCHED(R, 7)]);
+        g4(v[0], v[5], v[10], v[15], v[1], v[6], v[11], v[12], v[2], v[7], v[8], v[13], v[3], v[4], v[9], v[14],
+           m[SCHED(R, 8)], m[SCHED(R, 9)], m[SCHED(R, 10)], m[SCHED(R, 11)], m[SCHED(R, 12)], m[SCHED(R, 13)],
+           m[SCHED(R, 14)], m[SCHED(R, 15)]);
+        return;
+    }
     gv<VAR>(v[0], v[4], v[8], v[12], m[SCHED(R, 0)], m[SCHED(R, 1)]);
     gv<VAR>(v[1], v[5], v[9], v[13], m[SCHED(R, 2)], m[SCHED(R, 3)]);
     gv<VAR>(v[2], v[6], v[10], v[14], m[SCHED(R, 4)], m[SCHED(R, 5)]);
@@ -316,11 +378,19 @@ int main(int argc, char **argv) {
     probe_op<LSHLADD>(iters);
     probe_op<XORSDWA>(iters);
     probe_op<MIX>(iters / 4);
+    for (int W : {2, 4, 8}) {
+        Result r = run([&](int blocks, uint32_t *o, Stamp *s) {
+            mixg_kernel<<<blocks, 256>>>(o, s, iters / 4, 0x9E3779B9u, 0x85EBCA6Bu);
+        }, W, 64.0 * (iters / 4), 3);
+        printf("mix4 grouped     W=%d  %8.3f ms  %7.2f T lane-instr/s  (mix4 row: ops counted in groups of 4)\n", W,
+               r.ms, r.lane_ops_t);
+    }
     probe_b3<1>(iters / 64);
     probe_b3<2>(iters / 128);
     std::vector<uint32_t> ref;
     probe_b3v<0>(iters / 64, &ref);
     probe_b3v<1>(iters / 64, &ref);
     probe_b3v<2>(iters / 64, &ref);
+    probe_b3v<3>(iters / 64, &ref);
     return 0;
 }
