@@ -38,15 +38,16 @@ sys.path.insert(0, str(ROOT))
 
 from carbonado_amd.sharding import max_over_ranks, object_range  # noqa: E402
 
-# BLAKE3 ceiling, measured (tools/valu_probe.hip, profiles/r6b_valu_probe.txt): the product's b3_compress
-# in a register-only loop at 8 waves/SIMD runs 5.685e10 compressions/s = 38.2 T "672-op" lane-ops/s.
-# gfx950 issues the VOP2 int ops (v_add_u32, v_xor_b32) and v_bitop3_b32 at the full SIMD-32 rate
-# (~69 T lane-ops/s measured, 78.6 nominal) but v_add3_u32, v_alignbit_b32, v_perm_b32, v_lshl_add_u32
-# and SDWA forms at half rate (~38 T); half of a compression's instructions are of the second kind.
-VALU_PEAK_TOPS = 38.2
-VALU_PEAK_SRC = ("measured BLAKE3 ceiling: b3_compress register loop, 8 waves/SIMD, 5.685e10 compressions/s x 672 "
-                 "(tools/valu_probe.hip, profiles/r6b_valu_probe.txt); VOP2 add/xor run at ~69 T lane-ops/s, the "
-                 "VOP3 add3/alignbit at ~38 T")
+# BLAKE3 ceiling, measured (tools/valu_probe.hip, profiles/r6q_valu_probe.txt): the product's b3_compress
+# (four G's issued step by step, b3_g4) in a register-only loop at 8 waves/SIMD runs 6.125e10
+# compressions/s = 41.2 T "672-op" lane-ops/s.  gfx950 issues the VOP2 int ops (v_add_u32, v_xor_b32)
+# and v_bitop3_b32 at the full SIMD-32 rate (~69 T lane-ops/s measured, 78.6 nominal) but v_add3_u32,
+# v_alignbit_b32, v_perm_b32, v_lshl_add_u32 and SDWA forms at half rate (~38 T); half of a
+# compression's instructions are of the second kind.
+VALU_PEAK_TOPS = 41.2
+VALU_PEAK_SRC = ("measured BLAKE3 ceiling: the product's b3_compress (b3_g4 order) in a register loop, 8 waves/SIMD, "
+                 "6.125e10 compressions/s x 672 (tools/valu_probe.hip VAR 3, profiles/r6q_valu_probe.txt); VOP2 "
+                 "add/xor issue at ~69 T lane-ops/s, the VOP3 add3/alignbit at ~38 T")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "GiB/s device-resident zfec 4-of-8 encode, 16 MiB objects; % HBM roofline"
 SEED = 0xCA4B0AD0
