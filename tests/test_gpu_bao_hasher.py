@@ -108,11 +108,13 @@ def test_hasher_churn_recycles_queue_blocks(gpu):
 
 
 @pytest.mark.parametrize("piece,total", [(4 << 20, (16 << 20) + 5), (65536, (2 << 20)), (65537, (2 << 20) + 999),
-                                         (1000, 300_000), (1 << 20, 64 << 20)])
+                                         (1000, 300_000), (1 << 20, 64 << 20), ((3 << 20) + 7, (40 << 20) + 3),
+                                         (32 << 20, (96 << 20) + 65536)])
 def test_hasher_incremental_appends(gpu, piece, total):
     """Appends of fixed size at chunk- and unit-misaligned boundaries: the
-    chunks hashed during update() (64-chunk units with bytes past them) plus
-    the ones finalize() hashes give the one-shot stream and hash."""
+    chunks hashed during update() (64-chunk units with bytes past them, one
+    launch per 32 MiB of them) plus the ones finalize() hashes give the
+    one-shot stream and hash."""
     from carbonado_amd.utils import BaoHasher
     rng = np.random.default_rng(piece ^ total)
     data = rng.integers(0, 256, total, dtype=np.uint8).tobytes()
@@ -129,7 +131,7 @@ def test_hasher_incremental_pinned_appends(gpu):
     boundaries inside appends; then the same hasher's stream vs the oracle."""
     import torch
     from carbonado_amd.utils import BaoHasher
-    total = (12 << 20) + 4097
+    total = (40 << 20) + 4097  # past the 32 MiB of units that trigger hashing during update()
     src = torch.randint(0, 256, (total,), dtype=torch.uint8).pin_memory()
     h = BaoHasher()
     piece = (4 << 20) - 3
