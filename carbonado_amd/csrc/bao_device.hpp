@@ -76,11 +76,56 @@ constexpr bool B3_GROUPED = B3_GROUPED_DEF;
 #define B3_XOR(d, x) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(d) : "v"(x))
 #define B3_ROT(d, n) asm volatile("v_alignbit_b32 %0, %0, %0, " #n : "+v"(d))
 #define B3_ADD(d, x) asm volatile("v_add_u32 %0, %0, %1" : "+v"(d) : "v"(x))
+// One asm statement per four G's (B3_ONEASM 1) with an `s_nop 0` after each
+// group of four VOP2 ops (the xors and adds), none after the VOP3 groups
+// (add3, alignbit).  With one statement per instruction the hazard
+// recognizer, blind inside asm, puts an `s_nop 0` before every group that
+// reads the previous group's results.  Measured (tools/valu_probe.hip VAR 3/4/6/7,
+// profiles/r7c, r7d): without any nop the compression loop runs 6 % slower at 8
+// waves/SIMD (5.73 vs 6.11e10/s) — a group issued right behind four
+// full-rate VOP2 producers stalls on them — and with nops after the VOP2
+// groups only it runs as fast at 8 waves and ~1 % faster at 2-3 waves
+// (5.60/5.76 vs 5.55/5.69e10/s), the occupancies of K13 and verify-decode.
+#ifndef B3_ONEASM_DEF
+#define B3_ONEASM_DEF 1
+#endif
 __device__ __forceinline__ void b3_g4(uint32_t &a0, uint32_t &b0, uint32_t &c0, uint32_t &d0, uint32_t &a1,
                                       uint32_t &b1, uint32_t &c1, uint32_t &d1, uint32_t &a2, uint32_t &b2,
                                       uint32_t &c2, uint32_t &d2, uint32_t &a3, uint32_t &b3, uint32_t &c3,
                                       uint32_t &d3, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t x2,
                                       uint32_t y2, uint32_t x3, uint32_t y3) {
+    if constexpr (B3_ONEASM_DEF) {
+        // operands: a0..a3 = 0..3, b = 4..7, c = 8..11, d = 12..15, x = 16..19, y = 20..23
+        asm volatile(
+            "v_add3_u32 %0, %0, %4, %16\n\tv_add3_u32 %1, %1, %5, %17\n\t"
+            "v_add3_u32 %2, %2, %6, %18\n\tv_add3_u32 %3, %3, %7, %19\n\t"
+            "v_xor_b32 %12, %12, %0\n\tv_xor_b32 %13, %13, %1\n\tv_xor_b32 %14, %14, %2\n\tv_xor_b32 %15, %15, %3\n\t"
+            "s_nop 0\n\t"
+            "v_alignbit_b32 %12, %12, %12, 16\n\tv_alignbit_b32 %13, %13, %13, 16\n\t"
+            "v_alignbit_b32 %14, %14, %14, 16\n\tv_alignbit_b32 %15, %15, %15, 16\n\t"
+            "v_add_u32 %8, %8, %12\n\tv_add_u32 %9, %9, %13\n\tv_add_u32 %10, %10, %14\n\tv_add_u32 %11, %11, %15\n\t"
+            "s_nop 0\n\t"
+            "v_xor_b32 %4, %4, %8\n\tv_xor_b32 %5, %5, %9\n\tv_xor_b32 %6, %6, %10\n\tv_xor_b32 %7, %7, %11\n\t"
+            "s_nop 0\n\t"
+            "v_alignbit_b32 %4, %4, %4, 12\n\tv_alignbit_b32 %5, %5, %5, 12\n\t"
+            "v_alignbit_b32 %6, %6, %6, 12\n\tv_alignbit_b32 %7, %7, %7, 12\n\t"
+            "v_add3_u32 %0, %0, %4, %20\n\tv_add3_u32 %1, %1, %5, %21\n\t"
+            "v_add3_u32 %2, %2, %6, %22\n\tv_add3_u32 %3, %3, %7, %23\n\t"
+            "v_xor_b32 %12, %12, %0\n\tv_xor_b32 %13, %13, %1\n\tv_xor_b32 %14, %14, %2\n\tv_xor_b32 %15, %15, %3\n\t"
+            "s_nop 0\n\t"
+            "v_alignbit_b32 %12, %12, %12, 8\n\tv_alignbit_b32 %13, %13, %13, 8\n\t"
+            "v_alignbit_b32 %14, %14, %14, 8\n\tv_alignbit_b32 %15, %15, %15, 8\n\t"
+            "v_add_u32 %8, %8, %12\n\tv_add_u32 %9, %9, %13\n\tv_add_u32 %10, %10, %14\n\tv_add_u32 %11, %11, %15\n\t"
+            "s_nop 0\n\t"
+            "v_xor_b32 %4, %4, %8\n\tv_xor_b32 %5, %5, %9\n\tv_xor_b32 %6, %6, %10\n\tv_xor_b32 %7, %7, %11\n\t"
+            "s_nop 0\n\t"
+            "v_alignbit_b32 %4, %4, %4, 7\n\tv_alignbit_b32 %5, %5, %5, 7\n\t"
+            "v_alignbit_b32 %6, %6, %6, 7\n\tv_alignbit_b32 %7, %7, %7, 7"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3),
+              "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3)
+            : "v"(x0), "v"(x1), "v"(x2), "v"(x3), "v"(y0), "v"(y1), "v"(y2), "v"(y3));
+        return;
+    }
     B3_ADD3(a0, b0, x0); B3_ADD3(a1, b1, x1); B3_ADD3(a2, b2, x2); B3_ADD3(a3, b3, x3);
     B3_XOR(d0, a0); B3_XOR(d1, a1); B3_XOR(d2, a2); B3_XOR(d3, a3);
     B3_ROT(d0, 16); B3_ROT(d1, 16); B3_ROT(d2, 16); B3_ROT(d3, 16);

@@ -78,6 +78,19 @@ __device__ __forceinline__ uint32_t gf_addr(uint32_t x, int b, uint32_t tb) {
     return ((x >> (8 * b)) & 0xFFu) * ROWB + tb;
 }
 
+// The four table addresses of x's bytes in four VALU ops (GFP): the address
+// pair of bytes 0 and 2 (hi = 0) or 1 and 3 (hi = 1) in one register, byte k
+// times 64 in bits 6-13 / 22-29 and tb in both halves' low 6 bits, then split
+// with a mask and a shift.  Per byte that is 1 VOP3 + 1.5 VOP2 against 2 VALU
+// (one a VOP3, often both) for gf_addr.  The and-or is asm: written in C the
+// compiler folds the halves back into per-byte extracts.
+__device__ __forceinline__ uint32_t gf_pair(uint32_t x, int hi, uint32_t tb2) {
+    const uint32_t sh = hi ? x >> 2 : x << 6;
+    uint32_t t;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(t) : "v"(sh), "s"(0x3FC03FC0u), "v"(tb2));
+    return t;
+}
+
 template <bool NT>
 __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
     if (NT) __builtin_nontemporal_store(v, bao::glb(reinterpret_cast<u32x4 *>(p)));
@@ -167,7 +180,12 @@ struct Tree {
 // SS 1: the step's 8 whole-line stores issued two after each of the first
 // four rounds of the first compression (scheduling barriers around them)
 // instead of as one burst between the compressions.
-template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0>
+// O32: every object's input and stream are < 4 GiB (the host checks), so
+// loads and stores address them as the wave's object base (SGPRs) plus a
+// 32-bit per-lane offset: global_load/store with saddr, no 64-bit VALU adds
+// per access.  GFP 1: table addresses through gf_pair.
+template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
+          bool O32 = false, int GFP = 0>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -187,11 +205,12 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     const int lane = threadIdx.x & 63;
     uint32_t *rows = reinterpret_cast<uint32_t *>(lds + TAB_BYTES) + wave * 64 * RW;
     const int rep = lane % FR, grp = (lane & 31) / FR;
-    uint32_t tb[4];
+    uint32_t tb[4], tb2[4];
     uint64_t ioff[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {  // lane group grp walks the data shards in the rotated order (j + grp) mod 4
         tb[j] = (uint32_t)((((j + grp) & 3) * FR + rep) * 4);
+        tb2[j] = tb[j] | (tb[j] << 16);
         ioff[j] = (uint64_t)((j + grp) & 3) * a.C;
     }
     const int gl = lane & 7, cu = lane >> 3;
@@ -206,6 +225,12 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * BW;
         const uint8_t *ib = a.in + obj * a.in_stride;
         if (KIND == 1) {  // chunk ub + 8 t + cu, bytes 128 s + 16 gl
+            if (O32) {
+                const uint32_t o = (uint32_t)((ub + cu) * 1024) + 128u * s + 16u * gl;
+#pragma unroll
+                for (int t = 0; t < NV; ++t) v[t] = *reinterpret_cast<const u32x4 *>(ib + (uint64_t)(o + 8192u * t));
+                return;
+            }
             const uint8_t *b = ib + (ub + cu) * 1024 + 128 * (uint64_t)s + 16 * gl;
 #pragma unroll
             for (int t = 0; t < NV; ++t) v[t] = *reinterpret_cast<const u32x4 *>(b + (uint64_t)t * 8192);
@@ -215,7 +240,9 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         const bool full = FULL || (ub + 8 <= a.cols && 3 * a.C + (ub + 8) * 1024 <= a.valid);  // wave-uniform
         if (full) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const u32x4 *>(ib + ioff[j] + off);
+            for (int j = 0; j < 4; ++j)
+                v[j] = O32 ? *reinterpret_cast<const u32x4 *>(ib + (uint64_t)((uint32_t)ioff[j] + (uint32_t)off))
+                           : *reinterpret_cast<const u32x4 *>(ib + ioff[j] + off);
         } else if (KIND == 0) {
             const bool col = ub + cu < a.cols;
 #pragma unroll
@@ -251,7 +278,8 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         const bool mine = FULL || hu < a.cols;
         const uint64_t ci = (uint64_t)(lane >> 3) * TS + hu;
         const uint64_t hco = FULL ? a.coff[ci] : 0;          // tree role: my chunk's stream offset
-        uint8_t *lsp[8];
+        uint8_t *lsp[8];   // !O32: chunk (t, ub + cu)'s slot
+        uint32_t lso[8];   // O32: its offset in the stream
         uint32_t ldd[8];
         {
             uint64_t co[8];  // all 8 offset loads in flight together
@@ -260,12 +288,26 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             for (int t = 0; t < 8; ++t) co[t] = a.coff[(uint64_t)t * TS + c0];
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                lsp[t] = ob + co[t];
-                if (DG == 5 || DG == 6) lsp[t] = reinterpret_cast<uint8_t *>((uintptr_t)lsp[t] & ~(uintptr_t)127);
-                ldd[t] = (DG == 5 || DG == 6) ? 0u : (uint32_t)(-(uintptr_t)lsp[t]) & 127u;
+                uint8_t *p = ob + co[t];
+                if (DG == 5 || DG == 6) p = reinterpret_cast<uint8_t *>((uintptr_t)p & ~(uintptr_t)127);
+                ldd[t] = (DG == 5 || DG == 6) ? 0u : (uint32_t)(-(uintptr_t)p) & 127u;
+                if (O32) lso[t] = (uint32_t)(p - ob);
+                else lsp[t] = p;
             }
         }
-        auto lat = [&](int t, uint32_t x) -> uint8_t * { return lsp[t] + x; };
+        auto lat = [&](int t, uint32_t x) -> uint8_t * {
+            return O32 ? ob + (uint64_t)(lso[t] + x) : lsp[t] + x;
+        };
+        // head/tail stores (steps 0 and 7): their offsets do not depend on the
+        // step, and hoisted out of the step loop they become 24 64-bit
+        // addresses held across it (+17 VGPRs); the empty asm keeps each one
+        // computed where it is used, folded into the store's saddr form
+        auto lat_ht = [&](int t, uint32_t x) -> uint8_t * {
+            if (!O32) return lsp[t] + x;
+            uint32_t o = lso[t] + x;
+            asm volatile("" : "+v"(o));
+            return ob + (uint64_t)o;
+        };
         uint32_t h[8];
 #pragma unroll
         for (int w = 0; w < 8; ++w) h[w] = bao::IV(w);
@@ -287,15 +329,22 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                 // left it one register for them, an lgkmcnt(0) per lookup)
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
-                    uint32_t x[4];
+                    uint32_t x[4], ad[4][4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) x[j] = zf::comp(v[j], d);
+                    for (int j = 0; j < 4; ++j) {
+                        x[j] = zf::comp(v[j], d);
+                        if (GFP) {
+                            const uint32_t t02 = gf_pair(x[j], 0, tb2[j]), t13 = gf_pair(x[j], 1, tb2[j]);
+                            ad[j][0] = t02 & 0xFFFFu; ad[j][2] = t02 >> 16;
+                            ad[j][1] = t13 & 0xFFFFu; ad[j][3] = t13 >> 16;
+                        }
+                    }
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         uint32_t e[4];
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
-                            e[j] = *reinterpret_cast<const uint32_t *>(lds + gf_addr(x[j], b, tb[j]));
+                            e[j] = *reinterpret_cast<const uint32_t *>(lds + (GFP ? ad[j][b] : gf_addr(x[j], b, tb[j])));
                         // v_bitop3 (gfx950): three of the four terms in one instruction
                         acc[d * 4 + b] = __builtin_amdgcn_bitop3_b32(e[0], e[1], e[2], 0x96) ^ e[3];
                     }
@@ -389,19 +438,19 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                         const uint32_t *row = rows + (t * 8 + cu) * RW;
                         if (s == 0) {  // head [0, d)
                             const uint32_t hd = d & 8u;
-                            if (hd && gl == 0) *bao::glb(reinterpret_cast<u32x2 *>(lat(t, 0))) = piece(row, 0);
+                            if (hd && gl == 0) *bao::glb(reinterpret_cast<u32x2 *>(lat_ht(t, 0))) = piece(row, 0);
                             const uint32_t x = 16u * gl + hd;
                             if (x + 16 <= d) {
                                 const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                                *bao::glb(reinterpret_cast<u32x4 *>(lat(t, x))) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                                *bao::glb(reinterpret_cast<u32x4 *>(lat_ht(t, x))) = u32x4{lo.x, lo.y, hi.x, hi.y};
                             }
                         } else {  // tail [896 + d, 1024)
                             const uint32_t x = 896u + d + 16u * gl;
                             if (x + 16 <= 1024) {
                                 const u32x2 lo = piece(row, x), hi = piece(row, x + 8);
-                                *bao::glb(reinterpret_cast<u32x4 *>(lat(t, x))) = u32x4{lo.x, lo.y, hi.x, hi.y};
+                                *bao::glb(reinterpret_cast<u32x4 *>(lat_ht(t, x))) = u32x4{lo.x, lo.y, hi.x, hi.y};
                             } else if (x + 8 == 1024) {
-                                *bao::glb(reinterpret_cast<u32x2 *>(lat(t, x))) = piece(row, x);
+                                *bao::glb(reinterpret_cast<u32x2 *>(lat_ht(t, x))) = piece(row, x);
                             }
                         }
                     }

@@ -15,6 +15,21 @@ uint64_t zfec_bao_scratch_len(uint64_t zlen, uint64_t count) {
 
 namespace {
 
+// K13 with 32-bit per-lane offsets from the object bases (O32) and the
+// packed GF table addresses (GFP); -DK13_O32_DEF=0 / -DK13_GFP_DEF=0 build
+// the 64-bit-address / per-byte-address forms for A/B.
+#ifndef K13_O32_DEF
+#define K13_O32_DEF 1
+#endif
+#ifndef K13_GFP_DEF
+#define K13_GFP_DEF 1
+#endif
+constexpr bool K13_O32 = K13_O32_DEF;
+constexpr int K13_GFP = K13_GFP_DEF;
+// the stream of an object of shard length C is < 8.6 C bytes and its input
+// 4 C: 32-bit offsets for C < 256 MiB
+bool o32_ok(uint64_t C_or_n) { return C_or_n < (1ull << 28); }
+
 // CHIP_L123=0 keeps the K4-per-level path from level 1 for non-FULL streams (A/B)
 bool l123_on() {
     static const bool on = [] {
@@ -78,14 +93,19 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     const bool full = a.cols % 8 == 0 && n >= 4 * C;  // levels 1-3 in the kernel (N >= 64, 8 subtrees a block)
     // general path: both compressions' message words read at once (MP 1): -1.5 % kernel time
     // (tools/fused_tune, profiles/r6f/r6h/r6i); the FULL path measured no gain from it
-    constexpr auto KF = zfec_bao_fused_kernel<true, true>;
-    constexpr auto KG = zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1>;
+    constexpr auto KF64 = zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, false, K13_GFP>;
+    constexpr auto KG64 = zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, false, K13_GFP>;
+    constexpr auto KF32 = zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, K13_O32, K13_GFP>;
+    constexpr auto KG32 = zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, K13_O32, K13_GFP>;
     static bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(KF), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)LDS_BYTES) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void *>(KG), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)LDS_BYTES) == hipSuccess;
+        bool ok = true;
+        for (auto k : {KF64, KG64, KF32, KG32})
+            ok &= hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)LDS_BYTES) == hipSuccess;
+        return ok;
     }();
+    const bool o32 = o32_ok(C);
+    const auto KF = o32 ? KF32 : KF64, KG = o32 ? KG32 : KG64;
     (void)attr;
     (void)hipGetLastError();
     const uint64_t n0 = full ? a.N / 8 : a.N;  // nodes per object in `cv`
@@ -174,11 +194,15 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     uint32_t *q = nullptr;
     if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
     a.queue = q + QUEUE_K13;
-    constexpr auto K = zfec_bao_fused_kernel<true, true, 1, 0, 1>;
+    constexpr auto K64 = zfec_bao_fused_kernel<true, true, 1, 0, 1>;
+    constexpr auto K32 = zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 0, 0, K13_O32>;
     static bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(K), hipFuncAttributeMaxDynamicSharedMemorySize,
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(K64), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)LDS_BYTES) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(K32), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)LDS_BYTES) == hipSuccess;
     }();
+    const auto K = o32_ok(n) ? K32 : K64;
     (void)attr;
     (void)hipGetLastError();
     const uint64_t n3 = a.cvs;

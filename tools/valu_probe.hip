@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../carbonado_amd/csrc/bao_device.hpp"
@@ -196,9 +197,59 @@ __device__ __forceinline__ void g4(uint32_t &a0, uint32_t &b0, uint32_t &c0, uin
     XOR(b0, c0); XOR(b1, c1); XOR(b2, c2); XOR(b3, c3);
     ROT(b0, 7); ROT(b1, 7); ROT(b2, 7); ROT(b3, 7);
 }
+// One asm statement per four G's with SEP between the 12 groups of four
+// (VAR 4: "s_nop 0", VAR 5: "s_nop 1", VAR 6: nothing, VAR 7: s_nop 0 after
+// the VOP2 groups only, VAR 8: after the VOP3 groups only): does the hazard recognizer's s_nop between dependent
+// groups (VAR 3) cost or help?
+#define G4B(S3, S2)                                                                                   \
+    "v_add3_u32 %0, %0, %4, %16\n\tv_add3_u32 %1, %1, %5, %17\n\tv_add3_u32 %2, %2, %6, %18\n\t"    \
+    "v_add3_u32 %3, %3, %7, %19\n\t" S3                                                               \
+    "v_xor_b32 %12, %12, %0\n\tv_xor_b32 %13, %13, %1\n\tv_xor_b32 %14, %14, %2\n\tv_xor_b32 %15, %15, %3\n\t" S2 \
+    "v_alignbit_b32 %12, %12, %12, 16\n\tv_alignbit_b32 %13, %13, %13, 16\n\t"                          \
+    "v_alignbit_b32 %14, %14, %14, 16\n\tv_alignbit_b32 %15, %15, %15, 16\n\t" S3                        \
+    "v_add_u32 %8, %8, %12\n\tv_add_u32 %9, %9, %13\n\tv_add_u32 %10, %10, %14\n\tv_add_u32 %11, %11, %15\n\t" S2 \
+    "v_xor_b32 %4, %4, %8\n\tv_xor_b32 %5, %5, %9\n\tv_xor_b32 %6, %6, %10\n\tv_xor_b32 %7, %7, %11\n\t" S2 \
+    "v_alignbit_b32 %4, %4, %4, 12\n\tv_alignbit_b32 %5, %5, %5, 12\n\t"                                \
+    "v_alignbit_b32 %6, %6, %6, 12\n\tv_alignbit_b32 %7, %7, %7, 12\n\t" S3                              \
+    "v_add3_u32 %0, %0, %4, %20\n\tv_add3_u32 %1, %1, %5, %21\n\tv_add3_u32 %2, %2, %6, %22\n\t"    \
+    "v_add3_u32 %3, %3, %7, %23\n\t" S3                                                               \
+    "v_xor_b32 %12, %12, %0\n\tv_xor_b32 %13, %13, %1\n\tv_xor_b32 %14, %14, %2\n\tv_xor_b32 %15, %15, %3\n\t" S2 \
+    "v_alignbit_b32 %12, %12, %12, 8\n\tv_alignbit_b32 %13, %13, %13, 8\n\t"                            \
+    "v_alignbit_b32 %14, %14, %14, 8\n\tv_alignbit_b32 %15, %15, %15, 8\n\t" S3                          \
+    "v_add_u32 %8, %8, %12\n\tv_add_u32 %9, %9, %13\n\tv_add_u32 %10, %10, %14\n\tv_add_u32 %11, %11, %15\n\t" S2 \
+    "v_xor_b32 %4, %4, %8\n\tv_xor_b32 %5, %5, %9\n\tv_xor_b32 %6, %6, %10\n\tv_xor_b32 %7, %7, %11\n\t" S2 \
+    "v_alignbit_b32 %4, %4, %4, 7\n\tv_alignbit_b32 %5, %5, %5, 7\n\t"                                  \
+    "v_alignbit_b32 %6, %6, %6, 7\n\tv_alignbit_b32 %7, %7, %7, 7"
+#define G4A(SEP) G4B(SEP, SEP)
+template <int NOPK>
+__device__ __forceinline__ void g4a(uint32_t &a0, uint32_t &b0, uint32_t &c0, uint32_t &d0, uint32_t &a1, uint32_t &b1,
+                                    uint32_t &c1, uint32_t &d1, uint32_t &a2, uint32_t &b2, uint32_t &c2, uint32_t &d2,
+                                    uint32_t &a3, uint32_t &b3, uint32_t &c3, uint32_t &d3, uint32_t x0, uint32_t y0,
+                                    uint32_t x1, uint32_t y1, uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) {
+#define G4A_OPS                                                                                        \
+    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3), "+v"(c0), "+v"(c1), \
+      "+v"(c2), "+v"(c3), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3)                                      \
+    : "v"(x0), "v"(x1), "v"(x2), "v"(x3), "v"(y0), "v"(y1), "v"(y2), "v"(y3)
+    if constexpr (NOPK == 0) asm volatile(G4A("s_nop 0\n\t") G4A_OPS);
+    else if constexpr (NOPK == 1) asm volatile(G4A("s_nop 1\n\t") G4A_OPS);
+    else if constexpr (NOPK == 2) asm volatile(G4B("", "s_nop 0\n\t") G4A_OPS);  // after VOP2 groups only
+    else if constexpr (NOPK == 3) asm volatile(G4B("s_nop 0\n\t", "") G4A_OPS);  // after VOP3 groups only
+    else asm volatile(G4A("") G4A_OPS);
+#undef G4A_OPS
+}
 template <int VAR, int R>
 __device__ __forceinline__ void rv(uint32_t (&v)[16], const uint32_t (&m)[16]) {
     using chip::bao::SCHED;
+    if constexpr (VAR >= 4) {
+        constexpr int K = VAR == 4 ? 0 : VAR == 5 ? 1 : VAR == 7 ? 2 : VAR == 8 ? 3 : -1;
+        g4a<K>(v[0], v[4], v[8], v[12], v[1], v[5], v[9], v[13], v[2], v[6], v[10], v[14], v[3], v[7], v[11], v[15],
+               m[SCHED(R, 0)], m[SCHED(R, 1)], m[SCHED(R, 2)], m[SCHED(R, 3)], m[SCHED(R, 4)], m[SCHED(R, 5)],
+               m[SCHED(R, 6)], m[SCHED(R, 7)]);
+        g4a<K>(v[0], v[5], v[10], v[15], v[1], v[6], v[11], v[12], v[2], v[7], v[8], v[13], v[3], v[4], v[9], v[14],
+               m[SCHED(R, 8)], m[SCHED(R, 9)], m[SCHED(R, 10)], m[SCHED(R, 11)], m[SCHED(R, 12)], m[SCHED(R, 13)],
+               m[SCHED(R, 14)], m[SCHED(R, 15)]);
+        return;
+    }
     if constexpr (VAR == 3) {
         g4(v[0], v[4], v[8], v[12], v[1], v[5], v[9], v[13], v[2], v[6], v[10], v[14], v[3], v[7], v[11], v[15],
            m[SCHED(R, 0)], m[SCHED(R, 1)], m[SCHED(R, 2)], m[SCHED(R, 3)], m[SCHED(R, 4)], m[SCHED(R, 5)],
@@ -325,7 +376,7 @@ static void probe_op(int iters) {
 
 template <int VAR>
 static void probe_b3v(int iters, std::vector<uint32_t> *ref) {
-    for (int W : {2, 4, 8}) {
+    for (int W : {2, 3, 4, 8}) {
         Result r = run([&](int blocks, uint32_t *o, Stamp *s) {
             b3v_kernel<VAR><<<blocks, 256>>>(o, s, iters, 12345u);
         }, W, 672.0 * iters, 3);
@@ -368,6 +419,9 @@ int main(int argc, char **argv) {
     printf("device %s, %d CUs, clockRate %d kHz; nominal: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.64 T lane-op/s "
            "(2-cycle wave64 issue), 39.32 at 4 cycles\n",
            p.gcnArchName, p.multiProcessorCount, p.clockRate);
+    // argv[2] == "b3": only the BLAKE3 rows (x1/x2 states = the product's b3_compress)
+    const bool b3only = argc > 2 && std::string(argv[2]) == "b3";
+    if (!b3only) {
     probe_op<ADD>(iters);
     probe_op<ADD3>(iters);
     probe_op<XOR>(iters);
@@ -385,9 +439,22 @@ int main(int argc, char **argv) {
         printf("mix4 grouped     W=%d  %8.3f ms  %7.2f T lane-instr/s  (mix4 row: ops counted in groups of 4)\n", W,
                r.ms, r.lane_ops_t);
     }
+    }
+    std::vector<uint32_t> ref;
+    if (b3only) {  // warm the clock up, then the variants back to back
+        probe_b3v<0>(iters / 64, &ref);
+        probe_b3v<3>(iters / 64, &ref);
+        probe_b3v<4>(iters / 64, &ref);
+        probe_b3v<5>(iters / 64, &ref);
+        probe_b3v<6>(iters / 64, &ref);
+        probe_b3v<7>(iters / 64, &ref);
+        probe_b3v<8>(iters / 64, &ref);
+        probe_b3v<3>(iters / 64, &ref);
+        probe_b3<1>(iters / 64);
+        return 0;
+    }
     probe_b3<1>(iters / 64);
     probe_b3<2>(iters / 128);
-    std::vector<uint32_t> ref;
     probe_b3v<0>(iters / 64, &ref);
     probe_b3v<1>(iters / 64, &ref);
     probe_b3v<2>(iters / 64, &ref);
