@@ -62,6 +62,7 @@ struct Variant {
     std::string name;
     void (*fn)(fused::FusedArgs);
     int kind;  // 0: zfec 4-of-8 + bao of the shards, 1: bao of the content
+    bool spec = false;  // K13S: 12-wave workgroups, roles on separate waves
 };
 
 int main(int argc, char **argv) {
@@ -106,7 +107,11 @@ int main(int argc, char **argv) {
     }
     const char *which = argc > 3 ? argv[3] : "all";
     std::vector<Variant> all = {
-        {"K0 FULL (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
+        {"K0 FULL (product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 0},
+        {"K0 FULL O32 GFP0", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 0>, 0},
+        {"K0 FULL O32=0 GFP0 (r6 product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
+        {"K0 FULL K13S spec", fused::zfec_bao_spec_kernel<true>, 0, true},
+        {"K0 FULL K13S spec NPB1", fused::zfec_bao_spec_kernel<true, 1>, 0, true},
         {"K0 FULL MP1", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 1>, 0},
         {"K0 FULL ORD2 MP1", fused::zfec_bao_fused_kernel<true, true, 2, 0, 0, true, 1>, 0},
         {"K1 MP1", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 1>, 1},
@@ -136,13 +141,14 @@ int main(int argc, char **argv) {
         {"K1 DG1 no line stores/reads", fused::zfec_bao_fused_kernel<true, true, 1, 1, 1>, 1},
         {"K1 DG7 piece reads, no stores", fused::zfec_bao_fused_kernel<true, true, 1, 7, 1>, 1},
         {"K1 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 1>, 1},
-        {"K0 FULL (product, again)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0}};
+        {"K0 FULL K13S spec (again)", fused::zfec_bao_spec_kernel<true>, 0, true},
+        {"K0 FULL (product, again)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 0}};
     std::vector<Variant> vs;
     for (auto &v : all)
         if (!strcmp(which, "all") || strstr(v.name.c_str(), which)) vs.push_back(v);
     for (auto &v : vs)
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(v.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)fused::LDS_BYTES);
+                                  (int)(v.spec ? fused::S_LDS_BYTES : fused::LDS_BYTES));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -153,9 +159,12 @@ int main(int argc, char **argv) {
             const fused::FusedArgs &a = A[vs[v].kind];
             const uint64_t blocks = count * a.bpo;
             const unsigned grid = (unsigned)std::min<uint64_t>(256, (blocks + fused::FW - 1) / fused::FW);
-            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
+            const unsigned tpb = vs[v].spec ? (vs[v].name.find("NPB1") != std::string::npos ? fused::stpb<1>() : fused::STPB)
+                                            : fused::FTPB;
+            const size_t ldsb = vs[v].spec ? fused::S_LDS_BYTES : fused::LDS_BYTES;
+            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(tpb), ldsb, 0, a);
             CK(hipEventRecord(e0));
-            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
+            hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(tpb), ldsb, 0, a);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float t;
@@ -164,7 +173,7 @@ int main(int argc, char **argv) {
             if (rd == 0) {  // output of this variant: streams + CVs
                 CK(hipMemset(out, 0, count * bstride));
                 CK(hipMemset(cv, 0, count * N0 * 32));
-                hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(fused::FTPB), fused::LDS_BYTES, 0, a);
+                hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(tpb), ldsb, 0, a);
                 CK(hipDeviceSynchronize());
                 sums[v] = checksum(out, count * bstride) ^ (checksum(cv, count * N0 * 32) * 3);
             }
