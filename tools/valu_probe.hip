@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../carbonado_amd/csrc/bao_device.hpp"
+#include "b3g8_asm.h"
 
 #define CK(x)                                                                                 \
     do {                                                                                      \
@@ -374,6 +375,109 @@ static void probe_op(int iters) {
     fflush(stdout);
 }
 
+// Two independent compressions per lane, their eight G's advanced step by
+// step as one asm statement per half-round (VAR 10: no nops, 11: s_nop 0
+// after the VOP2 groups), against the compiler's own interleaving of two
+// plain-C compressions (VAR 12).  Counted as 2 compressions per iteration.
+template <int VAR>
+__device__ __forceinline__ void g8(uint32_t (&v)[16], uint32_t (&u)[16], const uint32_t *m, const uint32_t *n, int i0,
+                                   int i1, int i2, int i3, int j0, int j1, int j2, int j3, int k0, int k1, int k2,
+                                   int k3, int l0, int l1, int l2, int l3, int x0, int y0, int x1, int y1, int x2, int y2,
+                                   int x3, int y3) {
+#define G8_OPS                                                                                                 \
+    : "+v"(v[i0]), "+v"(v[i1]), "+v"(v[i2]), "+v"(v[i3]), "+v"(v[j0]), "+v"(v[j1]), "+v"(v[j2]), "+v"(v[j3]),   \
+      "+v"(v[k0]), "+v"(v[k1]), "+v"(v[k2]), "+v"(v[k3]), "+v"(v[l0]), "+v"(v[l1]), "+v"(v[l2]), "+v"(v[l3]),   \
+      "+v"(u[i0]), "+v"(u[i1]), "+v"(u[i2]), "+v"(u[i3]), "+v"(u[j0]), "+v"(u[j1]), "+v"(u[j2]), "+v"(u[j3]),   \
+      "+v"(u[k0]), "+v"(u[k1]), "+v"(u[k2]), "+v"(u[k3]), "+v"(u[l0]), "+v"(u[l1]), "+v"(u[l2]), "+v"(u[l3])    \
+    : "v"(m[x0]), "v"(m[x1]), "v"(m[x2]), "v"(m[x3]), "v"(n[x0]), "v"(n[x1]), "v"(n[x2]), "v"(n[x3]),           \
+      "v"(m[y0]), "v"(m[y1]), "v"(m[y2]), "v"(m[y3]), "v"(n[y0]), "v"(n[y1]), "v"(n[y2]), "v"(n[y3])
+    if constexpr (VAR == 10) asm volatile(G8ASM_PLAIN G8_OPS);
+    else asm volatile(G8ASM_NOP G8_OPS);
+#undef G8_OPS
+}
+template <int VAR, int R>
+__device__ __forceinline__ void r2(uint32_t (&v)[16], uint32_t (&u)[16], const uint32_t (&m)[16], const uint32_t (&n)[16]) {
+    using chip::bao::SCHED;
+    using chip::bao::rotr;
+    if constexpr (VAR == 12) {
+        B3G(v[0], v[4], v[8], v[12], m[SCHED(R, 0)], m[SCHED(R, 1)]);
+        B3G(u[0], u[4], u[8], u[12], n[SCHED(R, 0)], n[SCHED(R, 1)]);
+        B3G(v[1], v[5], v[9], v[13], m[SCHED(R, 2)], m[SCHED(R, 3)]);
+        B3G(u[1], u[5], u[9], u[13], n[SCHED(R, 2)], n[SCHED(R, 3)]);
+        B3G(v[2], v[6], v[10], v[14], m[SCHED(R, 4)], m[SCHED(R, 5)]);
+        B3G(u[2], u[6], u[10], u[14], n[SCHED(R, 4)], n[SCHED(R, 5)]);
+        B3G(v[3], v[7], v[11], v[15], m[SCHED(R, 6)], m[SCHED(R, 7)]);
+        B3G(u[3], u[7], u[11], u[15], n[SCHED(R, 6)], n[SCHED(R, 7)]);
+        B3G(v[0], v[5], v[10], v[15], m[SCHED(R, 8)], m[SCHED(R, 9)]);
+        B3G(u[0], u[5], u[10], u[15], n[SCHED(R, 8)], n[SCHED(R, 9)]);
+        B3G(v[1], v[6], v[11], v[12], m[SCHED(R, 10)], m[SCHED(R, 11)]);
+        B3G(u[1], u[6], u[11], u[12], n[SCHED(R, 10)], n[SCHED(R, 11)]);
+        B3G(v[2], v[7], v[8], v[13], m[SCHED(R, 12)], m[SCHED(R, 13)]);
+        B3G(u[2], u[7], u[8], u[13], n[SCHED(R, 12)], n[SCHED(R, 13)]);
+        B3G(v[3], v[4], v[9], v[14], m[SCHED(R, 14)], m[SCHED(R, 15)]);
+        B3G(u[3], u[4], u[9], u[14], n[SCHED(R, 14)], n[SCHED(R, 15)]);
+        return;
+    }
+    g8<VAR>(v, u, m, n, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, SCHED(R, 0), SCHED(R, 1), SCHED(R, 2),
+            SCHED(R, 3), SCHED(R, 4), SCHED(R, 5), SCHED(R, 6), SCHED(R, 7));
+    g8<VAR>(v, u, m, n, 0, 1, 2, 3, 5, 6, 7, 4, 10, 11, 8, 9, 15, 12, 13, 14, SCHED(R, 8), SCHED(R, 9), SCHED(R, 10),
+            SCHED(R, 11), SCHED(R, 12), SCHED(R, 13), SCHED(R, 14), SCHED(R, 15));
+}
+template <int VAR>
+__global__ __launch_bounds__(256) void b3x2_kernel(uint32_t *out, Stamp *st, int iters, uint32_t seed) {
+    using chip::bao::IV;
+    uint32_t h[8], g[8], m[16], n[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { m[i] = seed * (i + 1) + threadIdx.x; n[i] = m[i] ^ 0x5A5A5A5Au; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { h[i] = IV(i) + threadIdx.x; g[i] = IV(i) + 7 * threadIdx.x; }
+    const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; ++it) {
+        uint32_t v[16] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], IV(0), IV(1), IV(2), IV(3),
+                          (uint32_t)it, 0u, 64u, 0u};
+        uint32_t u[16] = {g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], IV(0), IV(1), IV(2), IV(3),
+                          (uint32_t)it, 1u, 64u, 0u};
+        r2<VAR, 0>(v, u, m, n); r2<VAR, 1>(v, u, m, n); r2<VAR, 2>(v, u, m, n); r2<VAR, 3>(v, u, m, n);
+        r2<VAR, 4>(v, u, m, n); r2<VAR, 5>(v, u, m, n); r2<VAR, 6>(v, u, m, n);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { h[i] = v[i] ^ v[i + 8]; g[i] = u[i] ^ u[i + 8]; }
+        m[it & 15] ^= h[it & 7];
+        n[it & 15] ^= g[it & 7];
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s ^= h[i] ^ g[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+    if ((threadIdx.x & 63) == 0) {
+        Stamp q{t0, t1, r0, r1};
+        st[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = q;
+    }
+}
+template <int VAR>
+static void probe_b3x2(int iters, std::vector<uint32_t> *ref) {
+    for (int W : {1, 2, 3, 4, 8}) {
+        Result r = run([&](int blocks, uint32_t *o, Stamp *s) { b3x2_kernel<VAR><<<blocks, 256>>>(o, s, iters, 12345u); },
+                       W, 2 * 672.0 * iters, 3);
+        printf("blake3 x2 interleaved VAR %d W=%d  %8.3f ms  %7.2f T lane-op/s (672/compress)  %.3e compress/s  clk %.2f GHz\n",
+               VAR, W, r.ms, r.lane_ops_t, r.lane_ops_t * 1e12 / 672.0, r.clock_ghz);
+    }
+    uint32_t *d = nullptr;
+    Stamp *st = nullptr;
+    CK(hipMalloc(&d, 256 * 256 * 4));
+    CK(hipMalloc(&st, 256 * 4 * sizeof(Stamp)));
+    b3x2_kernel<VAR><<<256, 256>>>(d, st, 50, 777u);
+    std::vector<uint32_t> h(256 * 256);
+    CK(hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+    if (ref->empty()) *ref = h;
+    printf("blake3 x2 VAR %d output %s VAR 12\n", VAR, h == *ref ? "==" : "!=");
+    CK(hipFree(d));
+    CK(hipFree(st));
+    fflush(stdout);
+}
+
 template <int VAR>
 static void probe_b3v(int iters, std::vector<uint32_t> *ref) {
     for (int W : {2, 3, 4, 8}) {
@@ -441,6 +545,16 @@ int main(int argc, char **argv) {
     }
     }
     std::vector<uint32_t> ref;
+    if (argc > 2 && std::string(argv[2]) == "b3x2") {  // two states per lane (VAR 10-12)
+        probe_b3v<0>(iters / 64, &ref);
+        probe_b3v<7>(iters / 64, &ref);
+        std::vector<uint32_t> ref2;
+        probe_b3x2<12>(iters / 128, &ref2);
+        probe_b3x2<10>(iters / 128, &ref2);
+        probe_b3x2<11>(iters / 128, &ref2);
+        probe_b3v<7>(iters / 64, &ref);
+        return 0;
+    }
     if (b3only) {  // warm the clock up, then the variants back to back
         probe_b3v<0>(iters / 64, &ref);
         probe_b3v<3>(iters / 64, &ref);
