@@ -184,8 +184,10 @@ struct Tree {
 // loads and stores address them as the wave's object base (SGPRs) plus a
 // 32-bit per-lane offset: global_load/store with saddr, no 64-bit VALU adds
 // per access.  GFP 1: table addresses through gf_pair.
+// WPG: waves per workgroup (FW; tools/fused_tune runs 4 = one wave per SIMD
+// to measure the kernel's sensitivity to occupancy).
 template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
-          bool O32 = false, int GFP = 0>
+          bool O32 = false, int GFP = 0, int WPG = FW>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     const uint64_t TS = KIND ? 8 : a.cols;   // chunk index step between the 8 lane groups
     if (KIND == 0) {  // table: lds[x][s][r] = T_s[x], FR replicas
         uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
-        for (int i = threadIdx.x; i < 256 * 4 * FR; i += FTPB) {
+        for (int i = threadIdx.x; i < 256 * 4 * FR; i += 64 * WPG) {
             const int x = i / (4 * FR);
             const int s = (i - x * (4 * FR)) / FR;
             dst[i] = a.table[s * 256 + x];
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     }
     const int gl = lane & 7, cu = lane >> 3;
     const uint64_t total = a.count * a.bpo;
-    const uint64_t GW = (uint64_t)gridDim.x * FW;
+    const uint64_t GW = (uint64_t)gridDim.x * WPG;
 
     // Loads of a step.  A block whose input columns all lie below `valid`
     // (every block of an object without zfec padding) takes plain loads whose
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         if (lane == 0) b = atomicAdd(a.queue, 1u);
         return (uint64_t)__builtin_amdgcn_readfirstlane(b);
     };
-    uint64_t blk = DQ ? grab() : (uint64_t)blockIdx.x * FW + wave;
+    uint64_t blk = DQ ? grab() : (uint64_t)blockIdx.x * WPG + wave;
     u32x4 v[NV], v2[NV];  // this step's loads; ORD 3: the next step's too
     if (blk < total) {
         load_step(blk, 0, v);
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             }
             auto one_line = [&](int t) {
                 if (DG == 8)  // diagnostic: the same stores into 8 KiB per wave (L2-resident)
-                    st16<NT>(a.out + ((uint64_t)(blockIdx.x * FW + wave) * 8192 + t * 1024 + lane * 16), q[t]);
+                    st16<NT>(a.out + ((uint64_t)(blockIdx.x * WPG + wave) * 8192 + t * 1024 + lane * 16), q[t]);
                 else
                     st16<NT>(lat(t, ldd[t] + 128u * (s - 1) + 16u * gl), q[t]);
             };
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     }
     if (DQ && lane == 0) {  // the last wave out leaves the queue zero for the next launch
         const uint32_t done = atomicAdd(a.queue + 32, 1u);
-        if (done + 1 == gridDim.x * (uint32_t)FW) {
+        if (done + 1 == gridDim.x * (uint32_t)WPG) {
             a.queue[0] = 0u;
             a.queue[32] = 0u;
         }

@@ -111,6 +111,7 @@ int main(int argc, char **argv) {
         {"K0 FULL O32 GFP0", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 0>, 0},
         {"K0 FULL O32=0 GFP0 (r6 product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
         {"K0 FULL K13S spec", fused::zfec_bao_spec_kernel<true>, 0, true},
+        {"K0 FULL product WPG4 (1 wave/SIMD)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1, 4>, 0},
         {"K0 FULL K13S spec NPB1", fused::zfec_bao_spec_kernel<true, 1>, 0, true},
         {"K0 FULL MP1", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 1>, 0},
         {"K0 FULL ORD2 MP1", fused::zfec_bao_fused_kernel<true, true, 2, 0, 0, true, 1>, 0},
@@ -160,7 +161,7 @@ int main(int argc, char **argv) {
             const uint64_t blocks = count * a.bpo;
             const unsigned grid = (unsigned)std::min<uint64_t>(256, (blocks + fused::FW - 1) / fused::FW);
             const unsigned tpb = vs[v].spec ? (vs[v].name.find("NPB1") != std::string::npos ? fused::stpb<1>() : fused::STPB)
-                                            : fused::FTPB;
+                                 : vs[v].name.find("WPG4") != std::string::npos ? 256u : fused::FTPB;
             const size_t ldsb = vs[v].spec ? fused::S_LDS_BYTES : fused::LDS_BYTES;
             hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(tpb), ldsb, 0, a);
             CK(hipEventRecord(e0));
