@@ -27,8 +27,13 @@ namespace {
 constexpr bool K13_O32 = K13_O32_DEF;
 constexpr int K13_GFP = K13_GFP_DEF;
 // the stream of an object of shard length C is < 8.6 C bytes and its input
-// 4 C: 32-bit offsets for C < 256 MiB
-bool o32_ok(uint64_t C_or_n) { return C_or_n < (1ull << 28); }
+// 4 C: 32-bit offsets for C < 256 MiB.  CHIP_K13_O32=0 (read per call, so a
+// test can flip it) takes the 64-bit-address kernels at any size.
+bool o32_ok(uint64_t C_or_n) {
+    const char *e = std::getenv("CHIP_K13_O32");
+    if (e && e[0] == '0' && e[1] == 0) return false;
+    return C_or_n < (1ull << 28);
+}
 
 // CHIP_L123=0 keeps the K4-per-level path from level 1 for non-FULL streams (A/B)
 bool l123_on() {

@@ -168,3 +168,38 @@ def test_level15_shape_batch_level12_bit_exact(gpu):
         assert len(enc) == blen
         assert out[o, :blen].cpu().numpy().tobytes() == enc, o
         assert hashes[o].cpu().numpy().tobytes() == h, o
+
+
+@pytest.mark.parametrize("level", [12, 4])
+@pytest.mark.parametrize("n", [N, 16_779_371])
+def test_fused_64bit_address_forms_match(gpu, monkeypatch, level, n):
+    """The fused kernels address every object through 32-bit lane offsets from
+    its base when the shard length is < 256 MiB (all BASELINE sizes), and
+    through 64-bit addresses above that.  CHIP_K13_O32=0 forces the 64-bit
+    forms at this size: both must give the oracle's streams and hashes (level
+    12: zfec + bao, FULL path at 16 MiB, general path at the level-15 shard
+    length; level 4: bao of the content, content mode + tail kernel)."""
+    import torch
+    from carbonado_amd import device
+    rng = np.random.default_rng(n + level)
+    count = 2
+    host = rng.integers(0, 256, (count, n), dtype=np.uint8)
+    row = (n + 15) // 16 * 16
+    inp = torch.zeros((count, row), dtype=torch.uint8)
+    inp[:, :n] = torch.from_numpy(host)
+    inp = inp.cuda()
+    outs = []
+    for o32 in ("1", "0"):
+        monkeypatch.setenv("CHIP_K13_O32", o32)
+        scratch = device.encode_scratch(level, n, count)
+        oenc = O.encode(host[0].tobytes(), level)
+        blen = len(oenc[0])
+        out = torch.zeros((count, (blen + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+        hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+        olen, _ = device.encode_batch(level, inp, n, out, hashes, scratch)
+        torch.cuda.synchronize()
+        assert olen == blen
+        outs.append((out.cpu(), hashes.cpu()))
+        assert out[0, :blen].cpu().numpy().tobytes() == oenc[0]
+        assert hashes[0].cpu().numpy().tobytes() == oenc[1]
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
