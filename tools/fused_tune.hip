@@ -11,7 +11,7 @@
 #include <string>
 #include <vector>
 
-#include "../carbonado_amd/csrc/fused_device.hpp"
+#include "fused_variants.hpp"
 #include "../carbonado_amd/csrc/gf256.hpp"
 #include "../carbonado_amd/csrc/hbm_alloc.hpp"
 
@@ -183,15 +183,16 @@ int main(int argc, char **argv) {
         const uint64_t N = N0, n3 = N / 8, work = count * n3;
         uint8_t *cv3;
         CK(hipMalloc(&cv3, count * n3 * 32));
-        void (*kv[4])(const uint8_t *, uint64_t, uint64_t, const uint64_t *, uint8_t *, uint64_t, uint8_t *, uint64_t) = {
+        void (*kv[5])(const uint8_t *, uint64_t, uint64_t, const uint64_t *, uint8_t *, uint64_t, uint8_t *, uint64_t) = {
             fused::bao_levels123_kernel<1>, fused::bao_levels123_kernel<2>, fused::bao_levels123_kernel<0>,
-            fused::bao_levels123_lds_kernel};
-        const char *kn[4] = {"8-B node stores (product)", "16-B node stores", "no node stores (diagnostic)",
-                             "LDS-staged node stores, 4 lanes per node"};
-        std::vector<float> t3[4];
-        unsigned long long sum3[4] = {0, 0, 0, 0};
+            fused::bao_levels123_lds_kernel, fused::bao_levels123_seg_kernel};
+        const char *kn[5] = {"8-B node stores", "16-B node stores", "no node stores (diagnostic)",
+                             "LDS-staged node stores, 4 lanes per node (product)",
+                             "node stacks as whole 64-B segments (SEG)"};
+        std::vector<float> t3[5];
+        unsigned long long sum3[5] = {0, 0, 0, 0, 0};
         for (int rd = 0; rd < rounds + 1; ++rd)
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 5; ++k) {
                 const int tpb = k == 3 ? 64 : 256;
                 CK(hipEventRecord(e0));
                 hipLaunchKernelGGL(kv[k], dim3((unsigned)((work + tpb - 1) / tpb)), dim3(tpb), 0, 0, cv, N, count,
@@ -203,9 +204,9 @@ int main(int argc, char **argv) {
                 if (rd) t3[k].push_back(t);
                 if (rd == 0) sum3[k] = checksum(out, count * bstride) ^ (checksum(cv3, count * n3 * 32) * 3);
             }
-        printf("levels 1-3 outputs: LDS-staged %s 8-B stores; 16-B %s\n", sum3[3] == sum3[0] ? "==" : "!=",
-               sum3[1] == sum3[0] ? "==" : "!=");
-        for (int k = 0; k < 4; ++k) {
+        printf("levels 1-3 outputs: LDS-staged %s 8-B stores; 16-B %s; SEG %s\n", sum3[3] == sum3[0] ? "==" : "!=",
+               sum3[1] == sum3[0] ? "==" : "!=", sum3[4] == sum3[0] ? "==" : "!=");
+        for (int k = 0; k < 5; ++k) {
             std::sort(t3[k].begin(), t3[k].end());
             printf("levels 1-3 from chunk CVs (bao_levels123_kernel), %s, %llu objects: median %.3f ms\n", kn[k],
                    (unsigned long long)count, t3[k][t3[k].size() / 2]);
