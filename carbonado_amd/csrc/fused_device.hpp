@@ -187,7 +187,7 @@ struct Tree {
 // WPG: waves per workgroup (FW; tools/fused_tune runs 4 = one wave per SIMD
 // to measure the kernel's sensitivity to occupancy).
 template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
-          bool O32 = false, int GFP = 0, int WPG = FW>
+          bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -230,7 +230,10 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
             if (O32) {
                 const uint32_t o = (uint32_t)((ub + cu) * 1024) + 128u * s + 16u * gl;
 #pragma unroll
-                for (int t = 0; t < NV; ++t) v[t] = *reinterpret_cast<const u32x4 *>(ib + (uint64_t)(o + 8192u * t));
+                for (int t = 0; t < NV; ++t) {
+                    const u32x4 *src = reinterpret_cast<const u32x4 *>(ib + (uint64_t)(o + 8192u * t));
+                    v[t] = NTL ? __builtin_nontemporal_load(src) : *src;
+                }
                 return;
             }
             const uint8_t *b = ib + (ub + cu) * 1024 + 128 * (uint64_t)s + 16 * gl;
@@ -243,7 +246,9 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         if (full) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                v[j] = O32 ? *reinterpret_cast<const u32x4 *>(ib + (uint64_t)((uint32_t)ioff[j] + (uint32_t)off))
+                v[j] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
+                                 ib + (O32 ? (uint64_t)((uint32_t)ioff[j] + (uint32_t)off) : ioff[j] + off)))
+                     : O32 ? *reinterpret_cast<const u32x4 *>(ib + (uint64_t)((uint32_t)ioff[j] + (uint32_t)off))
                            : *reinterpret_cast<const u32x4 *>(ib + ioff[j] + off);
         } else if (KIND == 0) {
             const bool col = ub + cu < a.cols;

@@ -24,8 +24,15 @@ namespace {
 #ifndef K13_GFP_DEF
 #define K13_GFP_DEF 1
 #endif
+#ifndef K13_NTL_DEF
+#define K13_NTL_DEF 1
+#endif
 constexpr bool K13_O32 = K13_O32_DEF;
 constexpr int K13_GFP = K13_GFP_DEF;
+// content mode (bao of the content, KIND 1): input loads nontemporal, +1.5-1.9 %
+// (A/B r7u); the zfec+bao kernels keep plain loads (FULL path even, general
+// path -2..-4 % with them)
+constexpr bool K13_NTL = K13_NTL_DEF;
 // the stream of an object of shard length C is < 8.6 C bytes and its input
 // 4 C: 32-bit offsets for C < 256 MiB.  CHIP_K13_O32=0 (read per call, so a
 // test can flip it) takes the 64-bit-address kernels at any size.
@@ -200,7 +207,7 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
     a.queue = q + QUEUE_K13;
     constexpr auto K64 = zfec_bao_fused_kernel<true, true, 1, 0, 1>;
-    constexpr auto K32 = zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 0, 0, K13_O32>;
+    constexpr auto K32 = zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 0, 0, K13_O32, 0, FW, K13_NTL>;
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(K64), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)LDS_BYTES) == hipSuccess &&
