@@ -114,6 +114,9 @@ struct KernelInfo {
     int bpc_cap;  // workgroups per CU to launch (0 = occupancy limit)
 };
 
+#ifndef ZF_NTL_DEF
+#define ZF_NTL_DEF 0
+#endif
 template <int K, int NG>
 KernelInfo make_info() {
     constexpr int R = replicas_for(K);
@@ -124,7 +127,7 @@ KernelInfo make_info() {
     if constexpr (K > 4) {
         ki.fn = gf_apply_kernel<K, NG, 1, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
     } else if constexpr (K == 4 && NG == 1) {
-        ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true>;
+        ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true, (bool)ZF_NTL_DEF>;
         ki.u = 2;
         ki.bpc_cap = 2;
     } else {
