@@ -187,7 +187,7 @@ struct Tree {
 // WPG: waves per workgroup (FW; tools/fused_tune runs 4 = one wave per SIMD
 // to measure the kernel's sensitivity to occupancy).
 template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
-          bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false>
+          bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false, int PRIO = 0>
 __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -320,6 +320,9 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
         for (int w = 0; w < 8; ++w) h[w] = bao::IV(w);
 
         for (int s = 0; s < 8; ++s) {
+            // PRIO 1 (tools/fused_tune): the GF and store roles at raised wave
+            // priority, the compressions at the base one
+            if (PRIO) __builtin_amdgcn_s_setprio(1);
             // ---- GF role: 8 pieces of 16 B into the rows of chunks (sh, cu) ----
             if (KIND == 1) {  // content: the 8 loaded pieces are the rows' bytes
                 const int wo = dofs(s) + 4 * gl;
@@ -500,8 +503,11 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
                 }
             };
             if (ORD >= 1) {
+                if (PRIO) __builtin_amdgcn_s_setprio(0);
                 hash(0);
+                if (PRIO) __builtin_amdgcn_s_setprio(1);
                 line_stores();
+                if (PRIO) __builtin_amdgcn_s_setprio(0);
                 hash(1);
             } else {
                 line_stores();
