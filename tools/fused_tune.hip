@@ -112,6 +112,8 @@ int main(int argc, char **argv) {
         {"K0 FULL O32=0 GFP0 (r6 product)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0>, 0},
         {"K0 FULL K13S spec", fused::zfec_bao_spec_kernel<true>, 0, true},
         {"K0 FULL product PRIO1 (GF/stores at raised priority)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1, 8, false, 1>, 0},
+        {"K1 product PRIO1 (loads/stores at raised priority)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 0, 0, true, 0, 8, true, 1>, 1},
+        {"K1 product NTL (as the library)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 0, 0, true, 0, 8, true>, 1},
         {"K0 FULL product NTL (nontemporal loads)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1, 8, true>, 0},
         {"K0 FULL product WPG4 (1 wave/SIMD)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1, 4>, 0},
         {"K0 FULL K13S spec NPB1", fused::zfec_bao_spec_kernel<true, 1>, 0, true},
