@@ -48,6 +48,9 @@ VALU_PEAK_TOPS = 41.2
 VALU_PEAK_SRC = ("measured BLAKE3 ceiling: the product's b3_compress (b3_g4 order) in a register loop, 8 waves/SIMD, "
                  "6.125e10 compressions/s x 672 (tools/valu_probe.hip VAR 3, profiles/r6q_valu_probe.txt); VOP2 "
                  "add/xor issue at ~69 T lane-ops/s, the VOP3 add3/alignbit at ~38 T")
+# hardware VALU issue peak: a wave64 VOP2 op every 2 cycles per SIMD = 32 lane-ops/cycle x 4 SIMDs x
+# 256 CUs x 2.4 GHz (measured ~69 T for v_add/v_xor at 2 waves/SIMD; half of BLAKE3's ops issue at half rate)
+HW_VALU_PEAK_TOPS = 78.6
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "GiB/s device-resident zfec 4-of-8 encode, 16 MiB objects; % HBM roofline"
 SEED = 0xCA4B0AD0
@@ -118,7 +121,8 @@ def parse(argv=None):
                          "each object's output on the GPU vs the C oracle's zfec (or encode()) + BLAKE3 on 16 host "
                          "threads, outside the timed region")
     ap.add_argument("--no-verify-all", action="store_true",
-                    help="encode / decode / e2e modes (which check every object by default): object 0 only")
+                    help="encode / decode / e2e / bao / bao-decode modes (which check every object by default): "
+                         "object 0 only")
     ap.add_argument("--no-aliased", action="store_true",
                     help="encode mode: skip the second, in-place (aliased data shards) measurement")
     ap.add_argument("--scatter", action="store_true",
@@ -149,7 +153,7 @@ def parse(argv=None):
         args.objects = 64  # host-API paths: a bounded host-memory working set
     if args.mode == "file" and args.objects == ap.get_default("objects"):
         args.objects = 128  # 2 GiB of input files + 2.1 GiB of output files on the box's disk
-    if args.mode not in ("encode", "decode", "e2e"):
+    if args.mode not in ("encode", "decode", "e2e", "bao", "bao-decode"):
         args.no_verify_all = True
     return args
 
@@ -306,7 +310,7 @@ def live_traffic(args, argv: list, timeout_s: float = 240.0) -> dict:
             "seconds": round(time.perf_counter() - t0, 1)}
 
 
-def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
+def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1, seconds: float | None = None):
     """Time the CPU oracle (scalar fec.c-style restatement of zfec-rs / the
     BLAKE3+bao restatement) on whole objects for ~cpu_seconds: 1 thread (the
     reference crate is single-threaded), or `threads` host threads each
@@ -382,13 +386,14 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
             c += 1
             if time.perf_counter() >= deadline or c >= 4096:
                 return c
+    budget = args.cpu_seconds if seconds is None else seconds
     t0 = time.perf_counter()
     if threads <= 1:
-        done = worker(t0 + args.cpu_seconds)
+        done = worker(t0 + budget)
     else:
         from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(threads) as ex:
-            done = sum(ex.map(worker, [t0 + args.cpu_seconds] * threads))
+            done = sum(ex.map(worker, [t0 + budget] * threads))
     el = time.perf_counter() - t0
     what = {"bao": "bao encode", "bao-decode": "bao decode (verify + content)", "e2e": f"encode() level {args.level}", "pipeline": f"encode() level {args.level}",
             "file": f"encode() level {args.level} (in memory, no file I/O, no header)",
@@ -402,6 +407,31 @@ def cpu_baseline(args, n: int, sample_obj: bytes | None, threads: int = 1):
                       f"{' + host_oracle.c' if args.mode in ('e2e', 'e2e-decode', 'file') and args.level & 3 else ''}, scalar "
                       f"restatement of the reference crates, "
                       f"{'1 thread' if threads <= 1 else f'{threads} threads, objects in parallel'}, {el:.1f} s"}
+
+
+PCIE_SPEC_GBS = 63.0  # PCIe Gen5 x16, per direction (spec)
+# one direction alone, pinned host memory, the runtime's DMA path (tools/pageable_probe.hip,
+# profiles/r1w_pageable_probe.txt): the practical per-direction ceilings on the GPU box
+PCIE_MEASURED_GBS = {"h2d": 55.6, "d2h": 55.0}
+
+
+def pcie_roofline(h2d_bytes: int, d2h_bytes: int, step_s: float, duplex_achieved: float) -> dict:
+    """Roofline of a host-buffer path (H2D and D2H overlapped): each direction
+    priced separately, since the traffic is asymmetric (encode() writes ~2x
+    what it reads).  `bound` names the binding direction, the one at the
+    higher fraction of its own peak; the duplex sum is kept alongside."""
+    rate = {d: b / step_s / 1e9 for d, b in (("h2d", h2d_bytes), ("d2h", d2h_bytes))}
+    bind = max(rate, key=lambda d: rate[d] / PCIE_SPEC_GBS)
+    return {"bound": f"pcie-{bind}", "achieved": round(rate[bind], 2), "peak": PCIE_SPEC_GBS, "unit": "GB/s",
+            "frac": round(rate[bind] / PCIE_SPEC_GBS, 4),
+            "frac_of_measured": round(rate[bind] / PCIE_MEASURED_GBS[bind], 4),
+            "peak_measured": PCIE_MEASURED_GBS[bind],
+            "h2d_GBps": round(rate["h2d"], 2), "d2h_GBps": round(rate["d2h"], 2),
+            "h2d_frac": round(rate["h2d"] / PCIE_SPEC_GBS, 4), "d2h_frac": round(rate["d2h"] / PCIE_SPEC_GBS, 4),
+            "duplex_GBps": round(duplex_achieved, 2), "duplex_frac": round(duplex_achieved / (2 * PCIE_SPEC_GBS), 4),
+            "note": ("PCIe Gen5 x16: 63 GB/s per direction (spec); peak_measured = that direction alone from "
+                     "pinned memory on the GPU box (profiles/r1w_pageable_probe.txt); H2D and D2H overlap, rates "
+                     "over the whole step's wall time")}
 
 
 def scrub_corrupt_offset(n: int, o: int) -> int:
@@ -585,6 +615,7 @@ class Workload:
             self.step = step
             self.blen = len(self.encs[0])
             self.alg_bytes = count * 2 * self.blen  # PCIe: the damaged stream up, the repaired stream down
+            self.h2d_bytes, self.d2h_bytes = count * self.blen, count * self.blen
             self.kernel = ("scrub(): H2D + bao node check + zfec decode of intact shards + fused re-encode + D2H, "
                            "one call per object (host API)")
             self.kernel_sym = "scrub"
@@ -647,6 +678,7 @@ class Workload:
                 self.finalize_ms.append((time.perf_counter() - t0) * 1e3)
             self.step = step
             self.alg_bytes = host.size  # PCIe: the content up (the hash comes back)
+            self.h2d_bytes, self.d2h_bytes = host.size, 0
             self.kernel = ("BaoHasher: H2D appends into a grow-only HBM buffer, chunk CVs hashed during update() "
                            "(64-chunk units with bytes past them), finalize(): last chunks + slot layout + parent "
                            "levels")
@@ -690,6 +722,7 @@ class Workload:
             step()
             self.final_len = max(r[1].output_len for r in self.results) + 160
             self.alg_bytes = count * (n + self.final_len)  # PCIe bytes: H2D input + D2H encoding
+            self.h2d_bytes, self.d2h_bytes = count * n, count * self.final_len
             self.kernel = (f"file::encode level {lv}: read files -> pinned -> H2D + zfec/bao kernels (+ host "
                            f"snap/ecies) -> D2H -> header (BIP-340) + body written{' + fsync' if args.fsync else ''}")
             self.kernel_sym = "file"
@@ -718,6 +751,7 @@ class Workload:
             self.step = step
             step()
             self.alg_bytes = count * (max(self.enc_len) + n)  # PCIe bytes: H2D encoding + D2H content
+            self.h2d_bytes, self.d2h_bytes = count * max(self.enc_len), count * n
             stages = ("ecies + " if lv & 1 else "") + ("unsnap + " if lv & 2 else "")
             host = f" + host {stages[:-3]} on {args.host_threads} threads" if stages else ""
             self.kernel = f"decode() level {lv}: H2D + bao verify kernels + D2H{host}, {slots} slots"
@@ -758,6 +792,7 @@ class Workload:
             self.step = step
             step()
             self.alg_bytes = count * (n + self.final_len)  # PCIe bytes: H2D input + D2H encoding
+            self.h2d_bytes, self.d2h_bytes = count * n, count * self.final_len
             stages = ("snap + " if lv & 2 else "") + ("ecies + " if lv & 1 else "")
             host = f"host {stages[:-3]} on {args.host_threads} threads + " if stages else ""
             self.kernel = f"encode() level {lv}: {host}H2D + gf_apply + bao kernels + D2H, {slots} slots"
@@ -813,30 +848,11 @@ class Workload:
         generated on each rank, so this only shows RCCL seeing N ranks and
         the per-link rate of the input-staging collective."""
         grp = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))  # a stuck collective ends the run, not the node's slot
-        per = int(gib * 2**30)
-        local = torch.empty(per, dtype=torch.uint8, device=self.dev)
-        chunks = None
-        if rank == 0:
-            full = torch.empty(world * per, dtype=torch.uint8, device=self.dev)
-            full.random_(0, 256)
-            chunks = list(full.chunk(world))
-        dist.scatter(local, chunks, src=0, group=grp)  # warm the communicator
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        dist.scatter(local, chunks, src=0, group=grp)
-        torch.cuda.synchronize()
-        el = max_over_ranks(time.perf_counter() - t0)
-        ok = True
-        if rank == 0:
-            ok = bool(torch.equal(local, chunks[0]))
-        del local, chunks
+        res = scatter_sample(rank, world, int(gib * 2**30), self.dev, grp)
         torch.cuda.empty_cache()
-        return {"ranks": world, "bytes_per_rank": per, "seconds": round(el, 4),
-                "GiB_per_s_total": round((world - 1) * per / el / 2**30, 2),
-                "GiB_per_s_per_receiver": round(per / el / 2**30, 2), "root_slice_ok": ok,
-                "how": "RCCL scatter (backend nccl) from rank 0 over xGMI, outside the timed region; the timed "
-                       "steps' inputs are generated on each rank"}
+        res["how"] = ("RCCL scatter (backend nccl) from rank 0 over xGMI, outside the timed region; the timed "
+                      "steps' inputs are generated on each rank")
+        return res
 
     def time_steps(self, steps: int, warmup: int, world: int, step=None):
         step = step or self.step
@@ -870,23 +886,29 @@ class Workload:
             return self._verify_all_decode()
         if self.args.mode == "e2e":
             return self._verify_all_e2e(threads)
+        if self.args.mode == "bao-decode":
+            return self._verify_all_bao_decode()
         from concurrent.futures import ThreadPoolExecutor
         from carbonado_amd import device
         from oracle import oracle as O
         t0 = time.perf_counter()
         count, k, m, C = self.count, self.k, self.m, self.C
         pipeline = self.args.mode == "pipeline"
-        olen = self.blen if pipeline else m * C  # bytes of each object's output
+        bao = self.args.mode == "bao"
+        olen = self.blen if (pipeline or bao) else m * C  # bytes of each object's output
         digests = torch.empty((count, 32), dtype=torch.uint8, device=self.dev)
         scratch = device.bao_scratch(olen, count, self.dev)
         device.bao_encode_batch(self.out, olen, None, digests, scratch)
         torch.cuda.synchronize()
         gpu = digests.cpu().numpy()
-        hashes = self.hashes.cpu().numpy() if pipeline else None
+        hashes = self.hashes.cpu().numpy() if (pipeline or bao) else None
         del scratch
         host_in = self.inp.cpu().numpy()
 
         def check(o):
+            if bao:  # encoding::bao (encoding.rs:38-44): the stream and its hash
+                stream, h = O.bao_encode(host_in[o].tobytes())
+                return O.blake3(stream) == gpu[o].tobytes() and h == hashes[o].tobytes()
             if pipeline:
                 enc, h, _ = O.encode(host_in[o].tobytes(), self.args.level)
                 return O.blake3(enc) == gpu[o].tobytes() and (not self.args.level & 4 or
@@ -896,7 +918,9 @@ class Workload:
             oks = list(ex.map(check, range(count)))
         bad = [o for o, ok in enumerate(oks) if not ok]
         return {"ok": not bad, "objects": count, "mismatched": bad[:16], "seconds": round(time.perf_counter() - t0, 1),
-                "how": (f"BLAKE3 of each object's level-{self.args.level} encoding on the GPU + its bao hash vs the "
+                "how": (f"BLAKE3 of each object's bao stream on the GPU + its bao hash vs the oracle's bao encode "
+                        f"(stream BLAKE3 + root hash) on {threads} threads" if bao else
+                        f"BLAKE3 of each object's level-{self.args.level} encoding on the GPU + its bao hash vs the "
                         f"oracle's encode() + BLAKE3 on {threads} threads" if pipeline else
                         f"BLAKE3 of each object's {m} shards on the GPU vs oracle zfec + BLAKE3 on {threads} threads")}
 
@@ -914,6 +938,23 @@ class Workload:
         return {"ok": not bad, "objects": self.count, "mismatched": bad[:16],
                 "seconds": round(time.perf_counter() - t0, 1),
                 "how": "every decoded object's n bytes vs its resident input, compared on the device"}
+
+    def _verify_all_bao_decode(self):
+        """decoding::bao of every object (decoding.rs:53-60): every status is
+        0 (every node verified) and every decoded content equals the object's
+        resident input, compared on the device 64 objects at a time."""
+        t0 = time.perf_counter()
+        n, bad = self.n, []
+        st = self.status.cpu().tolist()
+        bad_status = [o for o, v in enumerate(st) if v != 0]
+        for o0 in range(0, self.count, 64):
+            o1 = min(self.count, o0 + 64)
+            diff = (self.out[o0:o1, :n] != self.inp[o0:o1, :n]).any(dim=1)
+            bad += [o0 + int(i) for i in torch.nonzero(diff).flatten().tolist()]
+        torch.cuda.synchronize()
+        return {"ok": not bad and not bad_status, "objects": self.count, "mismatched": bad[:16],
+                "bad_status": bad_status[:16], "seconds": round(time.perf_counter() - t0, 1),
+                "how": "every object's status == 0 and its decoded content vs its resident input, on the device"}
 
     def _verify_all_e2e(self, threads: int):
         """encode() of every object (encoding.rs:86-172) against the C oracle
@@ -1016,6 +1057,35 @@ class Workload:
         return ok, sample
 
 
+def scatter_sample(rank: int, world: int, per: int, dev, group) -> dict:
+    """Rank 0 scatters `per` bytes to every rank once (after one warm-up
+    scatter), timed between barriers; every rank checks its slice (a
+    counter pattern, so each rank knows what it must receive)."""
+    gpu = dev.type == "cuda"
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
+    local = torch.empty(per, dtype=torch.uint8, device=dev)
+    chunks = None
+    base = torch.arange(256, dtype=torch.uint8, device=dev).repeat(per // 256 + 1)[:per]
+
+    def slice_of(r):  # rank r's bytes: a byte ramp shifted by 37 r (uint8 arithmetic wraps)
+        return base + (37 * r) % 256
+    if rank == 0:
+        chunks = [slice_of(r) for r in range(world)]
+    dist.scatter(local, chunks, src=0, group=group)  # warm the communicator
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    dist.scatter(local, chunks, src=0, group=group)
+    sync()
+    el = max_over_ranks(time.perf_counter() - t0)
+    oks = [None] * world
+    dist.all_gather_object(oks, bool(torch.equal(local, slice_of(rank))))
+    del local, chunks, base
+    return {"ranks": world, "bytes_per_rank": per, "seconds": round(el, 4),
+            "GiB_per_s_total": round((world - 1) * per / el / 2**30, 2),
+            "GiB_per_s_per_receiver": round(per / el / 2**30, 2), "every_slice_ok": all(oks)}
+
+
 class DryRun:
     """Control-plane rehearsal without a device (CPU gloo tests)."""
 
@@ -1051,6 +1121,9 @@ def main():
         live = live_traffic(args, sys.argv[1:])  # before this process touches the GPU
     wl = DryRun(args, rank) if args.dry_run else Workload(args, rank, local, world)
     scatter = None
+    if world > 1 and args.dry_run and args.scatter_gib > 0:  # the same collective over gloo, CPU tensors
+        scatter = scatter_sample(rank, world, 1 << 20, torch.device("cpu"), None)
+        scatter["how"] = "dry run: the RCCL sample's scatter over gloo with 1 MiB CPU tensors per rank"
     if world > 1 and not args.dry_run and not args.scatter and args.scatter_gib > 0:
         if torch.cuda.device_count() >= world:
             try:  # outside the metric: an RCCL failure is reported, not fatal to the measurement
@@ -1073,7 +1146,7 @@ def main():
     if rank == 0 and not args.no_verify and not args.dry_run:
         verified, sample = wl.verify_object0()
     verified_all = None
-    want_all = ((args.mode in ("encode", "decode", "e2e") and not args.no_verify_all) or
+    want_all = ((args.mode in ("encode", "decode", "e2e", "bao", "bao-decode") and not args.no_verify_all) or
                 (args.mode == "pipeline" and args.verify_all))
     if want_all and not args.no_verify and not args.dry_run:
         # every rank checks its own objects (N > 1: the whole global set), rank 0 reports;
@@ -1169,9 +1242,8 @@ def main():
                                                            "WRITE_SIZE": live["WRITE_SIZE_KiB"]},
                                     "pmc_kernel": live["kernel"]})
         if args.mode.startswith("e2e") or args.mode in ("scrub", "hasher", "file"):
-            res["roofline"].update({"bound": "pcie", "peak": 2 * 63.0,
-                                    "frac": round(achieved / 126.0, 4),
-                                    "note": "PCIe Gen5 x16, 63 GB/s per direction (spec), H2D and D2H overlapped"})
+            res["roofline"].update(pcie_roofline(getattr(wl, "h2d_bytes", 0), getattr(wl, "d2h_bytes", 0),
+                                                 max_elapsed / args.steps, achieved))
             res["data"] = ("synthetic (uniform random bytes), pinned host buffers" if args.mode.startswith("e2e")
                            else "synthetic (uniform random bytes) in files on the box's local disk, read and "
                                 "written through the page cache" if args.mode == "file"
@@ -1193,6 +1265,10 @@ def main():
                                "alg_ops_per_launch": ops, "hbm_achieved_GBps": hbm["achieved"],
                                "avg_launch_ms": hbm["avg_launch_ms"], "min_launch_ms": hbm["min_launch_ms"],
                                "peak_source": VALU_PEAK_SRC,
+                               "peak_kind": "measured BLAKE3-loop ceiling (the product's own best compression "
+                                            "loop), not a hardware figure",
+                               "hw_valu_peak_TOPS": HW_VALU_PEAK_TOPS,
+                               "frac_of_hw_valu": round(tops / HW_VALU_PEAK_TOPS, 4),
                                "note": "ops = 672 per BLAKE3 compression (content blocks + parents); peak = the "
                                        "measured compression ceiling x 672"
                                        + ("; achieved over the whole step (every kernel of the level)"
@@ -1250,10 +1326,11 @@ def main():
                               "how": "RCCL scatter from rank 0 over xGMI (outside the timed region)"}
         if args.dry_run:
             res["dry_run"] = True
-        elif not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(args, n, sample)
+        if not args.no_cpu_baseline:
+            # rank 0, after the timed region and the checks, at any N (the other ranks are done)
+            res["cpu_baseline"] = cpu_baseline(args, n, sample, seconds=0.5 if args.dry_run else None)
             threads = min(args.cpu_threads, os.cpu_count() or 1)
-            if threads > 1:
+            if threads > 1 and not args.dry_run:
                 res["cpu_baseline_all_cores"] = cpu_baseline(args, n, sample, threads)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -121,8 +121,8 @@ __device__ __forceinline__ void b3_g4(uint32_t &a0, uint32_t &b0, uint32_t &c0, 
             "s_nop 0\n\t"
             "v_alignbit_b32 %4, %4, %4, 7\n\tv_alignbit_b32 %5, %5, %5, 7\n\t"
             "v_alignbit_b32 %6, %6, %6, 7\n\tv_alignbit_b32 %7, %7, %7, 7"
-            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3),
-              "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3)
+            : "+&v"(a0), "+&v"(a1), "+&v"(a2), "+&v"(a3), "+&v"(b0), "+&v"(b1), "+&v"(b2), "+&v"(b3),
+              "+&v"(c0), "+&v"(c1), "+&v"(c2), "+&v"(c3), "+&v"(d0), "+&v"(d1), "+&v"(d2), "+&v"(d3)
             : "v"(x0), "v"(x1), "v"(x2), "v"(x3), "v"(y0), "v"(y1), "v"(y2), "v"(y3));
         return;
     }

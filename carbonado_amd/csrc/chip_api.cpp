@@ -2467,7 +2467,17 @@ int chip_bao_hasher_update(chip_bao_hasher *h, const uint8_t *buf, uint64_t n) {
     if (st != CHIP_OK) return st;
     if (h->content.cap < h->len + n) CHIP_HIP(hipStreamSynchronize(h->hstream));  // hashing reads the old buffer
     CHIP_HIP(grow_keep(h->content, h->len + n, h->len, h->stream));
+    // the caller may reuse buf on return: a staged copy is done with it already, a direct one
+    // (pinned buf) is waited for on every return path below, the error paths included
+    struct SyncDirect {
+        hipStream_t s;
+        bool on;
+        ~SyncDirect() {
+            if (on) (void)hipStreamSynchronize(s);
+        }
+    } sync_direct{h->stream, false};
     CHIP_HIP(h2d(c->stage, static_cast<uint8_t *>(h->content.p) + h->len, buf, n, h->stream));
+    sync_direct.on = !staged(buf, n);
     h->len += n;
     // units u with bytes past them ((u + 1) * 64 KiB < len): full chunks, none of them the last;
     // hashed on the second stream once their bytes have landed, so the copies never wait for it.
@@ -2485,9 +2495,10 @@ int chip_bao_hasher_update(chip_bao_hasher *h, const uint8_t *buf, uint64_t n) {
                                    static_cast<uint8_t *>(h->cv0.p), h->hstream));
         h->units = ready;
     }
-    // the caller may reuse buf on return: a staged copy is done with it already,
-    // a direct one (pinned buf) is waited for
-    if (!staged(buf, n)) CHIP_HIP(hipStreamSynchronize(h->stream));
+    if (sync_direct.on) {
+        sync_direct.on = false;
+        CHIP_HIP(hipStreamSynchronize(h->stream));
+    }
     return CHIP_OK;
 }
 

@@ -405,9 +405,11 @@ CHIP_API int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, u
  * node of every stream is verified on the device in one pass, then each
  * stream's shards (the slices decoding.rs:173-183 verifies): status[o]
  * (host) = CHIP_ERR_UNNECESSARY_SCRUB for an intact stream, CHIP_ERR_ZFEC
- * with fewer than 4 authentic shards, else the repaired stream is written to
- * d_out + o*out_stride and status[o] = CHIP_OK or the reference's scrub error
- * (padding / length mismatch, invalid scrubbed hash).  d_scratch:
+ * with fewer than 4 authentic shards, else the stream is repaired and
+ * status[o] = CHIP_OK or the reference's scrub error (padding / length
+ * mismatch, invalid scrubbed hash).  Row o of d_out (d_out + o*out_stride)
+ * is written only when status[o] == CHIP_OK (the repaired stream's hash
+ * matched); every other row is left untouched.  d_scratch:
  * chip_scrub_scratch_len(len, count) bytes.  Pointers and strides multiples
  * of 16.  Synchronous: returns when every status is final. */
 CHIP_API uint64_t chip_scrub_scratch_len(uint64_t len, uint64_t count);

@@ -60,3 +60,23 @@ def test_live_traffic_two_passes(tmp_path, monkeypatch):
     assert "gf_apply_kernel<4, 1," in r["kernel"]
     # a mode without an HBM-bound kernel gets no passes
     assert "error" in bench.live_traffic(bench.parse(["--mode", "bao"]), [])
+
+
+def test_pcie_roofline_names_the_binding_direction():
+    """E2E lines price each PCIe direction on its own:
+    cfg4 moves ~2.1x as many bytes D2H as H2D, so D2H binds and the frac is
+    against one direction's 63 GB/s, not the 126 GB/s duplex sum."""
+    import bench
+    n, out = 16 << 20, 35_660_232
+    r = bench.pcie_roofline(1024 * n, 1024 * out, 0.7088, 75.5)
+    assert r["bound"] == "pcie-d2h" and r["peak"] == 63.0 and r["unit"] == "GB/s"
+    assert abs(r["d2h_GBps"] - 1024 * out / 0.7088 / 1e9) < 0.01
+    assert abs(r["frac"] - r["d2h_GBps"] / 63.0) < 1e-3 and 0.8 < r["frac"] < 0.84
+    assert r["h2d_GBps"] < r["d2h_GBps"] and r["achieved"] == r["d2h_GBps"]
+    assert abs(r["frac_of_measured"] - r["d2h_GBps"] / 55.0) < 1e-3
+    assert r["duplex_frac"] == round(75.5 / 126.0, 4)
+    # decode reads the stream up and writes the content down: H2D binds
+    r = bench.pcie_roofline(1024 * out, 1024 * n, 0.8, 0)
+    assert r["bound"] == "pcie-h2d" and r["peak_measured"] == 55.6
+    # the hasher only uploads
+    assert bench.pcie_roofline(1 << 30, 0, 0.05, 0)["bound"] == "pcie-h2d"

@@ -1,0 +1,228 @@
+"""The Rust side of the drop-in boundary (carbonado-hip/), checked on CPU.
+
+This image has no Rust toolchain, so the crate is checked by parsing it:
+
+* every `CHIP_API` prototype of include/carbonado_hip.h has exactly one
+  `extern "C"` declaration in carbonado-hip/src/ffi.rs and vice versa, with
+  the same arity and the C <-> Rust type of every parameter and return value
+  (fails if either side drifts);
+* the `#[repr(C)]` structs have the header's fields, in order, with the
+  mapped types; the C sizes are the ones lib.rs's own unit test asserts;
+* the status codes and constants agree, and lib.rs maps every status;
+* carbonado-hip/reroute.patch applies to the reference crate and reroutes
+  the five seam functions (encoding.rs:39,48, decoding.rs:21,35,54).
+"""
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "carbonado_hip.h"
+CRATE = ROOT / "carbonado-hip"
+FFI = CRATE / "src" / "ffi.rs"
+LIB = CRATE / "src" / "lib.rs"
+REFERENCE = Path("/root/reference")
+
+C_BASE = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": "u64", "int32_t": "i32",
+          "int": "c_int", "char": "c_char", "float": "f32", "double": "f64", "ssize_t": "isize",
+          "size_t": "usize", "void": "c_void"}
+
+
+def _strip_comments(text: str) -> str:
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    return re.sub(r"//[^\n]*", " ", text)
+
+
+def c_to_rust(ctype: str, array: bool = False) -> str:
+    """C declaration type -> the Rust FFI type it must be bound as.
+    `const T *const *` -> `*const *const T'`; an array parameter decays to a
+    pointer; a bare `void` return is the empty string."""
+    toks = re.findall(r"\w+|\*", ctype)
+    base_const = False
+    base = None
+    i = 0
+    while i < len(toks) and toks[i] != "*":
+        if toks[i] == "const":
+            base_const = True
+        else:
+            base = toks[i]
+        i += 1
+    assert base is not None, ctype
+    t = C_BASE.get(base, base)
+    ptrs = toks[i:]
+    if not ptrs and not array:
+        return "" if t == "c_void" else t
+    pointee_const = base_const
+    j = 0
+    while j < len(ptrs):
+        assert ptrs[j] == "*", ctype
+        t = ("*const " if pointee_const else "*mut ") + t
+        pointee_const = j + 1 < len(ptrs) and ptrs[j + 1] == "const"
+        j += 2 if pointee_const else 1
+    if array:
+        t = ("*const " if pointee_const else "*mut ") + t
+    return t
+
+
+def header_prototypes() -> dict:
+    text = _strip_comments(HEADER.read_text())
+    protos = {}
+    for ret, name, params in re.findall(r"CHIP_API\s+([^;{}()]*?)\b(chip_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
+        ps = []
+        params = " ".join(params.split())
+        if params and params != "void":
+            for p in params.split(","):
+                p = p.strip()
+                m = re.match(r"(.*?)(\w+)\s*(\[[^\]]*\])?$", p)
+                assert m, p
+                ps.append((m.group(2), c_to_rust(m.group(1), array=bool(m.group(3)))))
+        protos[name] = (c_to_rust(ret), ps)
+    return protos
+
+
+def rust_declarations() -> dict:
+    text = _strip_comments(FFI.read_text())
+    decls = {}
+    for block in re.findall(r'extern\s+"C"\s*\{(.*?)\n\}', text, flags=re.S):
+        for name, params, ret in re.findall(r"pub\s+fn\s+(chip_\w+)\s*\(([^)]*)\)\s*(?:->\s*([^;]+?))?\s*;",
+                                            block, flags=re.S):
+            assert name not in decls, f"{name} declared twice"
+            ps = []
+            params = " ".join(params.split())
+            for p in filter(None, (x.strip() for x in params.split(","))):
+                pname, ptype = (s.strip() for s in p.split(":", 1))
+                ps.append((pname, " ".join(ptype.split())))
+            decls[name] = (" ".join(ret.split()) if ret else "", ps)
+    return decls
+
+
+def test_every_export_declared_with_matching_types():
+    h, r = header_prototypes(), rust_declarations()
+    assert len(h) == 58, sorted(h)
+    assert set(h) == set(r), {"missing in ffi.rs": sorted(set(h) - set(r)),
+                              "not in the header": sorted(set(r) - set(h))}
+    for name, (cret, cps) in h.items():
+        rret, rps = r[name]
+        assert cret == rret, f"{name}: return {cret!r} in C, {rret!r} in Rust"
+        assert len(cps) == len(rps), f"{name}: {len(cps)} parameters in C, {len(rps)} in Rust"
+        for (cn, ct), (rn, rt) in zip(cps, rps):
+            assert ct == rt, f"{name}({cn}): C maps to {ct!r}, Rust declares {rt!r}"
+            assert rn == cn or (cn, rn) == ("in", "input"), f"{name}: parameter {cn!r} named {rn!r}"
+
+
+def test_batch_entry_points_and_allocator_are_declared():
+    """the cfg3 / bao batch paths, chip_init, the error string and
+    the allocator Rust callers need for the fast placement."""
+    r = rust_declarations()
+    for name in ("chip_zfec_decode_batch_dev", "chip_bao_encode_batch_dev", "chip_bao_decode_batch_dev",
+                 "chip_init", "chip_last_device_error", "chip_device_alloc", "chip_device_free",
+                 "chip_zfec_encode_batch_dev", "chip_encode_batch_dev", "chip_decode_batch_dev",
+                 "chip_scrub_batch_dev"):
+        assert name in r
+    lib = LIB.read_text()
+    # the batch wrappers' default buffers come from chip_device_alloc
+    assert re.search(r"fn alloc\(count: u64, row: u64\).*?DeviceBuffer::new", lib, flags=re.S)
+    assert re.search(r"fn new\(bytes: usize\).*?ffi::chip_device_alloc\(", lib, flags=re.S)
+    assert "ffi::chip_device_free(" in lib
+    for w in ("zfec_encode_batch", "zfec_decode_batch", "bao_encode_batch", "bao_decode_batch", "encode_batch",
+              "decode_batch", "scrub_batch"):
+        assert re.search(rf"pub fn {w}\(", lib), w
+
+
+def _c_struct_fields(name: str) -> list:
+    text = _strip_comments(HEADER.read_text())
+    m = re.search(r"typedef struct " + name + r"\s*\{(.*?)\}", text, flags=re.S)
+    out = []
+    for line in m.group(1).split(";"):
+        line = " ".join(line.split())
+        if not line:
+            continue
+        f = re.match(r"(.*?)(\w+)\s*(?:\[(\d+)\])?$", line)
+        ct = c_to_rust(f.group(1))
+        out.append((f.group(2), f"[{ct}; {f.group(3)}]" if f.group(3) else ct))
+    return out
+
+
+def _rust_struct_fields(name: str) -> list:
+    text = _strip_comments(FFI.read_text())
+    m = re.search(r"#\[repr\(C\)\][^{]*?pub struct " + name + r"\s*\{(.*?)\n\}", text, flags=re.S)
+    assert m, name
+    return [(a, " ".join(b.split())) for a, b in re.findall(r"pub\s+(\w+)\s*:\s*([^,]+),", m.group(1))]
+
+
+@pytest.mark.parametrize("name", ["chip_encode_info", "chip_ecies_inject", "chip_header"])
+def test_struct_layouts_match(name):
+    assert _c_struct_fields(name) == _rust_struct_fields(name)
+
+
+def test_c_struct_sizes_are_the_ones_lib_rs_asserts(tmp_path):
+    src = tmp_path / "sz.c"
+    src.write_text('#include "carbonado_hip.h"\n#include <stdio.h>\nint main(void){printf("%zu %zu %zu\\n",'
+                   "sizeof(chip_encode_info), sizeof(chip_ecies_inject), sizeof(chip_header));return 0;}\n")
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", str(HEADER.parent), str(src), "-o", str(exe)], check=True)
+    sizes = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    lib = LIB.read_text()
+    for ty, sz in zip(("ChipEncodeInfo", "ffi::chip_ecies_inject", "ChipHeader"), sizes):
+        assert f"size_of::<{ty}>(), {sz})" in lib, (ty, sz)
+
+
+def test_status_codes_and_constants_agree():
+    text = _strip_comments(HEADER.read_text())
+    enum = dict((k, int(v)) for k, v in re.findall(r"\b(CHIP_(?:OK|ERR_\w+))\s*=\s*(\d+)", text))
+    defines = dict((k, int(v.rstrip("u"))) for k, v in re.findall(r"#define (CHIP_\w+) (\d+u?)", text))
+    ffi = _strip_comments(FFI.read_text())
+    consts = dict((k, int(v)) for k, v in re.findall(r"pub const (CHIP_\w+): \w+ = (\d+);", ffi))
+    assert len(enum) == 23  # CHIP_OK + 22 error codes
+    for k, v in {**enum, **defines}.items():
+        assert consts.get(k) == v, (k, v, consts.get(k))
+    lib = _strip_comments(LIB.read_text())
+    arms = set(re.findall(r"ffi::(CHIP_ERR_\w+) =>", lib))
+    assert arms == {k for k in enum if k != "CHIP_OK"}, sorted(set(enum) ^ arms)
+    rev = set(re.findall(r"=> ffi::(CHIP_ERR_\w+),", lib))
+    assert rev == arms  # ChipError::status() maps every variant back
+
+
+def test_reroute_patch_targets_the_five_seams():
+    patch = (CRATE / "reroute.patch").read_text()
+    files = re.findall(r"^\+\+\+ b/(\S+)", patch, flags=re.M)
+    assert files == ["Cargo.toml", "src/decoding.rs", "src/encoding.rs", "src/error.rs"]
+    added = "\n".join(l[1:] for l in patch.splitlines() if l.startswith("+") and not l.startswith("+++"))
+    for call in ("carbonado_hip::bao_encode(", "carbonado_hip::zfec_encode(", "carbonado_hip::zfec_decode(",
+                 "carbonado_hip::zfec_decode_shares(", "carbonado_hip::bao_decode("):
+        assert call in added, call
+    # every rerouted call sits behind the feature, the CPU path stays the default
+    assert added.count('#[cfg(feature = "hip")]') >= 5
+    assert 'hip = ["dep:carbonado-hip"]' in added
+    # the public API (lib.rs:21-29) is untouched
+    assert "src/lib.rs" not in files
+    # each wrapper the patch calls exists in the crate
+    lib = LIB.read_text()
+    for fn in ("bao_encode", "zfec_encode", "zfec_decode", "zfec_decode_shares", "bao_decode"):
+        assert re.search(rf"pub fn {fn}\(", lib), fn
+
+
+@pytest.mark.skipif(not (REFERENCE / "src" / "encoding.rs").exists() or shutil.which("patch") is None,
+                    reason="the reference crate is only present in the build container")
+def test_reroute_patch_applies_to_the_reference(tmp_path):
+    for rel in ("Cargo.toml", "src/encoding.rs", "src/decoding.rs", "src/error.rs"):
+        (tmp_path / rel).parent.mkdir(parents=True, exist_ok=True)
+        shutil.copy(REFERENCE / rel, tmp_path / rel)
+    out = subprocess.run(["patch", "-p1", "--forward", "-i", str(CRATE / "reroute.patch")], cwd=tmp_path,
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    enc = (tmp_path / "src/encoding.rs").read_text()
+    assert "pub fn zfec(input: &[u8]) -> Result<(Vec<u8>, u32, u32), CarbonadoError>" in enc
+    assert "fn zfec_cpu(" in enc
+
+
+def test_c_to_rust_mapping_rules():
+    assert c_to_rust("const uint8_t *const *") == "*const *const u8"
+    assert c_to_rust("void **") == "*mut *mut c_void"
+    assert c_to_rust("uint8_t", array=True) == "*mut u8"
+    assert c_to_rust("const char *") == "*const c_char"
+    assert c_to_rust("void") == "" and c_to_rust("ssize_t") == "isize"
+    assert c_to_rust("const chip_ecies_inject *") == "*const chip_ecies_inject"

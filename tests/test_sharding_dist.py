@@ -154,3 +154,9 @@ def test_bench_cfg5_eight_ranks_dry_run():
     assert (res["config"]["k"], res["config"]["m"]) == (8, 16)
     assert len(res["roofline"]["per_rank_avg_launch_ms"]) == 8
     assert 1 <= res["verify_threads_per_rank"] <= 16
+    # the N>1 line carries the CPU baseline (rank 0, after the timed region) and the
+    # scatter sample (gloo stands in for RCCL in the dry run): every rank got its slice
+    cb = res["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] == "port" and "8-of-16" in cb["sample"]
+    sc = res["scatter"]
+    assert sc["ranks"] == 8 and sc["every_slice_ok"] is True and sc["bytes_per_rank"] > 0
