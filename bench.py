@@ -810,7 +810,7 @@ class Workload:
             self.kernel = "bao_chunk_kernel<1> (verify + content) + bao_parent_kernel<1> levels"
             self.kernel_sym = "bao_chunk_kernel<1,"
         else:
-            blen = L.chip_bao_encoded_len(n)
+            self.blen = blen = L.chip_bao_encoded_len(n)
             self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.bao_scratch(n, count, dev)

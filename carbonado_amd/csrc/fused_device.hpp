@@ -161,7 +161,8 @@ struct Tree {
 // 2 = no hashing, 3 = no GF (rows get the data shards only), 4 = neither
 // stores nor hashing, 5 = every chunk's lines 128-B aligned (no partial
 // lines), 6 = 5 without hashing, 7 = the line stores' LDS reads without the
-// stores, 8 = the whole-line stores aimed at 8 KiB per wave (L2 hits).
+// stores, 8 = the whole-line stores aimed at 8 KiB per wave (L2 hits),
+// 10 = GF table lookups without bank conflicts (wrong products).
 // FULL: cols % 8 == 0 and no zfec padding (valid >= 4 C): every block is 8
 // whole columns of plain loads, levels 1-3 run in the wave (Tree) and `cv`
 // receives level-3 CVs; otherwise lanes are predicated and `cv` receives the
@@ -188,7 +189,7 @@ struct Tree {
 // to measure the kernel's sensitivity to occupancy).
 template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
           bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false, int PRIO = 0>
-__global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
+__global__ __launch_bounds__(64 * WPG) void zfec_bao_fused_kernel(FusedArgs a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int NV = KIND ? 8 : 4;         // 16-B loads per lane per step
@@ -205,7 +206,9 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    uint32_t *rows = reinterpret_cast<uint32_t *>(lds + TAB_BYTES) + wave * 64 * RW;
+    // WPG > FW (tools/fused_tune occupancy diagnostic only, wrong output): the
+    // extra waves share the first waves' rows, the LDS holds FW waves' rows
+    uint32_t *rows = reinterpret_cast<uint32_t *>(lds + TAB_BYTES) + (WPG > FW ? wave % FW : wave) * 64 * RW;
     const int rep = lane % FR, grp = (lane & 31) / FR;
     uint32_t tb[4], tb2[4];
     uint64_t ioff[4];
@@ -343,6 +346,10 @@ __global__ __launch_bounds__(FTPB) void zfec_bao_fused_kernel(FusedArgs a) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         x[j] = zf::comp(v[j], d);
+                        // DG 10 (diagnostic, wrong bytes): lanes l and l + 16 look up
+                        // table rows of opposite parity, so no two lanes of a 32-lane
+                        // half meet on one bank (FR 4: bank = 16 (x & 1) + 4 s + r)
+                        if (DG == 10) x[j] = (x[j] & 0xFEFEFEFEu) | ((uint32_t)((lane >> 4) & 1) * 0x01010101u);
                         if (GFP) {
                             const uint32_t t02 = gf_pair(x[j], 0, tb2[j]), t13 = gf_pair(x[j], 1, tb2[j]);
                             ad[j][0] = t02 & 0xFFFFu; ad[j][2] = t02 >> 16;

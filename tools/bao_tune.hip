@@ -94,7 +94,10 @@ int main(int argc, char **argv) {
     // stores, XG 1, DQ), hash-only encode for the VALU ceiling.  A decode variant issuing the content
     // stores after the next step's loads (read back from the rows) measured the same (r2x_bao_tune.txt)
     std::vector<V> vs = {mk<0, 2, false, 3, 8, 0, 1, true>(true), mk<1, 2, true, 0, 1, 0, 1, true>(true),
-                         mk<0, 2, false, 0, 1, 0, 1, true>(false)};
+                         mk<0, 2, false, 0, 1, 0, 1, true>(false),
+                         // round 4: decode without the duplicated border-line fetches
+                         // (diagnostic, wrong output), then the product again
+                         mk<1, 2, true, 0, 1, 6, 1, true>(true), mk<1, 2, true, 0, 1, 0, 1, true>(true)};
     // earlier: product encode / decode / in-place with XG 0 and 1 (profiles/r1x_ab_bao_xcd_order.txt)
     // round-1 store diagnostics (profiles/r1x_bao_store_diagnostics.txt): mk<0, 2, false>(false) hash-only,
     // mk<0, 2, false, 3, 1, SE>(true) for SE 2..5, mk<0, 1, false, 3>(true), mk<1, 1, false>(true)

@@ -147,7 +147,16 @@ int main(int argc, char **argv) {
         {"K1 DG7 piece reads, no stores", fused::zfec_bao_fused_kernel<true, true, 1, 7, 1>, 1},
         {"K1 DG2 no hash", fused::zfec_bao_fused_kernel<true, true, 1, 2, 1>, 1},
         {"K0 FULL K13S spec (again)", fused::zfec_bao_spec_kernel<true>, 0, true},
-        {"K0 FULL (product, again)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 0}};
+        {"K0 FULL (product, again)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 0},
+        // round 4: occupancy and LDS-conflict diagnostics (wrong output)
+        {"K0 DG10 GF lookups conflict-free", fused::zfec_bao_fused_kernel<true, true, 1, 10, 0, true, 0, 0, true, 1>, 0},
+        {"K0 DG3 no GF (product params)", fused::zfec_bao_fused_kernel<true, true, 1, 3, 0, true, 0, 0, true, 1>, 0},
+        {"K0 DG1 no line stores/reads (product params)", fused::zfec_bao_fused_kernel<true, true, 1, 1, 0, true, 0, 0, true, 1>, 0},
+        {"K0 DG7 piece reads, no stores (product params)", fused::zfec_bao_fused_kernel<true, true, 1, 7, 0, true, 0, 0, true, 1>, 0},
+        {"K0 DG-occ WPG12 3 waves/SIMD rows aliased", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1, 12>, 0},
+        {"K0 general product", fused::zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, true, 1>, 0},
+        {"K0 general DG-occ WPG12 3 waves/SIMD rows aliased", fused::zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, true, 1, 12>, 0},
+        {"K0 FULL (product, third)", fused::zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 0}};
     std::vector<Variant> vs;
     for (auto &v : all)
         if (!strcmp(which, "all") || strstr(v.name.c_str(), which)) vs.push_back(v);
@@ -165,7 +174,8 @@ int main(int argc, char **argv) {
             const uint64_t blocks = count * a.bpo;
             const unsigned grid = (unsigned)std::min<uint64_t>(256, (blocks + fused::FW - 1) / fused::FW);
             const unsigned tpb = vs[v].spec ? (vs[v].name.find("NPB1") != std::string::npos ? fused::stpb<1>() : fused::STPB)
-                                 : vs[v].name.find("WPG4") != std::string::npos ? 256u : fused::FTPB;
+                                 : vs[v].name.find("WPG4") != std::string::npos ? 256u
+                                 : vs[v].name.find("WPG12") != std::string::npos ? 768u : fused::FTPB;
             const size_t ldsb = vs[v].spec ? fused::S_LDS_BYTES : fused::LDS_BYTES;
             hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(tpb), ldsb, 0, a);
             CK(hipEventRecord(e0));

@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof
+#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -20,6 +20,7 @@ for s in "$@"; do
     bao) run bench_bao 600 python3 bench.py --mode bao --no-cpu-baseline ;;
     baodec) run bench_bao_decode 600 python3 bench.py --mode bao-decode --cpu-seconds 8 ;;
     pipe12) run bench_pipe12 600 python3 bench.py --mode pipeline --level 12 --verify-all ;;
+    pipe12l15) run bench_pipe12_l15shape 600 python3 bench.py --mode pipeline --level 12 --object-bytes 16779371 --verify-all ;;
     pdec12) run bench_pdec12 600 python3 bench.py --mode pipeline-decode --level 12 ;;
     pdec4) run bench_pdec4 600 python3 bench.py --mode pipeline-decode --level 4 ;;
     pdec8) run bench_pdec8 600 python3 bench.py --mode pipeline-decode --level 8 ;;
@@ -34,6 +35,14 @@ for s in "$@"; do
     file15) run bench_file15 600 python3 bench.py --mode file --level 15 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     file12) run bench_file12 600 python3 bench.py --mode file --level 12 --steps 3 --warmup 1 --no-cpu-baseline ;;
     prof) bash tools/gpu_prof.sh $TAG ;;
+    encodetorch) run bench_encode_alloc_torch 600 python3 bench.py --alloc torch --no-cpu-baseline --live-pmc off ;;
+    mixprobe) run mix_probe_bal 300 ./tools/mix_probe 1024 3 bal ;;
+    ftune) run fused_tune 300 ./tools/fused_tune 256 5 ;;
+    ftunepmc) run fused_tune_pmc 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU -d $O/ftpmc -o ftpmc --output-format csv -- ./tools/fused_tune 256 1 ;;
+    baotune) run bao_tune 300 ./tools/bao_tune 256 32 5 ;;
+    baotunepmc) run bao_tune_fetch 300 rocprofv3 --pmc FETCH_SIZE -d $O/btpmc -o btpmc --output-format csv -- ./tools/bao_tune 256 32 1 1,3 ;;
+    numaprobe) run numa_probe 120 python3 tools/numa_probe.py ;;
+    valuprobe) run valu_probe_b3x2 300 ./tools/valu_probe 40000 b3x2 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
