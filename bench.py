@@ -1314,6 +1314,11 @@ def main():
         if scatter is not None:
             res["scatter"] = scatter
         if args.mode == "hasher" and not args.dry_run:
+            from carbonado_amd import device as _dev
+            try:
+                res["host_topology"] = _dev.host_topology()
+            except Exception as e:  # diagnostic only
+                res["host_topology"] = {"error": str(e)[:200]}
             fm = sorted(wl.finalize_ms[-args.steps:])
             res["finalize_ms"] = {"median": round(fm[len(fm) // 2], 3), "max": round(fm[-1], 3),
                                   "how": "host wall time of finalize() after the last update() of each timed step "

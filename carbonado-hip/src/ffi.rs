@@ -140,6 +140,7 @@ extern "C" {
     pub fn chip_torch_alloc(size: isize, device: c_int, stream: *mut c_void) -> *mut c_void;
     pub fn chip_torch_free(ptr: *mut c_void, size: isize, device: c_int, stream: *mut c_void);
     pub fn chip_stream_queue_block(stream: *mut c_void, addr: *mut u64) -> c_int;
+    pub fn chip_host_topology(json: *mut c_char, cap: u64, len: *mut u64) -> c_int;
 
     // ---- size helpers (host only)
     pub fn chip_calc_padding_len(input_len: u64, k: u32, padding: *mut u32, chunk_len: *mut u32) -> c_int;

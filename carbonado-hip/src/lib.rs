@@ -505,6 +505,18 @@ impl Drop for BaoHasher {
     }
 }
 
+/// Where this process's host-copy path sits on the box (JSON): the GPU's
+/// NUMA node, the staging ring's node, the copy workers' nodes (diagnostic).
+pub fn host_topology() -> Result<String> {
+    abi()?;
+    let mut len = 0u64;
+    let _ = unsafe { ffi::chip_host_topology(ptr::null_mut(), 0, &mut len) };
+    let mut buf = vec![0u8; len.max(1) as usize];
+    check(unsafe { ffi::chip_host_topology(buf.as_mut_ptr() as *mut std::os::raw::c_char, len, &mut len) })?;
+    buf.truncate(len.saturating_sub(1) as usize);
+    Ok(String::from_utf8_lossy(&buf).into_owned())
+}
+
 // ---- device-resident batch API ----------------------------------------------
 
 /// A HIP stream handle (`hipStream_t`); [`Stream::DEFAULT`] = the library's

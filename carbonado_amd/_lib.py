@@ -86,6 +86,7 @@ SIGNATURES = {
     "chip_device_alloc_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double)]),
     "chip_stream_queue_block": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "chip_host_topology": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "chip_torch_alloc": (ctypes.c_void_p, [ctypes.c_ssize_t, ctypes.c_int, ctypes.c_void_p]),
     "chip_torch_free": (None, [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_int, ctypes.c_void_p]),
     "chip_calc_padding_len": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, c_u32p, c_u32p]),

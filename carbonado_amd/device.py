@@ -215,3 +215,16 @@ def decode_host_batch(fmt: int, enc: torch.Tensor, in_len, hashes: torch.Tensor,
     if rc and (raise_first or not any(statuses)):
         raise status_to_error(rc)
     return [olen[o] for o in range(count)], statuses
+
+
+def host_topology() -> dict:
+    """Where this process's host-copy path sits (chip_host_topology): the
+    GPU's NUMA node, the calling thread's staging ring node and the copy
+    workers' nodes (diagnostic)."""
+    import json
+    L = _lib.lib()
+    n = ctypes.c_uint64(0)
+    L.chip_host_topology(None, 0, ctypes.byref(n))
+    buf = ctypes.create_string_buffer(max(1, n.value))
+    check(L.chip_host_topology(buf, n.value, ctypes.byref(n)))
+    return json.loads(buf.value.decode())

@@ -206,6 +206,14 @@ CHIP_API void chip_torch_free(void *ptr, ssize_t size, int device, void *stream)
  * (DESIGN.md §3 K1 "Counter blocks"). */
 CHIP_API int chip_stream_queue_block(void *stream, uint64_t *addr);
 
+/* Diagnostic: where this process's host-copy path sits on the box, as a JSON
+ * object: the GPU's PCI address and NUMA node, the calling thread's pinned
+ * staging ring's node, the copy workers and the nodes of the CPUs they last
+ * copied on.  The ring and the workers are placed on the GPU's node
+ * (CHIP_NUMA=0: runtime defaults).  *len = bytes needed including the NUL;
+ * a short buffer returns CHIP_ERR_BUFFER_TOO_SMALL. */
+CHIP_API int chip_host_topology(char *json, uint64_t cap, uint64_t *len);
+
 /* ---- size helpers (host only, no device needed) ----------------------- */
 /* utils.rs:47-58 with FEC_K generalised to k: target = ceil(n/(1024k))*1024k,
  * padding = target - n, chunk_len = target / k (integer maths; the reference's

@@ -65,3 +65,23 @@ def test_hasher_pageable_and_pinned_appends(gpu):
     allb = b"".join(p.tobytes() for p in pieces)
     assert bytes(h.finalize()) == O.blake3(allb)
     assert h.read_all() == O.bao_encode(allb)[0]
+
+
+def test_host_topology_ring_and_workers_on_the_gpu_node(gpu):
+    """chip_host_topology after a staged copy: the ring exists, and with NUMA
+    placement on (the default) the ring's pages and every copy worker that
+    has run sit on the GPU's node whenever the process may use its CPUs."""
+    import carbonado_amd as ca
+    from carbonado_amd.device import host_topology
+    d = np.random.default_rng(3).integers(0, 256, 24 << 20, dtype=np.uint8)
+    enc, h, info = ca.encode(b"", d, 12)  # pageable in and out: through the ring
+    t = host_topology()
+    for key in ("gpu_pci", "gpu_node", "ring_node", "copy_workers", "copy_workers_pinned",
+                "copy_workers_by_last_cpu_node", "numa_placement"):
+        assert key in t, t
+    assert t["ring_node"] >= 0, t
+    if t["numa_placement"] and t["gpu_node"] >= 0 and t["gpu_local_cpus_allowed"] > 0:
+        assert t["copy_workers_pinned"], t
+        assert t["ring_node"] == t["gpu_node"], t
+        ran = {k: v for k, v in t["copy_workers_by_last_cpu_node"].items() if k != "idle"}
+        assert set(ran) <= {str(t["gpu_node"])}, t

@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc
+#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -32,6 +32,7 @@ for s in "$@"; do
     scrub) run bench_scrub 600 python3 bench.py --mode scrub --steps 2 --warmup 1 --cpu-seconds 8 ;;
     scrubb) run bench_scrub_batch 600 python3 bench.py --mode scrub-batch --steps 5 --warmup 1 --cpu-seconds 8 ;;
     hasher) run bench_hasher 600 python3 bench.py --mode hasher --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    hasher3) for i in 1 2 3; do run bench_hasher_numa_$i 300 python3 bench.py --mode hasher --steps 3 --warmup 1 --no-cpu-baseline; CHIP_NUMA=0 run bench_hasher_nonuma_$i 300 python3 bench.py --mode hasher --steps 3 --warmup 1 --no-cpu-baseline; done ;;
     file15) run bench_file15 600 python3 bench.py --mode file --level 15 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     file12) run bench_file12 600 python3 bench.py --mode file --level 12 --steps 3 --warmup 1 --no-cpu-baseline ;;
     prof) bash tools/gpu_prof.sh $TAG ;;
