@@ -89,6 +89,21 @@ constexpr bool B3_GROUPED = B3_GROUPED_DEF;
 #ifndef B3_ONEASM_DEF
 #define B3_ONEASM_DEF 1
 #endif
+// B3_PK16 1: the rotate by 16 of each G as v_pk_add_u16 with swapped halves
+// (x.hi + 0 | (x.lo + 0) << 16) instead of v_alignbit_b32 (tools/valu_probe
+// "pk", VAR 13/14); the other rotations stay alignbit.
+#ifndef B3_PK16_DEF
+#define B3_PK16_DEF 0
+#endif
+#if B3_PK16_DEF
+#define B3_ROT16_4                                                                                     \
+    "v_pk_add_u16 %12, %12, 0 op_sel:[1,0] op_sel_hi:[0,0]\n\tv_pk_add_u16 %13, %13, 0 op_sel:[1,0] op_sel_hi:[0,0]\n\t" \
+    "v_pk_add_u16 %14, %14, 0 op_sel:[1,0] op_sel_hi:[0,0]\n\tv_pk_add_u16 %15, %15, 0 op_sel:[1,0] op_sel_hi:[0,0]\n\t"
+#else
+#define B3_ROT16_4                                                                                     \
+    "v_alignbit_b32 %12, %12, %12, 16\n\tv_alignbit_b32 %13, %13, %13, 16\n\t"                          \
+    "v_alignbit_b32 %14, %14, %14, 16\n\tv_alignbit_b32 %15, %15, %15, 16\n\t"
+#endif
 __device__ __forceinline__ void b3_g4(uint32_t &a0, uint32_t &b0, uint32_t &c0, uint32_t &d0, uint32_t &a1,
                                       uint32_t &b1, uint32_t &c1, uint32_t &d1, uint32_t &a2, uint32_t &b2,
                                       uint32_t &c2, uint32_t &d2, uint32_t &a3, uint32_t &b3, uint32_t &c3,
@@ -101,8 +116,7 @@ __device__ __forceinline__ void b3_g4(uint32_t &a0, uint32_t &b0, uint32_t &c0, 
             "v_add3_u32 %2, %2, %6, %18\n\tv_add3_u32 %3, %3, %7, %19\n\t"
             "v_xor_b32 %12, %12, %0\n\tv_xor_b32 %13, %13, %1\n\tv_xor_b32 %14, %14, %2\n\tv_xor_b32 %15, %15, %3\n\t"
             "s_nop 0\n\t"
-            "v_alignbit_b32 %12, %12, %12, 16\n\tv_alignbit_b32 %13, %13, %13, 16\n\t"
-            "v_alignbit_b32 %14, %14, %14, 16\n\tv_alignbit_b32 %15, %15, %15, 16\n\t"
+            B3_ROT16_4
             "v_add_u32 %8, %8, %12\n\tv_add_u32 %9, %9, %13\n\tv_add_u32 %10, %10, %14\n\tv_add_u32 %11, %11, %15\n\t"
             "s_nop 0\n\t"
             "v_xor_b32 %4, %4, %8\n\tv_xor_b32 %5, %5, %9\n\tv_xor_b32 %6, %6, %10\n\tv_xor_b32 %7, %7, %11\n\t"

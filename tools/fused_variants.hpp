@@ -1,7 +1,7 @@
 // fused_variants.hpp — measured-and-not-kept variants of the fused kernels,
 // kept for tools/fused_tune.hip only (not part of the library):
 //  * K13S, zfec_bao_spec_kernel: K13's FULL path with hashing and GF/line
-//    stores on separate waves (profiles/r7jk_k13s_not_kept: 15-20 % slower);
+//    stores on separate waves (profiles/NOT_KEPT.md, r7jk: 15-20 % slower);
 //  * bao_levels123_seg_kernel: the general path's levels-1-3 pass writing
 //    whole 64-B segments (profiles/r7q: 0.499 vs 0.380 ms per 256 objects).
 #pragma once

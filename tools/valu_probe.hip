@@ -34,10 +34,11 @@
         }                                                                                     \
     } while (0)
 
-enum Op { ADD = 0, ADD3, XOR, BITOP3, ALIGNBIT, FMA, PERM, LSHLADD, XORSDWA, MIX, NOPS };
+enum Op { ADD = 0, ADD3, XOR, BITOP3, ALIGNBIT, FMA, PERM, LSHLADD, XORSDWA, MIX, PKSWAP, LSHLOR, XAD, OR3, NOPS };
 static const char *op_name[NOPS] = {"v_add_u32", "v_add3_u32", "v_xor_b32", "v_bitop3_b32",
                                     "v_alignbit_b32", "v_fma_f32", "v_perm_b32", "v_lshl_add_u32",
-                                    "v_xor_b32_sdwa", "mix4"};
+                                    "v_xor_b32_sdwa", "mix4", "v_pk_add_u16 swap", "v_lshl_or_b32",
+                                    "v_xad_u32", "v_or3_b32"};
 
 template <int OP>
 __device__ __forceinline__ void one(uint32_t &x, uint32_t a, uint32_t b) {
@@ -52,6 +53,12 @@ __device__ __forceinline__ void one(uint32_t &x, uint32_t a, uint32_t b) {
     if constexpr (OP == XORSDWA)
         asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
                      : "+v"(x) : "v"(a));
+    // round 4: rotate-by-16 as a packed 16-bit add with swapped halves (x.hi + 0 | x.lo + 0 << 16),
+    // and three more VOP3 integer forms
+    if constexpr (OP == PKSWAP) asm volatile("v_pk_add_u16 %0, %0, 0 op_sel:[1,0] op_sel_hi:[0,0]" : "+v"(x));
+    if constexpr (OP == LSHLOR) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(x) : "v"(a));
+    if constexpr (OP == XAD) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
+    if constexpr (OP == OR3) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
     // one of each class on the chain in BLAKE3's G order: counted as 4 instructions
     if constexpr (OP == MIX) {
         asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(a));
@@ -222,6 +229,27 @@ __device__ __forceinline__ void g4(uint32_t &a0, uint32_t &b0, uint32_t &c0, uin
     "v_alignbit_b32 %4, %4, %4, 7\n\tv_alignbit_b32 %5, %5, %5, 7\n\t"                                  \
     "v_alignbit_b32 %6, %6, %6, 7\n\tv_alignbit_b32 %7, %7, %7, 7"
 #define G4A(SEP) G4B(SEP, SEP)
+// VAR 13 / 14 (round 4): the rotate by 16 as v_pk_add_u16 with swapped halves
+// (S16 after it: VAR 13 none, VAR 14 "s_nop 0"); nops after the VOP2 groups as VAR 7
+#define G4P(S16)                                                                                      \
+    "v_add3_u32 %0, %0, %4, %16\n\tv_add3_u32 %1, %1, %5, %17\n\tv_add3_u32 %2, %2, %6, %18\n\t"    \
+    "v_add3_u32 %3, %3, %7, %19\n\t"                                                                  \
+    "v_xor_b32 %12, %12, %0\n\tv_xor_b32 %13, %13, %1\n\tv_xor_b32 %14, %14, %2\n\tv_xor_b32 %15, %15, %3\n\ts_nop 0\n\t" \
+    "v_pk_add_u16 %12, %12, 0 op_sel:[1,0] op_sel_hi:[0,0]\n\tv_pk_add_u16 %13, %13, 0 op_sel:[1,0] op_sel_hi:[0,0]\n\t" \
+    "v_pk_add_u16 %14, %14, 0 op_sel:[1,0] op_sel_hi:[0,0]\n\tv_pk_add_u16 %15, %15, 0 op_sel:[1,0] op_sel_hi:[0,0]\n\t" S16 \
+    "v_add_u32 %8, %8, %12\n\tv_add_u32 %9, %9, %13\n\tv_add_u32 %10, %10, %14\n\tv_add_u32 %11, %11, %15\n\ts_nop 0\n\t" \
+    "v_xor_b32 %4, %4, %8\n\tv_xor_b32 %5, %5, %9\n\tv_xor_b32 %6, %6, %10\n\tv_xor_b32 %7, %7, %11\n\ts_nop 0\n\t" \
+    "v_alignbit_b32 %4, %4, %4, 12\n\tv_alignbit_b32 %5, %5, %5, 12\n\t"                                \
+    "v_alignbit_b32 %6, %6, %6, 12\n\tv_alignbit_b32 %7, %7, %7, 12\n\t"                                \
+    "v_add3_u32 %0, %0, %4, %20\n\tv_add3_u32 %1, %1, %5, %21\n\tv_add3_u32 %2, %2, %6, %22\n\t"    \
+    "v_add3_u32 %3, %3, %7, %23\n\t"                                                                  \
+    "v_xor_b32 %12, %12, %0\n\tv_xor_b32 %13, %13, %1\n\tv_xor_b32 %14, %14, %2\n\tv_xor_b32 %15, %15, %3\n\ts_nop 0\n\t" \
+    "v_alignbit_b32 %12, %12, %12, 8\n\tv_alignbit_b32 %13, %13, %13, 8\n\t"                            \
+    "v_alignbit_b32 %14, %14, %14, 8\n\tv_alignbit_b32 %15, %15, %15, 8\n\t"                            \
+    "v_add_u32 %8, %8, %12\n\tv_add_u32 %9, %9, %13\n\tv_add_u32 %10, %10, %14\n\tv_add_u32 %11, %11, %15\n\ts_nop 0\n\t" \
+    "v_xor_b32 %4, %4, %8\n\tv_xor_b32 %5, %5, %9\n\tv_xor_b32 %6, %6, %10\n\tv_xor_b32 %7, %7, %11\n\ts_nop 0\n\t" \
+    "v_alignbit_b32 %4, %4, %4, 7\n\tv_alignbit_b32 %5, %5, %5, 7\n\t"                                  \
+    "v_alignbit_b32 %6, %6, %6, 7\n\tv_alignbit_b32 %7, %7, %7, 7"
 template <int NOPK>
 __device__ __forceinline__ void g4a(uint32_t &a0, uint32_t &b0, uint32_t &c0, uint32_t &d0, uint32_t &a1, uint32_t &b1,
                                     uint32_t &c1, uint32_t &d1, uint32_t &a2, uint32_t &b2, uint32_t &c2, uint32_t &d2,
@@ -231,7 +259,9 @@ __device__ __forceinline__ void g4a(uint32_t &a0, uint32_t &b0, uint32_t &c0, ui
     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3), "+v"(c0), "+v"(c1), \
       "+v"(c2), "+v"(c3), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3)                                      \
     : "v"(x0), "v"(x1), "v"(x2), "v"(x3), "v"(y0), "v"(y1), "v"(y2), "v"(y3)
-    if constexpr (NOPK == 0) asm volatile(G4A("s_nop 0\n\t") G4A_OPS);
+    if constexpr (NOPK == 13) asm volatile(G4P("") G4A_OPS);
+    else if constexpr (NOPK == 14) asm volatile(G4P("s_nop 0\n\t") G4A_OPS);
+    else if constexpr (NOPK == 0) asm volatile(G4A("s_nop 0\n\t") G4A_OPS);
     else if constexpr (NOPK == 1) asm volatile(G4A("s_nop 1\n\t") G4A_OPS);
     else if constexpr (NOPK == 2) asm volatile(G4B("", "s_nop 0\n\t") G4A_OPS);  // after VOP2 groups only
     else if constexpr (NOPK == 3) asm volatile(G4B("s_nop 0\n\t", "") G4A_OPS);  // after VOP3 groups only
@@ -242,7 +272,7 @@ template <int VAR, int R>
 __device__ __forceinline__ void rv(uint32_t (&v)[16], const uint32_t (&m)[16]) {
     using chip::bao::SCHED;
     if constexpr (VAR >= 4) {
-        constexpr int K = VAR == 4 ? 0 : VAR == 5 ? 1 : VAR == 7 ? 2 : VAR == 8 ? 3 : -1;
+        constexpr int K = VAR == 4 ? 0 : VAR == 5 ? 1 : VAR == 7 ? 2 : VAR == 8 ? 3 : VAR >= 13 ? VAR : -1;
         g4a<K>(v[0], v[4], v[8], v[12], v[1], v[5], v[9], v[13], v[2], v[6], v[10], v[14], v[3], v[7], v[11], v[15],
                m[SCHED(R, 0)], m[SCHED(R, 1)], m[SCHED(R, 2)], m[SCHED(R, 3)], m[SCHED(R, 4)], m[SCHED(R, 5)],
                m[SCHED(R, 6)], m[SCHED(R, 7)]);
@@ -545,6 +575,20 @@ int main(int argc, char **argv) {
     }
     }
     std::vector<uint32_t> ref;
+    if (argc > 2 && std::string(argv[2]) == "pk") {  // round 4: rot16 as a packed swap (VAR 13/14 vs 7)
+        probe_op<PKSWAP>(iters);
+        probe_op<ALIGNBIT>(iters);
+        probe_op<LSHLOR>(iters);
+        probe_op<XAD>(iters);
+        probe_op<OR3>(iters);
+        probe_b3v<0>(iters / 64, &ref);
+        probe_b3v<7>(iters / 64, &ref);
+        probe_b3v<13>(iters / 64, &ref);
+        probe_b3v<14>(iters / 64, &ref);
+        probe_b3v<7>(iters / 64, &ref);
+        probe_b3v<13>(iters / 64, &ref);
+        return 0;
+    }
     if (argc > 2 && std::string(argv[2]) == "b3x2") {  // two states per lane (VAR 10-12)
         probe_b3v<0>(iters / 64, &ref);
         probe_b3v<7>(iters / 64, &ref);
