@@ -32,6 +32,7 @@
 
 #include "chip_internal.hpp"
 #include "gf256.hpp"
+#include "hbm_alloc.hpp"
 #include "host_stages.hpp"
 
 namespace chip {
@@ -2585,6 +2586,11 @@ struct chip_bao_hasher {
     hipStream_t hstream = nullptr;  // update()'s chunk hashing, behind the copies through `copied`
     hipEvent_t copied = nullptr;
     DevBuf content, enc, scratch, hash, cv0, cv1;
+    // content and cv0 grow in place behind a reserved VA range (no copy, no
+    // device sync per growth); va_* says which of them live there
+    chip::hbm::Growable gcontent, gcv0;
+    bool va_content = false, va_cv0 = false;
+    uint64_t va_content_bytes = 0;  // content VA reserved (16 GiB; CHIP_HASHER_VA_MIB at creation, tests)
     uint64_t len = 0, enc_len = 0;
     uint64_t units = 0;  // 64-chunk units whose chunk CVs are in cv0
     bool finalized = false;
@@ -2601,6 +2607,61 @@ uint64_t hasher_batch_units() {
         return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)512;
     }();
     return u;
+}
+
+// CHIP_HASHER_VA=0: the hasher grows by copying (grow_keep), as before round 4 (A/B)
+bool hasher_va_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_HASHER_VA");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    return on;
+}
+
+hipError_t grow_keep(DevBuf &b, size_t need, size_t used, hipStream_t s);
+
+// VA reserved per hasher: 16 GiB of content in place (its chunk CVs: 1/32)
+constexpr uint64_t HASHER_VA_CONTENT = 16ull << 30, HASHER_VA_CV = 1ull << 30;
+uint64_t hasher_va_content() {
+    const char *e = std::getenv("CHIP_HASHER_VA_MIB");
+    const uint64_t mib = e ? std::strtoull(e, nullptr, 10) : 0;
+    return mib ? mib << 20 : HASHER_VA_CONTENT;
+}
+
+// Grow a hasher buffer to `need` bytes keeping its first `used`: in place
+// behind its reserved VA range (hbm::Growable) when it lives there, else by
+// copying into a larger allocation after `wait_s` (whose kernels read the old
+// buffer) is idle.  A buffer that outgrows its VA range moves to a plain
+// allocation once.
+hipError_t hasher_grow(DevBuf &b, chip::hbm::Growable &g, bool &in_va, size_t need, size_t used, hipStream_t copy_s,
+                       hipStream_t wait_s, uint64_t reserve) {
+    if (b.cap >= need) return hipSuccess;
+    if ((in_va || !b.p) && hasher_va_on()) {
+        hipError_t e = g.grow(need, reserve);
+        if (e == hipSuccess) {
+            b.p = g.va;
+            b.cap = g.mapped;
+            in_va = true;
+            return hipSuccess;
+        }
+        (void)hipGetLastError();
+    }
+    hipError_t e = hipStreamSynchronize(wait_s);
+    if (e != hipSuccess) return e;
+    if (!in_va) return grow_keep(b, need, used, copy_s);
+    DevBuf nb;  // out of the VA range: one copy into plain memory
+    if ((e = grow_keep(nb, std::max(need, 2 * (size_t)g.mapped), 0, copy_s)) != hipSuccess) return e;
+    if (used && (e = hipMemcpyAsync(nb.p, b.p, used, hipMemcpyDeviceToDevice, copy_s)) == hipSuccess)
+        e = hipStreamSynchronize(copy_s);
+    if (e != hipSuccess) {
+        (void)hipFree(nb.p);
+        return e;
+    }
+    g.release();
+    in_va = false;
+    b = nb;
+    nb.p = nullptr;
+    return hipSuccess;
 }
 
 // grow keeping the first `used` bytes (geometric, so appends are amortised O(1))
@@ -2635,6 +2696,7 @@ int chip_bao_hasher_new(chip_bao_hasher **out) {
     int st = ctx_get(&c);  // device check + hipSetDevice
     if (st != CHIP_OK) return st;
     auto *h = new chip_bao_hasher();
+    h->va_content_bytes = hasher_va_content();
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->hstream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->copied, hipEventDisableTiming);
@@ -2658,8 +2720,8 @@ int chip_bao_hasher_update(chip_bao_hasher *h, const uint8_t *buf, uint64_t n) {
     Ctx *c;
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    if (h->content.cap < h->len + n) CHIP_HIP(hipStreamSynchronize(h->hstream));  // hashing reads the old buffer
-    CHIP_HIP(grow_keep(h->content, h->len + n, h->len, h->stream));
+    CHIP_HIP(hasher_grow(h->content, h->gcontent, h->va_content, h->len + n, h->len, h->stream, h->hstream,
+                         h->va_content_bytes));
     // the caller may reuse buf on return: a staged copy is done with it already, a direct one
     // (pinned buf) is waited for on every return path below, the error paths included
     struct SyncDirect {
@@ -2678,10 +2740,8 @@ int chip_bao_hasher_update(chip_bao_hasher *h, const uint8_t *buf, uint64_t n) {
     // append cost the appends 14 % (profiles/r6t); finalize hashes what is left.
     const uint64_t ready = (h->len - 1) / 65536;
     if (hasher_batch_units() && ready >= h->units + hasher_batch_units()) {
-        if (h->cv0.cap < ready * 64 * 32) {
-            CHIP_HIP(hipStreamSynchronize(h->hstream));
-            CHIP_HIP(grow_keep(h->cv0, std::max<uint64_t>(ready * 64 * 32, 1 << 20), h->units * 64 * 32, h->hstream));
-        }
+        CHIP_HIP(hasher_grow(h->cv0, h->gcv0, h->va_cv0, std::max<uint64_t>(ready * 64 * 32, 1 << 20),
+                             h->units * 64 * 32, h->hstream, h->hstream, HASHER_VA_CV));
         CHIP_HIP(hipEventRecord(h->copied, h->stream));
         CHIP_HIP(hipStreamWaitEvent(h->hstream, h->copied, 0));
         CHIP_HIP(hasher_chunks_dev(static_cast<const uint8_t *>(h->content.p), h->len, h->units * 64, ready * 64,
@@ -2704,7 +2764,8 @@ int chip_bao_hasher_finalize(chip_bao_hasher *h, uint8_t hash[CHIP_HASH_LEN]) {
         if (st != CHIP_OK) return st;
         const uint64_t n = h->len;
         h->enc_len = bao_encoded_len(n);
-        CHIP_HIP(grow_keep(h->content, 16, h->len, h->stream));
+        CHIP_HIP(hasher_grow(h->content, h->gcontent, h->va_content, 16, h->len, h->stream, h->hstream,
+                             h->va_content_bytes));
         CHIP_HIP(grow(h->enc, h->enc_len));
         CHIP_HIP(grow(h->hash, 32));
         if (h->units == 0) {  // under 64 KiB + 1 byte in all: the batch path in one go
@@ -2715,7 +2776,8 @@ int chip_bao_hasher_finalize(chip_bao_hasher *h, uint8_t hash[CHIP_HASH_LEN]) {
         } else {  // only the last chunks are hashed here
             const uint64_t N = (n + 1023) / 1024;
             CHIP_HIP(hipStreamSynchronize(h->hstream));  // update()'s chunk CVs are in cv0
-            CHIP_HIP(grow_keep(h->cv0, N * 32, h->units * 64 * 32, h->stream));
+            CHIP_HIP(hasher_grow(h->cv0, h->gcv0, h->va_cv0, N * 32, h->units * 64 * 32, h->stream, h->hstream,
+                                 HASHER_VA_CV));
             CHIP_HIP(grow(h->cv1, (N + 1) / 2 * 32));
             CHIP_HIP(hasher_finish_dev(static_cast<const uint8_t *>(h->content.p), n, h->units * 64,
                                        static_cast<uint8_t *>(h->cv0.p), static_cast<uint8_t *>(h->cv1.p),
@@ -2756,7 +2818,11 @@ void chip_bao_hasher_free(chip_bao_hasher *h) {
         std::lock_guard<std::mutex> lk(h->mu);
         if (h->hstream) (void)hipStreamSynchronize(h->hstream);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
-        for (DevBuf *b : {&h->content, &h->enc, &h->scratch, &h->hash, &h->cv0, &h->cv1})
+        if (h->va_content) h->gcontent.release();
+        else if (h->content.p) (void)hipFree(h->content.p);
+        if (h->va_cv0) h->gcv0.release();
+        else if (h->cv0.p) (void)hipFree(h->cv0.p);
+        for (DevBuf *b : {&h->enc, &h->scratch, &h->hash, &h->cv1})
             if (b->p) (void)hipFree(b->p);
         if (h->hstream) (void)hipStreamDestroy(h->hstream);
         if (h->stream) {

@@ -243,6 +243,13 @@ class Allocator {
         return true;
     }
 
+    // A never-used VA range of `bytes` (GROUP aligned) with nothing mapped:
+    // the home of a Growable buffer.
+    uint8_t *reserve(uint64_t bytes) {
+        std::lock_guard<std::mutex> lk(mu_);
+        return take_va(bytes);
+    }
+
   private:
     std::mutex mu_;
     std::map<uint8_t *, Allocation> live_;
@@ -308,6 +315,73 @@ class Allocator {
         (void)hipEventDestroy(e1);
         (void)hipStreamDestroy(s);
         return reps.empty() ? 1u : (uint32_t)reps.size();
+    }
+};
+
+// A device buffer that grows in place: a large never-used VA range (from the
+// allocator's arena, so never mapped twice) with physical pieces mapped
+// behind it as it grows.  Growing copies nothing and waits for nothing (a
+// hipMalloc + copy + hipFree growth synchronises the device each time); the
+// bytes already written stay where they are, so work in flight over them is
+// undisturbed.  Pieces double (8 MiB ... 1 GiB), so 1 GiB takes 8 maps.
+// `grow` past the reserved range fails: the caller falls back (BaoHasher:
+// one copy into plain memory).
+struct Growable {
+    uint8_t *va = nullptr;
+    uint64_t va_bytes = 0, mapped = 0;
+    std::vector<std::pair<hipMemGenericAllocationHandle_t, uint64_t>> h;  // piece, its size, in VA order
+
+    // `reserve`: the VA range to take on the first call (GROUP multiples)
+    hipError_t grow(uint64_t need, uint64_t reserve = 16 * GROUP) {
+        if (need <= mapped) return hipSuccess;
+        if (!va) {
+            va_bytes = std::max<uint64_t>(reserve, (need + GROUP - 1) / GROUP * GROUP);
+            va = Allocator::get().reserve(va_bytes);
+            if (!va) return hipErrorOutOfMemory;
+        }
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        hipMemAllocationProp prop{};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = dev;
+        hipMemAccessDesc acc{};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        while (mapped < need) {
+            uint64_t sz = std::min<uint64_t>(GROUP, std::max<uint64_t>(PIECE, mapped));
+            while (mapped + sz < need && sz < GROUP) sz *= 2;  // one map for a large append
+            if (mapped + sz > va_bytes) return hipErrorOutOfMemory;
+            hipMemGenericAllocationHandle_t x;
+            if ((e = hipMemCreate(&x, sz, &prop, 0)) != hipSuccess) return e;
+            if ((e = hipMemMap(va + mapped, sz, 0, x, 0)) != hipSuccess) {
+                (void)hipMemRelease(x);
+                return e;
+            }
+            if ((e = hipMemSetAccess(va + mapped, sz, &acc, 1)) != hipSuccess) {
+                (void)hipMemUnmap(va + mapped, sz);
+                (void)hipMemRelease(x);
+                return e;
+            }
+            h.emplace_back(x, sz);
+            mapped += sz;
+        }
+        return hipSuccess;
+    }
+
+    // Unmap and release every piece (the caller has synchronised the work
+    // that used them); the VA range is retired with them.
+    void release() {
+        uint64_t off = 0;
+        for (auto &x : h) {
+            (void)hipMemUnmap(va + off, x.second);
+            (void)hipMemRelease(x.first);
+            off += x.second;
+        }
+        h.clear();
+        va = nullptr;
+        va_bytes = mapped = 0;
     }
 };
 

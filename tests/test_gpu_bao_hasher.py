@@ -141,3 +141,38 @@ def test_hasher_incremental_pinned_appends(gpu):
     enc, oh = O.bao_encode(data)
     assert h.finalize() == oh
     assert h.read_all() == enc
+
+
+def test_hasher_grows_in_place_across_pieces(gpu):
+    """Round 4: the content grows behind a reserved VA range (8 MiB ... 1 GiB
+    physical pieces, no copy, no device sync).  600 MiB in 8 MiB + 13-byte
+    appends crosses several piece boundaries while update()-time hashing of
+    the earlier units is in flight; hash and stream equal the oracle's."""
+    from carbonado_amd.utils import BaoHasher
+    rng = np.random.default_rng(41)
+    data = rng.integers(0, 256, 600 << 20, dtype=np.uint8)
+    h = BaoHasher()
+    step = (8 << 20) + 13
+    for off in range(0, data.size, step):
+        h.update(data[off:off + step])
+    raw = data.tobytes()
+    assert h.finalize() == O.blake3(raw)
+    enc = h.read_all()
+    assert len(enc) == O.lib().orc_bao_encoded_len(len(raw))
+    assert O.blake3(enc) == O.blake3(O.bao_encode(raw)[0])
+
+
+def test_hasher_outgrows_its_va_range(gpu, monkeypatch):
+    """A hasher whose content outgrows its reserved VA range (1 GiB here via
+    CHIP_HASHER_VA_MIB, 16 GiB by default) moves once into plain memory and
+    keeps every byte."""
+    from carbonado_amd.utils import BaoHasher
+    monkeypatch.setenv("CHIP_HASHER_VA_MIB", "1024")
+    rng = np.random.default_rng(43)
+    data = rng.integers(0, 256, (1 << 30) + (200 << 20) + 7, dtype=np.uint8)
+    h = BaoHasher()  # the reserve is read when the hasher is made
+    monkeypatch.delenv("CHIP_HASHER_VA_MIB")
+    step = 64 << 20
+    for off in range(0, data.size, step):
+        h.update(data[off:off + step])
+    assert h.finalize() == O.blake3(data.tobytes())
