@@ -254,7 +254,29 @@ def pmc_kernel_sym(args) -> str | None:
     return None
 
 
-def live_traffic(args, argv: list, timeout_s: float = 240.0) -> dict:
+DIST_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+            "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+            "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE", "TORCH_NCCL_ASYNC_ERROR_HANDLING")
+
+
+def child_env(local_rank: int | None) -> dict:
+    """Environment of a profiled single-GPU child: no torch.distributed
+    variables (it runs alone), and at N > 1 only this rank's GPU visible."""
+    env = {k: v for k, v in os.environ.items() if k not in DIST_ENV}
+    env["TMPDIR"] = "/tmp"
+    if local_rank is not None:
+        picked = False
+        for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+            if env.get(var):
+                ids = [x for x in env[var].split(",") if x.strip()]
+                env[var] = ids[local_rank % len(ids)]
+                picked = True
+        if not picked:
+            env["HIP_VISIBLE_DEVICES"] = str(local_rank)
+    return env
+
+
+def live_traffic(args, argv: list, timeout_s: float = 240.0, local_rank: int | None = None) -> dict:
     """roofline.traffic measured in this run: the same workload in two child
     processes under rocprofv3, one counter pass each (FETCH_SIZE uses 3 TCC
     counters and WRITE_SIZE 2, so they cannot share a pass), then the
@@ -277,9 +299,9 @@ def live_traffic(args, argv: list, timeout_s: float = 240.0) -> dict:
     steps = 2
     child = [sys.executable, str(Path(__file__).resolve())] + list(argv) + [
         "--steps", str(steps), "--warmup", "1", "--live-pmc", "off", "--no-cpu-baseline", "--no-verify",
-        "--no-verify-all", "--no-aliased", "--traffic-json", "none"]
+        "--no-verify-all", "--no-aliased", "--traffic-json", "none", "--gpus", "1"]
     tmp = Path(tempfile.mkdtemp(prefix="chip_pmc_", dir="/tmp"))
-    env = dict(os.environ, TMPDIR="/tmp")
+    env = child_env(local_rank)
     vals, name = {}, None
     t0 = time.perf_counter()
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -1116,9 +1138,14 @@ def main():
     live = None
     under_profiler = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ) or \
         "rocprofiler" in os.environ.get("LD_PRELOAD", "")
-    if (not args.dry_run and world == 1 and not under_profiler and
+    if (not args.dry_run and not under_profiler and
             (args.live_pmc == "on" or (args.live_pmc == "auto" and pmc_kernel_sym(args) is not None))):
-        live = live_traffic(args, sys.argv[1:])  # before this process touches the GPU
+        # before this process touches the GPU; at N > 1 every rank profiles its own GPU in
+        # parallel (a rehearsal with several ranks on one GPU skips it: they would share it)
+        if world == 1:
+            live = live_traffic(args, sys.argv[1:])
+        elif torch.cuda.device_count() >= world:
+            live = live_traffic(args, sys.argv[1:], local_rank=local)
     wl = DryRun(args, rank) if args.dry_run else Workload(args, rank, local, world)
     scatter = None
     if world > 1 and args.dry_run and args.scatter_gib > 0:  # the same collective over gloo, CPU tensors
@@ -1137,6 +1164,10 @@ def main():
     elapsed, launch_ms = wl.time_steps(args.steps, args.warmup, world)
     max_elapsed = max_over_ranks(elapsed)
     rank_avg_ms = gather_floats(sum(launch_ms) / len(launch_ms), world)
+    rank_live = [live]
+    if world > 1:
+        rank_live = [None] * world
+        dist.all_gather_object(rank_live, live)
     rank_alloc = [getattr(wl, "alloc_info", {})]
     if world > 1:  # each rank's buffers' memory classes (placement differs per GPU)
         rank_alloc = [None] * world
@@ -1182,8 +1213,8 @@ def main():
             if live:
                 traffic_src = f"{traffic_src or 'none'} (live PMC failed: {live['error']})"
             elif world > 1 and traffic_src:
-                traffic_src = (f"committed fallback {traffic_src}: the live PMC passes run at N=1 only (one "
-                               "profiled child per GPU would need every rank's GPU twice more)")
+                traffic_src = (f"committed fallback {traffic_src}: no live PMC at this N (ranks sharing a GPU, or "
+                               "the passes are off)")
         if args.mode == "bao":
             workload = f"bao encode, {args.objects} x {args.object_mib:g} MiB objects per GPU"
         elif args.mode == "bao-decode":
@@ -1279,6 +1310,11 @@ def main():
             if pipe and "pmc_kernel" in hbm:
                 res["roofline"]["note_traffic"] = ("traffic: the one dominant kernel's launch (the parent-level "
                                                    "kernels after it move a few % more); alg bytes: the whole step")
+        if world > 1 and any(r and "bytes" in r for r in rank_live):
+            res["roofline"]["per_rank_traffic_ratio"] = [
+                round(r["bytes"] / wl.alg_bytes, 4) if r and "bytes" in r else None for r in rank_live]
+            res["roofline"]["per_rank_traffic_note"] = ("each rank's own rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                                        "passes on its own GPU, before the timed region")
         if world > 1:
             fr = [wl.alg_bytes / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS if res["roofline"]["unit"] == "GB/s" else 1)
                   for ms in rank_avg_ms]

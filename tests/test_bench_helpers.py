@@ -34,6 +34,12 @@ a = sys.argv[1:]
 ctr, d, tag = a[a.index("--pmc") + 1], Path(a[a.index("-d") + 1]), a[a.index("-o") + 1]
 cmd = a[a.index("--") + 1:]
 assert "--live-pmc" in cmd and cmd[cmd.index("--live-pmc") + 1] == "off", cmd
+assert cmd[-2:] == ["--gpus", "1"], cmd  # the child runs alone on one GPU
+import os
+exp = os.environ.get("EXPECT_HIP")
+if exp is not None:  # a rank's child: only its GPU visible, no torch.distributed variables
+    assert os.environ.get("HIP_VISIBLE_DEVICES") == exp, os.environ.get("HIP_VISIBLE_DEVICES")
+    assert "WORLD_SIZE" not in os.environ and "RANK" not in os.environ and "MASTER_PORT" not in os.environ
 d.mkdir(parents=True, exist_ok=True)
 val = {"FETCH_SIZE": [999.0, 100.0, 200.0], "WRITE_SIZE": [5.0, 300.0, 500.0]}[ctr]
 with open(d / f"{tag}_counter_collection.csv", "w") as f:
@@ -60,6 +66,29 @@ def test_live_traffic_two_passes(tmp_path, monkeypatch):
     assert "gf_apply_kernel<4, 1," in r["kernel"]
     # a mode without an HBM-bound kernel gets no passes
     assert "error" in bench.live_traffic(bench.parse(["--mode", "bao"]), [])
+
+
+@pytest.mark.parametrize("visible,expect", [(None, "3"), ("4,5,6,7", "7")])
+def test_live_traffic_per_rank_child(tmp_path, monkeypatch, visible, expect):
+    """N > 1: every rank profiles its own GPU before the timed region; the
+    child sees only that GPU (LOCAL_RANK-th of the visible ones) and none of
+    the torch.distributed variables, and runs with --gpus 1."""
+    import shutil
+    import bench
+    fake = tmp_path / "rocprofv3"
+    fake.write_text(FAKE_ROCPROF)
+    fake.chmod(0o755)
+    monkeypatch.setattr(shutil, "which", lambda name: str(fake))
+    for k, v in {"WORLD_SIZE": "8", "RANK": "3", "LOCAL_RANK": "3", "MASTER_PORT": "29500",
+                 "MASTER_ADDR": "127.0.0.1", "EXPECT_HIP": expect}.items():
+        monkeypatch.setenv(k, v)
+    if visible is None:
+        monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    else:
+        monkeypatch.setenv("HIP_VISIBLE_DEVICES", visible)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    r = bench.live_traffic(bench.parse(["--gpus", "8"]), ["--gpus", "8"], timeout_s=60, local_rank=3)
+    assert r.get("bytes") == (2 * 150 + 400) * 1024, r
 
 
 def test_pcie_roofline_names_the_binding_direction():
