@@ -470,6 +470,13 @@ bool staged(const void *host, size_t n) {
     return m == 2 || !host_pinned(host);
 }
 
+// Copies INTO the pinned ring go through host::ring_copy (non-temporal
+// stores, host_stages.cpp); the other direction is a plain memcpy.
+void copy_bytes(void *dst, const void *src, size_t n, bool nt) {
+    if (nt) host::ring_copy(dst, src, n);
+    else std::memcpy(dst, src, n);
+}
+
 // memcpy between the ring and pageable memory on a few threads: one thread
 // moves ~20 GB/s, the ring DMA 55 GB/s.  A persistent pool (CHIP_COPY_THREADS
 // total, default 8, 1 = the calling thread only; 8 over 4: host scrub() +15 %,
@@ -481,10 +488,11 @@ class CopyPool {
         static CopyPool *p = new CopyPool();  // never destroyed: workers park on the condvar at exit
         return *p;
     }
-    void copy(void *dst, const void *src, size_t n) {
+    // nt: dst is the pinned ring, read next by the DMA engine (copy_bytes)
+    void copy(void *dst, const void *src, size_t n, bool nt = false) {
         // (a forked child has no workers: it copies alone)
         if (workers_ == 0 || n < (size_t(1) << 20) || getpid() != pid_ || !job_.try_lock()) {
-            std::memcpy(dst, src, n);
+            copy_bytes(dst, src, n, nt);
             return;
         }
         const size_t parts = workers_ + 1;
@@ -496,11 +504,12 @@ class CopyPool {
             s_ = static_cast<const uint8_t *>(src);
             n_ = n;
             part_ = part;
+            nt_ = nt;
             pending_ = workers_;
             ++gen_;
         }
         cv_.notify_all();
-        std::memcpy(dst, src, std::min(part, n));
+        copy_bytes(dst, src, std::min(part, n), nt);
         {
             std::unique_lock<std::mutex> lk(mu_);
             done_.wait(lk, [&] { return pending_ == 0; });
@@ -546,14 +555,15 @@ class CopyPool {
             uint8_t *d;
             const uint8_t *s;
             size_t n, part;
+            bool nt;
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&] { return gen_ != seen; });
                 seen = gen_;
-                d = d_, s = s_, n = n_, part = part_;
+                d = d_, s = s_, n = n_, part = part_, nt = nt_;
             }
             const size_t lo = std::min(n, i * part), hi = std::min(n, lo + part);
-            if (hi > lo) std::memcpy(d + lo, s + lo, hi - lo);
+            if (hi > lo) copy_bytes(d + lo, s + lo, hi - lo, nt);
             if (i < MAXW) last_cpu_[i] = sched_getcpu();
             std::lock_guard<std::mutex> lk(mu_);
             if (--pending_ == 0) done_.notify_one();
@@ -572,6 +582,7 @@ class CopyPool {
     uint8_t *d_ = nullptr;
     const uint8_t *s_ = nullptr;
     size_t n_ = 0, part_ = 0;
+    bool nt_ = false;
 };
 
 hipError_t stage_slot(Staging &sg, int k) {  // wait until ring slot k is free
@@ -603,7 +614,7 @@ hipError_t h2d(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s)
         const size_t len = std::min(Staging::PIECE, n - off);
         const int k = sg.next++ % Staging::R;
         if ((e = stage_slot(sg, k)) != hipSuccess) break;
-        CopyPool::get().copy(sg.ring + k * Staging::PIECE, static_cast<const uint8_t *>(src) + off, len);
+        CopyPool::get().copy(sg.ring + k * Staging::PIECE, static_cast<const uint8_t *>(src) + off, len, true);
         e = hipMemcpyAsync(static_cast<uint8_t *>(dst) + off, sg.ring + k * Staging::PIECE, len,
                            hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipEventRecord(sg.ev[k], s);

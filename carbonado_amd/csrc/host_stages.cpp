@@ -728,5 +728,45 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
     return CHIP_OK;
 }
 
+namespace {
+
+bool nt_copy_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_NT_COPY");
+        if (v && v[0] == '0' && v[1] == 0) return false;
+        __builtin_cpu_init();
+        return __builtin_cpu_supports("avx2") != 0;
+    }();
+    return on;
+}
+
+__attribute__((target("avx2"))) void nt_copy_avx2(uint8_t *d, const uint8_t *s, size_t n) {
+    size_t head = (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31;
+    if (head > n) head = n;
+    std::memcpy(d, s, head);
+    size_t i = head;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 64));
+        const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 96), e);
+    }
+    for (; i + 32 <= n; i += 32)
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i)));
+    std::memcpy(d + i, s + i, n - i);
+    _mm_sfence();  // the streaming stores are globally visible before the DMA is enqueued
+}
+
+}  // namespace
+
+void ring_copy(void *dst, const void *src, size_t n) {
+    if (n >= 4096 && nt_copy_on()) nt_copy_avx2(static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), n);
+    else std::memcpy(dst, src, n);
+}
+
 }  // namespace host
 }  // namespace chip

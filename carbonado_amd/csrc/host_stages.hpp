@@ -43,5 +43,11 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
 // Public key (65 B uncompressed) of a 32-byte secret; for tests and tooling.
 int ecies_public_key(const uint8_t *secret, uint8_t out[65]);
 
+// memcpy into pinned staging memory that only the DMA engine reads next:
+// non-temporal (streaming) stores skip the read-for-ownership of every
+// destination line and keep it out of the CPU caches (AVX2; memcpy without
+// it, or with CHIP_NT_COPY=0).
+void ring_copy(void *dst, const void *src, size_t n);
+
 }  // namespace host
 }  // namespace chip

@@ -130,6 +130,16 @@ int main(int argc, char **argv) {
         ++iters;
         const size_t n = rnd(4) == 0 ? rnd(300000) : rnd(5000);
         const Bytes d = rnd(2) ? compressible(n) : [&] { Bytes r(n); for (auto &x : r) x = (uint8_t)rng(); return r; }();
+        // ring_copy (non-temporal stores into the staging ring): every length and both alignments
+        {
+            const size_t so = rnd(64), dof = rnd(64);
+            Bytes src(n + so), dst(n + dof + 64, 0xA5);
+            for (size_t i = 0; i < n; ++i) src[so + i] = d[i];
+            ring_copy(dst.data() + dof, src.data() + so, n);
+            EXPECT(std::memcmp(dst.data() + dof, d.data(), n) == 0, "ring_copy n=%zu", n);
+            for (size_t i = 0; i < dof; ++i) EXPECT(dst[i] == 0xA5, "ring_copy wrote before dst");
+            for (size_t i = dof + n; i < dst.size(); ++i) EXPECT(dst[i] == 0xA5, "ring_copy wrote past dst");
+        }
         // snappy framing
         Bytes frame(snap_max_len(n));
         uint64_t fl = 0;
