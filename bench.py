@@ -1145,7 +1145,7 @@ def main():
         if world == 1:
             live = live_traffic(args, sys.argv[1:])
         elif torch.cuda.device_count() >= world:
-            live = live_traffic(args, sys.argv[1:], local_rank=local)
+            live = live_traffic(args, sys.argv[1:], timeout_s=150.0, local_rank=local)
     wl = DryRun(args, rank) if args.dry_run else Workload(args, rank, local, world)
     scatter = None
     if world > 1 and args.dry_run and args.scatter_gib > 0:  # the same collective over gloo, CPU tensors
