@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy
+#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy prof12 prof15s
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -36,6 +36,8 @@ for s in "$@"; do
     file15) run bench_file15 600 python3 bench.py --mode file --level 15 --steps 3 --warmup 1 --cpu-seconds 8 ;;
     file12) run bench_file12 600 python3 bench.py --mode file --level 12 --steps 3 --warmup 1 --no-cpu-baseline ;;
     prof) bash tools/gpu_prof.sh $TAG ;;
+    prof12) bash tools/gpu_prof.sh $TAG/p12 --mode pipeline --level 12 ;;
+    prof15s) bash tools/gpu_prof.sh $TAG/p15s --mode pipeline --level 12 --object-bytes 16779371 ;;
     encodetorch) run bench_encode_alloc_torch 600 python3 bench.py --alloc torch --no-cpu-baseline --live-pmc off ;;
     mixprobe) run mix_probe_bal 300 ./tools/mix_probe 1024 3 bal ;;
     ftune) run fused_tune 300 ./tools/fused_tune 256 5 ;;
