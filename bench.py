@@ -132,6 +132,9 @@ def parse(argv=None):
                     help="N>1 without --scatter: GiB per rank that rank 0 scatters over RCCL/xGMI once, timed and "
                          "reported as `scatter` (the inputs themselves are generated on each rank); 0 = none")
     ap.add_argument("--dry-run", action="store_true", help="no device: exercise the multi-rank control plane")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="leave the process's CPUs and memory policy alone (default: once the GPU is known, the "
+                         "main thread runs on the GPU's NUMA node and allocates host memory there)")
     ap.add_argument("--traffic-json", default="auto",
                     help="PMC summary (profiles/*_pmc.json, tools/pmc_summary.py) with the measured HBM "
                          "bytes per launch of this kernel; 'auto' = newest matching file, 'none' = null; used "
@@ -456,6 +459,37 @@ def pcie_roofline(h2d_bytes: int, d2h_bytes: int, step_s: float, duplex_achieved
                      "over the whole step's wall time")}
 
 
+def bind_to_gpu_node() -> dict:
+    """A NUMA-aware host for one GPU: the calling (main) thread moves to the
+    CPUs of the GPU's NUMA node and prefers that node for the memory it
+    touches first, so the host buffers the workload makes next sit next to
+    the GPU's PCIe root (the library already keeps its staging ring and copy
+    threads there).  The GPU box is two sockets; without this the process
+    lands on either (BaoHasher)."""
+    import ctypes
+    from carbonado_amd.device import host_topology
+    t = host_topology()
+    node, pci = t.get("gpu_node", -1), t.get("gpu_pci", "")
+    if node is None or node < 0 or not pci:
+        return {"bound": False, "why": "GPU NUMA node unknown"}
+    try:
+        cpus = set()
+        for part in Path(f"/sys/bus/pci/devices/{pci}/local_cpulist").read_text().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+    except (OSError, ValueError) as e:
+        return {"bound": False, "why": f"local_cpulist: {e}"}
+    cpus &= os.sched_getaffinity(0)
+    if not cpus:
+        return {"bound": False, "why": "none of the GPU's CPUs are allowed"}
+    os.sched_setaffinity(0, cpus)
+    libc = ctypes.CDLL(None, use_errno=True)
+    mask = ctypes.c_ulong(1 << node)
+    MPOL_PREFERRED, SYS_set_mempolicy = 1, 238  # x86_64
+    pol = libc.syscall(SYS_set_mempolicy, MPOL_PREFERRED, ctypes.byref(mask), 64 + 1) == 0
+    return {"bound": True, "gpu_node": node, "cpus": len(cpus), "mempolicy_preferred": pol}
+
+
 def scrub_corrupt_offset(n: int, o: int) -> int:
     """Stream offset of a content byte inside data shard o % 4 of a level-12
     encoding of n bytes (one byte per object is flipped for --mode scrub):
@@ -498,6 +532,8 @@ class Workload:
         torch.cuda.set_device(dev)
         if L.chip_init(dev.index) != 0:
             raise SystemExit(f"libcarbonado_hip: no usable gfx950 device: {L.chip_last_device_error().decode()}")
+        # before any host buffer of the workload exists
+        self.host_binding = {"bound": False, "why": "--no-numa-bind"} if args.no_numa_bind else bind_to_gpu_node()
         self.k, self.m = k, m = args.k, args.m
         self.n = n = int(args.object_mib * (1 << 20))
         self.count = count = args.objects
@@ -1349,6 +1385,8 @@ def main():
                          "(all 8 shards written, 48 MiB per object) is the graded figure")}
         if scatter is not None:
             res["scatter"] = scatter
+        if not args.dry_run:
+            res["host_binding"] = getattr(wl, "host_binding", None)
         if args.mode == "hasher" and not args.dry_run:
             from carbonado_amd import device as _dev
             try:
