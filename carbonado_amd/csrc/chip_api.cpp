@@ -2602,6 +2602,7 @@ struct chip_bao_hasher {
     chip::hbm::Growable gcontent, gcv0;
     bool va_content = false, va_cv0 = false;
     uint64_t va_content_bytes = 0;  // content VA reserved (16 GiB; CHIP_HASHER_VA_MIB at creation, tests)
+    int dev = -1;                   // device its streams and buffers live on
     uint64_t len = 0, enc_len = 0;
     uint64_t units = 0;  // 64-chunk units whose chunk CVs are in cv0
     bool finalized = false;
@@ -2618,6 +2619,22 @@ uint64_t hasher_batch_units() {
         return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)512;
     }();
     return u;
+}
+
+// One freed hasher is kept, emptied, with its two streams, its event and its
+// grown buffers, and handed to the next chip_bao_hasher_new on the same
+// device: stream creation and destruction, a GiB of hipMalloc / hipFree and
+// the in-place buffers' mappings cost milliseconds per hasher otherwise (a
+// mapped VA range is reused as is, never remapped).  CHIP_HASHER_CACHE=0: off.
+std::mutex g_hasher_spare_mu;
+chip_bao_hasher *g_hasher_spare = nullptr;
+
+bool hasher_cache_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_HASHER_CACHE");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    return on;
 }
 
 // CHIP_HASHER_VA=0: the hasher grows by copying (grow_keep), as before round 4 (A/B)
@@ -2706,8 +2723,18 @@ int chip_bao_hasher_new(chip_bao_hasher **out) {
     Ctx *c;
     int st = ctx_get(&c);  // device check + hipSetDevice
     if (st != CHIP_OK) return st;
+    {  // the last freed hasher's streams and grown buffers, if it lived on this device
+        std::lock_guard<std::mutex> lk(g_hasher_spare_mu);
+        if (g_hasher_spare && g_hasher_spare->dev == c->dev &&
+            g_hasher_spare->va_content_bytes == hasher_va_content()) {
+            *out = g_hasher_spare;
+            g_hasher_spare = nullptr;
+            return CHIP_OK;
+        }
+    }
     auto *h = new chip_bao_hasher();
     h->va_content_bytes = hasher_va_content();
+    h->dev = c->dev;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->hstream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->copied, hipEventDisableTiming);
@@ -2829,6 +2856,16 @@ void chip_bao_hasher_free(chip_bao_hasher *h) {
         std::lock_guard<std::mutex> lk(h->mu);
         if (h->hstream) (void)hipStreamSynchronize(h->hstream);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
+        if (hasher_cache_on()) {  // park it, emptied, for the next chip_bao_hasher_new
+            std::lock_guard<std::mutex> sk(g_hasher_spare_mu);
+            if (!g_hasher_spare) {
+                h->len = h->enc_len = h->units = 0;
+                h->finalized = false;
+                std::memset(h->h, 0, sizeof h->h);
+                g_hasher_spare = h;
+                return;
+            }
+        }
         if (h->va_content) h->gcontent.release();
         else if (h->content.p) (void)hipFree(h->content.p);
         if (h->va_cv0) h->gcv0.release();

@@ -176,3 +176,24 @@ def test_hasher_outgrows_its_va_range(gpu, monkeypatch):
     for off in range(0, data.size, step):
         h.update(data[off:off + step])
     assert h.finalize() == O.blake3(data.tobytes())
+
+
+def test_hasher_reuses_a_freed_hashers_resources(gpu):
+    """A freed hasher's streams and grown buffers go to the next one (one
+    spare, CHIP_HASHER_CACHE=0 disables it).  Large, then small, then
+    larger: every hasher starts empty and gives the oracle's hash and
+    stream, whatever the previous one left in the reused buffers."""
+    import gc
+    from carbonado_amd.utils import BaoHasher
+    rng = np.random.default_rng(47)
+    for total in [(40 << 20) + 3, 1500, 0, (70 << 20) + 65537, 65536]:
+        data = rng.integers(0, 256, total, dtype=np.uint8).tobytes()
+        h = BaoHasher()
+        assert len(h) == 0
+        for off in range(0, total, 3 << 20):
+            h.update(data[off:off + (3 << 20)])
+        assert len(h) == total
+        assert h.finalize() == O.blake3(data)
+        assert h.read_all() == O.bao_encode(data)[0]
+        del h
+        gc.collect()
