@@ -851,6 +851,17 @@ class Workload:
             step()
             self.alg_bytes = count * (n + self.final_len)  # PCIe bytes: H2D input + D2H encoding
             self.h2d_bytes, self.d2h_bytes = count * n, count * self.final_len
+            self.copy_back = "whole stream"
+            if lv & 12 == 12 and os.environ.get("CHIP_E2E_SPLIT", "1") != "0":
+                # split copy-back (chip_api.cpp SplitGeo): the host writes each stream's
+                # header and data-shard chunks (zl/2 bytes, zl = the bao header) itself;
+                # the nodes between them and the tail cross PCIe
+                host_made = sum(8 + int.from_bytes(self.h_out[o, :8].numpy().tobytes(), "little") // 2
+                                for o in range(count))
+                self.d2h_bytes = sum(self.olens) - host_made + 32 * count
+                self.alg_bytes = self.h2d_bytes + self.d2h_bytes
+                self.copy_back = (f"split: host writes header + data chunks ({host_made // count} B/object), "
+                                  f"{self.d2h_bytes // count} B/object D2H")
             stages = ("snap + " if lv & 2 else "") + ("ecies + " if lv & 1 else "")
             host = f"host {stages[:-3]} on {args.host_threads} threads + " if stages else ""
             self.kernel = f"encode() level {lv}: {host}H2D + gf_apply + bao kernels + D2H, {slots} slots"
@@ -1387,6 +1398,8 @@ def main():
             res["scatter"] = scatter
         if not args.dry_run:
             res["host_binding"] = getattr(wl, "host_binding", None)
+        if getattr(wl, "copy_back", None):
+            res["copy_back"] = wl.copy_back
         if args.mode == "hasher" and not args.dry_run:
             from carbonado_amd import device as _dev
             try:

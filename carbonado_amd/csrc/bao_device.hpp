@@ -1202,6 +1202,28 @@ static __global__ __launch_bounds__(256) void bao_gather_kernel(const uint8_t *s
     }
 }
 
+// The parent nodes in front of chunks [0, nd) of `count` streams (N chunks,
+// coff = bao_chunk_table(N)), in stream order, to nodes + o * nodes_stride.
+// encode() from host memory at Zfec|Bao: chunks [0, nd) are the data shards,
+// which the host already holds, so only these nodes and the stream's tail
+// cross PCIe (chip_api.cpp SplitGeo).  Lane = 8 B of one run of nodes; the
+// runs sit at 8 mod 64, so 8-B accesses.
+static __global__ __launch_bounds__(256) void bao_data_nodes_kernel(const uint8_t *stream, uint64_t stride,
+                                                                    const uint64_t *coff, uint64_t nd,
+                                                                    uint64_t count, uint8_t *nodes,
+                                                                    uint64_t nodes_stride) {
+    const uint64_t per = nd * 8, total = count * per;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 256) {
+        const uint64_t o = t / per, r = t % per, i = r / 8, q = r % 8;
+        const uint64_t end = coff[i], beg = i ? coff[i - 1] + 1024 : 8;
+        const uint64_t before = (beg - 8 - 1024 * i) / 64;  // data-region nodes ahead of this run
+        const uint8_t *s = stream + o * stride + beg + 8 * q;
+        uint8_t *d = nodes + o * nodes_stride + 64 * before + 8 * q;
+        for (uint64_t b = 0; b < end - beg; b += 64)
+            *reinterpret_cast<uint64_t *>(d + b) = *reinterpret_cast<const uint64_t *>(s + b);
+    }
+}
+
 // Per-node verification flags of `count` streams of content length n:
 // chunk_flags [count][N], parent_flags [count][N-1] (stream order).
 template <int BAO_NTS_UNUSED = 0>

@@ -130,6 +130,25 @@ hipError_t bao_gather_content(const uint8_t *d_stream, uint64_t n, uint64_t c0, 
     return hipGetLastError();
 }
 
+uint64_t bao_data_node_count(uint64_t N, uint64_t nd) {
+    return nd ? (chunk_stream_off(nd - 1, N) + 1024 - 8 - 1024 * nd) / 64 : 0;
+}
+
+hipError_t bao_data_nodes(const uint8_t *d_stream, uint64_t stride, uint64_t N, uint64_t nd, uint64_t count,
+                          uint8_t *d_nodes, uint64_t nodes_stride, hipStream_t stream) {
+    if (!nd || !count) return hipSuccess;
+    if (nd > N || (stride % 8) || (nodes_stride % 8) || nodes_stride < 64 * bao_data_node_count(N, nd))
+        return hipErrorInvalidValue;
+    const uint64_t *coff = nullptr;
+    hipError_t e = bao_chunk_table(N, &coff);
+    if (e != hipSuccess) return e;
+    uint64_t blocks = (count * nd * 8 + 255) / 256;
+    blocks = blocks > 16384 ? 16384 : blocks;
+    hipLaunchKernelGGL(bao_data_nodes_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d_stream, stride, coff,
+                       nd, count, d_nodes, nodes_stride);
+    return hipGetLastError();
+}
+
 hipError_t bao_encode_inplace_dev(uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count, uint8_t *d_hash,
                                   void *d_scratch, hipStream_t stream) {
     // CPL 8: no content stores here, so the wider lane span costs nothing and

@@ -145,6 +145,13 @@ hipError_t hasher_chunks_dev(const uint8_t *content, uint64_t n, uint64_t c0, ui
                              hipStream_t stream);
 hipError_t hasher_finish_dev(const uint8_t *content, uint64_t n, uint64_t c_done, uint8_t *cv0, uint8_t *cv1,
                              uint8_t *d_out, uint8_t *d_hash, hipStream_t stream);
+// The parent nodes in front of chunks [0, nd) of `count` streams of N chunks
+// (their data region when the content is a zfec output: nd = N/2), in stream
+// order, to d_nodes (nodes_stride >= 64 * bao_data_node_count(N, nd), both
+// strides multiples of 8).
+uint64_t bao_data_node_count(uint64_t N, uint64_t nd);
+hipError_t bao_data_nodes(const uint8_t *d_stream, uint64_t stride, uint64_t N, uint64_t nd, uint64_t count,
+                          uint8_t *d_nodes, uint64_t nodes_stride, hipStream_t stream);
 // Stream layout (host side, same formulas as the kernels).
 uint64_t bao_chunk_offset(uint64_t i, uint64_t N);
 uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N);

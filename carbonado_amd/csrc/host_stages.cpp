@@ -768,5 +768,41 @@ void ring_copy(void *dst, const void *src, size_t n) {
     else std::memcpy(dst, src, n);
 }
 
+// one 1024-B chunk into its stream slot (8 mod 64): the whole lines with
+// streaming stores, the two partial ones (shared with parent nodes / the
+// device-copied tail) with plain stores; the caller fences once
+__attribute__((target("avx2"))) static void chunk_nt(uint8_t *d, const uint8_t *s) {
+    const size_t head = (64 - (reinterpret_cast<uintptr_t>(d) & 63)) & 63;
+    std::memcpy(d, s, head);
+    size_t i = head;
+    for (; i + 64 <= 1024; i += 64) {
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i)));
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 32),
+                            _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 32)));
+    }
+    std::memcpy(d + i, s + i, 1024 - i);
+}
+
+__attribute__((target("avx2"))) static void fence_nt() { _mm_sfence(); }
+
+void fill_data_chunks(uint8_t *out, const uint64_t *coff, uint64_t nd, uint64_t zl, const uint8_t *src, uint64_t n) {
+    for (int b = 0; b < 8; ++b) out[b] = static_cast<uint8_t>(zl >> (8 * b));  // bao header: u64 LE length
+    const bool nt = nt_copy_on();
+    alignas(64) uint8_t pad[1024];
+    for (uint64_t i = 0; i < nd; ++i) {
+        const uint64_t off = 1024 * i;
+        const uint8_t *s = src + (off < n ? off : 0);
+        if (off + 1024 > n) {  // the zfec padding: zeros past the input
+            const uint64_t v = off < n ? n - off : 0;
+            if (v) std::memcpy(pad, s, v);
+            std::memset(pad + v, 0, 1024 - v);
+            s = pad;
+        }
+        if (nt) chunk_nt(out + coff[i], s);
+        else std::memcpy(out + coff[i], s, 1024);
+    }
+    if (nt) fence_nt();
+}
+
 }  // namespace host
 }  // namespace chip

@@ -48,6 +48,11 @@ int ecies_public_key(const uint8_t *secret, uint8_t out[65]);
 // destination line and keep it out of the CPU caches (AVX2; memcpy without
 // it, or with CHIP_NT_COPY=0).
 void ring_copy(void *dst, const void *src, size_t n);
+// The host-made part of a Zfec|Bao stream (encode() from host memory): its
+// header (u64 LE zl) and data chunk i = src[1024 i, 1024 i + 1024), zero past
+// n, at out + coff[i] for i < nd (the data shards of the zfec output are the
+// zero-padded input itself).  Streaming stores for the whole lines.
+void fill_data_chunks(uint8_t *out, const uint64_t *coff, uint64_t nd, uint64_t zl, const uint8_t *src, uint64_t n);
 
 }  // namespace host
 }  // namespace chip

@@ -135,6 +135,37 @@ def test_encode_host_batch_ragged_host_stage_sizes(gpu):
             assert out[o, :olen[o]].numpy().tobytes() == enc and hashes[o].numpy().tobytes() == h, (level, o)
 
 
+@pytest.mark.parametrize("n", [1, 1000, 4096, 70_001, (1 << 20) + 5, 3 << 20])
+@pytest.mark.parametrize("level", [12, 13, 15])
+def test_encode_host_batch_split_copy_back(gpu, level, n):
+    """Zfec|Bao from host memory: the host writes each stream's header and
+    data-shard chunks itself, the device gathers the parent nodes between them
+    and the tail crosses PCIe (chip_api.cpp SplitGeo).  Output pre-filled with
+    0xA5 so a byte nobody wrote shows; nine objects over two slots of two
+    objects each, so slots are reused and nodes scattered while the next slice
+    stages; count 1 separately (pitch = the stream length)."""
+    import torch
+    from carbonado_amd import device
+    count = 9
+    rng = np.random.default_rng(n + level)
+    inp = torch.from_numpy(rng.integers(0, 256, (count, n + 3), dtype=np.uint8)).pin_memory()
+    cap = device._lib.lib().chip_encode_max_len(n)
+    eph = np.stack([np.frombuffer(H.sha256(b"s%d" % o), np.uint8) for o in range(count)])
+    nonce = np.stack([np.frombuffer(H.sha256(b"t%d" % o)[:16], np.uint8) for o in range(count)])
+    for cnt in (count, 1):
+        out = torch.full((cnt, cap + 8), 0xA5, dtype=torch.uint8).pin_memory()
+        hashes = torch.zeros((cnt, 32), dtype=torch.uint8).pin_memory()
+        olen, _ = device.encode_host_batch(level, inp[:cnt], n, out, hashes, nslots=2, slice_bytes=2 * n + 2,
+                                           pubkey=PUB, ephemeral_sk=eph[:cnt], nonce=nonce[:cnt], host_threads=3)
+        for o in range(cnt):
+            enc, h, _ = O.encode_full(inp[o, :n].numpy().tobytes(), level, PUB, eph[o].tobytes(),
+                                      nonce[o].tobytes())
+            assert olen[o] == len(enc)
+            assert out[o, :olen[o]].numpy().tobytes() == enc, (cnt, o)
+            assert hashes[o].numpy().tobytes() == h
+            assert (out[o, olen[o]:].numpy() == 0xA5).all()  # nothing past the stream
+
+
 @pytest.mark.parametrize("name", SAMPLES)
 @pytest.mark.parametrize("level", [1, 2, 3, 14, 15])
 def test_codec_samples_host_levels(gpu, golden, golden_dir, name, level):
