@@ -958,6 +958,16 @@ struct Scratch {
     }
 };
 
+// CHIP_STREAM_ENCRYPT=0: snap_compress into a full-size scratch, then
+// ecies_encrypt (the two-pass form, for A/B runs)
+bool stream_encrypt_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_STREAM_ENCRYPT");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    return on;
+}
+
 // bound of the host stages' output for an n-byte input
 uint64_t host_stage_max(uint8_t format, uint64_t n) {
     uint64_t m = (format & CHIP_FORMAT_SNAPPY) ? host::snap_max_len(n) : n;
@@ -969,11 +979,23 @@ uint64_t host_stage_max(uint8_t format, uint64_t n) {
 // the snap output when both stages run.
 int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const uint8_t *eph, const uint8_t *nonce,
                      const uint8_t *in, uint64_t n, uint8_t *dst, uint64_t cap, Scratch &tmp,
-                     uint64_t *len, uint64_t *bc, uint64_t *be) {
+                     uint64_t *len, uint64_t *bc, uint64_t *be, const host::ChunkSink *sink = nullptr,
+                     uint64_t *filled = nullptr) {
     const bool snap = format & CHIP_FORMAT_SNAPPY, ecies = format & CHIP_FORMAT_ECIES;
     const uint8_t *cur = in;
     uint64_t cur_n = n;
     *bc = *be = 0;
+    if (filled) *filled = 0;
+    if (ecies && pk && stream_encrypt_on()) {
+        // one pass: snappy block -> window -> AES-GCM -> dst (-> stream slots)
+        int st = host::ecies_encrypt_stream(pk, pklen, eph, nonce, in, n, snap, dst, cap, &cur_n,
+                                            tmp.get(host::SNAP_ECIES_WINDOW), sink, filled);
+        if (st != CHIP_OK) return st;
+        *be = cur_n;
+        if (snap) *bc = cur_n - host::ECIES_OVERHEAD;
+        *len = cur_n;
+        return CHIP_OK;
+    }
     if (snap) {
         uint8_t *sd = dst;
         uint64_t scap = cap;
@@ -2242,6 +2264,10 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             // data region of its streams (split copy-back)
             uint8_t *stage = hs ? (sl ? static_cast<uint8_t *>(sl->stage.p) : stage_host.data()) : nullptr;
             const uint32_t nt = (uint32_t)std::min<uint64_t>(T, std::max(cnt, pp.g ? pp.cnt : 0));
+            // the geometry an incompressible object's stream will have: ECIES places
+            // its chunks block by block against it (host::ChunkSink)
+            const uint64_t n_pred = split_fmt && hs ? split_chunks(h_max) : 0;
+            const SplitGeo *g_pred = n_pred >= 2 ? &geos.get(n_pred) : nullptr;
             auto work = [&](uint32_t t) {
                 Scratch &tmp = scratch[t];
                 if (pp.g)
@@ -2249,22 +2275,34 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                 for (uint64_t j = t; j < cnt; j += nt) {
                     const uint64_t o = o0 + j;
                     const uint8_t *obj = in + o * in_stride;
-                    uint64_t olen = n;
+                    uint64_t olen = n, filled = 0;
+                    uint8_t *row = out + o * out_stride;
                     if (hs) {
+                        const host::ChunkSink sink{row, g_pred ? g_pred->coff.data() : nullptr,
+                                                   g_pred ? g_pred->nd : 0};
                         sts[j] = host_stages_into(format, pubkey, pubkey_len,
                                                   inject && inject->ephemeral_sk ? inject->ephemeral_sk + 32 * o
                                                                                  : nullptr,
                                                   inject && inject->nonce ? inject->nonce + 16 * o : nullptr, obj, n,
-                                                  stage + j * h_al, h_al, tmp, &len[j], &bc[j], &be[j]);
+                                                  stage + j * h_al, h_al, tmp, &len[j], &bc[j], &be[j],
+                                                  g_pred ? &sink : nullptr, &filled);
                         if (sts[j] != CHIP_OK) continue;
                         obj = stage + j * h_al;
                         olen = len[j];
                     }
-                    if (split_fmt) {  // a ragged slice copies its streams back whole over this
+                    // the stream's header and data chunks (a ragged slice copies its
+                    // streams back whole over this; chunks placed against a wrong
+                    // prediction lie inside the stream and are overwritten too)
+                    if (split_fmt) {
                         const uint64_t N = split_chunks(olen);
                         if (N >= 2) {
                             const SplitGeo &g = geos.get(N);
-                            host::fill_data_chunks(out + o * out_stride, g.coff.data(), g.nd, 1024 * N, obj, olen);
+                            if (filled > 1 && N == n_pred) {  // chunks [1, filled) are in place
+                                host::fill_data_chunks(row, g.coff.data(), 1, 1024 * N, obj, olen);
+                                host::fill_chunk_range(row, g.coff.data(), filled, g.nd, obj, olen);
+                            } else {
+                                host::fill_data_chunks(row, g.coff.data(), g.nd, 1024 * N, obj, olen);
+                            }
                         }
                     }
                 }

@@ -283,6 +283,24 @@ uint64_t snap_max_len(uint64_t n) {
     return sizeof(STREAM_ID) + 8 * ((n + MAX_BLOCK - 1) / MAX_BLOCK) + n;
 }
 
+// One chunk of the frame stream for len (<= MAX_BLOCK) input bytes: its 8-B
+// header into hdr, its body (compressed into tmp, or the input itself when
+// compression saves less than 1/8: FrameEncoder's rule) at *body.
+static size_t snap_block(const uint8_t *src, size_t len, uint8_t hdr[8], uint8_t *tmp, const uint8_t **body) {
+    const uint32_t crc = crc_masked(src, len);
+    const size_t clen = compress_raw(tmp, src, len);
+    const bool raw = clen >= len - len / 8;
+    const size_t blen = raw ? len : clen;
+    const uint32_t chunk_len = (uint32_t)(4 + blen);
+    hdr[0] = raw ? 0x01 : 0x00;
+    hdr[1] = (uint8_t)chunk_len;
+    hdr[2] = (uint8_t)(chunk_len >> 8);
+    hdr[3] = (uint8_t)(chunk_len >> 16);
+    std::memcpy(hdr + 4, &crc, 4);
+    *body = raw ? src : tmp;
+    return blen;
+}
+
 int snap_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
     // FrameEncoder writes nothing at all for an empty input (no stream id).
     if (n == 0) {
@@ -296,19 +314,10 @@ int snap_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uin
     d += sizeof(STREAM_ID);
     for (uint64_t o = 0; o < n; o += MAX_BLOCK) {
         const size_t len = (size_t)((n - o) < MAX_BLOCK ? (n - o) : MAX_BLOCK);
-        const uint8_t *src = in + o;
-        const uint32_t crc = crc_masked(src, len);
-        const size_t clen = compress_raw(tmp.data(), src, len);
-        const bool raw = clen >= len - len / 8;
-        const size_t body = raw ? len : clen;
-        const uint32_t chunk_len = (uint32_t)(4 + body);
-        out[d] = raw ? 0x01 : 0x00;
-        out[d + 1] = (uint8_t)chunk_len;
-        out[d + 2] = (uint8_t)(chunk_len >> 8);
-        out[d + 3] = (uint8_t)(chunk_len >> 16);
-        std::memcpy(out + d + 4, &crc, 4);
-        std::memcpy(out + d + 8, raw ? src : tmp.data(), body);
-        d += 8 + body;
+        const uint8_t *body;
+        const size_t blen = snap_block(in + o, len, out + d, tmp.data(), &body);
+        std::memcpy(out + d + 8, body, blen);
+        d += 8 + blen;
     }
     *out_len = d;
     return CHIP_OK;
@@ -514,9 +523,11 @@ int ecies_public_key(const uint8_t *secret, uint8_t out[65]) {
     return CHIP_OK;
 }
 
-int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
-                  const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
-    if (cap < n + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
+// ECIES header (ephemeral public key, nonce) into out[0, 81) and the
+// AES-256-GCM context keyed for the ciphertext at out + 97; the tag goes to
+// out[81, 97) when the ciphertext is done.
+static int ecies_begin(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                       uint8_t *out, EVP_CIPHER_CTX *c) {
     PtPtr peer(parse_public(pubkey, pubkey_len));
     if (!peer.p) return CHIP_ERR_ECIES;
     uint8_t sk[32];
@@ -536,20 +547,74 @@ int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph
     uint8_t key[32];
     if (!derive_key(k.p, peer.p, out, key)) return CHIP_ERR_ECIES;
 
-    uint8_t *iv = out + 65, *tag = out + 81, *ct = out + 97;
+    uint8_t *iv = out + 65;
     if (nonce) std::memcpy(iv, nonce, 16);
     else if (RAND_bytes(iv, 16) != 1) return CHIP_ERR_ECIES;
-    CipherCtx cc;
-    bool ok = cc.c && EVP_EncryptInit_ex(cc.c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
-              EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
-              EVP_EncryptInit_ex(cc.c, nullptr, nullptr, key, iv) == 1 && gcm_update(cc.c, true, in, n, ct);
+    const bool ok = c && EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+                    EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
+                    EVP_EncryptInit_ex(c, nullptr, nullptr, key, iv) == 1;
     OPENSSL_cleanse(key, 32);
+    return ok ? CHIP_OK : CHIP_ERR_ECIES;
+}
+
+static int ecies_end(EVP_CIPHER_CTX *c, uint8_t *out, uint64_t ct_len, uint64_t *out_len) {
     int fin = 0;
-    ok = ok && EVP_EncryptFinal_ex(cc.c, ct + n, &fin) == 1 && fin == 0 &&
-         EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_GET_TAG, 16, tag) == 1;
+    const bool ok = EVP_EncryptFinal_ex(c, out + 97 + ct_len, &fin) == 1 && fin == 0 &&
+                    EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, out + 81) == 1;
     if (!ok) return CHIP_ERR_ECIES;
-    *out_len = n + ECIES_OVERHEAD;
+    *out_len = ct_len + ECIES_OVERHEAD;
     return CHIP_OK;
+}
+
+int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                  const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    if (cap < n + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
+    CipherCtx cc;
+    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, out, cc.c);
+    if (st != CHIP_OK) return st;
+    if (!gcm_update(cc.c, true, in, n, out + 97)) return CHIP_ERR_ECIES;
+    return ecies_end(cc.c, out, n, out_len);
+}
+
+int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                         const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                         uint8_t *window, const ChunkSink *sink, uint64_t *filled) {
+    const uint64_t m = snap ? snap_max_len(n) : n;
+    if (cap < m + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (filled) *filled = 0;
+    CipherCtx cc;
+    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, out, cc.c);
+    if (st != CHIP_OK) return st;
+    uint8_t *ct = out + 97;
+    uint64_t off = 0, done = 1;  // ciphertext bytes; chunks [1, done) placed (chunk 0 holds the tag)
+    if (snap && n) {
+        if (!gcm_update(cc.c, true, STREAM_ID, sizeof(STREAM_ID), ct)) return CHIP_ERR_ECIES;
+        off = sizeof(STREAM_ID);
+    }
+    for (uint64_t o = 0; o < n; o += MAX_BLOCK) {
+        const size_t len = (size_t)((n - o) < MAX_BLOCK ? (n - o) : MAX_BLOCK);
+        if (snap) {
+            uint8_t hdr[8];
+            const uint8_t *body;
+            const size_t blen = snap_block(in + o, len, hdr, window, &body);
+            if (!gcm_update(cc.c, true, hdr, 8, ct + off) || !gcm_update(cc.c, true, body, blen, ct + off + 8))
+                return CHIP_ERR_ECIES;
+            off += 8 + blen;
+        } else {
+            if (!gcm_update(cc.c, true, in + o, len, ct + off)) return CHIP_ERR_ECIES;
+            off += len;
+        }
+        if (sink) {  // the chunks this block completed, while they are in cache
+            const uint64_t c1 = std::min<uint64_t>(sink->nd, (97 + off) / 1024);
+            if (c1 > done) {
+                fill_chunk_range(sink->out, sink->coff, done, c1, out, 97 + off);
+                done = c1;
+            }
+        }
+    }
+    st = ecies_end(cc.c, out, off, out_len);
+    if (st == CHIP_OK && filled) *filled = sink ? done : 0;
+    return st;
 }
 
 int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
@@ -787,9 +852,13 @@ __attribute__((target("avx2"))) static void fence_nt() { _mm_sfence(); }
 
 void fill_data_chunks(uint8_t *out, const uint64_t *coff, uint64_t nd, uint64_t zl, const uint8_t *src, uint64_t n) {
     for (int b = 0; b < 8; ++b) out[b] = static_cast<uint8_t>(zl >> (8 * b));  // bao header: u64 LE length
+    fill_chunk_range(out, coff, 0, nd, src, n);
+}
+
+void fill_chunk_range(uint8_t *out, const uint64_t *coff, uint64_t c0, uint64_t c1, const uint8_t *src, uint64_t n) {
     const bool nt = nt_copy_on();
     alignas(64) uint8_t pad[1024];
-    for (uint64_t i = 0; i < nd; ++i) {
+    for (uint64_t i = c0; i < c1; ++i) {
         const uint64_t off = 1024 * i;
         const uint8_t *s = src + (off < n ? off : 0);
         if (off + 1024 > n) {  // the zfec padding: zeros past the input

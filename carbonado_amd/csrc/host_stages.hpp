@@ -53,6 +53,26 @@ void ring_copy(void *dst, const void *src, size_t n);
 // n, at out + coff[i] for i < nd (the data shards of the zfec output are the
 // zero-padded input itself).  Streaming stores for the whole lines.
 void fill_data_chunks(uint8_t *out, const uint64_t *coff, uint64_t nd, uint64_t zl, const uint8_t *src, uint64_t n);
+// chunks [c0, c1) only (no header)
+void fill_chunk_range(uint8_t *out, const uint64_t *coff, uint64_t c0, uint64_t c1, const uint8_t *src, uint64_t n);
+
+// Where the chunks of the stream being made go: out + coff[i], i < nd.
+struct ChunkSink {
+    uint8_t *out;
+    const uint64_t *coff;
+    uint64_t nd;
+};
+// ECIES over snap_compress(in) (snap) or over in, in one pass: each 64 KiB
+// block is framed into `window` (SNAP_ECIES_WINDOW bytes of caller scratch),
+// encrypted into out, and -- with a sink -- the chunks of out it completed are
+// copied to their stream slots while still in cache (chunks [1, *filled);
+// chunk 0 waits for the tag, the last for the length: the caller places the
+// rest once it knows the stream's geometry matches the sink's).  Output
+// identical to snap_compress + ecies_encrypt.
+constexpr uint64_t SNAP_ECIES_WINDOW = 32 + 65536 + 65536 / 6;
+int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                         const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                         uint8_t *window, const ChunkSink *sink, uint64_t *filled);
 
 }  // namespace host
 }  // namespace chip

@@ -161,6 +161,24 @@ def test_ecies_matches_oracle(ca, keyform):
         assert H.ecies_decrypt(sk, e) == d
 
 
+@pytest.mark.parametrize("level", [1, 3])
+def test_one_pass_encrypt_matches_oracle(ca, level):
+    """encode() at Ecies (|Snappy) frames and encrypts block by block through a
+    window (host_stages.cpp ecies_encrypt_stream): the same bytes and
+    EncodeInfo as snap_compress followed by ecies_encrypt, for empty, tiny,
+    compressible, incompressible and multi-block inputs."""
+    sk = H.sha256(b"one pass encrypt")
+    pub = H.public_key(sk)
+    eph, nonce = H.sha256(b"ope"), H.sha256(b"opn")[:16]
+    for d in _inputs() + [bytes(np.random.default_rng(5).integers(0, 256, 65536 * 3, dtype=np.uint8))]:
+        enc, h, info = ca.encode(pub, d, level, ephemeral_sk=eph, nonce=nonce)
+        oenc, oh, oinfo = O.encode_full(d, level, pub, eph, nonce)
+        assert enc == oenc, len(d)
+        assert info.bytes_compressed == oinfo["bytes_compressed"]
+        assert info.bytes_encrypted == oinfo["bytes_encrypted"]
+        assert ca.decode(sk, h, enc, info.padding_len, level) == d
+
+
 def test_ecies_random_envelopes_decrypt(ca):
     """Without injection every call draws a fresh ephemeral key and nonce."""
     sk = H.sha256(b"rng receiver")
