@@ -576,46 +576,6 @@ int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph
     return ecies_end(cc.c, out, n, out_len);
 }
 
-int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
-                         const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
-                         uint8_t *window, const ChunkSink *sink, uint64_t *filled) {
-    const uint64_t m = snap ? snap_max_len(n) : n;
-    if (cap < m + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
-    if (filled) *filled = 0;
-    CipherCtx cc;
-    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, out, cc.c);
-    if (st != CHIP_OK) return st;
-    uint8_t *ct = out + 97;
-    uint64_t off = 0, done = 1;  // ciphertext bytes; chunks [1, done) placed (chunk 0 holds the tag)
-    if (snap && n) {
-        if (!gcm_update(cc.c, true, STREAM_ID, sizeof(STREAM_ID), ct)) return CHIP_ERR_ECIES;
-        off = sizeof(STREAM_ID);
-    }
-    for (uint64_t o = 0; o < n; o += MAX_BLOCK) {
-        const size_t len = (size_t)((n - o) < MAX_BLOCK ? (n - o) : MAX_BLOCK);
-        if (snap) {
-            uint8_t hdr[8];
-            const uint8_t *body;
-            const size_t blen = snap_block(in + o, len, hdr, window, &body);
-            if (!gcm_update(cc.c, true, hdr, 8, ct + off) || !gcm_update(cc.c, true, body, blen, ct + off + 8))
-                return CHIP_ERR_ECIES;
-            off += 8 + blen;
-        } else {
-            if (!gcm_update(cc.c, true, in + o, len, ct + off)) return CHIP_ERR_ECIES;
-            off += len;
-        }
-        if (sink) {  // the chunks this block completed, while they are in cache
-            const uint64_t c1 = std::min<uint64_t>(sink->nd, (97 + off) / 1024);
-            if (c1 > done) {
-                fill_chunk_range(sink->out, sink->coff, done, c1, out, 97 + off);
-                done = c1;
-            }
-        }
-    }
-    st = ecies_end(cc.c, out, off, out_len);
-    if (st == CHIP_OK && filled) *filled = sink ? done : 0;
-    return st;
-}
 
 int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
                   uint64_t cap, uint64_t *out_len) {
@@ -805,7 +765,7 @@ bool nt_copy_on() {
     return on;
 }
 
-__attribute__((target("avx2"))) void nt_copy_avx2(uint8_t *d, const uint8_t *s, size_t n) {
+__attribute__((target("avx2"))) void nt_copy_avx2(uint8_t *d, const uint8_t *s, size_t n, bool fence = true) {
     size_t head = (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31;
     if (head > n) head = n;
     std::memcpy(d, s, head);
@@ -823,7 +783,7 @@ __attribute__((target("avx2"))) void nt_copy_avx2(uint8_t *d, const uint8_t *s, 
     for (; i + 32 <= n; i += 32)
         _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i)));
     std::memcpy(d + i, s + i, n - i);
-    _mm_sfence();  // the streaming stores are globally visible before the DMA is enqueued
+    if (fence) _mm_sfence();  // the streaming stores are globally visible before the DMA is enqueued
 }
 
 }  // namespace
@@ -871,6 +831,100 @@ void fill_chunk_range(uint8_t *out, const uint64_t *coff, uint64_t c0, uint64_t 
         else std::memcpy(out + coff[i], s, 1024);
     }
     if (nt) fence_nt();
+}
+
+bool nt_stage_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_NT_STAGE");
+        return !(v && v[0] == '0' && v[1] == 0) && nt_copy_on();
+    }();
+    return on;
+}
+
+namespace {
+
+// The ECIES output as it is produced, cut into the 1024-B chunks of the
+// Zfec|Bao stream it becomes: whole chunks [1, nd) go to their slots
+// (chunk 0 holds the tag, written last), a chunk split across two blocks is
+// assembled in `part`.  `pos` = output offset of the next byte pushed.
+struct ChunkAssembler {
+    const ChunkSink *sink;
+    bool nt;
+    uint64_t pos = 97;
+    alignas(64) uint8_t part[1024];
+    void slot(uint64_t ci, const uint8_t *src) {
+        if (nt) chunk_nt(sink->out + sink->coff[ci], src);
+        else std::memcpy(sink->out + sink->coff[ci], src, 1024);
+    }
+    void push(const uint8_t *p, size_t len) {
+        while (len) {
+            const uint64_t ci = pos / 1024, at = pos % 1024;
+            const size_t take = (size_t)std::min<uint64_t>(len, 1024 - at);
+            if (ci >= 1 && ci < sink->nd) {
+                if (at == 0 && take == 1024) {
+                    slot(ci, p);
+                } else {
+                    std::memcpy(part + at, p, take);
+                    if (at + take == 1024) slot(ci, part);
+                }
+            }
+            p += take;
+            len -= take;
+            pos += take;
+        }
+    }
+    uint64_t done() const { return std::max<uint64_t>(1, std::min<uint64_t>(sink->nd, pos / 1024)); }
+};
+
+}  // namespace
+
+int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                         const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                         uint8_t *window, const ChunkSink *sink, uint64_t *filled) {
+    const uint64_t m = snap ? snap_max_len(n) : n;
+    if (cap < m + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (filled) *filled = 0;
+    CipherCtx cc;
+    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, out, cc.c);
+    if (st != CHIP_OK) return st;
+    uint8_t *ct = out + 97;
+    uint8_t *piece = window + SNAP_ECIES_WINDOW / 2;  // one block's ciphertext (the sink path)
+    const bool nt = sink && nt_stage_on();
+    ChunkAssembler as{sink, nt_copy_on()};
+    uint64_t off = 0;  // ciphertext bytes so far
+    if (snap && n) {
+        if (!gcm_update(cc.c, true, STREAM_ID, sizeof(STREAM_ID), ct)) return CHIP_ERR_ECIES;
+        if (sink) as.push(ct, sizeof(STREAM_ID));
+        off = sizeof(STREAM_ID);
+    }
+    for (uint64_t o = 0; o < n; o += MAX_BLOCK) {
+        const size_t len = (size_t)((n - o) < MAX_BLOCK ? (n - o) : MAX_BLOCK);
+        // the block's ciphertext: straight into out, or (sink) into the cache-resident
+        // piece buffer, from which it is streamed to out and cut into chunks
+        uint8_t *dst = sink ? piece : ct + off;
+        size_t plen;
+        if (snap) {
+            uint8_t hdr[8];
+            const uint8_t *body;
+            const size_t blen = snap_block(in + o, len, hdr, window, &body);
+            if (!gcm_update(cc.c, true, hdr, 8, dst) || !gcm_update(cc.c, true, body, blen, dst + 8))
+                return CHIP_ERR_ECIES;
+            plen = 8 + blen;
+        } else {
+            if (!gcm_update(cc.c, true, in + o, len, dst)) return CHIP_ERR_ECIES;
+            plen = len;
+        }
+        if (sink) {
+            if (nt) nt_copy_avx2(ct + off, piece, plen, false);
+            else std::memcpy(ct + off, piece, plen);
+            as.push(piece, plen);
+        }
+        off += plen;
+    }
+    if (nt || (sink && as.nt)) fence_nt();
+    st = ecies_end(cc.c, out, off, out_len);
+    if (st == CHIP_OK && filled) *filled = sink ? as.done() : 0;
+    return st;
 }
 
 }  // namespace host

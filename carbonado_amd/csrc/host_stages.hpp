@@ -63,13 +63,16 @@ struct ChunkSink {
     uint64_t nd;
 };
 // ECIES over snap_compress(in) (snap) or over in, in one pass: each 64 KiB
-// block is framed into `window` (SNAP_ECIES_WINDOW bytes of caller scratch),
-// encrypted into out, and -- with a sink -- the chunks of out it completed are
-// copied to their stream slots while still in cache (chunks [1, *filled);
-// chunk 0 waits for the tag, the last for the length: the caller places the
-// rest once it knows the stream's geometry matches the sink's).  Output
-// identical to snap_compress + ecies_encrypt.
-constexpr uint64_t SNAP_ECIES_WINDOW = 32 + 65536 + 65536 / 6;
+// block is framed into `window` (SNAP_ECIES_WINDOW bytes of caller scratch)
+// and encrypted into out.  With a sink (encode() from host memory at
+// Ecies|Zfec|Bao) the block's ciphertext goes to the second half of the
+// window first, is streamed from there into out (non-temporal: out is pinned
+// staging only the DMA reads; CHIP_NT_STAGE=0 plain stores) and cut into the
+// stream's chunks [1, *filled) at their slots; chunk 0 waits for the tag, the
+// last for the length: the caller places the rest once it knows the stream's
+// geometry matches the sink's.  Output identical to snap_compress +
+// ecies_encrypt.
+constexpr uint64_t SNAP_ECIES_WINDOW = 2 * (64 + 65536 + 65536 / 6);
 int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                          const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
                          uint8_t *window, const ChunkSink *sink, uint64_t *filled);

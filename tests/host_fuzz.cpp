@@ -168,6 +168,41 @@ int main(int argc, char **argv) {
                 else if (s2 == 0) EXPECT(l2 == n && same(o2.data(), d.data(), n), "mutated dec+unsnap");
             }
         }
+        // one-pass ECIES (|snappy) with and without a chunk sink: the same bytes as
+        // snap_compress + ecies_encrypt; chunks [1, filled) at their slots, nothing else written
+        {
+            uint8_t eph[32], iv[16];
+            for (auto &x : eph) x = (uint8_t)rng();
+            eph[0] &= 0x7f;
+            eph[31] |= 1;
+            for (auto &x : iv) x = (uint8_t)rng();
+            const bool snap = rnd(2);
+            const Bytes &plain = snap ? frame : d;
+            Bytes ref(plain.size() + ECIES_OVERHEAD);
+            uint64_t rl = 0;
+            EXPECT(ecies_encrypt(pub, 65, eph, iv, plain.data(), plain.size(), ref.data(), ref.size(), &rl) == 0,
+                   "ref enc");
+            const uint64_t cap = (snap ? snap_max_len(n) : n) + ECIES_OVERHEAD;
+            Bytes win(SNAP_ECIES_WINDOW), out(cap);
+            const uint64_t nd = rl / 1024 + rnd(3);
+            std::vector<uint64_t> coff(nd);
+            for (uint64_t i = 0; i < nd; ++i) coff[i] = 8 + 1088 * i + 64 * rnd(2) * (i > 0);
+            Bytes strm(8 + 1088 * (nd + 1), 0xA5);
+            const ChunkSink sink{strm.data(), coff.data(), nd};
+            uint64_t ol = 0, filled = 0;
+            const bool with_sink = rnd(2) && nd;
+            EXPECT(ecies_encrypt_stream(pub, 65, eph, iv, d.data(), n, snap, out.data(), cap, &ol, win.data(),
+                                        with_sink ? &sink : nullptr, &filled) == 0, "stream enc");
+            EXPECT(ol == rl && same(out.data(), ref.data(), rl), "stream enc bytes n=%zu snap=%d", n, (int)snap);
+            if (with_sink) {
+                Bytes want(strm.size(), 0xA5);
+                for (uint64_t i = 1; i < filled; ++i) std::memcpy(want.data() + coff[i], ref.data() + 1024 * i, 1024);
+                EXPECT(filled <= std::max<uint64_t>(1, nd) && 1024 * filled <= rl + 1024, "filled %llu",
+                       (unsigned long long)filled);
+                EXPECT(strm == want, "sink chunks n=%zu snap=%d filled=%llu", n, (int)snap,
+                       (unsigned long long)filled);
+            }
+        }
         // the 160-byte file header
         chip_header h{};
         uint8_t hash[32], meta[8], aux[32], bytes[CHIP_HEADER_LEN];
