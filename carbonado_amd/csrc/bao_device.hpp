@@ -1224,6 +1224,27 @@ static __global__ __launch_bounds__(256) void bao_data_nodes_kernel(const uint8_
     }
 }
 
+// Content bytes [0, nbytes) of `count` streams (chunk i at coff[i] of each
+// row) to contiguous rows: encode() from host memory at Ecies|Zfec|Bao,
+// whose host stage wrote the zfec input straight into the stream's chunk
+// slots.  Lane = 8 B (the slots sit at 8 mod 64).
+static __global__ __launch_bounds__(256) void bao_gather_rows_kernel(const uint8_t *stream, uint64_t stride,
+                                                                     const uint64_t *coff, uint64_t count,
+                                                                     uint64_t nbytes, uint8_t *out,
+                                                                     uint64_t out_stride) {
+    const uint64_t words = (nbytes + 7) / 8, total = count * words;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 256) {
+        const uint64_t o = t / words, b = 8 * (t % words);
+        const uint8_t *s = stream + o * stride + coff[b / 1024] + b % 1024;
+        uint8_t *d = out + o * out_stride + b;
+        if (b + 8 <= nbytes) {
+            *reinterpret_cast<uint64_t *>(d) = *reinterpret_cast<const uint64_t *>(s);
+        } else {
+            for (uint64_t q = 0; b + q < nbytes; ++q) d[q] = s[q];
+        }
+    }
+}
+
 // Per-node verification flags of `count` streams of content length n:
 // chunk_flags [count][N], parent_flags [count][N-1] (stream order).
 template <int BAO_NTS_UNUSED = 0>

@@ -149,6 +149,20 @@ hipError_t bao_data_nodes(const uint8_t *d_stream, uint64_t stride, uint64_t N, 
     return hipGetLastError();
 }
 
+hipError_t bao_gather_rows(const uint8_t *d_stream, uint64_t stride, uint64_t N, uint64_t count, uint64_t nbytes,
+                           uint8_t *d_out, uint64_t out_stride, hipStream_t stream) {
+    if (!count || !nbytes) return hipSuccess;
+    if (nbytes > 1024 * N || (stride % 8) || (out_stride % 8) || out_stride < nbytes) return hipErrorInvalidValue;
+    const uint64_t *coff = nullptr;
+    hipError_t e = bao_chunk_table(N, &coff);
+    if (e != hipSuccess) return e;
+    uint64_t blocks = (count * ((nbytes + 7) / 8) + 255) / 256;
+    blocks = blocks > 16384 ? 16384 : blocks;
+    hipLaunchKernelGGL(bao_gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d_stream, stride, coff,
+                       count, nbytes, d_out, out_stride);
+    return hipGetLastError();
+}
+
 hipError_t bao_encode_inplace_dev(uint8_t *d_stream, uint64_t stride, uint64_t n, uint64_t count, uint8_t *d_hash,
                                   void *d_scratch, hipStream_t stream) {
     // CPL 8: no content stores here, so the wider lane span costs nothing and

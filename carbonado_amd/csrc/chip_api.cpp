@@ -88,7 +88,7 @@ struct DevBuf {
 // (`stage` is pinned host memory holding the host-stage output of a slice)
 struct Slot {
     hipStream_t stream = nullptr;
-    DevBuf in, mid, out, hash, scratch, nodes;
+    DevBuf in, mid, out, hash, scratch, nodes, sin;  // sin: data regions taken from host rows
     DevBuf stage, hnodes;  // pinned
 };
 
@@ -146,7 +146,7 @@ struct Ctx {
         }
         stream = nullptr;
         for (Slot &sl : slots) {
-            for (DevBuf *b : {&sl.in, &sl.mid, &sl.out, &sl.hash, &sl.scratch, &sl.nodes})
+            for (DevBuf *b : {&sl.in, &sl.mid, &sl.out, &sl.hash, &sl.scratch, &sl.nodes, &sl.sin})
                 if (b->p) (void)hipFree(b->p);
             for (DevBuf *b : {&sl.stage, &sl.hnodes})
                 if (b->p) (void)hipHostFree(b->p);
@@ -2065,6 +2065,20 @@ struct SplitGeo {
     }
 };
 
+// CHIP_E2E_DIRECT=0: Ecies objects go through the pinned staging rows
+bool direct_rows_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_E2E_DIRECT");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    return on;
+}
+
+bool is_pinned(const void *p) {
+    unsigned int flags = 0;
+    return p && hipHostGetFlags(&flags, const_cast<void *>(p)) == hipSuccess;
+}
+
 bool e2e_split_on() {
     static const bool on = [] {
         const char *v = std::getenv("CHIP_E2E_SPLIT");
@@ -2113,12 +2127,20 @@ struct SplitPending {
 int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_encode_info &inf,
                        const uint8_t *src, uint64_t src_pitch, uint64_t cur_n, uint64_t zlen, uint64_t final_len,
                        uint64_t cnt, uint8_t *out, uint64_t out_pitch, uint8_t *hashes,
-                       const SplitGeo *split = nullptr) {
+                       const SplitGeo *split = nullptr, bool from_rows = false) {
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
     const uint64_t n_al = (cur_n + 15) / 16 * 16, z_al = (zlen + 15) / 16 * 16, f_al = (final_len + 15) / 16 * 16;
     uint8_t *d_in = static_cast<uint8_t *>(sl.in.p);
-    if (cur_n)
+    if (from_rows && split && cur_n) {
+        // the host stage wrote each object's zfec input into its stream's chunk slots
+        // in out: the data regions come over and the chunks are gathered into rows
+        const uint64_t t_al = (split->t0 + 15) / 16 * 16;
+        uint8_t *d_sin = static_cast<uint8_t *>(sl.sin.p);
+        CHIP_HIP(hipMemcpy2DAsync(d_sin, t_al, out, out_pitch, split->t0, cnt, hipMemcpyHostToDevice, sl.stream));
+        CHIP_HIP(bao_gather_rows(d_sin, t_al, split->N, cnt, cur_n, d_in, n_al, sl.stream));
+    } else if (cur_n) {
         CHIP_HIP(hipMemcpy2DAsync(d_in, n_al, src, src_pitch, cur_n, cnt, hipMemcpyHostToDevice, sl.stream));
+    }
     const uint8_t *d_cur = d_in;
     uint64_t cur_stride = n_al;
     if (zfec && bao && zlen) {  // fused: shards written into the bao streams, hashed in place
@@ -2216,6 +2238,11 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     S = S < 1 ? 1 : (S > count ? count : S);
     // split copy-back (SplitGeo): Zfec|Bao streams of at least 2 chunks
     const bool split_fmt = zfec && bao && c && e2e_split_on() && zlen_max >= 2048;
+    // ...and with ECIES, the host stage writes each stream's data region straight
+    // into out (pinned), which the device then reads: no staging copy at all
+    const bool direct_fmt = split_fmt && hs && (format & CHIP_FORMAT_ECIES) && stream_encrypt_on() &&
+                            direct_rows_on() && is_pinned(out);
+    SplitGeos geos;
     if (c) {
         if (c->slots.size() < nslots) c->slots.resize(nslots);
         for (uint32_t k = 0; k < nslots; ++k) {
@@ -2233,16 +2260,17 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             if (split_fmt) {  // the data region's nodes: fewer than the stream's N chunks
                 CHIP_HIP(grow(sl.nodes, S * 64 * (zlen_max / 1024)));
                 CHIP_HIP(grow_pinned(sl.hnodes, S * 64 * (zlen_max / 1024)));
+                if (direct_fmt) CHIP_HIP(grow(sl.sin, S * ((geos.get(zlen_max / 1024).t0 + 15) / 16 * 16)));
             }
         }
     }
     const std::vector<uint8_t> enc = zfec_enc_matrix(CHIP_FEC_K, CHIP_FEC_M);
-    SplitGeos geos;
     std::vector<SplitPending> pend(nslots);  // per slot: the slice whose nodes are still to be placed
     std::vector<uint8_t> stage_host;  // host stages without a device part
     if (!c) stage_host.resize(S * h_al);
     std::vector<uint64_t> len(S), bc(S), be(S);
     std::vector<int> sts(S);
+    std::vector<uint8_t> in_rows(S);  // object's data region written straight into out (direct)
     std::vector<Scratch> scratch(T);  // per host thread, reused across slices
     auto drain = [&]() {
         if (c)
@@ -2256,7 +2284,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
         const uint8_t *src = in + o0 * in_stride;
         uint64_t src_pitch = count > 1 ? in_stride : n;
         uint64_t cur_n = n;
-        bool uniform = true;
+        bool uniform = true, rows = false;
         SplitPending &pp = pend[i % nslots];  // this slot's previous slice (its stream is done)
         if (hs || split_fmt) {
             // on T threads while earlier slices run on the device: the nodes of this
@@ -2268,6 +2296,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             // its chunks block by block against it (host::ChunkSink)
             const uint64_t n_pred = split_fmt && hs ? split_chunks(h_max) : 0;
             const SplitGeo *g_pred = n_pred >= 2 ? &geos.get(n_pred) : nullptr;
+            const bool direct = direct_fmt && g_pred;
             auto work = [&](uint32_t t) {
                 Scratch &tmp = scratch[t];
                 if (pp.g)
@@ -2277,18 +2306,29 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                     const uint8_t *obj = in + o * in_stride;
                     uint64_t olen = n, filled = 0;
                     uint8_t *row = out + o * out_stride;
+                    in_rows[j] = 0;
                     if (hs) {
                         const host::ChunkSink sink{row, g_pred ? g_pred->coff.data() : nullptr,
-                                                   g_pred ? g_pred->nd : 0};
+                                                   g_pred ? g_pred->nd : 0, direct, 1024 * n_pred};
                         sts[j] = host_stages_into(format, pubkey, pubkey_len,
                                                   inject && inject->ephemeral_sk ? inject->ephemeral_sk + 32 * o
                                                                                  : nullptr,
                                                   inject && inject->nonce ? inject->nonce + 16 * o : nullptr, obj, n,
-                                                  stage + j * h_al, h_al, tmp, &len[j], &bc[j], &be[j],
-                                                  g_pred ? &sink : nullptr, &filled);
+                                                  direct ? nullptr : stage + j * h_al, h_al, tmp, &len[j], &bc[j],
+                                                  &be[j], g_pred ? &sink : nullptr, &filled);
                         if (sts[j] != CHIP_OK) continue;
-                        obj = stage + j * h_al;
                         olen = len[j];
+                        if (direct) {
+                            if (split_chunks(olen) == n_pred) {  // the data region is complete in out
+                                host::fill_chunk_range(row, g_pred->coff.data(), filled, g_pred->nd, nullptr, 0);
+                                in_rows[j] = 1;
+                                continue;
+                            }
+                            // another geometry (compressible input): the output back from the slots
+                            host::gather_chunks(stage + j * h_al, row, g_pred->coff.data(), olen);
+                            filled = 0;
+                        }
+                        obj = stage + j * h_al;
                     }
                     // the stream's header and data chunks (a ragged slice copies its
                     // streams back whole over this; chunks placed against a wrong
@@ -2322,6 +2362,13 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                 src_pitch = h_al;
                 cur_n = len[0];
                 for (uint64_t j = 1; j < cnt; ++j) uniform &= len[j] == cur_n;
+                rows = direct && uniform;
+                for (uint64_t j = 0; j < cnt; ++j) rows &= in_rows[j] != 0;
+                if (direct && !rows)  // a ragged slice: from the staging rows, as without `direct`
+                    for (uint64_t j = 0; j < cnt; ++j)
+                        if (in_rows[j])
+                            host::gather_chunks(stage + j * h_al, out + (o0 + j) * out_stride,
+                                                g_pred->coff.data(), len[j]);
             }
         }
         if (!hs) {
@@ -2354,7 +2401,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             const SplitGeo *g = split_fmt && zl >= 2048 ? &geos.get(zl / 1024) : nullptr;
             const uint64_t opitch = count > 1 ? out_stride : fl;
             st = batch_slice_device(*sl, format, &p2, inf, src, src_pitch, cur_n, zl, fl, cnt, out + o0 * out_stride,
-                                    opitch, hashes + 32 * o0, g);
+                                    opitch, hashes + 32 * o0, g, rows);
             if (st != CHIP_OK) {
                 drain();
                 return st;

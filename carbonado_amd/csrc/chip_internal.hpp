@@ -152,6 +152,10 @@ hipError_t hasher_finish_dev(const uint8_t *content, uint64_t n, uint64_t c_done
 uint64_t bao_data_node_count(uint64_t N, uint64_t nd);
 hipError_t bao_data_nodes(const uint8_t *d_stream, uint64_t stride, uint64_t N, uint64_t nd, uint64_t count,
                           uint8_t *d_nodes, uint64_t nodes_stride, hipStream_t stream);
+// Content bytes [0, nbytes) of `count` streams of N chunks from their chunk
+// slots to contiguous rows (nbytes <= 1024 N; strides multiples of 8).
+hipError_t bao_gather_rows(const uint8_t *d_stream, uint64_t stride, uint64_t N, uint64_t count, uint64_t nbytes,
+                           uint8_t *d_out, uint64_t out_stride, hipStream_t stream);
 // Stream layout (host side, same formulas as the kernels).
 uint64_t bao_chunk_offset(uint64_t i, uint64_t N);
 uint64_t bao_parent_offset(uint64_t s, int level, uint64_t N);

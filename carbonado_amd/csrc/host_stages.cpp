@@ -559,7 +559,8 @@ static int ecies_begin(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t
 
 static int ecies_end(EVP_CIPHER_CTX *c, uint8_t *out, uint64_t ct_len, uint64_t *out_len) {
     int fin = 0;
-    const bool ok = EVP_EncryptFinal_ex(c, out + 97 + ct_len, &fin) == 1 && fin == 0 &&
+    uint8_t none[16];  // GCM's final step emits no bytes
+    const bool ok = EVP_EncryptFinal_ex(c, none, &fin) == 1 && fin == 0 &&
                     EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, out + 81) == 1;
     if (!ok) return CHIP_ERR_ECIES;
     *out_len = ct_len + ECIES_OVERHEAD;
@@ -844,14 +845,16 @@ bool nt_stage_on() {
 namespace {
 
 // The ECIES output as it is produced, cut into the 1024-B chunks of the
-// Zfec|Bao stream it becomes: whole chunks [1, nd) go to their slots
-// (chunk 0 holds the tag, written last), a chunk split across two blocks is
-// assembled in `part`.  `pos` = output offset of the next byte pushed.
+// Zfec|Bao stream it becomes: whole chunks [1, nd) go to their slots, a chunk
+// split across two blocks is assembled in `part`; chunk 0 (which holds the
+// tag) is kept in `first` until finish().  `pos` = output offset of the next
+// byte pushed.
 struct ChunkAssembler {
     const ChunkSink *sink;
     bool nt;
     uint64_t pos = 97;
     alignas(64) uint8_t part[1024];
+    alignas(64) uint8_t first[1024];
     void slot(uint64_t ci, const uint8_t *src) {
         if (nt) chunk_nt(sink->out + sink->coff[ci], src);
         else std::memcpy(sink->out + sink->coff[ci], src, 1024);
@@ -860,7 +863,9 @@ struct ChunkAssembler {
         while (len) {
             const uint64_t ci = pos / 1024, at = pos % 1024;
             const size_t take = (size_t)std::min<uint64_t>(len, 1024 - at);
-            if (ci >= 1 && ci < sink->nd) {
+            if (ci == 0) {
+                std::memcpy(first + at, p, take);
+            } else if (ci < sink->nd) {
                 if (at == 0 && take == 1024) {
                     slot(ci, p);
                 } else {
@@ -874,6 +879,20 @@ struct ChunkAssembler {
         }
     }
     uint64_t done() const { return std::max<uint64_t>(1, std::min<uint64_t>(sink->nd, pos / 1024)); }
+    // the rest of the output's chunks: the stream header, chunk 0 (ECIES
+    // header + the first ciphertext bytes) and the last partial chunk, zero
+    // padded; returns the chunks placed ([0, ceil(pos / 1024)))
+    uint64_t finish(const uint8_t head[97]) {
+        for (int b = 0; b < 8; ++b) sink->out[b] = static_cast<uint8_t>(sink->zl >> (8 * b));
+        std::memcpy(first, head, 97);
+        if (pos < 1024) std::memset(first + pos, 0, 1024 - pos);
+        slot(0, first);
+        if (pos % 1024 && pos > 1024) {
+            std::memset(part + pos % 1024, 0, 1024 - pos % 1024);
+            slot(pos / 1024, part);
+        }
+        return (pos + 1023) / 1024;
+    }
 };
 
 }  // namespace
@@ -882,32 +901,40 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
                          const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
                          uint8_t *window, const ChunkSink *sink, uint64_t *filled) {
     const uint64_t m = snap ? snap_max_len(n) : n;
-    if (cap < m + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (out && cap < m + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (!out && !(sink && sink->complete)) return CHIP_ERR_INVALID_ARG;
+    if (sink && sink->complete && (sink->nd < 1 || 1024 * sink->nd < m + ECIES_OVERHEAD)) return CHIP_ERR_INVALID_ARG;
     if (filled) *filled = 0;
+    uint8_t head[97];
+    uint8_t *hdr = out ? out : head;
     CipherCtx cc;
-    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, out, cc.c);
+    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, hdr, cc.c);
     if (st != CHIP_OK) return st;
-    uint8_t *ct = out + 97;
+    uint8_t *ct = out ? out + 97 : nullptr;
     uint8_t *piece = window + SNAP_ECIES_WINDOW / 2;  // one block's ciphertext (the sink path)
     const bool nt = sink && nt_stage_on();
     ChunkAssembler as{sink, nt_copy_on()};
     uint64_t off = 0;  // ciphertext bytes so far
     if (snap && n) {
-        if (!gcm_update(cc.c, true, STREAM_ID, sizeof(STREAM_ID), ct)) return CHIP_ERR_ECIES;
-        if (sink) as.push(ct, sizeof(STREAM_ID));
+        uint8_t *d = sink ? piece : ct;
+        if (!gcm_update(cc.c, true, STREAM_ID, sizeof(STREAM_ID), d)) return CHIP_ERR_ECIES;
+        if (sink) {
+            if (ct) std::memcpy(ct, piece, sizeof(STREAM_ID));
+            as.push(piece, sizeof(STREAM_ID));
+        }
         off = sizeof(STREAM_ID);
     }
     for (uint64_t o = 0; o < n; o += MAX_BLOCK) {
         const size_t len = (size_t)((n - o) < MAX_BLOCK ? (n - o) : MAX_BLOCK);
         // the block's ciphertext: straight into out, or (sink) into the cache-resident
-        // piece buffer, from which it is streamed to out and cut into chunks
+        // piece buffer, from which it is cut into chunks (and streamed to out, if any)
         uint8_t *dst = sink ? piece : ct + off;
         size_t plen;
         if (snap) {
-            uint8_t hdr[8];
+            uint8_t bh[8];
             const uint8_t *body;
-            const size_t blen = snap_block(in + o, len, hdr, window, &body);
-            if (!gcm_update(cc.c, true, hdr, 8, dst) || !gcm_update(cc.c, true, body, blen, dst + 8))
+            const size_t blen = snap_block(in + o, len, bh, window, &body);
+            if (!gcm_update(cc.c, true, bh, 8, dst) || !gcm_update(cc.c, true, body, blen, dst + 8))
                 return CHIP_ERR_ECIES;
             plen = 8 + blen;
         } else {
@@ -915,16 +942,26 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
             plen = len;
         }
         if (sink) {
-            if (nt) nt_copy_avx2(ct + off, piece, plen, false);
-            else std::memcpy(ct + off, piece, plen);
+            if (ct) {
+                if (nt) nt_copy_avx2(ct + off, piece, plen, false);
+                else std::memcpy(ct + off, piece, plen);
+            }
             as.push(piece, plen);
         }
         off += plen;
     }
+    st = ecies_end(cc.c, hdr, off, out_len);
+    if (st == CHIP_OK && sink) {
+        const uint64_t placed = sink->complete ? as.finish(hdr) : as.done();
+        if (filled) *filled = placed;
+    }
     if (nt || (sink && as.nt)) fence_nt();
-    st = ecies_end(cc.c, out, off, out_len);
-    if (st == CHIP_OK && filled) *filled = sink ? as.done() : 0;
     return st;
+}
+
+void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n) {
+    for (uint64_t i = 0; 1024 * i < n; ++i)
+        std::memcpy(dst + 1024 * i, row + coff[i], (size_t)std::min<uint64_t>(1024, n - 1024 * i));
 }
 
 }  // namespace host

@@ -57,25 +57,34 @@ void fill_data_chunks(uint8_t *out, const uint64_t *coff, uint64_t nd, uint64_t 
 void fill_chunk_range(uint8_t *out, const uint64_t *coff, uint64_t c0, uint64_t c1, const uint8_t *src, uint64_t n);
 
 // Where the chunks of the stream being made go: out + coff[i], i < nd.
+// complete: every chunk the output touches is written (with the stream's
+// header: content length zl), so no contiguous output is needed; the zero
+// chunks after them are the caller's.
 struct ChunkSink {
     uint8_t *out;
     const uint64_t *coff;
     uint64_t nd;
+    bool complete = false;
+    uint64_t zl = 0;
 };
 // ECIES over snap_compress(in) (snap) or over in, in one pass: each 64 KiB
 // block is framed into `window` (SNAP_ECIES_WINDOW bytes of caller scratch)
 // and encrypted into out.  With a sink (encode() from host memory at
 // Ecies|Zfec|Bao) the block's ciphertext goes to the second half of the
-// window first, is streamed from there into out (non-temporal: out is pinned
-// staging only the DMA reads; CHIP_NT_STAGE=0 plain stores) and cut into the
-// stream's chunks [1, *filled) at their slots; chunk 0 waits for the tag, the
-// last for the length: the caller places the rest once it knows the stream's
-// geometry matches the sink's.  Output identical to snap_compress +
-// ecies_encrypt.
+// window first and is cut from there into the stream's chunks at their slots
+// (and streamed into out, if given: non-temporal, out being pinned staging
+// only the DMA reads; CHIP_NT_STAGE=0 plain stores).  Without `complete`,
+// chunks [1, *filled) are placed and the caller places the rest once it knows
+// the stream's geometry matches the sink's; with it, out may be null, the
+// header and chunks [0, *filled) are placed (the last one zero padded) and the
+// caller zeroes [*filled, nd) once the geometry is confirmed.  Output
+// identical to snap_compress + ecies_encrypt.
 constexpr uint64_t SNAP_ECIES_WINDOW = 2 * (64 + 65536 + 65536 / 6);
 int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                          const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
                          uint8_t *window, const ChunkSink *sink, uint64_t *filled);
+// the first n bytes of a stream's content from its chunk slots row + coff[i]
+void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n);
 
 }  // namespace host
 }  // namespace chip

@@ -184,23 +184,40 @@ int main(int argc, char **argv) {
                    "ref enc");
             const uint64_t cap = (snap ? snap_max_len(n) : n) + ECIES_OVERHEAD;
             Bytes win(SNAP_ECIES_WINDOW), out(cap);
-            const uint64_t nd = rl / 1024 + rnd(3);
+            // complete: the sink takes every chunk the output touches (and may be the only output)
+            const bool complete = rnd(2);
+            const uint64_t nd = complete ? (cap + 1023) / 1024 + rnd(3) : rl / 1024 + rnd(3);
             std::vector<uint64_t> coff(nd);
             for (uint64_t i = 0; i < nd; ++i) coff[i] = 8 + 1088 * i + 64 * rnd(2) * (i > 0);
             Bytes strm(8 + 1088 * (nd + 1), 0xA5);
-            const ChunkSink sink{strm.data(), coff.data(), nd};
+            const uint64_t zl = 1024 * rng() % (1ull << 40);
+            const ChunkSink sink{strm.data(), coff.data(), nd, complete, zl};
             uint64_t ol = 0, filled = 0;
             const bool with_sink = rnd(2) && nd;
-            EXPECT(ecies_encrypt_stream(pub, 65, eph, iv, d.data(), n, snap, out.data(), cap, &ol, win.data(),
-                                        with_sink ? &sink : nullptr, &filled) == 0, "stream enc");
-            EXPECT(ol == rl && same(out.data(), ref.data(), rl), "stream enc bytes n=%zu snap=%d", n, (int)snap);
+            const bool no_out = with_sink && complete && rnd(2);
+            EXPECT(ecies_encrypt_stream(pub, 65, eph, iv, d.data(), n, snap, no_out ? nullptr : out.data(), cap, &ol,
+                                        win.data(), with_sink ? &sink : nullptr, &filled) == 0, "stream enc");
+            EXPECT(ol == rl && (no_out || same(out.data(), ref.data(), rl)), "stream enc bytes n=%zu snap=%d", n,
+                   (int)snap);
             if (with_sink) {
                 Bytes want(strm.size(), 0xA5);
-                for (uint64_t i = 1; i < filled; ++i) std::memcpy(want.data() + coff[i], ref.data() + 1024 * i, 1024);
-                EXPECT(filled <= std::max<uint64_t>(1, nd) && 1024 * filled <= rl + 1024, "filled %llu",
+                Bytes padded(ref.begin(), ref.begin() + rl);
+                padded.resize((rl + 1023) / 1024 * 1024, 0);
+                if (complete) {
+                    for (int b = 0; b < 8; ++b) want[b] = (uint8_t)(zl >> (8 * b));
+                    EXPECT(filled == (rl + 1023) / 1024, "complete filled %llu", (unsigned long long)filled);
+                }
+                for (uint64_t i = complete ? 0 : 1; i < filled; ++i)
+                    std::memcpy(want.data() + coff[i], padded.data() + 1024 * i, 1024);
+                EXPECT(filled <= std::max<uint64_t>(1, nd) && 1024 * filled <= rl + 1023, "filled %llu",
                        (unsigned long long)filled);
-                EXPECT(strm == want, "sink chunks n=%zu snap=%d filled=%llu", n, (int)snap,
-                       (unsigned long long)filled);
+                EXPECT(strm == want, "sink chunks n=%zu snap=%d complete=%d filled=%llu", n, (int)snap,
+                       (int)complete, (unsigned long long)filled);
+                if (complete) {  // gather_chunks reads the output back from the slots
+                    Bytes back(rl);
+                    gather_chunks(back.data(), strm.data(), coff.data(), rl);
+                    EXPECT(back == Bytes(ref.begin(), ref.begin() + rl), "gather_chunks");
+                }
             }
         }
         // the 160-byte file header
