@@ -2074,11 +2074,6 @@ bool direct_rows_on() {
     return on;
 }
 
-bool is_pinned(const void *p) {
-    unsigned int flags = 0;
-    return p && hipHostGetFlags(&flags, const_cast<void *>(p)) == hipSuccess;
-}
-
 bool e2e_split_on() {
     static const bool on = [] {
         const char *v = std::getenv("CHIP_E2E_SPLIT");
@@ -2241,7 +2236,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     // ...and with ECIES, the host stage writes each stream's data region straight
     // into out (pinned), which the device then reads: no staging copy at all
     const bool direct_fmt = split_fmt && hs && (format & CHIP_FORMAT_ECIES) && stream_encrypt_on() &&
-                            direct_rows_on() && is_pinned(out);
+                            direct_rows_on() && out && host_pinned(out);
     SplitGeos geos;
     if (c) {
         if (c->slots.size() < nslots) c->slots.resize(nslots);
