@@ -440,6 +440,19 @@ PCIE_SPEC_GBS = 63.0  # PCIe Gen5 x16, per direction (spec)
 PCIE_MEASURED_GBS = {"h2d": 55.6, "d2h": 55.0}
 
 
+def bao_data_region_len(N: int) -> int:
+    """End of the data region of a Zfec|Bao stream of N chunks: the end of chunk
+    N/2 - 1 (bao pre-order: chunk i at 8 + 1024 i + 64 (P(i) + c(i)), c(s) the
+    parents whose leftmost chunk is s; bao_kernels.hip header)."""
+    def ceil_log2(x):
+        return (x - 1).bit_length()
+
+    def c(s):
+        return ceil_log2(N) if s == 0 else min((s & -s).bit_length() - 1, ceil_log2(N - s))
+    last = N // 2 - 1
+    return 8 + 1024 * last + 64 * (sum(c(s) for s in range(last)) + c(last)) + 1024
+
+
 def pcie_roofline(h2d_bytes: int, d2h_bytes: int, step_s: float, duplex_achieved: float) -> dict:
     """Roofline of a host-buffer path (H2D and D2H overlapped): each direction
     priced separately, since the traffic is asymmetric (encode() writes ~2x
@@ -859,9 +872,15 @@ class Workload:
                 host_made = sum(8 + int.from_bytes(self.h_out[o, :8].numpy().tobytes(), "little") // 2
                                 for o in range(count))
                 self.d2h_bytes = sum(self.olens) - host_made + 32 * count
-                self.alg_bytes = self.h2d_bytes + self.d2h_bytes
                 self.copy_back = (f"split: host writes header + data chunks ({host_made // count} B/object), "
                                   f"{self.d2h_bytes // count} B/object D2H")
+                if lv & 1 and os.environ.get("CHIP_E2E_DIRECT", "1") != "0":
+                    # direct: the ECIES output is written into the stream's data region in
+                    # host memory, and that region [0, t0) is what crosses H2D
+                    zls = [int.from_bytes(self.h_out[o, :8].numpy().tobytes(), "little") for o in range(count)]
+                    self.h2d_bytes = sum(bao_data_region_len(z // 1024) for z in zls)
+                    self.copy_back += f"; direct: {self.h2d_bytes // count} B/object H2D (the data region)"
+                self.alg_bytes = self.h2d_bytes + self.d2h_bytes
             stages = ("snap + " if lv & 2 else "") + ("ecies + " if lv & 1 else "")
             host = f"host {stages[:-3]} on {args.host_threads} threads + " if stages else ""
             self.kernel = f"encode() level {lv}: {host}H2D + gf_apply + bao kernels + D2H, {slots} slots"

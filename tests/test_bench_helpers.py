@@ -109,3 +109,15 @@ def test_pcie_roofline_names_the_binding_direction():
     assert r["bound"] == "pcie-h2d" and r["peak_measured"] == 55.6
     # the hasher only uploads
     assert bench.pcie_roofline(1 << 30, 0, 0.05, 0)["bound"] == "pcie-h2d"
+
+
+@pytest.mark.parametrize("N", [2, 8, 10, 16, 34, 40, 64])
+def test_bao_data_region_len_matches_the_oracle_stream(N):
+    """bench.bao_data_region_len(N) = end of chunk N/2 - 1 in the oracle's bao
+    stream of N distinct chunks (the H2D bytes of the direct e2e path)."""
+    content = b"".join(bytes([i % 251 + 1]) * 1024 for i in range(N))
+    enc, _ = O.bao_encode(content)
+    last = N // 2 - 1
+    off = enc.find(bytes([last % 251 + 1]) * 1024)
+    import bench
+    assert off > 0 and bench.bao_data_region_len(N) == off + 1024
