@@ -18,6 +18,7 @@
 #include <cctype>
 #include <condition_variable>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <sstream>
 #include <memory>
@@ -2102,6 +2103,69 @@ uint64_t split_chunks(uint64_t len) {
     return (uint64_t)CHIP_FEC_M * C / 1024;
 }
 
+// A team of host threads for one batch call: run(nt, fn) runs fn(t) for
+// t < nt on the caller and nt - 1 parked workers and returns when all are
+// done.  The workers are made once per call instead of once per slice (a
+// slice's host work is a few ms; 16 thread creations and joins per slice
+// were a visible part of it).
+class Team {
+  public:
+    explicit Team(uint32_t n) : n_(n ? n : 1) {
+        for (uint32_t t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+    }
+    ~Team() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    void run(uint32_t nt, const std::function<void(uint32_t)> &fn) {
+        nt = std::max<uint32_t>(1, std::min(nt, n_));
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            active_ = nt;
+            pending_ = nt - 1;
+            ++gen_;
+        }
+        if (nt > 1) cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void loop(uint32_t t) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(uint32_t)> *fn;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                if (t >= active_) continue;
+                fn = fn_;
+            }
+            (*fn)(t);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    uint32_t n_;
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint32_t)> *fn_ = nullptr;
+    uint32_t active_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 // a slice waiting for its nodes: cnt objects, compact buffers at hnodes + j * nstride
 struct SplitPending {
     const SplitGeo *g = nullptr;
@@ -2230,7 +2294,11 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     T = std::min<uint32_t>(T, 64);
     const uint64_t h_al = (h_max + 15) / 16 * 16;  // pinned staging pitch
     uint64_t S = slice_bytes / (h_max ? h_max : 1);
-    S = S < 1 ? 1 : (S > count ? count : S);
+    S = S < 1 ? 1 : S;
+    // host work per object (host stages, split copy-back): a slice of at least half
+    // the team is rounded up to a multiple of it, so every thread gets the same share
+    if ((hs || (zfec && bao)) && S >= (T + 1) / 2) S = (S + T - 1) / T * T;
+    S = S > count ? count : S;
     // split copy-back (SplitGeo): Zfec|Bao streams of at least 2 chunks
     const bool split_fmt = zfec && bao && c && e2e_split_on() && zlen_max >= 2048;
     // ...and with ECIES, the host stage writes each stream's data region straight
@@ -2266,6 +2334,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     std::vector<uint64_t> len(S), bc(S), be(S);
     std::vector<int> sts(S);
     std::vector<uint8_t> in_rows(S);  // object's data region written straight into out (direct)
+    std::unique_ptr<Team> team(hs || split_fmt ? new Team(std::min<uint32_t>(T, (uint32_t)S)) : nullptr);
     std::vector<Scratch> scratch(T);  // per host thread, reused across slices
     auto drain = [&]() {
         if (c)
@@ -2342,10 +2411,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                     }
                 }
             };
-            std::vector<std::thread> pool;
-            for (uint32_t t = 1; t < nt; ++t) pool.emplace_back(work, t);
-            work(0);
-            for (auto &th : pool) th.join();
+            team->run(nt, work);
             pp = SplitPending{};
             if (hs) {
                 for (uint64_t j = 0; j < cnt; ++j)
@@ -2422,16 +2488,13 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     if (c)
         for (uint32_t k = 0; k < nslots; ++k) CHIP_HIP(hipStreamSynchronize(c->slots[k].stream));
     // the nodes of the last slices into place
-    std::vector<std::thread> pool;
     for (uint32_t k = 0; k < nslots; ++k) {
         if (!pend[k].g) continue;
         const uint32_t nt = (uint32_t)std::min<uint64_t>(T, pend[k].cnt);
-        for (uint32_t t = 0; t < nt; ++t)
-            pool.emplace_back([&pend, k, t, nt] {
-                for (uint64_t j = t; j < pend[k].cnt; j += nt) pend[k].scatter(j);
-            });
+        team->run(nt, [&pend, k, nt](uint32_t t) {
+            for (uint64_t j = t; j < pend[k].cnt; j += nt) pend[k].scatter(j);
+        });
     }
-    for (auto &th : pool) th.join();
     return CHIP_OK;
 }
 

@@ -355,3 +355,27 @@ def test_secp256k1_scalar_mult_matches_oracles(ca):
         e = ca.encoding.ecies(pub, b"m" * i, ephemeral_sk=eph, nonce=nonce)
         assert e == O.c_ecies_encrypt(pub, b"m" * i, eph, nonce)
         assert ca.decoding.ecies(e, sk) == b"m" * i
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_encode_host_batch_host_levels(ca, threads):
+    """chip_encode_host_batch at the host-only levels (Ecies / Snappy, no device
+    part) on a team of host threads over several slices (the slice rounded up to
+    a multiple of the team): every object equals the oracle's encode()."""
+    import torch
+    from carbonado_amd import device
+    sk = H.sha256(b"team receiver")
+    pub = H.public_key(sk)
+    n, count = 20_001, 11
+    inp = torch.from_numpy(np.random.default_rng(threads).integers(0, 256, (count, n), dtype=np.uint8))
+    cap = device._lib.lib().chip_encode_max_len(n)
+    out = torch.zeros((count, cap), dtype=torch.uint8)
+    hashes = torch.zeros((count, 32), dtype=torch.uint8)
+    eph = np.stack([np.frombuffer(H.sha256(b"te%d" % o), np.uint8) for o in range(count)])
+    nonce = np.stack([np.frombuffer(H.sha256(b"tn%d" % o)[:16], np.uint8) for o in range(count)])
+    for level in (1, 2, 3):
+        olen, _ = device.encode_host_batch(level, inp, n, out, hashes, 3, slice_bytes=3 * n, pubkey=pub,
+                                           ephemeral_sk=eph, nonce=nonce, host_threads=threads)
+        for o in range(count):
+            enc, _, _ = O.encode_full(inp[o].numpy().tobytes(), level, pub, eph[o].tobytes(), nonce[o].tobytes())
+            assert out[o, :olen[o]].numpy().tobytes() == enc, (level, o)
