@@ -14,6 +14,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cctype>
 #include <condition_variable>
@@ -2110,8 +2111,17 @@ uint64_t split_chunks(uint64_t len) {
 // were a visible part of it).
 class Team {
   public:
-    explicit Team(uint32_t n) : n_(n ? n : 1) {
-        for (uint32_t t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+    explicit Team(uint32_t n) : n_(n ? n : 1), persistent_(team_on()) {
+        if (persistent_)
+            for (uint32_t t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+    }
+    // CHIP_TEAM=0: fresh threads for every run (A/B runs)
+    static bool team_on() {
+        static const bool on = [] {
+            const char *v = std::getenv("CHIP_TEAM");
+            return !(v && v[0] == '0' && v[1] == 0);
+        }();
+        return on;
     }
     ~Team() {
         {
@@ -2124,6 +2134,13 @@ class Team {
     }
     void run(uint32_t nt, const std::function<void(uint32_t)> &fn) {
         nt = std::max<uint32_t>(1, std::min(nt, n_));
+        if (!persistent_) {
+            std::vector<std::thread> pool;
+            for (uint32_t t = 1; t < nt; ++t) pool.emplace_back(fn, t);
+            fn(0);
+            for (auto &th : pool) th.join();
+            return;
+        }
         {
             std::lock_guard<std::mutex> lk(mu_);
             fn_ = &fn;
@@ -2157,6 +2174,7 @@ class Team {
         }
     }
     uint32_t n_;
+    bool persistent_;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
@@ -2164,6 +2182,29 @@ class Team {
     uint32_t active_ = 0, pending_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
+};
+
+// CHIP_E2E_TRACE=1: where a chip_encode_host_batch call's wall time went
+// (host work of the slices on the team, waits for a slot's stream, the final
+// drain), one line on stderr per call
+struct CallTrace {
+    bool on = [] {
+        const char *v = std::getenv("CHIP_E2E_TRACE");
+        return v && v[0] == '1';
+    }();
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    double host = 0, host_max = 0, wait = 0, drain = 0;
+    double now() const {
+        return on ? std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() : 0.0;
+    }
+    void report(uint64_t slices, uint64_t S) const {
+        if (!on) return;
+        std::fprintf(stderr,
+                     "[chip e2e] %llu slices of %llu: wall %.1f ms, host %.1f ms (slice max %.2f), "
+                     "slot waits %.1f ms, drain %.1f ms\n",
+                     (unsigned long long)slices, (unsigned long long)S, now() * 1e3, host * 1e3, host_max * 1e3,
+                     wait * 1e3, drain * 1e3);
+    }
 };
 
 // a slice waiting for its nodes: cnt objects, compact buffers at hnodes + j * nstride
@@ -2335,6 +2376,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     std::vector<int> sts(S);
     std::vector<uint8_t> in_rows(S);  // object's data region written straight into out (direct)
     std::unique_ptr<Team> team(hs || split_fmt ? new Team(std::min<uint32_t>(T, (uint32_t)S)) : nullptr);
+    CallTrace tr;
     std::vector<Scratch> scratch(T);  // per host thread, reused across slices
     auto drain = [&]() {
         if (c)
@@ -2343,7 +2385,9 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     const uint64_t nslices = (count + S - 1) / S;
     for (uint64_t i = 0; i < nslices; ++i) {
         Slot *sl = c ? &c->slots[i % nslots] : nullptr;
+        const double t_a = tr.now();
         if (sl && i >= nslots) CHIP_HIP(hipStreamSynchronize(sl->stream));  // slot's previous slice is done
+        tr.wait += tr.now() - t_a;
         const uint64_t o0 = i * S, cnt = (count - o0) < S ? (count - o0) : S;
         const uint8_t *src = in + o0 * in_stride;
         uint64_t src_pitch = count > 1 ? in_stride : n;
@@ -2411,7 +2455,11 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                     }
                 }
             };
+            const double t_h = tr.now();
             team->run(nt, work);
+            const double dh = tr.now() - t_h;
+            tr.host += dh;
+            tr.host_max = std::max(tr.host_max, dh);
             pp = SplitPending{};
             if (hs) {
                 for (uint64_t j = 0; j < cnt; ++j)
@@ -2485,8 +2533,11 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             }
         }
     }
+    const double t_d = tr.now();
     if (c)
         for (uint32_t k = 0; k < nslots; ++k) CHIP_HIP(hipStreamSynchronize(c->slots[k].stream));
+    tr.drain = tr.now() - t_d;
+    tr.report(nslices, S);
     // the nodes of the last slices into place
     for (uint32_t k = 0; k < nslots; ++k) {
         if (!pend[k].g) continue;
