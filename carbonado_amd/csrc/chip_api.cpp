@@ -2104,88 +2104,18 @@ uint64_t split_chunks(uint64_t len) {
     return (uint64_t)CHIP_FEC_M * C / 1024;
 }
 
-// A team of host threads for one batch call: run(nt, fn) runs fn(t) for
-// t < nt on the caller and nt - 1 parked workers and returns when all are
-// done.  The workers are made once per call instead of once per slice (a
-// slice's host work is a few ms; 16 thread creations and joins per slice
-// were a visible part of it).
-class Team {
-  public:
-    explicit Team(uint32_t n) : n_(n ? n : 1), persistent_(team_on()) {
-        if (persistent_)
-            for (uint32_t t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
-    }
-    // CHIP_TEAM=0: fresh threads for every run (A/B runs)
-    static bool team_on() {
-        static const bool on = [] {
-            const char *v = std::getenv("CHIP_TEAM");
-            return !(v && v[0] == '0' && v[1] == 0);
-        }();
-        return on;
-    }
-    ~Team() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-            ++gen_;
-        }
-        cv_.notify_all();
-        for (auto &t : th_) t.join();
-    }
-    void run(uint32_t nt, const std::function<void(uint32_t)> &fn) {
-        nt = std::max<uint32_t>(1, std::min(nt, n_));
-        if (!persistent_) {
-            std::vector<std::thread> pool;
-            for (uint32_t t = 1; t < nt; ++t) pool.emplace_back(fn, t);
-            fn(0);
-            for (auto &th : pool) th.join();
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            fn_ = &fn;
-            active_ = nt;
-            pending_ = nt - 1;
-            ++gen_;
-        }
-        if (nt > 1) cv_.notify_all();
-        fn(0);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return pending_ == 0; });
-        fn_ = nullptr;
-    }
-
-  private:
-    void loop(uint32_t t) {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(uint32_t)> *fn;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
-                if (stop_) return;
-                if (t >= active_) continue;
-                fn = fn_;
-            }
-            (*fn)(t);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_.notify_one();
-        }
-    }
-    uint32_t n_;
-    bool persistent_;
-    std::vector<std::thread> th_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_;
-    const std::function<void(uint32_t)> *fn_ = nullptr;
-    uint32_t active_ = 0, pending_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
+// fn(t) for t < nt on the caller and nt - 1 fresh threads.  (A persistent
+// team parked on a condition variable measured 30 % slower on the GPU box:
+// woken workers pile onto the waker's cores, r9p_session.)
+void run_threads(uint32_t nt, const std::function<void(uint32_t)> &fn) {
+    std::vector<std::thread> pool;
+    for (uint32_t t = 1; t < nt; ++t) pool.emplace_back(fn, t);
+    fn(0);
+    for (auto &th : pool) th.join();
+}
 
 // CHIP_E2E_TRACE=1: where a chip_encode_host_batch call's wall time went
-// (host work of the slices on the team, waits for a slot's stream, the final
+// (host work of the slices on their threads, waits for a slot's stream, the final
 // drain), one line on stderr per call
 struct CallTrace {
     bool on = [] {
@@ -2336,8 +2266,8 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     const uint64_t h_al = (h_max + 15) / 16 * 16;  // pinned staging pitch
     uint64_t S = slice_bytes / (h_max ? h_max : 1);
     S = S < 1 ? 1 : S;
-    // host work per object (host stages, split copy-back): a slice of at least half
-    // the team is rounded up to a multiple of it, so every thread gets the same share
+    // host work per object (host stages, split copy-back): a slice of at least half as
+    // many objects as host threads is rounded up to a multiple of them (equal shares)
     if ((hs || (zfec && bao)) && S >= (T + 1) / 2) S = (S + T - 1) / T * T;
     S = S > count ? count : S;
     // split copy-back (SplitGeo): Zfec|Bao streams of at least 2 chunks
@@ -2375,7 +2305,6 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     std::vector<uint64_t> len(S), bc(S), be(S);
     std::vector<int> sts(S);
     std::vector<uint8_t> in_rows(S);  // object's data region written straight into out (direct)
-    std::unique_ptr<Team> team(hs || split_fmt ? new Team(std::min<uint32_t>(T, (uint32_t)S)) : nullptr);
     CallTrace tr;
     std::vector<Scratch> scratch(T);  // per host thread, reused across slices
     auto drain = [&]() {
@@ -2456,7 +2385,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                 }
             };
             const double t_h = tr.now();
-            team->run(nt, work);
+            run_threads(nt, work);
             const double dh = tr.now() - t_h;
             tr.host += dh;
             tr.host_max = std::max(tr.host_max, dh);
@@ -2542,7 +2471,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     for (uint32_t k = 0; k < nslots; ++k) {
         if (!pend[k].g) continue;
         const uint32_t nt = (uint32_t)std::min<uint64_t>(T, pend[k].cnt);
-        team->run(nt, [&pend, k, nt](uint32_t t) {
+        run_threads(nt, [&pend, k, nt](uint32_t t) {
             for (uint64_t j = t; j < pend[k].cnt; j += nt) pend[k].scatter(j);
         });
     }

@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 teamab
+#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -65,8 +65,6 @@ for s in "$@"; do
     slicesweep) for i in 1 2; do for cfg in "272 3" "544 3" "272 4" "544 2" "1088 2"; do set -- $cfg
                   run bench_e2e15_s$1_k$2_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify --slice-mib $1 --slots $2; done; done ;;
     e2e3) for i in 1 2 3; do run bench_e2e15_team_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify; done ;;
-    teamab) for i in 1 2 3; do CHIP_E2E_TRACE=1 run bench_e2e15_team_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify
-                              CHIP_E2E_TRACE=1 CHIP_TEAM=0 run bench_e2e15_spawn_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify; done ;;
     valupk) run valu_probe_pk 300 ./tools/valu_probe 40000 pk ;;
     valuprobe) run valu_probe_b3x2 300 ./tools/valu_probe 40000 b3x2 ;;
     *) echo "unknown step $s"; exit 2 ;;

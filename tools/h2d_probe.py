@@ -20,6 +20,7 @@ def main():
     src = torch.empty(total, dtype=torch.uint8).pin_memory()
     src.random_(0, 256)
     dst = torch.empty(total, dtype=torch.uint8, device=dev)
+    dst2 = torch.empty(total, dtype=torch.uint8, device=dev)
     out = {}
     for mib in (1, 2, 4, 8, 16, 64, 256):
         piece = mib << 20
@@ -32,6 +33,33 @@ def main():
             torch.cuda.synchronize()
             best = min(best, time.perf_counter() - t0)
         out[f"pinned_{mib}MiB_GBps"] = round(total / best / 1e9, 2)
+    # both directions at once (encode() E2E moves ~18 MB each way per object):
+    # H2D on one stream, D2H on another, 16 MiB pieces, pinned both sides
+    back = torch.empty(total, dtype=torch.uint8).pin_memory()
+    s_up, s_down = torch.cuda.Stream(), torch.cuda.Stream()
+    piece = 16 << 20
+    best = 1e9
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for off in range(0, total, piece):
+            with torch.cuda.stream(s_up):
+                dst[off:off + piece].copy_(src[off:off + piece], non_blocking=True)
+            with torch.cuda.stream(s_down):
+                back[off:off + piece].copy_(dst2[off:off + piece], non_blocking=True)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    out["duplex_16MiB_each_way_GBps"] = round(total / best / 1e9, 2)
+    out["duplex_16MiB_total_GBps"] = round(2 * total / best / 1e9, 2)
+    best = 1e9
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for off in range(0, total, piece):
+            back[off:off + piece].copy_(dst2[off:off + piece], non_blocking=True)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    out["d2h_16MiB_GBps"] = round(total / best / 1e9, 2)
     # the library's staged path: a pageable source through the pinned ring (4 MiB pieces)
     from carbonado_amd.utils import BaoHasher
     import numpy as np
