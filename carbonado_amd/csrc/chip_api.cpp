@@ -2030,33 +2030,6 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
 
 namespace {
 
-// Rows between host and HBM for the batch pipelines.  hipMemcpy2DAsync goes
-// to the SDMA engine as one rectangular device-to-device copy whichever the
-// direction (the pinned host side is device-mapped), so an H2D of one slot
-// and a D2H of another contend for it; row-by-row 1D copies are queued per
-// direction (CHIP_COPY_ROWS: 1 rows, 0 rectangles; default rows).
-bool copy_rows_on() {
-    static const bool on = [] {
-        const char *v = std::getenv("CHIP_COPY_ROWS");
-        return !(v && v[0] == '0' && v[1] == 0);
-    }();
-    return on;
-}
-
-hipError_t copy_rows(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t rows,
-                     hipMemcpyKind kind, hipStream_t s) {
-    if (!width || !rows) return hipSuccess;
-    if (rows == 1 || (dpitch == width && spitch == width))
-        return hipMemcpyAsync(dst, src, width * rows, kind, s);
-    if (!copy_rows_on()) return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s);
-    for (size_t r = 0; r < rows; ++r) {
-        hipError_t e = hipMemcpyAsync(static_cast<uint8_t *>(dst) + r * dpitch,
-                                      static_cast<const uint8_t *>(src) + r * spitch, width, kind, s);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
-
 // encode() at Zfec|Bao from host memory, split copy-back: the stream's data
 // region [0, t0) -- its header, the data-shard chunks [0, nd) and the parent
 // nodes between them -- is half of the stream, and all of it but the nodes
@@ -2193,10 +2166,10 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
         // in out: the data regions come over and the chunks are gathered into rows
         const uint64_t t_al = (split->t0 + 15) / 16 * 16;
         uint8_t *d_sin = static_cast<uint8_t *>(sl.sin.p);
-        CHIP_HIP(copy_rows(d_sin, t_al, out, out_pitch, split->t0, cnt, hipMemcpyHostToDevice, sl.stream));
+        CHIP_HIP(hipMemcpy2DAsync(d_sin, t_al, out, out_pitch, split->t0, cnt, hipMemcpyHostToDevice, sl.stream));
         CHIP_HIP(bao_gather_rows(d_sin, t_al, split->N, cnt, cur_n, d_in, n_al, sl.stream));
     } else if (cur_n) {
-        CHIP_HIP(copy_rows(d_in, n_al, src, src_pitch, cur_n, cnt, hipMemcpyHostToDevice, sl.stream));
+        CHIP_HIP(hipMemcpy2DAsync(d_in, n_al, src, src_pitch, cur_n, cnt, hipMemcpyHostToDevice, sl.stream));
     }
     const uint8_t *d_cur = d_in;
     uint64_t cur_stride = n_al;
@@ -2212,10 +2185,10 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
                                         sl.stream));
                 CHIP_HIP(hipMemcpyAsync(sl.hnodes.p, sl.nodes.p, cnt * ns, hipMemcpyDeviceToHost, sl.stream));
             }
-            CHIP_HIP(copy_rows(out + split->t0, out_pitch, d_str + split->t0, f_al, final_len - split->t0, cnt,
+            CHIP_HIP(hipMemcpy2DAsync(out + split->t0, out_pitch, d_str + split->t0, f_al, final_len - split->t0, cnt,
                                       hipMemcpyDeviceToHost, sl.stream));
         } else if (final_len) {
-            CHIP_HIP(copy_rows(out, out_pitch, sl.out.p, f_al, final_len, cnt, hipMemcpyDeviceToHost,
+            CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, sl.out.p, f_al, final_len, cnt, hipMemcpyDeviceToHost,
                                       sl.stream));
         }
         return CHIP_OK;
@@ -2238,7 +2211,7 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
         for (uint64_t o = 0; o < cnt; ++o) std::memset(hashes + 32 * o, 0, 32);
     }
     if (final_len)
-        CHIP_HIP(copy_rows(out, out_pitch, d_res, res_stride, final_len, cnt, hipMemcpyDeviceToHost,
+        CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, d_res, res_stride, final_len, cnt, hipMemcpyDeviceToHost,
                                   sl.stream));
     return CHIP_OK;
 }
@@ -2677,7 +2650,7 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
             if (geo[o].st != CHIP_OK) continue;
             const uint64_t n = in_len[o], blen = geo[o].blen, olen = geo[o].olen;
             uint8_t *d_in = static_cast<uint8_t *>(sl.in.p) + j0 * i_al;
-            if (n) CHIP_HIP(copy_rows(d_in, i_al, in + o * in_stride, count > 1 ? in_stride : n, n, gcnt,
+            if (n) CHIP_HIP(hipMemcpy2DAsync(d_in, i_al, in + o * in_stride, count > 1 ? in_stride : n, n, gcnt,
                                              hipMemcpyHostToDevice, sl.stream));
             const uint8_t *d_res = d_in;
             uint64_t res_pitch = i_al;
@@ -2701,7 +2674,7 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
                     for (uint64_t j = 0; j < gcnt; ++j) status[o + j] = CHIP_ERR_BUFFER_TOO_SMALL;
                     continue;
                 }
-                CHIP_HIP(copy_rows(dst, dpitch, d_res, res_pitch, olen, gcnt, hipMemcpyDeviceToHost, sl.stream));
+                CHIP_HIP(hipMemcpy2DAsync(dst, dpitch, d_res, res_pitch, olen, gcnt, hipMemcpyDeviceToHost, sl.stream));
             }
         }
         return CHIP_OK;
