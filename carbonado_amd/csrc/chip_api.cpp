@@ -90,9 +90,6 @@ struct DevBuf {
 // (`stage` is pinned host memory holding the host-stage output of a slice)
 struct Slot {
     hipStream_t stream = nullptr;
-    // copy-stream mode (chip_encode_host_batch): H2D done / kernels done / the
-    // slice's D2H done (the slot may be reused)
-    hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_done = nullptr;
     DevBuf in, mid, out, hash, scratch, nodes, sin;  // sin: data regions taken from host rows
     DevBuf stage, hnodes;  // pinned
 };
@@ -122,7 +119,6 @@ struct Ctx {
     hipStream_t stream = nullptr;
     DevBuf in, mid, out, scratch, small, x1, x2, flags;
     std::vector<Slot> slots;
-    hipStream_t up = nullptr, down = nullptr;  // the batch pipeline's H2D and D2H copy streams
     Staging stage;
     // pinned arena for the few-byte copies of a call (hashes, status words,
     // node flags): see small_h2d / small_d2h / small_sync
@@ -151,24 +147,16 @@ struct Ctx {
             (void)hipStreamDestroy(stream);
         }
         stream = nullptr;
-        for (hipStream_t *cs : {&up, &down})
-            if (*cs) {
-                (void)hipStreamSynchronize(*cs);
-                (void)hipStreamDestroy(*cs);
-                *cs = nullptr;
-            }
         for (Slot &sl : slots) {
+            for (DevBuf *b : {&sl.in, &sl.mid, &sl.out, &sl.hash, &sl.scratch, &sl.nodes, &sl.sin})
+                if (b->p) (void)hipFree(b->p);
+            for (DevBuf *b : {&sl.stage, &sl.hnodes})
+                if (b->p) (void)hipHostFree(b->p);
             if (sl.stream) {
                 (void)hipStreamSynchronize(sl.stream);
                 stream_queue_release(sl.stream);
                 (void)hipStreamDestroy(sl.stream);
             }
-            for (hipEvent_t e : {sl.ev_in, sl.ev_k, sl.ev_done})
-                if (e) (void)hipEventDestroy(e);
-            for (DevBuf *b : {&sl.in, &sl.mid, &sl.out, &sl.hash, &sl.scratch, &sl.nodes, &sl.sin})
-                if (b->p) (void)hipFree(b->p);
-            for (DevBuf *b : {&sl.stage, &sl.hnodes})
-                if (b->p) (void)hipHostFree(b->p);
         }
         slots.clear();
         ready = false;
@@ -2042,24 +2030,6 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
 
 namespace {
 
-// work on `to` waits for what is queued on `from` (nothing to do on one stream)
-hipError_t join(hipStream_t from, hipEvent_t ev, hipStream_t to) {
-    if (from == to) return hipSuccess;
-    hipError_t e = hipEventRecord(ev, from);
-    return e != hipSuccess ? e : hipStreamWaitEvent(to, ev, 0);
-}
-
-// CHIP_COPY_STREAMS=0: each slot's copies on its own stream (A/B runs).  By
-// default chip_encode_host_batch queues every slice's H2D on one stream and
-// every D2H on another, the kernels on the slot's stream between them.
-bool copy_streams_on() {
-    static const bool on = [] {
-        const char *v = std::getenv("CHIP_COPY_STREAMS");
-        return !(v && v[0] == '0' && v[1] == 0);
-    }();
-    return on;
-}
-
 // encode() at Zfec|Bao from host memory, split copy-back: the stream's data
 // region [0, t0) -- its header, the data-shard chunks [0, nd) and the parent
 // nodes between them -- is half of the stream, and all of it but the nodes
@@ -2187,49 +2157,40 @@ struct SplitPending {
 int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_encode_info &inf,
                        const uint8_t *src, uint64_t src_pitch, uint64_t cur_n, uint64_t zlen, uint64_t final_len,
                        uint64_t cnt, uint8_t *out, uint64_t out_pitch, uint8_t *hashes,
-                       const SplitGeo *split = nullptr, bool from_rows = false, hipStream_t cin = nullptr,
-                       hipStream_t cout = nullptr) {
+                       const SplitGeo *split = nullptr, bool from_rows = false) {
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
     const uint64_t n_al = (cur_n + 15) / 16 * 16, z_al = (zlen + 15) / 16 * 16, f_al = (final_len + 15) / 16 * 16;
     uint8_t *d_in = static_cast<uint8_t *>(sl.in.p);
-    // copies on the pipeline's H2D / D2H streams (copy-stream mode) or on the slot's;
-    // the slot's buffers are free once its last D2H is done (the ragged path calls
-    // this once per object on one slot; across slices the caller has waited already)
-    if (!cin) cin = sl.stream;
-    if (!cout) cout = sl.stream;
-    if (cin != sl.stream) CHIP_HIP(hipStreamWaitEvent(cin, sl.ev_done, 0));
     if (from_rows && split && cur_n) {
         // the host stage wrote each object's zfec input into its stream's chunk slots
         // in out: the data regions come over and the chunks are gathered into rows
         const uint64_t t_al = (split->t0 + 15) / 16 * 16;
         uint8_t *d_sin = static_cast<uint8_t *>(sl.sin.p);
-        CHIP_HIP(hipMemcpy2DAsync(d_sin, t_al, out, out_pitch, split->t0, cnt, hipMemcpyHostToDevice, cin));
-        CHIP_HIP(join(cin, sl.ev_in, sl.stream));
+        CHIP_HIP(hipMemcpy2DAsync(d_sin, t_al, out, out_pitch, split->t0, cnt, hipMemcpyHostToDevice, sl.stream));
         CHIP_HIP(bao_gather_rows(d_sin, t_al, split->N, cnt, cur_n, d_in, n_al, sl.stream));
     } else if (cur_n) {
-        CHIP_HIP(hipMemcpy2DAsync(d_in, n_al, src, src_pitch, cur_n, cnt, hipMemcpyHostToDevice, cin));
-        CHIP_HIP(join(cin, sl.ev_in, sl.stream));
+        CHIP_HIP(hipMemcpy2DAsync(d_in, n_al, src, src_pitch, cur_n, cnt, hipMemcpyHostToDevice, sl.stream));
     }
     const uint8_t *d_cur = d_in;
     uint64_t cur_stride = n_al;
     if (zfec && bao && zlen) {  // fused: shards written into the bao streams, hashed in place
         CHIP_HIP(zfec_bao_dev(d_in, n_al, cur_n, cnt, inf.chunk_len, static_cast<uint8_t *>(sl.out.p), f_al,
                               static_cast<uint8_t *>(sl.hash.p), sl.scratch.p, sl.stream));
-        uint8_t *d_str = static_cast<uint8_t *>(sl.out.p);
-        const uint64_t ns = split ? 64 * split->nb : 0;
-        if (ns)
-            CHIP_HIP(bao_data_nodes(d_str, f_al, split->N, split->nd, cnt, static_cast<uint8_t *>(sl.nodes.p), ns,
-                                    sl.stream));
-        CHIP_HIP(join(sl.stream, sl.ev_k, cout));
-        CHIP_HIP(hipMemcpyAsync(hashes, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, cout));
+        CHIP_HIP(hipMemcpyAsync(hashes, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, sl.stream));
         if (split) {
-            if (ns) CHIP_HIP(hipMemcpyAsync(sl.hnodes.p, sl.nodes.p, cnt * ns, hipMemcpyDeviceToHost, cout));
+            const uint64_t ns = 64 * split->nb;
+            uint8_t *d_str = static_cast<uint8_t *>(sl.out.p);
+            if (ns) {
+                CHIP_HIP(bao_data_nodes(d_str, f_al, split->N, split->nd, cnt, static_cast<uint8_t *>(sl.nodes.p), ns,
+                                        sl.stream));
+                CHIP_HIP(hipMemcpyAsync(sl.hnodes.p, sl.nodes.p, cnt * ns, hipMemcpyDeviceToHost, sl.stream));
+            }
             CHIP_HIP(hipMemcpy2DAsync(out + split->t0, out_pitch, d_str + split->t0, f_al, final_len - split->t0, cnt,
-                                      hipMemcpyDeviceToHost, cout));
+                                      hipMemcpyDeviceToHost, sl.stream));
         } else if (final_len) {
-            CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, sl.out.p, f_al, final_len, cnt, hipMemcpyDeviceToHost, cout));
+            CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, sl.out.p, f_al, final_len, cnt, hipMemcpyDeviceToHost,
+                                      sl.stream));
         }
-        CHIP_HIP(hipEventRecord(sl.ev_done, cout));
         return CHIP_OK;
     }
     if (zfec) {
@@ -2245,14 +2206,13 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
                                 static_cast<uint8_t *>(sl.hash.p), sl.scratch.p, sl.stream));
         d_res = static_cast<const uint8_t *>(sl.out.p);
         res_stride = f_al;
+        CHIP_HIP(hipMemcpyAsync(hashes, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, sl.stream));
     } else {
         for (uint64_t o = 0; o < cnt; ++o) std::memset(hashes + 32 * o, 0, 32);
     }
-    CHIP_HIP(join(sl.stream, sl.ev_k, cout));
-    if (bao) CHIP_HIP(hipMemcpyAsync(hashes, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, cout));
     if (final_len)
-        CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, d_res, res_stride, final_len, cnt, hipMemcpyDeviceToHost, cout));
-    CHIP_HIP(hipEventRecord(sl.ev_done, cout));
+        CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, d_res, res_stride, final_len, cnt, hipMemcpyDeviceToHost,
+                                  sl.stream));
     return CHIP_OK;
 }
 
@@ -2310,13 +2270,6 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     // many objects as host threads is rounded up to a multiple of them (equal shares)
     if ((hs || (zfec && bao)) && S >= (T + 1) / 2) S = (S + T - 1) / T * T;
     S = S > count ? count : S;
-    hipStream_t cin = nullptr, cout = nullptr;  // copy-stream mode
-    if (c && copy_streams_on()) {
-        for (hipStream_t *cs : {&c->up, &c->down})
-            if (!*cs) CHIP_HIP(hipStreamCreateWithFlags(cs, hipStreamNonBlocking));
-        cin = c->up;
-        cout = c->down;
-    }
     // split copy-back (SplitGeo): Zfec|Bao streams of at least 2 chunks
     const bool split_fmt = zfec && bao && c && e2e_split_on() && zlen_max >= 2048;
     // ...and with ECIES, the host stage writes each stream's data region straight
@@ -2329,9 +2282,6 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
         for (uint32_t k = 0; k < nslots; ++k) {
             Slot &sl = c->slots[k];
             if (!sl.stream) CHIP_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-            for (hipEvent_t *e : {&sl.ev_in, &sl.ev_k, &sl.ev_done})
-                if (!*e) CHIP_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-            CHIP_HIP(hipEventRecord(sl.ev_done, sl.stream));  // a recorded, complete event to start from
             CHIP_HIP(grow(sl.in, S * h_al));
             if (zfec && !bao) CHIP_HIP(grow(sl.mid, S * ((zlen_max + 15) / 16 * 16)));  // Zfec|Bao: fused
             if (bao) {
@@ -2358,17 +2308,14 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     CallTrace tr;
     std::vector<Scratch> scratch(T);  // per host thread, reused across slices
     auto drain = [&]() {
-        if (c) {
+        if (c)
             for (uint32_t k = 0; k < nslots; ++k) (void)hipStreamSynchronize(c->slots[k].stream);
-            for (hipStream_t cs : {c->up, c->down})
-                if (cs) (void)hipStreamSynchronize(cs);
-        }
     };
     const uint64_t nslices = (count + S - 1) / S;
     for (uint64_t i = 0; i < nslices; ++i) {
         Slot *sl = c ? &c->slots[i % nslots] : nullptr;
         const double t_a = tr.now();
-        if (sl && i >= nslots) CHIP_HIP(hipEventSynchronize(sl->ev_done));  // slot's previous slice is done
+        if (sl && i >= nslots) CHIP_HIP(hipStreamSynchronize(sl->stream));  // slot's previous slice is done
         tr.wait += tr.now() - t_a;
         const uint64_t o0 = i * S, cnt = (count - o0) < S ? (count - o0) : S;
         const uint8_t *src = in + o0 * in_stride;
@@ -2492,7 +2439,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             const SplitGeo *g = split_fmt && zl >= 2048 ? &geos.get(zl / 1024) : nullptr;
             const uint64_t opitch = count > 1 ? out_stride : fl;
             st = batch_slice_device(*sl, format, &p2, inf, src, src_pitch, cur_n, zl, fl, cnt, out + o0 * out_stride,
-                                    opitch, hashes + 32 * o0, g, rows, cin, cout);
+                                    opitch, hashes + 32 * o0, g, rows);
             if (st != CHIP_OK) {
                 drain();
                 return st;
@@ -2507,8 +2454,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                 (void)encode_info_for(format, n, len[j], 0, 0, &inf, &zl, &fl);
                 const GfPlan pj = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, enc);
                 st = batch_slice_device(*sl, format, &pj, inf, src + j * src_pitch, src_pitch, len[j], zl, fl, 1,
-                                        out + (o0 + j) * out_stride, fl, hashes + 32 * (o0 + j), nullptr, false,
-                                        cin, cout);
+                                        out + (o0 + j) * out_stride, fl, hashes + 32 * (o0 + j));
                 if (st != CHIP_OK) {
                     drain();
                     return st;
@@ -2517,11 +2463,8 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
         }
     }
     const double t_d = tr.now();
-    if (c) {
+    if (c)
         for (uint32_t k = 0; k < nslots; ++k) CHIP_HIP(hipStreamSynchronize(c->slots[k].stream));
-        for (hipStream_t cs : {c->up, c->down})
-            if (cs) CHIP_HIP(hipStreamSynchronize(cs));
-    }
     tr.drain = tr.now() - t_d;
     tr.report(nslices, S);
     // the nodes of the last slices into place

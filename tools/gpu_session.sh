@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full csab sdmaab
+#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -69,10 +69,6 @@ for s in "$@"; do
     sdmaab) for i in 1 2; do HSA_ENABLE_SDMA=0 run bench_e2e15_nosdma_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify
                              run bench_e2e15_sdma_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify; done ;;
     e2ed15full) run bench_e2ed15_full 600 python3 bench.py --mode e2e-decode --level 15 --steps 3 --warmup 1 --cpu-seconds 8 ;;
-    csab) for i in 1 2; do run bench_e2e15_cs_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify
-                           CHIP_COPY_STREAMS=0 run bench_e2e15_slotcs_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify
-                           run bench_e2e12_cs_$i 300 python3 bench.py --mode e2e --level 12 --objects 512 --steps 4 --warmup 1 --no-cpu-baseline --no-verify
-                           CHIP_COPY_STREAMS=0 run bench_e2e12_slotcs_$i 300 python3 bench.py --mode e2e --level 12 --objects 512 --steps 4 --warmup 1 --no-cpu-baseline --no-verify; done ;;
     valupk) run valu_probe_pk 300 ./tools/valu_probe 40000 pk ;;
     valuprobe) run valu_probe_b3x2 300 ./tools/valu_probe 40000 b3x2 ;;
     *) echo "unknown step $s"; exit 2 ;;
