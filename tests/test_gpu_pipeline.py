@@ -166,6 +166,39 @@ def test_encode_host_batch_split_copy_back(gpu, level, n):
             assert (out[o, olen[o]:].numpy() == 0xA5).all()  # nothing past the stream
 
 
+@pytest.mark.parametrize("kind", ["ragged", "uniform_compressible"])
+def test_encode_host_batch_direct_fallbacks(gpu, kind):
+    """Pinned output at Ecies|Snappy|Zfec|Bao: the host stage encrypts straight
+    into the chunk slots laid out for the incompressible size.  Objects that
+    compress get another geometry: their output is read back from the slots
+    and placed again (ragged slices: per-object launches; a uniform slice of
+    equally compressible objects: the staged split path).  Every object equals
+    the oracle's, nothing is written past a stream."""
+    import torch
+    from carbonado_amd import device
+    n = 150_000
+    rng = np.random.default_rng(31)
+    if kind == "ragged":
+        rows = [rng.integers(0, 256, n, dtype=np.uint8), np.zeros(n, np.uint8),
+                rng.integers(0, 256, n, dtype=np.uint8), np.frombuffer((b"carbonado " * n)[:n], np.uint8),
+                rng.integers(0, 256, n, dtype=np.uint8), rng.integers(0, 3, n, dtype=np.uint8)]
+    else:
+        rows = [np.frombuffer((b"abcdefgh" * n)[:n], np.uint8) for _ in range(6)]
+    count = len(rows)
+    inp = torch.from_numpy(np.stack(rows)).pin_memory()
+    cap = device._lib.lib().chip_encode_max_len(n)
+    out = torch.full((count, cap + 8), 0xA5, dtype=torch.uint8).pin_memory()
+    hashes = torch.zeros((count, 32), dtype=torch.uint8).pin_memory()
+    eph = np.stack([np.frombuffer(H.sha256(b"f%d" % o), np.uint8) for o in range(count)])
+    nonce = np.stack([np.frombuffer(H.sha256(b"g%d" % o)[:16], np.uint8) for o in range(count)])
+    olen, _ = device.encode_host_batch(15, inp, n, out, hashes, nslots=2, slice_bytes=2 * n, pubkey=PUB,
+                                       ephemeral_sk=eph, nonce=nonce, host_threads=2)
+    for o in range(count):
+        enc, h, _ = O.encode_full(rows[o].tobytes(), 15, PUB, eph[o].tobytes(), nonce[o].tobytes())
+        assert out[o, :olen[o]].numpy().tobytes() == enc and hashes[o].numpy().tobytes() == h, o
+        assert (out[o, olen[o]:].numpy() == 0xA5).all(), o
+
+
 @pytest.mark.parametrize("name", SAMPLES)
 @pytest.mark.parametrize("level", [1, 2, 3, 14, 15])
 def test_codec_samples_host_levels(gpu, golden, golden_dir, name, level):
