@@ -438,6 +438,9 @@ PCIE_SPEC_GBS = 63.0  # PCIe Gen5 x16, per direction (spec)
 # one direction alone, pinned host memory, the runtime's DMA path (tools/pageable_probe.hip,
 # profiles/r1w_pageable_probe.txt): the practical per-direction ceilings on the GPU box
 PCIE_MEASURED_GBS = {"h2d": 55.6, "d2h": 55.0}
+# both directions at once: two pinned 16 MiB-piece copy streams side by side
+# (tools/h2d_probe.py, profiles/r9q_session/h2d_probe.log: 47.1 GB/s each way)
+PCIE_MEASURED_DUPLEX_GBS = 94.2
 
 
 def bao_data_region_len(N: int) -> int:
@@ -467,9 +470,12 @@ def pcie_roofline(h2d_bytes: int, d2h_bytes: int, step_s: float, duplex_achieved
             "h2d_GBps": round(rate["h2d"], 2), "d2h_GBps": round(rate["d2h"], 2),
             "h2d_frac": round(rate["h2d"] / PCIE_SPEC_GBS, 4), "d2h_frac": round(rate["d2h"] / PCIE_SPEC_GBS, 4),
             "duplex_GBps": round(duplex_achieved, 2), "duplex_frac": round(duplex_achieved / (2 * PCIE_SPEC_GBS), 4),
+            "duplex_peak_measured": PCIE_MEASURED_DUPLEX_GBS,
+            "duplex_frac_of_measured": round((rate["h2d"] + rate["d2h"]) / PCIE_MEASURED_DUPLEX_GBS, 4),
             "note": ("PCIe Gen5 x16: 63 GB/s per direction (spec); peak_measured = that direction alone from "
-                     "pinned memory on the GPU box (profiles/r1w_pageable_probe.txt); H2D and D2H overlap, rates "
-                     "over the whole step's wall time")}
+                     "pinned memory on the GPU box (profiles/r1w_pageable_probe.txt); duplex_peak_measured = both "
+                     "directions at once (profiles/r9q_session/h2d_probe.log); H2D and D2H overlap, rates over "
+                     "the whole step's wall time")}
 
 
 def bind_to_gpu_node() -> dict:
