@@ -998,6 +998,12 @@ int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const ui
         *len = cur_n;
         return CHIP_OK;
     }
+    if (snap && !ecies && sink && stream_encrypt_on()) {  // frames cut into the stream's chunk slots as they go
+        int st = host::snap_compress_stream(in, n, dst, cap, &cur_n, tmp.get(host::SNAP_ECIES_WINDOW), sink, filled);
+        if (st != CHIP_OK) return st;
+        *bc = *len = cur_n;
+        return CHIP_OK;
+    }
     if (snap) {
         uint8_t *sd = dst;
         uint64_t scap = cap;
@@ -2274,8 +2280,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     const bool split_fmt = zfec && bao && c && e2e_split_on() && zlen_max >= 2048;
     // ...and with ECIES, the host stage writes each stream's data region straight
     // into out (pinned), which the device then reads: no staging copy at all
-    const bool direct_fmt = split_fmt && hs && (format & CHIP_FORMAT_ECIES) && stream_encrypt_on() &&
-                            direct_rows_on() && out && host_pinned(out);
+    const bool direct_fmt = split_fmt && hs && stream_encrypt_on() && direct_rows_on() && out && host_pinned(out);
     SplitGeos geos;
     if (c) {
         if (c->slots.size() < nslots) c->slots.resize(nslots);

@@ -852,7 +852,8 @@ namespace {
 struct ChunkAssembler {
     const ChunkSink *sink;
     bool nt;
-    uint64_t pos = 97;
+    uint64_t hl = 97;  // bytes of a header written last (ECIES: key, nonce, tag); 0 for a snappy frame
+    uint64_t pos = hl;
     alignas(64) uint8_t part[1024];
     alignas(64) uint8_t first[1024];
     void slot(uint64_t ci, const uint8_t *src) {
@@ -863,7 +864,7 @@ struct ChunkAssembler {
         while (len) {
             const uint64_t ci = pos / 1024, at = pos % 1024;
             const size_t take = (size_t)std::min<uint64_t>(len, 1024 - at);
-            if (ci == 0) {
+            if (ci == 0 && hl) {
                 std::memcpy(first + at, p, take);
             } else if (ci < sink->nd) {
                 if (at == 0 && take == 1024) {
@@ -878,16 +879,22 @@ struct ChunkAssembler {
             pos += take;
         }
     }
-    uint64_t done() const { return std::max<uint64_t>(1, std::min<uint64_t>(sink->nd, pos / 1024)); }
-    // the rest of the output's chunks: the stream header, chunk 0 (ECIES
-    // header + the first ciphertext bytes) and the last partial chunk, zero
-    // padded; returns the chunks placed ([0, ceil(pos / 1024)))
-    uint64_t finish(const uint8_t head[97]) {
+    // chunks placed: [1, done()) with a held header, [0, done()) without
+    uint64_t done() const {
+        const uint64_t c = std::min<uint64_t>(sink->nd, pos / 1024);
+        return hl ? std::max<uint64_t>(1, c) : c;
+    }
+    // the rest of the output's chunks: the stream header, chunk 0 (with a
+    // held header: it + the first bytes after it) and the last partial chunk,
+    // zero padded; returns the chunks placed ([0, ceil(pos / 1024)))
+    uint64_t finish(const uint8_t *head) {
         for (int b = 0; b < 8; ++b) sink->out[b] = static_cast<uint8_t>(sink->zl >> (8 * b));
-        std::memcpy(first, head, 97);
-        if (pos < 1024) std::memset(first + pos, 0, 1024 - pos);
-        slot(0, first);
-        if (pos % 1024 && pos > 1024) {
+        if (hl) {
+            std::memcpy(first, head, hl);
+            if (pos < 1024) std::memset(first + pos, 0, 1024 - pos);
+            slot(0, first);
+        }
+        if (pos % 1024 && (pos > 1024 || !hl)) {
             std::memset(part + pos % 1024, 0, 1024 - pos % 1024);
             slot(pos / 1024, part);
         }
@@ -957,6 +964,44 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
     }
     if (nt || (sink && as.nt)) fence_nt();
     return st;
+}
+
+int snap_compress_stream(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                         uint8_t *window, const ChunkSink *sink, uint64_t *filled) {
+    const uint64_t m = snap_max_len(n);
+    if (out && cap < m) return CHIP_ERR_BUFFER_TOO_SMALL;
+    if (!out && !(sink && sink->complete)) return CHIP_ERR_INVALID_ARG;
+    if (sink && sink->complete && 1024 * sink->nd < m) return CHIP_ERR_INVALID_ARG;
+    if (filled) *filled = 0;
+    *out_len = 0;
+    if (n == 0) return CHIP_OK;  // FrameEncoder writes nothing for an empty input
+    const bool nt = sink && out && nt_stage_on();
+    ChunkAssembler as{sink, nt_copy_on(), 0};
+    uint64_t d = 0;
+    auto emit = [&](const uint8_t *p, size_t len) {
+        if (out) {
+            if (nt) nt_copy_avx2(out + d, p, len, false);
+            else std::memcpy(out + d, p, len);
+        }
+        if (sink) as.push(p, len);
+        d += len;
+    };
+    emit(STREAM_ID, sizeof(STREAM_ID));
+    for (uint64_t o = 0; o < n; o += MAX_BLOCK) {
+        const size_t len = (size_t)((n - o) < MAX_BLOCK ? (n - o) : MAX_BLOCK);
+        uint8_t hdr[8];
+        const uint8_t *body;
+        const size_t blen = snap_block(in + o, len, hdr, window, &body);
+        emit(hdr, 8);
+        emit(body, blen);
+    }
+    *out_len = d;
+    if (sink) {
+        const uint64_t placed = sink->complete ? as.finish(nullptr) : as.done();
+        if (filled) *filled = placed;
+    }
+    if (nt || (sink && as.nt)) fence_nt();
+    return CHIP_OK;
 }
 
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n) {

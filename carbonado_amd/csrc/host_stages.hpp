@@ -83,6 +83,10 @@ constexpr uint64_t SNAP_ECIES_WINDOW = 2 * (64 + 65536 + 65536 / 6);
 int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                          const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
                          uint8_t *window, const ChunkSink *sink, uint64_t *filled);
+// snap_compress with the same sink (encode() at Snappy|Zfec|Bao): the frame's
+// chunks [0, *filled) placed as they complete, `out` optional when complete.
+int snap_compress_stream(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                         uint8_t *window, const ChunkSink *sink, uint64_t *filled);
 // the first n bytes of a stream's content from its chunk slots row + coff[i]
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n);
 

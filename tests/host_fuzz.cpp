@@ -220,6 +220,35 @@ int main(int argc, char **argv) {
                 }
             }
         }
+        // snap_compress_stream: the frame of snap_compress, chunks [0, filled) at their slots
+        {
+            const bool complete = rnd(2);
+            const uint64_t m = snap_max_len(n);
+            const uint64_t nd = complete ? (m + 1023) / 1024 + rnd(3) : fl / 1024 + rnd(3);
+            std::vector<uint64_t> coff(nd);
+            for (uint64_t i = 0; i < nd; ++i) coff[i] = 8 + 1088 * i + 64 * rnd(2) * (i > 0);
+            Bytes strm(8 + 1088 * (nd + 1), 0xA5), win(SNAP_ECIES_WINDOW), out2(m + 1);
+            const uint64_t zl = 1024 * (1 + rnd(1000));
+            const ChunkSink sink{strm.data(), coff.data(), nd, complete, zl};
+            const bool with_sink = rnd(2) && nd;
+            const bool no_out = with_sink && complete && rnd(2);
+            uint64_t ol = 0, filled = 0;
+            EXPECT(snap_compress_stream(d.data(), n, no_out ? nullptr : out2.data(), out2.size(), &ol, win.data(),
+                                        with_sink ? &sink : nullptr, &filled) == 0, "snap stream n=%zu", n);
+            EXPECT(ol == fl && (no_out || same(out2.data(), frame.data(), fl)), "snap stream bytes n=%zu", n);
+            if (with_sink && n) {
+                Bytes want(strm.size(), 0xA5);
+                Bytes padded(frame.begin(), frame.end());
+                padded.resize((fl + 1023) / 1024 * 1024, 0);
+                if (complete) {
+                    for (int b = 0; b < 8; ++b) want[b] = (uint8_t)(zl >> (8 * b));
+                    EXPECT(filled == (fl + 1023) / 1024, "snap complete filled");
+                }
+                for (uint64_t i = 0; i < filled; ++i) std::memcpy(want.data() + coff[i], padded.data() + 1024 * i, 1024);
+                EXPECT(strm == want, "snap sink chunks n=%zu complete=%d filled=%llu", n, (int)complete,
+                       (unsigned long long)filled);
+            }
+        }
         // the 160-byte file header
         chip_header h{};
         uint8_t hash[32], meta[8], aux[32], bytes[CHIP_HEADER_LEN];

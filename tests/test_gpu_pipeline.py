@@ -136,7 +136,7 @@ def test_encode_host_batch_ragged_host_stage_sizes(gpu):
 
 
 @pytest.mark.parametrize("n", [1, 1000, 4096, 70_001, (1 << 20) + 5, 3 << 20])
-@pytest.mark.parametrize("level", [12, 13, 15])
+@pytest.mark.parametrize("level", [12, 13, 14, 15])
 def test_encode_host_batch_split_copy_back(gpu, level, n):
     """Zfec|Bao from host memory: the host writes each stream's header and
     data-shard chunks itself, the device gathers the parent nodes between them
@@ -166,9 +166,10 @@ def test_encode_host_batch_split_copy_back(gpu, level, n):
             assert (out[o, olen[o]:].numpy() == 0xA5).all()  # nothing past the stream
 
 
+@pytest.mark.parametrize("level", [14, 15])
 @pytest.mark.parametrize("kind", ["ragged", "uniform_compressible"])
-def test_encode_host_batch_direct_fallbacks(gpu, kind):
-    """Pinned output at Ecies|Snappy|Zfec|Bao: the host stage encrypts straight
+def test_encode_host_batch_direct_fallbacks(gpu, kind, level):
+    """Pinned output at (Ecies|)Snappy|Zfec|Bao: the host stage writes straight
     into the chunk slots laid out for the incompressible size.  Objects that
     compress get another geometry: their output is read back from the slots
     and placed again (ragged slices: per-object launches; a uniform slice of
@@ -191,10 +192,10 @@ def test_encode_host_batch_direct_fallbacks(gpu, kind):
     hashes = torch.zeros((count, 32), dtype=torch.uint8).pin_memory()
     eph = np.stack([np.frombuffer(H.sha256(b"f%d" % o), np.uint8) for o in range(count)])
     nonce = np.stack([np.frombuffer(H.sha256(b"g%d" % o)[:16], np.uint8) for o in range(count)])
-    olen, _ = device.encode_host_batch(15, inp, n, out, hashes, nslots=2, slice_bytes=2 * n, pubkey=PUB,
+    olen, _ = device.encode_host_batch(level, inp, n, out, hashes, nslots=2, slice_bytes=2 * n, pubkey=PUB,
                                        ephemeral_sk=eph, nonce=nonce, host_threads=2)
     for o in range(count):
-        enc, h, _ = O.encode_full(rows[o].tobytes(), 15, PUB, eph[o].tobytes(), nonce[o].tobytes())
+        enc, h, _ = O.encode_full(rows[o].tobytes(), level, PUB, eph[o].tobytes(), nonce[o].tobytes())
         assert out[o, :olen[o]].numpy().tobytes() == enc and hashes[o].numpy().tobytes() == h, o
         assert (out[o, olen[o]:].numpy() == 0xA5).all(), o
 

@@ -69,6 +69,8 @@ for s in "$@"; do
     sdmaab) for i in 1 2; do HSA_ENABLE_SDMA=0 run bench_e2e15_nosdma_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify
                              run bench_e2e15_sdma_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify; done ;;
     e2ed15full) run bench_e2ed15_full 600 python3 bench.py --mode e2e-decode --level 15 --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    e2e14) run bench_e2e14 300 python3 bench.py --mode e2e --level 14 --objects 512 --steps 4 --warmup 1 --no-cpu-baseline
+           CHIP_E2E_DIRECT=0 run bench_e2e14_staged 300 python3 bench.py --mode e2e --level 14 --objects 512 --steps 4 --warmup 1 --no-cpu-baseline --no-verify ;;
     valupk) run valu_probe_pk 300 ./tools/valu_probe 40000 pk ;;
     valuprobe) run valu_probe_b3x2 300 ./tools/valu_probe 40000 b3x2 ;;
     *) echo "unknown step $s"; exit 2 ;;
