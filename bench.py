@@ -881,7 +881,7 @@ class Workload:
                 self.copy_back = (f"split: host writes header + data chunks ({host_made // count} B/object), "
                                   f"{self.d2h_bytes // count} B/object D2H")
                 if lv & 3 and os.environ.get("CHIP_E2E_DIRECT", "1") != "0":
-                    # direct: the ECIES output is written into the stream's data region in
+                    # direct: the host-stage output is written into the stream's data region in
                     # host memory, and that region [0, t0) is what crosses H2D
                     zls = [int.from_bytes(self.h_out[o, :8].numpy().tobytes(), "little") for o in range(count)]
                     self.h2d_bytes = sum(bao_data_region_len(z // 1024) for z in zls)
