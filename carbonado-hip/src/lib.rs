@@ -785,7 +785,10 @@ pub fn scrub_batch(input: &DeviceRows, len: u64, hashes: &DeviceBuffer, padding:
 /// encode() of `count` objects in HOST memory, H2D / kernels / D2H and the
 /// host stages overlapped over `nslots` device slots.  Returns the encoded
 /// length of every object; streams at `out[o * out_stride..]`, hashes at
-/// `hashes[32 o..]`.
+/// `hashes[32 o..]`.  At Zfec|Bao the library writes each stream's header and
+/// data-shard chunks from the host and copies only the rest back; with a host
+/// stage and `out` in pinned memory it also reads the device's input from
+/// `out` (the call holds `&mut out` for its whole duration, so that is safe).
 #[allow(clippy::too_many_arguments)]
 pub fn encode_host_batch(format: u8, pubkey: &[u8], input: &[u8], n: usize, count: usize, in_stride: usize,
                          out: &mut [u8], out_stride: usize, hashes: &mut [u8], infos: Option<&mut [ChipEncodeInfo]>,
