@@ -904,6 +904,10 @@ struct ChunkAssembler {
 
 }  // namespace
 
+// window halves: snap_block's compression scratch, then one block's frame piece
+static_assert(SNAP_ECIES_WINDOW / 2 >= MAX_COMPRESS_BLOCK && SNAP_ECIES_WINDOW / 2 >= 8 + MAX_BLOCK,
+              "SNAP_ECIES_WINDOW too small");
+
 int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                          const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
                          uint8_t *window, const ChunkSink *sink, uint64_t *filled) {
