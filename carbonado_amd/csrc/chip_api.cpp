@@ -2665,7 +2665,9 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
                 CHIP_HIP(hipMemcpyAsync(d_hash, hashes + 32 * o, 32 * gcnt, hipMemcpyHostToDevice, sl.stream));
                 CHIP_HIP(hipMemsetAsync(d_st, 0, 4 * gcnt, sl.stream));
                 uint8_t *d_mid = static_cast<uint8_t *>(sl.mid.p) + j0 * m_al;
-                CHIP_HIP(bao_decode_dev(d_in, i_al, blen, gcnt, d_hash, d_mid, m_al, d_st, sl.scratch.p, sl.stream));
+                // every byte verified; only the bytes zfec keeps (the data shards) written
+                CHIP_HIP(bao_decode_prefix_dev(d_in, i_al, blen, gcnt, d_hash, d_mid, m_al, zfec ? olen : blen, d_st,
+                                               sl.scratch.p, sl.stream));
                 CHIP_HIP(hipMemcpyAsync(h_st + j0, d_st, 4 * gcnt, hipMemcpyDeviceToHost, sl.stream));
                 d_res = d_mid;
                 res_pitch = m_al;
