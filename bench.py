@@ -125,6 +125,9 @@ def parse(argv=None):
                          "object 0 only")
     ap.add_argument("--no-aliased", action="store_true",
                     help="encode mode: skip the second, in-place (aliased data shards) measurement")
+    ap.add_argument("--no-box-ceiling", action="store_true",
+                    help="encode mode: skip the box-ceiling diagnostic (the same memory pattern without the GF "
+                         "arithmetic, with GPU clocks and partition modes), run after the checks")
     ap.add_argument("--scatter", action="store_true",
                     help="N>1: rank 0 generates every object and scatters them over RCCL/xGMI (timed "
                          "separately, outside `value`)")
@@ -156,7 +159,8 @@ def parse(argv=None):
         args.objects = 64  # host-API paths: a bounded host-memory working set
     if args.mode == "file" and args.objects == ap.get_default("objects"):
         args.objects = 128  # 2 GiB of input files + 2.1 GiB of output files on the box's disk
-    if args.mode not in ("encode", "decode", "e2e", "bao", "bao-decode"):
+    if args.mode not in ("encode", "decode", "e2e", "bao", "bao-decode", "pipeline-decode", "e2e-decode", "scrub",
+                         "scrub-batch", "file"):
         args.no_verify_all = True
     return args
 
@@ -177,6 +181,25 @@ def spawn_ranks(n: int) -> int:
     rcs = [p.wait() for p in procs]
     bad = [rc for rc in rcs if rc != 0]
     return bad[0] if bad else 0
+
+
+def visible_gpus_no_hip() -> int:
+    """GPUs this process may use, counted without initialising HIP (a rank
+    decides whether to profile itself before it touches the GPU: torch's
+    device_count can fall back to hipGetDeviceCount): the visibility
+    variable if set, else the KFD topology's GPU nodes (simd_count > 0)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip():
+            return len([x for x in v.split(",") if x.strip()])
+    gpus = 0
+    for props in Path("/sys/class/kfd/kfd/topology/nodes").glob("*/properties"):
+        try:
+            kv = dict(line.split()[:2] for line in props.read_text().splitlines() if len(line.split()) >= 2)
+        except OSError:
+            continue
+        gpus += int(kv.get("simd_count", "0")) > 0
+    return gpus
 
 
 def setup_dist(args):
@@ -302,7 +325,7 @@ def live_traffic(args, argv: list, timeout_s: float = 240.0, local_rank: int | N
     steps = 2
     child = [sys.executable, str(Path(__file__).resolve())] + list(argv) + [
         "--steps", str(steps), "--warmup", "1", "--live-pmc", "off", "--no-cpu-baseline", "--no-verify",
-        "--no-verify-all", "--no-aliased", "--traffic-json", "none", "--gpus", "1"]
+        "--no-verify-all", "--no-aliased", "--no-box-ceiling", "--traffic-json", "none", "--gpus", "1"]
     tmp = Path(tempfile.mkdtemp(prefix="chip_pmc_", dir="/tmp"))
     env = child_env(local_rank)
     vals, name = {}, None
@@ -441,6 +464,77 @@ PCIE_MEASURED_GBS = {"h2d": 55.6, "d2h": 55.0}
 # both directions at once: two pinned 16 MiB-piece copy streams side by side
 # (tools/h2d_probe.py, profiles/r9q_session/h2d_probe.log: 47.1 GB/s each way)
 PCIE_MEASURED_DUPLEX_GBS = 94.2
+
+
+class ClockSampler:
+    """The GPU's current SCLK / MCLK / FCLK (the `*` level of sysfs
+    pp_dpm_*) sampled every 10 ms on a host thread between start() and
+    stop(), plus its compute / memory partition modes, read from the PCI
+    device directory the library reports (chip_host_topology's gpu_pci).
+    Diagnostic only: anything unreadable is reported as such."""
+
+    FILES = ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk")
+
+    def __init__(self, dev):
+        import threading
+        self.base, self.err = None, None
+        try:
+            from carbonado_amd import device
+            pci = device.host_topology().get("gpu_pci")
+            if pci and Path(f"/sys/bus/pci/devices/{pci}").is_dir():
+                self.base = Path(f"/sys/bus/pci/devices/{pci}")
+            else:
+                self.err = f"no sysfs directory for gpu_pci={pci!r}"
+        except Exception as e:  # diagnostic only
+            self.err = f"{type(e).__name__}: {e}"[:200]
+        self.samples = {f: [] for f in self.FILES}
+        self.stop_ev = threading.Event()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    @staticmethod
+    def current_mhz(text: str):
+        for line in text.splitlines():
+            if line.rstrip().endswith("*"):
+                for tok in line.split():
+                    if tok.lower().endswith("mhz"):
+                        try:
+                            return int(float(tok[:-3]))
+                        except ValueError:
+                            return None
+        return None
+
+    def _read(self, name: str):
+        try:
+            return (self.base / name).read_text()
+        except OSError:
+            return None
+
+    def _run(self):
+        while not self.stop_ev.is_set():
+            for f in self.FILES:
+                t = self._read(f)
+                v = self.current_mhz(t) if t else None
+                if v is not None:
+                    self.samples[f].append(v)
+            self.stop_ev.wait(0.01)
+
+    def start(self):
+        if self.base is not None:
+            self.thread.start()
+
+    def stop(self) -> dict:
+        if self.base is None:
+            return {"unavailable": self.err}
+        self.stop_ev.set()
+        self.thread.join()
+        out = {"sysfs": str(self.base)}
+        for f in self.FILES:
+            s = self.samples[f]
+            out[f[7:] + "_MHz"] = {"min": min(s), "max": max(s), "samples": len(s)} if s else None
+        for f in ("current_compute_partition", "current_memory_partition"):
+            t = self._read(f)
+            out[f.replace("current_", "")] = t.strip() if t else None
+        return out
 
 
 def bao_data_region_len(N: int) -> int:
@@ -823,8 +917,9 @@ class Workload:
             self.h_out = torch.empty((count, n + 1024), dtype=torch.uint8, pin_memory=True)
 
             def step():
-                device.decode_host_batch(lv, self.h_enc, self.enc_len, self.h_hash, self.pads, self.h_out,
-                                         secret_key=self.sk, nslots=slots, host_threads=args.host_threads)
+                self.dec_len, self.dec_status = device.decode_host_batch(
+                    lv, self.h_enc, self.enc_len, self.h_hash, self.pads, self.h_out, secret_key=self.sk,
+                    nslots=slots, host_threads=args.host_threads)
             self.step = step
             step()
             self.alg_bytes = count * (max(self.enc_len) + n)  # PCIe bytes: H2D encoding + D2H content
@@ -980,8 +1075,12 @@ class Workload:
             return self._verify_all_decode()
         if self.args.mode == "e2e":
             return self._verify_all_e2e(threads)
-        if self.args.mode == "bao-decode":
+        if self.args.mode in ("bao-decode", "pipeline-decode"):
             return self._verify_all_bao_decode()
+        if self.args.mode == "e2e-decode":
+            return self._verify_all_e2e_decode(threads)
+        if self.args.mode in ("scrub", "scrub-batch", "file"):
+            return self._verify_all_repaired(threads)
         from concurrent.futures import ThreadPoolExecutor
         from carbonado_amd import device
         from oracle import oracle as O
@@ -1034,9 +1133,11 @@ class Workload:
                 "how": "every decoded object's n bytes vs its resident input, compared on the device"}
 
     def _verify_all_bao_decode(self):
-        """decoding::bao of every object (decoding.rs:53-60): every status is
-        0 (every node verified) and every decoded content equals the object's
-        resident input, compared on the device 64 objects at a time."""
+        """decoding::bao of every object (decoding.rs:53-60), or decode() at a
+        device-only level (decoding.rs:80-114) for pipeline-decode: every
+        status is 0 (every node verified) and every decoded content equals
+        the object's resident input, compared on the device 64 objects at a
+        time."""
         t0 = time.perf_counter()
         n, bad = self.n, []
         st = self.status.cpu().tolist()
@@ -1049,6 +1150,67 @@ class Workload:
         return {"ok": not bad and not bad_status, "objects": self.count, "mismatched": bad[:16],
                 "bad_status": bad_status[:16], "seconds": round(time.perf_counter() - t0, 1),
                 "how": "every object's status == 0 and its decoded content vs its resident input, on the device"}
+
+    def _verify_all_e2e_decode(self, threads: int):
+        """decode() of every object from host memory (decoding.rs:80-114):
+        every status is 0, every decoded length is n and every decoded
+        object's bytes equal its input (pinned host memory, compared on
+        `threads` host threads; numpy releases the GIL)."""
+        from concurrent.futures import ThreadPoolExecutor
+        import numpy as np
+        t0 = time.perf_counter()
+        n, got, want = self.n, self.h_out.numpy(), self.inp.numpy()
+        bad_status = [o for o, v in enumerate(self.dec_status) if v != 0]
+
+        def check(o):
+            return self.dec_len[o] == n and np.array_equal(got[o, :n], want[o])
+        with ThreadPoolExecutor(threads) as ex:
+            oks = list(ex.map(check, range(self.count)))
+        bad = [o for o, ok in enumerate(oks) if not ok]
+        return {"ok": not bad and not bad_status, "objects": self.count, "mismatched": bad[:16],
+                "bad_status": bad_status[:16], "seconds": round(time.perf_counter() - t0, 1),
+                "how": f"every object's status == 0, decoded length == n and decoded bytes (host memory) vs its "
+                       f"input, on {threads} threads"}
+
+    def _verify_all_repaired(self, threads: int):
+        """scrub() (decoding.rs:159-212) and file::decode (file.rs:395-440)
+        of every object: scrub — every repaired stream equals the intact
+        encoding and every status is what the damage calls for; file — every
+        written file decodes (header signature checked, the device decode
+        path) back to its input."""
+        t0 = time.perf_counter()
+        mode = self.args.mode
+        if mode == "scrub":
+            bad = [o for o in range(self.count) if self.fixed[o] != self.encs[o]]
+            how = "every object's scrub() output vs its intact level-12 encoding (host API)"
+            return {"ok": not bad, "objects": self.count, "mismatched": bad[:16],
+                    "seconds": round(time.perf_counter() - t0, 1), "how": how}
+        if mode == "scrub-batch":
+            st = self.scrub_status
+            want = [0 if o in self.orig else 12 for o in range(self.count)]
+            bad_status = [o for o in range(self.count) if st is None or st[o] != want[o]]
+            bad = [o for o in self.orig if not torch.equal(self.out[o, :self.blen], self.orig[o])]
+            return {"ok": not bad and not bad_status, "objects": self.count, "repaired": len(self.orig),
+                    "mismatched": bad[:16], "bad_status": bad_status[:16],
+                    "seconds": round(time.perf_counter() - t0, 1),
+                    "how": "every object's status (damaged: 0 = repaired, intact: 12 = UnnecessaryScrub) and every "
+                           "repaired stream vs its pre-damage bytes, on the device"}
+        from concurrent.futures import ThreadPoolExecutor
+        from carbonado_amd import file as cfile
+        host = self.inp.numpy()
+
+        def check(o):
+            path, info = self.results[o]
+            hdr, back = cfile.decode(self.sk, path.read_bytes())
+            return (back == host[o].tobytes() and hdr.format == self.args.level and
+                    hdr.encoded_len == info.output_len)
+        with ThreadPoolExecutor(min(threads, 4)) as ex:
+            oks = list(ex.map(check, range(self.count)))
+        bad = [o for o, ok in enumerate(oks) if not ok]
+        return {"ok": not bad, "objects": self.count, "mismatched": bad[:16],
+                "seconds": round(time.perf_counter() - t0, 1),
+                "how": f"every written file read back, file::decode (header + signature + decode() on the device) "
+                       f"vs its input, on {min(threads, 4)} threads"}
 
     def _verify_all_e2e(self, threads: int):
         """encode() of every object (encoding.rs:86-172) against the C oracle
@@ -1093,6 +1255,38 @@ class Workload:
         ok = self.out[0].cpu().numpy().tobytes() == O.zfec_encode(self.inp[0].cpu().numpy().tobytes(), k, m)[0]
         return el, ms, ok
 
+    def box_ceiling(self, reps: int = 5) -> dict:
+        """What this box's HBM gives the headline's access pattern on the
+        same buffers: chip_hbm_pattern_batch_dev (the encode's loads, stores,
+        grid and run queue, no GF arithmetic) timed with HIP events, one
+        warm-up + `reps` launches, outside the timed region and after every
+        check (it overwrites the output).  GPU clocks and partition modes are
+        sampled from sysfs while it runs."""
+        from carbonado_amd import device
+        n, k, m = self.n, self.k, self.m
+        launch = lambda: device.hbm_pattern_batch(self.inp_full, n, self.out, k, m)  # noqa: E731
+        launch()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        sampler = ClockSampler(self.dev)
+        sampler.start()
+        ms = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            launch()
+            b.record(stream)
+            b.synchronize()
+            ms.append(a.elapsed_time(b))
+        clocks = sampler.stop()
+        ms.sort()
+        med = ms[len(ms) // 2]
+        ach = self.alg_bytes / (med * 1e-3) / 1e9
+        return {"GBps": round(ach, 1), "frac_of_peak": round(ach / HBM_PEAK_GBS, 4), "median_ms": round(med, 4),
+                "min_ms": round(ms[0], 4), "launches": reps, "clocks": clocks,
+                "how": f"chip_hbm_pattern_batch_dev: the encode's {k}-read/{m}-write pattern on the same buffers, "
+                       f"grid and run queue without the GF arithmetic, HIP events, median of {reps}"}
+
     def verify_object0(self):
         from oracle import oracle as O
         sample = self.inp[0].cpu().numpy().tobytes()
@@ -1136,10 +1330,10 @@ class Workload:
         elif self.args.mode == "e2e-decode":
             ok = self.h_out[0, :self.n].numpy().tobytes() == sample
         elif self.args.mode == "pipeline-decode":
-            # every object: status 0 and the decoded bytes equal the input (on the device);
-            # object 0's encoding is the oracle's encode()
+            # object 0: status 0, decoded bytes equal the input, and its encoding is the
+            # oracle's encode() (every object's status and bytes: verified_all_objects)
             enc, h, _ = O.encode(sample, self.args.level)
-            ok = (bool((self.status == 0).all()) and torch.equal(self.out[:, :self.n], self.inp[:, :self.n]) and
+            ok = (int(self.status[0]) == 0 and torch.equal(self.out[0, :self.n], self.inp[0, :self.n]) and
                   self.enc[0, :self.blen].cpu().numpy().tobytes() == enc)
         elif self.args.mode == "file":
             from carbonado_amd import file as cfile
@@ -1192,6 +1386,14 @@ class DryRun:
         self.scatter_s = None
         self.alloc_info = {"in": {"classes_found": 0, "classes_used": 0, "alloc_s": 0.0, "rank": rank}}
 
+    def box_ceiling(self, reps: int = 5) -> dict:
+        """The box-ceiling record's keys with placeholder timings (no device)."""
+        sampler = ClockSampler(None)
+        sampler.start()
+        clocks = sampler.stop()
+        return {"GBps": 6000.0, "frac_of_peak": 0.75, "median_ms": 1.0, "min_ms": 1.0, "launches": reps,
+                "clocks": clocks, "how": "dry run: placeholder timings, no device"}
+
     def time_steps(self, steps: int, warmup: int, world: int):
         barrier(world)
         t0 = time.perf_counter()
@@ -1216,7 +1418,7 @@ def main():
         # parallel (a rehearsal with several ranks on one GPU skips it: they would share it)
         if world == 1:
             live = live_traffic(args, sys.argv[1:])
-        elif torch.cuda.device_count() >= world:
+        elif visible_gpus_no_hip() >= world:
             live = live_traffic(args, sys.argv[1:], timeout_s=150.0, local_rank=local)
     wl = DryRun(args, rank) if args.dry_run else Workload(args, rank, local, world)
     scatter = None
@@ -1249,7 +1451,8 @@ def main():
     if rank == 0 and not args.no_verify and not args.dry_run:
         verified, sample = wl.verify_object0()
     verified_all = None
-    want_all = ((args.mode in ("encode", "decode", "e2e", "bao", "bao-decode") and not args.no_verify_all) or
+    want_all = ((args.mode in ("encode", "decode", "e2e", "bao", "bao-decode", "pipeline-decode", "e2e-decode",
+                               "scrub", "scrub-batch", "file") and not args.no_verify_all) or
                 (args.mode == "pipeline" and args.verify_all))
     if want_all and not args.no_verify and not args.dry_run:
         # every rank checks its own objects (N > 1: the whole global set), rank 0 reports;
@@ -1264,10 +1467,25 @@ def main():
                             "seconds_max": max(v["seconds"] for v in every), "how": mine["how"] + ", on every rank"}
         else:
             verified_all = mine
+    if args.mode == "hasher" and verified is not None:
+        # one stream over every object's bytes: the object-0 check above is already the whole input
+        verified_all = {"ok": bool(verified), "objects": args.objects,
+                        "how": "the hasher's one digest over all objects' bytes (4 MiB appends) vs the oracle's "
+                               "BLAKE3 of the same bytes"}
     aliased = None
     if args.mode == "encode" and not args.dry_run and not args.no_aliased:
         a_el, a_ms, a_ok = wl.time_aliased(args.steps, args.warmup, world)
         aliased = (max_over_ranks(a_el), a_ms, a_ok)
+    box = None
+    if args.mode == "encode" and not args.no_box_ceiling and (args.k, args.m) in ((4, 8), (8, 16)):
+        try:  # diagnostic, after the checks (it overwrites the outputs); every rank on its own GPU
+            box = wl.box_ceiling()
+        except Exception as e:
+            box = {"error": f"{type(e).__name__}: {e}"[:300]}
+        if world > 1:
+            every = [None] * world
+            dist.all_gather_object(every, box.get("GBps"))
+            box["GBps_by_rank"] = every
 
     if rank == 0:
         k, m = args.k, args.m
@@ -1406,6 +1624,11 @@ def main():
             res["verify_threads_per_rank"] = verify_threads(world)
         if verified_all is not None:
             res["verified_all_objects"] = verified_all
+        if box is not None:
+            res["box_ceiling"] = box
+            if box.get("GBps"):
+                res["roofline"]["box_ceiling_GBps"] = box["GBps"]
+                res["roofline"]["frac_of_box_ceiling"] = round(achieved / box["GBps"], 4)
         if aliased is not None:
             a_max, a_ms, a_ok = aliased
             a_bytes = args.objects * (n + (m - k) * wl.C)

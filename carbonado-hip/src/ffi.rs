@@ -1,4 +1,4 @@
-//! Raw bindings of `include/carbonado_hip.h` (ABI 4), one declaration per
+//! Raw bindings of `include/carbonado_hip.h` (ABI 5), one declaration per
 //! `CHIP_API` prototype, in the header's order.  Kept in lock-step with the
 //! header by `tests/test_rust_shim.py` (name, arity, C <-> Rust type of every
 //! parameter and return value, struct layouts, constants).
@@ -10,7 +10,7 @@
 
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const CHIP_ABI_VERSION: c_int = 4;
+pub const CHIP_ABI_VERSION: c_int = 5;
 pub const CHIP_HASH_LEN: usize = 32; // bao::HASH_SIZE
 pub const CHIP_SLICE_LEN: usize = 1024; // constants.rs:9 SLICE_LEN
 pub const CHIP_FEC_K: u32 = 4; // constants.rs:11 FEC_K
@@ -183,6 +183,8 @@ extern "C" {
     // ---- device-resident batch API (the throughput path)
     pub fn chip_zfec_encode_batch_dev(k: u32, m: u32, d_in: *const u8, in_stride: u64, n: u64, count: u64,
                                       d_out: *mut u8, out_stride: u64, stream: *mut c_void) -> c_int;
+    pub fn chip_hbm_pattern_batch_dev(k: u32, m: u32, d_in: *const u8, in_stride: u64, n: u64, count: u64,
+                                      d_out: *mut u8, out_stride: u64, stream: *mut c_void) -> c_int;
     pub fn chip_zfec_decode_batch_dev(k: u32, m: u32, d_in: *const u8, in_stride: u64, chunk_len: u64,
                                       idx: *const u32, nshares: u32, count: u64, d_out: *mut u8,
                                       out_stride: u64, stream: *mut c_void) -> c_int;
@@ -224,6 +226,8 @@ extern "C" {
     pub fn chip_bao_hasher_read_all(h: *mut chip_bao_hasher, out: *mut u8, out_cap: u64, out_len: *mut u64)
         -> c_int;
     pub fn chip_bao_hasher_free(h: *mut chip_bao_hasher);
+    pub fn chip_bao_hasher_drop_cache() -> u64;
+    pub fn chip_bao_hasher_cached_bytes() -> u64;
 
     // ---- host-memory batch (host -> HBM -> host)
     pub fn chip_encode_host_batch(format: u8, pubkey: *const u8, pubkey_len: u64, inject: *const chip_ecies_inject,

@@ -505,6 +505,17 @@ impl Drop for BaoHasher {
     }
 }
 
+/// Destroy every parked (freed, kept for reuse) hasher; returns the device
+/// bytes freed.  Parked hashers hold at most CHIP_HASHER_PARK_MIB (3 GiB).
+pub fn drop_hasher_cache() -> u64 {
+    unsafe { ffi::chip_bao_hasher_drop_cache() }
+}
+
+/// Device bytes the parked hashers hold.
+pub fn hasher_cached_bytes() -> u64 {
+    unsafe { ffi::chip_bao_hasher_cached_bytes() }
+}
+
 /// Where this process's host-copy path sits on the box (JSON): the GPU's
 /// NUMA node, the staging ring's node, the copy workers' nodes (diagnostic).
 pub fn host_topology() -> Result<String> {
@@ -520,12 +531,26 @@ pub fn host_topology() -> Result<String> {
 // ---- device-resident batch API ----------------------------------------------
 
 /// A HIP stream handle (`hipStream_t`); [`Stream::DEFAULT`] = the library's
-/// per-thread stream.  The batch calls enqueue on it and return.
+/// per-thread stream.  The batch calls enqueue on it and return.  The handle
+/// is private: safe code gets only [`Stream::DEFAULT`]; a caller's own stream
+/// comes in through [`Stream::from_raw`], whose caller vouches for it.
 #[derive(Clone, Copy, Debug)]
-pub struct Stream(pub *mut c_void);
+pub struct Stream(*mut c_void);
 
 impl Stream {
     pub const DEFAULT: Stream = Stream(ptr::null_mut());
+
+    /// # Safety
+    /// `raw` must be a live `hipStream_t` of the device the library runs on,
+    /// and stay alive until the work enqueued on it through this handle has
+    /// finished.
+    pub unsafe fn from_raw(raw: *mut c_void) -> Stream {
+        Stream(raw)
+    }
+
+    pub fn as_raw(&self) -> *mut c_void {
+        self.0
+    }
 }
 
 unsafe impl Send for Stream {}

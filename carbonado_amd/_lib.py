@@ -126,6 +126,9 @@ SIGNATURES = {
     "chip_zfec_encode_batch_dev": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
                                                   ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "chip_hbm_pattern_batch_dev": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                                  ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "chip_zfec_decode_batch_dev": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
                                                   ctypes.c_uint64, ctypes.c_uint64, c_u32p, ctypes.c_uint32,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
@@ -166,6 +169,8 @@ SIGNATURES = {
     "chip_bao_hasher_len": (ctypes.c_uint64, [ctypes.c_void_p]),
     "chip_bao_hasher_read_all": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, c_u64p]),
     "chip_bao_hasher_free": (None, [ctypes.c_void_p]),
+    "chip_bao_hasher_drop_cache": (ctypes.c_uint64, []),
+    "chip_bao_hasher_cached_bytes": (ctypes.c_uint64, []),
     "chip_decode_host_batch": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                               ctypes.c_void_p, c_u64p, ctypes.c_uint64, ctypes.c_uint64, c_u32p,
                                               ctypes.c_void_p, ctypes.c_uint64, c_u64p,

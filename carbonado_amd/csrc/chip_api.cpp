@@ -1173,6 +1173,27 @@ int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint
     return CHIP_OK;
 }
 
+int chip_hbm_pattern_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride, uint64_t n,
+                               uint64_t count, uint8_t *d_out, uint64_t out_stride, void *stream) {
+    if (!((k == 4 && m == 8) || (k == 8 && m == 16))) return CHIP_ERR_ZFEC;
+    if ((!d_in && n) || !d_out || d_in == d_out || (in_stride % 16) || (out_stride % 16) || misaligned16(d_in) ||
+        misaligned16(d_out))
+        return CHIP_ERR_INVALID_ARG;
+    int st = use_device();
+    if (st != CHIP_OK) return st;
+    uint32_t pad;
+    uint64_t C;
+    calc_pad(n, k, &pad, &C);
+    if (count > 1 && (out_stride < (uint64_t)m * C || in_stride < n)) return CHIP_ERR_INVALID_ARG;
+    GfPlan p = encode_plan(k, m, C, zfec_enc_matrix(k, m), false);
+    CHIP_HIP(zf_run(count, static_cast<hipStream_t>(stream), [&](uint64_t o0, uint64_t cnt, hipStream_t s) {
+        GfLaunch L{d_in + o0 * in_stride, d_out + o0 * out_stride, in_stride, out_stride, n, C, cnt};
+        L.pattern_only = true;
+        return gf_apply(p, L, s);
+    }));
+    return CHIP_OK;
+}
+
 int chip_zfec_encode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t n, uint8_t *out,
                      uint64_t out_cap, uint32_t *padding, uint32_t *chunk_len) {
     if (!valid_km(k, m)) return CHIP_ERR_ZFEC;
@@ -2666,8 +2687,14 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
                 CHIP_HIP(hipMemsetAsync(d_st, 0, 4 * gcnt, sl.stream));
                 uint8_t *d_mid = static_cast<uint8_t *>(sl.mid.p) + j0 * m_al;
                 // every byte verified; only the bytes zfec keeps (the data shards) written
-                CHIP_HIP(bao_decode_prefix_dev(d_in, i_al, blen, gcnt, d_hash, d_mid, m_al, zfec ? olen : blen, d_st,
-                                               sl.scratch.p, sl.stream));
+                // (CHIP_DECODE_PREFIX=0: round 4's whole-content verify-decode, the A/B of DESIGN §6)
+                static const bool prefix = env_int("CHIP_DECODE_PREFIX", 1) != 0;
+                if (prefix)
+                    CHIP_HIP(bao_decode_prefix_dev(d_in, i_al, blen, gcnt, d_hash, d_mid, m_al, zfec ? olen : blen,
+                                                   d_st, sl.scratch.p, sl.stream));
+                else
+                    CHIP_HIP(bao_decode_dev(d_in, i_al, blen, gcnt, d_hash, d_mid, m_al, d_st, sl.scratch.p,
+                                            sl.stream));
                 CHIP_HIP(hipMemcpyAsync(h_st + j0, d_st, 4 * gcnt, hipMemcpyDeviceToHost, sl.stream));
                 d_res = d_mid;
                 res_pitch = m_al;
@@ -2871,7 +2898,7 @@ struct chip_bao_hasher {
     // device sync per growth); va_* says which of them live there
     chip::hbm::Growable gcontent, gcv0;
     bool va_content = false, va_cv0 = false;
-    uint64_t va_content_bytes = 0;  // content VA reserved (16 GiB; CHIP_HASHER_VA_MIB at creation, tests)
+    uint64_t va_content_bytes = 0;  // first content VA reservation (1 GiB; CHIP_HASHER_VA_MIB at creation)
     int dev = -1;                   // device its streams and buffers live on
     uint64_t len = 0, enc_len = 0;
     uint64_t units = 0;  // 64-chunk units whose chunk CVs are in cv0
@@ -2891,13 +2918,59 @@ uint64_t hasher_batch_units() {
     return u;
 }
 
-// One freed hasher is kept, emptied, with its two streams, its event and its
-// grown buffers, and handed to the next chip_bao_hasher_new on the same
+// Freed hashers are kept, emptied, with their two streams, their event and
+// their grown buffers, and handed to the next chip_bao_hasher_new on the same
 // device: stream creation and destruction, a GiB of hipMalloc / hipFree and
 // the in-place buffers' mappings cost milliseconds per hasher otherwise (a
-// mapped VA range is reused as is, never remapped).  CHIP_HASHER_CACHE=0: off.
+// mapped VA range is reused as is, never remapped).  Bounded: at most
+// HASHER_PARK_COUNT parked hashers, and their buffers together at most
+// hasher_park_bytes() (CHIP_HASHER_PARK_MIB, 3 GiB by default: the 1 GiB
+// content of the hasher bench, its 1.06 GiB stream and the CV buffers); a
+// hasher that would take the pool past it is parked without its buffers
+// (streams only), so hashing one large file does not keep its HBM for the
+// rest of the process.  chip_bao_hasher_drop_cache frees them all.
+// CHIP_HASHER_CACHE=0: off.
+constexpr size_t HASHER_PARK_COUNT = 4;
 std::mutex g_hasher_spare_mu;
-chip_bao_hasher *g_hasher_spare = nullptr;
+std::vector<chip_bao_hasher *> g_hasher_spares;
+
+uint64_t hasher_park_bytes() {
+    static const uint64_t b = [] {
+        const char *e = std::getenv("CHIP_HASHER_PARK_MIB");
+        return (e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)3072) << 20;
+    }();
+    return b;
+}
+
+// device bytes a hasher holds (mapped VA pieces and plain buffers)
+uint64_t hasher_bytes(const chip_bao_hasher *h) {
+    uint64_t s = (h->va_content ? h->gcontent.mapped : h->content.cap) + (h->va_cv0 ? h->gcv0.mapped : h->cv0.cap);
+    for (const DevBuf *b : {&h->enc, &h->scratch, &h->hash, &h->cv1}) s += b->cap;
+    return s;
+}
+
+// Free every buffer of a hasher whose work is done (its VA ranges retire).
+void hasher_release_buffers(chip_bao_hasher *h) {
+    if (h->va_content) h->gcontent.release();
+    else if (h->content.p) (void)hipFree(h->content.p);
+    if (h->va_cv0) h->gcv0.release();
+    else if (h->cv0.p) (void)hipFree(h->cv0.p);
+    for (DevBuf *b : {&h->enc, &h->scratch, &h->hash, &h->cv1})
+        if (b->p) (void)hipFree(b->p);
+    for (DevBuf *b : {&h->content, &h->cv0, &h->enc, &h->scratch, &h->hash, &h->cv1}) *b = DevBuf{};
+    h->va_content = h->va_cv0 = false;
+}
+
+void hasher_destroy(chip_bao_hasher *h) {
+    hasher_release_buffers(h);
+    if (h->hstream) (void)hipStreamDestroy(h->hstream);
+    if (h->stream) {
+        stream_queue_release(h->stream);
+        (void)hipStreamDestroy(h->stream);
+    }
+    if (h->copied) (void)hipEventDestroy(h->copied);
+    delete h;
+}
 
 bool hasher_cache_on() {
     static const bool on = [] {
@@ -2918,8 +2991,13 @@ bool hasher_va_on() {
 
 hipError_t grow_keep(DevBuf &b, size_t need, size_t used, hipStream_t s);
 
-// VA reserved per hasher: 16 GiB of content in place (its chunk CVs: 1/32)
-constexpr uint64_t HASHER_VA_CONTENT = 16ull << 30, HASHER_VA_CV = 1ull << 30;
+// VA reserved per hasher buffer: the first reservation holds 1 GiB of content
+// (or twice the first growth), its chunk CVs 1 GiB (the arena's unit); a
+// buffer that outgrows its range moves once into a fresh range 4x its need
+// (one device copy of the bytes so far, ~0.4 ms per GiB).  A range is never
+// mapped twice (hbm_alloc.hpp), so a released hasher retires its ranges: VA
+// spent grows with the bytes hashed (at most ~5x), not a flat 17 GiB each.
+constexpr uint64_t HASHER_VA_CONTENT = 1ull << 30, HASHER_VA_CV = 1ull << 30;
 uint64_t hasher_va_content() {
     const char *e = std::getenv("CHIP_HASHER_VA_MIB");
     const uint64_t mib = e ? std::strtoull(e, nullptr, 10) : 0;
@@ -2927,15 +3005,15 @@ uint64_t hasher_va_content() {
 }
 
 // Grow a hasher buffer to `need` bytes keeping its first `used`: in place
-// behind its reserved VA range (hbm::Growable) when it lives there, else by
-// copying into a larger allocation after `wait_s` (whose kernels read the old
-// buffer) is idle.  A buffer that outgrows its VA range moves to a plain
-// allocation once.
+// behind its reserved VA range (hbm::Growable) when it lives there; past the
+// range, into a fresh range 4x the need (one copy after `wait_s`, whose
+// kernels read the old buffer, is idle); without the VA API (or
+// CHIP_HASHER_VA=0), by copying into a larger plain allocation.
 hipError_t hasher_grow(DevBuf &b, chip::hbm::Growable &g, bool &in_va, size_t need, size_t used, hipStream_t copy_s,
                        hipStream_t wait_s, uint64_t reserve) {
     if (b.cap >= need) return hipSuccess;
     if ((in_va || !b.p) && hasher_va_on()) {
-        hipError_t e = g.grow(need, reserve);
+        hipError_t e = g.grow(need, std::max<uint64_t>(reserve, 2 * (uint64_t)need));
         if (e == hipSuccess) {
             b.p = g.va;
             b.cap = g.mapped;
@@ -2943,11 +3021,30 @@ hipError_t hasher_grow(DevBuf &b, chip::hbm::Growable &g, bool &in_va, size_t ne
             return hipSuccess;
         }
         (void)hipGetLastError();
+        if (!in_va) {
+            g.release();  // a first growth that failed part way: its pieces and range go
+        } else {
+            chip::hbm::Growable ng;  // past the range: a fresh one, 4x the need
+            e = ng.grow(need, 4 * (uint64_t)need);
+            if (e == hipSuccess) e = hipStreamSynchronize(wait_s);
+            if (e == hipSuccess && used) e = hipMemcpyAsync(ng.va, b.p, used, hipMemcpyDeviceToDevice, copy_s);
+            if (e == hipSuccess) e = hipStreamSynchronize(copy_s);
+            if (e == hipSuccess) {
+                g.release();
+                g = std::move(ng);
+                b.p = g.va;
+                b.cap = g.mapped;
+                return hipSuccess;
+            }
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(copy_s);
+            ng.release();
+        }
     }
     hipError_t e = hipStreamSynchronize(wait_s);
     if (e != hipSuccess) return e;
     if (!in_va) return grow_keep(b, need, used, copy_s);
-    DevBuf nb;  // out of the VA range: one copy into plain memory
+    DevBuf nb;  // no fresh range to be had: one copy into plain memory
     if ((e = grow_keep(nb, std::max(need, 2 * (size_t)g.mapped), 0, copy_s)) != hipSuccess) return e;
     if (used && (e = hipMemcpyAsync(nb.p, b.p, used, hipMemcpyDeviceToDevice, copy_s)) == hipSuccess)
         e = hipStreamSynchronize(copy_s);
@@ -2993,13 +3090,15 @@ int chip_bao_hasher_new(chip_bao_hasher **out) {
     Ctx *c;
     int st = ctx_get(&c);  // device check + hipSetDevice
     if (st != CHIP_OK) return st;
-    {  // the last freed hasher's streams and grown buffers, if it lived on this device
+    {  // the most recently freed hasher's streams and grown buffers that lived on this device
         std::lock_guard<std::mutex> lk(g_hasher_spare_mu);
-        if (g_hasher_spare && g_hasher_spare->dev == c->dev &&
-            g_hasher_spare->va_content_bytes == hasher_va_content()) {
-            *out = g_hasher_spare;
-            g_hasher_spare = nullptr;
-            return CHIP_OK;
+        for (size_t i = g_hasher_spares.size(); i-- > 0;) {
+            chip_bao_hasher *s = g_hasher_spares[i];
+            if (s->dev == c->dev && s->va_content_bytes == hasher_va_content()) {
+                g_hasher_spares.erase(g_hasher_spares.begin() + (std::ptrdiff_t)i);
+                *out = s;
+                return CHIP_OK;
+            }
         }
     }
     auto *h = new chip_bao_hasher();
@@ -3128,28 +3227,42 @@ void chip_bao_hasher_free(chip_bao_hasher *h) {
         if (h->stream) (void)hipStreamSynchronize(h->stream);
         if (hasher_cache_on()) {  // park it, emptied, for the next chip_bao_hasher_new
             std::lock_guard<std::mutex> sk(g_hasher_spare_mu);
-            if (!g_hasher_spare) {
+            if (g_hasher_spares.size() < HASHER_PARK_COUNT) {
+                uint64_t parked = 0;
+                for (const chip_bao_hasher *s : g_hasher_spares) parked += hasher_bytes(s);
+                if (parked + hasher_bytes(h) > hasher_park_bytes()) hasher_release_buffers(h);  // streams only
                 h->len = h->enc_len = h->units = 0;
                 h->finalized = false;
                 std::memset(h->h, 0, sizeof h->h);
-                g_hasher_spare = h;
+                g_hasher_spares.push_back(h);
                 return;
             }
         }
-        if (h->va_content) h->gcontent.release();
-        else if (h->content.p) (void)hipFree(h->content.p);
-        if (h->va_cv0) h->gcv0.release();
-        else if (h->cv0.p) (void)hipFree(h->cv0.p);
-        for (DevBuf *b : {&h->enc, &h->scratch, &h->hash, &h->cv1})
-            if (b->p) (void)hipFree(b->p);
-        if (h->hstream) (void)hipStreamDestroy(h->hstream);
-        if (h->stream) {
-            stream_queue_release(h->stream);
-            (void)hipStreamDestroy(h->stream);
-        }
-        if (h->copied) (void)hipEventDestroy(h->copied);
     }
-    delete h;
+    hasher_destroy(h);
+}
+
+uint64_t chip_bao_hasher_drop_cache(void) {
+    std::vector<chip_bao_hasher *> all;
+    {
+        std::lock_guard<std::mutex> sk(g_hasher_spare_mu);
+        all.swap(g_hasher_spares);
+    }
+    uint64_t freed = 0;
+    for (chip_bao_hasher *h : all) {  // parked hashers: their work was synchronised when they were freed
+        freed += hasher_bytes(h);
+        (void)hipSetDevice(h->dev);
+        hasher_destroy(h);
+    }
+    if (!all.empty()) (void)use_device();
+    return freed;
+}
+
+uint64_t chip_bao_hasher_cached_bytes(void) {
+    std::lock_guard<std::mutex> sk(g_hasher_spare_mu);
+    uint64_t s = 0;
+    for (const chip_bao_hasher *h : g_hasher_spares) s += hasher_bytes(h);
+    return s;
 }
 
 }  // extern "C"

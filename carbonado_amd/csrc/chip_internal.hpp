@@ -57,6 +57,9 @@ struct GfLaunch {
     // optional: at most this many workgroups per CU (0 = occupancy), leaving
     // room for a kernel that runs beside it on another stream
     int wg_per_cu = 0;
+    // diagnostic (chip_hbm_pattern_batch_dev): the same launch with the GF
+    // arithmetic taken out — the bare memory pattern the kernel is priced by
+    bool pattern_only = false;
 };
 
 // Enqueue the matrix apply.  Tables are cached device-side per plan key.

@@ -82,6 +82,73 @@ __global__ __launch_bounds__(TPB) void gf_apply_generic_kernel(GenericArgs a) {
     }
 }
 
+// ---- box ceiling: gf_apply's memory pattern without the arithmetic ----------
+// The same loads (K masked 16-B loads per lane per column tile, shards walked
+// in the lane group's rotated order, super-tiles of U tiles with the next
+// one's loads in flight), the same stores (K copies + NP computed rows, 16 B
+// per lane each, NT as the product), the same run queue, grid and LDS
+// footprint (set by the launch), but every computed row is an XOR of two
+// loads instead of K*16 table lookups.  What this box's HBM gives the
+// headline's access pattern on the caller's buffers: bench.py prices the
+// headline against it (frac_of_box_ceiling) so a slow box explains itself.
+template <int K, int NP, int U, bool NT>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void hbm_pattern_kernel(ApplyArgs a) {
+    constexpr int R = replicas_for(K);
+    const int grp = ((int)threadIdx.x & 31) / R;
+    uint64_t ioff[K], coff[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        ioff[j] = a.in_off[(j + grp) % K];
+        coff[j] = a.copy_off[(j + grp) % K];
+    }
+    const uint64_t spo = (a.tiles_per_obj + U - 1) / U;
+    __shared__ uint32_t q_slot[2];
+    QueueIter<6> iter(spo * a.count, a.chunk, a.queue, q_slot, a.xcd_mask);
+    auto load_tile = [&](uint64_t t, u32x4 (&v)[U][K]) {
+        const uint64_t obj = t / spo;
+        const uint64_t col0 = (t - obj * spo) * (uint64_t)(U * TILE) + threadIdx.x * VEC;
+        const uint8_t *ib = a.in + obj * a.in_stride;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint64_t col = col0 + (uint64_t)u * TILE;
+                v[u][j] = col < a.C ? load16_masked(ib, ioff[j] + col, a.valid) : u32x4{0u, 0u, 0u, 0u};
+            }
+    };
+    uint64_t st;
+    bool have = iter.next(st);
+    u32x4 v[U][K];
+    if (have) load_tile(st, v);
+    while (have) {
+        uint64_t st_next;
+        const bool have_next = iter.next(st_next);
+        u32x4 vn[U][K];
+        if (have_next) load_tile(st_next, vn);
+        const uint64_t obj = st / spo;
+        const uint64_t col0 = (st - obj * spo) * (uint64_t)(U * TILE) + threadIdx.x * VEC;
+        uint8_t *ob = a.out + obj * a.out_stride;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t col = col0 + (uint64_t)u * TILE;
+            if (col >= a.C) continue;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (coff[j] != NO_OUT) store16<NT>(ob + coff[j] + col, v[u][j]);
+#pragma unroll
+            for (int q = 0; q < NP; ++q)
+                if (a.par_off[q] != NO_OUT) store16<NT>(ob + a.par_off[q] + col, v[u][q % K] ^ v[u][(q + 1) % K]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) v[u][j] = vn[u][j];
+        st = st_next;
+        have = have_next;
+    }
+    iter.finish();
+}
+
 // ---- host side ----------------------------------------------------------
 typedef void (*KernelFn)(ApplyArgs);
 
@@ -381,6 +448,12 @@ hipError_t gf_apply_pass(const GfPlan &p, const GfLaunch &L, hipStream_t stream,
     if (bl) {  // wave-level runs of 1 KiB units
         const uint64_t per_wave = (L.C / 1024) * L.count / (4 * (grid ? grid : 1));
         a.chunk = per_wave < 1 ? 1 : (per_wave < ZF_BL_RUN ? per_wave : ZF_BL_RUN);
+    }
+    if (L.pattern_only) {  // the product's grid, run length and LDS footprint; no arithmetic
+        if (bl) return hipErrorInvalidValue;
+        if (p.k == 4 && ng == 1 && ki.u == 2) fn = hbm_pattern_kernel<4, 4, 2, ZF_NT>;
+        else if (p.k == 8 && ng == 2 && ki.u == 1) fn = hbm_pattern_kernel<8, 8, 1, false>;
+        else return hipErrorInvalidValue;
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(TPB), lds, stream, a);
     return hipGetLastError();

@@ -37,6 +37,18 @@ def zfec_encode_batch(inp: torch.Tensor, n: int, out: torch.Tensor, k: int = FEC
                                                 _stream()))
 
 
+def hbm_pattern_batch(inp: torch.Tensor, n: int, out: torch.Tensor, k: int = FEC_K, m: int = FEC_M) -> None:
+    """Diagnostic: zfec_encode_batch's memory pattern (same loads, stores,
+    grid and run queue) without the GF arithmetic — `out` receives XORs of
+    data shards, not parity (chip_hbm_pattern_batch_dev)."""
+    assert inp.is_cuda and out.is_cuda and inp.is_contiguous() and out.is_contiguous()
+    assert inp.shape[0] == out.shape[0] and inp.data_ptr() != out.data_ptr()
+    need = _lib.lib().chip_zfec_encoded_len(n, k, m)
+    assert out.shape[1] >= need and inp.shape[1] >= n
+    check(_lib.lib().chip_hbm_pattern_batch_dev(k, m, _p(inp), inp.shape[1], n, inp.shape[0], _p(out),
+                                                out.shape[1], _stream()))
+
+
 def zfec_decode_batch(enc: torch.Tensor, chunk_len: int, indices, out: torch.Tensor,
                       k: int = FEC_K, m: int = FEC_M) -> None:
     """enc: uint8 [count, >= m*chunk_len] (shard i at i*chunk_len); `indices`

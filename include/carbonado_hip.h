@@ -59,7 +59,7 @@ extern "C" {
 #define CHIP_API
 #endif
 
-#define CHIP_ABI_VERSION 4
+#define CHIP_ABI_VERSION 5
 #define CHIP_HASH_LEN 32   /* bao::HASH_SIZE */
 #define CHIP_SLICE_LEN 1024 /* constants.rs:9 SLICE_LEN */
 #define CHIP_FEC_K 4        /* constants.rs:11 FEC_K */
@@ -321,6 +321,16 @@ CHIP_API int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8
 CHIP_API int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
                                uint64_t n, uint64_t count, uint8_t *d_out, uint64_t out_stride,
                                void *stream);
+/* Diagnostic (ABI 5): the memory pattern of chip_zfec_encode_batch_dev with
+ * the same arguments — the same loads, stores, grid, run queue and LDS
+ * footprint — with the GF(2^8) arithmetic taken out (the parity rows written
+ * are XORs of two data shards, NOT parity).  Its rate is what this box's HBM
+ * gives the encode's access pattern on these buffers: the ceiling the encode
+ * is compared with (bench.py box_ceiling).  (k, m) = (4, 8) or (8, 16);
+ * d_out != d_in; CHIP_ERR_ZFEC for other shapes. */
+CHIP_API int chip_hbm_pattern_batch_dev(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
+                                        uint64_t n, uint64_t count, uint8_t *d_out, uint64_t out_stride,
+                                        void *stream);
 /* Erasure decode of `count` encoded objects (chunk_len-byte shards, shard i of
  * object o at d_in + o*in_stride + i*chunk_len).  idx[0..nshares) names the
  * shares that survive (same pattern for every object); the k*chunk_len data
@@ -441,6 +451,13 @@ CHIP_API int chip_bao_hasher_finalize(chip_bao_hasher *h, uint8_t hash[CHIP_HASH
 CHIP_API uint64_t chip_bao_hasher_len(chip_bao_hasher *h);
 CHIP_API int chip_bao_hasher_read_all(chip_bao_hasher *h, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 CHIP_API void chip_bao_hasher_free(chip_bao_hasher *h);
+/* Freed hashers are parked for reuse by the next chip_bao_hasher_new (their
+ * streams, and their device buffers while all parked buffers together stay
+ * within CHIP_HASHER_PARK_MIB, 3 GiB by default; at most 4 hashers).
+ * drop_cache destroys every parked hasher and returns the device bytes it
+ * freed; cached_bytes reports what the parked hashers hold (ABI 5). */
+CHIP_API uint64_t chip_bao_hasher_drop_cache(void);
+CHIP_API uint64_t chip_bao_hasher_cached_bytes(void);
 
 /* ---- host-memory batch (end-to-end: host -> HBM -> host) -------------- */
 /* encode() for `count` objects of n bytes that live in HOST memory (object o

@@ -41,7 +41,7 @@ def test_library_loads_and_binds_every_symbol():
     L = _lib.lib()
     for name in header_symbols():
         assert getattr(L, name) is not None
-    assert L.chip_abi_version() == 4
+    assert L.chip_abi_version() == 5
     assert L.chip_strerror(3).decode().startswith("Input bytes must divide evenly")
 
 

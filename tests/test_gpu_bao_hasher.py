@@ -163,8 +163,9 @@ def test_hasher_grows_in_place_across_pieces(gpu):
 
 
 def test_hasher_outgrows_its_va_range(gpu, monkeypatch):
-    """A hasher whose content outgrows its reserved VA range (1 GiB here via
-    CHIP_HASHER_VA_MIB, 16 GiB by default) moves once into plain memory and
+    """A hasher whose content outgrows its first VA range (1 GiB:
+    CHIP_HASHER_VA_MIB, the default too; ranges are whole GiB) moves once
+    into a fresh range 4x its need (one device copy of the bytes so far) and
     keeps every byte."""
     from carbonado_amd.utils import BaoHasher
     monkeypatch.setenv("CHIP_HASHER_VA_MIB", "1024")
@@ -197,3 +198,65 @@ def test_hasher_reuses_a_freed_hashers_resources(gpu):
         assert h.read_all() == O.bao_encode(data)[0]
         del h
         gc.collect()
+
+
+def test_freed_large_hasher_does_not_keep_its_hbm(gpu):
+    """a freed hasher is parked for reuse, but the parked buffers
+    are capped (CHIP_HASHER_PARK_MIB, 3 GiB): after hashing 4 GiB (content
+    past its first 1 GiB VA range, moved once into a fresh 4x range) and
+    freeing the hasher, the device holds at most the cap more than before,
+    and drop_cache gives everything back."""
+    import gc
+    import torch
+    from carbonado_amd.utils import BaoHasher
+    L = gpu
+    L.chip_bao_hasher_drop_cache()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    block = np.random.default_rng(61).integers(0, 256, 256 << 20, dtype=np.uint8)
+    h = BaoHasher()
+    for _ in range(16):
+        h.update(block)
+    assert len(h) == 4 << 30
+    digest = h.finalize()
+    assert digest == O.blake3(block.tobytes() * 16)
+    del h
+    gc.collect()
+    cached = L.chip_bao_hasher_cached_bytes()
+    assert cached <= 3 << 30, cached
+    held = free0 - torch.cuda.mem_get_info()[0]
+    assert held <= (3 << 30) + (256 << 20), held
+    L.chip_bao_hasher_drop_cache()
+    assert L.chip_bao_hasher_cached_bytes() == 0
+    held = free0 - torch.cuda.mem_get_info()[0]
+    assert held <= 256 << 20, held
+
+
+def test_many_live_hashers_then_a_class_balanced_buffer(gpu):
+    """every hasher reserves VA for in-place growth and a released
+    range is retired (never mapped twice).  Three rounds of 100 hashers alive
+    at once (300 in all, 4 parked between rounds) reserve about 1 GiB each
+    (was 17 GiB); afterwards chip_device_alloc(1 GiB) still takes the
+    class-balanced path, and every digest is exact."""
+    import gc
+    from carbonado_amd.utils import BaoHasher
+    L = gpu
+    data = np.random.default_rng(67).integers(0, 256, 100_003, dtype=np.uint8)
+    want = O.blake3(data.tobytes())
+    for _ in range(3):
+        hs = [BaoHasher() for _ in range(100)]
+        for h in hs:
+            h.update(data)
+        assert all(h.finalize() == want for h in hs)
+        del hs
+        gc.collect()
+    L.chip_bao_hasher_drop_cache()
+    import ctypes
+    p = ctypes.c_void_p()
+    assert L.chip_device_alloc(1 << 30, ctypes.byref(p)) == 0
+    try:
+        f, u, s = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_double()
+        assert L.chip_device_alloc_info(p, ctypes.byref(f), ctypes.byref(u), ctypes.byref(s)) == 0
+        assert f.value >= 1 and u.value >= 1
+    finally:
+        assert L.chip_device_free(p) == 0

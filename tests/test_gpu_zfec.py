@@ -199,3 +199,35 @@ def test_batch_in_place_aliased_data_shards(gpu, k, m, n):
     got = buf.cpu().numpy()
     for o in range(count):
         assert got[o].tobytes() == O.zfec_encode(host[o].tobytes(), k, m)[0], o
+
+
+@pytest.mark.parametrize("k,m,n", [(4, 8, (1 << 20) + 5), (4, 8, 16 << 20), (8, 16, (1 << 20) + 5)])
+def test_hbm_pattern_probe_writes_its_pattern(gpu, k, m, n):
+    """chip_hbm_pattern_batch_dev (bench.py's box ceiling) runs the encode's
+    memory pattern: data shards copied, computed row q = shard q%k XOR shard
+    (q+1)%k — every output byte written (the same tiles as the encode)."""
+    import torch
+    from carbonado_amd import device
+    count = 3
+    inp = torch.randint(0, 256, (count, n), dtype=torch.uint8, device="cuda")
+    C = gpu.chip_zfec_encoded_len(n, k, m) // m
+    out = torch.full((count, m * C), 0xA5, dtype=torch.uint8, device="cuda")
+    device.hbm_pattern_batch(inp, n, out, k, m)
+    torch.cuda.synchronize()
+    padded = torch.zeros((count, k * C), dtype=torch.uint8, device="cuda")
+    padded[:, :n] = inp
+    sh = padded.view(count, k, C)
+    got = out.view(count, m, C)
+    assert torch.equal(got[:, :k], sh)
+    for q in range(m - k):
+        assert torch.equal(got[:, k + q], sh[:, q % k] ^ sh[:, (q + 1) % k]), q
+
+
+def test_hbm_pattern_probe_refuses_other_shapes(gpu):
+    import torch
+    from carbonado_amd import _lib
+    inp = torch.zeros((1, 4096), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((1, 8192), dtype=torch.uint8, device="cuda")
+    L = _lib.lib()
+    assert L.chip_hbm_pattern_batch_dev(3, 6, inp.data_ptr(), 4096, 4096, 1, out.data_ptr(), 8192, None) == 7
+    assert L.chip_hbm_pattern_batch_dev(4, 8, inp.data_ptr(), 4096, 4096, 1, inp.data_ptr(), 4096, None) == 1

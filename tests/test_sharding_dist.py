@@ -105,6 +105,8 @@ def test_bench_spawns_its_own_ranks_dry_run():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["global_objects"] == 2 * res["config"]["objects_per_gpu"]
     assert len(res["roofline"]["per_rank_avg_launch_ms"]) == 2
+    assert res["box_ceiling"]["GBps"] > 0 and "frac_of_box_ceiling" in res["roofline"]
+    assert res["box_ceiling"]["clocks"].keys() & {"unavailable", "sclk_MHz"}
 
 
 def test_bench_refuses_world_size_mismatch():
@@ -160,3 +162,9 @@ def test_bench_cfg5_eight_ranks_dry_run():
     assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] == "port" and "8-of-16" in cb["sample"]
     sc = res["scatter"]
     assert sc["ranks"] == 8 and sc["every_slice_ok"] is True and sc["bytes_per_rank"] > 0
+    # the box-ceiling diagnostic: every rank's ceiling, the headline priced against it,
+    # clocks / partition modes (reported unavailable without a device)
+    box = res["box_ceiling"]
+    assert len(box["GBps_by_rank"]) == 8 and all(g > 0 for g in box["GBps_by_rank"])
+    assert "clocks" in box and res["roofline"]["box_ceiling_GBps"] == box["GBps"]
+    assert 0 < res["roofline"]["frac_of_box_ceiling"]

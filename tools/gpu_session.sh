@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
+#          e2e12 e2ed15 e2edab seg1m prof1m scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -16,7 +16,7 @@ for s in "$@"; do
     encode) run bench_encode 600 python3 bench.py ;;
     decode) run bench_decode 600 python3 bench.py --config cfg3 --no-cpu-baseline ;;
     8of16) run bench_8of16 600 python3 bench.py --config cfg5 --no-cpu-baseline ;;
-    2rank) run bench_2rank_one_gpu 600 python3 bench.py --gpus 2 --objects 256 --no-cpu-baseline ;;
+    2rank) run bench_2rank_one_gpu 600 python3 bench.py --gpus 2 --objects 256 ;;
     bao) run bench_bao 600 python3 bench.py --mode bao --no-cpu-baseline ;;
     baodec) run bench_bao_decode 600 python3 bench.py --mode bao-decode --cpu-seconds 8 ;;
     pipe12) run bench_pipe12 600 python3 bench.py --mode pipeline --level 12 --verify-all ;;
@@ -69,6 +69,13 @@ for s in "$@"; do
     sdmaab) for i in 1 2; do HSA_ENABLE_SDMA=0 run bench_e2e15_nosdma_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify
                              run bench_e2e15_sdma_$i 300 python3 bench.py --config cfg4 --steps 6 --warmup 2 --no-cpu-baseline --no-verify; done ;;
     e2ed15full) run bench_e2ed15_full 600 python3 bench.py --mode e2e-decode --level 15 --steps 3 --warmup 1 --cpu-seconds 8 ;;
+    e2edab) for i in 1 2; do run bench_e2ed15_full_prefix_$i 400 python3 bench.py --mode e2e-decode --level 15 --steps 4 --warmup 1 --no-cpu-baseline
+                           CHIP_DECODE_PREFIX=0 run bench_e2ed15_full_whole_$i 400 python3 bench.py --mode e2e-decode --level 15 --steps 4 --warmup 1 --no-cpu-baseline; done ;;
+    seg1m) run bench_e2e15_1mib 600 python3 bench.py --mode e2e --level 15 --object-bytes 1048576 --objects 16384 --steps 3 --warmup 1 --cpu-seconds 8
+           run bench_e2ed15_1mib 600 python3 bench.py --mode e2e-decode --level 15 --object-bytes 1048576 --objects 16384 --steps 3 --warmup 1 --no-cpu-baseline
+           run bench_pipe12_1mib_l15shape 600 python3 bench.py --mode pipeline --level 12 --object-bytes 1048811 --objects 16384 --verify-all --no-cpu-baseline
+           run bench_pipe12_1mib 600 python3 bench.py --mode pipeline --level 12 --object-bytes 1048576 --objects 16384 --verify-all --no-cpu-baseline ;;
+    prof1m) bash tools/gpu_prof.sh $TAG/p1m --mode pipeline --level 12 --object-bytes 1048811 --objects 16384 ;;
     e2e14) run bench_e2e14 300 python3 bench.py --mode e2e --level 14 --objects 512 --steps 4 --warmup 1 --no-cpu-baseline
            CHIP_E2E_DIRECT=0 run bench_e2e14_staged 300 python3 bench.py --mode e2e --level 14 --objects 512 --steps 4 --warmup 1 --no-cpu-baseline --no-verify ;;
     valupk) run valu_probe_pk 300 ./tools/valu_probe 40000 pk ;;
