@@ -1,0 +1,190 @@
+// api_common.hpp — what the C-ABI translation units of libcarbonado_hip share
+// (include/carbonado_hip.h).  Host-side orchestration only: argument checks
+// and error mapping that mirror the reference stage functions (file:line
+// cited per entry point), staging of host buffers into per-thread device
+// scratch, and the encode()/decode() glue.  Every byte of shard/stream data is
+// produced by the HIP kernels in zfec_kernels.hip, bao_kernels.hip,
+// fused_kernels.hip and small_kernels.hip; there is no CPU compute path for
+// zfec or bao.  The snappy/ECIES stages that the reference runs before zfec
+// (and after it on decode) are host stages by design (host_stages.cpp).
+//
+// The entry points, by concern:
+//   api_context.cpp    device selection, the per-thread context, small
+//                      copies, library info, sizes, batch-buffer allocation
+//   api_host_copy.cpp  host <-> HBM copies (pinned ring, copy threads, NUMA)
+//   api_plans.cpp      zfec plans, encode() at Zfec|Bao on the device, bao
+//                      and slice geometry, EncodeInfo, host-stage glue
+//   api_stages.cpp     the stage functions and the device-resident batches
+//   api_scrub.cpp      verify_slice / extract_slice / scrub (single, batch)
+//   api_encode.cpp     encode() from host memory (single, host batch)
+//   api_decode.cpp     decode() from host memory (single, host batch)
+//   api_hasher.cpp     the streaming BaoHasher
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "chip_internal.hpp"
+#include "gf256.hpp"
+#include "host_stages.hpp"
+
+#define CHIP_HIP(expr)                                  \
+    do {                                                \
+        hipError_t e__ = (expr);                        \
+        if (e__ != hipSuccess) {                        \
+            ::chip::set_device_error(e__);              \
+            return CHIP_ERR_DEVICE;                     \
+        }                                               \
+    } while (0)
+
+namespace chip {
+namespace api {
+
+// ---- device and per-thread context (api_context.cpp) ----------------------
+extern std::atomic<int> g_device;  // the process's device (one GPU per process, see chip_init)
+extern std::atomic<int> g_cus;
+extern thread_local std::string t_last_err;
+
+bool is_gfx950(int d, int *cus);
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+
+// one pipeline slot of chip_encode_host_batch: its own stream and buffers
+// (`stage` is pinned host memory holding the host-stage output of a slice)
+struct Slot {
+    hipStream_t stream = nullptr;
+    DevBuf in, mid, out, hash, scratch, nodes, sin;  // sin: data regions taken from host rows
+    DevBuf stage, hnodes;  // pinned
+};
+
+// Pinned ring for copies between PAGEABLE host memory and HBM (see h2d/d2h).
+struct Staging {
+    static constexpr int R = 4;
+    static constexpr size_t PIECE = size_t(4) << 20;
+    uint8_t *ring = nullptr;
+    hipEvent_t ev[R] = {};
+    bool armed[R] = {};
+    unsigned next = 0;  // ring slot of the next piece (rotates across calls)
+    void release();
+};
+
+struct Ctx {
+    bool ready = false;
+    int dev = -1;  // device the stream and buffers live on
+    hipStream_t stream = nullptr;
+    DevBuf in, mid, out, scratch, small, x1, x2, flags;
+    std::vector<Slot> slots;
+    Staging stage;
+    // pinned arena for the few-byte copies of a call (hashes, status words,
+    // node flags): see small_h2d / small_d2h / small_sync
+    DevBuf hs;
+    size_t hs_used = 0;
+    struct HsOut {
+        void *dst;
+        const uint8_t *src;
+        size_t n;
+    };
+    std::vector<HsOut> hs_out;
+    void release();
+    ~Ctx() { release(); }
+};
+
+hipError_t grow(DevBuf &b, size_t bytes);         // grow-only device buffer (contents dropped)
+hipError_t grow_pinned(DevBuf &b, size_t bytes);  // the same, pinned host memory
+// the calling thread's context on the process's device (created on first use)
+int ctx_get(Ctx **out);
+// few-byte copies of a call through the context's pinned arena; `dst` of a
+// small_d2h receives its bytes at the next small_sync
+hipError_t small_h2d(Ctx *c, void *ddst, const void *src, size_t n);
+hipError_t small_d2h(Ctx *c, void *dst, const void *dsrc, size_t n);
+hipError_t small_sync(Ctx *c);
+
+// ---- host <-> HBM copies (api_host_copy.cpp) --------------------------------
+bool host_pinned(const void *p);
+bool staged(const void *host, size_t n);  // pageable (or CHIP_HOST_COPY=staged): through the pinned ring
+// host -> HBM on s; on return `src` may be reused
+hipError_t h2d(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s);
+// HBM -> host after the work already on s; returns when `dst` holds the bytes
+hipError_t d2h(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s);
+
+// ---- plans and geometry (api_plans.cpp) ------------------------------------
+int env_int(const char *name, int dflt);
+bool valid_km(uint32_t k, uint32_t m);
+void calc_pad(uint64_t n, uint32_t k, uint32_t *pad, uint64_t *C);  // utils.rs:47-58, k generalised
+// rows 0..k-1 copied, k..m-1 computed (aliased: in place, parity rows only)
+GfPlan encode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint8_t> &enc, bool aliased = false);
+// encode() at Zfec|Bao of device-resident objects (K13, or KS for small ones)
+hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
+                        uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s);
+int decode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint32_t> &sel,
+                const std::vector<uint64_t> &slot_off, GfPlan *out);
+int select_shares(uint32_t k, uint32_t m, const uint32_t *idx, uint32_t nshares, std::vector<uint32_t> *sel_pos);
+uint64_t n_chunks_of(uint64_t n);
+int ceil_log2_u64(uint64_t x);
+void slice_chunks(uint64_t n, uint64_t start, uint64_t len, uint64_t *c0, uint64_t *c1);
+struct SliceNode {
+    bool parent;
+    uint64_t off, len, index;  // stream offset, bytes, chunk index or parent index (stream order)
+};
+void slice_nodes(uint64_t n, uint64_t c0, uint64_t c1, std::vector<SliceNode> *out);
+int encode_info_for(uint8_t format, uint64_t input_len, uint64_t cur, uint64_t bc, uint64_t be,
+                    chip_encode_info *inf, uint64_t *zlen, uint64_t *final_len);
+bool has_host_stages(uint8_t format);
+
+// grow-only, uninitialised host scratch (std::vector::resize would zero-fill
+// and page-fault 16 MiB per object)
+struct Scratch {
+    std::unique_ptr<uint8_t[]> p;
+    size_t cap = 0;
+    uint8_t *get(size_t n) {
+        if (n > cap) {
+            p.reset(new uint8_t[n]);
+            cap = n;
+        }
+        return p.get();
+    }
+};
+
+bool stream_encrypt_on();
+uint64_t host_stage_max(uint8_t format, uint64_t n);
+int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const uint8_t *eph, const uint8_t *nonce,
+                     const uint8_t *in, uint64_t n, uint8_t *dst, uint64_t cap, Scratch &tmp,
+                     uint64_t *len, uint64_t *bc, uint64_t *be, const host::ChunkSink *sink = nullptr,
+                     uint64_t *filled = nullptr);
+
+// K1 reads and writes 16-B vectors and its tail load relies on 16-B aligned
+// shard addresses (zfec_device.hpp load16_masked).
+inline bool misaligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
+int zfec_decode_device(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t in_stride,
+                       const std::vector<uint64_t> &slot_off, const std::vector<uint32_t> &sel, uint64_t C,
+                       uint64_t count, uint8_t *d_out, uint64_t out_stride, hipStream_t s);
+bool bao_content_len(uint64_t len, uint64_t *n);
+int bao_encode_ctx(Ctx *c, const uint8_t *d_in, uint64_t n, bool want_stream, uint8_t hash[32]);
+int bao_decode_ctx(Ctx *c, const uint8_t *d_enc, uint64_t len, uint64_t n, const uint8_t *hash, uint8_t *d_dst,
+                   uint64_t out_limit = ~0ull, uint32_t *deferred = nullptr);
+int bao_header(const uint8_t *enc, uint64_t len, uint64_t *n);
+int node_check_ctx(Ctx *c, uint64_t n, const uint8_t *hash, std::vector<uint8_t> *cf, std::vector<uint8_t> *pf);
+bool slice_ok(uint64_t n, uint64_t c0, uint64_t c1, const std::vector<uint8_t> &cf, const std::vector<uint8_t> &pf);
+int scrub_repair_enqueue(Ctx *c, const uint8_t *d_stream, uint64_t n, uint64_t len, const std::vector<uint32_t> &good,
+                         uint32_t padding, uint64_t C, uint8_t *d_dst, uint8_t *d_h2);
+
+// A zfec batch: one launch (the dynamic run queue balances the XCDs inside it).
+template <typename F>  // launch(o0, cnt, stream) -> hipError_t, objects [o0, o0 + cnt)
+hipError_t zf_run(uint64_t count, hipStream_t s, F launch) {
+    return launch(0, count, s);
+}
+
+}  // namespace api
+}  // namespace chip

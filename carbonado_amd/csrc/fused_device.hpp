@@ -116,6 +116,7 @@ struct Tree {
     bool ok = false;  // ... valid
     int lane;
     uint8_t *cv;
+    bool wr = true;  // write the nodes (false: tools/fused_tune diagnostic DG 11)
     __device__ Tree(int l, uint8_t *c) : node(nullptr), cvi(0), lane(l), cv(c) {
 #pragma unroll
         for (int w = 0; w < 8; ++w) pr[w] = 0u;
@@ -143,7 +144,7 @@ struct Tree {
         if (act) {
             uint32_t p[8];
             bao::b3_parent(l, r, false, p);
-            bao::node_io<0, NT>(my, l, r);
+            if (wr) bao::node_io<0, NT>(my, l, r);
             if (r3) {
                 bao::store_cv(cv + (mc / 8) * 32, p);
             } else {
@@ -162,7 +163,13 @@ struct Tree {
 // stores nor hashing, 5 = every chunk's lines 128-B aligned (no partial
 // lines), 6 = 5 without hashing, 7 = the line stores' LDS reads without the
 // stores, 8 = the whole-line stores aimed at 8 KiB per wave (L2 hits),
-// 10 = GF table lookups without bank conflicts (wrong products).
+// 10 = GF table lookups without bank conflicts (wrong products); read-traffic
+// attribution (tools/k13_fetch): 11 = FULL without the in-wave tree's node
+// stores, 12 = general with the level 1-3 node slots in front of each chunk
+// zero-filled at step 0 (lines whole inside the kernel), 13 = general without
+// the level-0 CV stores, 14 = general with the level-0 CVs in a block-padded
+// layout [obj][shard][8 bpo] (each block's 8 CVs of a shard = one aligned
+// 256-B run).
 // FULL: cols % 8 == 0 and no zfec padding (valid >= 4 C): every block is 8
 // whole columns of plain loads, levels 1-3 run in the wave (Tree) and `cv`
 // receives level-3 CVs; otherwise lanes are predicated and `cv` receives the
@@ -262,6 +269,7 @@ __global__ __launch_bounds__(64 * WPG) void zfec_bao_fused_kernel(FusedArgs a) {
     };
 
     Tree<NT> tree(lane, a.cv);
+    tree.wr = DG != 11;
     // Blocks: DQ takes them from a queue (one atomic per block and wave, lane
     // 0, vector memory), so waves on slower XCDs simply take fewer; otherwise
     // a static stride of GW.  The next block is known before the current one
@@ -448,6 +456,17 @@ __global__ __launch_bounds__(64 * WPG) void zfec_bao_fused_kernel(FusedArgs a) {
                         for (int t = 0; t < 8; ++t) one_line(t);
                     }
                 }
+                if (DG == 12 && s == 0 && gcol) {  // zero the level 1-3 node slots in front of each chunk
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const uint64_t c = (uint64_t)t * TS + ub + cu;
+                        uint32_t k = 0;
+                        for (uint32_t l = 1; l <= 3; ++l)
+                            if (c % (1ull << l) == 0 && c + (1ull << (l - 1)) < a.N) k = l;
+                        for (uint32_t i = gl; i < 8 * k; i += 8)
+                            *bao::glb(reinterpret_cast<u32x2 *>(lat_ht(t, 8 * i) - 64 * k)) = u32x2{0u, 0u};
+                    }
+                }
                 if (ST && (s == 0 || s == 7) && gcol) {
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {
@@ -525,8 +544,10 @@ __global__ __launch_bounds__(64 * WPG) void zfec_bao_fused_kernel(FusedArgs a) {
         }
         if (FULL) {
             tree.step(h, ob + hco - 64, obj * 8 * a.cvs + ci, true);
-        } else if (mine) {
-            auto *cvp = bao::glb(reinterpret_cast<u32x4 *>(a.cv + (obj * a.N + ci) * 32));
+        } else if (mine && DG != 13) {
+            const uint64_t cvi = DG == 14 ? obj * 8 * (8 * a.bpo) + (uint64_t)(lane >> 3) * (8 * a.bpo) + hu
+                                          : obj * a.N + ci;
+            auto *cvp = bao::glb(reinterpret_cast<u32x4 *>(a.cv + cvi * 32));
             cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
             cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
         }

@@ -87,8 +87,8 @@ __global__ __launch_bounds__(TPB) void gf_apply_generic_kernel(GenericArgs a) {
 // in the lane group's rotated order, super-tiles of U tiles with the next
 // one's loads in flight), the same stores (K copies + NP computed rows, 16 B
 // per lane each, NT as the product), the same run queue, grid and LDS
-// footprint (set by the launch), but every computed row is an XOR of two
-// loads instead of K*16 table lookups.  What this box's HBM gives the
+// footprint (set by the launch), but computed row q is the XOR of the K
+// loads and the byte q instead of K*16 table lookups.  What this box's HBM gives the
 // headline's access pattern on the caller's buffers: bench.py prices the
 // headline against it (frac_of_box_ceiling) so a slow box explains itself.
 template <int K, int NP, int U, bool NT>
@@ -135,9 +135,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void h
 #pragma unroll
             for (int j = 0; j < K; ++j)
                 if (coff[j] != NO_OUT) store16<NT>(ob + coff[j] + col, v[u][j]);
+            u32x4 x = v[u][0];  // the XOR of all K shards: the same whatever the lane's shard order
+#pragma unroll
+            for (int j = 1; j < K; ++j) x ^= v[u][j];
 #pragma unroll
             for (int q = 0; q < NP; ++q)
-                if (a.par_off[q] != NO_OUT) store16<NT>(ob + a.par_off[q] + col, v[u][q % K] ^ v[u][(q + 1) % K]);
+                if (a.par_off[q] != NO_OUT) store16<NT>(ob + a.par_off[q] + col, x ^ (0x01010101u * (uint32_t)q));
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)

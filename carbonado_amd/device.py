@@ -39,8 +39,9 @@ def zfec_encode_batch(inp: torch.Tensor, n: int, out: torch.Tensor, k: int = FEC
 
 def hbm_pattern_batch(inp: torch.Tensor, n: int, out: torch.Tensor, k: int = FEC_K, m: int = FEC_M) -> None:
     """Diagnostic: zfec_encode_batch's memory pattern (same loads, stores,
-    grid and run queue) without the GF arithmetic — `out` receives XORs of
-    data shards, not parity (chip_hbm_pattern_batch_dev)."""
+    grid and run queue) without the GF arithmetic — `out` receives the data
+    shards and, per computed row q, their XOR with every byte XOR q; not
+    parity (chip_hbm_pattern_batch_dev)."""
     assert inp.is_cuda and out.is_cuda and inp.is_contiguous() and out.is_contiguous()
     assert inp.shape[0] == out.shape[0] and inp.data_ptr() != out.data_ptr()
     need = _lib.lib().chip_zfec_encoded_len(n, k, m)

@@ -323,8 +323,8 @@ CHIP_API int chip_zfec_encode_batch_dev(uint32_t k, uint32_t m, const uint8_t *d
                                void *stream);
 /* Diagnostic (ABI 5): the memory pattern of chip_zfec_encode_batch_dev with
  * the same arguments — the same loads, stores, grid, run queue and LDS
- * footprint — with the GF(2^8) arithmetic taken out (the parity rows written
- * are XORs of two data shards, NOT parity).  Its rate is what this box's HBM
+ * footprint — with the GF(2^8) arithmetic taken out (computed row q is the
+ * XOR of the k data shards with every byte XOR q, NOT parity).  Its rate is what this box's HBM
  * gives the encode's access pattern on these buffers: the ceiling the encode
  * is compared with (bench.py box_ceiling).  (k, m) = (4, 8) or (8, 16);
  * d_out != d_in; CHIP_ERR_ZFEC for other shapes. */

@@ -204,23 +204,28 @@ def test_batch_in_place_aliased_data_shards(gpu, k, m, n):
 @pytest.mark.parametrize("k,m,n", [(4, 8, (1 << 20) + 5), (4, 8, 16 << 20), (8, 16, (1 << 20) + 5)])
 def test_hbm_pattern_probe_writes_its_pattern(gpu, k, m, n):
     """chip_hbm_pattern_batch_dev (bench.py's box ceiling) runs the encode's
-    memory pattern: data shards copied, computed row q = shard q%k XOR shard
-    (q+1)%k — every output byte written (the same tiles as the encode)."""
+    memory pattern: data shards copied, computed row q = the XOR of the k data
+    shards with every byte XOR q — every output byte written (the same tiles
+    as the encode)."""
     import torch
     from carbonado_amd import device
     count = 3
-    inp = torch.randint(0, 256, (count, n), dtype=torch.uint8, device="cuda")
+    row = (n + 15) // 16 * 16  # batch rows are 16-B aligned; bytes past n read as zero
+    inp = torch.randint(0, 256, (count, row), dtype=torch.uint8, device="cuda")
     C = gpu.chip_zfec_encoded_len(n, k, m) // m
     out = torch.full((count, m * C), 0xA5, dtype=torch.uint8, device="cuda")
     device.hbm_pattern_batch(inp, n, out, k, m)
     torch.cuda.synchronize()
     padded = torch.zeros((count, k * C), dtype=torch.uint8, device="cuda")
-    padded[:, :n] = inp
+    padded[:, :n] = inp[:, :n]
     sh = padded.view(count, k, C)
     got = out.view(count, m, C)
     assert torch.equal(got[:, :k], sh)
+    x = sh[:, 0].clone()
+    for j in range(1, k):
+        x ^= sh[:, j]
     for q in range(m - k):
-        assert torch.equal(got[:, k + q], sh[:, q % k] ^ sh[:, (q + 1) % k]), q
+        assert torch.equal(got[:, k + q], x ^ q), q
 
 
 def test_hbm_pattern_probe_refuses_other_shapes(gpu):
