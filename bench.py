@@ -270,13 +270,15 @@ def pmc_kernel_sym(args) -> str | None:
     fused = os.environ.get("CHIP_FUSED", "1") != "0"
     n = int(args.object_mib * (1 << 20))
     if args.mode == "encode":
-        return f"gf_apply_kernel<{args.k}, {(args.m - args.k + 3) // 4},"
+        return f"zfec_apply_kernel<{args.k}, {(args.m - args.k + 3) // 4}>"
     if args.mode == "decode":
-        return f"gf_apply_kernel<{args.k}, 1,"
-    if fused and ((args.mode == "bao" and n >= 65536) or (args.mode == "pipeline" and args.level & 12 == 12)):
+        return f"zfec_apply_kernel<{args.k}, 1>"
+    if fused and args.mode == "bao" and n >= 65536:
+        return "bao_content_fused_kernel"
+    if fused and args.mode == "pipeline" and args.level & 12 == 12:
         return "zfec_bao_fused_kernel"
     if args.mode == "bao-decode" or (args.mode == "pipeline-decode" and args.level & 4):
-        return "bao_chunk_kernel<1,"
+        return "bao_chunk_kernel_verify"
     return None
 
 
@@ -691,8 +693,8 @@ class Workload:
             self.step = lambda: device.zfec_encode_batch(self.inp_full, n, self.out, k, m)
             self.alg_bytes = count * (n + m * C)  # read the input + write all m shards
             ng = (m - k + 3) // 4
-            self.kernel = f"gf_apply_kernel<{k},{ng}>"
-            self.kernel_sym = f"gf_apply_kernel<{k}, {ng},"
+            self.kernel = f"zfec_apply_kernel<{k}, {ng}>"
+            self.kernel_sym = f"zfec_apply_kernel<{k}, {ng}>"
         elif args.mode == "decode":
             self.enc = batch_buf((count, m * C), "enc")
             device.zfec_encode_batch(self.inp, n, self.enc, k, m)
@@ -701,8 +703,8 @@ class Workload:
             self.out = batch_buf((count, k * C), "out")
             self.step = lambda: device.zfec_decode_batch(self.enc, C, self.keep, self.out, k, m)
             self.alg_bytes = count * (2 * k * C)  # read k shares + write k data shards
-            self.kernel = f"gf_apply_kernel<{k},1> (decode, erased {sorted(erased)})"
-            self.kernel_sym = f"gf_apply_kernel<{k}, 1,"
+            self.kernel = f"zfec_apply_kernel<{k}, 1> (decode, erased {sorted(erased)})"
+            self.kernel_sym = f"zfec_apply_kernel<{k}, 1>"
         elif args.mode == "pipeline":
             lv = args.level
             if lv & 3:
@@ -720,16 +722,16 @@ class Workload:
             self.alg_bytes = count * (n + zlen + zlen + (blen - zlen)) if two else count * (n + blen)
             self.zlen = zlen
             if lv & 12 == 12 and not two:
-                self.kernel = (f"encode() level {lv} on the device: zfec_bao_fused_kernel (zfec 4-of-8 + chunk "
+                self.kernel = (f"encode() level {lv} on the device: zfec_bao_fused_kernel_full/_general (zfec 4-of-8 + chunk "
                                "hashing + tree levels 1-3 in one pass) + parent levels from level 4")
                 self.kernel_sym = "zfec_bao_fused_kernel"
             elif two:
-                self.kernel = (f"encode() level {lv} on the device: gf_apply_kernel + bao_chunk_kernel + parent "
+                self.kernel = (f"encode() level {lv} on the device: gf_apply_bl_kernel + bao_chunk_kernel_inplace + parent "
                                "levels (zfec writes the shards into their bao chunk slots; bao hashes in place)")
             elif lv & 4:
-                self.kernel = f"encode() level {lv} on the device: bao_chunk_kernel + parent levels"
+                self.kernel = f"encode() level {lv} on the device: bao_content_fused_kernel / bao_chunk_kernel_encode + parent levels"
             else:
-                self.kernel = f"encode() level {lv} on the device: gf_apply_kernel"
+                self.kernel = f"encode() level {lv} on the device: zfec_apply_kernel"
             if not (lv & 12 == 12 and not two):
                 self.kernel_sym = "pipeline"
         elif args.mode == "pipeline-decode":
@@ -756,7 +758,7 @@ class Workload:
             # without Bao only the primaries' bytes are read
             self.alg_bytes = count * (blen + n) if lv & 4 else count * 2 * n
             if lv & 4:
-                self.kernel = (f"decode() level {lv} on the device: bao_chunk_kernel MODE 1 (every chunk and "
+                self.kernel = (f"decode() level {lv} on the device: bao_chunk_kernel_verify (every chunk and "
                                f"parent verified{', only the 4 data shards written' if lv & 8 else ''}) + parent "
                                "check levels")
             else:
@@ -824,7 +826,7 @@ class Workload:
             self.scrub_comps = (count + len(self.damaged)) * (zlen // 64 + zlen // 1024 - 1)
             self.alg_bytes = count * blen + len(self.damaged) * (2 * blen + zlen)
             self.kernel = (f"scrub() of {count} device-resident level-12 streams, {len(self.damaged)} damaged: "
-                           "bao_chunk_kernel MODE 2 + bao_parent_check_kernel (every node), scrub_mask_kernel, "
+                           "bao_chunk_kernel_check + bao_parent_check_kernel (every node), scrub_mask_kernel, "
                            "then per damaged stream gather + zfec decode + fused re-encode")
             self.kernel_sym = "scrub-batch"
         elif args.mode == "hasher":
@@ -996,8 +998,8 @@ class Workload:
             self.status = torch.full((count,), -1, dtype=torch.int32, device=dev)
             self.step = lambda: device.bao_decode_batch(self.enc, n, self.hashes, self.out, self.status, self.scratch)
             self.alg_bytes = count * (blen + n)  # read the stream, write the content
-            self.kernel = "bao_chunk_kernel<1> (verify + content) + bao_parent_kernel<1> levels"
-            self.kernel_sym = "bao_chunk_kernel<1,"
+            self.kernel = "bao_chunk_kernel_verify (verify + content) + bao_parent_kernel<1> levels"
+            self.kernel_sym = "bao_chunk_kernel_verify"
         else:
             self.blen = blen = L.chip_bao_encoded_len(n)
             self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
@@ -1006,11 +1008,11 @@ class Workload:
             self.step = lambda: device.bao_encode_batch(self.inp_full, n, self.out, self.hashes, self.scratch)
             self.alg_bytes = count * (n + blen)
             fused = n >= 65536 and os.environ.get("CHIP_FUSED", "1") != "0"
-            self.kernel = ("zfec_bao_fused_kernel content mode (chunk hashing + tree levels 1-3, 64 consecutive "
+            self.kernel = ("bao_content_fused_kernel (K13 content mode: chunk hashing + tree levels 1-3, 64 consecutive "
                            "chunks per wave) + bao_parent_kernel levels from level 4"
                            + ("" if n % 65536 == 0 else " + bao_tail_kernel (the last < 64 chunks)") if fused else
-                           "bao_chunk_kernel + bao_parent_kernel levels")
-            self.kernel_sym = "zfec_bao_fused_kernel" if fused else "bao_chunk_kernel<0,"
+                           "bao_chunk_kernel_encode + bao_parent_kernel levels")
+            self.kernel_sym = "bao_content_fused_kernel" if fused else "bao_chunk_kernel_encode"
         torch.cuda.synchronize()
 
     def _scatter_inputs(self, rank: int, world: int) -> float:

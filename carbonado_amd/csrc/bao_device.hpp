@@ -419,8 +419,10 @@ __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x
 // XG 1: XCD-grouped block order (block b runs logical block (b % 8) * (B/8) + b/8,
 // so each XCD sweeps one contiguous eighth of the batch; B % 8 == 0 only).
 // DQ: persistent grid, wave tasks from the run queue a.queue (zero at launch).
+// This is the kernel body; ChunkKernel below names the kernel launched for a
+// configuration.
 template <int MODE, int CPL, bool NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0, bool DQ = false>
-__global__ __launch_bounds__(K3_TPB) void bao_chunk_kernel(ChunkArgs a) {
+__device__ __forceinline__ void bao_chunk_body(const ChunkArgs &a) {
     constexpr int LOG = ilog2(CPL);
     constexpr int NSTEP = 8 * CPL;
     // SP 3: [pad 4 | step-parity-0 data 32 | step-parity-1 data 32] words per row
@@ -1115,6 +1117,14 @@ hipError_t run_parent_levels(uint8_t *cv_prev, uint64_t stride_prev, uint64_t cn
     return hipSuccess;
 }
 
+// The K3 kernel of a configuration: ChunkKernel<...>::fn.  The library
+// (bao_kernels.hip) specialises it for the configurations it ships, each a
+// kernel of its own name (bao_chunk_kernel_encode, _verify, _check,
+// _inplace, and their _static forms without the run queue);
+// tools/bao_variants.hpp defines it for every configuration.
+template <int MODE, int CPL, bool NTS, int SP, int SU, int SE, int XG, bool DQ>
+struct ChunkKernel;
+
 // Enqueue K3 over `waves` wave tasks: with DQ a persistent grid of resident
 // workgroups taking wave tasks from the stream's run queue, else one wave per
 // task.
@@ -1125,7 +1135,7 @@ hipError_t launch_chunk_kernel(ChunkArgs ca, hipStream_t stream, size_t pad_lds)
     bool dq = DQ && waves < (1ull << 31);
     if (dq) {  // persistent grid of resident workgroups, wave tasks from the stream's run queue
         uint32_t *q = nullptr;
-        const void *fn = reinterpret_cast<const void *>(bao_chunk_kernel<MODE, CPL, NTS, SP, SU, SE, XG, true>);
+        const void *fn = reinterpret_cast<const void *>(ChunkKernel<MODE, CPL, NTS, SP, SU, SE, XG, true>::fn);
         // per instance and LDS pad, asked once: the query costs ~6 us of API
         // time, which single small objects paid on every call (profiles/r4c)
         static std::mutex occ_mu;
@@ -1147,12 +1157,12 @@ hipError_t launch_chunk_kernel(ChunkArgs ca, hipStream_t stream, size_t pad_lds)
         if (dq) {
             ca.queue = q + QUEUE_K3;
             const uint64_t grid = std::min<uint64_t>(blocks, (uint64_t)per_cu * (uint64_t)num_cus());
-            hipLaunchKernelGGL((bao_chunk_kernel<MODE, CPL, NTS, SP, SU, SE, XG, true>), dim3((unsigned)grid),
+            hipLaunchKernelGGL((ChunkKernel<MODE, CPL, NTS, SP, SU, SE, XG, true>::fn), dim3((unsigned)grid),
                                dim3(K3_TPB), pad_lds, stream, ca);
         }
     }
     if (!dq)
-        hipLaunchKernelGGL((bao_chunk_kernel<MODE, CPL, NTS, SP, SU, SE, XG>), dim3((unsigned)blocks),
+        hipLaunchKernelGGL((ChunkKernel<MODE, CPL, NTS, SP, SU, SE, XG, false>::fn), dim3((unsigned)blocks),
                            dim3(K3_TPB), pad_lds, stream, ca);
     return hipGetLastError();
 }

@@ -65,6 +65,38 @@ constexpr int BAO_SU = 8;
 // +5.6-7.8 % from the same change, tools/fused_tune r2l).
 constexpr bool BAO_DQ = true;
 
+}  // namespace
+
+// The product's K3 configurations, one kernel each (bao_device.hpp ChunkKernel):
+// encode (MODE 0, the stream written), verify-decode (MODE 1, the content
+// written, whole or a prefix), node check (MODE 2, scrub), in-place encode
+// (MODE 3, the two-kernel Zfec|Bao path); _static: without the run queue (a
+// batch of 2^31 wave tasks or more).
+#define CHIP_K3(NAME, MODE, CPL, NTS, SP, SU)                                                   \
+    __global__ __launch_bounds__(K3_TPB) void NAME(ChunkArgs a) {                              \
+        bao_chunk_body<MODE, CPL, NTS, SP, SU, 0, BAO_XG, BAO_DQ>(a);                          \
+    }                                                                                         \
+    __global__ __launch_bounds__(K3_TPB) void NAME##_static(ChunkArgs a) {                     \
+        bao_chunk_body<MODE, CPL, NTS, SP, SU, 0, BAO_XG, false>(a);                           \
+    }                                                                                         \
+    template <>                                                                               \
+    struct ChunkKernel<MODE, CPL, NTS, SP, SU, 0, BAO_XG, true> {                             \
+        static constexpr void (*fn)(ChunkArgs) = NAME;                                        \
+    };                                                                                        \
+    template <>                                                                               \
+    struct ChunkKernel<MODE, CPL, NTS, SP, SU, 0, BAO_XG, false> {                            \
+        static constexpr void (*fn)(ChunkArgs) = NAME##_static;                               \
+    };
+namespace bao {
+CHIP_K3(bao_chunk_kernel_encode, 0, BAO_CPL, BAO_NTS, BAO_SP, BAO_SU)
+CHIP_K3(bao_chunk_kernel_verify, 1, BAO_CPL, BAO_DEC_NTS, 0, 1)
+CHIP_K3(bao_chunk_kernel_check, 2, 1, false, 0, 1)
+CHIP_K3(bao_chunk_kernel_inplace, 3, 8, BAO_NTS, 0, 1)
+}  // namespace bao
+#undef CHIP_K3
+
+namespace {
+
 template <int MODE>
 hipError_t run_bao(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,

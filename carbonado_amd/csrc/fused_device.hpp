@@ -194,9 +194,13 @@ struct Tree {
 // per access.  GFP 1: table addresses through gf_pair.
 // WPG: waves per workgroup (FW; tools/fused_tune runs 4 = one wave per SIMD
 // to measure the kernel's sensitivity to occupancy).
+//
+// This is the kernel body; the product's launches are the few configurations
+// fused_kernels.hip wraps in kernels of their own (zfec_bao_fused_kernel_full,
+// _general, bao_content_fused_kernel), the tuner's are tools/fused_variants.hpp's.
 template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
           bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false, int PRIO = 0>
-__global__ __launch_bounds__(64 * WPG) void zfec_bao_fused_kernel(FusedArgs a) {
+__device__ __forceinline__ void zfec_bao_fused_body(const FusedArgs &a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int NV = KIND ? 8 : 4;         // 16-B loads per lane per step

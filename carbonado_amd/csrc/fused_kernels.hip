@@ -51,6 +51,40 @@ bool l123_on() {
     return on;
 }
 
+}  // namespace
+
+namespace fused {
+
+// The product's K13 configurations (fused_device.hpp documents the template
+// arguments): encode() at Zfec|Bao with levels 1-3 in the wave (FULL) or from
+// the level-0 CVs (general: 8 does not divide the shard's chunk count, or
+// zfec padding; both message words of a step read at once, MP 1: -1.5 %
+// kernel time, tools/fused_tune, profiles/r6f/r6h/r6i; the FULL path measured
+// no gain from it), and bao of the content (KIND 1).  _a64: 64-bit addresses
+// for shards of 256 MiB and more.
+__global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_full(fused::FusedArgs a) {
+    fused::zfec_bao_fused_body<true, true, 1, 0, 0, true, 0, 0, K13_O32, K13_GFP>(a);
+}
+__global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_general(fused::FusedArgs a) {
+    fused::zfec_bao_fused_body<true, false, 1, 0, 0, true, 1, 0, K13_O32, K13_GFP>(a);
+}
+__global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_full_a64(fused::FusedArgs a) {
+    fused::zfec_bao_fused_body<true, true, 1, 0, 0, true, 0, 0, false, K13_GFP>(a);
+}
+__global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_general_a64(fused::FusedArgs a) {
+    fused::zfec_bao_fused_body<true, false, 1, 0, 0, true, 1, 0, false, K13_GFP>(a);
+}
+__global__ __launch_bounds__(fused::FTPB) void bao_content_fused_kernel(fused::FusedArgs a) {
+    fused::zfec_bao_fused_body<true, true, 1, 0, 1, true, 0, 0, K13_O32, 0, fused::FW, K13_NTL>(a);
+}
+__global__ __launch_bounds__(fused::FTPB) void bao_content_fused_kernel_a64(fused::FusedArgs a) {
+    fused::zfec_bao_fused_body<true, true, 1, 0, 1>(a);
+}
+
+}  // namespace fused
+
+namespace {
+
 // One launch per part of the batch small enough for the kernel's 32-bit block
 // queue (< 2^31 blocks; a part is whole objects).  cv_nodes: CVs per object
 // the kernel writes into a.cv.
@@ -103,12 +137,10 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
     a.queue = q + QUEUE_K13;
     const bool full = a.cols % 8 == 0 && n >= 4 * C;  // levels 1-3 in the kernel (N >= 64, 8 subtrees a block)
-    // general path: both compressions' message words read at once (MP 1): -1.5 % kernel time
-    // (tools/fused_tune, profiles/r6f/r6h/r6i); the FULL path measured no gain from it
-    constexpr auto KF64 = zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, false, K13_GFP>;
-    constexpr auto KG64 = zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, false, K13_GFP>;
-    constexpr auto KF32 = zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, K13_O32, K13_GFP>;
-    constexpr auto KG32 = zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, K13_O32, K13_GFP>;
+    constexpr auto KF64 = zfec_bao_fused_kernel_full_a64;
+    constexpr auto KG64 = zfec_bao_fused_kernel_general_a64;
+    constexpr auto KF32 = zfec_bao_fused_kernel_full;
+    constexpr auto KG32 = zfec_bao_fused_kernel_general;
     static bool attr = [] {
         bool ok = true;
         for (auto k : {KF64, KG64, KF32, KG32})
@@ -206,8 +238,8 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     uint32_t *q = nullptr;
     if ((e = stream_queue(stream, &q)) != hipSuccess) return e;
     a.queue = q + QUEUE_K13;
-    constexpr auto K64 = zfec_bao_fused_kernel<true, true, 1, 0, 1>;
-    constexpr auto K32 = zfec_bao_fused_kernel<true, true, 1, 0, 1, true, 0, 0, K13_O32, 0, FW, K13_NTL>;
+    constexpr auto K64 = bao_content_fused_kernel_a64;
+    constexpr auto K32 = bao_content_fused_kernel;
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(K64), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)LDS_BYTES) == hipSuccess &&

@@ -252,13 +252,15 @@ struct TileIter {
     }
 };
 
-// RO: replica-count override, WPE: waves/EU hint, SB: scheduling fence every SB
-// shards (bounds the table lookups in flight; 0 = none), PF: load the next
-// super-tile's shards before computing the current one, NTL: nontemporal
-// input loads — tools/zfec_tune.
+// The kernel body.  RO: replica-count override, WPE: waves/EU hint, SB:
+// scheduling fence every SB shards (bounds the table lookups in flight; 0 =
+// none), PF: load the next super-tile's shards before computing the current
+// one, NTL: nontemporal input loads, TR: per-workgroup trace — tools/zfec_tune.
+// The product's kernels are zfec_kernels.hip's zfec_apply_kernel<K, NG> (one
+// configuration per shape, ApplyCfg); the tuner's, tools/zfec_variants.hpp's.
 template <int K, int NG, int U, int MAP, bool NT, int RO = 0, int WPE = 1, int SB = 0, bool PF = false,
           bool NTL = false, bool TR = false>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_kernel(ApplyArgs a) {
+__device__ __forceinline__ void gf_apply_body(const ApplyArgs &a) {
     constexpr int R = RO ? RO : replicas_for(K);
     using E = typename Entry<NG>::T;
     constexpr int W = 4 * NG;            // bytes per table entry

@@ -188,21 +188,34 @@ struct KernelInfo {
 #define ZF_NTL_DEF 0
 #endif
 template <int K, int NG>
+struct ApplyCfg {
+    static constexpr bool K4 = K == 4 && NG == 1;  // the 4-of-8 shape
+    static constexpr int U = K4 ? 2 : 1;
+    static constexpr int WPE = (K > 4 || K4) ? 2 : 1;
+    static constexpr int SB = K > 4 ? 1 : 0;
+    static constexpr bool PF = K > 4 ? K <= 8 : K4;
+    static constexpr bool NT = K > 4 ? (NG == 1 && ZF_NT) : ZF_NT;
+    static constexpr bool NTL = K4 && ZF_NTL_DEF;
+    static constexpr int BPC_CAP = K4 ? 2 : 0;
+};
+
+// The product's zfec apply kernel for K input shards and NG dword groups of
+// computed rows (4 NG rows), in its ApplyCfg configuration.
+template <int K, int NG>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(ApplyCfg<K, NG>::WPE))) void zfec_apply_kernel(
+    ApplyArgs a) {
+    using C = ApplyCfg<K, NG>;
+    gf_apply_body<K, NG, C::U, ZF_MAP, C::NT, 0, C::WPE, C::SB, C::PF, C::NTL>(a);
+}
+
+template <int K, int NG>
 KernelInfo make_info() {
     constexpr int R = replicas_for(K);
     KernelInfo ki;
     ki.lds = (size_t)256 * K * R * 4 * NG;
-    ki.u = 1;
-    ki.bpc_cap = 0;
-    if constexpr (K > 4) {
-        ki.fn = gf_apply_kernel<K, NG, 1, ZF_MAP, (NG == 1 && ZF_NT), 0, 2, 1, (K <= 8)>;
-    } else if constexpr (K == 4 && NG == 1) {
-        ki.fn = gf_apply_kernel<4, 1, 2, ZF_MAP, ZF_NT, 0, 2, 0, true, (bool)ZF_NTL_DEF>;
-        ki.u = 2;
-        ki.bpc_cap = 2;
-    } else {
-        ki.fn = gf_apply_kernel<K, NG, 1, ZF_MAP, ZF_NT>;
-    }
+    ki.fn = zfec_apply_kernel<K, NG>;
+    ki.u = ApplyCfg<K, NG>::U;
+    ki.bpc_cap = ApplyCfg<K, NG>::BPC_CAP;
     return ki;
 }
 

@@ -46,7 +46,7 @@ with open(d / f"{tag}_counter_collection.csv", "w") as f:
     f.write("Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n")
     f.write("1,at::fill_kernel,%s,1\n" % ctr)
     for i, v in enumerate(val):
-        f.write('%d,"chip::zf::gf_apply_kernel<4, 1, 2, 6, true>(chip::zf::ApplyArgs)",%s,%s\n' % (i + 2, ctr, v))
+        f.write('%d,"chip::(anonymous namespace)::zfec_apply_kernel<4, 1>(chip::zf::ApplyArgs)",%s,%s\n' % (i + 2, ctr, v))
 '''
 
 
@@ -63,7 +63,7 @@ def test_live_traffic_two_passes(tmp_path, monkeypatch):
     r = bench.live_traffic(args, [], timeout_s=60)
     assert r["FETCH_SIZE_KiB"] == 150.0 and r["WRITE_SIZE_KiB"] == 400.0, r
     assert r["bytes"] == (2 * 150 + 400) * 1024
-    assert "gf_apply_kernel<4, 1," in r["kernel"]
+    assert "zfec_apply_kernel<4, 1>" in r["kernel"]
     # a mode without an HBM-bound kernel gets no passes
     assert "error" in bench.live_traffic(bench.parse(["--mode", "bao"]), [])
 

@@ -16,7 +16,7 @@
 #include <vector>
 
 #include "../carbonado_amd/csrc/gf256.hpp"
-#include "../carbonado_amd/csrc/zfec_device.hpp"
+#include "zfec_variants.hpp"
 #include "../carbonado_amd/csrc/hbm_alloc.hpp"
 
 using namespace chip;

@@ -9,7 +9,7 @@
 #include <string>
 #include <vector>
 
-#include "../carbonado_amd/csrc/bao_device.hpp"
+#include "bao_variants.hpp"
 
 using namespace chip;
 using namespace chip::bao;

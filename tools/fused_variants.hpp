@@ -1,5 +1,6 @@
-// fused_variants.hpp — measured-and-not-kept variants of the fused kernels,
-// kept for tools/fused_tune.hip only (not part of the library):
+// fused_variants.hpp — the tuner's K13 kernels (any configuration of the body)
+// and measured-and-not-kept variants of the fused kernels, for tools/ only
+// (not part of the library):
 //  * K13S, zfec_bao_spec_kernel: K13's FULL path with hashing and GF/line
 //    stores on separate waves (profiles/NOT_KEPT.md, r7jk: 15-20 % slower);
 //  * bao_levels123_seg_kernel: the general path's levels-1-3 pass writing
@@ -10,6 +11,16 @@
 
 namespace chip {
 namespace fused {
+
+// The tuner's K13 variants: any configuration of the kernel body
+// (fused_device.hpp zfec_bao_fused_body documents the arguments), each its
+// own kernel.  The library instantiates only the configurations it ships
+// (fused_kernels.hip: zfec_bao_fused_kernel_full / _general, ...).
+template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
+          bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false, int PRIO = 0>
+__global__ __launch_bounds__(64 * WPG) void zfec_bao_fused_kernel(FusedArgs a) {
+    zfec_bao_fused_body<NT, FULL, ORD, DG, KIND, DQ, MP, SS, O32, GFP, WPG, NTL, PRIO>(a);
+}
 
 // K13S (tools/fused_tune only; measured 15-20 % SLOWER than K13, profiles/r7j,
 // r7k, not in the library): the FULL path of K13 with its roles on different

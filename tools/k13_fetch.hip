@@ -17,7 +17,7 @@
 #include <string>
 #include <vector>
 
-#include "../carbonado_amd/csrc/fused_device.hpp"
+#include "fused_variants.hpp"
 #include "../carbonado_amd/csrc/gf256.hpp"
 #include "../carbonado_amd/csrc/hbm_alloc.hpp"
 
@@ -51,7 +51,9 @@ struct Shape {
     uint64_t *coff;
 };
 
-static Shape make_shape(const char *name, uint64_t n) {
+// in_align: the input rows' stride alignment (256, or 16: the C-ABI's minimum,
+// which bench.py's pipeline rows used for n = 16779371)
+static Shape make_shape(const char *name, uint64_t n, uint64_t in_align = 256) {
     Shape s{};
     s.name = name;
     s.n = n;
@@ -59,7 +61,7 @@ static Shape make_shape(const char *name, uint64_t n) {
     s.cols = s.C / 1024;
     s.N = 8 * s.cols;
     s.bpo = (s.cols + 7) / 8;
-    s.in_stride = (n + 255) / 256 * 256;
+    s.in_stride = (n + in_align - 1) / in_align * in_align;
     s.out_stride = (8 + 8 * s.C + 64 * (s.N - 1) + 255) / 256 * 256;
     std::vector<uint64_t> coff(s.N);
     for (uint64_t i = 0; i < s.N; ++i) coff[i] = bao::chunk_stream_off(i, s.N);
@@ -71,14 +73,17 @@ static Shape make_shape(const char *name, uint64_t n) {
 struct Variant {
     const char *label;
     void (*fn)(fused::FusedArgs);
-    int shape;  // 0: 16 MiB, 1: level-15 shape
+    int shape;  // 0: 16 MiB, 1: level-15 shape, 2: level-15 shape with 16-B row stride, 3: 16 MiB rows + 16 B
     bool full;
 };
 
 int main(int argc, char **argv) {
     const uint64_t count = argc > 1 ? atoll(argv[1]) : 256;
     const int reps = argc > 2 ? atoi(argv[2]) : 3;
-    Shape sh[2] = {make_shape("16MiB", 16ull << 20), make_shape("L15 (16779371 B)", 16779371ull)};
+    Shape sh[4] = {make_shape("16MiB", 16ull << 20), make_shape("L15 (16779371 B)", 16779371ull),
+                   make_shape("L15, 16-B row stride", 16779371ull, 16), make_shape("16MiB", 16ull << 20, 256)};
+    sh[3].in_stride = (16ull << 20) + 16;
+    sh[3].name = "16MiB, rows 16 MiB + 16 B";
     const uint64_t in_bytes = count * sh[1].in_stride, out_bytes = count * sh[1].out_stride;
     uint8_t *in, *out, *cv;
     CK(hbm::Allocator::get().alloc(in_bytes, reinterpret_cast<void **>(&in)));
@@ -113,6 +118,8 @@ int main(int argc, char **argv) {
         {"FULL DG11 no tree node stores @16MiB", zfec_bao_fused_kernel<true, true, 1, 11, 0, true, 0, 0, true, 1>, 0, true},
         {"general DG13 no level-0 CV stores @16MiB", zfec_bao_fused_kernel<true, false, 1, 13, 0, true, 1, 0, true, 1>, 0, false},
         {"general DG14 block-padded CV layout @16MiB", zfec_bao_fused_kernel<true, false, 1, 14, 0, true, 1, 0, true, 1>, 0, false},
+        {"general product @L15 16-B rows", zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, true, 1>, 2, false},
+        {"FULL product @16MiB+16 rows", zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 3, true},
         {"FULL product @16MiB (again)", zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 0, true},
         {"general product @L15 (again)", zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, true, 1>, 1, false},
     };

@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "../carbonado_amd/csrc/gf256.hpp"
-#include "../carbonado_amd/csrc/zfec_device.hpp"
+#include "zfec_variants.hpp"
 
 using namespace chip;
 using namespace chip::zf;

@@ -11,8 +11,8 @@
 #include <vector>
 
 #include "../carbonado_amd/csrc/gf256.hpp"
-#include "../carbonado_amd/csrc/zfec_device.hpp"
-#include "../carbonado_amd/csrc/bao_device.hpp"
+#include "zfec_variants.hpp"
+#include "bao_variants.hpp"
 
 using namespace chip;
 using namespace chip::zf;
