@@ -33,6 +33,12 @@
  *   - Output buffers are caller-allocated (the Rust shim does
  *     Vec::with_capacity + set_len).  Sizes are computable up front with the
  *     *_len helpers.  A too-small buffer returns CHIP_ERR_BUFFER_TOO_SMALL.
+ *   - Every entry point that fills a caller buffer and succeeds writes EVERY
+ *     byte below the length it reports in *out_len (chip_zfec_encode: all
+ *     m*chunk_len bytes), never a byte at or past out_cap: a caller may hand
+ *     over uninitialised memory (the Rust shim's set_len, the Python
+ *     wrappers' uninitialised bytes objects).  tests/test_gpu_written.py
+ *     checks it for each such entry point with 0xA5- and 0x5A-filled buffers.
  *   - Every function returns a chip_status (0 = OK).  The mapping to
  *     CarbonadoError (src/error.rs) is given per code.
  *   - Host-pointer entry points are synchronous and thread-safe (one HIP

@@ -226,3 +226,38 @@ def test_c_to_rust_mapping_rules():
     assert c_to_rust("const char *") == "*const c_char"
     assert c_to_rust("void") == "" and c_to_rust("ssize_t") == "isize"
     assert c_to_rust("const chip_ecies_inject *") == "*const chip_ecies_inject"
+
+
+def test_reroute_error_mapping():
+    """The `hip` feature's From<ChipError> (reroute.patch, error.rs) returns
+    the CPU path's own CarbonadoError variant for every status a rerouted
+    seam can return (error.rs:45-79), except too-few-shares: the CPU path's
+    ZfecError wraps a zfec_rs::Error that only the unvendored zfec-rs can
+    build, so that arm is explicit and documented."""
+    patch = (CRATE / "reroute.patch").read_text()
+    added = "\n".join(l[1:] for l in patch.splitlines() if l.startswith("+") and not l.startswith("+++"))
+    arms = dict(re.findall(r"C::(\w+)(?:\(\w+\))? => CarbonadoError::(\w+)", added))
+    assert arms == {
+        "UnevenZfecChunks": "UnevenZfecChunks",
+        "HashDecode": "HashDecodeError",
+        "BaoHashMismatch": "BaoDecodeError",
+        "BaoTruncated": "BaoDecodeError",
+        "UnnecessaryScrub": "UnnecessaryScrub",
+        "ScrubbedPaddingMismatch": "ScrubbedPaddingMismatch",
+        "InvalidScrubbedHash": "InvalidScrubbedHash",
+        "InvalidHeaderLength": "InvalidHeaderLength",
+        "Zfec": "HipError",
+    }, arms
+    assert "other => CarbonadoError::HipError(other)" in added
+    assert "HipError(carbonado_hip::ChipError)" in added
+    integ = (ROOT / "INTEGRATION.md").read_text()
+    assert "C::Zfec => CarbonadoError::ZfecError" in integ  # the arm a maintainer with zfec-rs swaps in
+    # every ChipError variant named in an arm exists in lib.rs
+    lib = _strip_comments(LIB.read_text())
+    for v in arms:
+        assert re.search(rf"\n\s+{v}(\(|,)", lib), v
+    err = REFERENCE / "src" / "error.rs"
+    if err.exists():  # the CarbonadoError variants the arms return exist in the reference
+        ref = err.read_text()
+        for v in set(arms.values()) - {"HipError"}:
+            assert re.search(rf"\n\s+{v}(\(|,)", ref), v
