@@ -676,9 +676,10 @@ class Workload:
                 return t
             return torch.empty(shape, dtype=torch.uint8, device=dev)
         self.batch_buf = batch_buf
-        # bao mode: 16-B aligned object rows for any n (the content mode's rule), handed over whole
-        # (bao, pipeline modes: 16-B aligned object rows for any n, the batch entry points' rule)
-        row = ((n + 15) // 16 * 16 if args.mode in ("bao", "pipeline", "pipeline-decode", "bao-decode") else n) + \
+        # bao, pipeline modes: object rows at a 256-B pitch for any n (the batch entry points take
+        # 16-B multiples; at 16 B every 128-B piece a wave loads straddles two lines and K13 fetches
+        # 1.21x the input, tools/k13_fetch, profiles/r10c_session), handed over whole
+        row = ((n + 255) // 256 * 256 if args.mode in ("bao", "pipeline", "pipeline-decode", "bao-decode") else n) + \
             args.in_pad_kib * 1024
         self.inp_full = batch_buf((count, row), "in")
         self.inp = self.inp_full[:, :n] if row != n else self.inp_full
@@ -711,7 +712,7 @@ class Workload:
                 raise SystemExit("--mode pipeline runs the device-only levels (Bao/Zfec bits); use --mode e2e")
             zlen = m * C if lv & 8 else n
             self.blen = blen = L.chip_bao_encoded_len(zlen) if lv & 4 else zlen
-            self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
+            self.out = batch_buf((count, (blen + 255) // 256 * 256), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.encode_scratch(lv, n, count, dev)
             self.step = lambda: device.encode_batch(lv, self.inp_full, n, self.out, self.hashes, self.scratch)
@@ -742,14 +743,14 @@ class Workload:
             zlen = m * C if lv & 8 else n
             self.blen = blen = L.chip_bao_encoded_len(zlen) if lv & 4 else zlen
             self.zlen = zlen
-            self.enc = batch_buf((count, (blen + 15) // 16 * 16), "enc")
+            self.enc = batch_buf((count, (blen + 255) // 256 * 256), "enc")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             esc = device.encode_scratch(lv, n, count, dev)
             _, info = device.encode_batch(lv, self.inp_full, n, self.enc, self.hashes, esc)
             torch.cuda.synchronize()
             del esc
             self.pad = info.padding_len
-            self.out = batch_buf((count, (n + 15) // 16 * 16), "out")
+            self.out = batch_buf((count, (n + 255) // 256 * 256), "out")
             self.status = torch.full((count,), -1, dtype=torch.int32, device=dev)
             self.scratch = device.decode_scratch(lv, blen, count, dev)
             self.step = lambda: device.decode_batch(lv, self.enc, blen, self.hashes, self.pad, self.out, self.status,
@@ -796,7 +797,7 @@ class Workload:
             zlen = m * C
             self.zlen = zlen
             self.blen = blen = L.chip_bao_encoded_len(zlen)
-            row = (blen + 15) // 16 * 16
+            row = (blen + 255) // 256 * 256
             self.enc = batch_buf((count, row), "enc")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             esc = device.encode_scratch(12, n, count, dev)
@@ -990,7 +991,7 @@ class Workload:
             self.kernel_sym = "e2e"
         elif args.mode == "bao-decode":
             blen = L.chip_bao_encoded_len(n)
-            self.enc = batch_buf((count, (blen + 15) // 16 * 16), "enc")
+            self.enc = batch_buf((count, (blen + 255) // 256 * 256), "enc")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.bao_scratch(n, count, dev)
             device.bao_encode_batch(self.inp_full, n, self.enc, self.hashes, self.scratch)
@@ -1002,7 +1003,7 @@ class Workload:
             self.kernel_sym = "bao_chunk_kernel_verify"
         else:
             self.blen = blen = L.chip_bao_encoded_len(n)
-            self.out = batch_buf((count, (blen + 15) // 16 * 16), "out")
+            self.out = batch_buf((count, (blen + 255) // 256 * 256), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.bao_scratch(n, count, dev)
             self.step = lambda: device.bao_encode_batch(self.inp_full, n, self.out, self.hashes, self.scratch)

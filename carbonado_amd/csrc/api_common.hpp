@@ -119,6 +119,12 @@ hipError_t h2d(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s)
 // HBM -> host after the work already on s; returns when `dst` holds the bytes
 hipError_t d2h(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s);
 
+// Pitch of the device rows the library lays out itself (slot buffers): a
+// multiple of 256 B, so every row's shards start on a 128-B line.  With
+// 16-B rows each 128-B piece a wave loads straddles two lines and K13 /
+// K1 fetch 1.21x the input bytes (tools/k13_fetch, profiles/r10c_session).
+inline uint64_t row_pitch(uint64_t n) { return (n + 255) / 256 * 256; }
+
 // ---- plans and geometry (api_plans.cpp) ------------------------------------
 int env_int(const char *name, int dflt);
 bool valid_km(uint32_t k, uint32_t m);

@@ -101,7 +101,7 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
     if (slice_bytes == 0) slice_bytes = 256ull << 20;
     uint32_t T = host_threads ? host_threads : std::max(1u, std::thread::hardware_concurrency());
     T = std::min<uint32_t>(T, 64);
-    const uint64_t i_al = (in_max + 15) / 16 * 16, m_al = (mid_max + 15) / 16 * 16, o_al = (olen_max + 15) / 16 * 16;
+    const uint64_t i_al = row_pitch(in_max), m_al = row_pitch(mid_max), o_al = (olen_max + 15) / 16 * 16;
     uint64_t S = slice_bytes / (in_max ? in_max : 1);
     S = S < 1 ? 1 : (S > count ? count : S);
     if (c->slots.size() < nslots) c->slots.resize(nslots);

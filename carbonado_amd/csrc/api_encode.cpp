@@ -218,12 +218,12 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
                        uint64_t cnt, uint8_t *out, uint64_t out_pitch, uint8_t *hashes,
                        const SplitGeo *split = nullptr, bool from_rows = false) {
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
-    const uint64_t n_al = (cur_n + 15) / 16 * 16, z_al = (zlen + 15) / 16 * 16, f_al = (final_len + 15) / 16 * 16;
+    const uint64_t n_al = row_pitch(cur_n), z_al = row_pitch(zlen), f_al = row_pitch(final_len);
     uint8_t *d_in = static_cast<uint8_t *>(sl.in.p);
     if (from_rows && split && cur_n) {
         // the host stage wrote each object's zfec input into its stream's chunk slots
         // in out: the data regions come over and the chunks are gathered into rows
-        const uint64_t t_al = (split->t0 + 15) / 16 * 16;
+        const uint64_t t_al = row_pitch(split->t0);
         uint8_t *d_sin = static_cast<uint8_t *>(sl.sin.p);
         CHIP_HIP(hipMemcpy2DAsync(d_sin, t_al, out, out_pitch, split->t0, cnt, hipMemcpyHostToDevice, sl.stream));
         CHIP_HIP(bao_gather_rows(d_sin, t_al, split->N, cnt, cur_n, d_in, n_al, sl.stream));
@@ -340,10 +340,10 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
         for (uint32_t k = 0; k < nslots; ++k) {
             Slot &sl = c->slots[k];
             if (!sl.stream) CHIP_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-            CHIP_HIP(grow(sl.in, S * h_al));
-            if (zfec && !bao) CHIP_HIP(grow(sl.mid, S * ((zlen_max + 15) / 16 * 16)));  // Zfec|Bao: fused
+            CHIP_HIP(grow(sl.in, S * row_pitch(h_max)));
+            if (zfec && !bao) CHIP_HIP(grow(sl.mid, S * row_pitch(zlen_max)));  // Zfec|Bao: fused
             if (bao) {
-                CHIP_HIP(grow(sl.out, S * ((final_max + 15) / 16 * 16)));
+                CHIP_HIP(grow(sl.out, S * row_pitch(final_max)));
                 CHIP_HIP(grow(sl.scratch, zfec ? std::max(zfec_bao_scratch_len(zlen_max, S), bao_scratch_len(zlen_max, S))
                                                 : bao_scratch_len(zlen_max, S)));
             }
@@ -352,7 +352,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             if (split_fmt) {  // the data region's nodes: fewer than the stream's N chunks
                 CHIP_HIP(grow(sl.nodes, S * 64 * (zlen_max / 1024)));
                 CHIP_HIP(grow_pinned(sl.hnodes, S * 64 * (zlen_max / 1024)));
-                if (direct_fmt) CHIP_HIP(grow(sl.sin, S * ((geos.get(zlen_max / 1024).t0 + 15) / 16 * 16)));
+                if (direct_fmt) CHIP_HIP(grow(sl.sin, S * row_pitch(geos.get(zlen_max / 1024).t0)));
             }
         }
     }

@@ -317,7 +317,10 @@ CHIP_API int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8
  * (bytes beyond n inside the padded object read as zero, exactly as
  * encoding.rs:53-55 pads), its m*chunk_len-byte output at d_out + o*out_stride.
  * d_in, d_out, in_stride and out_stride must be multiples of 16
- * (CHIP_ERR_INVALID_ARG otherwise).  Every batch entry point below refuses
+ * (CHIP_ERR_INVALID_ARG otherwise); multiples of 256 are the fast layout (every
+ * row's shards then start on a 128-B memory line: at a 16-B pitch each piece
+ * a wave loads straddles two lines and the kernels fetch 1.21x the input,
+ * DESIGN.md §2).  Every batch entry point below refuses
  * (CHIP_ERR_INVALID_ARG) strides under the row length when count > 1: rows
  * would overlap.
  * In place: d_out == d_in (and out_stride == in_stride) means each object's
