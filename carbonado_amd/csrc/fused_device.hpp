@@ -61,7 +61,25 @@ struct FusedArgs {
     uint8_t *cv;                    // level-0 CVs [count][N], or level-3 CVs [count][cvs] (FULL)
     uint32_t *queue;                // block queue (DQ): [0] next block, [32] waves done; zero at launch
     uint64_t cvs;                   // FULL: level-3 CVs per object = ceil(N / 8)
+    uint8_t *cv3;                   // RT: level-3 CVs [count][cvs] (the groups the waves complete)
 };
+
+// RT (general path, runs of RT blocks): whether the aligned 8-chunk group g
+// of a stream of 8 shards of `cols` chunk-columns each is completed inside a
+// wave.  The group's chunks must lie in one shard t, at columns [u0, u0 + 8);
+// its last column lies in block (u0 + 7) / 8, which completes it; the part
+// before that block (u0 % 8 != 0: rows whose shard starts off the 8-chunk
+// grid) lies in the previous block, processed by the same wave just before
+// unless the completing block starts a run.  Everything else (groups across
+// two shards, groups across a run boundary) is completed by the level-1-3
+// pass from the level-0 CVs the waves store for exactly those chunks.
+__host__ __device__ inline bool group_in_wave(uint64_t g, uint64_t cols, uint64_t bpo, uint64_t rt) {
+    const uint64_t c0 = 8 * g, t = c0 / cols;
+    if ((c0 + 7) / cols != t) return false;
+    const uint64_t u0 = c0 - t * cols, b = (u0 + 7) / 8;
+    if (b >= bpo) return false;
+    return u0 % 8 == 0 || b % rt != 0;
+}
 
 __device__ __forceinline__ int dofs(int step) { return 4 + (step & 1) * 32; }
 
@@ -199,7 +217,7 @@ struct Tree {
 // fused_kernels.hip wraps in kernels of their own (zfec_bao_fused_kernel_full,
 // _general, bao_content_fused_kernel), the tuner's are tools/fused_variants.hpp's.
 template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
-          bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false, int PRIO = 0>
+          bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false, int PRIO = 0, int RT = 0>
 __device__ __forceinline__ void zfec_bao_fused_body(const FusedArgs &a) {
     static_assert(KIND == 0 || FULL, "content bao: FULL blocks only");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -272,7 +290,12 @@ __device__ __forceinline__ void zfec_bao_fused_body(const FusedArgs &a) {
         }
     };
 
-    Tree<NT> tree(lane, a.cv);
+    // RT > 0 (general path): the blocks come in runs of RT consecutive blocks of
+    // one object (the queue hands out runs), so a wave holds each block's
+    // predecessor and completes levels 1-3 of the aligned groups that start
+    // in it (group_in_wave), as the FULL path does for all groups
+    constexpr bool RUNS = !FULL && RT > 0 && KIND == 0;
+    Tree<NT> tree(lane, RUNS ? a.cv3 : a.cv);
     tree.wr = DG != 11;
     // Blocks: DQ takes them from a queue (one atomic per block and wave, lane
     // 0, vector memory), so waves on slower XCDs simply take fewer; otherwise
@@ -283,14 +306,33 @@ __device__ __forceinline__ void zfec_bao_fused_body(const FusedArgs &a) {
         if (lane == 0) b = atomicAdd(a.queue, 1u);
         return (uint64_t)__builtin_amdgcn_readfirstlane(b);
     };
-    uint64_t blk = DQ ? grab() : (uint64_t)blockIdx.x * WPG + wave;
+    const uint64_t rpo = RUNS ? (a.bpo + RT - 1) / RT : 1;  // runs per object
+    uint64_t run_last = 0, srun = (uint64_t)blockIdx.x * WPG + wave;
+    auto run_first = [&](uint64_t r) -> uint64_t {  // first block of run r (total: none left)
+        if (r >= a.count * rpo) return total;
+        const uint64_t o = r / rpo, b0 = o * a.bpo + (r - o * rpo) * RT;
+        run_last = (b0 + RT < (o + 1) * a.bpo ? b0 + RT : (o + 1) * a.bpo) - 1;
+        return b0;
+    };
+    auto next_block = [&](uint64_t b) -> uint64_t {
+        if (RUNS) {
+            if (b < run_last) return b + 1;
+            if (!DQ) srun += GW;
+            return run_first(DQ ? grab() : srun);
+        }
+        return DQ ? grab() : b + GW;
+    };
+    uint64_t blk = RUNS ? run_first(DQ ? grab() : srun) : DQ ? grab() : (uint64_t)blockIdx.x * WPG + wave;
+    uint32_t hp[8];  // RUNS: the previous block's chunk CVs
+#pragma unroll
+    for (int w = 0; w < 8; ++w) hp[w] = 0u;
     u32x4 v[NV], v2[NV];  // this step's loads; ORD 3: the next step's too
     if (blk < total) {
         load_step(blk, 0, v);
         if (ORD == 3) load_step(blk, 1, v2);
     }
     for (uint64_t nxt; blk < total; blk = nxt) {
-        nxt = DQ ? grab() : blk + GW;
+        nxt = next_block(blk);
         const uint64_t obj = blk / a.bpo, ub = (blk - obj * a.bpo) * BW;
         uint8_t *ob = a.out + obj * a.out_stride;
         if (ub == 0 && lane == 0)  // u64 LE content length
@@ -548,6 +590,30 @@ __device__ __forceinline__ void zfec_bao_fused_body(const FusedArgs &a) {
         }
         if (FULL) {
             tree.step(h, ob + hco - 64, obj * 8 * a.cvs + ci, true);
+        } else if (RUNS) {
+            // row t's aligned group that this block completes: columns [ub - d, ub - d + 8),
+            // element j held by lane 8t + ((j - d) & 7) of this block (j >= d) or of the
+            // previous one (j < d), d = the row's offset from the 8-chunk grid
+            const int t = lane >> 3, j = lane & 7;
+            const uint32_t d = (uint32_t)(((uint64_t)t * a.cols) & 7);
+            const uint64_t gc0 = (uint64_t)t * a.cols + ub - d;  // its first chunk
+            const bool ok = ub >= d && group_in_wave(gc0 / 8, a.cols, a.bpo, RT);
+            const int src = (lane & ~7) | ((j - (int)d) & 7);
+            uint32_t g[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                const uint32_t x = (uint32_t)__shfl((int)h[w], src), y = (uint32_t)__shfl((int)hp[w], src);
+                g[w] = j >= (int)d ? x : y;
+                hp[w] = h[w];
+            }
+            const uint64_t ec = gc0 + j;  // my element's chunk
+            tree.step(g, ob + (ok ? a.coff[ec] : 64) - 64, obj * 8 * a.cvs + ec, ok);
+            // my own chunk's level-0 CV when its group is left to the level-1-3 pass
+            if (mine && !group_in_wave(ci / 8, a.cols, a.bpo, RT)) {
+                auto *cvp = bao::glb(reinterpret_cast<u32x4 *>(a.cv + (obj * a.N + ci) * 32));
+                cvp[0] = u32x4{h[0], h[1], h[2], h[3]};
+                cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
+            }
         } else if (mine && DG != 13) {
             const uint64_t cvi = DG == 14 ? obj * 8 * (8 * a.bpo) + (uint64_t)(lane >> 3) * (8 * a.bpo) + hu
                                           : obj * a.N + ci;
@@ -556,7 +622,7 @@ __device__ __forceinline__ void zfec_bao_fused_body(const FusedArgs &a) {
             cvp[1] = u32x4{h[4], h[5], h[6], h[7]};
         }
     }
-    if (FULL) {  // drain: level 2 of the last block, level 3 of the last two
+    if (FULL || RUNS) {  // drain: level 2 of the last block, level 3 of the last two
         uint32_t z[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
         tree.step(z, nullptr, 0, false);
         tree.step(z, nullptr, 0, false);
@@ -703,15 +769,19 @@ __global__ __launch_bounds__(256) void bao_levels123_kernel(const uint8_t *cv0, 
 // level's nodes go to LDS first, then the wave writes them four lanes per
 // node, 16 nodes (64 contiguous bytes each) per store instruction instead of
 // 64 lanes at 64 places 8 KiB apart.
+// rt > 0: only the groups K13's run mode left (group_in_wave false; cols,
+// bpo: the zfec shards' chunk-columns and K13's blocks per object).
 __global__ __launch_bounds__(64) void bao_levels123_lds_kernel(const uint8_t *cv0, uint64_t N, uint64_t count,
                                                                const uint64_t *coff, uint8_t *out,
-                                                               uint64_t out_stride, uint8_t *cv3, uint64_t n3) {
+                                                               uint64_t out_stride, uint8_t *cv3, uint64_t n3,
+                                                               uint64_t cols = 0, uint64_t bpo = 0, uint64_t rt = 0) {
     __shared__ bao::u32x4 buf[64 * 4 * 4];  // [lane][node][16-B unit] of the current level
     __shared__ uint64_t naddr[64 * 4];      // [lane][node]: its slot (0: not a real node)
     const int lane = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
-    const bool on = gid < count * n3;
+    bool on = gid < count * n3;
     const uint64_t obj = on ? gid / n3 : 0, g = on ? gid - obj * n3 : 0, s0 = 8 * g;
+    if (rt && on && group_in_wave(g, cols, bpo, rt)) on = false;  // completed in K13's wave
     const uint32_t cnt = !on ? 0u : (N - s0 < 8 ? (uint32_t)(N - s0) : 8u);
     uint32_t c[8][8];
 #pragma unroll

@@ -443,3 +443,36 @@ def test_decode_batch_dev_errors(gpu):
     torch.cuda.synchronize()
     assert status.cpu().tolist() == [5, 0]
     enc[0, :8] = hdr
+
+
+@pytest.mark.parametrize("cols", [129, 130, 131, 132, 133, 134, 135, 136, 257, 4097])
+def test_encode_batch_dev_k13_runs(gpu, cols):
+    """K13's general path in run mode (fused_device.hpp RT: blocks in runs of
+    16, levels 1-3 of the aligned groups done in the wave, the rest from the
+    level-0 CVs): shards of `cols` chunk-columns, so every offset of a shard
+    from the 8-chunk grid (cols % 8 = 1..7, and 0 with zfec padding), 17 to
+    513 blocks per object (several runs, ragged last run), three objects in
+    one launch — every stream and hash == the oracle's encode() level 12."""
+    import torch
+    from carbonado_amd import device
+    count = 3
+    rng = np.random.default_rng(cols)
+    n = (cols - 1) * 4096 + int(rng.integers(1, 4096))  # zfec padding > 0: the general path
+    stride = (n + 255) // 256 * 256
+    host = rng.integers(0, 256, (count, stride), dtype=np.uint8)
+    inp = torch.from_numpy(host).cuda()
+    oenc0, _, _ = O.encode(host[0, :n].tobytes(), 12)
+    ostride = (len(oenc0) + 255) // 256 * 256
+    out = torch.full((count, ostride), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.full((count, 32), 0x5A, dtype=torch.uint8, device="cuda")
+    scratch = device.encode_scratch(12, n, count)
+    olen, info = device.encode_batch(12, inp, n, out, hashes, scratch)
+    torch.cuda.synchronize()
+    assert info.chunk_len == cols * 1024
+    got, gh = out.cpu().numpy(), hashes.cpu().numpy()
+    for o in range(count):
+        enc, h, _ = O.encode(host[o, :n].tobytes(), 12)
+        assert olen == len(enc)
+        assert got[o, :olen].tobytes() == enc, o
+        assert (got[o, olen:] == 0xA5).all()
+        assert gh[o].tobytes() == h

@@ -17,9 +17,9 @@ namespace fused {
 // own kernel.  The library instantiates only the configurations it ships
 // (fused_kernels.hip: zfec_bao_fused_kernel_full / _general, ...).
 template <bool NT, bool FULL, int ORD = 1, int DG = 0, int KIND = 0, bool DQ = true, int MP = 0, int SS = 0,
-          bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false, int PRIO = 0>
+          bool O32 = false, int GFP = 0, int WPG = FW, bool NTL = false, int PRIO = 0, int RT = 0>
 __global__ __launch_bounds__(64 * WPG) void zfec_bao_fused_kernel(FusedArgs a) {
-    zfec_bao_fused_body<NT, FULL, ORD, DG, KIND, DQ, MP, SS, O32, GFP, WPG, NTL, PRIO>(a);
+    zfec_bao_fused_body<NT, FULL, ORD, DG, KIND, DQ, MP, SS, O32, GFP, WPG, NTL, PRIO, RT>(a);
 }
 
 // K13S (tools/fused_tune only; measured 15-20 % SLOWER than K13, profiles/r7j,

@@ -90,6 +90,8 @@ int main(int argc, char **argv) {
     CK(hbm::Allocator::get().alloc(out_bytes, reinterpret_cast<void **>(&out)));
     const uint64_t cv_bytes = count * 8 * (8 * sh[1].bpo) * 32;  // >= count * N * 32 for both shapes
     CK(hipMalloc(&cv, cv_bytes));
+    uint8_t *cv3;  // run mode: level-3 CVs
+    CK(hipMalloc(&cv3, count * sh[1].N / 8 * 32));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, in_bytes / 8, 0xCA4B0AD0ull);
     CK(hipMemset(out, 0, out_bytes));
     std::vector<uint8_t> enc = zfec_enc_matrix(4, 8);
@@ -122,6 +124,11 @@ int main(int argc, char **argv) {
         {"FULL product @16MiB+16 rows", zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 3, true},
         {"FULL product @16MiB (again)", zfec_bao_fused_kernel<true, true, 1, 0, 0, true, 0, 0, true, 1>, 0, true},
         {"general product @L15 (again)", zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, true, 1>, 1, false},
+        {"general RT16 MP0 @L15 (run mode)", zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 0, 0, true, 1, 8, false, 0, 16>, 1, false},
+        {"general RT16 MP1 @L15", zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, true, 1, 8, false, 0, 16>, 1, false},
+        {"general RT8 MP0 @L15", zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 0, 0, true, 1, 8, false, 0, 8>, 1, false},
+        {"general RT32 MP0 @L15", zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 0, 0, true, 1, 8, false, 0, 32>, 1, false},
+        {"general product @L15 (third)", zfec_bao_fused_kernel<true, false, 1, 0, 0, true, 1, 0, true, 1>, 1, false},
     };
     for (const auto &v : vs)
         CK(hipFuncSetAttribute(reinterpret_cast<const void *>(v.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -139,6 +146,7 @@ int main(int argc, char **argv) {
         a.out = out; a.out_stride = s.out_stride;
         a.count = count; a.N = s.N; a.cols = s.cols; a.bpo = s.bpo;
         a.table = dtab; a.coff = s.coff; a.cv = cv; a.queue = dq; a.cvs = s.N / 8;
+        a.cv3 = cv3;
         if (v.full && (s.cols % 8 || s.n < 4 * s.C)) { fprintf(stderr, "FULL needs cols %% 8 == 0\n"); return 1; }
         const uint64_t blocks = count * s.bpo;
         const unsigned grid = (unsigned)std::min<uint64_t>(256, (blocks + fused::FW - 1) / fused::FW);
