@@ -173,6 +173,51 @@ void run_threads(uint32_t nt, const std::function<void(uint32_t)> &fn) {
     for (auto &th : pool) th.join();
 }
 
+// CHIP_ECIES_PREP=0: each object's scalar multiplications inside its host stage
+bool ecies_prep_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_ECIES_PREP");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    return on;
+}
+
+// The ECIES key material of a slice's objects (host::ecies_prepare: two
+// scalar multiplications each, no data) computed on nt threads while the
+// caller waits for the slice's slot: the slot wait is host time the data
+// stages cannot use, the key material is the part of them that does not
+// need the data.  The caller claims objects too once its wait is over.
+struct KeyPrep {
+    std::vector<host::EciesKey> keys;
+    std::vector<int> sts;
+    std::atomic<uint64_t> next{0};
+    uint64_t cnt = 0;
+    const uint8_t *peer = nullptr, *eph = nullptr;  // eph: injected secrets of the slice's objects
+    std::vector<std::thread> pool;
+    void claim() {
+        for (uint64_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < cnt;)
+            sts[j] = host::ecies_prepare(peer, eph ? eph + 32 * j : nullptr, &keys[j]);
+    }
+    void start(uint32_t nt, const uint8_t *peer_, const uint8_t *eph_, uint64_t cnt_) {
+        if (keys.size() < cnt_) keys.resize(cnt_), sts.resize(cnt_);
+        peer = peer_, eph = eph_, cnt = cnt_;
+        next.store(0, std::memory_order_relaxed);
+        for (uint32_t t = 0; t < nt; ++t) pool.emplace_back([this] { claim(); });
+    }
+    void finish() {
+        claim();
+        for (auto &th : pool) th.join();
+        pool.clear();
+    }
+    void wipe() {
+        for (uint64_t j = 0; j < cnt; ++j) host::ecies_key_wipe(&keys[j]);
+    }
+    ~KeyPrep() {
+        for (auto &th : pool) th.join();
+        wipe();
+    }
+};
+
 // CHIP_E2E_TRACE=1: where a chip_encode_host_batch call's wall time went
 // (host work of the slices on their threads, waits for a slot's stream, the final
 // drain), one line on stderr per call
@@ -182,7 +227,7 @@ struct CallTrace {
         return v && v[0] == '1';
     }();
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    double host = 0, host_max = 0, wait = 0, drain = 0;
+    double host = 0, host_max = 0, wait = 0, drain = 0, prep = 0;
     double now() const {
         return on ? std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() : 0.0;
     }
@@ -190,9 +235,9 @@ struct CallTrace {
         if (!on) return;
         std::fprintf(stderr,
                      "[chip e2e] %llu slices of %llu: wall %.1f ms, host %.1f ms (slice max %.2f), "
-                     "slot waits %.1f ms, drain %.1f ms\n",
+                     "slot waits %.1f ms (with ECIES key prep %.1f ms), drain %.1f ms\n",
                      (unsigned long long)slices, (unsigned long long)S, now() * 1e3, host * 1e3, host_max * 1e3,
-                     wait * 1e3, drain * 1e3);
+                     wait * 1e3, prep * 1e3, drain * 1e3);
     }
 };
 
@@ -365,6 +410,15 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     std::vector<uint8_t> in_rows(S);  // object's data region written straight into out (direct)
     CallTrace tr;
     std::vector<Scratch> scratch(T);  // per host thread, reused across slices
+    // ECIES on the streaming path: the receiver key parsed once, each slice's
+    // key material prepared during its slot wait (KeyPrep)
+    const bool prep = (format & CHIP_FORMAT_ECIES) && stream_encrypt_on() && ecies_prep_on();
+    uint8_t peer[65];
+    if (prep) {
+        st = host::ecies_peer(pubkey, pubkey_len, peer);
+        if (st != CHIP_OK) return st;
+    }
+    KeyPrep kp;
     auto drain = [&]() {
         if (c)
             for (uint32_t k = 0; k < nslots; ++k) (void)hipStreamSynchronize(c->slots[k].stream);
@@ -372,10 +426,29 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     const uint64_t nslices = (count + S - 1) / S;
     for (uint64_t i = 0; i < nslices; ++i) {
         Slot *sl = c ? &c->slots[i % nslots] : nullptr;
-        const double t_a = tr.now();
-        if (sl && i >= nslots) CHIP_HIP(hipStreamSynchronize(sl->stream));  // slot's previous slice is done
-        tr.wait += tr.now() - t_a;
         const uint64_t o0 = i * S, cnt = (count - o0) < S ? (count - o0) : S;
+        if (prep)
+            kp.start(std::min<uint64_t>(T, cnt), peer,
+                     inject && inject->ephemeral_sk ? inject->ephemeral_sk + 32 * o0 : nullptr, cnt);
+        const double t_a = tr.now();
+        if (sl && i >= nslots) {
+            const hipError_t e = hipStreamSynchronize(sl->stream);  // slot's previous slice is done
+            if (e != hipSuccess) {
+                kp.finish();
+                set_device_error(e);
+                return CHIP_ERR_DEVICE;
+            }
+        }
+        tr.wait += tr.now() - t_a;
+        if (prep) {
+            kp.finish();
+            tr.prep += tr.now() - t_a;
+            for (uint64_t j = 0; j < cnt; ++j)
+                if (kp.sts[j] != CHIP_OK) {
+                    drain();
+                    return kp.sts[j];
+                }
+        }
         const uint8_t *src = in + o0 * in_stride;
         uint64_t src_pitch = count > 1 ? in_stride : n;
         uint64_t cur_n = n;
@@ -410,7 +483,8 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                                                                                  : nullptr,
                                                   inject && inject->nonce ? inject->nonce + 16 * o : nullptr, obj, n,
                                                   direct ? nullptr : stage + j * h_al, h_al, tmp, &len[j], &bc[j],
-                                                  &be[j], g_pred ? &sink : nullptr, &filled);
+                                                  &be[j], g_pred ? &sink : nullptr, &filled,
+                                                  prep ? &kp.keys[j] : nullptr);
                         if (sts[j] != CHIP_OK) continue;
                         olen = len[j];
                         if (direct) {
@@ -448,6 +522,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             tr.host += dh;
             tr.host_max = std::max(tr.host_max, dh);
             pp = SplitPending{};
+            if (prep) kp.wipe();
             if (hs) {
                 for (uint64_t j = 0; j < cnt; ++j)
                     if (sts[j] != CHIP_OK) {

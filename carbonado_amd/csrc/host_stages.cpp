@@ -523,6 +523,67 @@ int ecies_public_key(const uint8_t *secret, uint8_t out[65]) {
     return CHIP_OK;
 }
 
+int ecies_peer(const uint8_t *pubkey, uint64_t pubkey_len, uint8_t peer[65]) {
+    PtPtr pt(parse_public(pubkey, pubkey_len));
+    if (!pt.p) return CHIP_ERR_ECIES;
+    BnPtr x(BN_new()), y(BN_new());
+    if (!x.p || !y.p || EC_POINT_get_affine_coordinates(ec().g, pt.p, x.p, y.p, ec().bn) != 1 ||
+        BN_bn2binpad(x.p, peer + 1, 32) != 32 || BN_bn2binpad(y.p, peer + 33, 32) != 32)
+        return CHIP_ERR_ECIES;
+    peer[0] = 0x04;
+    return CHIP_OK;
+}
+
+// 0 < k < n (libsecp256k1 SecretKey::parse), without BIGNUM arithmetic
+static bool scalar_ok(const uint8_t k[32]) {
+    uint64_t x[4];
+    for (int i = 0; i < 4; ++i) {
+        uint64_t w = 0;
+        for (int j = 0; j < 8; ++j) w = (w << 8) | k[(3 - i) * 8 + j];
+        x[i] = w;
+    }
+    unsigned long long t;
+    unsigned char b = _subborrow_u64(0, x[0], k1::N0, &t);
+    b = _subborrow_u64(b, x[1], k1::N1, &t);
+    b = _subborrow_u64(b, x[2], k1::N2, &t);
+    b = _subborrow_u64(b, x[3], k1::N3, &t);
+    return b && (x[0] | x[1] | x[2] | x[3]) != 0;
+}
+
+int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out) {
+    uint8_t sk[32];
+    if (eph_sk) {
+        std::memcpy(sk, eph_sk, 32);
+        if (!scalar_ok(sk)) return CHIP_ERR_ECIES;
+    } else {
+        do {  // SecretKey::random: rejection-sample a valid scalar
+            if (RAND_bytes(sk, 32) != 1) return CHIP_ERR_ECIES;
+        } while (!scalar_ok(sk));
+    }
+    uint8_t master[130];
+    bool ok = k1::to65(k1::mul_g(sk), out->eph_pub);
+    std::memcpy(master, out->eph_pub, 65);
+    ok = ok && k1::to65(k1::mul(sk, k1::fe_from_be(peer + 1), k1::fe_from_be(peer + 33)), master + 65);
+    OPENSSL_cleanse(sk, sizeof sk);
+    ok = ok && hkdf_sha256_32(master, 130, out->key);
+    OPENSSL_cleanse(master, sizeof master);
+    return ok ? CHIP_OK : CHIP_ERR_ECIES;
+}
+
+void ecies_key_wipe(EciesKey *k) { OPENSSL_cleanse(k, sizeof *k); }
+
+// Header and cipher context from prepared key material (ecies_prepare).
+static int ecies_begin_prepared(const EciesKey &k, const uint8_t *nonce, uint8_t *out, EVP_CIPHER_CTX *c) {
+    std::memcpy(out, k.eph_pub, 65);
+    uint8_t *iv = out + 65;
+    if (nonce) std::memcpy(iv, nonce, 16);
+    else if (RAND_bytes(iv, 16) != 1) return CHIP_ERR_ECIES;
+    const bool ok = c && EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+                    EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
+                    EVP_EncryptInit_ex(c, nullptr, nullptr, k.key, iv) == 1;
+    return ok ? CHIP_OK : CHIP_ERR_ECIES;
+}
+
 // ECIES header (ephemeral public key, nonce) into out[0, 81) and the
 // AES-256-GCM context keyed for the ciphertext at out + 97; the tag goes to
 // out[81, 97) when the ciphertext is done.
@@ -910,7 +971,7 @@ static_assert(SNAP_ECIES_WINDOW / 2 >= MAX_COMPRESS_BLOCK && SNAP_ECIES_WINDOW /
 
 int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                          const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
-                         uint8_t *window, const ChunkSink *sink, uint64_t *filled) {
+                         uint8_t *window, const ChunkSink *sink, uint64_t *filled, const EciesKey *prepared) {
     const uint64_t m = snap ? snap_max_len(n) : n;
     if (out && cap < m + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
     if (!out && !(sink && sink->complete)) return CHIP_ERR_INVALID_ARG;
@@ -919,7 +980,8 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
     uint8_t head[97];
     uint8_t *hdr = out ? out : head;
     CipherCtx cc;
-    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, hdr, cc.c);
+    int st = prepared ? ecies_begin_prepared(*prepared, nonce, hdr, cc.c)
+                      : ecies_begin(pubkey, pubkey_len, eph_sk, nonce, hdr, cc.c);
     if (st != CHIP_OK) return st;
     uint8_t *ct = out ? out + 97 : nullptr;
     uint8_t *piece = window + SNAP_ECIES_WINDOW / 2;  // one block's ciphertext (the sink path)

@@ -43,6 +43,21 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
 // Public key (65 B uncompressed) of a 32-byte secret; for tests and tooling.
 int ecies_public_key(const uint8_t *secret, uint8_t out[65]);
 
+// The key material of one ecies_encrypt, split from the bytes: the ephemeral
+// public key (the envelope's first 65 bytes) and the AES-256-GCM key.  Its
+// cost is two scalar multiplications, independent of the data, so a batch
+// computes it ahead (encode() from host memory: while the slice's slot is
+// still busy on the device).  ecies_peer parses and checks the receiver key
+// once per batch (65 B uncompressed out); ecies_prepare draws (eph_sk null)
+// or takes the ephemeral secret.  A prepared key is used once, then wiped.
+struct EciesKey {
+    uint8_t eph_pub[65];
+    uint8_t key[32];
+};
+int ecies_peer(const uint8_t *pubkey, uint64_t pubkey_len, uint8_t peer[65]);
+int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out);
+void ecies_key_wipe(EciesKey *k);
+
 // memcpy into pinned staging memory that only the DMA engine reads next:
 // non-temporal (streaming) stores skip the read-for-ownership of every
 // destination line and keep it out of the CPU caches (AVX2; memcpy without
@@ -80,9 +95,11 @@ struct ChunkSink {
 // caller zeroes [*filled, nd) once the geometry is confirmed.  Output
 // identical to snap_compress + ecies_encrypt.
 constexpr uint64_t SNAP_ECIES_WINDOW = 2 * (64 + 65536 + 65536 / 6);
+// prepared: the key material from ecies_prepare (pubkey / eph_sk unused then).
 int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                          const uint8_t *in, uint64_t n, bool snap, uint8_t *out, uint64_t cap, uint64_t *out_len,
-                         uint8_t *window, const ChunkSink *sink, uint64_t *filled);
+                         uint8_t *window, const ChunkSink *sink, uint64_t *filled,
+                         const EciesKey *prepared = nullptr);
 // snap_compress with the same sink (encode() at Snappy|Zfec|Bao): the frame's
 // chunks [0, *filled) placed as they complete, `out` optional when complete.
 int snap_compress_stream(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,

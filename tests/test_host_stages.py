@@ -379,3 +379,33 @@ def test_encode_host_batch_host_levels(ca, threads):
         for o in range(count):
             enc, _, _ = O.encode_full(inp[o].numpy().tobytes(), level, pub, eph[o].tobytes(), nonce[o].tobytes())
             assert out[o, :olen[o]].numpy().tobytes() == enc, (level, o)
+
+
+def test_encode_host_batch_ecies_key_prep(ca):
+    """The batch prepares each object's ECIES key material during its slice's
+    slot wait (api_encode.cpp KeyPrep): drawn ephemeral keys still differ per
+    object and decrypt with the receiver's secret; a bad receiver key or an
+    injected ephemeral secret outside (0, n) fails the call as ecies() does."""
+    import torch
+    from carbonado_amd import device
+    from carbonado_amd.error import EciesError
+    sk = H.sha256(b"prep receiver")
+    pub = H.public_key(sk)
+    n, count = 3000, 9
+    inp = torch.from_numpy(np.random.default_rng(5).integers(0, 256, (count, n), dtype=np.uint8))
+    cap = device._lib.lib().chip_encode_max_len(n)
+    out = torch.zeros((count, cap), dtype=torch.uint8)
+    hashes = torch.zeros((count, 32), dtype=torch.uint8)
+    olen, _ = device.encode_host_batch(1, inp, n, out, hashes, 2, slice_bytes=4 * n, pubkey=pub, host_threads=3)
+    heads = {out[o, :65].numpy().tobytes() for o in range(count)}
+    assert len(heads) == count
+    for o in range(count):
+        assert H.ecies_decrypt(sk, out[o, :olen[o]].numpy().tobytes()) == inp[o].numpy().tobytes()
+    with pytest.raises(EciesError):
+        device.encode_host_batch(1, inp, n, out, hashes, 2, slice_bytes=4 * n, pubkey=b"\x04" + bytes(64))
+    eph = np.stack([np.frombuffer(H.sha256(b"pe%d" % o), np.uint8) for o in range(count)])
+    eph[6] = 0  # zero is not a valid secret key
+    nonce = np.zeros((count, 16), np.uint8)
+    with pytest.raises(EciesError):
+        device.encode_host_batch(1, inp, n, out, hashes, 2, slice_bytes=4 * n, pubkey=pub, ephemeral_sk=eph,
+                                 nonce=nonce, host_threads=3)
