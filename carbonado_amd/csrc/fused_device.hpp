@@ -293,7 +293,9 @@ __device__ __forceinline__ void zfec_bao_fused_body(const FusedArgs &a) {
     // RT > 0 (general path): the blocks come in runs of RT consecutive blocks of
     // one object (the queue hands out runs), so a wave holds each block's
     // predecessor and completes levels 1-3 of the aligned groups that start
-    // in it (group_in_wave), as the FULL path does for all groups
+    // in it (group_in_wave), as the FULL path does for all groups.  A tuner
+    // variant (tools/k13_fetch), not shipped: 13 % slower kernel than RT = 0
+    // at the level-15 shard length (profiles/r10e_session)
     constexpr bool RUNS = !FULL && RT > 0 && KIND == 0;
     Tree<NT> tree(lane, RUNS ? a.cv3 : a.cv);
     tree.wr = DG != 11;

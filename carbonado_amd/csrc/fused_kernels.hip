@@ -33,14 +33,6 @@ constexpr int K13_GFP = K13_GFP_DEF;
 // (A/B r7u); the zfec+bao kernels keep plain loads (FULL path even, general
 // path -2..-4 % with them)
 constexpr bool K13_NTL = K13_NTL_DEF;
-// general path (8 does not divide the shard's chunk-columns, or zfec padding):
-// blocks in runs of K13_RT, levels 1-3 of the aligned groups a wave holds done
-// in the wave (fused_device.hpp RT); 0 = every level-0 CV to memory and the
-// levels-1-3 pass over all groups (round 4)
-#ifndef K13_RT_DEF
-#define K13_RT_DEF 16
-#endif
-constexpr int K13_RT = K13_RT_DEF;
 // the stream of an object of shard length C is < 8.6 C bytes and its input
 // 4 C: 32-bit offsets for C < 256 MiB.  CHIP_K13_O32=0 (read per call, so a
 // test can flip it) takes the 64-bit-address kernels at any size.
@@ -48,16 +40,6 @@ bool o32_ok(uint64_t C_or_n) {
     const char *e = std::getenv("CHIP_K13_O32");
     if (e && e[0] == '0' && e[1] == 0) return false;
     return C_or_n < (1ull << 28);
-}
-
-// CHIP_K13_RT=0: the general path as in round 4 (every level-0 CV to memory,
-// levels 1-3 of every group in the separate pass; A/B runs)
-bool k13_rt_on() {
-    static const bool on = [] {
-        const char *v = std::getenv("CHIP_K13_RT");
-        return !(v && v[0] == '0' && v[1] == 0);
-    }();
-    return on;
 }
 
 }  // namespace
@@ -74,19 +56,17 @@ namespace fused {
 __global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_full(fused::FusedArgs a) {
     fused::zfec_bao_fused_body<true, true, 1, 0, 0, true, 0, 0, K13_O32, K13_GFP>(a);
 }
+// (The general path's run mode, fused_device.hpp RT, is a tuner variant: the
+// kernel 13 % slower than this one at the level-15 shard length, the pipeline
+// line 962 against 1009 GiB/s, profiles/r10e_session.)
 __global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_general(fused::FusedArgs a) {
-    fused::zfec_bao_fused_body<true, false, 1, 0, 0, true, K13_RT ? 0 : 1, 0, K13_O32, K13_GFP, fused::FW, false, 0,
-                               K13_RT>(a);
-}
-__global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_general_r4(fused::FusedArgs a) {
     fused::zfec_bao_fused_body<true, false, 1, 0, 0, true, 1, 0, K13_O32, K13_GFP>(a);
 }
 __global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_full_a64(fused::FusedArgs a) {
     fused::zfec_bao_fused_body<true, true, 1, 0, 0, true, 0, 0, false, K13_GFP>(a);
 }
 __global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_general_a64(fused::FusedArgs a) {
-    fused::zfec_bao_fused_body<true, false, 1, 0, 0, true, K13_RT ? 0 : 1, 0, false, K13_GFP, fused::FW, false, 0,
-                               K13_RT>(a);
+    fused::zfec_bao_fused_body<true, false, 1, 0, 0, true, 1, 0, false, K13_GFP>(a);
 }
 __global__ __launch_bounds__(fused::FTPB) void bao_content_fused_kernel(fused::FusedArgs a) {
     fused::zfec_bao_fused_body<true, true, 1, 0, 1, true, 0, 0, K13_O32, 0, fused::FW, K13_NTL>(a);
@@ -156,31 +136,26 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     constexpr auto KG64 = zfec_bao_fused_kernel_general_a64;
     constexpr auto KF32 = zfec_bao_fused_kernel_full;
     constexpr auto KG32 = zfec_bao_fused_kernel_general;
-    constexpr auto KG4 = zfec_bao_fused_kernel_general_r4;
     static bool attr = [] {
         bool ok = true;
-        for (auto k : {KF64, KG64, KF32, KG32, KG4})
+        for (auto k : {KF64, KG64, KF32, KG32})
             ok &= hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)LDS_BYTES) == hipSuccess;
         return ok;
     }();
     const bool o32 = o32_ok(C);
-    // general path: the run mode (levels 1-3 of most groups in the wave) unless CHIP_K13_RT=0
-    const bool rt = !full && K13_RT > 0 && (k13_rt_on() || !o32);
-    const auto KF = o32 ? KF32 : KF64, KG = !rt ? KG4 : o32 ? KG32 : KG64;
+    const auto KF = o32 ? KF32 : KF64, KG = o32 ? KG32 : KG64;
     (void)attr;
     (void)hipGetLastError();
     const uint64_t n0 = full ? a.N / 8 : a.N;  // nodes per object in `cv`
     uint8_t *next = a.cv + count * n0 * 32;
-    if (rt) a.cv3 = next;  // level-3 CVs of the groups the waves complete
     if ((e = launch_parts(a, n0, full ? KF : KG, stream)) != hipSuccess) return e;
     if (full) return bao::run_parent_levels<0, false>(a.cv, n0, n0, 4, next, (n0 + 1) / 2, a.N, count, d_out,
                                                       out_stride, d_hash, nullptr, stream);
-    // levels 1-3 of the groups left (run mode) or of all groups, then from level 4
+    // levels 1-3 of every group from the level-0 CVs, then from level 4
     const uint64_t n3 = (a.N + 7) / 8, work = count * n3;
     hipLaunchKernelGGL(fused::bao_levels123_lds_kernel, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, stream,
-                       a.cv, a.N, count, coff, d_out, out_stride, next, n3, a.cols, a.bpo,
-                       (uint64_t)(rt ? K13_RT : 0));
+                       a.cv, a.N, count, coff, d_out, out_stride, next, n3, a.cols, a.bpo, (uint64_t)0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return bao::run_parent_levels<0, false>(next, n3, n3, 4, a.cv, (n3 + 1) / 2, a.N, count, d_out, out_stride,
                                             d_hash, nullptr, stream);

@@ -561,9 +561,9 @@ int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out) 
         } while (!scalar_ok(sk));
     }
     uint8_t master[130];
-    bool ok = k1::to65(k1::mul_g(sk), out->eph_pub);
+    bool ok = k1::to65_pair(k1::mul_g(sk), k1::mul(sk, k1::fe_from_be(peer + 1), k1::fe_from_be(peer + 33)),
+                            out->eph_pub, master + 65);
     std::memcpy(master, out->eph_pub, 65);
-    ok = ok && k1::to65(k1::mul(sk, k1::fe_from_be(peer + 1), k1::fe_from_be(peer + 33)), master + 65);
     OPENSSL_cleanse(sk, sizeof sk);
     ok = ok && hkdf_sha256_32(master, 130, out->key);
     OPENSSL_cleanse(master, sizeof master);
@@ -589,33 +589,13 @@ static int ecies_begin_prepared(const EciesKey &k, const uint8_t *nonce, uint8_t
 // out[81, 97) when the ciphertext is done.
 static int ecies_begin(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                        uint8_t *out, EVP_CIPHER_CTX *c) {
-    PtPtr peer(parse_public(pubkey, pubkey_len));
-    if (!peer.p) return CHIP_ERR_ECIES;
-    uint8_t sk[32];
-    if (eph_sk) {
-        std::memcpy(sk, eph_sk, 32);
-    } else {
-        for (;;) {  // SecretKey::random: rejection-sample a valid scalar
-            if (RAND_bytes(sk, 32) != 1) return CHIP_ERR_ECIES;
-            BnPtr t(parse_secret(sk, 32));
-            if (t.p) break;
-        }
-    }
-    BnPtr k(parse_secret(sk, 32));
-    OPENSSL_cleanse(sk, 32);
-    if (!k.p) return CHIP_ERR_ECIES;
-    if (!mul_g65(k.p, out)) return CHIP_ERR_ECIES;
-    uint8_t key[32];
-    if (!derive_key(k.p, peer.p, out, key)) return CHIP_ERR_ECIES;
-
-    uint8_t *iv = out + 65;
-    if (nonce) std::memcpy(iv, nonce, 16);
-    else if (RAND_bytes(iv, 16) != 1) return CHIP_ERR_ECIES;
-    const bool ok = c && EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
-                    EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
-                    EVP_EncryptInit_ex(c, nullptr, nullptr, key, iv) == 1;
-    OPENSSL_cleanse(key, 32);
-    return ok ? CHIP_OK : CHIP_ERR_ECIES;
+    uint8_t peer[65];
+    EciesKey k;
+    int st = ecies_peer(pubkey, pubkey_len, peer);
+    if (st == CHIP_OK) st = ecies_prepare(peer, eph_sk, &k);
+    if (st == CHIP_OK) st = ecies_begin_prepared(k, nonce, out, c);
+    ecies_key_wipe(&k);
+    return st;
 }
 
 static int ecies_end(EVP_CIPHER_CTX *c, uint8_t *out, uint64_t ct_len, uint64_t *out_len) {

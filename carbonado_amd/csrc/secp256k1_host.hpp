@@ -38,127 +38,125 @@ namespace k1 {
 
 typedef unsigned __int128 u128;
 
+// Field elements: five 52-bit limbs, value = sum v[i] 2^(52 i), reduced
+// lazily.  "Magnitude" m bounds the limbs by about m 2^52 (v[4]: m 2^48).
+// fe_mul / fe_sqr / fe_sub / fe_mul21 / fe_weak return magnitude 1 (limbs
+// < 2^52 + 2^34); fe_add adds magnitudes and is the only function that
+// grows them.  fe_mul and fe_sqr accept magnitude <= 8 (limbs < 2^56: five
+// 112-bit products per column fit 128 bits), fe_sub a subtrahend of
+// magnitude <= 8.  fe_norm gives the unique representative in [0, p) for
+// output and zero tests.  No branches or table indices on the values.
 struct Fe {
-    uint64_t v[4];  // little-endian limbs, fully reduced (< p)
+    uint64_t v[5];
 };
 
-constexpr uint64_t RC = 0x1000003D1ull;  // 2^256 mod p
-constexpr uint64_t P0 = 0xFFFFFFFEFFFFFC2Full, P1 = ~0ull, P2 = ~0ull, P3 = ~0ull;
+constexpr uint64_t M52 = 0xFFFFFFFFFFFFFull, M48 = 0xFFFFFFFFFFFFull;
+constexpr uint64_t RC = 0x1000003D1ull;      // 2^256 mod p
+constexpr uint64_t R260 = 0x1000003D10ull;   // 2^260 mod p (limb 5 folds onto limb 0)
+// 16 p, limb by limb (each limb >= 16 x a magnitude-1 limb bound / 2): a - b = a + 16p - b
+constexpr uint64_t P16_0 = 0xFFFFEFFFFFC2Full * 16, P16_1 = M52 * 16, P16_4 = M48 * 16;
 
-// r[0..3] + hi * 2^256 (hi < 2^64) -> fully reduced.  Carry chains use the
-// x86-64 add/sub-with-carry intrinsics (plain __int128 shifts compiled to a
-// slow serial chain: 41 ns per addition).
-inline void fe_reduce5(const uint64_t r[4], uint64_t hi, Fe &out) {
-    unsigned long long a0, a1, a2, a3;
-    const u128 m = (u128)hi * RC;
-    unsigned char c = _addcarry_u64(0, r[0], (uint64_t)m, &a0);
-    c = _addcarry_u64(c, r[1], (uint64_t)(m >> 64), &a1);
-    c = _addcarry_u64(c, r[2], 0, &a2);
-    c = _addcarry_u64(c, r[3], 0, &a3);
-    // one more 2^256 (then a is small and this cannot carry out)
-    unsigned char c2 = _addcarry_u64(0, a0, (uint64_t)c * RC, &a0);
-    c2 = _addcarry_u64(c2, a1, 0, &a1);
-    c2 = _addcarry_u64(c2, a2, 0, &a2);
-    (void)_addcarry_u64(c2, a3, 0, &a3);
-    // a < 2^256 < 2p: subtract p once if a >= p
-    unsigned long long s0, s1, s2, s3;
-    unsigned char b = _subborrow_u64(0, a0, P0, &s0);
-    b = _subborrow_u64(b, a1, P1, &s1);
-    b = _subborrow_u64(b, a2, P2, &s2);
-    b = _subborrow_u64(b, a3, P3, &s3);
-    const uint64_t keep = 0 - (uint64_t)b;  // all ones: a < p, keep a
-    out.v[0] = (a0 & keep) | (s0 & ~keep);
-    out.v[1] = (a1 & keep) | (s1 & ~keep);
-    out.v[2] = (a2 & keep) | (s2 & ~keep);
-    out.v[3] = (a3 & keep) | (s3 & ~keep);
+// carry the limbs down to 52 bits, the bits above 2^256 folded with RC
+inline Fe fe_weak(const Fe &a) {
+    uint64_t t0 = a.v[0], t1 = a.v[1], t2 = a.v[2], t3 = a.v[3], t4 = a.v[4];
+    const uint64_t x = t4 >> 48;
+    t4 &= M48;
+    t0 += x * RC;
+    t1 += t0 >> 52, t0 &= M52;
+    t2 += t1 >> 52, t1 &= M52;
+    t3 += t2 >> 52, t2 &= M52;
+    t4 += t3 >> 52, t3 &= M52;
+    return Fe{{t0, t1, t2, t3, t4}};
+}
+
+// [0, p): two carry passes (value < 2^256), then p subtracted once if value >= p
+inline Fe fe_norm(const Fe &a) {
+    Fe r = fe_weak(fe_weak(a));
+    // value + (2^256 - p) reaches 2^256 iff value >= p
+    uint64_t u0 = r.v[0] + RC, u1 = r.v[1] + (u0 >> 52), u2, u3, u4;
+    u0 &= M52;
+    u2 = r.v[2] + (u1 >> 52), u1 &= M52;
+    u3 = r.v[3] + (u2 >> 52), u2 &= M52;
+    u4 = r.v[4] + (u3 >> 52), u3 &= M52;
+    const uint64_t ge = 0 - (u4 >> 48);  // all ones: value >= p, take the sum mod 2^256
+    u4 &= M48;
+    return Fe{{(u0 & ge) | (r.v[0] & ~ge), (u1 & ge) | (r.v[1] & ~ge), (u2 & ge) | (r.v[2] & ~ge),
+               (u3 & ge) | (r.v[3] & ~ge), (u4 & ge) | (r.v[4] & ~ge)}};
+}
+
+// the ten columns of a product (52 bits, t[5] < 2^63, t[9] the top carry)
+// folded to magnitude 1: t[5 + k] 2^(260 + 52 k) = t[5 + k] R260 2^(52 k)
+inline Fe fe_fold(const uint64_t t[10]) {
+    u128 c = (u128)t[5] * R260 + t[0];
+    const uint64_t r0 = (uint64_t)c & M52;
+    c = (c >> 52) + (u128)t[6] * R260 + t[1];
+    const uint64_t r1 = (uint64_t)c & M52;
+    c = (c >> 52) + (u128)t[7] * R260 + t[2];
+    const uint64_t r2 = (uint64_t)c & M52;
+    c = (c >> 52) + (u128)t[8] * R260 + t[3];
+    const uint64_t r3 = (uint64_t)c & M52;
+    c = (c >> 52) + (u128)t[9] * R260 + t[4];
+    const uint64_t r4 = (uint64_t)c & M48;
+    c = (u128)(uint64_t)(c >> 48) * RC + r0;  // the bits above 2^256 (< 2^50)
+    return Fe{{(uint64_t)c & M52, r1 + (uint64_t)(c >> 52), r2, r3, r4}};
+}
+
+// The column sums are independent of each other (balanced trees of
+// products); the 52-bit carries run through columns 0-4 and 5-8 as two
+// chains side by side, column 4's carry joining t[5] (< 2^63) at the end.
+inline Fe fe_cols(u128 c0, u128 c1, u128 c2, u128 c3, u128 c4, u128 c5, u128 c6, u128 c7, u128 c8) {
+    uint64_t t[10];
+    t[0] = (uint64_t)c0 & M52;
+    c1 += c0 >> 52;
+    t[5] = (uint64_t)c5 & M52;
+    c6 += c5 >> 52;
+    t[1] = (uint64_t)c1 & M52;
+    c2 += c1 >> 52;
+    t[6] = (uint64_t)c6 & M52;
+    c7 += c6 >> 52;
+    t[2] = (uint64_t)c2 & M52;
+    c3 += c2 >> 52;
+    t[7] = (uint64_t)c7 & M52;
+    c8 += c7 >> 52;
+    t[3] = (uint64_t)c3 & M52;
+    c4 += c3 >> 52;
+    t[8] = (uint64_t)c8 & M52;
+    t[9] = (uint64_t)(c8 >> 52);
+    t[4] = (uint64_t)c4 & M52;
+    t[5] += (uint64_t)(c4 >> 52);
+    return fe_fold(t);
 }
 
 inline Fe fe_mul(const Fe &a, const Fe &b) {
-    uint64_t t[8];
-    {  // schoolbook 4 x 4, row by row
-        uint64_t carry = 0;
-        for (int j = 0; j < 4; ++j) {
-            const u128 acc = (u128)a.v[0] * b.v[j] + carry;
-            t[j] = (uint64_t)acc;
-            carry = (uint64_t)(acc >> 64);
-        }
-        t[4] = carry;
-        for (int i = 1; i < 4; ++i) {
-            carry = 0;
-            for (int j = 0; j < 4; ++j) {
-                const u128 acc = (u128)a.v[i] * b.v[j] + t[i + j] + carry;
-                t[i + j] = (uint64_t)acc;
-                carry = (uint64_t)(acc >> 64);
-            }
-            t[i + 4] = carry;
-        }
-    }
-    // fold the high half: t_hi * 2^256 = t_hi * RC (RC < 2^33: each product < 2^97)
-    uint64_t r[4];
-    unsigned long long x;
-    u128 p0 = (u128)t[4] * RC, p1 = (u128)t[5] * RC, p2 = (u128)t[6] * RC, p3 = (u128)t[7] * RC;
-    unsigned char c = _addcarry_u64(0, t[0], (uint64_t)p0, &x);
-    r[0] = x;
-    c = _addcarry_u64(c, t[1], (uint64_t)p1, &x);
-    unsigned char d = _addcarry_u64(0, x, (uint64_t)(p0 >> 64), &x);
-    r[1] = x;
-    c = _addcarry_u64(c, t[2], (uint64_t)p2, &x);
-    d = _addcarry_u64(d, x, (uint64_t)(p1 >> 64), &x);
-    r[2] = x;
-    c = _addcarry_u64(c, t[3], (uint64_t)p3, &x);
-    d = _addcarry_u64(d, x, (uint64_t)(p2 >> 64), &x);
-    r[3] = x;
-    const uint64_t hi = (uint64_t)(p3 >> 64) + c + d;
-    Fe out;
-    fe_reduce5(r, hi, out);
-    return out;
+    const uint64_t *x = a.v, *y = b.v;
+    auto m = [](uint64_t u, uint64_t v) { return (u128)u * v; };
+    return fe_cols(m(x[0], y[0]), m(x[0], y[1]) + m(x[1], y[0]), (m(x[0], y[2]) + m(x[1], y[1])) + m(x[2], y[0]),
+                   (m(x[0], y[3]) + m(x[1], y[2])) + (m(x[2], y[1]) + m(x[3], y[0])),
+                   (m(x[0], y[4]) + m(x[1], y[3])) + (m(x[2], y[2]) + m(x[3], y[1])) + m(x[4], y[0]),
+                   (m(x[1], y[4]) + m(x[2], y[3])) + (m(x[3], y[2]) + m(x[4], y[1])),
+                   (m(x[2], y[4]) + m(x[3], y[3])) + m(x[4], y[2]), m(x[3], y[4]) + m(x[4], y[3]), m(x[4], y[4]));
 }
 
-inline Fe fe_sqr(const Fe &a) { return fe_mul(a, a); }
-
-inline Fe fe_add(const Fe &a, const Fe &b) {
-    unsigned long long r[4];
-    unsigned char c = _addcarry_u64(0, a.v[0], b.v[0], &r[0]);
-    c = _addcarry_u64(c, a.v[1], b.v[1], &r[1]);
-    c = _addcarry_u64(c, a.v[2], b.v[2], &r[2]);
-    c = _addcarry_u64(c, a.v[3], b.v[3], &r[3]);
-    const uint64_t rr[4] = {r[0], r[1], r[2], r[3]};
-    Fe out;
-    fe_reduce5(rr, c, out);
-    return out;
+inline Fe fe_sqr(const Fe &a) {  // 15 products: the cross terms once, doubled
+    const uint64_t *x = a.v;
+    const uint64_t d0 = 2 * x[0], d1 = 2 * x[1], d2 = 2 * x[2], d3 = 2 * x[3];
+    auto m = [](uint64_t u, uint64_t v) { return (u128)u * v; };
+    return fe_cols(m(x[0], x[0]), m(d0, x[1]), m(d0, x[2]) + m(x[1], x[1]), m(d0, x[3]) + m(d1, x[2]),
+                   (m(d0, x[4]) + m(d1, x[3])) + m(x[2], x[2]), m(d1, x[4]) + m(d2, x[3]),
+                   m(d2, x[4]) + m(x[3], x[3]), m(d3, x[4]), m(x[4], x[4]));
 }
 
-inline Fe fe_sub(const Fe &a, const Fe &b) {
-    unsigned long long r[4];
-    unsigned char bw = _subborrow_u64(0, a.v[0], b.v[0], &r[0]);
-    bw = _subborrow_u64(bw, a.v[1], b.v[1], &r[1]);
-    bw = _subborrow_u64(bw, a.v[2], b.v[2], &r[2]);
-    bw = _subborrow_u64(bw, a.v[3], b.v[3], &r[3]);
-    // a - b < 0: add p (the carry out of that addition is the wrap back)
-    const uint64_t m = 0 - (uint64_t)bw;
-    Fe out;
-    unsigned long long x;
-    unsigned char c = _addcarry_u64(0, r[0], P0 & m, &x);
-    out.v[0] = x;
-    c = _addcarry_u64(c, r[1], P1 & m, &x);
-    out.v[1] = x;
-    c = _addcarry_u64(c, r[2], P2 & m, &x);
-    out.v[2] = x;
-    (void)_addcarry_u64(c, r[3], P3 & m, &x);
-    out.v[3] = x;
-    return out;
+inline Fe fe_add(const Fe &a, const Fe &b) {  // magnitudes add
+    return Fe{{a.v[0] + b.v[0], a.v[1] + b.v[1], a.v[2] + b.v[2], a.v[3] + b.v[3], a.v[4] + b.v[4]}};
+}
+
+inline Fe fe_sub(const Fe &a, const Fe &b) {  // a + 16p - b (b of magnitude <= 8)
+    return fe_weak(Fe{{a.v[0] + P16_0 - b.v[0], a.v[1] + P16_1 - b.v[1], a.v[2] + P16_1 - b.v[2],
+                       a.v[3] + P16_1 - b.v[3], a.v[4] + P16_4 - b.v[4]}});
 }
 
 inline Fe fe_mul21(const Fe &a) {  // b3 = 3 * 7
-    uint64_t r[4];
-    u128 acc = 0;
-    for (int i = 0; i < 4; ++i) {
-        acc = (acc >> 64) + (u128)a.v[i] * 21u;
-        r[i] = (uint64_t)acc;
-    }
-    Fe out;
-    fe_reduce5(r, (uint64_t)(acc >> 64), out);
-    return out;
+    return fe_weak(Fe{{a.v[0] * 21, a.v[1] * 21, a.v[2] * 21, a.v[3] * 21, a.v[4] * 21}});
 }
 
 inline Fe fe_sqr_n(Fe a, int n) {
@@ -186,26 +184,36 @@ inline Fe fe_inv(const Fe &a) {
     return fe_mul(fe_sqr_n(t, 2), a);
 }
 
+// 32 big-endian bytes (< 2^256) -> magnitude 1
 inline Fe fe_from_be(const uint8_t b[32]) {
-    Fe f;
+    uint64_t w[4];
     for (int i = 0; i < 4; ++i) {
-        uint64_t w = 0;
-        for (int j = 0; j < 8; ++j) w = (w << 8) | b[(3 - i) * 8 + j];
-        f.v[i] = w;
+        uint64_t x = 0;
+        for (int j = 0; j < 8; ++j) x = (x << 8) | b[(3 - i) * 8 + j];
+        w[i] = x;
     }
-    return f;
+    return Fe{{w[0] & M52, ((w[0] >> 52) | (w[1] << 12)) & M52, ((w[1] >> 40) | (w[2] << 24)) & M52,
+               ((w[2] >> 28) | (w[3] << 36)) & M52, w[3] >> 16}};
 }
 
 inline void fe_to_be(const Fe &f, uint8_t b[32]) {
+    const Fe n = fe_norm(f);
+    const uint64_t w[4] = {n.v[0] | (n.v[1] << 52), (n.v[1] >> 12) | (n.v[2] << 40), (n.v[2] >> 24) | (n.v[3] << 28),
+                           (n.v[3] >> 36) | (n.v[4] << 16)};
     for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 8; ++j) b[(3 - i) * 8 + j] = (uint8_t)(f.v[i] >> (56 - 8 * j));
+        for (int j = 0; j < 8; ++j) b[(3 - i) * 8 + j] = (uint8_t)(w[i] >> (56 - 8 * j));
+}
+
+inline bool fe_is_zero(const Fe &f) {
+    const Fe n = fe_norm(f);
+    return (n.v[0] | n.v[1] | n.v[2] | n.v[3] | n.v[4]) == 0;
 }
 
 struct Pt {
     Fe x, y, z;  // projective; infinity = (0 : 1 : 0)
 };
 
-inline Pt pt_inf() { return Pt{{{0, 0, 0, 0}}, {{1, 0, 0, 0}}, {{0, 0, 0, 0}}}; }
+inline Pt pt_inf() { return Pt{{{0, 0, 0, 0, 0}}, {{1, 0, 0, 0, 0}}, {{0, 0, 0, 0, 0}}}; }
 
 // Renes-Costello-Batina Algorithm 7 (a = 0): complete addition
 inline Pt pt_add(const Pt &p, const Pt &q) {
@@ -271,7 +279,7 @@ inline Pt pt_select(const Pt (&table)[16], uint32_t w) {
         const uint64_t m = 0 - (((uint64_t)(i ^ w) - 1) >> 63);  // all ones iff i == w
         const uint64_t *s = reinterpret_cast<const uint64_t *>(&table[i]);
         uint64_t *d = reinterpret_cast<uint64_t *>(&r);
-        for (int k = 0; k < 12; ++k) d[k] |= s[k] & m;
+        for (size_t k = 0; k < sizeof(Pt) / 8; ++k) d[k] |= s[k] & m;
     }
     return r;
 }
@@ -279,20 +287,6 @@ inline Pt pt_select(const Pt (&table)[16], uint32_t w) {
 inline uint32_t nibble(const uint8_t k[32], int j) {  // j-th 4-bit window from the least significant end
     const uint8_t b = k[31 - j / 2];
     return (j & 1) ? (b >> 4) : (b & 15u);
-}
-
-// k * P for an affine point P = (x, y)
-inline Pt mul(const uint8_t k[32], const Fe &x, const Fe &y) {
-    Pt table[16];
-    table[0] = pt_inf();
-    table[1] = Pt{x, y, {{1, 0, 0, 0}}};
-    for (int i = 2; i < 16; ++i) table[i] = pt_add(table[i - 1], table[1]);
-    Pt r = pt_inf();
-    for (int j = 63; j >= 0; --j) {
-        r = pt_dbl(pt_dbl(pt_dbl(pt_dbl(r))));
-        r = pt_add(r, pt_select(table, nibble(k, j)));
-    }
-    return r;
 }
 
 inline const Fe &gx() {
@@ -315,7 +309,7 @@ inline const Fe &gy() {
 struct GTable {
     Pt t[64][16];
     GTable() {
-        Pt base{gx(), gy(), {{1, 0, 0, 0}}};
+        Pt base{gx(), gy(), {{1, 0, 0, 0, 0}}};
         for (int j = 0; j < 64; ++j) {
             t[j][0] = pt_inf();
             t[j][1] = base;
@@ -339,12 +333,24 @@ inline Pt mul_g(const uint8_t k[32]) {
 
 // affine (x, y) of a point other than infinity, as 0x04 || x || y
 inline bool to65(const Pt &p, uint8_t out[65]) {
-    const Fe &z = p.z;
-    if ((z.v[0] | z.v[1] | z.v[2] | z.v[3]) == 0) return false;  // infinity (public: a failed operation)
-    const Fe zi = fe_inv(z);
+    if (fe_is_zero(p.z)) return false;  // infinity (public: a failed operation)
+    const Fe zi = fe_inv(p.z);
     out[0] = 0x04;
     fe_to_be(fe_mul(p.x, zi), out + 1);
     fe_to_be(fe_mul(p.y, zi), out + 33);
+    return true;
+}
+
+// to65 of two points with one inversion (1 / z1 = z2 / (z1 z2), and so on)
+inline bool to65_pair(const Pt &p, const Pt &q, uint8_t op[65], uint8_t oq[65]) {
+    if (fe_is_zero(p.z) || fe_is_zero(q.z)) return false;
+    const Fe i = fe_inv(fe_mul(p.z, q.z));
+    const Fe pi = fe_mul(i, q.z), qi = fe_mul(i, p.z);
+    op[0] = oq[0] = 0x04;
+    fe_to_be(fe_mul(p.x, pi), op + 1);
+    fe_to_be(fe_mul(p.y, pi), op + 33);
+    fe_to_be(fe_mul(q.x, qi), oq + 1);
+    fe_to_be(fe_mul(q.y, qi), oq + 33);
     return true;
 }
 
@@ -456,6 +462,86 @@ inline bool sc_is_zero(const Sc &a) { return (a.v[0] | a.v[1] | a.v[2] | a.v[3])
 inline void sc_clear(Sc &a) {
     volatile uint64_t *p = a.v;
     for (int i = 0; i < 4; ++i) p[i] = 0;
+}
+
+// ---- k * P with the endomorphism (GLV) ------------------------------------
+// lambda (x, y) = (beta x, y) for the cube roots of unity lambda mod n and
+// beta mod p.  k = k1 + k2 lambda (mod n) with |k1|, |k2| < 2^128 (the
+// lattice split: c1 = round(b2 k / n), c2 = round(-b1 k / n) through
+// g = round(2^384 b / n); k2 = c1 (-b1) + c2 (-b2), k1 = k - k2 lambda), so
+// k P = k1 P + k2 (lambda P) takes 128 doublings instead of 256.  Negative
+// halves are taken as n - k_i with the point's y negated.  Every step is
+// the same for every k (masks, full table scans, fixed loop counts).
+constexpr Sc GLV_G1 = {{0xe893209a45dbb031ull, 0x3daa8a1471e8ca7full, 0xe86c90e49284eb15ull, 0x3086d221a7d46bcdull}};
+constexpr Sc GLV_G2 = {{0x1571b4ae8ac47f71ull, 0x221208ac9df506c6ull, 0x6f547fa90abfe4c4ull, 0xe4437ed6010e8828ull}};
+constexpr Sc GLV_MB1 = {{0x6f547fa90abfe4c3ull, 0xe4437ed6010e8828ull, 0, 0}};  // -b1
+constexpr Sc GLV_MB2 = {{0xd765cda83db1562cull, 0x8a280ac50774346dull, 0xfffffffffffffffeull,
+                         0xffffffffffffffffull}};  // -b2 mod n
+constexpr Sc GLV_MLAM = {{0xe0cfc810b51283cfull, 0xa880b9fc8ec739c2ull, 0x5ad9e3fd77ed9ba4ull,
+                          0xac9c52b33fa3cf1full}};  // -lambda mod n
+
+inline const Fe &glv_beta() {
+    static const uint8_t b[32] = {0x7a, 0xe9, 0x6a, 0x2b, 0x65, 0x7c, 0x07, 0x10, 0x6e, 0x64, 0x47,
+                                  0x9e, 0xac, 0x34, 0x34, 0xe9, 0x9c, 0xf0, 0x49, 0x75, 0x12, 0xf5,
+                                  0x89, 0x95, 0xc1, 0x39, 0x6c, 0x28, 0x71, 0x95, 0x01, 0xee};
+    static const Fe f = fe_from_be(b);
+    return f;
+}
+
+// round(k g / 2^384) (< 2^128)
+inline Sc sc_mulshift384(const Sc &k, const Sc &g) {
+    uint64_t l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    sc_mac<4, 4, 8>(l, k.v, g.v);
+    unsigned long long lo, hi;
+    const unsigned char c = _addcarry_u64(0, l[6], l[5] >> 63, &lo);
+    (void)_addcarry_u64(c, l[7], 0, &hi);
+    return Sc{{lo, hi, 0, 0}};
+}
+
+// all ones iff a > (n - 1) / 2
+inline uint64_t sc_high_mask(const Sc &a) {
+    constexpr uint64_t H0 = 0xDFE92F46681B20A0ull, H1 = 0x5D576E7357A4501Dull, H2 = 0xFFFFFFFFFFFFFFFFull,
+                       H3 = 0x7FFFFFFFFFFFFFFFull;
+    unsigned long long t;
+    unsigned char b = _subborrow_u64(0, H0, a.v[0], &t);
+    b = _subborrow_u64(b, H1, a.v[1], &t);
+    b = _subborrow_u64(b, H2, a.v[2], &t);
+    b = _subborrow_u64(b, H3, a.v[3], &t);
+    return 0 - (uint64_t)b;
+}
+
+inline Fe fe_cmov(const Fe &a, const Fe &b, uint64_t m) {  // m all ones: b, else a
+    Fe r;
+    for (int i = 0; i < 5; ++i) r.v[i] = (a.v[i] & ~m) | (b.v[i] & m);
+    return r;
+}
+
+inline uint32_t sc_nibble(const Sc &a, int j) { return (uint32_t)(a.v[j >> 4] >> (4 * (j & 15))) & 15u; }
+
+// k * P for an affine point P = (x, y), 0 < k < n
+inline Pt mul(const uint8_t k[32], const Fe &x, const Fe &y) {
+    const Sc s = sc_from_be(k);
+    const Sc c1 = sc_mulshift384(s, GLV_G1), c2 = sc_mulshift384(s, GLV_G2);
+    const Sc k2 = sc_add(sc_mul(c1, GLV_MB1), sc_mul(c2, GLV_MB2));
+    const Sc k1 = sc_add(s, sc_mul(k2, GLV_MLAM));
+    const uint64_t n1 = sc_high_mask(k1), n2 = sc_high_mask(k2);
+    const Sc a1 = sc_cond_neg(k1, n1 != 0), a2 = sc_cond_neg(k2, n2 != 0);
+    const Fe zero = {{0, 0, 0, 0, 0}};
+    // T1[i] = i (+-P), T2[i] = lambda T1[i] with y negated again when the signs differ
+    Pt t1[16], t2[16];
+    t1[0] = pt_inf();
+    t1[1] = Pt{x, fe_cmov(y, fe_sub(zero, y), n1), {{1, 0, 0, 0, 0}}};
+    for (int i = 2; i < 16; ++i) t1[i] = pt_add(t1[i - 1], t1[1]);
+    const uint64_t flip = n1 ^ n2;
+    for (int i = 0; i < 16; ++i)
+        t2[i] = Pt{fe_mul(t1[i].x, glv_beta()), fe_cmov(t1[i].y, fe_sub(zero, t1[i].y), flip), t1[i].z};
+    Pt r = pt_inf();
+    for (int j = 32; j >= 0; --j) {  // 33 windows: 132 bits, |k_i| < 2^128
+        r = pt_dbl(pt_dbl(pt_dbl(pt_dbl(r))));
+        r = pt_add(r, pt_select(t1, sc_nibble(a1, j)));
+        r = pt_add(r, pt_select(t2, sc_nibble(a2, j)));
+    }
+    return r;
 }
 
 }  // namespace k1

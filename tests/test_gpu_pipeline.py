@@ -446,12 +446,11 @@ def test_decode_batch_dev_errors(gpu):
 
 
 @pytest.mark.parametrize("cols", [129, 130, 131, 132, 133, 134, 135, 136, 257, 4097])
-def test_encode_batch_dev_k13_runs(gpu, cols):
-    """K13's general path in run mode (fused_device.hpp RT: blocks in runs of
-    16, levels 1-3 of the aligned groups done in the wave, the rest from the
-    level-0 CVs): shards of `cols` chunk-columns, so every offset of a shard
+def test_encode_batch_dev_k13_general_cols(gpu, cols):
+    """K13's general path (level-0 CVs to memory, levels 1-3 in the separate
+    pass): shards of `cols` chunk-columns, so every offset of a shard
     from the 8-chunk grid (cols % 8 = 1..7, and 0 with zfec padding), 17 to
-    513 blocks per object (several runs, ragged last run), three objects in
+    513 blocks per object, three objects in
     one launch — every stream and hash == the oracle's encode() level 12."""
     import torch
     from carbonado_amd import device
