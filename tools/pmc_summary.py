@@ -27,6 +27,7 @@ def main():
     tag = sys.argv[1]
     kern = sys.argv[2] if len(sys.argv) > 2 else "gf_apply_kernel"
     src = ROOT / "gpurun_out" / tag
+    tag = tag.replace("/", "_")  # a session's sub-run (gpu_session.sh prof15s: TAG/p15s)
     dst = ROOT / "profiles"
     dst.mkdir(exist_ok=True)
     stats = src / "prof" / "stats_kernel_stats.csv"
