@@ -767,18 +767,21 @@ __global__ __launch_bounds__(256) void bao_levels123_kernel(const uint8_t *cv0, 
     bao::store_cv(cv3 + (obj * n3 + g) * 32, c[0]);
 }
 
-// The same with the node stores coalesced (NW 3): one wave per block; each
-// level's nodes go to LDS first, then the wave writes them four lanes per
-// node, 16 nodes (64 contiguous bytes each) per store instruction instead of
-// 64 lanes at 64 places 8 KiB apart.
+// The same with the node stores coalesced (NW 3): one wave per block; the
+// nodes go to LDS first, then the wave writes them four lanes per node, 16
+// nodes (64 contiguous bytes each) per store instruction instead of 64 lanes
+// at 64 places 8 KiB apart.  QS: nodes per lane staged at once (4: a whole
+// level, 16 KiB of LDS per wave; 1: node by node, 4 KiB, so LDS no longer
+// caps the waves per CU below what the registers allow).
 // rt > 0: only the groups K13's run mode left (group_in_wave false; cols,
 // bpo: the zfec shards' chunk-columns and K13's blocks per object).
+template <int QS>
 __global__ __launch_bounds__(64) void bao_levels123_lds_kernel(const uint8_t *cv0, uint64_t N, uint64_t count,
                                                                const uint64_t *coff, uint8_t *out,
                                                                uint64_t out_stride, uint8_t *cv3, uint64_t n3,
                                                                uint64_t cols = 0, uint64_t bpo = 0, uint64_t rt = 0) {
-    __shared__ bao::u32x4 buf[64 * 4 * 4];  // [lane][node][16-B unit] of the current level
-    __shared__ uint64_t naddr[64 * 4];      // [lane][node]: its slot (0: not a real node)
+    __shared__ bao::u32x4 buf[64 * QS * 4];  // [lane][node][16-B unit] of the nodes staged
+    __shared__ uint64_t naddr[64 * QS];      // [lane][node]: its slot (0: not a real node)
     const int lane = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
     bool on = gid < count * n3;
@@ -798,37 +801,41 @@ __global__ __launch_bounds__(64) void bao_levels123_lds_kernel(const uint8_t *cv
     uint8_t *ob = out + obj * out_stride;
 #pragma unroll
     for (int l = 1; l <= 3; ++l) {
-        const int nq = 8 >> l;
         const uint32_t span = 1u << l, half = span >> 1;
 #pragma unroll
-        for (int q = 0; q < (8 >> l); ++q) {
-            const uint32_t left = q * span;
-            const int li = q * 2, ri = q * 2 + 1;
-            const bool real = left + half < cnt;
-            bao::u32x4 *b = buf + (lane * nq + q) * 4;
-            b[0] = bao::u32x4{c[li][0], c[li][1], c[li][2], c[li][3]};
-            b[1] = bao::u32x4{c[li][4], c[li][5], c[li][6], c[li][7]};
-            b[2] = bao::u32x4{c[ri][0], c[ri][1], c[ri][2], c[ri][3]};
-            b[3] = bao::u32x4{c[ri][4], c[ri][5], c[ri][6], c[ri][7]};
-            naddr[lane * nq + q] = real ? (uint64_t)(uintptr_t)(ob + coff[s0 + left] - 64 * l) : 0ull;
-            if (real) {
-                uint32_t p[8];
-                bao::b3_parent(c[li], c[ri], false, p);
+        for (int q0 = 0; q0 < (8 >> l); q0 += QS) {
+            const int ns = (8 >> l) - q0 < QS ? (8 >> l) - q0 : QS;  // nodes per lane this round
 #pragma unroll
-                for (int w = 0; w < 8; ++w) c[q][w] = p[w];
-            } else {
+            for (int j = 0; j < ns; ++j) {
+                const int q = q0 + j;
+                const uint32_t left = q * span;
+                const int li = q * 2, ri = q * 2 + 1;
+                const bool real = left + half < cnt;
+                bao::u32x4 *b = buf + (lane * ns + j) * 4;
+                b[0] = bao::u32x4{c[li][0], c[li][1], c[li][2], c[li][3]};
+                b[1] = bao::u32x4{c[li][4], c[li][5], c[li][6], c[li][7]};
+                b[2] = bao::u32x4{c[ri][0], c[ri][1], c[ri][2], c[ri][3]};
+                b[3] = bao::u32x4{c[ri][4], c[ri][5], c[ri][6], c[ri][7]};
+                naddr[lane * ns + j] = real ? (uint64_t)(uintptr_t)(ob + coff[s0 + left] - 64 * l) : 0ull;
+                if (real) {
+                    uint32_t p[8];
+                    bao::b3_parent(c[li], c[ri], false, p);
 #pragma unroll
-                for (int w = 0; w < 8; ++w) c[q][w] = c[li][w];
+                    for (int w = 0; w < 8; ++w) c[q][w] = p[w];
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 8; ++w) c[q][w] = c[li][w];
+                }
             }
+            bao::wave_sync();
+            for (int i = 0; i < ns * 4; ++i) {  // unit k = i * 64 + lane: node k / 4, 16-B unit k % 4
+                const int k = i * 64 + lane;
+                const uint64_t a = naddr[k >> 2];
+                if (a) *(__attribute__((address_space(1))) bao::u32x4_a8 *)(uintptr_t)(a + 16 * (k & 3)) =
+                    bao::u32x4_a8{buf[k].x, buf[k].y, buf[k].z, buf[k].w};
+            }
+            bao::wave_sync();
         }
-        bao::wave_sync();
-        for (int i = 0; i < nq * 4; ++i) {  // unit k = i * 64 + lane: node k / 4, 16-B unit k % 4
-            const int k = i * 64 + lane;
-            const uint64_t a = naddr[k >> 2];
-            if (a) *(__attribute__((address_space(1))) bao::u32x4_a8 *)(uintptr_t)(a + 16 * (k & 3)) =
-                bao::u32x4_a8{buf[k].x, buf[k].y, buf[k].z, buf[k].w};
-        }
-        bao::wave_sync();
     }
     if (on) bao::store_cv(cv3 + (obj * n3 + g) * 32, c[0]);
 }

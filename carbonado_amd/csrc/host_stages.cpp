@@ -24,7 +24,6 @@
 
 #include <openssl/ec.h>
 #include <openssl/evp.h>
-#include <openssl/hmac.h>
 #include <openssl/obj_mac.h>
 #include <openssl/rand.h>
 
@@ -454,19 +453,50 @@ EC_POINT *parse_public(const uint8_t *pk, uint64_t len) {
     return pt;
 }
 
+// OpenSSL 3 looks an algorithm up in its provider store (under a global
+// lock) on every init through EVP_sha256() / aes256_gcm() and every
+// one-shot HMAC(); the per-object inits of a 16-thread batch serialised on
+// it.  Fetched once here, each init only takes a reference.
+const EVP_MD *sha256_md() {
+    static EVP_MD *m = EVP_MD_fetch(nullptr, "SHA2-256", nullptr);
+    return m;
+}
+const EVP_CIPHER *aes256_gcm() {
+    static EVP_CIPHER *c = EVP_CIPHER_fetch(nullptr, "AES-256-GCM", nullptr);
+    return c;
+}
+
+struct MdCtx {
+    EVP_MD_CTX *m = EVP_MD_CTX_new();
+    ~MdCtx() { EVP_MD_CTX_free(m); }
+};
+
+// HMAC-SHA256 with a 32-byte key (RFC 2104: the key zero-padded to the
+// 64-byte block): H((K ^ opad) || H((K ^ ipad) || msg))
+bool hmac_sha256_k32(const uint8_t key[32], const uint8_t *msg, size_t n, uint8_t out[32]) {
+    thread_local MdCtx ctx;
+    EVP_MD_CTX *m = ctx.m;
+    uint8_t pad[64], inner[32];
+    for (int i = 0; i < 64; ++i) pad[i] = (uint8_t)((i < 32 ? key[i] : 0) ^ 0x36);
+    unsigned int l = 0;
+    bool ok = m && EVP_DigestInit_ex2(m, sha256_md(), nullptr) == 1 && EVP_DigestUpdate(m, pad, 64) == 1 &&
+              EVP_DigestUpdate(m, msg, n) == 1 && EVP_DigestFinal_ex(m, inner, &l) == 1 && l == 32;
+    for (int i = 0; i < 64; ++i) pad[i] = (uint8_t)((i < 32 ? key[i] : 0) ^ 0x5c);
+    ok = ok && EVP_DigestInit_ex2(m, sha256_md(), nullptr) == 1 && EVP_DigestUpdate(m, pad, 64) == 1 &&
+         EVP_DigestUpdate(m, inner, 32) == 1 && EVP_DigestFinal_ex(m, out, &l) == 1 && l == 32;
+    OPENSSL_cleanse(pad, sizeof pad);
+    OPENSSL_cleanse(inner, sizeof inner);
+    return ok;
+}
+
 // HKDF-SHA256 (RFC 5869) with no salt and no info, 32-byte output: one HMAC
 // for the extract step, one for T(1).
 bool hkdf_sha256_32(const uint8_t *ikm, size_t n, uint8_t out[32]) {
-    uint8_t zero[32] = {0}, prk[32];
-    unsigned int l = 0;
-    if (!HMAC(EVP_sha256(), zero, 32, ikm, n, prk, &l) || l != 32) return false;
-    const uint8_t one = 0x01;
-    uint8_t t[32];
-    if (!HMAC(EVP_sha256(), prk, 32, &one, 1, t, &l) || l != 32) return false;
-    std::memcpy(out, t, 32);
+    const uint8_t zero[32] = {0}, one = 0x01;
+    uint8_t prk[32];
+    const bool ok = hmac_sha256_k32(zero, ikm, n, prk) && hmac_sha256_k32(prk, &one, 1, out);
     OPENSSL_cleanse(prk, 32);
-    OPENSSL_cleanse(t, 32);
-    return true;
+    return ok;
 }
 
 // k * G as 0x04 || x || y (secp256k1_host.hpp: constant time, ~25x OpenSSL's
@@ -578,7 +608,7 @@ static int ecies_begin_prepared(const EciesKey &k, const uint8_t *nonce, uint8_t
     uint8_t *iv = out + 65;
     if (nonce) std::memcpy(iv, nonce, 16);
     else if (RAND_bytes(iv, 16) != 1) return CHIP_ERR_ECIES;
-    const bool ok = c && EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+    const bool ok = c && EVP_EncryptInit_ex(c, aes256_gcm(), nullptr, nullptr, nullptr) == 1 &&
                     EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
                     EVP_EncryptInit_ex(c, nullptr, nullptr, k.key, iv) == 1;
     return ok ? CHIP_OK : CHIP_ERR_ECIES;
@@ -637,7 +667,7 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
     CipherCtx cc;
     uint8_t tagbuf[16];
     std::memcpy(tagbuf, tag, 16);
-    bool ok = cc.c && EVP_DecryptInit_ex(cc.c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+    bool ok = cc.c && EVP_DecryptInit_ex(cc.c, aes256_gcm(), nullptr, nullptr, nullptr) == 1 &&
               EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
               EVP_DecryptInit_ex(cc.c, nullptr, nullptr, key, iv) == 1 && gcm_update(cc.c, false, ct, m, out) &&
               EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_TAG, 16, tagbuf) == 1;
@@ -678,7 +708,7 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
     uint8_t tagbuf[16];
     std::memcpy(tagbuf, in + 81, 16);
     CipherCtx cc;
-    bool dec_ok = cc.c && EVP_DecryptInit_ex(cc.c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+    bool dec_ok = cc.c && EVP_DecryptInit_ex(cc.c, aes256_gcm(), nullptr, nullptr, nullptr) == 1 &&
                   EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
                   EVP_DecryptInit_ex(cc.c, nullptr, nullptr, key, iv) == 1;
     OPENSSL_cleanse(key, 32);

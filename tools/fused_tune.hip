@@ -198,19 +198,29 @@ int main(int argc, char **argv) {
         uint8_t *cv3;
         CK(hipMalloc(&cv3, count * n3 * 32));
         void (*kv[5])(const uint8_t *, uint64_t, uint64_t, const uint64_t *, uint8_t *, uint64_t, uint8_t *, uint64_t) = {
-            fused::bao_levels123_kernel<1>, fused::bao_levels123_kernel<2>, fused::bao_levels123_kernel<0>,
-            fused::bao_levels123_lds_kernel, fused::bao_levels123_seg_kernel};
-        const char *kn[5] = {"8-B node stores", "16-B node stores", "no node stores (diagnostic)",
-                             "LDS-staged node stores, 4 lanes per node (product)",
-                             "node stacks as whole 64-B segments (SEG)"};
-        std::vector<float> t3[5];
-        unsigned long long sum3[5] = {0, 0, 0, 0, 0};
+            fused::bao_levels123_kernel<1>, fused::bao_levels123_kernel<2>, fused::bao_levels123_kernel<0>, nullptr,
+            fused::bao_levels123_seg_kernel};
+        void (*kq[7])(const uint8_t *, uint64_t, uint64_t, const uint64_t *, uint8_t *, uint64_t, uint8_t *, uint64_t,
+                      uint64_t, uint64_t, uint64_t) = {nullptr, nullptr, nullptr, fused::bao_levels123_lds_kernel<4>,
+                                                       nullptr, fused::bao_levels123_lds_kernel<1>,
+                                                       fused::bao_levels123_lds_kernel<2>};
+        const char *kn[7] = {"8-B node stores", "16-B node stores", "no node stores (diagnostic)",
+                             "LDS-staged node stores, a level per round (QS 4, round 4)",
+                             "node stacks as whole 64-B segments (SEG)",
+                             "LDS-staged node stores, a node per round (QS 1)",
+                             "LDS-staged node stores, two nodes per round (QS 2)"};
+        std::vector<float> t3[7];
+        unsigned long long sum3[7] = {0, 0, 0, 0, 0, 0, 0};
         for (int rd = 0; rd < rounds + 1; ++rd)
-            for (int k = 0; k < 5; ++k) {
-                const int tpb = k == 3 ? 64 : 256;
+            for (int k = 0; k < 7; ++k) {
+                const int tpb = (k == 3 || k >= 5) ? 64 : 256;
                 CK(hipEventRecord(e0));
-                hipLaunchKernelGGL(kv[k], dim3((unsigned)((work + tpb - 1) / tpb)), dim3(tpb), 0, 0, cv, N, count,
-                                   dcoff[0], out, bstride, cv3, n3);
+                if (kq[k])
+                    hipLaunchKernelGGL(kq[k], dim3((unsigned)((work + tpb - 1) / tpb)), dim3(tpb), 0, 0, cv, N, count,
+                                       dcoff[0], out, bstride, cv3, n3, (uint64_t)0, (uint64_t)0, (uint64_t)0);
+                else
+                    hipLaunchKernelGGL(kv[k], dim3((unsigned)((work + tpb - 1) / tpb)), dim3(tpb), 0, 0, cv, N, count,
+                                       dcoff[0], out, bstride, cv3, n3);
                 CK(hipEventRecord(e1));
                 CK(hipEventSynchronize(e1));
                 float t;
@@ -218,9 +228,10 @@ int main(int argc, char **argv) {
                 if (rd) t3[k].push_back(t);
                 if (rd == 0) sum3[k] = checksum(out, count * bstride) ^ (checksum(cv3, count * n3 * 32) * 3);
             }
-        printf("levels 1-3 outputs: LDS-staged %s 8-B stores; 16-B %s; SEG %s\n", sum3[3] == sum3[0] ? "==" : "!=",
-               sum3[1] == sum3[0] ? "==" : "!=", sum3[4] == sum3[0] ? "==" : "!=");
-        for (int k = 0; k < 5; ++k) {
+        printf("levels 1-3 outputs: LDS-staged %s 8-B stores; 16-B %s; SEG %s; QS 1 %s; QS 2 %s\n",
+               sum3[3] == sum3[0] ? "==" : "!=", sum3[1] == sum3[0] ? "==" : "!=", sum3[4] == sum3[0] ? "==" : "!=",
+               sum3[5] == sum3[0] ? "==" : "!=", sum3[6] == sum3[0] ? "==" : "!=");
+        for (int k = 0; k < 7; ++k) {
             std::sort(t3[k].begin(), t3[k].end());
             printf("levels 1-3 from chunk CVs (bao_levels123_kernel), %s, %llu objects: median %.3f ms\n", kn[k],
                    (unsigned long long)count, t3[k][t3[k].size() / 2]);
