@@ -970,7 +970,7 @@ class Workload:
             self.h2d_bytes, self.d2h_bytes = count * n, count * self.final_len
             self.copy_back = "whole stream"
             if lv & 12 == 12 and os.environ.get("CHIP_E2E_SPLIT", "1") != "0":
-                # split copy-back (chip_api.cpp SplitGeo): the host writes each stream's
+                # split copy-back (api_encode.cpp SplitGeo): the host writes each stream's
                 # header and data-shard chunks (zl/2 bytes, zl = the bao header) itself;
                 # the nodes between them and the tail cross PCIe
                 host_made = sum(8 + int.from_bytes(self.h_out[o, :8].numpy().tobytes(), "little") // 2

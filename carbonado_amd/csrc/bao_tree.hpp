@@ -335,7 +335,7 @@ static __global__ __launch_bounds__(256) void bao_gather_kernel(const uint8_t *s
 // coff = bao_chunk_table(N)), in stream order, to nodes + o * nodes_stride.
 // encode() from host memory at Zfec|Bao: chunks [0, nd) are the data shards,
 // which the host already holds, so only these nodes and the stream's tail
-// cross PCIe (chip_api.cpp SplitGeo).  Lane = 8 B of one run of nodes; the
+// cross PCIe (api_encode.cpp SplitGeo).  Lane = 8 B of one run of nodes; the
 // runs sit at 8 mod 64, so 8-B accesses.
 static __global__ __launch_bounds__(256) void bao_data_nodes_kernel(const uint8_t *stream, uint64_t stride,
                                                                     const uint64_t *coff, uint64_t nd,

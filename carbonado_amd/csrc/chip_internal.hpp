@@ -7,8 +7,10 @@
 //                        erasure decode are the same kernel)
 //   bao_kernels.hip      K3/K4/K5: BLAKE3 chunk CVs, parent levels, bao
 //                        pre-order layout, verify-decode
-//   chip_api.cpp         the C-ABI (include/carbonado_hip.h): host staging,
+//   fused_kernels.hip    K13: zfec + bao in one pass; content-mode bao
+//   api_*.cpp            the C-ABI (include/carbonado_hip.h): host staging,
 //                        per-thread streams, error mapping, pipeline glue
+//                        (api_common.hpp lists the files by concern)
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -2,7 +2,8 @@
 // (/root/reference/src/file.rs): the 160-byte signed Header and
 // file::encode / file::decode.  Host code: the header is 160 bytes per object
 // and one BIP-340 signature, nothing for the GPU to do; the body is the
-// encode()/decode() path of chip_api.cpp (zfec + bao on the device).
+// encode()/decode() path of api_encode.cpp / api_decode.cpp (zfec + bao on
+// the device).
 //
 // Header bytes (Header::try_to_vec, file.rs:292-335):
 //   magic "CARBONADO01\n" 12 | pubkey 33 (compressed) | bao hash 32 |

@@ -199,7 +199,10 @@ def encode_host_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, ha
                                             ctypes.byref(inj) if inj is not None else None, _p(inp), n, count,
                                             inp.shape[1], _p(out), out.shape[1], olen, _p(hashes), info,
                                             nslots, slice_bytes, host_threads))
-    return [olen[o] for o in range(count)], [EncodeInfo.from_c(info[o]) for o in range(count)]
+    # field tuples through numpy (one C-speed pass), then EncodeInfo(*t): half
+    # the cost of from_c per object at 16384 objects
+    rows = np.ctypeslib.as_array(info)[:count].tolist() if count else []
+    return list(olen)[:count], [EncodeInfo(*r) for r in rows]
 
 
 def decode_host_batch(fmt: int, enc: torch.Tensor, in_len, hashes: torch.Tensor, padding, out: torch.Tensor,

@@ -101,3 +101,12 @@ def test_argument_errors_before_device():
         carbonado_amd.decoding.bao(b"\0" * 8, b"\0" * 31)  # utils.rs:38-45
     with pytest.raises(E.UnevenZfecChunks):
         carbonado_amd.decoding.zfec(np.zeros(1001, np.uint8), 0)  # decoding.rs:39-41
+
+
+def test_encode_info_fields_match_c_struct():
+    """device.encode_host_batch builds EncodeInfo(*row) from the C struct's
+    field tuples: the dataclass must list the fields in the struct's order."""
+    import dataclasses
+    from carbonado_amd import _lib
+    from carbonado_amd.structs import EncodeInfo
+    assert [f.name for f in dataclasses.fields(EncodeInfo)] == [n for n, _ in _lib.EncodeInfoC._fields_]

@@ -1,5 +1,5 @@
 """GPU: the single-object calls copy pageable host buffers through the pinned
-staging ring and pinned buffers directly (chip_api.cpp h2d/d2h); every
+staging ring and pinned buffers directly (api_host_copy.cpp h2d/d2h); every
 combination gives the oracle's bytes, including buffers that wrap the 4 x 4
 MiB ring several times, odd lengths and unaligned addresses."""
 import ctypes

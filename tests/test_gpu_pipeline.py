@@ -140,7 +140,7 @@ def test_encode_host_batch_ragged_host_stage_sizes(gpu):
 def test_encode_host_batch_split_copy_back(gpu, level, n):
     """Zfec|Bao from host memory: the host writes each stream's header and
     data-shard chunks itself, the device gathers the parent nodes between them
-    and the tail crosses PCIe (chip_api.cpp SplitGeo).  Output pre-filled with
+    and the tail crosses PCIe (api_encode.cpp SplitGeo).  Output pre-filled with
     0xA5 so a byte nobody wrote shows; nine objects over two slots of two
     objects each, so slots are reused and nodes scattered while the next slice
     stages; count 1 separately (pitch = the stream length)."""
