@@ -154,11 +154,10 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
                                                       out_stride, d_hash, nullptr, stream);
     // levels 1-3 of every group from the level-0 CVs, then from level 4
     const uint64_t n3 = (a.N + 7) / 8, work = count * n3;
-    static const bool qs4 = [] {  // A/B switch (round 5): CHIP_L123_QS=4 stages a whole level per round
-        const char *v = std::getenv("CHIP_L123_QS");
-        return v && v[0] == '4';
-    }();
-    hipLaunchKernelGGL(qs4 ? fused::bao_levels123_lds_kernel<4> : fused::bao_levels123_lds_kernel<1>, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, stream,
+    // a whole level's nodes staged per round (QS 4): node by node (QS 1, 4 KiB
+    // of LDS per wave) measured no better (0.391 vs 0.373 ms per 256 objects,
+    // tools/fused_tune r10g; pipeline lines equal within noise)
+    hipLaunchKernelGGL(fused::bao_levels123_lds_kernel<4>, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, stream,
                        a.cv, a.N, count, coff, d_out, out_stride, next, n3, a.cols, a.bpo, (uint64_t)0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return bao::run_parent_levels<0, false>(next, n3, n3, 4, a.cv, (n3 + 1) / 2, a.N, count, d_out, out_stride,

@@ -206,3 +206,38 @@ def test_bao_decode_mismatch_leaves_no_content(gpu, n):
     rc = L.chip_bao_decode(good.ctypes.data, good.size, hh.ctypes.data, 32, out.ctypes.data, out.size,
                            ctypes.byref(olen))
     assert rc == 0 and olen.value == n and out.tobytes() == d
+
+
+@pytest.mark.parametrize("n", [257 * 1024 + 77, 600 * 1024 + 5])
+def test_batch_bao_many_small_trees(gpu, n):
+    """2048 objects: the top-of-tree walk runs one wave per object
+    (bao_tree.hpp bao_top_kernel TPB 64, batches of >= 2048 trees), straight
+    from the chunk CVs (258 chunks) or after one K4 level (601 chunks).  Every
+    hash vs the oracle, three whole streams, the batch verify-decode, and one
+    damaged parent node flagged on its object only."""
+    import torch
+    from carbonado_amd import device
+    count = 2048
+    gen = torch.Generator(device="cuda").manual_seed(n % 997)
+    inp = torch.randint(0, 256, (count, n), dtype=torch.uint8, device="cuda", generator=gen)
+    blen = O.lib().orc_bao_encoded_len(n)
+    out = torch.empty((count, (blen + 255) // 256 * 256), dtype=torch.uint8, device="cuda")
+    hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+    scratch = device.bao_scratch(n, count)
+    device.bao_encode_batch(inp, n, out, hashes, scratch)
+    torch.cuda.synchronize()
+    h_in, h_hash = inp.cpu().numpy(), hashes.cpu().numpy()
+    for o in range(count):
+        assert h_hash[o].tobytes() == O.blake3(h_in[o].tobytes()), o
+    for o in (0, 1237, count - 1):
+        assert out[o, :blen].cpu().numpy().tobytes() == O.bao_encode(h_in[o].tobytes())[0], o
+    dec = torch.empty((count, n), dtype=torch.uint8, device="cuda")
+    status = torch.empty(count, dtype=torch.int32, device="cuda")
+    device.bao_decode_batch(out, n, hashes, dec, status, scratch)
+    torch.cuda.synchronize()
+    assert torch.equal(dec, inp) and int(status.abs().sum()) == 0
+    out[777, 8 + 3] ^= 1  # the root's left child CV
+    device.bao_decode_batch(out, n, hashes, dec, status, scratch)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    assert st[777] != 0 and int(np.abs(np.delete(st, 777)).sum()) == 0

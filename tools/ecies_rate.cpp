@@ -1,8 +1,8 @@
 // ecies_rate.cpp — per-object cost of the ECIES host stage on T threads
 // (host_stages.cpp): ecies_prepare (two scalar multiplications + HKDF),
 // ecies_encrypt of a 1-byte message, and the stream encrypt with a prepared
-// key.  Thread-microseconds per operation (wall x T / ops): flat in T when
-// the threads do not contend.  Build (in tools/):
+// key.  Thread-microseconds per operation (wall / ops per thread; every
+// thread does N): flat in T when the threads do not contend.  Build (in tools/):
 //   g++ -O2 -std=c++17 -I../carbonado_amd/csrc -I../include ecies_rate.cpp \
 //       ../carbonado_amd/lib/obj/host_host_stages.cpp.o -lcrypto -lpthread -o ecies_rate
 #include <chrono>
@@ -29,7 +29,7 @@ int main(int argc, char **argv) {
             std::vector<std::thread> th;
             for (int t = 0; t < T; ++t) th.emplace_back([&, t] { f(t); });
             for (auto &x : th) x.join();
-            return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / N * 1e6 * T;
+            return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / N * 1e6;
         };
         const double a = run([&](int t) {
             EciesKey k;

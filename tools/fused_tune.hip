@@ -200,24 +200,27 @@ int main(int argc, char **argv) {
         void (*kv[5])(const uint8_t *, uint64_t, uint64_t, const uint64_t *, uint8_t *, uint64_t, uint8_t *, uint64_t) = {
             fused::bao_levels123_kernel<1>, fused::bao_levels123_kernel<2>, fused::bao_levels123_kernel<0>, nullptr,
             fused::bao_levels123_seg_kernel};
-        void (*kq[7])(const uint8_t *, uint64_t, uint64_t, const uint64_t *, uint8_t *, uint64_t, uint8_t *, uint64_t,
+        void (*kq[8])(const uint8_t *, uint64_t, uint64_t, const uint64_t *, uint8_t *, uint64_t, uint8_t *, uint64_t,
                       uint64_t, uint64_t, uint64_t) = {nullptr, nullptr, nullptr, fused::bao_levels123_lds_kernel<4>,
                                                        nullptr, fused::bao_levels123_lds_kernel<1>,
-                                                       fused::bao_levels123_lds_kernel<2>};
-        const char *kn[7] = {"8-B node stores", "16-B node stores", "no node stores (diagnostic)",
-                             "LDS-staged node stores, a level per round (QS 4, round 4)",
+                                                       fused::bao_levels123_lds_kernel<2>,
+                                                       fused::bao_levels123_lds_kernel<4>};
+        const char *kn[8] = {"8-B node stores", "16-B node stores", "no node stores (diagnostic)",
+                             "LDS-staged node stores, a level per round (QS 4, product)",
                              "node stacks as whole 64-B segments (SEG)",
                              "LDS-staged node stores, a node per round (QS 1)",
-                             "LDS-staged node stores, two nodes per round (QS 2)"};
-        std::vector<float> t3[7];
-        unsigned long long sum3[7] = {0, 0, 0, 0, 0, 0, 0};
+                             "LDS-staged node stores, two nodes per round (QS 2)",
+                             "QS 4, stream base shifted 56 B: every node 64-B aligned (diagnostic, wrong bytes)"};
+        std::vector<float> t3[8];
+        unsigned long long sum3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int rd = 0; rd < rounds + 1; ++rd)
-            for (int k = 0; k < 7; ++k) {
+            for (int k = 0; k < 8; ++k) {
                 const int tpb = (k == 3 || k >= 5) ? 64 : 256;
                 CK(hipEventRecord(e0));
                 if (kq[k])
                     hipLaunchKernelGGL(kq[k], dim3((unsigned)((work + tpb - 1) / tpb)), dim3(tpb), 0, 0, cv, N, count,
-                                       dcoff[0], out, bstride, cv3, n3, (uint64_t)0, (uint64_t)0, (uint64_t)0);
+                                       dcoff[0], out + (k == 7 ? 56 : 0), bstride, cv3, n3, (uint64_t)0,
+                                       (uint64_t)0, (uint64_t)0);
                 else
                     hipLaunchKernelGGL(kv[k], dim3((unsigned)((work + tpb - 1) / tpb)), dim3(tpb), 0, 0, cv, N, count,
                                        dcoff[0], out, bstride, cv3, n3);
@@ -231,7 +234,7 @@ int main(int argc, char **argv) {
         printf("levels 1-3 outputs: LDS-staged %s 8-B stores; 16-B %s; SEG %s; QS 1 %s; QS 2 %s\n",
                sum3[3] == sum3[0] ? "==" : "!=", sum3[1] == sum3[0] ? "==" : "!=", sum3[4] == sum3[0] ? "==" : "!=",
                sum3[5] == sum3[0] ? "==" : "!=", sum3[6] == sum3[0] ? "==" : "!=");
-        for (int k = 0; k < 7; ++k) {
+        for (int k = 0; k < 8; ++k) {
             std::sort(t3[k].begin(), t3[k].end());
             printf("levels 1-3 from chunk CVs (bao_levels123_kernel), %s, %llu objects: median %.3f ms\n", kn[k],
                    (unsigned long long)count, t3[k][t3[k].size() / 2]);
