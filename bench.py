@@ -100,6 +100,9 @@ def parse(argv=None):
     ap.add_argument("--slice-mib", type=int, default=256, help="e2e mode: input bytes per pipeline slice")
     ap.add_argument("--in-pad-kib", type=int, default=0, help="encode/decode: extra bytes per input object row")
     ap.add_argument("--out-pad-kib", type=int, default=0, help="encode/decode: extra bytes per output object row")
+    ap.add_argument("--stream-offset", type=int, default=0,
+                    help="pipeline at Zfec|Bao: each stream starts this many bytes into its 256-B multiple row "
+                         "(56: every chunk and node on a 64-B boundary, include/carbonado_hip.h)")
     ap.add_argument("--prealloc-gib", type=float, default=0, help="allocate (and keep) this much HBM first")
     ap.add_argument("--alloc", choices=["chip", "contiguous", "torch"], default="chip",
                     help="device batch buffers: the library's class-balanced allocator (chip_device_alloc via "
@@ -712,10 +715,12 @@ class Workload:
                 raise SystemExit("--mode pipeline runs the device-only levels (Bao/Zfec bits); use --mode e2e")
             zlen = m * C if lv & 8 else n
             self.blen = blen = L.chip_bao_encoded_len(zlen) if lv & 4 else zlen
-            self.out = batch_buf((count, (blen + 255) // 256 * 256), "out")
+            self.soff = off = args.stream_offset if lv & 12 == 12 else 0
+            self.out = batch_buf((count, (off + blen + 255) // 256 * 256), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.encode_scratch(lv, n, count, dev)
-            self.step = lambda: device.encode_batch(lv, self.inp_full, n, self.out, self.hashes, self.scratch)
+            self.step = lambda: device.encode_batch(lv, self.inp_full, n, self.out, self.hashes, self.scratch,
+                                                    out_offset=off)
             # HBM bytes: the object read once, its stream written once.  At Zfec|Bao the fused
             # kernel (K13) hashes the shards on chip; CHIP_FUSED=0 runs K1-BL + K3, which
             # read the 8C bytes of shards back (counted then)
@@ -1093,8 +1098,17 @@ class Workload:
         bao = self.args.mode == "bao"
         olen = self.blen if (pipeline or bao) else m * C  # bytes of each object's output
         digests = torch.empty((count, 32), dtype=torch.uint8, device=self.dev)
-        scratch = device.bao_scratch(olen, count, self.dev)
-        device.bao_encode_batch(self.out, olen, None, digests, scratch)
+        off = getattr(self, "soff", 0) if pipeline else 0
+        if off:  # streams 8-B aligned in their rows: hashed from 16-B aligned copies, 64 rows at a time
+            scratch = device.bao_scratch(olen, 64, self.dev)
+            for o0 in range(0, count, 64):
+                o1 = min(count, o0 + 64)
+                rows = self.out[o0:o1, off:off + olen].contiguous()
+                device.bao_encode_batch(rows, olen, None, digests[o0:o1], scratch)
+                del rows
+        else:
+            scratch = device.bao_scratch(olen, count, self.dev)
+            device.bao_encode_batch(self.out, olen, None, digests, scratch)
         torch.cuda.synchronize()
         gpu = digests.cpu().numpy()
         hashes = self.hashes.cpu().numpy() if (pipeline or bao) else None
@@ -1328,7 +1342,7 @@ class Workload:
             ok = self.digest == O.blake3(self.inp.numpy().reshape(-1))
         elif self.args.mode == "pipeline":
             enc, h, _ = O.encode(sample, self.args.level)
-            ok = (self.out[0, :self.blen].cpu().numpy().tobytes() == enc and
+            ok = (self.out[0, self.soff:self.soff + self.blen].cpu().numpy().tobytes() == enc and
                   (self.hashes[0].cpu().numpy().tobytes() == h if self.args.level & 4 else True))
         elif self.args.mode == "e2e-decode":
             ok = self.h_out[0, :self.n].numpy().tobytes() == sample
@@ -1560,6 +1574,8 @@ def main():
                          "min_launch_ms": round(min(launch_ms), 4)},
             "verified_object0": verified,
         }
+        if getattr(wl, "soff", 0):
+            res["config"]["stream_offset"] = wl.soff
         if live and "bytes" in live:
             res["roofline"].update({"traffic_ratio": round(live["bytes"] / wl.alg_bytes, 4),
                                     "pmc_KiB_per_launch": {"FETCH_SIZE": live["FETCH_SIZE_KiB"],

@@ -131,6 +131,10 @@ bool valid_km(uint32_t k, uint32_t m);
 void calc_pad(uint64_t n, uint32_t k, uint32_t *pad, uint64_t *C);  // utils.rs:47-58, k generalised
 // rows 0..k-1 copied, k..m-1 computed (aliased: in place, parity rows only)
 GfPlan encode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint8_t> &enc, bool aliased = false);
+// whether zfec_bao_dev writes the streams with K13, which takes any 8-B
+// aligned stream base (its line stores split each chunk at the memory lines
+// wherever they fall); KS and the two-kernel path want 16-B aligned rows
+bool zfec_bao_any8(uint64_t C, uint64_t count);
 // encode() at Zfec|Bao of device-resident objects (K13, or KS for small ones)
 hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
                         uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s);

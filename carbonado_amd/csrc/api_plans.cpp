@@ -118,6 +118,10 @@ int pipe_wg_cfg() {
 // chip instead of read back from HBM; CHIP_FUSED=0 runs the two-kernel
 // overlapped pipeline below (A/B runs).  Scratch: zfec_bao_scratch_len.
 
+bool zfec_bao_any8(uint64_t C, uint64_t count) {
+    return fused_on() && !small_ok((uint64_t)CHIP_FEC_M * C, count, KS_TINY_N - 1);
+}
+
 hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
                         uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, void *d_scratch, hipStream_t s) {
     const uint64_t zlen = (uint64_t)CHIP_FEC_M * C;

@@ -243,13 +243,18 @@ int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_strid
                           uint8_t *d_out, uint64_t out_stride, uint64_t *out_len, uint8_t *d_hash,
                           chip_encode_info *info, void *d_scratch, void *stream) {
     if (has_host_stages(format) || format > 15) return CHIP_ERR_INVALID_ARG;
-    if ((!d_in && n) || !out_len || (!d_hash && count) || (in_stride % 16) || (out_stride % 16) ||
-        misaligned16(d_in) || misaligned16(d_out))
+    if ((!d_in && n) || !out_len || (!d_hash && count) || (in_stride % 16) || misaligned16(d_in))
         return CHIP_ERR_INVALID_ARG;
     chip_encode_info inf;
     uint64_t zlen, fl;
     int st = encode_info_for(format, n, n, 0, 0, &inf, &zlen, &fl);
     if (st != CHIP_OK) return st;
+    {  // output rows: 16-B aligned, or 8-B aligned where K13 writes the streams
+        const bool any8 = (format & CHIP_FORMAT_ZFEC) && (format & CHIP_FORMAT_BAO) && zlen &&
+                          zfec_bao_any8(inf.chunk_len, count);
+        const uint64_t a = any8 ? 8 : 16;
+        if ((out_stride % a) || (reinterpret_cast<uintptr_t>(d_out) % a)) return CHIP_ERR_INVALID_ARG;
+    }
     if ((fl && !d_out) || (count > 1 && out_stride < fl)) return CHIP_ERR_BUFFER_TOO_SMALL;
     if (count > 1 && in_stride < n) return CHIP_ERR_INVALID_ARG;  // rows would overlap
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;

@@ -104,21 +104,29 @@ def encode_scratch(fmt: int, n: int, count: int, device=None) -> torch.Tensor:
 
 
 def encode_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes: torch.Tensor,
-                 scratch: torch.Tensor):
+                 scratch: torch.Tensor, out_offset: int = 0):
     """encode() of device-resident objects at a level without host stages
     (Bao and/or Zfec bits): inp uint8 [count, in_stride] (first n bytes of each
-    row), out uint8 [count, >= encoded length], hashes uint8 [count, 32].
-    Zfec|Bao runs fused (shards hashed on chip, written into their bao slots).
-    Returns (encoded length, EncodeInfoC)."""
+    row), out uint8 [count, >= out_offset + encoded length], hashes uint8
+    [count, 32]; each encoding starts `out_offset` bytes into its row (56 with
+    a 256-B multiple row: STREAM_OFFSET, the fast layout of Zfec|Bao streams,
+    include/carbonado_hip.h).  Zfec|Bao runs fused (shards hashed on chip,
+    written into their bao slots).  Returns (encoded length, EncodeInfoC)."""
     assert inp.is_cuda and out.is_cuda and inp.is_contiguous() and out.is_contiguous()
     assert inp.shape[0] == out.shape[0] == hashes.shape[0] and inp.shape[1] >= n
     olen = ctypes.c_uint64()
     info = _lib.EncodeInfoC()
-    check(_lib.lib().chip_encode_batch_dev(fmt, _p(inp), inp.shape[1], n, inp.shape[0], _p(out), out.shape[1],
-                                           ctypes.byref(olen), _p(hashes), ctypes.byref(info), _p(scratch),
-                                           _stream()))
-    assert olen.value <= out.shape[1]
+    check(_lib.lib().chip_encode_batch_dev(fmt, _p(inp), inp.shape[1], n, inp.shape[0], _p(out) + out_offset,
+                                           out.shape[1], ctypes.byref(olen), _p(hashes), ctypes.byref(info),
+                                           _p(scratch), _stream()))
+    assert out_offset + olen.value <= out.shape[1]
     return olen.value, info
+
+
+# Where a Zfec|Bao stream starts in a row of 256-B multiple pitch for the fast
+# layout: its 8-byte header fills the end of a 64-B segment, so every chunk and
+# parent node after it starts on a 64-B boundary (include/carbonado_hip.h).
+STREAM_OFFSET = 56
 
 
 def decode_scratch(fmt: int, in_len: int, count: int, device=None) -> torch.Tensor:

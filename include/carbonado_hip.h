@@ -373,9 +373,16 @@ CHIP_API int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, 
  * them straight into their chunk slots of the bao stream (no zfec buffer,
  * the shards cross HBM once; CHIP_FUSED=0 selects the two-kernel path).
  * d_scratch: chip_encode_scratch_len(format, n, count) bytes.  Pointers and
- * strides must be multiples of 16; enqueued on `stream`, not synchronised.
- * Replaces, for these levels, encode() = zfec (encoding.rs:121-138) -> bao
- * (encoding.rs:140-147) in one call per batch. */
+ * strides must be multiples of 16 (CHIP_ERR_INVALID_ARG otherwise), except
+ * d_out and out_stride at Zfec|Bao for streams of more than 512 chunks
+ * (objects over 128 KiB), which the fused kernel writes at any 8-B phase:
+ * there they need only be multiples of 8.  The fast layout for those puts
+ * each stream at 56 mod 64 (d_out and out_stride), so that after its 8-byte
+ * header every chunk and parent node starts on a 64-B boundary and no store
+ * splits a 64-B segment (rows of a 256-B multiple pitch, the stream 56 bytes
+ * in).  Enqueued on `stream`, not synchronised.  Replaces, for these levels,
+ * encode() = zfec (encoding.rs:121-138) -> bao (encoding.rs:140-147) in one
+ * call per batch. */
 CHIP_API uint64_t chip_encode_scratch_len(uint8_t format, uint64_t n, uint64_t count);
 CHIP_API int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_stride, uint64_t n,
                                    uint64_t count, uint8_t *d_out, uint64_t out_stride, uint64_t *out_len,

@@ -475,3 +475,53 @@ def test_encode_batch_dev_k13_general_cols(gpu, cols):
         assert got[o, :olen].tobytes() == enc, o
         assert (got[o, olen:] == 0xA5).all()
         assert gh[o].tobytes() == h
+
+
+@pytest.mark.parametrize("cols,pad,off", [(129, True, 56), (133, True, 8), (136, False, 56), (4097, True, 56),
+                                          (256, False, 120)])
+def test_encode_batch_dev_stream_offset(gpu, cols, pad, off):
+    """Zfec|Bao streams at an 8-B phase in their rows (include/carbonado_hip.h:
+    56 mod 64 puts every chunk and node on a 64-B boundary): K13's FULL path
+    (cols % 8 == 0, no zfec padding) and general path, the row pitch a 256-B
+    multiple plus the offset phase; every stream and hash == the oracle's, no
+    byte before the offset or after the stream written."""
+    import torch
+    from carbonado_amd import device
+    count = 3
+    rng = np.random.default_rng(cols + off)
+    n = (cols - 1) * 4096 + int(rng.integers(1, 4096)) if pad else cols * 4096
+    stride = (n + 255) // 256 * 256
+    host = rng.integers(0, 256, (count, stride), dtype=np.uint8)
+    inp = torch.from_numpy(host).cuda()
+    oenc0, _, _ = O.encode(host[0, :n].tobytes(), 12)
+    ostride = (off + len(oenc0) + 255) // 256 * 256 + (off % 16)  # the phase repeats in every row
+    out = torch.full((count, ostride), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.full((count, 32), 0x5A, dtype=torch.uint8, device="cuda")
+    scratch = device.encode_scratch(12, n, count)
+    olen, info = device.encode_batch(12, inp, n, out, hashes, scratch, out_offset=off)
+    torch.cuda.synchronize()
+    got, gh = out.cpu().numpy(), hashes.cpu().numpy()
+    for o in range(count):
+        enc, h, _ = O.encode(host[o, :n].tobytes(), 12)
+        assert olen == len(enc)
+        assert got[o, off:off + olen].tobytes() == enc, o
+        assert (got[o, :off] == 0xA5).all() and (got[o, off + olen:] == 0xA5).all(), o
+        assert gh[o].tobytes() == h
+
+
+def test_encode_batch_dev_stream_offset_refused_where_not_k13(gpu):
+    """An 8-B (not 16-B) aligned stream base is refused where the batch does not
+    run K13 (small streams take KS): CHIP_ERR_INVALID_ARG, nothing written."""
+    import torch
+    from carbonado_amd import device
+    from carbonado_amd.error import CarbonadoError
+    n, count = 4096 * 8, 4  # 32 KiB objects: 64-chunk streams, KS below 64
+    inp = torch.zeros((count, n), dtype=torch.uint8, device="cuda")
+    out = torch.full((count, 1 << 17), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    scratch = device.encode_scratch(12, n, count)
+    small = 4096 * 3  # 24 KiB: 24-chunk streams (KS)
+    with pytest.raises(CarbonadoError):
+        device.encode_batch(12, inp[:, :small].contiguous(), small, out, hashes, scratch, out_offset=56)
+    torch.cuda.synchronize()
+    assert bool((out == 0xA5).all())
