@@ -260,10 +260,12 @@ struct SplitPending {
 // (SplitGeo): the region's nodes go to sl.hnodes, the tail to out.
 int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_encode_info &inf,
                        const uint8_t *src, uint64_t src_pitch, uint64_t cur_n, uint64_t zlen, uint64_t final_len,
-                       uint64_t cnt, uint8_t *out, uint64_t out_pitch, uint8_t *hashes,
+                       uint64_t cnt, uint8_t *out, uint64_t out_pitch, uint8_t *hashes, uint64_t stream_off,
                        const SplitGeo *split = nullptr, bool from_rows = false) {
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
-    const uint64_t n_al = row_pitch(cur_n), z_al = row_pitch(zlen), f_al = row_pitch(final_len);
+    // K13's streams 56 B into their rows: every chunk and node on a 64-B boundary
+    const uint64_t soff = zfec && bao && zlen && zfec_bao_any8(inf.chunk_len, cnt) ? stream_off : 0;
+    const uint64_t n_al = row_pitch(cur_n), z_al = row_pitch(zlen), f_al = row_pitch(final_len + soff);
     uint8_t *d_in = static_cast<uint8_t *>(sl.in.p);
     if (from_rows && split && cur_n) {
         // the host stage wrote each object's zfec input into its stream's chunk slots
@@ -278,12 +280,12 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
     const uint8_t *d_cur = d_in;
     uint64_t cur_stride = n_al;
     if (zfec && bao && zlen) {  // fused: shards written into the bao streams, hashed in place
-        CHIP_HIP(zfec_bao_dev(d_in, n_al, cur_n, cnt, inf.chunk_len, static_cast<uint8_t *>(sl.out.p), f_al,
-                              static_cast<uint8_t *>(sl.hash.p), sl.scratch.p, sl.stream));
+        uint8_t *d_str = static_cast<uint8_t *>(sl.out.p) + soff;
+        CHIP_HIP(zfec_bao_dev(d_in, n_al, cur_n, cnt, inf.chunk_len, d_str, f_al, static_cast<uint8_t *>(sl.hash.p),
+                              sl.scratch.p, sl.stream));
         CHIP_HIP(hipMemcpyAsync(hashes, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, sl.stream));
         if (split) {
             const uint64_t ns = 64 * split->nb;
-            uint8_t *d_str = static_cast<uint8_t *>(sl.out.p);
             if (ns) {
                 CHIP_HIP(bao_data_nodes(d_str, f_al, split->N, split->nd, cnt, static_cast<uint8_t *>(sl.nodes.p), ns,
                                         sl.stream));
@@ -292,8 +294,7 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
             CHIP_HIP(hipMemcpy2DAsync(out + split->t0, out_pitch, d_str + split->t0, f_al, final_len - split->t0, cnt,
                                       hipMemcpyDeviceToHost, sl.stream));
         } else if (final_len) {
-            CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, sl.out.p, f_al, final_len, cnt, hipMemcpyDeviceToHost,
-                                      sl.stream));
+            CHIP_HIP(hipMemcpy2DAsync(out, out_pitch, d_str, f_al, final_len, cnt, hipMemcpyDeviceToHost, sl.stream));
         }
         return CHIP_OK;
     }
@@ -380,6 +381,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
     // into out (pinned), which the device then reads: no staging copy at all
     const bool direct_fmt = split_fmt && hs && stream_encrypt_on() && direct_rows_on() && out && host_pinned(out);
     SplitGeos geos;
+    const uint64_t soff_cfg = stream_offset();  // where K13's streams sit in the slot rows (this call)
     if (c) {
         if (c->slots.size() < nslots) c->slots.resize(nslots);
         for (uint32_t k = 0; k < nslots; ++k) {
@@ -388,7 +390,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             CHIP_HIP(grow(sl.in, S * row_pitch(h_max)));
             if (zfec && !bao) CHIP_HIP(grow(sl.mid, S * row_pitch(zlen_max)));  // Zfec|Bao: fused
             if (bao) {
-                CHIP_HIP(grow(sl.out, S * row_pitch(final_max)));
+                CHIP_HIP(grow(sl.out, S * row_pitch(final_max + soff_cfg)));
                 CHIP_HIP(grow(sl.scratch, zfec ? std::max(zfec_bao_scratch_len(zlen_max, S), bao_scratch_len(zlen_max, S))
                                                 : bao_scratch_len(zlen_max, S)));
             }
@@ -572,7 +574,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
             const SplitGeo *g = split_fmt && zl >= 2048 ? &geos.get(zl / 1024) : nullptr;
             const uint64_t opitch = count > 1 ? out_stride : fl;
             st = batch_slice_device(*sl, format, &p2, inf, src, src_pitch, cur_n, zl, fl, cnt, out + o0 * out_stride,
-                                    opitch, hashes + 32 * o0, g, rows);
+                                    opitch, hashes + 32 * o0, soff_cfg, g, rows);
             if (st != CHIP_OK) {
                 drain();
                 return st;
@@ -587,7 +589,7 @@ int chip_encode_host_batch(uint8_t format, const uint8_t *pubkey, uint64_t pubke
                 (void)encode_info_for(format, n, len[j], 0, 0, &inf, &zl, &fl);
                 const GfPlan pj = encode_plan(CHIP_FEC_K, CHIP_FEC_M, inf.chunk_len, enc);
                 st = batch_slice_device(*sl, format, &pj, inf, src + j * src_pitch, src_pitch, len[j], zl, fl, 1,
-                                        out + (o0 + j) * out_stride, fl, hashes + 32 * (o0 + j));
+                                        out + (o0 + j) * out_stride, fl, hashes + 32 * (o0 + j), soff_cfg);
                 if (st != CHIP_OK) {
                     drain();
                     return st;

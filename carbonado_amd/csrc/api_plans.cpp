@@ -118,6 +118,12 @@ int pipe_wg_cfg() {
 // chip instead of read back from HBM; CHIP_FUSED=0 runs the two-kernel
 // overlapped pipeline below (A/B runs).  Scratch: zfec_bao_scratch_len.
 
+uint64_t stream_offset() {  // read per call (tests flip it); the caller reads it once per batch
+    const char *e = std::getenv("CHIP_STREAM_OFFSET");
+    const uint64_t o = e ? std::strtoull(e, nullptr, 10) : 0;
+    return std::min<uint64_t>(o, 248) & ~(uint64_t)7;
+}
+
 bool zfec_bao_any8(uint64_t C, uint64_t count) {
     return fused_on() && !small_ok((uint64_t)CHIP_FEC_M * C, count, KS_TINY_N - 1);
 }

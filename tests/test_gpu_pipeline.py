@@ -135,6 +135,16 @@ def test_encode_host_batch_ragged_host_stage_sizes(gpu):
             assert out[o, :olen[o]].numpy().tobytes() == enc and hashes[o].numpy().tobytes() == h, (level, o)
 
 
+@pytest.mark.parametrize("n", [(1 << 20) + 5, 3 << 20])
+@pytest.mark.parametrize("level", [12, 15])
+def test_encode_host_batch_stream_offset(gpu, level, n, monkeypatch):
+    """CHIP_STREAM_OFFSET=56: the slot rows hold K13's streams 56 B in (every
+    chunk and node on a 64-B boundary); the split copy-back, the node gather
+    and the whole-stream copy read them from there — the same bytes."""
+    monkeypatch.setenv("CHIP_STREAM_OFFSET", "56")
+    test_encode_host_batch_split_copy_back(gpu, level, n)
+
+
 @pytest.mark.parametrize("n", [1, 1000, 4096, 70_001, (1 << 20) + 5, 3 << 20])
 @pytest.mark.parametrize("level", [12, 13, 14, 15])
 def test_encode_host_batch_split_copy_back(gpu, level, n):
