@@ -116,7 +116,7 @@ def encode_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes:
     assert inp.shape[0] == out.shape[0] == hashes.shape[0] and inp.shape[1] >= n
     olen = ctypes.c_uint64()
     info = _lib.EncodeInfoC()
-    check(_lib.lib().chip_encode_batch_dev(fmt, _p(inp), inp.shape[1], n, inp.shape[0], _p(out) + out_offset,
+    check(_lib.lib().chip_encode_batch_dev(fmt, _p(inp), inp.shape[1], n, inp.shape[0], ctypes.c_void_p(out.data_ptr() + out_offset),
                                            out.shape[1], ctypes.byref(olen), _p(hashes), ctypes.byref(info),
                                            _p(scratch), _stream()))
     assert out_offset + olen.value <= out.shape[1]
