@@ -100,9 +100,12 @@ def parse(argv=None):
     ap.add_argument("--slice-mib", type=int, default=256, help="e2e mode: input bytes per pipeline slice")
     ap.add_argument("--in-pad-kib", type=int, default=0, help="encode/decode: extra bytes per input object row")
     ap.add_argument("--out-pad-kib", type=int, default=0, help="encode/decode: extra bytes per output object row")
-    ap.add_argument("--stream-offset", type=int, default=0,
+    ap.add_argument("--bao-stream-offset", type=int, default=0,
+                    help="bao mode: each stream starts this many bytes into its 256-B multiple row (A/B of 56)")
+    ap.add_argument("--stream-offset", type=int, default=56,
                     help="pipeline at Zfec|Bao: each stream starts this many bytes into its 256-B multiple row "
-                         "(56: every chunk and node on a 64-B boundary, include/carbonado_hip.h)")
+                         "(56, the default: every chunk and node on a 64-B boundary, include/carbonado_hip.h; "
+                         "0: streams at the row start, +4 to +11 %% slower, profiles/r10i_session)")
     ap.add_argument("--prealloc-gib", type=float, default=0, help="allocate (and keep) this much HBM first")
     ap.add_argument("--alloc", choices=["chip", "contiguous", "torch"], default="chip",
                     help="device batch buffers: the library's class-balanced allocator (chip_device_alloc via "
@@ -1008,10 +1011,12 @@ class Workload:
             self.kernel_sym = "bao_chunk_kernel_verify"
         else:
             self.blen = blen = L.chip_bao_encoded_len(n)
-            self.out = batch_buf((count, (blen + 255) // 256 * 256), "out")
+            self.soff = off = args.bao_stream_offset
+            self.out = batch_buf((count, (off + blen + 255) // 256 * 256), "out")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             self.scratch = device.bao_scratch(n, count, dev)
-            self.step = lambda: device.bao_encode_batch(self.inp_full, n, self.out, self.hashes, self.scratch)
+            self.step = lambda: device.bao_encode_batch(self.inp_full, n, self.out, self.hashes, self.scratch,
+                                                        out_offset=off)
             self.alg_bytes = count * (n + blen)
             fused = n >= 65536 and os.environ.get("CHIP_FUSED", "1") != "0"
             self.kernel = ("bao_content_fused_kernel (K13 content mode: chunk hashing + tree levels 1-3, 64 consecutive "
@@ -1098,7 +1103,7 @@ class Workload:
         bao = self.args.mode == "bao"
         olen = self.blen if (pipeline or bao) else m * C  # bytes of each object's output
         digests = torch.empty((count, 32), dtype=torch.uint8, device=self.dev)
-        off = getattr(self, "soff", 0) if pipeline else 0
+        off = getattr(self, "soff", 0) if (pipeline or bao) else 0
         if off:  # streams 8-B aligned in their rows: hashed from 16-B aligned copies, 64 rows at a time
             scratch = device.bao_scratch(olen, 64, self.dev)
             for o0 in range(0, count, 64):

@@ -136,7 +136,7 @@ GfPlan encode_plan(uint32_t k, uint32_t m, uint64_t C, const std::vector<uint8_t
 // wherever they fall); KS and the two-kernel path want 16-B aligned rows
 bool zfec_bao_any8(uint64_t C, uint64_t count);
 // where the library's own slot rows put a K13 stream (CHIP_STREAM_OFFSET, a
-// multiple of 8 below 256; 56: every chunk and node on a 64-B boundary)
+// multiple of 8 below 256; default 56: every chunk and node on a 64-B boundary)
 uint64_t stream_offset();
 // encode() at Zfec|Bao of device-resident objects (K13, or KS for small ones)
 hipError_t zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,

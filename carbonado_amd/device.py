@@ -89,12 +89,15 @@ def bao_scratch(n: int, count: int, device=None) -> torch.Tensor:
 
 
 def bao_encode_batch(inp: torch.Tensor, n: int, out: torch.Tensor | None, hashes: torch.Tensor,
-                     scratch: torch.Tensor) -> None:
-    """out: uint8 [count, >= bao_len(n)] or None (hash only); hashes: uint8 [count, 32]."""
+                     scratch: torch.Tensor, out_offset: int = 0) -> None:
+    """out: uint8 [count, >= out_offset + bao_len(n)] or None (hash only), each
+    stream `out_offset` bytes into its row (8-B multiple; 56: every chunk and
+    node on a 64-B boundary); hashes: uint8 [count, 32]."""
     assert inp.is_contiguous() and inp.shape[1] >= n  # the row stride is inp.shape[1]
     count = inp.shape[0]
     check(_lib.lib().chip_bao_encode_batch_dev(
-        _p(inp), inp.shape[1], n, count, _p(out) if out is not None else ctypes.c_void_p(0),
+        _p(inp), inp.shape[1], n, count,
+        ctypes.c_void_p(out.data_ptr() + out_offset) if out is not None else ctypes.c_void_p(0),
         out.shape[1] if out is not None else 0, _p(hashes), _p(scratch), _stream()))
 
 
@@ -116,9 +119,10 @@ def encode_batch(fmt: int, inp: torch.Tensor, n: int, out: torch.Tensor, hashes:
     assert inp.shape[0] == out.shape[0] == hashes.shape[0] and inp.shape[1] >= n
     olen = ctypes.c_uint64()
     info = _lib.EncodeInfoC()
-    check(_lib.lib().chip_encode_batch_dev(fmt, _p(inp), inp.shape[1], n, inp.shape[0], ctypes.c_void_p(out.data_ptr() + out_offset),
-                                           out.shape[1], ctypes.byref(olen), _p(hashes), ctypes.byref(info),
-                                           _p(scratch), _stream()))
+    check(_lib.lib().chip_encode_batch_dev(fmt, _p(inp), inp.shape[1], n, inp.shape[0],
+                                           ctypes.c_void_p(out.data_ptr() + out_offset), out.shape[1],
+                                           ctypes.byref(olen), _p(hashes), ctypes.byref(info), _p(scratch),
+                                           _stream()))
     assert out_offset + olen.value <= out.shape[1]
     return olen.value, info
 

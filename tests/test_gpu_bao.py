@@ -241,3 +241,26 @@ def test_batch_bao_many_small_trees(gpu, n):
     torch.cuda.synchronize()
     st = status.cpu().numpy()
     assert st[777] != 0 and int(np.abs(np.delete(st, 777)).sum()) == 0
+
+
+@pytest.mark.parametrize("n", [65536 + 1, 4 * 65536 + 9 * 1024, 9 * 1024 + 37])
+def test_batch_bao_stream_offset(gpu, n):
+    """bao streams 56 B into their rows (every chunk and node on a 64-B
+    boundary): the content-mode kernel, its tail kernel and K3 write the same
+    streams at that phase, nothing before or after them."""
+    import torch
+    from carbonado_amd import device
+    count, off = 5, 56
+    gen = torch.Generator(device="cuda").manual_seed(n % 991)
+    inp = torch.randint(0, 256, (count, (n + 255) // 256 * 256), dtype=torch.uint8, device="cuda", generator=gen)
+    blen = O.lib().orc_bao_encoded_len(n)
+    out = torch.full((count, (off + blen + 255) // 256 * 256), 0xA5, dtype=torch.uint8, device="cuda")
+    hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+    device.bao_encode_batch(inp, n, out, hashes, device.bao_scratch(n, count), out_offset=off)
+    torch.cuda.synchronize()
+    host, h_in = out.cpu().numpy(), inp.cpu().numpy()
+    for o in range(count):
+        oe, oh = O.bao_encode(h_in[o, :n].tobytes())
+        assert hashes[o].cpu().numpy().tobytes() == oh, o
+        assert host[o, off:off + blen].tobytes() == oe, o
+        assert (host[o, :off] == 0xA5).all() and (host[o, off + blen:] == 0xA5).all(), o

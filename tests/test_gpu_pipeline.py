@@ -137,11 +137,13 @@ def test_encode_host_batch_ragged_host_stage_sizes(gpu):
 
 @pytest.mark.parametrize("n", [(1 << 20) + 5, 3 << 20])
 @pytest.mark.parametrize("level", [12, 15])
-def test_encode_host_batch_stream_offset(gpu, level, n, monkeypatch):
-    """CHIP_STREAM_OFFSET=56: the slot rows hold K13's streams 56 B in (every
-    chunk and node on a 64-B boundary); the split copy-back, the node gather
-    and the whole-stream copy read them from there — the same bytes."""
-    monkeypatch.setenv("CHIP_STREAM_OFFSET", "56")
+@pytest.mark.parametrize("soff", ["0", "120"])
+def test_encode_host_batch_stream_offset(gpu, level, n, soff, monkeypatch):
+    """The slot rows hold K13's streams CHIP_STREAM_OFFSET bytes in (default
+    56: every chunk and node on a 64-B boundary, covered by the split
+    copy-back test); at the row start and at another 8-B phase the split
+    copy-back, the node gather and the whole-stream copy give the same bytes."""
+    monkeypatch.setenv("CHIP_STREAM_OFFSET", soff)
     test_encode_host_batch_split_copy_back(gpu, level, n)
 
 
