@@ -263,8 +263,11 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
                        uint64_t cnt, uint8_t *out, uint64_t out_pitch, uint8_t *hashes, uint64_t stream_off,
                        const SplitGeo *split = nullptr, bool from_rows = false) {
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
-    // K13's streams 56 B into their rows: every chunk and node on a 64-B boundary
-    const uint64_t soff = zfec && bao && zlen && zfec_bao_any8(inf.chunk_len, cnt) ? stream_off : 0;
+    // the streams 56 B into their rows: every chunk and node on a 64-B boundary
+    // (K13, and K3 / the content mode for Bao alone; not KS, below 513 chunks)
+    const bool any8 = bao && zlen &&
+                      (zfec ? zfec_bao_any8(inf.chunk_len, cnt) : (zlen + 1023) / 1024 > KS_MAX_N);
+    const uint64_t soff = any8 ? stream_off : 0;
     const uint64_t n_al = row_pitch(cur_n), z_al = row_pitch(zlen), f_al = row_pitch(final_len + soff);
     uint8_t *d_in = static_cast<uint8_t *>(sl.in.p);
     if (from_rows && split && cur_n) {
@@ -307,9 +310,9 @@ int batch_slice_device(Slot &sl, uint8_t format, const GfPlan *plan, const chip_
     const uint8_t *d_res = d_cur;
     uint64_t res_stride = cur_stride;
     if (bao) {
-        CHIP_HIP(bao_encode_dev(d_cur, cur_stride, zlen, cnt, static_cast<uint8_t *>(sl.out.p), f_al,
+        CHIP_HIP(bao_encode_dev(d_cur, cur_stride, zlen, cnt, static_cast<uint8_t *>(sl.out.p) + soff, f_al,
                                 static_cast<uint8_t *>(sl.hash.p), sl.scratch.p, sl.stream));
-        d_res = static_cast<const uint8_t *>(sl.out.p);
+        d_res = static_cast<const uint8_t *>(sl.out.p) + soff;
         res_stride = f_al;
         CHIP_HIP(hipMemcpyAsync(hashes, sl.hash.p, 32 * cnt, hipMemcpyDeviceToHost, sl.stream));
     } else {

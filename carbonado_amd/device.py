@@ -154,11 +154,13 @@ def decode_batch(fmt: int, enc: torch.Tensor, in_len: int, hashes: torch.Tensor,
 
 
 def bao_decode_batch(enc: torch.Tensor, n: int, hashes: torch.Tensor, out: torch.Tensor,
-                     status: torch.Tensor, scratch: torch.Tensor) -> None:
-    """status: int32/uint32 [count]; 0 = verified, 5 = hash mismatch."""
+                     status: torch.Tensor, scratch: torch.Tensor, in_offset: int = 0) -> None:
+    """status: int32/uint32 [count]; 0 = verified, 5 = hash mismatch.  Each
+    stream `in_offset` bytes into its row of enc (8-B multiple)."""
     count = enc.shape[0]
-    check(_lib.lib().chip_bao_decode_batch_dev(_p(enc), enc.shape[1], n, count, _p(hashes), _p(out),
-                                               out.shape[1], _p(status), _p(scratch), _stream()))
+    check(_lib.lib().chip_bao_decode_batch_dev(ctypes.c_void_p(enc.data_ptr() + in_offset), enc.shape[1], n, count,
+                                               _p(hashes), _p(out), out.shape[1], _p(status), _p(scratch),
+                                               _stream()))
 
 
 def scrub_scratch(length: int, count: int, device=None) -> torch.Tensor:

@@ -264,3 +264,15 @@ def test_batch_bao_stream_offset(gpu, n):
         assert hashes[o].cpu().numpy().tobytes() == oh, o
         assert host[o, off:off + blen].tobytes() == oe, o
         assert (host[o, :off] == 0xA5).all() and (host[o, off + blen:] == 0xA5).all(), o
+    # the verify-decode reads them at that phase too
+    dec = torch.empty((count, (n + 255) // 256 * 256), dtype=torch.uint8, device="cuda")
+    status = torch.empty(count, dtype=torch.int32, device="cuda")
+    scratch = device.bao_scratch(n, count)
+    device.bao_decode_batch(out, n, hashes, dec, status, scratch, in_offset=off)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0 and torch.equal(dec[:, :n], inp[:, :n])
+    out[2, off + blen - 1] ^= 1  # the last chunk's last byte
+    device.bao_decode_batch(out, n, hashes, dec, status, scratch, in_offset=off)
+    torch.cuda.synchronize()
+    st = status.cpu().tolist()
+    assert st[2] != 0 and st[:2] + st[3:] == [0] * (count - 1)

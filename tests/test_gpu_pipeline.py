@@ -79,6 +79,28 @@ def test_levels_random(gpu, n):
         assert ca.decode(b"", h, enc, info.padding_len, level) == d
 
 
+@pytest.mark.parametrize("level", [4, 5, 6])
+def test_encode_host_batch_bao_only_large(gpu, level):
+    """Bao without Zfec from host memory, streams of more than 512 chunks: the
+    slot rows hold them 56 B in (K3 / the content mode at that phase) and the
+    copy back reads them from there; == encode() per object."""
+    import torch
+    from carbonado_amd import device
+    n, count = (600 << 10) + 13, 3
+    rng = np.random.default_rng(level + 40)
+    inp = torch.from_numpy(rng.integers(0, 256, (count, n), dtype=np.uint8)).pin_memory()
+    cap = device._lib.lib().chip_encode_max_len(n)
+    out = torch.full((count, cap), 0xA5, dtype=torch.uint8).pin_memory()
+    hashes = torch.zeros((count, 32), dtype=torch.uint8).pin_memory()
+    eph = np.stack([np.frombuffer(H.sha256(b"bo%d" % o), np.uint8) for o in range(count)])
+    nonce = np.stack([np.frombuffer(H.sha256(b"bn%d" % o)[:16], np.uint8) for o in range(count)])
+    olen, _ = device.encode_host_batch(level, inp, n, out, hashes, nslots=2, slice_bytes=2 * n, pubkey=PUB,
+                                       ephemeral_sk=eph, nonce=nonce, host_threads=3)
+    for o in range(count):
+        enc, h, _ = O.encode_full(inp[o].numpy().tobytes(), level, PUB, eph[o].tobytes(), nonce[o].tobytes())
+        assert out[o, :olen[o]].numpy().tobytes() == enc and hashes[o].numpy().tobytes() == h, o
+
+
 @pytest.mark.parametrize("level", [4, 8, 12, 15])
 @pytest.mark.parametrize("pinned", [False, True])
 def test_encode_host_batch(gpu, level, pinned):
