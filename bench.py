@@ -753,10 +753,11 @@ class Workload:
             zlen = m * C if lv & 8 else n
             self.blen = blen = L.chip_bao_encoded_len(zlen) if lv & 4 else zlen
             self.zlen = zlen
-            self.enc = batch_buf((count, (blen + 255) // 256 * 256), "enc")
+            self.soff = off = args.stream_offset if lv & 12 == 12 else 0
+            self.enc = batch_buf((count, (off + blen + 255) // 256 * 256), "enc")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             esc = device.encode_scratch(lv, n, count, dev)
-            _, info = device.encode_batch(lv, self.inp_full, n, self.enc, self.hashes, esc)
+            _, info = device.encode_batch(lv, self.inp_full, n, self.enc, self.hashes, esc, out_offset=off)
             torch.cuda.synchronize()
             del esc
             self.pad = info.padding_len
@@ -764,7 +765,7 @@ class Workload:
             self.status = torch.full((count,), -1, dtype=torch.int32, device=dev)
             self.scratch = device.decode_scratch(lv, blen, count, dev)
             self.step = lambda: device.decode_batch(lv, self.enc, blen, self.hashes, self.pad, self.out, self.status,
-                                                    self.scratch)
+                                                    self.scratch, in_offset=off)
             # read each encoding once (every byte verified) and write the decoded object once;
             # without Bao only the primaries' bytes are read
             self.alg_bytes = count * (blen + n) if lv & 4 else count * 2 * n
@@ -1362,7 +1363,7 @@ class Workload:
             # oracle's encode() (every object's status and bytes: verified_all_objects)
             enc, h, _ = O.encode(sample, self.args.level)
             ok = (int(self.status[0]) == 0 and torch.equal(self.out[0, :self.n], self.inp[0, :self.n]) and
-                  self.enc[0, :self.blen].cpu().numpy().tobytes() == enc)
+                  self.enc[0, self.soff:self.soff + self.blen].cpu().numpy().tobytes() == enc)
         elif self.args.mode == "file":
             from carbonado_amd import file as cfile
             path, info = self.results[0]

@@ -297,12 +297,17 @@ int chip_decode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_strid
                           uint64_t *out_len, uint32_t *d_status, void *d_scratch, void *stream) {
     if (has_host_stages(format) || format > 15 || !out_len) return CHIP_ERR_INVALID_ARG;
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
-    if ((!d_in && in_len) || (count && !d_status) || (in_stride % 16) || (out_stride % 16) || misaligned16(d_in) ||
-        misaligned16(d_out))
+    if ((!d_in && in_len) || (count && !d_status) || (out_stride % 16) || misaligned16(d_out))
         return CHIP_ERR_INVALID_ARG;
+    uint64_t blen = in_len;  // bytes entering zfec (decoding.rs:90-99)
+    {  // input rows: 16-B aligned, or 8-B aligned streams where K3 reads them (over 512 chunks)
+        uint64_t cl = 0;
+        const bool in8 = bao && bao_content_len(in_len, &cl) && !small_ok(cl, count);
+        const uint64_t a = in8 ? 8 : 16;
+        if ((in_stride % a) || (reinterpret_cast<uintptr_t>(d_in) % a)) return CHIP_ERR_INVALID_ARG;
+    }
     if (bao && !d_hash) return CHIP_ERR_HASH_DECODE;
     if (bao && !d_scratch) return CHIP_ERR_INVALID_ARG;
-    uint64_t blen = in_len;  // bytes entering zfec (decoding.rs:90-99)
     if (bao && !bao_content_len(in_len, &blen)) return CHIP_ERR_BAO_TRUNCATED;
     uint64_t olen = blen;
     if (zfec) {

@@ -139,15 +139,17 @@ def decode_scratch(fmt: int, in_len: int, count: int, device=None) -> torch.Tens
 
 
 def decode_batch(fmt: int, enc: torch.Tensor, in_len: int, hashes: torch.Tensor, padding: int, out: torch.Tensor,
-                 status: torch.Tensor, scratch: torch.Tensor) -> int:
+                 status: torch.Tensor, scratch: torch.Tensor, in_offset: int = 0) -> int:
     """decode() of device-resident encodings at a level without host stages:
-    enc uint8 [count, in_stride] (first in_len bytes of each row), hashes uint8
-    [count, 32], out uint8 [count, >= decoded length], status int32 [count]
-    (0, or the chip_status of that object).  Returns the decoded length."""
+    enc uint8 [count, in_stride] (in_len bytes of each row from in_offset:
+    STREAM_OFFSET where encode_batch put them), hashes uint8 [count, 32], out
+    uint8 [count, >= decoded length], status int32 [count] (0, or the
+    chip_status of that object).  Returns the decoded length."""
     assert enc.is_cuda and out.is_cuda and enc.is_contiguous() and out.is_contiguous()
-    assert enc.shape[0] == out.shape[0] == status.shape[0] and enc.shape[1] >= in_len
+    assert enc.shape[0] == out.shape[0] == status.shape[0] and enc.shape[1] >= in_offset + in_len
     olen = ctypes.c_uint64()
-    check(_lib.lib().chip_decode_batch_dev(fmt, _p(enc), enc.shape[1], in_len, enc.shape[0], _p(hashes), padding,
+    check(_lib.lib().chip_decode_batch_dev(fmt, ctypes.c_void_p(enc.data_ptr() + in_offset), enc.shape[1], in_len,
+                                           enc.shape[0], _p(hashes), padding,
                                            _p(out), out.shape[1], ctypes.byref(olen), _p(status), _p(scratch),
                                            _stream()))
     return olen.value

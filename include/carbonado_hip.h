@@ -399,7 +399,10 @@ CHIP_API int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t
  * stream is verified and only the primaries' bytes are written (the shards
  * are indexed by position, decoding.rs:95-99: decode = the 4 data shards,
  * padding dropped).  d_scratch: chip_decode_scratch_len(format, in_len,
- * count) bytes.  Pointers and strides multiples of 16; enqueued on `stream`. */
+ * count) bytes.  Pointers and strides multiples of 16, except d_in and
+ * in_stride with the Bao bit for streams of more than 512 chunks: multiples
+ * of 8, and 56 mod 64 (as chip_encode_batch_dev's fast layout writes them)
+ * is the fast layout for reading them too.  Enqueued on `stream`. */
 CHIP_API uint64_t chip_decode_scratch_len(uint8_t format, uint64_t in_len, uint64_t count);
 CHIP_API int chip_decode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_stride, uint64_t in_len,
                                    uint64_t count, const uint8_t *d_hash, uint32_t padding, uint8_t *d_out,

@@ -541,6 +541,13 @@ def test_encode_batch_dev_stream_offset(gpu, cols, pad, off):
         assert got[o, off:off + olen].tobytes() == enc, o
         assert (got[o, :off] == 0xA5).all() and (got[o, off + olen:] == 0xA5).all(), o
         assert gh[o].tobytes() == h
+    # decode() reads them at that phase (every node verified, the data shards out)
+    dec = torch.empty((count, stride), dtype=torch.uint8, device="cuda")
+    status = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    dscr = device.decode_scratch(12, olen, count)
+    dlen = device.decode_batch(12, out, olen, hashes, info.padding_len, dec, status, dscr, in_offset=off)
+    torch.cuda.synchronize()
+    assert dlen == n and int(status.abs().sum()) == 0 and torch.equal(dec[:, :n], inp[:, :n])
 
 
 def test_encode_batch_dev_stream_offset_refused_where_not_k13(gpu):
