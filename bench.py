@@ -808,11 +808,12 @@ class Workload:
             zlen = m * C
             self.zlen = zlen
             self.blen = blen = L.chip_bao_encoded_len(zlen)
-            row = (blen + 255) // 256 * 256
+            self.soff = soff = args.stream_offset
+            row = (soff + blen + 255) // 256 * 256
             self.enc = batch_buf((count, row), "enc")
             self.hashes = torch.empty((count, 32), dtype=torch.uint8, device=dev)
             esc = device.encode_scratch(12, n, count, dev)
-            _, info = device.encode_batch(12, self.inp, n, self.enc, self.hashes, esc)
+            _, info = device.encode_batch(12, self.inp, n, self.enc, self.hashes, esc, out_offset=soff)
             torch.cuda.synchronize()
             del esc
             self.pad = info.padding_len
@@ -821,17 +822,17 @@ class Workload:
             torch.cuda.empty_cache()
             every = max(1, args.scrub_every)
             self.damaged = list(range(every // 2 % count, count, every))
-            self.orig = {o: self.enc[o, :blen].clone() for o in self.damaged}
+            self.orig = {o: self.enc[o, soff:soff + blen].clone() for o in self.damaged}
             for o in self.damaged:  # one byte of a data shard's chunk
                 off = scrub_corrupt_offset(n, o)
-                self.enc[o, off] ^= 0x40
+                self.enc[o, soff + off] ^= 0x40
             self.out = batch_buf((count, row), "out")
             self.scratch = device.scrub_scratch(blen, count, dev)
             self.scrub_status = None
 
             def step():
                 self.scrub_status = device.scrub_batch(self.enc, blen, self.hashes, self.pad, C, self.out,
-                                                       self.scratch)
+                                                       self.scratch, offset=soff)
             self.step = step
             # VALU: every chunk and parent of every stream re-hashed (node check), plus the
             # damaged streams' re-encode (zfec + bao); HBM bytes: the streams read once
@@ -1218,7 +1219,8 @@ class Workload:
             st = self.scrub_status
             want = [0 if o in self.orig else 12 for o in range(self.count)]
             bad_status = [o for o in range(self.count) if st is None or st[o] != want[o]]
-            bad = [o for o in self.orig if not torch.equal(self.out[o, :self.blen], self.orig[o])]
+            so = getattr(self, "soff", 0)
+            bad = [o for o in self.orig if not torch.equal(self.out[o, so:so + self.blen], self.orig[o])]
             return {"ok": not bad and not bad_status, "objects": self.count, "repaired": len(self.orig),
                     "mismatched": bad[:16], "bad_status": bad_status[:16],
                     "seconds": round(time.perf_counter() - t0, 1),
@@ -1348,8 +1350,8 @@ class Workload:
             st = self.scrub_status
             want = [0 if o in self.orig else 12 for o in range(self.count)]
             ok = (st is not None and list(st) == want and
-                  all(torch.equal(self.out[o, :self.blen], self.orig[o]) for o in self.orig) and
-                  self.enc[0, :self.blen].cpu().numpy().tobytes() == O.encode(sample, 12)[0])
+                  all(torch.equal(self.out[o, self.soff:self.soff + self.blen], self.orig[o]) for o in self.orig) and
+                  self.enc[0, self.soff:self.soff + self.blen].cpu().numpy().tobytes() == O.encode(sample, 12)[0])
         elif self.args.mode == "hasher":
             ok = self.digest == O.blake3(self.inp.numpy().reshape(-1))
         elif self.args.mode == "pipeline":
@@ -1414,6 +1416,7 @@ class DryRun:
         self.C = n // args.k
         self.scatter_s = None
         self.alloc_info = {"in": {"classes_found": 0, "classes_used": 0, "alloc_s": 0.0, "rank": rank}}
+        self.scrub_comps = args.objects * (args.m * self.C // 64)  # scrub-batch's VALU count (placeholder)
 
     def box_ceiling(self, reps: int = 5) -> dict:
         """The box-ceiling record's keys with placeholder timings (no device)."""

@@ -139,7 +139,11 @@ int chip_scrub_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t len, 
     if (!d_in || !d_hash || !d_out || !status || !d_scratch) return CHIP_ERR_INVALID_ARG;
     uint64_t n = 0;
     if (!bao_content_len(len, &n) || in_stride < len || out_stride < len) return CHIP_ERR_INVALID_ARG;
-    if (misaligned16(d_in) || misaligned16(d_out) || in_stride % 16 || out_stride % 16) return CHIP_ERR_INVALID_ARG;
+    // streams at any 8-B phase (56 mod 64: every chunk and node on a 64-B
+    // boundary): the check kernels read them in 8-B units or aligned lines,
+    // the gather with 8-B aligned loads, and repaired rows land by a copy
+    if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out) | in_stride | out_stride) % 8)
+        return CHIP_ERR_INVALID_ARG;
     const uint64_t C = chunk_len;
     if (C == 0 || C % 1024 || n != (uint64_t)CHIP_FEC_M * C) return CHIP_ERR_ZFEC;
     int st = use_device();

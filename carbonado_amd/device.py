@@ -171,20 +171,22 @@ def scrub_scratch(length: int, count: int, device=None) -> torch.Tensor:
 
 
 def scrub_batch(enc: torch.Tensor, length: int, hashes: torch.Tensor, padding: int, chunk_len: int,
-                out: torch.Tensor, scratch: torch.Tensor) -> np.ndarray:
+                out: torch.Tensor, scratch: torch.Tensor, offset: int = 0) -> np.ndarray:
     """scrub() (decoding.rs:159-212) of device-resident Bao|Zfec streams
     enc uint8 [count, >= length] with one EncodeInfo; repaired streams go to
     the rows of `out`.  Returns the per-object statuses (int32 numpy):
     0 = repaired, CHIP_ERR_UNNECESSARY_SCRUB = intact, else scrub's error.
     A row of `out` is written only where the status is 0 (its repaired
-    stream's hash matched); every other row is left untouched."""
+    stream's hash matched); every other row is left untouched.  The streams
+    sit `offset` bytes into their rows of enc and out (8-B multiple)."""
     assert enc.is_cuda and out.is_cuda and enc.is_contiguous() and out.is_contiguous()
     count = enc.shape[0]
     assert out.shape[0] == count and hashes.shape[0] == count
     status = np.zeros(count, dtype=np.int32)
-    check(_lib.lib().chip_scrub_batch_dev(_p(enc), enc.shape[1], length, count, _p(hashes), padding, chunk_len,
-                                          _p(out), out.shape[1], status.ctypes.data_as(ctypes.c_void_p),
-                                          _p(scratch), _stream()))
+    check(_lib.lib().chip_scrub_batch_dev(ctypes.c_void_p(enc.data_ptr() + offset), enc.shape[1], length, count,
+                                          _p(hashes), padding, chunk_len, ctypes.c_void_p(out.data_ptr() + offset),
+                                          out.shape[1], status.ctypes.data_as(ctypes.c_void_p), _p(scratch),
+                                          _stream()))
     return status
 
 

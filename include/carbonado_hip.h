@@ -448,7 +448,8 @@ CHIP_API int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, u
  * is written only when status[o] == CHIP_OK (the repaired stream's hash
  * matched); every other row is left untouched.  d_scratch:
  * chip_scrub_scratch_len(len, count) bytes.  Pointers and strides multiples
- * of 16.  Synchronous: returns when every status is final. */
+ * of 8 (the streams at 56 mod 64 are the fast layout, as for
+ * chip_encode_batch_dev).  Synchronous: returns when every status is final. */
 CHIP_API uint64_t chip_scrub_scratch_len(uint64_t len, uint64_t count);
 CHIP_API int chip_scrub_batch_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t len, uint64_t count,
                                   const uint8_t *d_hash, uint32_t padding, uint32_t chunk_len, uint8_t *d_out,

@@ -92,12 +92,14 @@ def test_scrub_multi_shard_and_unrecoverable(gpu):
         ca.scrub(corrupt([0, 1, 2, 3, 4]), h, info)
 
 
-def test_scrub_batch_matches_single(gpu):
+@pytest.mark.parametrize("off", [0, 56])
+def test_scrub_batch_matches_single(gpu, off):
     """chip_scrub_batch_dev over device-resident streams gives, object by
     object, the status and the repaired stream of the single-object scrub():
     intact, one / two / four damaged shards (the last repaired from the parity
     shards alone), five damaged shards and a damaged root node (too few
-    authentic shards)."""
+    authentic shards).  off 56: the streams 56 B into their rows (every chunk
+    and node on a 64-B boundary), read and repaired there."""
     import torch
     import carbonado_amd as ca
     from carbonado_amd import device as D
@@ -121,14 +123,15 @@ def test_scrub_batch_matches_single(gpu):
                 b[enc.index(chunk) + 100 + sh] ^= 0x21
         bad.append(bytes(b))
     count = len(bad)
-    stride = (L + 15) // 16 * 16
+    stride = (off + L + 15) // 16 * 16
     inp = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
     hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
     for o in range(count):
-        inp[o, :L] = torch.frombuffer(bytearray(bad[o]), dtype=torch.uint8).cuda()
+        inp[o, off:off + L] = torch.frombuffer(bytearray(bad[o]), dtype=torch.uint8).cuda()
         hashes[o] = torch.frombuffer(bytearray(encs[o][1]), dtype=torch.uint8).cuda()
     out = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
-    status = D.scrub_batch(inp, L, hashes, info.padding_len, info.chunk_len, out, D.scrub_scratch(L, count))
+    status = D.scrub_batch(inp, L, hashes, info.padding_len, info.chunk_len, out, D.scrub_scratch(L, count),
+                           offset=off)
     expect = [12, 0, 0, 0, 7, 7]
     assert list(status) == expect
     for o in range(count):
@@ -139,4 +142,4 @@ def test_scrub_batch_matches_single(gpu):
         assert st == status[o], o
         if st == 0:
             assert single == encs[o][0]
-            assert bytes(out[o, :L].cpu().numpy()) == encs[o][0]
+            assert bytes(out[o, off:off + L].cpu().numpy()) == encs[o][0]

@@ -168,3 +168,26 @@ def test_bench_cfg5_eight_ranks_dry_run():
     assert len(box["GBps_by_rank"]) == 8 and all(g > 0 for g in box["GBps_by_rank"])
     assert "clocks" in box and res["roofline"]["box_ceiling_GBps"] == box["GBps"]
     assert 0 < res["roofline"]["frac_of_box_ceiling"]
+
+
+@pytest.mark.parametrize("mode", ["encode", "decode", "bao", "bao-decode", "pipeline", "pipeline-decode", "e2e",
+                                  "e2e-decode", "scrub", "scrub-batch", "hasher", "file"])
+def test_bench_every_mode_dry_run(mode):
+    """Every bench mode's control plane runs without a device and prints one
+    line with the contract's keys (scrub-batch's VALU count once lacked a dry
+    placeholder)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, str(root / "bench.py"), "--mode", mode, "--steps", "2", "--warmup", "1",
+                          "--dry-run"], capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "config", "roofline"):
+        assert key in res, key
