@@ -25,7 +25,7 @@ def avg_counter(path: Path, kern: str):
 
 def main():
     tag = sys.argv[1]
-    kern = sys.argv[2] if len(sys.argv) > 2 else "gf_apply_kernel"
+    kern = sys.argv[2] if len(sys.argv) > 2 else "zfec_apply_kernel"
     src = ROOT / "gpurun_out" / tag
     tag = tag.replace("/", "_")  # a session's sub-run (gpu_session.sh prof15s: TAG/p15s)
     dst = ROOT / "profiles"
