@@ -73,7 +73,11 @@ int main(int argc, char **argv) {
     const uint64_t blen0 = 8 + 8 * C + 64 * (N0 - 1), bstride = (blen0 + 255) / 256 * 256;
     uint8_t *in, *out, *cv;
     CK(hbm::Allocator::get().alloc(count * n, reinterpret_cast<void **>(&in)));
-    CK(hbm::Allocator::get().alloc(count * bstride, reinterpret_cast<void **>(&out)));
+    CK(hbm::Allocator::get().alloc(count * bstride + 256, reinterpret_cast<void **>(&out)));
+    // FT_SOFF=56: every stream 56 B into its row (the library's layout since
+    // round 5: each chunk and node on a 64-B boundary); 0: at the row start
+    const uint64_t soff = getenv("FT_SOFF") ? (uint64_t)atoll(getenv("FT_SOFF")) & 248 : 0;
+    printf("streams %llu B into their rows\n", (unsigned long long)soff);
     CK(hipMalloc(&cv, count * N0 * 32));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, count * n / 8, 0xCA4B0AD0ull);
     std::vector<uint8_t> enc = zfec_enc_matrix(4, 8);
@@ -100,7 +104,7 @@ int main(int argc, char **argv) {
     for (int k = 0; k < 2; ++k) {
         fused::FusedArgs &a = A[k];
         a = fused::FusedArgs{};
-        a.in = in; a.in_stride = n; a.valid = n; a.C = k ? 0 : C; a.out = out; a.out_stride = bstride;
+        a.in = in; a.in_stride = n; a.valid = n; a.C = k ? 0 : C; a.out = out + soff; a.out_stride = bstride;
         a.count = count; a.N = k ? N1 : N0; a.cols = k ? 0 : C / 1024; a.bpo = k ? N1 / 64 : (C / 1024 + 7) / 8;
         a.table = dtab; a.coff = dcoff[k]; a.cv = cv; a.queue = dq;
         a.cvs = a.N / 8;  // level-3 CVs per object (FULL)
