@@ -42,12 +42,17 @@ namespace chip {
 namespace host {
 
 // ---------------------------------------------------------------- CRC-32C
-// One crc32q chain.  A three-chain version (segments joined by a table shift)
-// ran 3x faster single-threaded (4.3 -> 13.2 GiB/s) but made the level-15
-// decode end to end 25-30 % slower on the GPU box (16 host threads beside the
-// DMA traffic; profiles/r1u_e2ed15_crc_ab.txt), so it was dropped.
-__attribute__((target("sse4.2"))) uint32_t crc32c(const uint8_t *p, size_t n) {
-    uint64_t c = 0xFFFFFFFFu;
+// crc32q has a 3-cycle latency and issues every cycle, so one chain runs at a
+// third of the instruction's rate.  Three chains over consecutive segments of
+// B bytes, joined by the "append B zero bytes" map of the CRC register (a
+// linear map over GF(2)^32, applied through four 256-entry tables):
+// crc(c, X || Y) = zeros_|Y|(crc(c, X)) ^ crc(0, Y).  (A round-1 three-chain
+// version measured slower end to end on a different decode pipeline, r1u;
+// CHIP_CRC_CHAINS=1 keeps the one-chain form for the A/B.)
+namespace {
+
+__attribute__((target("sse4.2"))) inline uint32_t crc_raw1(uint32_t c32, const uint8_t *p, size_t n) {
+    uint64_t c = c32;
     while (n >= 8) {
         uint64_t v;
         std::memcpy(&v, p, 8);
@@ -55,9 +60,71 @@ __attribute__((target("sse4.2"))) uint32_t crc32c(const uint8_t *p, size_t n) {
         p += 8;
         n -= 8;
     }
-    uint32_t c32 = (uint32_t)c;
+    c32 = (uint32_t)c;
     while (n--) c32 = _mm_crc32_u8(c32, *p++);
-    return c32 ^ 0xFFFFFFFFu;
+    return c32;
+}
+
+// the register after B zero bytes, as tables over its four bytes
+struct CrcShift {
+    uint32_t t[4][256];
+    explicit CrcShift(size_t B) {
+        std::vector<uint8_t> z(B, 0);
+        uint32_t col[32];
+        for (int i = 0; i < 32; ++i) col[i] = crc_raw1(1u << i, z.data(), B);
+        for (int k = 0; k < 4; ++k)
+            for (int b = 0; b < 256; ++b) {
+                uint32_t x = 0;
+                for (int j = 0; j < 8; ++j)
+                    if (b >> j & 1) x ^= col[8 * k + j];
+                t[k][b] = x;
+            }
+    }
+    uint32_t operator()(uint32_t c) const {
+        return t[0][c & 255] ^ t[1][(c >> 8) & 255] ^ t[2][(c >> 16) & 255] ^ t[3][c >> 24];
+    }
+};
+
+// three chains over [p, p + 3B) in rounds; returns the register after them
+template <size_t B>
+__attribute__((target("sse4.2"))) inline uint32_t crc_raw3(uint32_t c0, const uint8_t *&p, size_t &n,
+                                                           const CrcShift &sh) {
+    while (n >= 3 * B) {
+        uint64_t a = c0, b = 0, c = 0;
+        for (size_t i = 0; i < B; i += 8) {
+            uint64_t x, y, z;
+            std::memcpy(&x, p + i, 8);
+            std::memcpy(&y, p + B + i, 8);
+            std::memcpy(&z, p + 2 * B + i, 8);
+            a = _mm_crc32_u64(a, x);
+            b = _mm_crc32_u64(b, y);
+            c = _mm_crc32_u64(c, z);
+        }
+        c0 = sh(sh((uint32_t)a) ^ (uint32_t)b) ^ (uint32_t)c;
+        p += 3 * B;
+        n -= 3 * B;
+    }
+    return c0;
+}
+
+bool crc_chains3() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_CRC_CHAINS");
+        return !(v && v[0] == '1' && v[1] == 0);
+    }();
+    return on;
+}
+
+}  // namespace
+
+uint32_t crc32c(const uint8_t *p, size_t n) {
+    uint32_t c = 0xFFFFFFFFu;
+    if (crc_chains3()) {
+        static const CrcShift s4k(4096), s256(256);
+        c = crc_raw3<4096>(c, p, n, s4k);
+        c = crc_raw3<256>(c, p, n, s256);
+    }
+    return crc_raw1(c, p, n) ^ 0xFFFFFFFFu;
 }
 
 static uint32_t crc_masked(const uint8_t *p, size_t n) {

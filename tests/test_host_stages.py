@@ -409,3 +409,15 @@ def test_encode_host_batch_ecies_key_prep(ca):
     with pytest.raises(EciesError):
         device.encode_host_batch(1, inp, n, out, hashes, 2, slice_bytes=4 * n, pubkey=pub, ephemeral_sk=eph,
                                  nonce=nonce, host_threads=3)
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 255, 256, 767, 768, 769, 3 * 256 + 8, 4095, 12287, 12288, 12289,
+                               12288 + 767, 3 * 12288 + 5, 65535, 65536, 65537])
+def test_snap_frame_crc_lengths(ca, n):
+    """The frame CRC-32C of every chunk length class: three crc32q chains over
+    segments of 4096 and 256 bytes, joined by table shifts, then one chain for
+    the rest (host_stages.cpp crc32c) — frames byte-exact with the oracle's,
+    random and compressible data."""
+    for data in (np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes(), bytes(n)):
+        assert ca.encoding.snap(data) == H.snap_compress(data), n
+        assert ca.decoding.snap(ca.encoding.snap(data)) == data
