@@ -618,7 +618,14 @@ pub struct DeviceRows {
     pub count: u64,
     pub row: u64,
     pub stride: u64,
+    off: u64, // where row 0 starts in `mem` (alloc_streams: STREAM_OFFSET)
 }
+
+/// Where `DeviceRows::alloc_streams` puts each bao stream in its row: after
+/// the stream's 8-byte header every chunk and parent node then starts on a
+/// 64-B boundary, which runs level 12 4-11 % and decode 4-12 % faster than
+/// streams at the row start.
+pub const STREAM_OFFSET: u64 = 56;
 
 unsafe impl Send for DeviceRows {}
 
@@ -629,7 +636,20 @@ impl DeviceRows {
         // costs the kernels 1.21x the read traffic)
         let stride = (row + 255) / 256 * 256;
         let buf = DeviceBuffer::new((count * stride).max(16) as usize)?;
-        Ok(DeviceRows { mem: Mem::Owned(buf), count, row, stride })
+        Ok(DeviceRows { mem: Mem::Owned(buf), count, row, stride, off: 0 })
+    }
+
+    /// Rows for the bao streams of `content_len`-byte contents (the output of
+    /// `encode_batch` at Zfec|Bao with content 8 * chunk_len, or of
+    /// `bao_encode_batch`), each stream STREAM_OFFSET bytes into its row when
+    /// it has more than 512 chunks (the entry points take those at any 8-B
+    /// phase; smaller streams stay at the row start).
+    pub fn alloc_streams(count: u64, content_len: u64) -> Result<DeviceRows> {
+        let len = bao_encoded_len(content_len as usize) as u64;
+        let off = if content_len > 512 * 1024 { STREAM_OFFSET } else { 0 };
+        let stride = (off + len + 255) / 256 * 256;
+        let buf = DeviceBuffer::new((count * stride).max(16) as usize)?;
+        Ok(DeviceRows { mem: Mem::Owned(buf), count, row: len, stride, off })
     }
 
     /// Wrap caller-owned device memory (any 16-B aligned allocation works,
@@ -643,28 +663,34 @@ impl DeviceRows {
             return Err(ChipError::InvalidArgument);
         }
         let bytes = if count == 0 { 0 } else { ((count - 1) * stride + row) as usize };
-        Ok(DeviceRows { mem: Mem::Borrowed(base, bytes), count, row, stride })
+        Ok(DeviceRows { mem: Mem::Borrowed(base, bytes), count, row, stride, off: 0 })
     }
 
+    /// Bytes from row 0's start to the end of the memory.
     fn bytes(&self) -> usize {
-        match &self.mem {
+        let total = match &self.mem {
             Mem::Owned(b) => b.len(),
             Mem::Borrowed(_, n) => *n,
-        }
+        };
+        total.saturating_sub(self.off as usize)
     }
 
+    /// Row 0's first byte.
     pub fn as_ptr(&self) -> *const u8 {
-        match &self.mem {
+        let base = match &self.mem {
             Mem::Owned(b) => b.as_ptr(),
             Mem::Borrowed(p, _) => *p as *const u8,
-        }
+        };
+        base.wrapping_add(self.off as usize)
     }
 
     pub fn as_mut_ptr(&mut self) -> *mut u8 {
-        match &mut self.mem {
+        let off = self.off as usize;
+        let base = match &mut self.mem {
             Mem::Owned(b) => b.as_mut_ptr(),
             Mem::Borrowed(p, _) => *p,
-        }
+        };
+        base.wrapping_add(off)
     }
 
     /// The rows hold `count` objects of at least `row` bytes each.
