@@ -250,8 +250,9 @@ int chip_encode_batch_dev(uint8_t format, const uint8_t *d_in, uint64_t in_strid
     int st = encode_info_for(format, n, n, 0, 0, &inf, &zlen, &fl);
     if (st != CHIP_OK) return st;
     {  // output rows: 16-B aligned, or 8-B aligned where K13 writes the streams
-        const bool any8 = (format & CHIP_FORMAT_ZFEC) && (format & CHIP_FORMAT_BAO) && zlen &&
-                          zfec_bao_any8(inf.chunk_len, count);
+        const bool bao8 = (format & CHIP_FORMAT_BAO) && zlen;
+        const bool any8 = bao8 && ((format & CHIP_FORMAT_ZFEC) ? zfec_bao_any8(inf.chunk_len, count)
+                                                                : (zlen + 1023) / 1024 > KS_MAX_N);
         const uint64_t a = any8 ? 8 : 16;
         if ((out_stride % a) || (reinterpret_cast<uintptr_t>(d_out) % a)) return CHIP_ERR_INVALID_ARG;
     }

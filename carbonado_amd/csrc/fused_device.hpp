@@ -775,11 +775,16 @@ __global__ __launch_bounds__(256) void bao_levels123_kernel(const uint8_t *cv0, 
 // caps the waves per CU below what the registers allow).
 // rt > 0: only the groups K13's run mode left (group_in_wave false; cols,
 // bpo: the zfec shards' chunk-columns and K13's blocks per object).
+// L > 0: levels L+1..L+3 from the N level-L CVs per object in cv0 (the same
+// groups of 8 one level-L stride up: a level-(L+l) node whose leftmost chunk
+// is c sits 64 (L + l) bytes before chunk c, its left spine being complete),
+// for the top of many small trees (fused_kernels.hip upper_levels); N > 8.
 template <int QS>
 __global__ __launch_bounds__(64) void bao_levels123_lds_kernel(const uint8_t *cv0, uint64_t N, uint64_t count,
                                                                const uint64_t *coff, uint8_t *out,
                                                                uint64_t out_stride, uint8_t *cv3, uint64_t n3,
-                                                               uint64_t cols = 0, uint64_t bpo = 0, uint64_t rt = 0) {
+                                                               uint64_t cols = 0, uint64_t bpo = 0, uint64_t rt = 0,
+                                                               uint32_t L = 0) {
     __shared__ bao::u32x4 buf[64 * QS * 4];  // [lane][node][16-B unit] of the nodes staged
     __shared__ uint64_t naddr[64 * QS];      // [lane][node]: its slot (0: not a real node)
     const int lane = threadIdx.x;
@@ -816,7 +821,8 @@ __global__ __launch_bounds__(64) void bao_levels123_lds_kernel(const uint8_t *cv
                 b[1] = bao::u32x4{c[li][4], c[li][5], c[li][6], c[li][7]};
                 b[2] = bao::u32x4{c[ri][0], c[ri][1], c[ri][2], c[ri][3]};
                 b[3] = bao::u32x4{c[ri][4], c[ri][5], c[ri][6], c[ri][7]};
-                naddr[lane * ns + j] = real ? (uint64_t)(uintptr_t)(ob + coff[s0 + left] - 64 * l) : 0ull;
+                naddr[lane * ns + j] =
+                    real ? (uint64_t)(uintptr_t)(ob + coff[(s0 + left) << L] - 64 * (L + l)) : 0ull;
                 if (real) {
                     uint32_t p[8];
                     bao::b3_parent(c[li], c[ri], false, p);

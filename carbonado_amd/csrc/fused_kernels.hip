@@ -104,6 +104,32 @@ hipError_t launch_parts(const fused::FusedArgs &a, uint64_t cv_nodes, void (*ker
     return hipSuccess;
 }
 
+// The tree above the level-3 CVs (cv3 [count][n3]; `spare` holds count *
+// ((n3 + 1) / 2) CVs).  Batches of many small trees (>= 2048 objects of 65 to
+// 512 level-3 nodes, e.g. 16384 x 1 MiB) run levels 4-6 in the levels pass
+// first (one lane per 8 level-3 nodes), so the one-wave-per-object top walk
+// starts at level 7 over n3 / 8 nodes instead of walking nine levels from a
+// few hundred.  CHIP_UPPER_PASS=0: the walk from level 4 (A/B).
+hipError_t upper_levels(uint8_t *cv3, uint64_t n3, uint8_t *spare, uint64_t N, uint64_t count, const uint64_t *coff,
+                        uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, hipStream_t stream) {
+    static const bool pass_on = [] {
+        const char *v = std::getenv("CHIP_UPPER_PASS");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    if (pass_on && count >= 2048 && n3 > 64 && n3 <= (uint64_t)bao::K4T_MAX) {
+        const uint64_t n6 = (n3 + 7) / 8, work = count * n6;
+        hipLaunchKernelGGL(fused::bao_levels123_lds_kernel<4>, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, stream,
+                           cv3, n3, count, coff, d_out, out_stride, spare, n6, (uint64_t)0, (uint64_t)0, (uint64_t)0,
+                           (uint32_t)3);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return bao::run_parent_levels<0, false>(spare, n6, n6, 7, cv3, (n6 + 1) / 2, N, count, d_out, out_stride,
+                                                d_hash, nullptr, stream);
+    }
+    return bao::run_parent_levels<0, false>(cv3, n3, n3, 4, spare, (n3 + 1) / 2, N, count, d_out, out_stride, d_hash,
+                                            nullptr, stream);
+}
+
 }  // namespace
 
 hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count, uint64_t C,
@@ -150,8 +176,7 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     const uint64_t n0 = full ? a.N / 8 : a.N;  // nodes per object in `cv`
     uint8_t *next = a.cv + count * n0 * 32;
     if ((e = launch_parts(a, n0, full ? KF : KG, stream)) != hipSuccess) return e;
-    if (full) return bao::run_parent_levels<0, false>(a.cv, n0, n0, 4, next, (n0 + 1) / 2, a.N, count, d_out,
-                                                      out_stride, d_hash, nullptr, stream);
+    if (full) return upper_levels(a.cv, n0, next, a.N, count, coff, d_out, out_stride, d_hash, stream);
     // levels 1-3 of every group from the level-0 CVs, then from level 4
     const uint64_t n3 = (a.N + 7) / 8, work = count * n3;
     // a whole level's nodes staged per round (QS 4): node by node (QS 1, 4 KiB
@@ -160,8 +185,7 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     hipLaunchKernelGGL(fused::bao_levels123_lds_kernel<4>, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, stream,
                        a.cv, a.N, count, coff, d_out, out_stride, next, n3, a.cols, a.bpo, (uint64_t)0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return bao::run_parent_levels<0, false>(next, n3, n3, 4, a.cv, (n3 + 1) / 2, a.N, count, d_out, out_stride,
-                                            d_hash, nullptr, stream);
+    return upper_levels(next, n3, a.cv, a.N, count, coff, d_out, out_stride, d_hash, stream);
 }
 
 // Row copy for the device-only levels without a kernel stage (decode at
@@ -258,8 +282,7 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     uint8_t *next = a.cv + count * n3 * 32;
-    return bao::run_parent_levels<0, false>(a.cv, n3, n3, 4, next, (n3 + 1) / 2, a.N, count, d_out, out_stride,
-                                            d_hash, nullptr, stream);
+    return upper_levels(a.cv, n3, next, a.N, count, coff, d_out, out_stride, d_hash, stream);
 }
 
 }  // namespace chip

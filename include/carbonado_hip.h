@@ -374,9 +374,9 @@ CHIP_API int chip_bao_decode_batch_dev(const uint8_t *d_in, uint64_t in_stride, 
  * the shards cross HBM once; CHIP_FUSED=0 selects the two-kernel path).
  * d_scratch: chip_encode_scratch_len(format, n, count) bytes.  Pointers and
  * strides must be multiples of 16 (CHIP_ERR_INVALID_ARG otherwise), except
- * d_out and out_stride at Zfec|Bao for streams of more than 512 chunks
- * (objects over 128 KiB), which the fused kernel writes at any 8-B phase:
- * there they need only be multiples of 8.  The fast layout for those puts
+ * d_out and out_stride with the Bao bit for streams of more than 512 chunks
+ * (objects over 128 KiB at Zfec|Bao, 512 KiB at Bao), which the kernels
+ * write at any 8-B phase: there they need only be multiples of 8.  The fast layout for those puts
  * each stream at 56 mod 64 (d_out and out_stride), so that after its 8-byte
  * header every chunk and parent node starts on a 64-B boundary and no store
  * splits a 64-B segment (rows of a 256-B multiple pitch, the stream 56 bytes

@@ -566,3 +566,41 @@ def test_encode_batch_dev_stream_offset_refused_where_not_k13(gpu):
         device.encode_batch(12, inp[:, :small].contiguous(), small, out, hashes, scratch, out_offset=56)
     torch.cuda.synchronize()
     assert bool((out == 0xA5).all())
+
+
+@pytest.mark.parametrize("level,n", [(12, 320 << 10), (12, (300 << 10) + 5), (4, (600 << 10) + 77)])
+def test_encode_batch_dev_many_small_trees_upper_pass(gpu, level, n):
+    """2048 objects whose trees have 65-512 level-3 nodes: levels 4-6 run in
+    the levels pass (fused_kernels.hip upper_levels) and the top walk starts
+    at level 7 — K13 FULL (320 KiB), general (zfec padding) and the content
+    mode (level 4).  Every hash vs the oracle, whole streams of three objects,
+    and the batch decode of all (status 0, bytes back)."""
+    import torch
+    from carbonado_amd import device
+    count = 2048
+    stride = (n + 255) // 256 * 256
+    gen = torch.Generator(device="cuda").manual_seed(n % 4093)
+    inp = torch.randint(0, 256, (count, stride), dtype=torch.uint8, device="cuda", generator=gen)
+    h_in = inp.cpu().numpy()
+    enc0, _, _ = O.encode(h_in[0, :n].tobytes(), level)
+    off = device.STREAM_OFFSET
+    out = torch.empty((count, (off + len(enc0) + 255) // 256 * 256), dtype=torch.uint8, device="cuda")
+    hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+    olen, info = device.encode_batch(level, inp, n, out, hashes, device.encode_scratch(level, n, count),
+                                     out_offset=off)
+    torch.cuda.synchronize()
+    gh = hashes.cpu().numpy()
+    for o in range(count):
+        if o in (0, 1031, count - 1):
+            enc, h, _ = O.encode(h_in[o, :n].tobytes(), level)
+            assert out[o, off:off + olen].cpu().numpy().tobytes() == enc, o
+            assert gh[o].tobytes() == h, o
+    # every hash: the root of each stream's tree
+    for o in range(count):
+        assert gh[o].tobytes() == O.encode(h_in[o, :n].tobytes(), level)[1], o
+    dec = torch.empty((count, stride), dtype=torch.uint8, device="cuda")
+    status = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    dlen = device.decode_batch(level, out, olen, hashes, info.padding_len, dec, status,
+                               device.decode_scratch(level, olen, count), in_offset=off)
+    torch.cuda.synchronize()
+    assert dlen == n and int(status.abs().sum()) == 0 and torch.equal(dec[:, :n], inp[:, :n])
