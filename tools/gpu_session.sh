@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 e2edab seg1m prof1m k13fetch ecbench l123ab soffab soffe2e baoab baodecab pdecab scrubbab ftsoff crcab upperab prepab scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
+#          e2e12 e2ed15 e2edab seg1m prof1m k13fetch ecbench l123ab soffab soffe2e baoab baodecab pdecab scrubbab ftsoff crcab upperab prepab scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s profbao profbaodec profpdec splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -38,6 +38,9 @@ for s in "$@"; do
     prof) bash tools/gpu_prof.sh $TAG ;;
     prof12) bash tools/gpu_prof.sh $TAG/p12 --mode pipeline --level 12 ;;
     prof15s) bash tools/gpu_prof.sh $TAG/p15s --mode pipeline --level 12 --object-bytes 16779371 ;;
+    profbao) bash tools/gpu_prof.sh $TAG/pbao --mode bao ;;
+    profbaodec) bash tools/gpu_prof.sh $TAG/pbaodec --mode bao-decode ;;
+    profpdec) bash tools/gpu_prof.sh $TAG/ppdec --mode pipeline-decode --level 12 ;;
     encodetorch) run bench_encode_alloc_torch 600 python3 bench.py --alloc torch --no-cpu-baseline --live-pmc off ;;
     mixprobe) run mix_probe_bal 300 ./tools/mix_probe 1024 3 bal ;;
     ftune) run fused_tune 300 ./tools/fused_tune 256 5 ;;
