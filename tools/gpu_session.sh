@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 e2edab seg1m prof1m k13fetch ecbench l123ab soffab soffe2e baoab baodecab pdecab scrubbab ftsoff crcab upperab prepab scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s profbao profbaodec profpdec splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
+#          e2e12 e2ed15 e2edab seg1m prof1m k13fetch ecbench soffab soffe2e baoab baodecab pdecab scrubbab ftsoff crcab upperab prepab scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s profbao profbaodec profpdec splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -80,10 +80,6 @@ for s in "$@"; do
            run bench_pipe12_1mib 600 python3 bench.py --mode pipeline --level 12 --object-bytes 1048576 --objects 16384 --verify-all --no-cpu-baseline ;;
     prof1m) bash tools/gpu_prof.sh $TAG/p1m --mode pipeline --level 12 --object-bytes 1048811 --objects 16384 ;;
     k13fetch) run k13_fetch 200 ./tools/k13_fetch 256 5 ;;
-    l123ab) for i in 1 2; do run bench_pipe12_l15shape_qs1_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 16779371 --no-cpu-baseline
-                           CHIP_L123_QS=4 run bench_pipe12_l15shape_qs4_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 16779371 --no-cpu-baseline
-                           run bench_pipe12_1mib_l15shape_qs1_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048811 --objects 16384 --no-cpu-baseline
-                           CHIP_L123_QS=4 run bench_pipe12_1mib_l15shape_qs4_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048811 --objects 16384 --no-cpu-baseline; done ;;
     soffab) for i in 1 2; do for o in 0 56; do
               run bench_pipe12_soff${o}_$i 300 python3 bench.py --mode pipeline --level 12 --no-cpu-baseline --stream-offset $o
               run bench_pipe12_l15shape_soff${o}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 16779371 --no-cpu-baseline --stream-offset $o
