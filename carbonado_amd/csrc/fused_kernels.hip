@@ -36,14 +36,6 @@ constexpr bool K13_NTL = K13_NTL_DEF;
 // the stream of an object of shard length C is < 8.6 C bytes and its input
 // 4 C: 32-bit offsets for C < 256 MiB.  CHIP_K13_O32=0 (read per call, so a
 // test can flip it) takes the 64-bit-address kernels at any size.
-bool k13_prio() {
-    static const bool on = [] {
-        const char *v = std::getenv("CHIP_K13_PRIO");
-        return v && v[0] == '1';
-    }();
-    return on;
-}
-
 bool o32_ok(uint64_t C_or_n) {
     const char *e = std::getenv("CHIP_K13_O32");
     if (e && e[0] == '0' && e[1] == 0) return false;
@@ -81,13 +73,6 @@ __global__ __launch_bounds__(fused::FTPB) void bao_content_fused_kernel(fused::F
 }
 __global__ __launch_bounds__(fused::FTPB) void bao_content_fused_kernel_a64(fused::FusedArgs a) {
     fused::zfec_bao_fused_body<true, true, 1, 0, 1>(a);
-}
-// A/B (round 5, CHIP_K13_PRIO=1): the GF and store roles at raised wave priority
-__global__ __launch_bounds__(fused::FTPB) void zfec_bao_fused_kernel_full_p1(fused::FusedArgs a) {
-    fused::zfec_bao_fused_body<true, true, 1, 0, 0, true, 0, 0, K13_O32, K13_GFP, fused::FW, false, 1>(a);
-}
-__global__ __launch_bounds__(fused::FTPB) void bao_content_fused_kernel_p1(fused::FusedArgs a) {
-    fused::zfec_bao_fused_body<true, true, 1, 0, 1, true, 0, 0, K13_O32, 0, fused::FW, K13_NTL, 1>(a);
 }
 
 }  // namespace fused
@@ -177,16 +162,15 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     constexpr auto KG64 = zfec_bao_fused_kernel_general_a64;
     constexpr auto KF32 = zfec_bao_fused_kernel_full;
     constexpr auto KG32 = zfec_bao_fused_kernel_general;
-    constexpr auto KF32P = zfec_bao_fused_kernel_full_p1;
     static bool attr = [] {
         bool ok = true;
-        for (auto k : {KF64, KG64, KF32, KG32, KF32P})
+        for (auto k : {KF64, KG64, KF32, KG32})
             ok &= hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)LDS_BYTES) == hipSuccess;
         return ok;
     }();
     const bool o32 = o32_ok(C);
-    const auto KF = o32 ? (k13_prio() ? KF32P : KF32) : KF64, KG = o32 ? KG32 : KG64;
+    const auto KF = o32 ? KF32 : KF64, KG = o32 ? KG32 : KG64;
     (void)attr;
     (void)hipGetLastError();
     const uint64_t n0 = full ? a.N / 8 : a.N;  // nodes per object in `cv`
@@ -277,15 +261,13 @@ hipError_t bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t n, ui
     a.queue = q + QUEUE_K13;
     constexpr auto K64 = bao_content_fused_kernel_a64;
     constexpr auto K32 = bao_content_fused_kernel;
-    constexpr auto K32P = bao_content_fused_kernel_p1;
     static bool attr = [] {
-        bool ok = true;
-        for (auto k : {K64, K32, K32P})
-            ok &= hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)LDS_BYTES) == hipSuccess;
-        return ok;
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(K64), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)LDS_BYTES) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(K32), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)LDS_BYTES) == hipSuccess;
     }();
-    const auto K = o32_ok(n) ? (k13_prio() ? K32P : K32) : K64;
+    const auto K = o32_ok(n) ? K32 : K64;
     (void)attr;
     (void)hipGetLastError();
     const uint64_t n3 = a.cvs;

@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 e2edab seg1m prof1m k13fetch ecbench soffab soffe2e baoab baodecab pdecab scrubbab ftsoff crcab upperab prioab prepab scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s profbao profbaodec profpdec splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
+#          e2e12 e2ed15 e2edab seg1m prof1m k13fetch ecbench soffab soffe2e baoab baodecab pdecab scrubbab ftsoff crcab upperab prepab scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s profbao profbaodec profpdec splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -106,10 +106,6 @@ for s in "$@"; do
                CHIP_UPPER_PASS=$u run bench_pipe12_1mib_up${u}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048576 --objects 16384 --no-cpu-baseline
                CHIP_UPPER_PASS=$u run bench_pipe12_1mib_l15shape_up${u}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048811 --objects 16384 --no-cpu-baseline
              done; done ;;
-    prioab) for i in 1 2; do for p in 0 1; do
-              CHIP_K13_PRIO=$p run bench_bao_prio${p}_$i 300 python3 bench.py --mode bao --no-cpu-baseline
-              CHIP_K13_PRIO=$p run bench_pipe12_prio${p}_$i 300 python3 bench.py --mode pipeline --level 12 --no-cpu-baseline
-            done; done ;;
     ecbench) run ec_bench 120 bash -c 'echo T 20 | ./tools/secp_field_check' && run ecies_rate 120 ./tools/ecies_rate 16 2000 ;;
     prepab) for i in 1 2; do V=--no-verify; [ $i = 1 ] && V=
             CHIP_E2E_TRACE=1 run bench_e2e15_1mib_prep_$i 400 python3 bench.py --mode e2e --level 15 --object-bytes 1048576 --objects 16384 --steps 4 --warmup 1 --no-cpu-baseline $V
