@@ -276,3 +276,58 @@ def test_batch_bao_stream_offset(gpu, n):
     torch.cuda.synchronize()
     st = status.cpu().tolist()
     assert st[2] != 0 and st[:2] + st[3:] == [0] * (count - 1)
+
+
+def _bao_parents(N):
+    """(level, offset) of every parent node of an N-chunk bao stream, in
+    pre-order (left subtree: the largest power of two below n chunks)."""
+    out, pos = [], 8
+
+    def rec(n):
+        nonlocal pos
+        if n == 1:
+            pos += 1024
+            return
+        left = 1 << ((n - 1).bit_length() - 1)
+        out.append(((n - 1).bit_length(), pos))
+        pos += 64
+        rec(left)
+        rec(n - left)
+    rec(N)
+    return out
+
+
+@pytest.mark.parametrize("n", [1000 * 1024 + 7, (16 << 20) + 3])
+def test_batch_bao_decode_flags_each_parent_level(gpu, n):
+    """Verify-decode checks every parent level: one object per level 2 .. 7
+    has one byte of one of its level-l nodes flipped (the levels 2-4 run in
+    one pass, K4v; 5 and above in K4 / the top walk), each flagged on its
+    own object only; the intact ones decode."""
+    import torch
+    from carbonado_amd import device
+    N = (n + 1023) // 1024
+    parents = _bao_parents(N)
+    levels = [2, 3, 4, 5, 6, 7]
+    count = len(levels) + 2
+    gen = torch.Generator(device="cuda").manual_seed(n % 887)
+    inp = torch.randint(0, 256, (count, (n + 255) // 256 * 256), dtype=torch.uint8, device="cuda", generator=gen)
+    blen = O.lib().orc_bao_encoded_len(n)
+    off = 56
+    enc = torch.empty((count, (off + blen + 255) // 256 * 256), dtype=torch.uint8, device="cuda")
+    hashes = torch.empty((count, 32), dtype=torch.uint8, device="cuda")
+    scratch = device.bao_scratch(n, count)
+    device.bao_encode_batch(inp, n, enc, hashes, scratch, out_offset=off)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(n)
+    for o, lv in enumerate(levels, start=1):
+        cands = [p for (l, p) in parents if l == lv]
+        pos = cands[int(rng.integers(0, len(cands)))] + int(rng.integers(0, 64))
+        enc[o, off + pos] ^= 0x10
+    dec = torch.empty((count, n), dtype=torch.uint8, device="cuda")
+    status = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    device.bao_decode_batch(enc, n, hashes, dec, status, scratch, in_offset=off)
+    torch.cuda.synchronize()
+    st = status.cpu().tolist()
+    assert st[0] == 0 and st[-1] == 0, st
+    assert all(x != 0 for x in st[1:-1]), st
+    assert torch.equal(dec[0], inp[0, :n]) and torch.equal(dec[-1], inp[-1, :n])
