@@ -203,59 +203,6 @@ inline uint64_t bao_scratch_len_t(uint64_t n, uint64_t count) {
 // cnt_prev nodes of level `level - 1`; cv_next (stride_next >= ceil(cnt_prev/2))
 // is the ping-pong buffer.  Parents are written into (MODE 0) or checked
 // against (MODE 1) the streams, the root into / against d_hash.
-// K4v: verify-decode's parent levels L+1..L+3 in one pass (the check
-// counterpart of fused_device.hpp's levels pass): one lane per group of 8
-// level-L CVs, up to 7 parents one after another with bao's promotion rule,
-// each real node's stored 64 bytes compared with its computed children (a
-// level-(L+l) node whose leftmost chunk is c sits 64 (L + l) bytes before
-// chunk c: its left spine is complete), the level-(L+3) CV out for the
-// levels above.  Three K4 launches, each reading its CVs back, become one.
-// n_prev > 8, so none of these nodes is the root.
-static __global__ __launch_bounds__(256) void bao_verify_levels_kernel(const uint8_t *cv_prev, uint64_t n_prev,
-                                                                       uint64_t count, const uint64_t *coff,
-                                                                       const uint8_t *stream, uint64_t stream_stride,
-                                                                       uint8_t *cv_next, uint64_t n_next, uint32_t L,
-                                                                       uint32_t *status) {
-    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (gid >= count * n_next) return;
-    const uint64_t obj = gid / n_next, g = gid - obj * n_next, s0 = 8 * g;
-    const uint32_t cnt = n_prev - s0 < 8 ? (uint32_t)(n_prev - s0) : 8u;
-    uint32_t c[8][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        if ((uint32_t)i < cnt) {
-            load_cv(cv_prev + (obj * n_prev + s0 + i) * 32, c[i]);
-        } else {
-#pragma unroll
-            for (int w = 0; w < 8; ++w) c[i][w] = 0u;
-        }
-    }
-    const uint8_t *sb = stream + obj * stream_stride;
-    bool ok = true;
-#pragma unroll
-    for (int l = 1; l <= 3; ++l) {
-        const uint32_t span = 1u << l, half = span >> 1;
-#pragma unroll
-        for (int q = 0; q < (8 >> l); ++q) {
-            const uint32_t left = q * span;
-            const int li = q * 2, ri = q * 2 + 1;
-            if (left + half < cnt) {  // a real node: both children exist
-                const uint8_t *node = sb + coff[(s0 + left) << L] - 64 * (L + l);
-                ok &= node_io<1, false>(const_cast<uint8_t *>(node), c[li], c[ri]);
-                uint32_t p[8];
-                b3_parent(c[li], c[ri], false, p);
-#pragma unroll
-                for (int w = 0; w < 8; ++w) c[q][w] = p[w];
-            } else {  // promoted (or empty): the left child
-#pragma unroll
-                for (int w = 0; w < 8; ++w) c[q][w] = c[li][w];
-            }
-        }
-    }
-    if (!ok) flag_mismatch(status, obj);
-    store_cv(cv_next + (obj * n_next + g) * 32, c[0]);
-}
-
 template <int MODE, bool BAO_NTS>
 hipError_t run_parent_levels(uint8_t *cv_prev, uint64_t stride_prev, uint64_t cnt_prev, int level, uint8_t *cv_next,
                              uint64_t stride_next, uint64_t N, uint64_t count, uint8_t *stream_buf, uint64_t sstride,
@@ -340,15 +287,6 @@ hipError_t launch_chunk_kernel(ChunkArgs ca, hipStream_t stream, size_t pad_lds)
 }
 
 // Enqueue K3 then one K4 launch per remaining level.
-// CHIP_VERIFY_PASS=0: verify-decode's parent levels one K4 launch per level (A/B)
-inline bool verify_pass_on() {
-    static const bool on = [] {
-        const char *v = std::getenv("CHIP_VERIFY_PASS");
-        return !(v && v[0] == '0' && v[1] == 0);
-    }();
-    return on;
-}
-
 template <int MODE, int BAO_CPL, bool BAO_NTS, int SP = 0, int SU = 1, int SE = 0, int XG = 0, bool DQ = false>
 hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64_t count,
                    uint8_t *d_out, uint64_t out_stride, uint8_t *d_hash, uint32_t *d_status,
@@ -372,16 +310,6 @@ hipError_t run_bao_t(const uint8_t *d_in, uint64_t in_stride, uint64_t n, uint64
 
     uint8_t *stream_buf = (MODE == 0 || MODE == 3) ? d_out : const_cast<uint8_t *>(d_in);
     const uint64_t sstride = (MODE == 0 || MODE == 3) ? out_stride : in_stride;
-    if (MODE == 1 && N0 > 8 && verify_pass_on()) {  // levels LOG+1..LOG+3 in one pass (K4v)
-        const uint64_t *coff = nullptr;
-        if ((e = bao_chunk_table(N, &coff)) != hipSuccess) return e;
-        const uint64_t n3 = (N0 + 7) / 8, work = count * n3;
-        hipLaunchKernelGGL(bao_verify_levels_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, bufA,
-                           N0, count, coff, stream_buf, sstride, bufB, n3, (uint32_t)LOG, d_status);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        return run_parent_levels<1, BAO_NTS>(bufB, n3, n3, LOG + 4, bufA, (n3 + 1) / 2, N, count, stream_buf, sstride,
-                                             d_hash, d_status, stream);
-    }
     return run_parent_levels<MODE == 3 ? 0 : MODE, BAO_NTS>(bufA, strideA, N0, LOG + 1, bufB, strideB, N, count,
                                                            stream_buf, sstride, d_hash, d_status, stream);
 }

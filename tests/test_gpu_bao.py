@@ -300,9 +300,8 @@ def _bao_parents(N):
 @pytest.mark.parametrize("n", [1000 * 1024 + 7, (16 << 20) + 3])
 def test_batch_bao_decode_flags_each_parent_level(gpu, n):
     """Verify-decode checks every parent level: one object per level 2 .. 7
-    has one byte of one of its level-l nodes flipped (the levels 2-4 run in
-    one pass, K4v; 5 and above in K4 / the top walk), each flagged on its
-    own object only; the intact ones decode."""
+    has one byte of one of its level-l nodes flipped (K4 per level, then the
+    top walk), each flagged on its own object only; the intact ones decode."""
     import torch
     from carbonado_amd import device
     N = (n + 1023) // 1024

@@ -106,10 +106,6 @@ for s in "$@"; do
                CHIP_UPPER_PASS=$u run bench_pipe12_1mib_up${u}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048576 --objects 16384 --no-cpu-baseline
                CHIP_UPPER_PASS=$u run bench_pipe12_1mib_l15shape_up${u}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048811 --objects 16384 --no-cpu-baseline
              done; done ;;
-    verifyab) for i in 1 2; do for v in 1 0; do
-               CHIP_VERIFY_PASS=$v run bench_bao_decode_vp${v}_$i 300 python3 bench.py --mode bao-decode --no-cpu-baseline
-               CHIP_VERIFY_PASS=$v run bench_pdec12_vp${v}_$i 300 python3 bench.py --mode pipeline-decode --level 12 --no-cpu-baseline
-             done; done ;;
     ecbench) run ec_bench 120 bash -c 'echo T 20 | ./tools/secp_field_check' && run ecies_rate 120 ./tools/ecies_rate 16 2000 ;;
     prepab) for i in 1 2; do V=--no-verify; [ $i = 1 ] && V=
             CHIP_E2E_TRACE=1 run bench_e2e15_1mib_prep_$i 400 python3 bench.py --mode e2e --level 15 --object-bytes 1048576 --objects 16384 --steps 4 --warmup 1 --no-cpu-baseline $V
