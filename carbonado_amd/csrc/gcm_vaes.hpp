@@ -1,0 +1,46 @@
+// gcm_vaes.hpp — AES-256-GCM for the host ECIES stage (ecies 0.2: AES-256-GCM
+// with a 16-byte nonce; encoding.rs:31-36, decoding.rs:62-69) on CPUs with
+// VAES + VPCLMULQDQ + AVX-512: sixteen blocks per step, the counter blocks
+// through four 512-bit AES lanes and their GHASH as four 512-bit carry-less
+// products summed before one reduction.  The image's OpenSSL 3.0.2 has no
+// such path (its AVX2 form runs 5.5 GiB/s per GPU-box thread, 60 % of the
+// level-15 host stage, profiles/r10q_session); host_stages.cpp falls back to
+// it where these instructions are missing, or with CHIP_GCM=openssl.
+// Byte-for-byte the same output and tags as OpenSSL's EVP AES-256-GCM
+// (tests/test_host_stages.py compares them over random keys, nonces,
+// lengths and update splits).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+namespace chip {
+namespace host {
+
+// Streaming AES-256-GCM without additional data: init, any number of
+// updates of any length, then tag (encrypt) or check (decrypt).
+struct Gcm {
+    alignas(64) uint8_t rk[15][16];   // AES-256 round keys
+    alignas(64) uint8_t hp[16][16];   // H^16 .. H^1, byte-reversed (hp[16 - k] = H^k)
+    alignas(16) uint8_t y[16];        // GHASH accumulator, byte-reversed
+    uint8_t j0[16];                   // the pre-counter block (tag mask)
+    uint8_t prefix[12];               // counter block bytes 0..11
+    uint32_t ctr = 0;                 // next counter value (bytes 12..15, big-endian)
+    uint8_t ks[16];                   // keystream of the partial block
+    uint8_t pend[16];                 // its ciphertext so far (GHASH input)
+    uint32_t npend = 0;
+    uint64_t len = 0;                 // ciphertext bytes so far
+    bool enc = true;
+
+    // key 32 bytes, iv of any nonzero length (ecies: 16)
+    void init(const uint8_t *key, const uint8_t *iv, size_t ivlen, bool encrypt);
+    void update(const uint8_t *in, size_t n, uint8_t *out);
+    void tag(uint8_t out[16]);  // ends the message
+    void wipe();
+};
+
+// VAES, VPCLMULQDQ, AVX-512 F/BW/VL, AES-NI and PCLMULQDQ all present
+bool gcm_fast_available();
+
+}  // namespace host
+}  // namespace chip

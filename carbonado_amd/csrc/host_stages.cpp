@@ -20,8 +20,10 @@
 // (AES-NI/VAES GCM, EC arithmetic); both values the reference draws from its
 // RNG can be injected for bit-exact tests.
 #include "host_stages.hpp"
+#include "gcm_vaes.hpp"
 #include "secp256k1_host.hpp"
 
+#include <openssl/crypto.h>
 #include <openssl/ec.h>
 #include <openssl/evp.h>
 #include <openssl/obj_mac.h>
@@ -593,23 +595,83 @@ bool derive_key(const BIGNUM *secret, const EC_POINT *peer, const uint8_t eph_pu
     return ok;
 }
 
-struct CipherCtx {
-    EVP_CIPHER_CTX *c = EVP_CIPHER_CTX_new();
-    ~CipherCtx() { EVP_CIPHER_CTX_free(c); }
-};
-
-// AES-256-GCM over arbitrarily long buffers (EVP takes int lengths)
-bool gcm_update(EVP_CIPHER_CTX *c, bool enc, const uint8_t *in, uint64_t n, uint8_t *out) {
-    constexpr uint64_t STEP = 1ull << 30;
-    for (uint64_t o = 0; o < n; o += STEP) {
-        const int len = (int)((n - o) < STEP ? (n - o) : STEP);
-        int got = 0;
-        const int ok = enc ? EVP_EncryptUpdate(c, out + o, &got, in + o, len)
-                           : EVP_DecryptUpdate(c, out + o, &got, in + o, len);
-        if (ok != 1 || got != len) return false;
-    }
-    return true;
+// AES-256-GCM with a 16-byte nonce and no additional data: the VAES path
+// (gcm_vaes.cpp) where the CPU has it, else OpenSSL's EVP (CHIP_GCM=openssl
+// forces it; same bytes and tags either way).
+bool gcm_vaes_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_GCM");
+        return gcm_fast_available() && !(v && std::strcmp(v, "openssl") == 0);
+    }();
+    return on;
 }
+
+struct CipherCtx {
+    const bool fast = gcm_vaes_on();
+    bool enc = true;
+    EVP_CIPHER_CTX *c = fast ? nullptr : EVP_CIPHER_CTX_new();
+    Gcm g;
+    ~CipherCtx() {
+        if (c) EVP_CIPHER_CTX_free(c);
+        if (fast) g.wipe();
+    }
+    bool init(const uint8_t key[32], const uint8_t iv[16], bool encrypt) {
+        enc = encrypt;
+        if (fast) {
+            g.init(key, iv, 16, encrypt);
+            return true;
+        }
+        if (!c) return false;
+        if (encrypt)
+            return EVP_EncryptInit_ex(c, aes256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+                   EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
+                   EVP_EncryptInit_ex(c, nullptr, nullptr, key, iv) == 1;
+        return EVP_DecryptInit_ex(c, aes256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+               EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
+               EVP_DecryptInit_ex(c, nullptr, nullptr, key, iv) == 1;
+    }
+    // any length (EVP takes int lengths: fed in 1 GiB steps)
+    bool update(const uint8_t *in, uint64_t n, uint8_t *out) {
+        if (fast) {
+            g.update(in, n, out);
+            return true;
+        }
+        constexpr uint64_t STEP = 1ull << 30;
+        for (uint64_t o = 0; o < n; o += STEP) {
+            const int len = (int)((n - o) < STEP ? (n - o) : STEP);
+            int got = 0;
+            const int ok = enc ? EVP_EncryptUpdate(c, out + o, &got, in + o, len)
+                               : EVP_DecryptUpdate(c, out + o, &got, in + o, len);
+            if (ok != 1 || got != len) return false;
+        }
+        return true;
+    }
+    // encrypt: the tag of the message
+    bool tag(uint8_t out[16]) {
+        if (fast) {
+            g.tag(out);
+            return true;
+        }
+        int fin = 0;
+        uint8_t none[16];  // GCM's final step emits no bytes
+        return EVP_EncryptFinal_ex(c, none, &fin) == 1 && fin == 0 &&
+               EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, out) == 1;
+    }
+    // decrypt: true when the message's tag equals `want`
+    bool check(const uint8_t want[16]) {
+        if (fast) {
+            uint8_t t[16];
+            g.tag(t);
+            const bool ok = CRYPTO_memcmp(t, want, 16) == 0;
+            OPENSSL_cleanse(t, 16);
+            return ok;
+        }
+        uint8_t w[16], none[16];
+        std::memcpy(w, want, 16);
+        int fin = 0;
+        return EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_TAG, 16, w) == 1 && EVP_DecryptFinal_ex(c, none, &fin) == 1;
+    }
+};
 
 }  // namespace
 
@@ -670,37 +732,30 @@ int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out) 
 void ecies_key_wipe(EciesKey *k) { OPENSSL_cleanse(k, sizeof *k); }
 
 // Header and cipher context from prepared key material (ecies_prepare).
-static int ecies_begin_prepared(const EciesKey &k, const uint8_t *nonce, uint8_t *out, EVP_CIPHER_CTX *c) {
+static int ecies_begin_prepared(const EciesKey &k, const uint8_t *nonce, uint8_t *out, CipherCtx &cc) {
     std::memcpy(out, k.eph_pub, 65);
     uint8_t *iv = out + 65;
     if (nonce) std::memcpy(iv, nonce, 16);
     else if (RAND_bytes(iv, 16) != 1) return CHIP_ERR_ECIES;
-    const bool ok = c && EVP_EncryptInit_ex(c, aes256_gcm(), nullptr, nullptr, nullptr) == 1 &&
-                    EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
-                    EVP_EncryptInit_ex(c, nullptr, nullptr, k.key, iv) == 1;
-    return ok ? CHIP_OK : CHIP_ERR_ECIES;
+    return cc.init(k.key, iv, true) ? CHIP_OK : CHIP_ERR_ECIES;
 }
 
 // ECIES header (ephemeral public key, nonce) into out[0, 81) and the
 // AES-256-GCM context keyed for the ciphertext at out + 97; the tag goes to
 // out[81, 97) when the ciphertext is done.
 static int ecies_begin(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
-                       uint8_t *out, EVP_CIPHER_CTX *c) {
+                       uint8_t *out, CipherCtx &cc) {
     uint8_t peer[65];
     EciesKey k;
     int st = ecies_peer(pubkey, pubkey_len, peer);
     if (st == CHIP_OK) st = ecies_prepare(peer, eph_sk, &k);
-    if (st == CHIP_OK) st = ecies_begin_prepared(k, nonce, out, c);
+    if (st == CHIP_OK) st = ecies_begin_prepared(k, nonce, out, cc);
     ecies_key_wipe(&k);
     return st;
 }
 
-static int ecies_end(EVP_CIPHER_CTX *c, uint8_t *out, uint64_t ct_len, uint64_t *out_len) {
-    int fin = 0;
-    uint8_t none[16];  // GCM's final step emits no bytes
-    const bool ok = EVP_EncryptFinal_ex(c, none, &fin) == 1 && fin == 0 &&
-                    EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, out + 81) == 1;
-    if (!ok) return CHIP_ERR_ECIES;
+static int ecies_end(CipherCtx &cc, uint8_t *out, uint64_t ct_len, uint64_t *out_len) {
+    if (!cc.tag(out + 81)) return CHIP_ERR_ECIES;
     *out_len = ct_len + ECIES_OVERHEAD;
     return CHIP_OK;
 }
@@ -709,10 +764,10 @@ int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph
                   const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
     if (cap < n + ECIES_OVERHEAD) return CHIP_ERR_BUFFER_TOO_SMALL;
     CipherCtx cc;
-    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, out, cc.c);
+    int st = ecies_begin(pubkey, pubkey_len, eph_sk, nonce, out, cc);
     if (st != CHIP_OK) return st;
-    if (!gcm_update(cc.c, true, in, n, out + 97)) return CHIP_ERR_ECIES;
-    return ecies_end(cc.c, out, n, out_len);
+    if (!cc.update(in, n, out + 97)) return CHIP_ERR_ECIES;
+    return ecies_end(cc, out, n, out_len);
 }
 
 
@@ -732,16 +787,9 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
     if (!derive_key(k.p, eph.p, in, key)) return CHIP_ERR_ECIES;
     const uint8_t *iv = in + 65, *tag = in + 81, *ct = in + 97;
     CipherCtx cc;
-    uint8_t tagbuf[16];
-    std::memcpy(tagbuf, tag, 16);
-    bool ok = cc.c && EVP_DecryptInit_ex(cc.c, aes256_gcm(), nullptr, nullptr, nullptr) == 1 &&
-              EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
-              EVP_DecryptInit_ex(cc.c, nullptr, nullptr, key, iv) == 1 && gcm_update(cc.c, false, ct, m, out) &&
-              EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_TAG, 16, tagbuf) == 1;
+    bool ok = cc.init(key, iv, false) && cc.update(ct, m, out);
     OPENSSL_cleanse(key, 32);
-    int fin = 0;
-    uint8_t dummy[16];
-    ok = ok && EVP_DecryptFinal_ex(cc.c, m ? out + m : dummy, &fin) == 1;
+    ok = ok && cc.check(tag);
     if (!ok) {
         if (m) OPENSSL_cleanse(out, m);  // never hand back unauthenticated plaintext
         return CHIP_ERR_ECIES;
@@ -772,12 +820,9 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
     uint8_t key[32];
     if (!derive_key(k.p, eph.p, in, key)) return CHIP_ERR_ECIES;
     const uint8_t *iv = in + 65, *ct = in + 97;
-    uint8_t tagbuf[16];
-    std::memcpy(tagbuf, in + 81, 16);
+    const uint8_t *tag = in + 81;
     CipherCtx cc;
-    bool dec_ok = cc.c && EVP_DecryptInit_ex(cc.c, aes256_gcm(), nullptr, nullptr, nullptr) == 1 &&
-                  EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
-                  EVP_DecryptInit_ex(cc.c, nullptr, nullptr, key, iv) == 1;
+    bool dec_ok = cc.init(key, iv, false);
     OPENSSL_cleanse(key, 32);
     if (!dec_ok) return CHIP_ERR_ECIES;
 
@@ -797,13 +842,13 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
         }
         while (wend < s) {  // a skipped chunk: decrypted (for the tag) and dropped
             const uint64_t step = std::min<uint64_t>(W, s - wend);
-            dec_ok &= gcm_update(cc.c, false, ct + wend, step, win);
+            dec_ok &= cc.update(ct + wend, step, win);
             wend += step;
         }
         wbeg = s;
         wend = s + keep;
         const uint64_t step = std::min<uint64_t>(W - keep, m - wend);
-        dec_ok &= gcm_update(cc.c, false, ct + wend, step, win + keep);
+        dec_ok &= cc.update(ct + wend, step, win + keep);
         wend += step;
         return win;
     };
@@ -870,13 +915,10 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
     }
     while (wend < m) {  // the rest of the ciphertext, for the tag
         const uint64_t step = std::min<uint64_t>(W, m - wend);
-        dec_ok &= gcm_update(cc.c, false, ct + wend, step, win);
+        dec_ok &= cc.update(ct + wend, step, win);
         wend += step;
     }
-    int fin = 0;
-    uint8_t dummy[16];
-    dec_ok = dec_ok && EVP_CIPHER_CTX_ctrl(cc.c, EVP_CTRL_GCM_SET_TAG, 16, tagbuf) == 1 &&
-             EVP_DecryptFinal_ex(cc.c, dummy, &fin) == 1;
+    dec_ok = dec_ok && cc.check(tag);
     OPENSSL_cleanse(win, W);
     if (!dec_ok) {
         if (d && out) OPENSSL_cleanse(out, std::min(d, ecap));  // never hand back unauthenticated plaintext
@@ -1057,8 +1099,8 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
     uint8_t head[97];
     uint8_t *hdr = out ? out : head;
     CipherCtx cc;
-    int st = prepared ? ecies_begin_prepared(*prepared, nonce, hdr, cc.c)
-                      : ecies_begin(pubkey, pubkey_len, eph_sk, nonce, hdr, cc.c);
+    int st = prepared ? ecies_begin_prepared(*prepared, nonce, hdr, cc)
+                      : ecies_begin(pubkey, pubkey_len, eph_sk, nonce, hdr, cc);
     if (st != CHIP_OK) return st;
     uint8_t *ct = out ? out + 97 : nullptr;
     uint8_t *piece = window + SNAP_ECIES_WINDOW / 2;  // one block's ciphertext (the sink path)
@@ -1067,7 +1109,7 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
     uint64_t off = 0;  // ciphertext bytes so far
     if (snap && n) {
         uint8_t *d = sink ? piece : ct;
-        if (!gcm_update(cc.c, true, STREAM_ID, sizeof(STREAM_ID), d)) return CHIP_ERR_ECIES;
+        if (!cc.update(STREAM_ID, sizeof(STREAM_ID), d)) return CHIP_ERR_ECIES;
         if (sink) {
             if (ct) std::memcpy(ct, piece, sizeof(STREAM_ID));
             as.push(piece, sizeof(STREAM_ID));
@@ -1084,11 +1126,11 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
             uint8_t bh[8];
             const uint8_t *body;
             const size_t blen = snap_block(in + o, len, bh, window, &body);
-            if (!gcm_update(cc.c, true, bh, 8, dst) || !gcm_update(cc.c, true, body, blen, dst + 8))
+            if (!cc.update(bh, 8, dst) || !cc.update(body, blen, dst + 8))
                 return CHIP_ERR_ECIES;
             plen = 8 + blen;
         } else {
-            if (!gcm_update(cc.c, true, in + o, len, dst)) return CHIP_ERR_ECIES;
+            if (!cc.update(in + o, len, dst)) return CHIP_ERR_ECIES;
             plen = len;
         }
         if (sink) {
@@ -1100,7 +1142,7 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
         }
         off += plen;
     }
-    st = ecies_end(cc.c, hdr, off, out_len);
+    st = ecies_end(cc, hdr, off, out_len);
     if (st == CHIP_OK && sink) {
         const uint64_t placed = sink->complete ? as.finish(hdr) : as.done();
         if (filled) *filled = placed;

@@ -421,3 +421,65 @@ def test_snap_frame_crc_lengths(ca, n):
     for data in (np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes(), bytes(n)):
         assert ca.encoding.snap(data) == H.snap_compress(data), n
         assert ca.decoding.snap(ca.encoding.snap(data)) == data
+
+
+_GCM_LENS = [0, 1, 15, 16, 17, 31, 255, 256, 257, 511, 4095, 4096 + 8, 65536 * 2 + 13, (1 << 20) + 3]
+
+
+def _gcm_envelopes(ca, seed):
+    """ECIES envelopes over _GCM_LENS plus encode() at level 1 (one-pass
+    snap+ecies: 8-byte block headers between bodies, so the cipher's update
+    splits fall off block boundaries) and their decrypts."""
+    sk = H.sha256(b"gcm paths")
+    pub = H.public_key(sk)
+    eph, nonce = H.sha256(b"gcm eph"), H.sha256(b"gcm nonce")[:16]
+    rng = np.random.default_rng(seed)
+    out = []
+    for n in _GCM_LENS:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        e = ca.encoding.ecies(pub, d, ephemeral_sk=eph, nonce=nonce)
+        assert ca.decoding.ecies(e, sk) == d
+        out.append(e)
+    d = (b"carbonado " * 30_000) + rng.integers(0, 256, 200_001, dtype=np.uint8).tobytes()
+    enc, h, info = ca.encode(pub, d, 1, ephemeral_sk=eph, nonce=nonce)
+    assert ca.decode(sk, h, enc, info.padding_len, 1) == d
+    out.append(enc)
+    return out, d
+
+
+def test_gcm_paths_match_oracle(ca):
+    """AES-256-GCM inside ECIES runs on the VAES/VPCLMULQDQ path
+    (gcm_vaes.cpp) where the CPU has it and on OpenSSL's EVP otherwise or
+    with CHIP_GCM=openssl: both give the C oracle's envelopes byte for byte
+    (lengths around the 16-B block and 256-B step, a 1 MiB body, and the
+    one-pass encrypt's unaligned update splits), and a flipped tag or
+    ciphertext byte is refused on either."""
+    import hashlib
+    import os
+    import subprocess
+    import sys
+    from carbonado_amd.error import EciesError
+    envs, d = _gcm_envelopes(ca, 21)
+    sk = H.sha256(b"gcm paths")
+    pub = H.public_key(sk)
+    eph, nonce = H.sha256(b"gcm eph"), H.sha256(b"gcm nonce")[:16]
+    rng = np.random.default_rng(21)
+    for n, e in zip(_GCM_LENS, envs):
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert e == O.c_ecies_encrypt(pub, m, eph, nonce), n
+    oenc, _, _ = O.encode_full(d, 1, pub, eph, nonce)
+    assert envs[-1] == oenc
+    for pos in (81, 96, 97, len(envs[9]) - 1):  # tag first/last byte, ciphertext first/last
+        bad = bytearray(envs[9])
+        bad[pos] ^= 1
+        with pytest.raises(EciesError):
+            ca.decoding.ecies(bytes(bad), sk)
+    digest = hashlib.sha256(b"".join(envs)).hexdigest()
+    code = ("import hashlib, sys; sys.path.insert(0, 'tests'); import carbonado_amd as ca; "
+            "from test_host_stages import _gcm_envelopes; "
+            "print(hashlib.sha256(b''.join(_gcm_envelopes(ca, 21)[0])).hexdigest())")
+    root = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, CHIP_GCM="openssl")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == digest
