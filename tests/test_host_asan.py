@@ -21,15 +21,16 @@ def fuzzer(tmp_path_factory):
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
            "-fno-omit-frame-pointer", str(ROOT / "tests" / "host_fuzz.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "host_stages.cpp"),
+           str(ROOT / "carbonado_amd" / "csrc" / "gcm_vaes.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "file_container.cpp"), "-I" + str(ROOT / "include"),
            "-lcrypto", "-lpthread", "-o", str(exe)]
     subprocess.run(cmd, check=True, capture_output=True, timeout=300)
     return exe
 
 
-@pytest.mark.parametrize("seed", ["0xF022", "0xBEEF"])
-def test_host_code_under_asan_ubsan(fuzzer, seed):
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+@pytest.mark.parametrize("seed,gcm", [("0xF022", "vaes"), ("0xBEEF", "vaes"), ("0xF022", "openssl")])
+def test_host_code_under_asan_ubsan(fuzzer, seed, gcm):
+    env = dict(os.environ, CHIP_GCM=gcm, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
     r = subprocess.run([str(fuzzer), "6", seed], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
