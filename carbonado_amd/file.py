@@ -146,7 +146,7 @@ def _host_buffer(shape):
 
 def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None = None,
                  metadata: bytes | None = None, slice_objects: int = 64, host_threads: int = 16,
-                 nslots: int = 3, io_threads: int = 8, fsync: bool = False, stats: dict | None = None) -> list:
+                 nslots: int = 3, io_threads: int = 16, fsync: bool = False, stats: dict | None = None) -> list:
     """file::encode (file.rs:409-440) over many flat files of one size, end to
     end: disk -> pinned host memory -> HBM (zfec + bao on the device, host
     Snappy/Ecies on `host_threads` threads) -> pinned host memory -> header +
