@@ -273,7 +273,11 @@ GCM_TARGET void tag_impl(Gcm &g, uint8_t out[16]) {
 void Gcm::init(const uint8_t *key, const uint8_t *iv, size_t ivlen, bool encrypt) {
     init_impl(*this, key, iv, ivlen, encrypt);
 }
-void Gcm::update(const uint8_t *in, size_t n, uint8_t *out) { update_impl(*this, in, n, out); }
+bool Gcm::update(const uint8_t *in, size_t n, uint8_t *out) {
+    if (n > GCM_MAX_BYTES - len) return false;
+    update_impl(*this, in, n, out);
+    return true;
+}
 void Gcm::tag(uint8_t out[16]) { tag_impl(*this, out); }
 void Gcm::wipe() {
     volatile uint8_t *p = reinterpret_cast<volatile uint8_t *>(this);

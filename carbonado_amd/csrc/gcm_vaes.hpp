@@ -17,6 +17,8 @@
 namespace chip {
 namespace host {
 
+constexpr uint64_t GCM_MAX_BYTES = (1ull << 36) - 32;
+
 // Streaming AES-256-GCM without additional data: init, any number of
 // updates of any length, then tag (encrypt) or check (decrypt).
 struct Gcm {
@@ -34,7 +36,9 @@ struct Gcm {
 
     // key 32 bytes, iv of any nonzero length (ecies: 16)
     void init(const uint8_t *key, const uint8_t *iv, size_t ivlen, bool encrypt);
-    void update(const uint8_t *in, size_t n, uint8_t *out);
+    // false (nothing processed) once the message would pass GCM's limit of
+    // 2^36 - 32 bytes (the 32-bit block counter; OpenSSL refuses it too)
+    bool update(const uint8_t *in, size_t n, uint8_t *out);
     void tag(uint8_t out[16]);  // ends the message
     void wipe();
 };

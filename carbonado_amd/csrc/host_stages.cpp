@@ -632,10 +632,7 @@ struct CipherCtx {
     }
     // any length (EVP takes int lengths: fed in 1 GiB steps)
     bool update(const uint8_t *in, uint64_t n, uint8_t *out) {
-        if (fast) {
-            g.update(in, n, out);
-            return true;
-        }
+        if (fast) return g.update(in, n, out);
         constexpr uint64_t STEP = 1ull << 30;
         for (uint64_t o = 0; o < n; o += STEP) {
             const int len = (int)((n - o) < STEP ? (n - o) : STEP);

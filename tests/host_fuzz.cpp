@@ -6,6 +6,8 @@
 // that every call either fails with a status or returns exactly the original
 // bytes, and letting the sanitizers catch any out-of-bounds access.
 //   host_fuzz SECONDS SEED
+#include <openssl/evp.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -13,6 +15,7 @@
 #include <random>
 #include <vector>
 
+#include "../carbonado_amd/csrc/gcm_vaes.hpp"
 #include "../carbonado_amd/csrc/host_stages.hpp"
 #include "../include/carbonado_hip.h"
 
@@ -93,6 +96,45 @@ static int fails = 0;
         }                                          \
     } while (0)
 
+// gcm_vaes.cpp against OpenSSL's EVP AES-256-GCM (16-byte IV, no AAD): the
+// message cut into random pieces (partial blocks, 256-B steps), in place or
+// not, encrypt then decrypt; same ciphertext and tag
+static void gcm_check(const Bytes &d) {
+    using chip::host::Gcm;
+    uint8_t key[32], iv[16], t1[16], t2[16];
+    for (auto &x : key) x = (uint8_t)rng();
+    for (auto &x : iv) x = (uint8_t)rng();
+    const size_t n = d.size();
+    Bytes ref(n + 16), got(d), back(n);
+    EVP_CIPHER_CTX *c = EVP_CIPHER_CTX_new();
+    int l = 0, f = 0;
+    EXPECT(EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) == 1 &&
+               EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 16, nullptr) == 1 &&
+               EVP_EncryptInit_ex(c, nullptr, nullptr, key, iv) == 1 &&
+               EVP_EncryptUpdate(c, ref.data(), &l, d.data(), (int)n) == 1 &&
+               EVP_EncryptFinal_ex(c, ref.data() + n, &f) == 1 &&
+               EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, t1) == 1,
+           "evp gcm n=%zu", n);
+    EVP_CIPHER_CTX_free(c);
+    auto pieces = [&](Gcm &g, const uint8_t *in, uint8_t *out) {
+        for (size_t o = 0; o < n;) {
+            const size_t k = std::min(n - o, (size_t)(rnd(3) == 0 ? rnd(17) : rnd(3) == 0 ? 256 * rnd(4) : rnd(2000)));
+            EXPECT(g.update(in + o, k, out + o), "gcm update");
+            o += k;
+        }
+    };
+    Gcm g;
+    g.init(key, iv, 16, true);
+    pieces(g, got.data(), got.data());  // in place
+    g.tag(t2);
+    EXPECT(same(got.data(), ref.data(), n) && !std::memcmp(t1, t2, 16), "vaes gcm encrypt n=%zu", n);
+    g.init(key, iv, 16, false);
+    pieces(g, got.data(), back.data());
+    g.tag(t2);
+    EXPECT(same(back.data(), d.data(), n) && !std::memcmp(t1, t2, 16), "vaes gcm decrypt n=%zu", n);
+    g.wipe();
+}
+
 // decompress with an exact-size buffer: an error, or exactly `orig`
 static void snap_check(const Bytes &frame, const Bytes &orig, bool must_match) {
     uint64_t len = 0;
@@ -125,11 +167,20 @@ int main(int argc, char **argv) {
     for (auto &x : sk) x = (uint8_t)rng();
     sk[0] &= 0x7f;
     EXPECT(ecies_public_key(sk, pub) == 0, "public key");
+    if (chip::host::gcm_fast_available()) {  // GCM's length limit (2^36 - 32 bytes), as OpenSSL's
+        chip::host::Gcm g;
+        uint8_t k[32] = {1}, iv[16] = {2}, b[32] = {0};
+        g.init(k, iv, 16, true);
+        g.len = chip::host::GCM_MAX_BYTES - 32;
+        EXPECT(g.update(b, 32, b), "gcm at its limit");
+        EXPECT(!g.update(b, 1, b), "gcm past its limit");
+    }
     long iters = 0;
     while (elapsed() < seconds) {
         ++iters;
         const size_t n = rnd(4) == 0 ? rnd(300000) : rnd(5000);
         const Bytes d = rnd(2) ? compressible(n) : [&] { Bytes r(n); for (auto &x : r) x = (uint8_t)rng(); return r; }();
+        if (chip::host::gcm_fast_available()) gcm_check(d);
         // ring_copy (non-temporal stores into the staging ring): every length and both alignments
         {
             const size_t so = rnd(64), dof = rnd(64);
