@@ -20,6 +20,7 @@ def fuzzer(tmp_path_factory):
     exe = tmp_path_factory.mktemp("asan") / "host_fuzz"
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
            "-fno-omit-frame-pointer", str(ROOT / "tests" / "host_fuzz.cpp"),
+           str(ROOT / "carbonado_amd" / "csrc" / "host_snap.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "host_stages.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "gcm_vaes.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "file_container.cpp"), "-I" + str(ROOT / "include"),

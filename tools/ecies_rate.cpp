@@ -4,7 +4,7 @@
 // key.  Thread-microseconds per operation (wall / ops per thread; every
 // thread does N): flat in T when the threads do not contend.  Build (in tools/):
 //   g++ -O2 -std=c++17 -I../carbonado_amd/csrc -I../include ecies_rate.cpp \
-//       ../carbonado_amd/lib/obj/host_host_stages.cpp.o ../carbonado_amd/lib/obj/host_gcm_vaes.cpp.o -lcrypto -lpthread -o ecies_rate
+//       ../carbonado_amd/lib/obj/host_host_snap.cpp.o ../carbonado_amd/lib/obj/host_host_stages.cpp.o ../carbonado_amd/lib/obj/host_gcm_vaes.cpp.o -lcrypto -lpthread -o ecies_rate
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>

@@ -3,7 +3,7 @@
 // object, CRC-32C alone, snap_compress, ecies_encrypt, the one-pass
 // ecies_encrypt_stream without and with a chunk sink, and a plain memcpy;
 // one thread, then T threads each on its own objects.
-//   g++ -std=c++17 -O3 tools/host_encode_probe.cpp carbonado_amd/csrc/host_stages.cpp carbonado_amd/csrc/gcm_vaes.cpp \
+//   g++ -std=c++17 -O3 tools/host_encode_probe.cpp carbonado_amd/csrc/host_snap.cpp carbonado_amd/csrc/host_stages.cpp carbonado_amd/csrc/gcm_vaes.cpp \
 //       carbonado_amd/csrc/file_container.cpp -Iinclude -lcrypto -lpthread -o tools/host_encode_probe
 //   host_encode_probe [THREADS] [REPS]
 #include <chrono>
