@@ -936,7 +936,7 @@ class Workload:
             def step():
                 self.dec_len, self.dec_status = device.decode_host_batch(
                     lv, self.h_enc, self.enc_len, self.h_hash, self.pads, self.h_out, secret_key=self.sk,
-                    nslots=slots, host_threads=args.host_threads)
+                    nslots=slots, slice_bytes=args.slice_mib << 20, host_threads=args.host_threads)
             self.step = step
             step()
             self.alg_bytes = count * (max(self.enc_len) + n)  # PCIe bytes: H2D encoding + D2H content
