@@ -483,3 +483,56 @@ def test_gcm_paths_match_oracle(ca):
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip().splitlines()[-1] == digest
+
+
+def test_snappy_interop_with_cpp_snappy(ca):
+    """An independent pin for the snappy block format: Google's C++ snappy as
+    bundled in pyarrow (parity with the snap crate's own compressor stays
+    unpinned).  Every compressed chunk of our frames decompresses
+    with it to its block, and frames made of its compressed blocks (masked
+    CRC-32C from the C oracle) decode with ours; on very compressible blocks
+    the two compressors emit the same bytes."""
+    pa = pytest.importorskip("pyarrow")
+    codec = pa.Codec("snappy")
+    L = O.lib()
+
+    def masked(b):
+        c = L.orc_crc32c(b, len(b)) & 0xFFFFFFFF
+        return ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xA282EAD8) & 0xFFFFFFFF
+
+    def chunks(f):
+        s, out = 10, []
+        while s < len(f):
+            ty, cl = f[s], int.from_bytes(f[s + 1:s + 4], "little")
+            out.append((ty, f[s + 4:s + 4 + cl]))
+            s += 4 + cl
+        return out
+
+    rng = np.random.default_rng(31)
+    text = b"".join(rng.choice([b"carbonado ", b"archive ", b"zfec ", b"bao "], 40_000).tolist())
+    cases = [b"hello world " * 1000, bytes(100_000), text,
+             rng.integers(0, 4, 200_000, dtype=np.uint8).tobytes(),
+             rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes(),
+             (GOLDEN / "samples" / "code.tar").read_bytes(), (GOLDEN / "samples" / "content.png").read_bytes()]
+    identical = 0
+    for d in cases:
+        f = ca.encoding.snap(d)
+        o = 0
+        for ty, body in chunks(f):
+            blk = d[o:o + 65536]
+            o += len(blk)
+            assert int.from_bytes(body[:4], "little") == masked(blk)
+            if ty == 0x00:
+                assert codec.decompress(body[4:], decompressed_size=len(blk), asbytes=True) == blk
+                identical += body[4:] == codec.compress(blk, asbytes=True)
+            else:
+                assert ty == 0x01 and body[4:] == blk
+        assert o == len(d)
+        # the other way: C++ snappy's blocks in a frame, decoded by ours
+        frame = bytearray(f[:10])
+        for i in range(0, len(d), 65536):
+            blk = d[i:i + 65536]
+            z = codec.compress(blk, asbytes=True)
+            frame += bytes([0x00]) + (4 + len(z)).to_bytes(3, "little") + masked(blk).to_bytes(4, "little") + z
+        assert ca.decoding.snap(bytes(frame)) == d
+    assert identical >= 8
