@@ -175,7 +175,7 @@ uint64_t host_stage_max(uint8_t format, uint64_t n);
 int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const uint8_t *eph, const uint8_t *nonce,
                      const uint8_t *in, uint64_t n, uint8_t *dst, uint64_t cap, Scratch &tmp,
                      uint64_t *len, uint64_t *bc, uint64_t *be, const host::ChunkSink *sink = nullptr,
-                     uint64_t *filled = nullptr, const host::EciesKey *prepared = nullptr);
+                     uint64_t *filled = nullptr, const host::EciesKey *prepared = nullptr, bool par = false);
 
 // K1 reads and writes 16-B vectors and its tail load relies on 16-B aligned
 // shard addresses (zfec_device.hpp load16_masked).

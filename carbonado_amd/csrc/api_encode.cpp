@@ -31,7 +31,7 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
         t_stage.resize(host_stage_max(format, n) + 1);
         int st = host_stages_into(format, pubkey, pubkey_len, inject ? inject->ephemeral_sk : nullptr,
                                   inject ? inject->nonce : nullptr, in, n, t_stage.data(), t_stage.size(), t_tmp,
-                                  &cur_n, &bc, &be);
+                                  &cur_n, &bc, &be, nullptr, nullptr, nullptr, true);
         if (st != CHIP_OK) return st;
         cur = t_stage.data();
     }

@@ -320,16 +320,20 @@ uint64_t host_stage_max(uint8_t format, uint64_t n) {
 int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const uint8_t *eph, const uint8_t *nonce,
                      const uint8_t *in, uint64_t n, uint8_t *dst, uint64_t cap, Scratch &tmp,
                      uint64_t *len, uint64_t *bc, uint64_t *be, const host::ChunkSink *sink,
-                     uint64_t *filled, const host::EciesKey *prepared) {
+                     uint64_t *filled, const host::EciesKey *prepared, bool par) {
     const bool snap = format & CHIP_FORMAT_SNAPPY, ecies = format & CHIP_FORMAT_ECIES;
     const uint8_t *cur = in;
     uint64_t cur_n = n;
     *bc = *be = 0;
     if (filled) *filled = 0;
     if (ecies && pk && stream_encrypt_on()) {
-        // one pass: snappy block -> window -> AES-GCM -> dst (-> stream slots)
-        int st = host::ecies_encrypt_stream(pk, pklen, eph, nonce, in, n, snap, dst, cap, &cur_n,
-                                            tmp.get(host::SNAP_ECIES_WINDOW), sink, filled, prepared);
+        // one pass: snappy block -> window -> AES-GCM -> dst (-> stream slots); one
+        // object alone (par): its snappy blocks on a few threads
+        int st = par && snap && !sink && !prepared
+                     ? host::ecies_encrypt_par(pk, pklen, eph, nonce, in, n, dst, cap, &cur_n,
+                                               tmp.get(host::SNAP_ECIES_WINDOW))
+                     : host::ecies_encrypt_stream(pk, pklen, eph, nonce, in, n, snap, dst, cap, &cur_n,
+                                                  tmp.get(host::SNAP_ECIES_WINDOW), sink, filled, prepared);
         if (st != CHIP_OK) return st;
         *be = cur_n;
         if (snap) *bc = cur_n - host::ECIES_OVERHEAD;

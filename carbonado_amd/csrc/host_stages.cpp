@@ -23,9 +23,16 @@
 
 #include <immintrin.h>
 
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/carbonado_hip.h"
@@ -763,6 +770,140 @@ int snap_compress_stream(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t c
     }
     if (nt || (sink && as.nt)) fence_nt();
     return CHIP_OK;
+}
+
+// ------------------------------------------- one object's stage on a few threads
+namespace {
+
+// Persistent workers for one object's host stage (chip_encode).  start(f)
+// runs f(1) .. f(W) on the workers; wait() returns once they are done.  A
+// caller that finds the pool busy (another thread's object) or in a forked
+// child takes the one-thread path instead.
+class StagePool {
+  public:
+    static StagePool &get() {
+        static StagePool *p = new StagePool();  // never destroyed: workers park on the condvar at exit
+        return *p;
+    }
+    int workers() const { return workers_; }
+    bool try_acquire() { return workers_ > 0 && getpid() == pid_ && job_.try_lock(); }
+    void start(std::function<void(int)> f) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            f_ = std::move(f);
+            pending_ = workers_;
+            ++gen_;
+        }
+        cv_.notify_all();
+    }
+    void wait_and_release() {
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_.wait(lk, [&] { return pending_ == 0; });
+            f_ = nullptr;
+        }
+        job_.unlock();
+    }
+
+  private:
+    StagePool() {
+        int t = 8;  // the calling thread + 7 workers; CHIP_STAGE_THREADS=1: one thread
+        if (const char *e = std::getenv("CHIP_STAGE_THREADS")) t = std::max(1, std::min(32, std::atoi(e)));
+        workers_ = t - 1;
+        pid_ = getpid();
+        for (int i = 1; i <= workers_; ++i) std::thread([this, i] { run(i); }).detach();
+    }
+    void run(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::function<void(int)> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                f = f_;
+            }
+            f(i);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    int workers_ = 0;
+    pid_t pid_ = 0;
+    std::mutex job_, mu_;
+    std::condition_variable cv_, done_;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    std::function<void(int)> f_;
+};
+
+// spin briefly, then yield, until `ready()`
+template <class F>
+void spin_until(F &&ready) {
+    for (int i = 0; !ready(); ++i) {
+        if (i < 2048) _mm_pause();
+        else std::this_thread::yield();
+    }
+}
+
+}  // namespace
+
+int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                      const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                      uint8_t *window) {
+    StagePool &pool = StagePool::get();
+    if (n < STAGE_PAR_MIN || !out || cap < snap_max_len(n) + ECIES_OVERHEAD || !pool.try_acquire())
+        return ecies_encrypt_stream(pubkey, pubkey_len, eph_sk, nonce, in, n, true, out, cap, out_len, window, nullptr,
+                                    nullptr);
+    struct Block {
+        uint8_t hdr[8];
+        const uint8_t *body;
+        size_t blen;
+        std::atomic<bool> done{false};
+    };
+    const uint64_t nb = (n + MAX_BLOCK - 1) / MAX_BLOCK;
+    static thread_local std::vector<uint8_t> t_scr;  // one compressed block per slot
+    if (t_scr.size() < nb * MAX_COMPRESS_BLOCK) t_scr.resize(nb * MAX_COMPRESS_BLOCK);
+    uint8_t *scr = t_scr.data();
+    std::unique_ptr<Block[]> blk(new Block[nb]);
+    std::atomic<uint64_t> next{0};
+    std::atomic<int> key_st{1};  // 1: pending
+    EciesKey key;
+    pool.start([&](int w) {
+        if (w == 1) {  // the key agreement, while the other workers compress
+            uint8_t peer[65];
+            int st = ecies_peer(pubkey, pubkey_len, peer);
+            if (st == CHIP_OK) st = ecies_prepare(peer, eph_sk, &key);
+            key_st.store(st, std::memory_order_release);
+        }
+        for (uint64_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < nb;) {
+            const uint64_t o = j * MAX_BLOCK;
+            const size_t len = (size_t)std::min<uint64_t>(MAX_BLOCK, n - o);
+            blk[j].blen = snap_block(in + o, len, blk[j].hdr, scr + j * MAX_COMPRESS_BLOCK, &blk[j].body);
+            blk[j].done.store(true, std::memory_order_release);
+        }
+    });
+    // this thread: AES-GCM over the frame in block order as the blocks complete
+    int st;
+    spin_until([&] { return (st = key_st.load(std::memory_order_acquire)) != 1; });
+    CipherCtx cc;
+    if (st == CHIP_OK) st = ecies_begin_prepared(key, nonce, out, cc);
+    ecies_key_wipe(&key);
+    uint64_t off = 0;
+    uint8_t *ct = out + 97;
+    if (st == CHIP_OK) {
+        bool ok = cc.update(STREAM_ID, sizeof(STREAM_ID), ct);
+        off = sizeof(STREAM_ID);
+        for (uint64_t j = 0; j < nb; ++j) {
+            spin_until([&] { return blk[j].done.load(std::memory_order_acquire); });
+            ok = ok && cc.update(blk[j].hdr, 8, ct + off) && cc.update(blk[j].body, blk[j].blen, ct + off + 8);
+            off += 8 + blk[j].blen;
+        }
+        if (!ok) st = CHIP_ERR_ECIES;
+    }
+    pool.wait_and_release();  // the workers are done with blk, scr and key
+    if (st != CHIP_OK) return st;
+    return ecies_end(cc, out, off, out_len);
 }
 
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n) {

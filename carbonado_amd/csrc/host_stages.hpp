@@ -104,6 +104,16 @@ int ecies_encrypt_stream(const uint8_t *pubkey, uint64_t pubkey_len, const uint8
 // chunks [0, *filled) placed as they complete, `out` optional when complete.
 int snap_compress_stream(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
                          uint8_t *window, const ChunkSink *sink, uint64_t *filled);
+// ecies_encrypt_stream(.., snap = true, no sink) for one object of at least
+// STAGE_PAR_MIN bytes on a few threads (encode()'s single-object path): the
+// snappy blocks compressed on persistent workers (CHIP_STAGE_THREADS, default
+// 8 with the caller; 1 = this thread only), the key agreement on one of them
+// meanwhile, AES-GCM on the calling thread in block order.  Same bytes; a
+// smaller object, or a pool busy with another call, takes the one-thread path.
+constexpr uint64_t STAGE_PAR_MIN = 256 * 1024;
+int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
+                      const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                      uint8_t *window);
 // the first n bytes of a stream's content from its chunk slots row + coff[i]
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n);
 

@@ -536,3 +536,54 @@ def test_snappy_interop_with_cpp_snappy(ca):
             frame += bytes([0x00]) + (4 + len(z)).to_bytes(3, "little") + masked(blk).to_bytes(4, "little") + z
         assert ca.decoding.snap(bytes(frame)) == d
     assert identical >= 8
+
+
+def _par_inputs():
+    rng = np.random.default_rng(41)
+    words = [b"carbonado ", b"archive ", b"zfec ", b"bao ", b"segment "]
+    text = b"".join(rng.choice(words, 400_000).tolist())
+    return [rng.integers(0, 256, 256 * 1024 - 1, dtype=np.uint8).tobytes(),  # one-thread path
+            rng.integers(0, 256, 256 * 1024, dtype=np.uint8).tobytes(),      # parallel from here on
+            text[:256 * 1024 + 1],
+            rng.integers(0, 4, (1 << 20) + 5, dtype=np.uint8).tobytes(),
+            text[:3 * (1 << 20) + 17],
+            rng.integers(0, 256, 2 * (1 << 20) + 65536, dtype=np.uint8).tobytes()]
+
+
+def test_single_object_parallel_stage_matches_oracle(ca):
+    """encode()'s single-object Ecies|Snappy stage from 256 KiB up runs its
+    snappy blocks on a few threads and AES-GCM on the caller in block order
+    (host_stages.cpp ecies_encrypt_par): byte-identical to the C oracle's
+    snap + ecies with the injected ephemeral key and nonce, at and around the
+    threshold, compressible and not, and it round-trips with fresh
+    randomness."""
+    sk = H.sha256(b"par receiver")
+    pub = H.public_key(sk)
+    eph, nonce = H.sha256(b"par eph"), H.sha256(b"par nonce")[:16]
+    for d in _par_inputs():
+        enc, h, info = ca.encode(pub, d, 3, ephemeral_sk=eph, nonce=nonce)
+        oenc, oh, oinfo = O.c_encode_full(d, 3, pub, eph, nonce)
+        assert enc == oenc, len(d)
+        assert info.bytes_compressed == oinfo["bytes_compressed"]
+        assert ca.decode(sk, h, enc, info.padding_len, 3) == d
+        fresh, h2, info2 = ca.encode(pub, d, 3)
+        assert fresh[:97] != enc[:97] and ca.decode(sk, h2, fresh, info2.padding_len, 3) == d
+
+
+def test_single_object_stage_concurrent_callers(ca):
+    """Several threads calling encode() at once: one gets the stage's worker
+    pool, the others take the one-thread path; every output is the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+    sk = H.sha256(b"par receiver")
+    pub = H.public_key(sk)
+    ins = _par_inputs()[1:]
+    jobs = [(d, H.sha256(b"eph %d" % i), H.sha256(b"nonce %d" % i)[:16]) for i, d in enumerate(ins * 3)]
+
+    def run(job):
+        d, e, nn = job
+        return ca.encode(pub, d, 3, ephemeral_sk=e, nonce=nn)[0]
+
+    with ThreadPoolExecutor(6) as ex:
+        outs = list(ex.map(run, jobs))
+    for (d, e, nn), got in zip(jobs, outs):
+        assert got == O.c_encode_full(d, 3, pub, e, nn)[0]
