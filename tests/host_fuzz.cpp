@@ -178,7 +178,7 @@ int main(int argc, char **argv) {
     long iters = 0;
     while (elapsed() < seconds) {
         ++iters;
-        const size_t n = rnd(4) == 0 ? rnd(300000) : rnd(5000);
+        const size_t n = rnd(4) == 0 ? rnd(600000) : rnd(5000);
         const Bytes d = rnd(2) ? compressible(n) : [&] { Bytes r(n); for (auto &x : r) x = (uint8_t)rng(); return r; }();
         if (chip::host::gcm_fast_available()) gcm_check(d);
         // ring_copy (non-temporal stores into the staging ring): every length and both alignments
@@ -269,6 +269,13 @@ int main(int argc, char **argv) {
                     gather_chunks(back.data(), strm.data(), coff.data(), rl);
                     EXPECT(back == Bytes(ref.begin(), ref.begin() + rl), "gather_chunks");
                 }
+            }
+            if (snap) {  // one object's stage on the worker pool (from STAGE_PAR_MIN; below it, the one-pass path)
+                Bytes pout(cap);
+                uint64_t pl = 0;
+                EXPECT(ecies_encrypt_par(pub, 65, eph, iv, d.data(), n, pout.data(), cap, &pl, win.data()) == 0,
+                       "par enc");
+                EXPECT(pl == rl && same(pout.data(), ref.data(), rl), "par enc bytes n=%zu", n);
             }
         }
         // snap_compress_stream: the frame of snap_compress, chunks [0, filled) at their slots

@@ -36,3 +36,26 @@ def test_host_code_under_asan_ubsan(fuzzer, seed, gcm):
     r = subprocess.run([str(fuzzer), "6", seed], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "0 failures" in r.stdout
+
+
+@pytest.fixture(scope="module")
+def tsan_fuzzer(tmp_path_factory):
+    if not shutil.which("g++"):
+        pytest.skip("no g++")
+    exe = tmp_path_factory.mktemp("tsan") / "host_fuzz"
+    src = ROOT / "carbonado_amd" / "csrc"
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", str(ROOT / "tests" / "host_fuzz.cpp"),
+           str(src / "host_snap.cpp"), str(src / "host_stages.cpp"), str(src / "gcm_vaes.cpp"),
+           str(src / "file_container.cpp"), "-I" + str(ROOT / "include"), "-lcrypto", "-lpthread", "-o", str(exe)]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+    return exe
+
+
+def test_host_code_under_tsan(tsan_fuzzer):
+    """The same fuzz under ThreadSanitizer: the single-object stage's worker
+    pool (ecies_encrypt_par) hands blocks to the calling thread through
+    atomics; any race there stops the run."""
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([str(tsan_fuzzer), "6", "0x5EED"], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "0 failures" in r.stdout
