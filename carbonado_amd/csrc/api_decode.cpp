@@ -78,7 +78,7 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
             uint64_t got = 0;
             int st = CHIP_OK;
             if ((format & CHIP_FORMAT_ECIES) && (format & CHIP_FORMAT_SNAPPY)) {
-                st = host::ecies_decrypt_snap(secret_key, sk_len, src, n, dst, out_stride, &got);
+                st = host::ecies_decrypt_snap_par(secret_key, sk_len, src, n, dst, out_stride, &got);
             } else if (format & CHIP_FORMAT_ECIES) {
                 uint8_t *t = tmp.get(n + 1);
                 st = host::ecies_decrypt(secret_key, sk_len, src, n, (format & CHIP_FORMAT_SNAPPY) ? t : dst,
@@ -358,8 +358,8 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         *out_len = cur_n;
         return CHIP_OK;
     }
-    if (ecies && snap)  // decoding.rs:101-111 in one pass
-        return host::ecies_decrypt_snap(secret_key, sk_len, cur, cur_n, out, out_cap, out_len);
+    if (ecies && snap)  // decoding.rs:101-111 in one pass (a large object on the stage's worker pool)
+        return host::ecies_decrypt_snap_par(secret_key, sk_len, cur, cur_n, out, out_cap, out_len);
     if (ecies) {  // decoding.rs:101-105
         uint8_t *dst = out;
         uint64_t cap = out_cap;

@@ -268,7 +268,54 @@ GCM_TARGET void tag_impl(Gcm &g, uint8_t out[16]) {
     st(out, _mm_xor_si128(s, aes_block(ld(g.j0), g.rk)));
 }
 
+// H^k (k >= 1) in the byte-reversed representation, by square and multiply
+GCM_TARGET __m128i h_pow(const Gcm &g, uint64_t k) {
+    __m128i r = ld(g.hp[15]), b = r;  // H
+    bool have = false;
+    for (; k; k >>= 1) {
+        if (k & 1) {
+            r = have ? gfmul(r, b) : b;
+            have = true;
+        }
+        if (k > 1) b = gfmul(b, b);
+    }
+    return r;
+}
+
+GCM_TARGET void join_impl(Gcm &g, const uint8_t *yp, uint64_t blocks_after) {
+    __m128i y = ld(yp);
+    if (blocks_after) y = gfmul(y, h_pow(g, blocks_after));
+    st(g.y, _mm_xor_si128(ld(g.y), y));
+}
+
 }  // namespace
+
+void Gcm::init_part(const Gcm &msg, uint64_t offset) {
+    std::memcpy(rk, msg.rk, sizeof rk);
+    std::memcpy(hp, msg.hp, sizeof hp);
+    std::memcpy(j0, msg.j0, sizeof j0);
+    std::memcpy(prefix, msg.prefix, sizeof prefix);
+    const uint32_t c0 = ((uint32_t)j0[12] << 24 | (uint32_t)j0[13] << 16 | (uint32_t)j0[14] << 8 | j0[15]) + 1;
+    ctr = c0 + (uint32_t)(offset / 16);  // inc32: the counter wraps in its 32 bits
+    std::memset(y, 0, sizeof y);
+    npend = 0;
+    len = 0;
+    enc = msg.enc;
+}
+void Gcm::part_ghash(uint8_t out[16]) {
+    if (npend) {
+        std::memset(pend + npend, 0, 16 - npend);
+        ghash_block(*this, pend);
+        npend = 0;
+    }
+    std::memcpy(out, y, 16);
+}
+void Gcm::join_part(const uint8_t y_part[16], uint64_t blocks_after) { join_impl(*this, y_part, blocks_after); }
+void Gcm::tag_joined(uint64_t total, uint8_t out[16]) {
+    npend = 0;
+    len = total;
+    tag_impl(*this, out);
+}
 
 void Gcm::init(const uint8_t *key, const uint8_t *iv, size_t ivlen, bool encrypt) {
     init_impl(*this, key, iv, ivlen, encrypt);

@@ -41,6 +41,16 @@ struct Gcm {
     bool update(const uint8_t *in, size_t n, uint8_t *out);
     void tag(uint8_t out[16]);  // ends the message
     void wipe();
+
+    // One message split over threads: each part is a Gcm made by init_part
+    // from the message's Gcm (after init) at a byte offset that is a multiple
+    // of 16, fed its bytes with update(), then part_ghash(); the message's
+    // Gcm joins every part's GHASH with the number of 16-B blocks of the
+    // message after that part, and tag_joined() gives the message's tag.
+    void init_part(const Gcm &msg, uint64_t offset);
+    void part_ghash(uint8_t out[16]);
+    void join_part(const uint8_t y_part[16], uint64_t blocks_after);
+    void tag_joined(uint64_t total, uint8_t out[16]);
 };
 
 // VAES, VPCLMULQDQ, AVX-512 F/BW/VL, AES-NI and PCLMULQDQ all present

@@ -25,6 +25,7 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
@@ -796,14 +797,12 @@ class StagePool {
         }
         cv_.notify_all();
     }
-    void wait_and_release() {
-        {
-            std::unique_lock<std::mutex> lk(mu_);
-            done_.wait(lk, [&] { return pending_ == 0; });
-            f_ = nullptr;
-        }
-        job_.unlock();
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        f_ = nullptr;
     }
+    void release() { job_.unlock(); }
 
   private:
     StagePool() {
@@ -852,58 +851,247 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
                       const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
                       uint8_t *window) {
     StagePool &pool = StagePool::get();
-    if (n < STAGE_PAR_MIN || !out || cap < snap_max_len(n) + ECIES_OVERHEAD || !pool.try_acquire())
+    if (n < STAGE_PAR_MIN || !out || cap < snap_max_len(n) + ECIES_OVERHEAD || !gcm_vaes_on() ||
+        !pool.try_acquire())
         return ecies_encrypt_stream(pubkey, pubkey_len, eph_sk, nonce, in, n, true, out, cap, out_len, window, nullptr,
                                     nullptr);
     struct Block {
         uint8_t hdr[8];
         const uint8_t *body;
         size_t blen;
-        std::atomic<bool> done{false};
     };
+    const int T = std::min(pool.workers() + 1, 32);
     const uint64_t nb = (n + MAX_BLOCK - 1) / MAX_BLOCK;
     static thread_local std::vector<uint8_t> t_scr;  // one compressed block per slot
     if (t_scr.size() < nb * MAX_COMPRESS_BLOCK) t_scr.resize(nb * MAX_COMPRESS_BLOCK);
     uint8_t *scr = t_scr.data();
-    std::unique_ptr<Block[]> blk(new Block[nb]);
+    std::vector<Block> blk(nb);
+    std::vector<uint64_t> boff(nb);  // frame offset of each block's chunk header
     std::atomic<uint64_t> next{0};
-    std::atomic<int> key_st{1};  // 1: pending
+    int key_st = CHIP_ERR_ECIES;
     EciesKey key;
-    pool.start([&](int w) {
-        if (w == 1) {  // the key agreement, while the other workers compress
-            uint8_t peer[65];
-            int st = ecies_peer(pubkey, pubkey_len, peer);
-            if (st == CHIP_OK) st = ecies_prepare(peer, eph_sk, &key);
-            key_st.store(st, std::memory_order_release);
-        }
+    // 1: the snappy blocks on every thread, the key agreement on one worker first
+    auto compress = [&] {
         for (uint64_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < nb;) {
             const uint64_t o = j * MAX_BLOCK;
             const size_t len = (size_t)std::min<uint64_t>(MAX_BLOCK, n - o);
             blk[j].blen = snap_block(in + o, len, blk[j].hdr, scr + j * MAX_COMPRESS_BLOCK, &blk[j].body);
-            blk[j].done.store(true, std::memory_order_release);
         }
+    };
+    pool.start([&](int w) {
+        if (w == 1) {
+            uint8_t peer[65];
+            key_st = ecies_peer(pubkey, pubkey_len, peer);
+            if (key_st == CHIP_OK) key_st = ecies_prepare(peer, eph_sk, &key);
+        }
+        compress();
     });
-    // this thread: AES-GCM over the frame in block order as the blocks complete
-    int st;
-    spin_until([&] { return (st = key_st.load(std::memory_order_acquire)) != 1; });
-    CipherCtx cc;
-    if (st == CHIP_OK) st = ecies_begin_prepared(key, nonce, out, cc);
-    ecies_key_wipe(&key);
-    uint64_t off = 0;
-    uint8_t *ct = out + 97;
-    if (st == CHIP_OK) {
-        bool ok = cc.update(STREAM_ID, sizeof(STREAM_ID), ct);
-        off = sizeof(STREAM_ID);
-        for (uint64_t j = 0; j < nb; ++j) {
-            spin_until([&] { return blk[j].done.load(std::memory_order_acquire); });
-            ok = ok && cc.update(blk[j].hdr, 8, ct + off) && cc.update(blk[j].body, blk[j].blen, ct + off + 8);
-            off += 8 + blk[j].blen;
-        }
-        if (!ok) st = CHIP_ERR_ECIES;
+    compress();
+    pool.wait();  // blk, boff and key_st are this thread's from here (the pool's mutex orders them)
+    uint8_t *iv = out + 65;
+    if (key_st == CHIP_OK) {
+        std::memcpy(out, key.eph_pub, 65);
+        if (nonce) std::memcpy(iv, nonce, 16);
+        else if (RAND_bytes(iv, 16) != 1) key_st = CHIP_ERR_ECIES;
     }
-    pool.wait_and_release();  // the workers are done with blk, scr and key
-    if (st != CHIP_OK) return st;
-    return ecies_end(cc, out, off, out_len);
+    if (key_st != CHIP_OK) {
+        pool.release();
+        ecies_key_wipe(&key);
+        return key_st;
+    }
+    uint64_t mf = sizeof(STREAM_ID);
+    for (uint64_t j = 0; j < nb; ++j) {
+        boff[j] = mf;
+        mf += 8 + blk[j].blen;
+    }
+    Gcm msg;
+    msg.init(key.key, iv, 16, true);
+    ecies_key_wipe(&key);
+    // 2: AES-GCM over T 16-B aligned pieces of the frame, one per thread, each
+    // reading its bytes from the identifier, chunk headers and bodies in place
+    uint8_t *ct = out + 97;
+    const uint64_t S = ((mf + T - 1) / T + 15) / 16 * 16;
+    uint8_t ys[32][16];
+    auto part = [&](int w) {
+        const uint64_t a = (uint64_t)w * S;
+        if (a >= mf) return;
+        const uint64_t b = std::min(mf, a + S);
+        Gcm g;
+        g.init_part(msg, a);
+        uint64_t pos = a;
+        uint64_t j = std::upper_bound(boff.begin(), boff.end(), pos) - boff.begin();  // blocks starting <= pos
+        j = j ? j - 1 : 0;
+        while (pos < b) {
+            const uint8_t *src;
+            uint64_t end;
+            if (pos < sizeof(STREAM_ID)) {
+                src = STREAM_ID + pos;
+                end = sizeof(STREAM_ID);
+            } else {
+                while (j + 1 < nb && boff[j + 1] <= pos) ++j;
+                if (pos < boff[j] + 8) {
+                    src = blk[j].hdr + (pos - boff[j]);
+                    end = boff[j] + 8;
+                } else {
+                    src = blk[j].body + (pos - boff[j] - 8);
+                    end = boff[j] + 8 + blk[j].blen;
+                }
+            }
+            const uint64_t len = std::min(end, b) - pos;
+            g.update(src, len, ct + pos);
+            pos += len;
+        }
+        g.part_ghash(ys[w]);
+        g.wipe();
+    };
+    pool.start(part);
+    part(0);
+    pool.wait();
+    pool.release();
+    const uint64_t blocks = (mf + 15) / 16;
+    for (int w = 0; w < T && (uint64_t)w * S < mf; ++w)
+        msg.join_part(ys[w], blocks - (std::min(mf, (uint64_t)(w + 1) * S) + 15) / 16);
+    msg.tag_joined(mf, out + 81);
+    msg.wipe();
+    OPENSSL_cleanse(ys, sizeof ys);
+    *out_len = mf + ECIES_OVERHEAD;
+    return CHIP_OK;
+}
+
+int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n,
+                           uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    StagePool &pool = StagePool::get();
+    if (n < ECIES_OVERHEAD + STAGE_PAR_MIN || !gcm_vaes_on() || !pool.try_acquire())
+        return ecies_decrypt_snap(secret, secret_len, in, n, out, cap, out_len);
+    struct Hold {  // the pool until every return below
+        StagePool &p;
+        ~Hold() { p.release(); }
+    } hold{pool};
+    BnPtr k(parse_secret(secret, secret_len));
+    if (!k.p) return CHIP_ERR_ECIES;
+    const uint64_t m = n - ECIES_OVERHEAD;
+    PtPtr eph(parse_public(in, 65));
+    if (!eph.p) return CHIP_ERR_ECIES;
+    uint8_t key[32];
+    if (!derive_key(k.p, eph.p, in, key)) return CHIP_ERR_ECIES;
+    const uint8_t *iv = in + 65, *tag = in + 81, *ct = in + 97;
+    Gcm msg;
+    msg.init(key, iv, 16, false);
+    OPENSSL_cleanse(key, 32);
+    // 1: the ciphertext in T 16-B aligned pieces, one per thread, into a
+    // plaintext buffer; the GHASH parts joined and the tag checked first
+    static thread_local std::vector<uint8_t> t_plain;
+    if (t_plain.size() < m) t_plain.resize(m);
+    uint8_t *P = t_plain.data();
+    const int T = std::min(pool.workers() + 1, 32);
+    const uint64_t S = ((m + T - 1) / T + 15) / 16 * 16;
+    uint8_t ys[32][16];
+    auto part = [&](int w) {
+        const uint64_t a = (uint64_t)w * S;
+        if (a >= m) return;
+        const uint64_t b = std::min(m, a + S);
+        Gcm g;
+        g.init_part(msg, a);
+        g.update(ct + a, b - a, P + a);
+        g.part_ghash(ys[w]);
+        g.wipe();
+    };
+    pool.start(part);
+    part(0);
+    pool.wait();
+    auto wipe_plain = [&] {  // the plaintext buffer, on every thread
+        auto w = [&](int i) {
+            const uint64_t a = (uint64_t)i * S;
+            if (a < m) OPENSSL_cleanse(P + a, std::min(S, m - a));
+        };
+        pool.start(w);
+        w(0);
+        pool.wait();
+    };
+    const uint64_t blocks = (m + 15) / 16;
+    for (int w = 0; w < T && (uint64_t)w * S < m; ++w)
+        msg.join_part(ys[w], blocks - (std::min(m, (uint64_t)(w + 1) * S) + 15) / 16);
+    uint8_t t[16];
+    msg.tag_joined(m, t);
+    msg.wipe();
+    OPENSSL_cleanse(ys, sizeof ys);
+    const bool tag_ok = CRYPTO_memcmp(t, tag, 16) == 0;
+    if (!tag_ok) {
+        wipe_plain();
+        return CHIP_ERR_ECIES;
+    }
+    // 2: snap_walk's size pass over the chunk headers (framing errors first)
+    struct Chunk {
+        uint64_t src, dl, doff, ulen;
+        uint32_t want;
+        uint8_t ty;
+    };
+    std::vector<Chunk> ch;
+    ch.reserve(m / MAX_BLOCK + 2);
+    uint64_t s = 0, d = 0;
+    bool ident = false;
+    int frame = CHIP_OK;
+    while (s < m) {
+        if (m - s < 4) { frame = CHIP_ERR_SNAP; break; }
+        const uint8_t ty = P[s];
+        const uint64_t clen = (uint64_t)P[s + 1] | ((uint64_t)P[s + 2] << 8) | ((uint64_t)P[s + 3] << 16);
+        s += 4;
+        if (clen > m - s) { frame = CHIP_ERR_SNAP; break; }
+        const uint8_t *body = P + s;
+        if (!ident && ty != 0xFF) { frame = CHIP_ERR_SNAP; break; }
+        if (ty == 0xFF) {
+            if (clen != 6 || std::memcmp(body, STREAM_ID + 4, 6) != 0) { frame = CHIP_ERR_SNAP; break; }
+            ident = true;
+        } else if (ty == 0x00 || ty == 0x01) {
+            if (clen < 4) { frame = CHIP_ERR_SNAP; break; }
+            Chunk c{s + 4, clen - 4, d, clen - 4, 0, ty};
+            std::memcpy(&c.want, body, 4);
+            if (ty == 0x01) {
+                if (c.dl > MAX_BLOCK) { frame = CHIP_ERR_SNAP; break; }
+            } else {
+                size_t used;
+                if (!get_varint(body + 4, c.dl, &c.ulen, &used) || c.ulen > MAX_BLOCK) { frame = CHIP_ERR_SNAP; break; }
+            }
+            ch.push_back(c);
+            d += c.ulen;
+        } else if (ty >= 0x02 && ty <= 0x7F) {
+            frame = CHIP_ERR_SNAP;  // reserved unskippable
+            break;
+        }  // 0x80..0xFE: padding / reserved skippable
+        s += clen;
+    }
+    if (frame != CHIP_OK || d > cap || (d && !out)) {
+        wipe_plain();
+        if (frame != CHIP_OK) return frame;
+        *out_len = d;
+        return CHIP_ERR_BUFFER_TOO_SMALL;
+    }
+    // 3: the chunks (CRC, raw copy or block decode) on every thread
+    std::atomic<uint64_t> next{0};
+    std::atomic<bool> bad{false};
+    auto content = [&](int) {
+        for (uint64_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < ch.size();) {
+            const Chunk &c = ch[j];
+            const uint8_t *data = P + c.src;
+            bool ok;
+            if (c.ty == 0x01) {
+                ok = crc_masked(data, c.dl) == c.want;
+                if (ok) std::memcpy(out + c.doff, data, c.dl);
+            } else {
+                size_t got;
+                ok = decompress_raw(data, c.dl, out + c.doff, c.ulen, &got) && got == c.ulen &&
+                     crc_masked(out + c.doff, c.ulen) == c.want;
+            }
+            if (!ok) bad.store(true, std::memory_order_relaxed);
+        }
+    };
+    pool.start(content);
+    content(0);
+    pool.wait();
+    wipe_plain();
+    if (bad.load()) return CHIP_ERR_SNAP;
+    *out_len = d;
+    return CHIP_OK;
 }
 
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n) {

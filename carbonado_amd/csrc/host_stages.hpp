@@ -106,14 +106,24 @@ int snap_compress_stream(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t c
                          uint8_t *window, const ChunkSink *sink, uint64_t *filled);
 // ecies_encrypt_stream(.., snap = true, no sink) for one object of at least
 // STAGE_PAR_MIN bytes on a few threads (encode()'s single-object path): the
-// snappy blocks compressed on persistent workers (CHIP_STAGE_THREADS, default
-// 8 with the caller; 1 = this thread only), the key agreement on one of them
-// meanwhile, AES-GCM on the calling thread in block order.  Same bytes; a
-// smaller object, or a pool busy with another call, takes the one-thread path.
+// snappy blocks compressed on persistent workers and the caller
+// (CHIP_STAGE_THREADS, default 8 with the caller; 1 = this thread only), the
+// key agreement on one worker meanwhile; then AES-GCM over 16-B aligned
+// pieces of the frame, one per thread, the GHASH parts joined (gcm_vaes.hpp).
+// Same bytes; a smaller object, a CPU without the VAES path, or a pool busy
+// with another call takes the one-thread path.
 constexpr uint64_t STAGE_PAR_MIN = 256 * 1024;
 int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                       const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
                       uint8_t *window);
+// ecies_decrypt_snap for one object of at least STAGE_PAR_MIN bytes of
+// ciphertext on the same pool: AES-GCM over 16-B aligned pieces into a
+// plaintext buffer, the tag checked from the joined GHASH parts; then the
+// frame's chunk headers walked (snap_walk's size pass) and the chunks
+// decoded on every thread; the plaintext buffer wiped on every path.  Same
+// output and status order as ecies_decrypt_snap, which it falls back to.
+int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n,
+                           uint8_t *out, uint64_t cap, uint64_t *out_len);
 // the first n bytes of a stream's content from its chunk slots row + coff[i]
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n);
 

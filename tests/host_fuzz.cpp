@@ -219,6 +219,27 @@ int main(int argc, char **argv) {
                 else if (s2 == 0) EXPECT(l2 == n && same(o2.data(), d.data(), n), "mutated dec+unsnap");
             }
         }
+        // the pool's decrypt + unsnap against the one-pass one: a (maybe mutated) frame under a
+        // valid tag, or a mutated envelope, with an exact, short or no output buffer
+        if (frame.size() >= 200000) {
+            const Bytes f2 = rnd(2) ? frame : mutate(frame);
+            Bytes ct(f2.size() + ECIES_OVERHEAD);
+            uint64_t cl = 0;
+            EXPECT(ecies_encrypt(pub, 65, nullptr, nullptr, f2.data(), f2.size(), ct.data(), ct.size(), &cl) == 0,
+                   "enc f2");
+            ct.resize(cl);
+            const Bytes env = rnd(4) ? ct : mutate(ct);
+            const int mode = (int)rnd(3);  // 0 exact-ish, 1 short, 2 no buffer
+            const uint64_t cap = mode == 0 ? n + 70000 : mode == 1 ? n / 2 : 0;
+            Bytes o1(cap + 1), o2(cap + 1);
+            uint64_t l1 = 0, l2 = 0;
+            const int s1 = ecies_decrypt_snap(sk, 32, env.data(), env.size(), mode == 2 ? nullptr : o1.data(), cap, &l1);
+            const int s2 = ecies_decrypt_snap_par(sk, 32, env.data(), env.size(), mode == 2 ? nullptr : o2.data(), cap,
+                                                  &l2);
+            EXPECT(s1 == s2, "par dec status %d vs %d n=%zu mode=%d", s2, s1, n, mode);
+            if (s1 == s2 && (s1 == 0 || s1 == CHIP_ERR_BUFFER_TOO_SMALL)) EXPECT(l1 == l2, "par dec len");
+            if (s1 == 0 && s2 == 0) EXPECT(same(o1.data(), o2.data(), l1), "par dec bytes");
+        }
         // one-pass ECIES (|snappy) with and without a chunk sink: the same bytes as
         // snap_compress + ecies_encrypt; chunks [1, filled) at their slots, nothing else written
         {
