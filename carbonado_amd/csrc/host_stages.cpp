@@ -788,23 +788,33 @@ class StagePool {
     }
     int workers() const { return workers_; }
     bool try_acquire() { return workers_ > 0 && getpid() == pid_ && job_.try_lock(); }
+    // Workers spin for a short while after each job before they park, so the
+    // next job of the same call (an object takes two or three) starts without
+    // a futex wake-up.
     void start(std::function<void(int)> f) {
+        f_ = std::move(f);
+        pending_.store(workers_, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> lk(mu_);
-            f_ = std::move(f);
-            pending_ = workers_;
-            ++gen_;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
     }
     void wait() {
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return pending_ == 0; });
+        for (int i = 0; pending_.load(std::memory_order_acquire) != 0; ++i) {
+            if (i < SPIN) {
+                _mm_pause();
+            } else {
+                std::unique_lock<std::mutex> lk(mu_);
+                done_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
+            }
+        }
         f_ = nullptr;
     }
     void release() { job_.unlock(); }
 
   private:
+    static constexpr int SPIN = 1 << 15;  // ~0.1 ms of pause instructions
     StagePool() {
         int t = 8;  // the calling thread + 7 workers; CHIP_STAGE_THREADS=1: one thread
         if (const char *e = std::getenv("CHIP_STAGE_THREADS")) t = std::max(1, std::min(32, std::atoi(e)));
@@ -815,24 +825,28 @@ class StagePool {
     void run(int i) {
         uint64_t seen = 0;
         for (;;) {
-            std::function<void(int)> f;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
-                f = f_;
+            for (int k = 0; gen_.load(std::memory_order_acquire) == seen; ++k) {
+                if (k < SPIN) {
+                    _mm_pause();
+                } else {
+                    std::unique_lock<std::mutex> lk(mu_);
+                    cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+                }
             }
-            f(i);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_.notify_one();
+            seen = gen_.load(std::memory_order_acquire);
+            f_(i);  // f_ stays put until every worker has counted itself done
+            if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> lk(mu_);
+                done_.notify_one();
+            }
         }
     }
     int workers_ = 0;
     pid_t pid_ = 0;
     std::mutex job_, mu_;
     std::condition_variable cv_, done_;
-    uint64_t gen_ = 0;
-    int pending_ = 0;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
     std::function<void(int)> f_;
 };
 
