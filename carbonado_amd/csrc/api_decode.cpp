@@ -285,6 +285,12 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
     thread_local std::vector<uint8_t> t_dev, t_mid;
     const uint8_t *cur = in;
     uint64_t cur_n = n;
+    uint8_t pre_eph[65], pre_key[32];  // key derived while the device works (Ecies|Snappy)
+    bool have_pre = false;
+    struct Wipe {
+        uint8_t *k;
+        ~Wipe() { host::secure_wipe(k, 32); }
+    } wipe_pre{pre_key};
     if (zfec || bao) {
         uint64_t blen = n;
         if (bao) {
@@ -338,6 +344,16 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             if (st != CHIP_OK) return st;
             d_cur = static_cast<const uint8_t *>(c->out.p);
         }
+        // While the device verifies: the ECIES key from the envelope header as the
+        // input holds it (content bytes [0, 65): chunk 0 of the bao stream, or the
+        // first shard); decrypt uses it only if the verified header is the same
+        if (ecies && snap && olen >= host::ECIES_OVERHEAD) {
+            const uint64_t h0 = bao ? bao_chunk_offset(0, (blen + 1023) / 1024) : 0;
+            if (h0 + 65 <= n && (!bao || blen >= 65)) {
+                std::memcpy(pre_eph, in + h0, 65);
+                have_pre = host::ecies_derive_key(secret_key, sk_len, pre_eph, pre_key) == CHIP_OK;
+            }
+        }
         if (olen) CHIP_HIP(d2h(c->stage, dst, d_cur, olen, c->stream));
         CHIP_HIP(small_sync(c));
         if (verdict) {  // never hand back unverified content
@@ -359,7 +375,8 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         return CHIP_OK;
     }
     if (ecies && snap)  // decoding.rs:101-111 in one pass (a large object on the stage's worker pool)
-        return host::ecies_decrypt_snap_par(secret_key, sk_len, cur, cur_n, out, out_cap, out_len);
+        return host::ecies_decrypt_snap_par(secret_key, sk_len, cur, cur_n, out, out_cap, out_len,
+                                            have_pre ? pre_key : nullptr, pre_eph);
     if (ecies) {  // decoding.rs:101-105
         uint8_t *dst = out;
         uint64_t cap = out_cap;

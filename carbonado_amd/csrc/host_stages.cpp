@@ -972,8 +972,19 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
     return CHIP_OK;
 }
 
+void secure_wipe(void *p, size_t n) { OPENSSL_cleanse(p, n); }
+
+int ecies_derive_key(const uint8_t *secret, uint64_t secret_len, const uint8_t eph[65], uint8_t key[32]) {
+    BnPtr k(parse_secret(secret, secret_len));
+    if (!k.p) return CHIP_ERR_ECIES;
+    PtPtr pt(parse_public(eph, 65));
+    if (!pt.p) return CHIP_ERR_ECIES;
+    return derive_key(k.p, pt.p, eph, key) ? CHIP_OK : CHIP_ERR_ECIES;
+}
+
 int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n,
-                           uint8_t *out, uint64_t cap, uint64_t *out_len) {
+                           uint8_t *out, uint64_t cap, uint64_t *out_len, const uint8_t *pre_key,
+                           const uint8_t *pre_eph) {
     StagePool &pool = StagePool::get();
     if (n < ECIES_OVERHEAD + STAGE_PAR_MIN || !gcm_vaes_on() || !pool.try_acquire())
         return ecies_decrypt_snap(secret, secret_len, in, n, out, cap, out_len);
@@ -981,13 +992,14 @@ int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uin
         StagePool &p;
         ~Hold() { p.release(); }
     } hold{pool};
-    BnPtr k(parse_secret(secret, secret_len));
-    if (!k.p) return CHIP_ERR_ECIES;
     const uint64_t m = n - ECIES_OVERHEAD;
-    PtPtr eph(parse_public(in, 65));
-    if (!eph.p) return CHIP_ERR_ECIES;
     uint8_t key[32];
-    if (!derive_key(k.p, eph.p, in, key)) return CHIP_ERR_ECIES;
+    if (pre_key && pre_eph && std::memcmp(pre_eph, in, 65) == 0) {
+        std::memcpy(key, pre_key, 32);
+    } else {
+        const int st = ecies_derive_key(secret, secret_len, in, key);
+        if (st != CHIP_OK) return st;
+    }
     const uint8_t *iv = in + 65, *tag = in + 81, *ct = in + 97;
     Gcm msg;
     msg.init(key, iv, 16, false);

@@ -122,8 +122,14 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
 // frame's chunk headers walked (snap_walk's size pass) and the chunks
 // decoded on every thread; the plaintext buffer wiped on every path.  Same
 // output and status order as ecies_decrypt_snap, which it falls back to.
+// key / key_eph: a key already derived (ecies_derive_key) for the ephemeral
+// public key key_eph, used when the envelope's own equals it.
 int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n,
-                           uint8_t *out, uint64_t cap, uint64_t *out_len);
+                           uint8_t *out, uint64_t cap, uint64_t *out_len, const uint8_t *key = nullptr,
+                           const uint8_t *key_eph = nullptr);
+// The AES key of an envelope whose ephemeral public key (65 B) is eph.
+int ecies_derive_key(const uint8_t *secret, uint64_t secret_len, const uint8_t eph[65], uint8_t key[32]);
+void secure_wipe(void *p, size_t n);
 // the first n bytes of a stream's content from its chunk slots row + coff[i]
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n);
 

@@ -604,3 +604,28 @@ def test_encode_batch_dev_many_small_trees_upper_pass(gpu, level, n):
                                device.decode_scratch(level, olen, count), in_offset=off)
     torch.cuda.synchronize()
     assert dlen == n and int(status.abs().sum()) == 0 and torch.equal(dec[:, :n], inp[:, :n])
+
+
+@pytest.mark.parametrize("level", [7, 11, 15])
+def test_decode_key_derived_during_device_work(gpu, level):
+    """decode() at Ecies|Snappy with Bao and/or Zfec derives the ECIES key from
+    the envelope header as the input holds it while the device verifies, and
+    decrypts with it only if the verified header equals those bytes
+    (api_decode.cpp; host_stages.cpp ecies_decrypt_snap_par).  Round trip at
+    1 MiB, a wrong receiver key, and the header's ephemeral key altered inside
+    the input: bao refuses the stream, and without bao the tag does."""
+    import carbonado_amd as ca
+    from carbonado_amd.error import BaoDecodeError, EciesError
+    d = np.random.default_rng(level).integers(0, 256, (1 << 20) + 3, dtype=np.uint8).tobytes()
+    enc, h, info = ca.encode(PUB, d, level)
+    assert ca.decode(SK, h, enc, info.padding_len, level) == d
+    with pytest.raises(EciesError):
+        ca.decode(H.sha256(b"someone else"), h, enc, info.padding_len, level)
+    envelope = O.decode(h, enc, info.padding_len, level & 12)
+    pos = enc.find(envelope[:65])
+    assert pos >= 0
+    bad = bytearray(enc)
+    bad[pos + 40] ^= 0x10  # inside the ephemeral public key
+    with pytest.raises(BaoDecodeError if level & 4 else EciesError):
+        ca.decode(SK, h, bytes(bad), info.padding_len, level)
+    assert ca.decode(SK, h, enc, info.padding_len, level) == d  # the stale derived key is not reused
