@@ -285,7 +285,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
     thread_local std::vector<uint8_t> t_dev, t_mid;
     const uint8_t *cur = in;
     uint64_t cur_n = n;
-    uint8_t pre_eph[65], pre_key[32];  // key derived while the device works (Ecies|Snappy)
+    uint8_t pre_eph[65], pre_key[32];  // ECIES key derived while the device works
     bool have_pre = false;
     struct Wipe {
         uint8_t *k;
@@ -347,7 +347,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         // While the device verifies: the ECIES key from the envelope header as the
         // input holds it (content bytes [0, 65): chunk 0 of the bao stream, or the
         // first shard); decrypt uses it only if the verified header is the same
-        if (ecies && snap && olen >= host::ECIES_OVERHEAD) {
+        if (ecies && olen >= host::ECIES_OVERHEAD) {
             const uint64_t h0 = bao ? bao_chunk_offset(0, (blen + 1023) / 1024) : 0;
             if (h0 + 65 <= n && (!bao || blen >= 65)) {
                 std::memcpy(pre_eph, in + h0, 65);
@@ -386,7 +386,9 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             cap = t_mid.size();
         }
         uint64_t got = 0;
-        int st = host::ecies_decrypt(secret_key, sk_len, cur, cur_n, dst, cap, &got);
+        int st = snap ? host::ecies_decrypt(secret_key, sk_len, cur, cur_n, dst, cap, &got)
+                      : host::ecies_decrypt_par(secret_key, sk_len, cur, cur_n, dst, cap, &got,
+                                                have_pre ? pre_key : nullptr, pre_eph);
         if (st != CHIP_OK) {
             if (st == CHIP_ERR_BUFFER_TOO_SMALL) *out_len = got;
             return st;

@@ -329,9 +329,10 @@ int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const ui
     if (ecies && pk && stream_encrypt_on()) {
         // one pass: snappy block -> window -> AES-GCM -> dst (-> stream slots); one
         // object alone (par): its snappy blocks on a few threads
-        int st = par && snap && !sink && !prepared
-                     ? host::ecies_encrypt_par(pk, pklen, eph, nonce, in, n, dst, cap, &cur_n,
-                                               tmp.get(host::SNAP_ECIES_WINDOW))
+        int st = par && !sink && !prepared
+                     ? (snap ? host::ecies_encrypt_par(pk, pklen, eph, nonce, in, n, dst, cap, &cur_n,
+                                                       tmp.get(host::SNAP_ECIES_WINDOW))
+                             : host::ecies_encrypt_par_plain(pk, pklen, eph, nonce, in, n, dst, cap, &cur_n))
                      : host::ecies_encrypt_stream(pk, pklen, eph, nonce, in, n, snap, dst, cap, &cur_n,
                                                   tmp.get(host::SNAP_ECIES_WINDOW), sink, filled, prepared);
         if (st != CHIP_OK) return st;

@@ -859,6 +859,44 @@ void spin_until(F &&ready) {
     }
 }
 
+// AES-GCM of m contiguous bytes in T 16-B aligned pieces, one per pool thread
+// (the caller holds the pool); the pieces' GHASH joined into msg
+void gcm_parts(StagePool &pool, Gcm &msg, const uint8_t *in, uint8_t *out, uint64_t m) {
+    const int T = std::min(pool.workers() + 1, 32);
+    const uint64_t S = ((m + T - 1) / T + 15) / 16 * 16;
+    uint8_t ys[32][16];
+    auto part = [&](int w) {
+        const uint64_t a = (uint64_t)w * S;
+        if (a >= m) return;
+        const uint64_t b = std::min(m, a + S);
+        Gcm g;
+        g.init_part(msg, a);
+        g.update(in + a, b - a, out + a);
+        g.part_ghash(ys[w]);
+        g.wipe();
+    };
+    pool.start(part);
+    part(0);
+    pool.wait();
+    const uint64_t blocks = (m + 15) / 16;
+    for (int w = 0; w < T && (uint64_t)w * S < m; ++w)
+        msg.join_part(ys[w], blocks - (std::min(m, (uint64_t)(w + 1) * S) + 15) / 16);
+    OPENSSL_cleanse(ys, sizeof ys);
+}
+
+// n bytes at p wiped on every pool thread
+void wipe_parts(StagePool &pool, uint8_t *p, uint64_t n) {
+    const int T = std::min(pool.workers() + 1, 32);
+    const uint64_t S = (n + T - 1) / T;
+    auto w = [&](int i) {
+        const uint64_t a = (uint64_t)i * S;
+        if (a < n) OPENSSL_cleanse(p + a, std::min(S, n - a));
+    };
+    pool.start(w);
+    w(0);
+    pool.wait();
+}
+
 }  // namespace
 
 int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
@@ -1004,43 +1042,16 @@ int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uin
     Gcm msg;
     msg.init(key, iv, 16, false);
     OPENSSL_cleanse(key, 32);
-    // 1: the ciphertext in T 16-B aligned pieces, one per thread, into a
-    // plaintext buffer; the GHASH parts joined and the tag checked first
+    // 1: the ciphertext in 16-B aligned pieces on the pool's threads into a
+    // plaintext buffer; the joined GHASH's tag checked first
     static thread_local std::vector<uint8_t> t_plain;
     if (t_plain.size() < m) t_plain.resize(m);
     uint8_t *P = t_plain.data();
-    const int T = std::min(pool.workers() + 1, 32);
-    const uint64_t S = ((m + T - 1) / T + 15) / 16 * 16;
-    uint8_t ys[32][16];
-    auto part = [&](int w) {
-        const uint64_t a = (uint64_t)w * S;
-        if (a >= m) return;
-        const uint64_t b = std::min(m, a + S);
-        Gcm g;
-        g.init_part(msg, a);
-        g.update(ct + a, b - a, P + a);
-        g.part_ghash(ys[w]);
-        g.wipe();
-    };
-    pool.start(part);
-    part(0);
-    pool.wait();
-    auto wipe_plain = [&] {  // the plaintext buffer, on every thread
-        auto w = [&](int i) {
-            const uint64_t a = (uint64_t)i * S;
-            if (a < m) OPENSSL_cleanse(P + a, std::min(S, m - a));
-        };
-        pool.start(w);
-        w(0);
-        pool.wait();
-    };
-    const uint64_t blocks = (m + 15) / 16;
-    for (int w = 0; w < T && (uint64_t)w * S < m; ++w)
-        msg.join_part(ys[w], blocks - (std::min(m, (uint64_t)(w + 1) * S) + 15) / 16);
+    gcm_parts(pool, msg, ct, P, m);
+    auto wipe_plain = [&] { wipe_parts(pool, P, m); };
     uint8_t t[16];
     msg.tag_joined(m, t);
     msg.wipe();
-    OPENSSL_cleanse(ys, sizeof ys);
     const bool tag_ok = CRYPTO_memcmp(t, tag, 16) == 0;
     if (!tag_ok) {
         wipe_plain();
@@ -1117,6 +1128,73 @@ int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uin
     wipe_plain();
     if (bad.load()) return CHIP_ERR_SNAP;
     *out_len = d;
+    return CHIP_OK;
+}
+
+int ecies_encrypt_par_plain(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk,
+                            const uint8_t *nonce, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap,
+                            uint64_t *out_len) {
+    StagePool &pool = StagePool::get();
+    if (n < STAGE_PAR_MIN || !out || cap < n + ECIES_OVERHEAD || !gcm_vaes_on() || !pool.try_acquire())
+        return ecies_encrypt(pubkey, pubkey_len, eph_sk, nonce, in, n, out, cap, out_len);
+    struct Hold {
+        StagePool &p;
+        ~Hold() { p.release(); }
+    } hold{pool};
+    uint8_t peer[65];
+    EciesKey key;
+    int st = ecies_peer(pubkey, pubkey_len, peer);
+    if (st == CHIP_OK) st = ecies_prepare(peer, eph_sk, &key);
+    uint8_t *iv = out + 65;
+    if (st == CHIP_OK) {
+        std::memcpy(out, key.eph_pub, 65);
+        if (nonce) std::memcpy(iv, nonce, 16);
+        else if (RAND_bytes(iv, 16) != 1) st = CHIP_ERR_ECIES;
+    }
+    if (st != CHIP_OK) {
+        ecies_key_wipe(&key);
+        return st;
+    }
+    Gcm msg;
+    msg.init(key.key, iv, 16, true);
+    ecies_key_wipe(&key);
+    gcm_parts(pool, msg, in, out + 97, n);
+    msg.tag_joined(n, out + 81);
+    msg.wipe();
+    *out_len = n + ECIES_OVERHEAD;
+    return CHIP_OK;
+}
+
+int ecies_decrypt_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
+                      uint64_t cap, uint64_t *out_len, const uint8_t *pre_key, const uint8_t *pre_eph) {
+    StagePool &pool = StagePool::get();
+    if (n < ECIES_OVERHEAD + STAGE_PAR_MIN || !out || cap < n - ECIES_OVERHEAD || !gcm_vaes_on() ||
+        !pool.try_acquire())
+        return ecies_decrypt(secret, secret_len, in, n, out, cap, out_len);
+    struct Hold {
+        StagePool &p;
+        ~Hold() { p.release(); }
+    } hold{pool};
+    const uint64_t m = n - ECIES_OVERHEAD;
+    uint8_t key[32];
+    if (pre_key && pre_eph && std::memcmp(pre_eph, in, 65) == 0) {
+        std::memcpy(key, pre_key, 32);
+    } else {
+        const int st = ecies_derive_key(secret, secret_len, in, key);
+        if (st != CHIP_OK) return st;
+    }
+    Gcm msg;
+    msg.init(key, in + 65, 16, false);
+    OPENSSL_cleanse(key, 32);
+    gcm_parts(pool, msg, in + 97, out, m);
+    uint8_t t[16];
+    msg.tag_joined(m, t);
+    msg.wipe();
+    if (CRYPTO_memcmp(t, in + 81, 16) != 0) {
+        wipe_parts(pool, out, m);  // never hand back unauthenticated plaintext
+        return CHIP_ERR_ECIES;
+    }
+    *out_len = m;
     return CHIP_OK;
 }
 

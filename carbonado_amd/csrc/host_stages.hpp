@@ -127,6 +127,16 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
 int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n,
                            uint8_t *out, uint64_t cap, uint64_t *out_len, const uint8_t *key = nullptr,
                            const uint8_t *key_eph = nullptr);
+// ecies_encrypt / ecies_decrypt (no snappy) for one object of at least
+// STAGE_PAR_MIN bytes with AES-GCM split over the same pool; same output and
+// statuses (a short buffer, a small object or a busy pool: the one-thread
+// functions).  On a bad tag the written plaintext is wiped.
+int ecies_encrypt_par_plain(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk,
+                            const uint8_t *nonce, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap,
+                            uint64_t *out_len);
+int ecies_decrypt_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
+                      uint64_t cap, uint64_t *out_len, const uint8_t *key = nullptr,
+                      const uint8_t *key_eph = nullptr);
 // The AES key of an envelope whose ephemeral public key (65 B) is eph.
 int ecies_derive_key(const uint8_t *secret, uint64_t secret_len, const uint8_t eph[65], uint8_t key[32]);
 void secure_wipe(void *p, size_t n);

@@ -291,12 +291,23 @@ int main(int argc, char **argv) {
                     EXPECT(back == Bytes(ref.begin(), ref.begin() + rl), "gather_chunks");
                 }
             }
-            if (snap) {  // one object's stage on the worker pool (from STAGE_PAR_MIN; below it, the one-pass path)
+            {  // one object's stage on the worker pool (from STAGE_PAR_MIN; below it, the one-thread paths)
                 Bytes pout(cap);
                 uint64_t pl = 0;
-                EXPECT(ecies_encrypt_par(pub, 65, eph, iv, d.data(), n, pout.data(), cap, &pl, win.data()) == 0,
-                       "par enc");
-                EXPECT(pl == rl && same(pout.data(), ref.data(), rl), "par enc bytes n=%zu", n);
+                const int ps = snap ? ecies_encrypt_par(pub, 65, eph, iv, d.data(), n, pout.data(), cap, &pl, win.data())
+                                    : ecies_encrypt_par_plain(pub, 65, eph, iv, d.data(), n, pout.data(), cap, &pl);
+                EXPECT(ps == 0, "par enc");
+                EXPECT(pl == rl && same(pout.data(), ref.data(), rl), "par enc bytes n=%zu snap=%d", n, (int)snap);
+                if (!snap) {  // and back, maybe through a flipped byte
+                    Bytes env(pout.begin(), pout.begin() + pl);
+                    if (rnd(2)) env[rnd(env.size())] ^= (uint8_t)(1u << rnd(8));
+                    Bytes o1(n + 1), o2(n + 1);
+                    uint64_t l1 = 0, l2 = 0;
+                    const int s1 = ecies_decrypt(sk, 32, env.data(), env.size(), o1.data(), o1.size(), &l1);
+                    const int s2 = ecies_decrypt_par(sk, 32, env.data(), env.size(), o2.data(), o2.size(), &l2);
+                    EXPECT(s1 == s2 && (s1 != 0 || (l1 == l2 && same(o1.data(), o2.data(), l1))),
+                           "par dec plain %d vs %d n=%zu", s2, s1, n);
+                }
             }
         }
         // snap_compress_stream: the frame of snap_compress, chunks [0, filled) at their slots

@@ -606,9 +606,9 @@ def test_encode_batch_dev_many_small_trees_upper_pass(gpu, level, n):
     assert dlen == n and int(status.abs().sum()) == 0 and torch.equal(dec[:, :n], inp[:, :n])
 
 
-@pytest.mark.parametrize("level", [7, 11, 15])
+@pytest.mark.parametrize("level", [5, 7, 9, 11, 13, 15])
 def test_decode_key_derived_during_device_work(gpu, level):
-    """decode() at Ecies|Snappy with Bao and/or Zfec derives the ECIES key from
+    """decode() at Ecies (|Snappy) with Bao and/or Zfec derives the ECIES key from
     the envelope header as the input holds it while the device verifies, and
     decrypts with it only if the verified header equals those bytes
     (api_decode.cpp; host_stages.cpp ecies_decrypt_snap_par).  Round trip at

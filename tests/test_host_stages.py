@@ -570,6 +570,27 @@ def test_single_object_parallel_stage_matches_oracle(ca):
         assert fresh[:97] != enc[:97] and ca.decode(sk, h2, fresh, info2.padding_len, 3) == d
 
 
+def test_single_object_parallel_gcm_without_snappy(ca):
+    """Ecies alone (level 1) from 256 KiB: AES-GCM split over the stage pool
+    (ecies_encrypt_par_plain / ecies_decrypt_par): the C oracle's envelope,
+    a flipped tag or ciphertext byte refused, fresh randomness round-trips."""
+    from carbonado_amd.error import EciesError
+    sk = H.sha256(b"par receiver")
+    pub = H.public_key(sk)
+    eph, nonce = H.sha256(b"plain eph"), H.sha256(b"plain nonce")[:16]
+    for d in _par_inputs():
+        enc, h, info = ca.encode(pub, d, 1, ephemeral_sk=eph, nonce=nonce)
+        assert enc == O.c_encode_full(d, 1, pub, eph, nonce)[0], len(d)
+        assert ca.decode(sk, h, enc, info.padding_len, 1) == d
+        for pos in (81, 96, 97, len(enc) // 2, len(enc) - 1):
+            bad = bytearray(enc)
+            bad[pos] ^= 4
+            with pytest.raises(EciesError):
+                ca.decode(sk, h, bytes(bad), info.padding_len, 1)
+        fresh, h2, info2 = ca.encode(pub, d, 1)
+        assert ca.decode(sk, h2, fresh, info2.padding_len, 1) == d
+
+
 def test_single_object_stage_concurrent_callers(ca):
     """Several threads calling encode() at once: one gets the stage's worker
     pool, the others take the one-thread path; every output is the oracle's."""

@@ -114,7 +114,7 @@ for s in "$@"; do
                  run bench_e2ed15_s${sl}_m${mib}_$i 300 python3 bench.py --mode e2e-decode --level 15 --steps 4 --warmup 1 --no-cpu-baseline --no-verify --slots $sl --slice-mib $mib
                done; done; done ;;
     stageab) for i in 1 2 3 4; do for t in 1 8; do
-               CHIP_STAGE_THREADS=$t run latency_stage${t}_$i 300 python3 tools/latency_probe.py 60 15,3 1048576,4194304
+               CHIP_STAGE_THREADS=$t run latency_stage${t}_$i 300 python3 tools/latency_probe.py 60 ${STAGE_LEVELS:-15,3} 1048576,4194304
              done; done ;;
     upperab) for i in 1 2; do for u in 1 0; do
                CHIP_UPPER_PASS=$u run bench_pipe12_1mib_up${u}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048576 --objects 16384 --no-cpu-baseline
