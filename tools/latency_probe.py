@@ -39,8 +39,8 @@ def main():
     for level in levels:
         for n in sizes:
             data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
-            pk = PUB if level & 2 else b""
-            sk = SK if level & 2 else b""
+            pk = PUB if level & 1 else b""
+            sk = SK if level & 1 else b""
             enc, h, info = ca.encode(pk, data, level)
             assert ca.decode(sk, h, enc, info.padding_len, level) == data
             e = med_us(lambda: ca.encode(pk, data, level), reps)
