@@ -63,7 +63,6 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
         olen_max = std::max(olen_max, geo[o].olen);
     }
     if (!zfec && !bao) {  // host stages only (or identity)
-        Scratch tmp;
         for (uint64_t o = 0; o < count; ++o) {
             if (status[o] != CHIP_OK) continue;
             const uint8_t *src = in + o * in_stride;
@@ -79,12 +78,8 @@ int chip_decode_host_batch(uint8_t format, const uint8_t *secret_key, uint64_t s
             int st = CHIP_OK;
             if ((format & CHIP_FORMAT_ECIES) && (format & CHIP_FORMAT_SNAPPY)) {
                 st = host::ecies_decrypt_snap_par(secret_key, sk_len, src, n, dst, out_stride, &got);
-            } else if (format & CHIP_FORMAT_ECIES) {
-                uint8_t *t = tmp.get(n + 1);
-                st = host::ecies_decrypt(secret_key, sk_len, src, n, (format & CHIP_FORMAT_SNAPPY) ? t : dst,
-                                         (format & CHIP_FORMAT_SNAPPY) ? n + 1 : out_stride, &got);
-                src = t;
-                n = got;
+            } else if (format & CHIP_FORMAT_ECIES) {  // Ecies alone here (Ecies|Snappy above)
+                st = host::ecies_decrypt_par(secret_key, sk_len, src, n, dst, out_stride, &got);
             }
             else if (format & CHIP_FORMAT_SNAPPY) st = host::snap_decompress(src, n, dst, out_stride, &got);
             status[o] = st;

@@ -608,3 +608,34 @@ def test_single_object_stage_concurrent_callers(ca):
         outs = list(ex.map(run, jobs))
     for (d, e, nn), got in zip(jobs, outs):
         assert got == O.c_encode_full(d, 3, pub, e, nn)[0]
+
+
+@pytest.mark.parametrize("level", [1, 3])
+def test_decode_host_batch_host_only_levels(ca, level):
+    """chip_decode_host_batch at host-only levels (no device part) decodes
+    object by object, each large one on the stage pool: every object back,
+    a tampered envelope fails alone with EciesError's status."""
+    import torch
+    from carbonado_amd import device
+    sk = H.sha256(b"par receiver")
+    pub = H.public_key(sk)
+    ins = _par_inputs()[:4]
+    encs = [ca.encode(pub, d, level)[0] for d in ins]
+    width = max(len(e) for e in encs)
+    enc = torch.zeros((len(encs), width), dtype=torch.uint8)
+    for i, e in enumerate(encs):
+        enc[i, :len(e)] = torch.frombuffer(bytearray(e), dtype=torch.uint8)
+    out = torch.zeros((len(encs), max(len(d) for d in ins) + 64), dtype=torch.uint8)
+    hashes = torch.zeros((len(encs), 32), dtype=torch.uint8)
+    lens, pads = [len(e) for e in encs], [0] * len(encs)
+    dlen, st = device.decode_host_batch(level, enc, lens, hashes, pads, out, secret_key=sk)
+    assert st == [0] * len(encs)
+    for i, d in enumerate(ins):
+        assert dlen[i] == len(d) and out[i, :len(d)].numpy().tobytes() == d
+    enc[1, lens[1] - 1] ^= 1
+    out.zero_()
+    dlen, st = device.decode_host_batch(level, enc, lens, hashes, pads, out, secret_key=sk, raise_first=False)
+    assert st[1] != 0 and st[0] == st[2] == st[3] == 0
+    assert not out[1].any()  # the failed object's plaintext was wiped
+    for i in (0, 2, 3):
+        assert out[i, :len(ins[i])].numpy().tobytes() == ins[i]
