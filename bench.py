@@ -96,7 +96,6 @@ def parse(argv=None):
     ap.add_argument("--fsync", action="store_true", help="file mode: fsync every output file")
     ap.add_argument("--file-slice", type=int, default=64, help="file mode: files per pipeline slice")
     ap.add_argument("--io-threads", type=int, default=16, help="file mode: reader / writer threads per stage")
-    ap.add_argument("--device-lanes", type=int, default=2, help="file mode: slices in the device stage at once")
     ap.add_argument("--level", type=int, default=12, help="e2e mode: Format bits (Bao|Zfec = 12)")
     ap.add_argument("--slots", type=int, default=3, help="e2e mode: pipeline slots (streams)")
     ap.add_argument("--slice-mib", type=int, default=256, help="e2e mode: input bytes per pipeline slice")
@@ -905,7 +904,7 @@ class Workload:
                 self.file_stats = {}
                 self.results = cfile.encode_files(self.paths, d, self.sk, lv, slice_objects=args.file_slice,
                                                   host_threads=args.host_threads, fsync=args.fsync,
-                                                  io_threads=args.io_threads, device_lanes=args.device_lanes,
+                                                  io_threads=args.io_threads,
                                                   stats=self.file_stats)
             self.step = step
             step()
@@ -1595,8 +1594,7 @@ def main():
         if getattr(wl, "soff", 0):
             res["config"]["stream_offset"] = wl.soff
         if args.mode == "file":
-            res["config"].update(file_slice=args.file_slice, io_threads=args.io_threads,
-                                 device_lanes=args.device_lanes)
+            res["config"].update(file_slice=args.file_slice, io_threads=args.io_threads)
         if live and "bytes" in live:
             res["roofline"].update({"traffic_ratio": round(live["bytes"] / wl.alg_bytes, 4),
                                     "pmc_KiB_per_launch": {"FETCH_SIZE": live["FETCH_SIZE_KiB"],

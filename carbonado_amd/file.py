@@ -146,8 +146,7 @@ def _host_buffer(shape):
 
 def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None = None,
                  metadata: bytes | None = None, slice_objects: int = 64, host_threads: int = 16,
-                 nslots: int = 3, io_threads: int = 16, fsync: bool = False, stats: dict | None = None,
-                 device_lanes: int = 2) -> list:
+                 nslots: int = 3, io_threads: int = 16, fsync: bool = False, stats: dict | None = None) -> list:
     """file::encode (file.rs:409-440) over many flat files of one size, end to
     end: disk -> pinned host memory -> HBM (zfec + bao on the device, host
     Snappy/Ecies on `host_threads` threads) -> pinned host memory -> header +
@@ -155,12 +154,8 @@ def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None =
     thread fills the next slice of `slice_objects` files while the device
     works on the current one and a writer thread signs and writes the
     previous one; each of those stages spreads its files over `io_threads`
-    threads.  The device stage runs `device_lanes` slices at once, one per
-    thread (each thread has its own library context: streams and slots), so
-    one call's fill (its first slice's host stage) overlaps another's drain
-    (its last slice's kernels and copy back).  Returns [(output path,
-    EncodeInfo)] in input order; `stats` (optional) receives the busy seconds
-    of each stage (the device's summed over its lanes)."""
+    threads.  Returns [(output path, EncodeInfo)] in input order; `stats`
+    (optional) receives the busy seconds of each stage."""
     import os
     import queue
     import threading
@@ -188,12 +183,11 @@ def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None =
     pub33 = Header.new(sk, pk, bytes(32), 0, 0, 0, 0, None).pubkey  # the stored (compressed) form
     cap = L.chip_encode_max_len(n)
     S = max(1, min(slice_objects, len(in_paths)))
-    slices = [list(range(i, min(i + S, len(in_paths)))) for i in range(0, len(in_paths), S)]
-    lanes = max(1, min(device_lanes, len(slices)))
-    nbuf = lanes + 1
+    nbuf = 2
     h_in = [_host_buffer((S, max(n, 1))) for _ in range(nbuf)]
     h_out = [_host_buffer((S, cap)) for _ in range(nbuf)]
     h_hash = [_host_buffer((S, 32)) for _ in range(nbuf)]
+    slices = [list(range(i, min(i + S, len(in_paths)))) for i in range(0, len(in_paths), S)]
     results: list = [None] * len(in_paths)
     free_in, ready_in = queue.Queue(), queue.Queue()
     free_out, ready_out = queue.Queue(), queue.Queue()
@@ -277,18 +271,18 @@ def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None =
             finally:
                 free_out.put(b)  # always returned, also while draining after a failure
 
-    busy_lock = threading.Lock()
-
-    def device_lane():
-        while not stop.is_set():
-            item = get(ready_in)
+    tr, tw = threading.Thread(target=reader), threading.Thread(target=writer)
+    tr.start()
+    tw.start()
+    try:
+        for _ in slices:
+            item = None if stop.is_set() else get(ready_in)
             if item is None:
-                ready_in.put(None)  # the end of the batch, for the other lanes too
-                return
+                break
             b, sl = item
             ob = get(free_out)
             if ob is None:
-                return
+                break
             cnt = len(sl)
             t0 = time.perf_counter()
             try:
@@ -296,21 +290,10 @@ def encode_files(in_paths, out_dir, sk: bytes, level: int, *, pk: bytes | None =
                                                         nslots, pubkey=pk, host_threads=host_threads)
             except BaseException as e:  # noqa: BLE001
                 fail(e)
-                return
-            with busy_lock:
-                busy["device_s"] += time.perf_counter() - t0
+                break
+            busy["device_s"] += time.perf_counter() - t0
             free_in.put(b)
             ready_out.put((ob, sl, olens, infos))
-
-    tr, tw = threading.Thread(target=reader), threading.Thread(target=writer)
-    tds = [threading.Thread(target=device_lane) for _ in range(lanes)]
-    tr.start()
-    tw.start()
-    try:
-        for t in tds:
-            t.start()
-        for t in tds:
-            t.join()
     finally:
         ready_out.put(None)
         if errors:

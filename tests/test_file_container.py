@@ -148,21 +148,17 @@ def test_file_encode_given_pubkey_and_metadata(ca):
 def _fake_device(fail_at=None):
     """Stand-in for device.encode_host_batch (no GPU here): copies each input
     into its output row; raises on slice number `fail_at`."""
-    import threading
     from carbonado_amd.structs import EncodeInfo
     calls = []
-    lock = threading.Lock()  # encode_files runs two device lanes at once
 
     def f(level, inp, n, out, hashes, nslots, pubkey=b"", host_threads=0):
-        with lock:
-            calls.append(inp.shape[0])
-            idx = len(calls)
-        if fail_at is not None and idx - 1 == fail_at:
+        calls.append(inp.shape[0])
+        if fail_at is not None and len(calls) - 1 == fail_at:
             raise RuntimeError("device stage failed")
         cnt = inp.shape[0]
         out[:, :n] = inp[:, :n]
         hashes.zero_()
-        hashes[:, 0] = idx
+        hashes[:, 0] = len(calls)
         hashes[:, 1] = __import__("torch").arange(cnt, dtype=__import__("torch").uint8)
         infos = [EncodeInfo(n, n, 0, 0.0, 0, 0, 0, 0.0, 0, 0, 0, 0) for _ in range(cnt)]
         return [n] * cnt, infos
@@ -190,7 +186,7 @@ def test_encode_files_pipeline_ok(ca, tmp_path, monkeypatch):
     out.mkdir()
     sk = H.sha256(b"writer")
     res = file.encode_files(paths, out, sk, 12, slice_objects=2, io_threads=2)
-    assert sorted(calls) == [1, 2, 2, 2]
+    assert calls == [2, 2, 2, 1]
     assert len(res) == 7 and all(r is not None for r in res)
     for i, (p, info) in enumerate(res):
         body = p.read_bytes()
