@@ -859,6 +859,17 @@ void spin_until(F &&ready) {
     }
 }
 
+// A calling thread's scratch of the pooled stage (compressed blocks, or a
+// plaintext buffer): kept for the next object up to SCRATCH_KEEP bytes, freed
+// on return beyond that, so one huge object does not pin its size per thread.
+constexpr size_t SCRATCH_KEEP = 64u << 20;
+struct ScratchCap {
+    std::vector<uint8_t> &v;
+    ~ScratchCap() {
+        if (v.size() > SCRATCH_KEEP) std::vector<uint8_t>().swap(v);
+    }
+};
+
 // AES-GCM of m contiguous bytes in T 16-B aligned pieces, one per pool thread
 // (the caller holds the pool); the pieces' GHASH joined into msg
 void gcm_parts(StagePool &pool, Gcm &msg, const uint8_t *in, uint8_t *out, uint64_t m) {
@@ -916,6 +927,7 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
     const uint64_t nb = (n + MAX_BLOCK - 1) / MAX_BLOCK;
     static thread_local std::vector<uint8_t> t_scr;  // one compressed block per slot
     if (t_scr.size() < nb * MAX_COMPRESS_BLOCK) t_scr.resize(nb * MAX_COMPRESS_BLOCK);
+    ScratchCap cap_scr{t_scr};
     uint8_t *scr = t_scr.data();
     std::vector<Block> blk(nb);
     std::vector<uint64_t> boff(nb);  // frame offset of each block's chunk header
@@ -1046,6 +1058,7 @@ int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uin
     // plaintext buffer; the joined GHASH's tag checked first
     static thread_local std::vector<uint8_t> t_plain;
     if (t_plain.size() < m) t_plain.resize(m);
+    ScratchCap cap_plain{t_plain};  // every return below wipes it first
     uint8_t *P = t_plain.data();
     gcm_parts(pool, msg, ct, P, m);
     auto wipe_plain = [&] { wipe_parts(pool, P, m); };
