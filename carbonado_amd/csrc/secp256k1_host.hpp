@@ -184,6 +184,26 @@ inline Fe fe_inv(const Fe &a) {
     return fe_mul(fe_sqr_n(t, 2), a);
 }
 
+// a^((p+1)/4), a square root of a when a is a square (p = 3 mod 4; the
+// caller checks r^2 == a).  The blocks of ones of (p+1)/4 are 223, 22 and 2
+// bits long: 253 squarings and 13 multiplications.
+inline Fe fe_sqrt_cand(const Fe &a) {
+    const Fe x2 = fe_mul(fe_sqr(a), a);
+    const Fe x3 = fe_mul(fe_sqr(x2), a);
+    const Fe x6 = fe_mul(fe_sqr_n(x3, 3), x3);
+    const Fe x9 = fe_mul(fe_sqr_n(x6, 3), x3);
+    const Fe x11 = fe_mul(fe_sqr_n(x9, 2), x2);
+    const Fe x22 = fe_mul(fe_sqr_n(x11, 11), x11);
+    const Fe x44 = fe_mul(fe_sqr_n(x22, 22), x22);
+    const Fe x88 = fe_mul(fe_sqr_n(x44, 44), x44);
+    const Fe x176 = fe_mul(fe_sqr_n(x88, 88), x88);
+    const Fe x220 = fe_mul(fe_sqr_n(x176, 44), x44);
+    const Fe x223 = fe_mul(fe_sqr_n(x220, 3), x3);
+    Fe t = fe_mul(fe_sqr_n(x223, 23), x22);
+    t = fe_mul(fe_sqr_n(t, 6), x2);
+    return fe_sqr_n(t, 2);
+}
+
 // 32 big-endian bytes (< 2^256) -> magnitude 1
 inline Fe fe_from_be(const uint8_t b[32]) {
     uint64_t w[4];
@@ -207,6 +227,24 @@ inline void fe_to_be(const Fe &f, uint8_t b[32]) {
 inline bool fe_is_zero(const Fe &f) {
     const Fe n = fe_norm(f);
     return (n.v[0] | n.v[1] | n.v[2] | n.v[3] | n.v[4]) == 0;
+}
+
+// A compressed point (0x02 / 0x03 || x, 33 bytes) -> affine x, y, as
+// libsecp256k1's PublicKey::parse and OpenSSL's oct2point accept it: false
+// unless x < p and x^3 + 7 is a square; y the root of the tag's parity.
+inline bool decompress(const uint8_t in[33], Fe &x, Fe &y) {
+    static const uint8_t P[32] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                  0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                  0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFE, 0xFF, 0xFF, 0xFC, 0x2F};
+    if ((in[0] != 0x02 && in[0] != 0x03) || std::memcmp(in + 1, P, 32) >= 0) return false;
+    x = fe_from_be(in + 1);
+    const Fe y2 = fe_add(fe_mul(fe_sqr(x), x), Fe{{7, 0, 0, 0, 0}});
+    Fe r = fe_sqrt_cand(y2);
+    if (!fe_is_zero(fe_sub(fe_sqr(r), y2))) return false;
+    r = fe_norm(r);
+    if ((r.v[0] & 1) != (uint64_t)(in[0] & 1)) r = fe_norm(fe_sub(Fe{{0, 0, 0, 0, 0}}, r));
+    y = r;
+    return true;
 }
 
 struct Pt {

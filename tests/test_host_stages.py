@@ -639,3 +639,26 @@ def test_decode_host_batch_host_only_levels(ca, level):
     assert not out[1].any()  # the failed object's plaintext was wiped
     for i in (0, 2, 3):
         assert out[i, :len(ins[i])].numpy().tobytes() == ins[i]
+
+
+def test_compressed_receiver_keys(ca):
+    """33-byte receiver keys are decompressed by the native field code
+    (secp256k1_host.hpp decompress: x < p, y = (x^3 + 7)^((p+1)/4) checked,
+    the tag's parity): the same envelope as with the 65-byte key for 64
+    random receivers, and EciesError for x >= p, an x off the curve and
+    other tags."""
+    from carbonado_amd.error import EciesError
+    P = 2**256 - 2**32 - 977
+    eph, nonce = H.sha256(b"cmp eph"), H.sha256(b"cmp nonce")[:16]
+    msg = b"compressed receiver " * 50
+    for i in range(64):
+        pub = H.public_key(H.sha256(b"cmp %d" % i))
+        x, y = int.from_bytes(pub[1:33], "big"), int.from_bytes(pub[33:], "big")
+        pk33 = bytes([2 + (y & 1)]) + pub[1:33]
+        assert ca.encoding.ecies(pk33, msg, ephemeral_sk=eph, nonce=nonce) == H.ecies_encrypt(pub, msg, eph, nonce)
+    off = next(x for x in range(1, 100) if pow((x**3 + 7) % P, (P - 1) // 2, P) != 1)
+    bad = [b"\x02" + P.to_bytes(32, "big"), b"\x03" + (P + 5).to_bytes(32, "big"),
+           b"\x02" + off.to_bytes(32, "big"), b"\x04" + pub[1:33], b"\x05" + pub[1:33], b"\x00" * 33]
+    for pk in bad:
+        with pytest.raises(EciesError):
+            ca.encoding.ecies(pk, msg, ephemeral_sk=eph, nonce=nonce)
