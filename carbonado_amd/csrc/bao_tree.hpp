@@ -198,6 +198,12 @@ inline uint64_t bao_scratch_len_t(uint64_t n, uint64_t count) {
     return count * 32 * (N0 + (N0 + 1) / 2);
 }
 
+// K4t with a quad (four lanes) per parent for up to TOP_QUAD_MAX objects,
+// whose tree top is latency-bound (small_kernels.hip; CHIP_TOP_QUAD=0: off)
+constexpr uint64_t TOP_QUAD_MAX = 8;
+bool top_quad_on();
+hipError_t top_quad_launch(int mode, const ParentArgs &pa, hipStream_t stream);
+
 // The tree above a level of node CVs: K4 per level, then K4t for the top
 // once a level has <= K4T_MAX nodes.  cv_prev [count][stride_prev] holds the
 // cnt_prev nodes of level `level - 1`; cv_next (stride_next >= ceil(cnt_prev/2))
@@ -216,6 +222,7 @@ hipError_t run_parent_levels(uint8_t *cv_prev, uint64_t stride_prev, uint64_t cn
         pa.N = N; pa.count = count; pa.stream = stream_buf; pa.stream_stride = sstride;
         pa.hash = d_hash; pa.status = d_status;
         if (cnt_prev <= (uint64_t)K4T_MAX && count <= 0x7fffffffull) {  // the rest of the tree, one launch
+            if (count <= TOP_QUAD_MAX && top_quad_on()) return top_quad_launch(MODE, pa, stream);
             const size_t lds = 2 * cnt_prev * 32;
             if (count >= 2048)
                 hipLaunchKernelGGL((bao_top_kernel<MODE, BAO_NTS, 64>), dim3((unsigned)count), dim3(64), lds, stream,

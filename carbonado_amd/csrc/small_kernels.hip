@@ -316,7 +316,99 @@ hipError_t launch(int mode, SmallArgs a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// K4t for one object with a quad per parent (small_kernel's phase 3 over a
+// level of cnt_prev <= K4T_MAX CVs): a single object's tree top is ~10
+// dependent levels, latency-bound with a lane per parent (r10zm: 24-29 us of
+// a 1 MiB call).  Same nodes, hash and verdict as bao_top_kernel.
+template <int MODE>
+__global__ __launch_bounds__(BIG_TPB) void top_quad_kernel(ParentArgs a) {
+    constexpr int QUADS = BIG_TPB / 4;
+    __shared__ __attribute__((aligned(16))) uint32_t cvs[2][K4T_MAX][8];
+    __shared__ __attribute__((aligned(16))) uint32_t msg[QUADS][16];
+    const int t = threadIdx.x, q = t & 3, g = t >> 2;
+    const uint64_t obj = blockIdx.x;
+    uint64_t cnt_prev = a.cnt_prev;
+    for (uint64_t i = t; i < cnt_prev; i += BIG_TPB) {
+        uint32_t c[8];
+        load_cv(a.cv_prev + (obj * a.stride_prev + i) * 32, c);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) cvs[0][i][w] = c[w];
+    }
+    __syncthreads();
+    const uint32_t slot = (uint32_t)(reinterpret_cast<uintptr_t>(&msg[g][0]) - reinterpret_cast<uintptr_t>(&msg[0][0]));
+    const uint8_t *mbase = reinterpret_cast<const uint8_t *>(&msg[0][0]);
+    const MsgIdx mi(q, slot);
+    const uint32_t iv0 = q == 0 ? IV(0) : q == 1 ? IV(1) : q == 2 ? IV(2) : IV(3);
+    const uint32_t iv1 = q == 0 ? IV(4) : q == 1 ? IV(5) : q == 2 ? IV(6) : IV(7);
+    bool ok = true;
+    int cur = 0;
+    for (int level = a.level; cnt_prev > 1; ++level) {
+        const uint64_t cnt = (cnt_prev + 1) / 2;
+        for (uint64_t p = g; p < cnt; p += QUADS) {
+            if (2 * p + 1 >= cnt_prev) {  // odd last node: promoted unchanged
+                cvs[cur ^ 1][p][q] = cvs[cur][2 * p][q];
+                cvs[cur ^ 1][p][4 + q] = cvs[cur][2 * p][4 + q];
+                continue;
+            }
+            // message = left CV || right CV: my 16 B are words 4q..4q+3
+            const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cvs[cur][2 * p + (q >> 1)][4 * (q & 1)]);
+            *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = mw;
+            wave_sync();
+            const bool root = cnt == 1;
+            uint32_t h0 = iv0, h1 = iv1;
+            compress4(h0, h1, mbase, mi, q, iv0, 0, 64, F_PARENT | (root ? F_ROOT : 0u));
+            wave_sync();
+            if (a.stream) {
+                uint8_t *node = a.stream + obj * a.stream_stride + parent_stream_off(p << level, level, a.N) + 16 * q;
+                if (MODE == 0) {
+                    store16_a8<false>(node, mw);
+                } else {
+                    const u32x4 st = load16_a8(node);
+                    ok &= st.x == mw.x && st.y == mw.y && st.z == mw.z && st.w == mw.w;
+                }
+            }
+            if (root) {
+                uint32_t *hp = reinterpret_cast<uint32_t *>(a.hash + obj * 32);
+                if (MODE == 0) {
+                    hp[q] = h0;
+                    hp[4 + q] = h1;
+                } else {
+                    ok &= hp[q] == h0 && hp[4 + q] == h1;
+                }
+            } else {
+                cvs[cur ^ 1][p][q] = h0;
+                cvs[cur ^ 1][p][4 + q] = h1;
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        cnt_prev = cnt;
+    }
+    if (MODE == 1 && !ok) flag_mismatch(a.status, obj);
+}
+
 }  // namespace small
+
+namespace bao {
+
+bool top_quad_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("CHIP_TOP_QUAD");
+        return !(e && !std::strcmp(e, "0"));
+    }();
+    return on;
+}
+
+hipError_t top_quad_launch(int mode, const ParentArgs &pa, hipStream_t stream) {
+    if (pa.cnt_prev > (uint64_t)K4T_MAX || pa.count == 0 || pa.count > 0x7fffffffull) return hipErrorInvalidValue;
+    if (mode == 0)
+        hipLaunchKernelGGL((small::top_quad_kernel<0>), dim3((unsigned)pa.count), dim3(small::BIG_TPB), 0, stream, pa);
+    else
+        hipLaunchKernelGGL((small::top_quad_kernel<1>), dim3((unsigned)pa.count), dim3(small::BIG_TPB), 0, stream, pa);
+    return hipGetLastError();
+}
+
+}  // namespace bao
 
 bool small_ok(uint64_t bao_n, uint64_t count, uint64_t tiny_max) {
     if (!small::enabled() || count == 0) return false;

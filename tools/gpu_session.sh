@@ -2,7 +2,7 @@
 # A GPU session of named steps, each under its own time limit, stopping at
 # the first failure.  bash tools/gpu_session.sh TAG step...
 #   steps: tests smoke encode decode 8of16 2rank bao baodec pipe12 pdec12 pdec4 pdec8 e2e15 e2e15full
-#          e2e12 e2ed15 e2edab seg1m prof1m k13fetch ecbench gcmab fileab e2edsweep stageab abilat soffab soffe2e baoab baodecab pdecab scrubbab ftsoff crcab upperab prepab scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s profbao profbaodec profpdec splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
+#          e2e12 e2ed15 e2edab seg1m prof1m k13fetch ecbench gcmab fileab e2edsweep stageab abilat topquadab soffab soffe2e baoab baodecab pdecab scrubbab ftsoff crcab upperab prepab scrub scrubb hasher file15 file12 prof pipe12l15 encodetorch mixprobe ftune ftunepmc valuprobe numaprobe baotune baotunepmc hasher3 valupk hasherva hashercopy hasherbind h2dprobe hashercache prof12 prof15s profbao profbaodec profpdec splitab streamab ntab ntab3 directab hostprobe slicesweep e2e3 e2eprof e2ed15full sdmaab
 set -e -o pipefail
 TAG=$1; shift
 O=$PWD/gpurun_out/$TAG
@@ -117,6 +117,7 @@ for s in "$@"; do
                CHIP_STAGE_THREADS=$t run latency_stage${t}_$i 300 python3 tools/latency_probe.py 60 ${STAGE_LEVELS:-15,3} 1048576,4194304
              done; done ;;
     abilat) run abi_latency 300 ./tools/abi_latency 50 ;;
+    topquadab) for i in 1 2; do for tq in 0 1; do CHIP_TOP_QUAD=$tq run abi_latency_tq${tq}_$i 300 ./tools/abi_latency 50; done; done ;;
     upperab) for i in 1 2; do for u in 1 0; do
                CHIP_UPPER_PASS=$u run bench_pipe12_1mib_up${u}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048576 --objects 16384 --no-cpu-baseline
                CHIP_UPPER_PASS=$u run bench_pipe12_1mib_l15shape_up${u}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048811 --objects 16384 --no-cpu-baseline
