@@ -325,6 +325,9 @@ __global__ __launch_bounds__(BIG_TPB) void top_quad_kernel(ParentArgs a) {
     constexpr int QUADS = BIG_TPB / 4;
     __shared__ __attribute__((aligned(16))) uint32_t cvs[2][K4T_MAX][8];
     __shared__ __attribute__((aligned(16))) uint32_t msg[QUADS][16];
+    // verify: every stored node of the walk fetched up front (one round of
+    // loads instead of one dependent global-memory wait per level)
+    __shared__ __attribute__((aligned(16))) u32x4 stored[MODE == 1 ? K4T_MAX * 4 : 4];
     const int t = threadIdx.x, q = t & 3, g = t >> 2;
     const uint64_t obj = blockIdx.x;
     uint64_t cnt_prev = a.cnt_prev;
@@ -334,7 +337,19 @@ __global__ __launch_bounds__(BIG_TPB) void top_quad_kernel(ParentArgs a) {
 #pragma unroll
         for (int w = 0; w < 8; ++w) cvs[0][i][w] = c[w];
     }
+    if (MODE == 1 && a.stream) {  // level by level: pairs floor(cnt / 2), 16 B per lane of a quad
+        const uint8_t *st = a.stream + obj * a.stream_stride;
+        uint64_t cnt = cnt_prev, base = 0;
+        for (int level = a.level; cnt > 1; ++level) {
+            const uint64_t pairs = cnt / 2;
+            for (uint64_t i = t; i < 4 * pairs; i += BIG_TPB)
+                stored[4 * base + i] = load16_a8(st + parent_stream_off((i >> 2) << level, level, a.N) + 16 * (i & 3));
+            base += pairs;
+            cnt = (cnt + 1) / 2;
+        }
+    }
     __syncthreads();
+    uint64_t nbase = 0;  // verify: index of this level's first node in `stored`
     const uint32_t slot = (uint32_t)(reinterpret_cast<uintptr_t>(&msg[g][0]) - reinterpret_cast<uintptr_t>(&msg[0][0]));
     const uint8_t *mbase = reinterpret_cast<const uint8_t *>(&msg[0][0]);
     const MsgIdx mi(q, slot);
@@ -359,11 +374,11 @@ __global__ __launch_bounds__(BIG_TPB) void top_quad_kernel(ParentArgs a) {
             compress4(h0, h1, mbase, mi, q, iv0, 0, 64, F_PARENT | (root ? F_ROOT : 0u));
             wave_sync();
             if (a.stream) {
-                uint8_t *node = a.stream + obj * a.stream_stride + parent_stream_off(p << level, level, a.N) + 16 * q;
                 if (MODE == 0) {
+                    uint8_t *node = a.stream + obj * a.stream_stride + parent_stream_off(p << level, level, a.N) + 16 * q;
                     store16_a8<false>(node, mw);
                 } else {
-                    const u32x4 st = load16_a8(node);
+                    const u32x4 st = stored[4 * (nbase + p) + q];
                     ok &= st.x == mw.x && st.y == mw.y && st.z == mw.z && st.w == mw.w;
                 }
             }
@@ -382,6 +397,7 @@ __global__ __launch_bounds__(BIG_TPB) void top_quad_kernel(ParentArgs a) {
         }
         __syncthreads();
         cur ^= 1;
+        nbase += cnt_prev / 2;
         cnt_prev = cnt;
     }
     if (MODE == 1 && !ok) flag_mismatch(a.status, obj);
