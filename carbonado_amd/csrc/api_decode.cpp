@@ -341,8 +341,10 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         }
         // While the device verifies: the ECIES key from the envelope header as the
         // input holds it (content bytes [0, 65): chunk 0 of the bao stream, or the
-        // first shard); decrypt uses it only if the verified header is the same
-        if (ecies && olen >= host::ECIES_OVERHEAD) {
+        // first shard); decrypt uses it only if the verified header is the same.
+        // Only for an envelope the pool path decrypts: the one-thread paths
+        // derive their own key, so a key derived here would be paid twice
+        if (ecies && host::ecies_par_eligible(olen)) {
             const uint64_t h0 = bao ? bao_chunk_offset(0, (blen + 1023) / 1024) : 0;
             if (h0 + 65 <= n && (!bao || blen >= 65)) {
                 std::memcpy(pre_eph, in + h0, 65);

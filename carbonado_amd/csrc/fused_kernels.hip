@@ -177,6 +177,12 @@ hipError_t zfec_bao_fused_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
     uint8_t *next = a.cv + count * n0 * 32;
     if ((e = launch_parts(a, n0, full ? KF : KG, stream)) != hipSuccess) return e;
     if (full) return upper_levels(a.cv, n0, next, a.N, count, coff, d_out, out_stride, d_hash, stream);
+    // A tree of at most 8 chunks (C == 1024: N == 8) has its root among
+    // levels 1-3; the levels pass would store it as a non-root parent, so the
+    // walk runs from level 1 over the chunk CVs and finalizes the root itself.
+    if (a.N <= 8)
+        return bao::run_parent_levels<0, false>(a.cv, a.N, a.N, 1, next, (a.N + 1) / 2, a.N, count, d_out,
+                                                out_stride, d_hash, nullptr, stream);
     // levels 1-3 of every group from the level-0 CVs, then from level 4
     const uint64_t n3 = (a.N + 7) / 8, work = count * n3;
     // a whole level's nodes staged per round (QS 4): node by node (QS 1, 4 KiB

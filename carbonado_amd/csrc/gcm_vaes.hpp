@@ -55,6 +55,9 @@ struct Gcm {
 
 // VAES, VPCLMULQDQ, AVX-512 F/BW/VL, AES-NI and PCLMULQDQ all present
 bool gcm_fast_available();
+// the ECIES stage uses Gcm (gcm_fast_available() and not CHIP_GCM=openssl;
+// host_stages.cpp), else OpenSSL's EVP
+bool gcm_vaes_on();
 
 }  // namespace host
 }  // namespace chip

@@ -137,6 +137,12 @@ int ecies_encrypt_par_plain(const uint8_t *pubkey, uint64_t pubkey_len, const ui
 int ecies_decrypt_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
                       uint64_t cap, uint64_t *out_len, const uint8_t *key = nullptr,
                       const uint8_t *key_eph = nullptr);
+// An envelope of n bytes is decrypted on the pool (ecies_decrypt_par /
+// ecies_decrypt_snap_par) unless the pool is busy: at least STAGE_PAR_MIN of
+// ciphertext, within GCM's length limit, on the VAES path.  A caller deriving
+// the key ahead (ecies_derive_key) does so only then: the one-thread paths
+// derive their own.
+bool ecies_par_eligible(uint64_t n);
 // The AES key of an envelope whose ephemeral public key (65 B) is eph.
 int ecies_derive_key(const uint8_t *secret, uint64_t secret_len, const uint8_t eph[65], uint8_t key[32]);
 void secure_wipe(void *p, size_t n);

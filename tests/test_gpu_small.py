@@ -192,3 +192,53 @@ def test_tiny_batches_randomized(gpu, seed):
         assert st[i] == (5 if i in hit else 0), (n, count, i, st[i])
         if i not in hit:
             assert bytes(dec[i, :n].cpu().numpy()) == objs[i], (n, count, i)
+
+
+_K13_C1024 = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+import carbonado_amd as ca
+from carbonado_amd import device as D
+from oracle import oracle as O
+ca._lib.lib().chip_init(0)
+bad = []
+for n in (1, 1000, 4095, 4096):
+    d = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+    oenc, oh, _ = O.encode(d, 12)
+    enc, h, info = ca.encode(b"", d, 12)
+    if enc != oenc or h != oh:
+        bad.append(("single", n))
+    # a device batch of 3 objects (count >= 2 also takes K13 with KS off)
+    count, stride = 3, max(16, (n + 15) // 16 * 16)
+    inp = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    for i in range(count):
+        inp[i, :n] = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+    out = torch.zeros((count, (len(oenc) + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+    D.encode_batch(12, inp, n, out, hashes, D.encode_scratch(12, n, count))
+    torch.cuda.synchronize()
+    for i in range(count):
+        if bytes(out[i, :len(oenc)].cpu().numpy()) != oenc or bytes(hashes[i].cpu().numpy()) != oh:
+            bad.append(("batch", n, i))
+print("BAD", bad) if bad else print("OK")
+"""
+
+
+def test_k13_one_column_shards_with_ks_off(gpu, tmp_path):
+    """K13's general path at C == 1024 (N == 8: the whole tree
+    lies in levels 1-3) must finalize the root itself.  KS normally takes
+    these objects, so the run switches it off (CHIP_SMALL=0, read once per
+    process) in a child process and compares streams and hashes with the
+    oracle, single objects and a device batch."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parents[1])
+    env = dict(os.environ, CHIP_SMALL="0")
+    out = subprocess.run([sys.executable, "-c", _K13_C1024, root], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.strip().endswith("OK"), out.stdout + out.stderr

@@ -22,6 +22,7 @@ def fuzzer(tmp_path_factory):
            "-fno-omit-frame-pointer", str(ROOT / "tests" / "host_fuzz.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "host_snap.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "host_stages.cpp"),
+           str(ROOT / "carbonado_amd" / "csrc" / "host_stages_par.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "gcm_vaes.cpp"),
            str(ROOT / "carbonado_amd" / "csrc" / "file_container.cpp"), "-I" + str(ROOT / "include"),
            "-lcrypto", "-lpthread", "-o", str(exe)]
@@ -45,7 +46,8 @@ def tsan_fuzzer(tmp_path_factory):
     exe = tmp_path_factory.mktemp("tsan") / "host_fuzz"
     src = ROOT / "carbonado_amd" / "csrc"
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", str(ROOT / "tests" / "host_fuzz.cpp"),
-           str(src / "host_snap.cpp"), str(src / "host_stages.cpp"), str(src / "gcm_vaes.cpp"),
+           str(src / "host_snap.cpp"), str(src / "host_stages.cpp"), str(src / "host_stages_par.cpp"),
+           str(src / "gcm_vaes.cpp"),
            str(src / "file_container.cpp"), "-I" + str(ROOT / "include"), "-lcrypto", "-lpthread", "-o", str(exe)]
     subprocess.run(cmd, check=True, capture_output=True, timeout=300)
     return exe
