@@ -80,7 +80,7 @@ pub enum ChipError {
     NoDevice(String),
     #[error("HIP runtime error: {0}")]
     Device(String),
-    #[error("libcarbonado_hip has ABI {0}, this crate binds ABI 4")]
+    #[error("libcarbonado_hip has ABI {0}, this crate binds ABI {abi}", abi = ffi::CHIP_ABI_VERSION)]
     AbiMismatch(i32),
     #[error("status {0}: {1}")]
     Other(i32, String),

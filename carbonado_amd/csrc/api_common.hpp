@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -85,6 +86,7 @@ struct Ctx {
     int dev = -1;  // device the stream and buffers live on
     hipStream_t stream = nullptr;
     DevBuf in, mid, out, scratch, small, x1, x2, flags;
+    DevBuf hin, hout;  // pinned, NUMA-local: a single object's zero-copy input / outputs (api_single.cpp)
     std::vector<Slot> slots;
     Staging stage;
     // pinned arena for the few-byte copies of a call (hashes, status words,
@@ -103,6 +105,12 @@ struct Ctx {
 
 hipError_t grow(DevBuf &b, size_t bytes);         // grow-only device buffer (contents dropped)
 hipError_t grow_pinned(DevBuf &b, size_t bytes);  // the same, pinned host memory
+// pinned host memory on the GPU's NUMA node (api_host_copy.cpp), for buffers
+// the kernels read or write over PCIe themselves (zero-copy)
+hipError_t grow_pinned_local(DevBuf &b, size_t bytes, unsigned flags = hipHostMallocDefault);
+// allocation flags of the zero-copy INPUT buffer (CHIP_ZC_IN=default|wc|
+// coherent|noncoherent, A/B of the GPU's PCIe read rate from it)
+unsigned zc_in_flags();
 // the calling thread's context on the process's device (created on first use)
 int ctx_get(Ctx **out);
 // few-byte copies of a call through the context's pinned arena; `dst` of a
@@ -118,6 +126,21 @@ bool staged(const void *host, size_t n);  // pageable (or CHIP_HOST_COPY=staged)
 hipError_t h2d(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s);
 // HBM -> host after the work already on s; returns when `dst` holds the bytes
 hipError_t d2h(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s);
+// d2h in two halves: begin enqueues (the first ring pieces' DMA), end copies
+// out and returns when `dst` holds the bytes; the caller may work between
+// them (nothing else may use the ring meanwhile).
+struct D2h {
+    void *dst = nullptr;
+    const void *src = nullptr;
+    size_t n = 0;
+    hipStream_t s = nullptr;
+    size_t np = 0;
+    unsigned base = 0;
+    bool direct = false;
+};
+hipError_t d2h_begin(Staging &sg, D2h &t, void *dst, const void *src, size_t n, hipStream_t s);
+hipError_t d2h_issue(Staging &sg, const D2h &t, size_t j);
+hipError_t d2h_end(Staging &sg, const D2h &t);
 
 // Pitch of the device rows the library lays out itself (slot buffers): a
 // multiple of 256 B, so every row's shards start on a 128-B line.  With
@@ -176,6 +199,22 @@ int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const ui
                      const uint8_t *in, uint64_t n, uint8_t *dst, uint64_t cap, Scratch &tmp,
                      uint64_t *len, uint64_t *bc, uint64_t *be, const host::ChunkSink *sink = nullptr,
                      uint64_t *filled = nullptr, const host::EciesKey *prepared = nullptr, bool par = false);
+
+// ---- one object from host memory on KM (api_single.cpp) ---------------------
+// encode() at Zfec|Bao (C > 0: the zfec shard length) or bao of the content
+// (C == 0) of cur_n bytes at `cur` into out[0, final_len) and the root hash,
+// with the split copy-back: the host writes the stream's header and the chunks
+// it already holds (the content / data shards) while the device hashes; only
+// the parity region and the parent nodes cross PCIe.  km_ok() must hold.
+int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uint64_t final_len, uint8_t *out,
+                     uint8_t hash[32]);
+// decode of one bao stream `in` (len bytes, content n, every node verified on
+// the device by KM) with the content bytes [0, olen) gathered from `in` by the
+// host meanwhile, into dst; on a mismatch dst is wiped and the status
+// returned.  km_ok() must hold.
+// `meanwhile` (optional) runs on the host after the gather, before the wait.
+int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const uint8_t *hash, uint8_t *dst,
+                     uint64_t olen, const std::function<void()> &meanwhile = {});
 
 // K1 reads and writes 16-B vectors and its tail load relies on 16-B aligned
 // shard addresses (zfec_device.hpp load16_masked).

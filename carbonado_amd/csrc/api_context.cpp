@@ -63,6 +63,10 @@ void Ctx::release() {
     stage.release();
     if (hs.p) (void)hipHostFree(hs.p);
     hs = DevBuf{};
+    for (DevBuf *b : {&hin, &hout}) {
+        if (b->p) (void)hipHostFree(b->p);
+        *b = DevBuf{};
+    }
     hs_used = 0;
     hs_out.clear();
     // best effort (at process teardown the runtime may already be gone)

@@ -312,53 +312,70 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         Ctx *c;
         int st = ctx_get(&c);
         if (st != CHIP_OK) return st;
-        const uint64_t in_bytes = bao ? bao_encoded_len(blen) : n;
-        CHIP_HIP(grow(c->in, in_bytes));
-        if (in_bytes) CHIP_HIP(h2d(c->stage, c->in.p, in, in_bytes, c->stream));
-        const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
-        uint32_t verdict = 0;  // bao's, read at the synchronisation below
-        if (bao && zfec) {  // decoding.rs:89-99: the positional shares' primaries are the content's
-            // first 4 C bytes, so zfec's decode is the prefix: verify all, write olen bytes
-            CHIP_HIP(grow(c->mid, olen));
-            st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p), olen, &verdict);
+        if (bao && km_ok(blen, 1)) {  // KM verifies; the host gathers [0, olen) from `in` meanwhile
+            // (at Bao|Zfec the positional shares' primaries are the content's first 4 C bytes)
+            // while the device verifies, also the ECIES key from the envelope header as `in` holds it
+            auto prekey = [&] {
+                if (!ecies || !host::ecies_par_eligible(olen)) return;
+                const uint64_t h0 = bao_chunk_offset(0, (blen + 1023) / 1024);
+                if (h0 + 65 <= n && blen >= 65) {
+                    std::memcpy(pre_eph, in + h0, 65);
+                    have_pre = host::ecies_derive_key(secret_key, sk_len, pre_eph, pre_key) == CHIP_OK;
+                }
+            };
+            st = single_decode_km(c, in, n, blen, hash, dst, olen, prekey);
             if (st != CHIP_OK) return st;
-            d_cur = static_cast<const uint8_t *>(c->mid.p);
-        } else if (bao) {  // decoding.rs:89-93
-            CHIP_HIP(grow(c->mid, blen));
-            st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p), ~0ull, &verdict);
-            if (st != CHIP_OK) return st;
-            d_cur = static_cast<const uint8_t *>(c->mid.p);
-        }
-        if (zfec && !bao && C) {  // decoding.rs:95-99: shards by position, primaries present
-            CHIP_HIP(grow(c->out, CHIP_FEC_K * C));
-            std::vector<uint32_t> sel(CHIP_FEC_K);
-            std::vector<uint64_t> slot_off(CHIP_FEC_K);
-            for (uint32_t s = 0; s < CHIP_FEC_K; ++s) { sel[s] = s; slot_off[s] = s * C; }
-            st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_cur, 0, slot_off, sel, C, 1,
-                                    static_cast<uint8_t *>(c->out.p), 0, c->stream);
-            if (st != CHIP_OK) return st;
-            d_cur = static_cast<const uint8_t *>(c->out.p);
-        }
-        // While the device verifies: the ECIES key from the envelope header as the
-        // input holds it (content bytes [0, 65): chunk 0 of the bao stream, or the
-        // first shard); decrypt uses it only if the verified header is the same.
-        // Only for an envelope the pool path decrypts: the one-thread paths
-        // derive their own key, so a key derived here would be paid twice
-        if (ecies && host::ecies_par_eligible(olen)) {
-            const uint64_t h0 = bao ? bao_chunk_offset(0, (blen + 1023) / 1024) : 0;
-            if (h0 + 65 <= n && (!bao || blen >= 65)) {
-                std::memcpy(pre_eph, in + h0, 65);
-                have_pre = host::ecies_derive_key(secret_key, sk_len, pre_eph, pre_key) == CHIP_OK;
+            cur = dst;
+            cur_n = olen;
+        } else {
+            const uint64_t in_bytes = bao ? bao_encoded_len(blen) : n;
+            CHIP_HIP(grow(c->in, in_bytes));
+            if (in_bytes) CHIP_HIP(h2d(c->stage, c->in.p, in, in_bytes, c->stream));
+            const uint8_t *d_cur = static_cast<const uint8_t *>(c->in.p);
+            uint32_t verdict = 0;  // bao's, read at the synchronisation below
+            if (bao && zfec) {  // decoding.rs:89-99: the positional shares' primaries are the content's
+                // first 4 C bytes, so zfec's decode is the prefix: verify all, write olen bytes
+                CHIP_HIP(grow(c->mid, olen));
+                st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p), olen, &verdict);
+                if (st != CHIP_OK) return st;
+                d_cur = static_cast<const uint8_t *>(c->mid.p);
+            } else if (bao) {  // decoding.rs:89-93
+                CHIP_HIP(grow(c->mid, blen));
+                st = bao_decode_ctx(c, d_cur, in_bytes, blen, hash, static_cast<uint8_t *>(c->mid.p), ~0ull, &verdict);
+                if (st != CHIP_OK) return st;
+                d_cur = static_cast<const uint8_t *>(c->mid.p);
             }
+            if (zfec && !bao && C) {  // decoding.rs:95-99: shards by position, primaries present
+                CHIP_HIP(grow(c->out, CHIP_FEC_K * C));
+                std::vector<uint32_t> sel(CHIP_FEC_K);
+                std::vector<uint64_t> slot_off(CHIP_FEC_K);
+                for (uint32_t s = 0; s < CHIP_FEC_K; ++s) { sel[s] = s; slot_off[s] = s * C; }
+                st = zfec_decode_device(CHIP_FEC_K, CHIP_FEC_M, d_cur, 0, slot_off, sel, C, 1,
+                                        static_cast<uint8_t *>(c->out.p), 0, c->stream);
+                if (st != CHIP_OK) return st;
+                d_cur = static_cast<const uint8_t *>(c->out.p);
+            }
+            // While the device verifies: the ECIES key from the envelope header as the
+            // input holds it (content bytes [0, 65): chunk 0 of the bao stream, or the
+            // first shard); decrypt uses it only if the verified header is the same.
+            // Only for an envelope the pool path decrypts: the one-thread paths
+            // derive their own key, so a key derived here would be paid twice
+            if (ecies && host::ecies_par_eligible(olen)) {
+                const uint64_t h0 = bao ? bao_chunk_offset(0, (blen + 1023) / 1024) : 0;
+                if (h0 + 65 <= n && (!bao || blen >= 65)) {
+                    std::memcpy(pre_eph, in + h0, 65);
+                    have_pre = host::ecies_derive_key(secret_key, sk_len, pre_eph, pre_key) == CHIP_OK;
+                }
+            }
+            if (olen) CHIP_HIP(d2h(c->stage, dst, d_cur, olen, c->stream));
+            CHIP_HIP(small_sync(c));
+            if (verdict) {  // never hand back unverified content
+                if (olen) std::memset(dst, 0, olen);
+                return (int)verdict;
+            }
+            cur = dst;
+            cur_n = olen;
         }
-        if (olen) CHIP_HIP(d2h(c->stage, dst, d_cur, olen, c->stream));
-        CHIP_HIP(small_sync(c));
-        if (verdict) {  // never hand back unverified content
-            if (olen) std::memset(dst, 0, olen);
-            return (int)verdict;
-        }
-        cur = dst;
-        cur_n = olen;
     }
     if (!ecies && !snap) {
         if (!(zfec || bao)) {

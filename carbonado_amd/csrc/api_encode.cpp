@@ -44,6 +44,12 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
     if (!zfec && !bao) {
         if (cur_n) std::memcpy(out, cur, cur_n);
         std::memset(hash, 0, 32);
+    } else if (bao && km_ok(cur_len, 1)) {  // one object on KM, the split copy-back (api_single.cpp)
+        Ctx *c;
+        st = ctx_get(&c);
+        if (st != CHIP_OK) return st;
+        st = single_encode_km(c, cur, cur_n, zfec ? inf.chunk_len : 0, final_len, out, hash);
+        if (st != CHIP_OK) return st;
     } else {
         Ctx *c;
         st = ctx_get(&c);

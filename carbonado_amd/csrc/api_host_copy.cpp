@@ -27,6 +27,7 @@ namespace api {
 // 16-29 GiB/s between processes, r7i, with unpinned threads free to run on
 // either socket).  CHIP_NUMA=0 keeps the runtime's defaults (A/B).
 namespace topo {
+hipError_t host_alloc_on(void **p, size_t bytes, int node, unsigned flags = hipHostMallocDefault);
 
 bool numa_on() {
     static const bool on = [] {
@@ -123,15 +124,15 @@ int page_node(const void *p) {
 
 // hipHostMalloc with the pages placed on `node` (MPOL_PREFERRED for the call,
 // hipHostMallocNumaUser so the runtime follows it), the thread's policy restored
-hipError_t host_alloc_on(void **p, size_t bytes, int node) {
-    if (node < 0 || node >= 64 || !numa_on()) return hipHostMalloc(p, bytes, hipHostMallocDefault);
+hipError_t host_alloc_on(void **p, size_t bytes, int node, unsigned flags) {
+    if (node < 0 || node >= 64 || !numa_on()) return hipHostMalloc(p, bytes, flags);
     constexpr int MPOL_DEFAULT_ = 0, MPOL_PREFERRED_ = 1;
     int old_mode = MPOL_DEFAULT_;
     unsigned long old_mask[16] = {0};
     const bool saved = syscall(SYS_get_mempolicy, &old_mode, old_mask, 16 * 64UL, nullptr, 0UL) == 0;
     unsigned long mask = 1UL << node;
     const bool set = syscall(SYS_set_mempolicy, MPOL_PREFERRED_, &mask, 64UL + 1) == 0;
-    hipError_t e = hipHostMalloc(p, bytes, set ? (hipHostMallocDefault | hipHostMallocNumaUser) : hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(p, bytes, set ? (flags | hipHostMallocNumaUser) : flags);
     if (set) {
         if (saved) (void)syscall(SYS_set_mempolicy, old_mode, old_mode == MPOL_DEFAULT_ ? nullptr : old_mask, 16 * 64UL);
         else (void)syscall(SYS_set_mempolicy, MPOL_DEFAULT_, nullptr, 0UL);
@@ -294,6 +295,38 @@ class CopyPool {
     bool nt_ = false;
 };
 
+hipError_t grow_pinned_local(DevBuf &b, size_t bytes, unsigned flags) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipHostFree(b.p);
+        if (e != hipSuccess) return e;
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    const size_t cap = ((bytes + (bytes >> 3)) + 4095) & ~size_t(4095);
+    const int dev = g_device;
+    hipError_t e = topo::host_alloc_on(&b.p, cap, dev >= 0 ? topo::gpu(dev).node : -1, flags);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return e;
+    }
+    b.cap = cap;
+    return hipSuccess;
+}
+
+unsigned zc_in_flags() {
+    static const unsigned f = [] {
+        const char *v = std::getenv("CHIP_ZC_IN");
+        if (!v) return (unsigned)hipHostMallocDefault;
+        if (!std::strcmp(v, "wc")) return (unsigned)hipHostMallocWriteCombined;
+        if (!std::strcmp(v, "coherent")) return (unsigned)hipHostMallocCoherent;
+        if (!std::strcmp(v, "noncoherent")) return (unsigned)hipHostMallocNonCoherent;
+        return (unsigned)hipHostMallocDefault;
+    }();
+    return f;
+}
+
 hipError_t stage_slot(Staging &sg, int k) {  // wait until ring slot k is free
     if (!sg.armed[k]) return hipSuccess;
     sg.armed[k] = false;
@@ -332,40 +365,57 @@ hipError_t h2d(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s)
     return e;
 }
 
-// HBM -> host after the work already on s; returns when `dst` holds the bytes.
-hipError_t d2h(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s) {
+// HBM -> host after the work already on s, in two halves so the caller can
+// work between them: d2h_begin enqueues the first ring pieces' DMA, d2h_end
+// copies every piece out (enqueuing the rest as ring slots free up) and
+// returns when `dst` holds the bytes.
+hipError_t d2h_begin(Staging &sg, D2h &t, void *dst, const void *src, size_t n, hipStream_t s) {
+    t = D2h{dst, src, n, s, 0, 0, false};
     if (!n) return hipSuccess;
     if (!staged(dst, n)) {
-        hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
-        return e == hipSuccess ? hipStreamSynchronize(s) : e;
+        t.direct = true;
+        return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
     }
     hipError_t e = stage_init(sg);
     if (e != hipSuccess) return e;
-    const size_t np = (n + Staging::PIECE - 1) / Staging::PIECE;
-    const unsigned base = sg.next;
-    sg.next += (unsigned)np;
-    auto slot = [&](size_t j) { return (int)((base + j) % Staging::R); };
-    auto issue = [&](size_t j) {
-        const int k = slot(j);
-        hipError_t r = stage_slot(sg, k);
-        const size_t off = j * Staging::PIECE;
-        if (r == hipSuccess)
-            r = hipMemcpyAsync(sg.ring + k * Staging::PIECE, static_cast<const uint8_t *>(src) + off,
-                               std::min(Staging::PIECE, n - off), hipMemcpyDeviceToHost, s);
-        if (r == hipSuccess) r = hipEventRecord(sg.ev[k], s);
-        if (r == hipSuccess) sg.armed[k] = true;
-        return r;
-    };
-    for (size_t j = 0; j < np && j < (size_t)Staging::R && e == hipSuccess; ++j) e = issue(j);
-    for (size_t j = 0; j < np && e == hipSuccess; ++j) {
-        const int k = slot(j);
+    t.np = (n + Staging::PIECE - 1) / Staging::PIECE;
+    t.base = sg.next;
+    sg.next += (unsigned)t.np;
+    for (size_t j = 0; j < t.np && j < (size_t)Staging::R && e == hipSuccess; ++j) e = d2h_issue(sg, t, j);
+    return e;
+}
+
+hipError_t d2h_issue(Staging &sg, const D2h &t, size_t j) {
+    const int k = (int)((t.base + j) % Staging::R);
+    hipError_t r = stage_slot(sg, k);
+    const size_t off = j * Staging::PIECE;
+    if (r == hipSuccess)
+        r = hipMemcpyAsync(sg.ring + k * Staging::PIECE, static_cast<const uint8_t *>(t.src) + off,
+                           std::min(Staging::PIECE, t.n - off), hipMemcpyDeviceToHost, t.s);
+    if (r == hipSuccess) r = hipEventRecord(sg.ev[k], t.s);
+    if (r == hipSuccess) sg.armed[k] = true;
+    return r;
+}
+
+hipError_t d2h_end(Staging &sg, const D2h &t) {
+    if (!t.n) return hipSuccess;
+    if (t.direct) return hipStreamSynchronize(t.s);
+    hipError_t e = hipSuccess;
+    for (size_t j = 0; j < t.np && e == hipSuccess; ++j) {
+        const int k = (int)((t.base + j) % Staging::R);
         if ((e = stage_slot(sg, k)) != hipSuccess) break;
         const size_t off = j * Staging::PIECE;
-        CopyPool::get().copy(static_cast<uint8_t *>(dst) + off, sg.ring + k * Staging::PIECE,
-                             std::min(Staging::PIECE, n - off));
-        if (j + Staging::R < np) e = issue(j + Staging::R);
+        CopyPool::get().copy(static_cast<uint8_t *>(t.dst) + off, sg.ring + k * Staging::PIECE,
+                             std::min(Staging::PIECE, t.n - off));
+        if (j + Staging::R < t.np) e = d2h_issue(sg, t, j + Staging::R);
     }
     return e;
+}
+
+hipError_t d2h(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s) {
+    D2h t;
+    hipError_t e = d2h_begin(sg, t, dst, src, n, s);
+    return e == hipSuccess ? d2h_end(sg, t) : e;
 }
 
 }  // namespace api

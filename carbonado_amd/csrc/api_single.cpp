@@ -1,0 +1,216 @@
+// api_single.cpp — one object from host memory on KM (multi_kernels.hip):
+// encode() at Zfec|Bao or Bao and decode() of a bao stream, for latency.
+//
+// A single object's call was the kernel's own 65-115 us (K13: 32 waves for
+// a 1 MiB object) and PCIe for every stream byte both ways (profiles/
+// r10zm_session, r11a).  Here the device runs KM (a quad of lanes per
+// compression, all CUs), and the copies move only what the host cannot make:
+//
+//  * zero-copy: the host copies the input (or the stream to verify) into
+//    pinned memory on the GPU's NUMA node on a few threads, and the kernels
+//    read it over PCIe themselves and write their outputs there.  No DMA and
+//    no copy-engine handoff sits on the critical path (each cost ~10-14 us
+//    besides the transfer, profiles/r11c_session), and the transfer overlaps
+//    the hashing.
+//  * encode: the host writes the stream's header and the chunks it already
+//    holds (the content, or the data shards = the zero-padded input) into the
+//    caller's buffer while the device hashes; only the parity region [t0,
+//    end) and the parent nodes in front of t0 (KM writes those compactly)
+//    come back.  At level 12 that is 1.13 of the stream's 2.2 MB per 1 MiB;
+//    for bao of the content only the nodes (1/16 of the content).
+//  * decode: every stream byte goes up (all of it is hashed), and the content
+//    the caller gets is gathered from the caller's own input by the host while
+//    the device verifies; only the verdict comes back, and the gathered bytes
+//    are wiped if it is a mismatch.
+#include "api_common.hpp"
+
+#include <chrono>
+#include <map>
+#include <mutex>
+
+namespace chip {
+namespace api {
+
+namespace {
+
+// The host-made part of a stream of N chunks whose first `nh` chunks the host
+// holds: their slots, the parent-node runs between them (dst: stream offset,
+// src: offset in KM's compact node buffer) and the end t0 of that region.
+struct HostGeo {
+    uint64_t N = 0, nh = 0, zl = 0, t0 = 8, nbytes = 0;  // nbytes: compact node bytes
+    std::vector<uint64_t> coff;
+    struct Run {
+        uint64_t dst, src, len;
+    };
+    std::vector<Run> runs;
+};
+
+const HostGeo &host_geo(uint64_t zl, uint64_t nh) {
+    thread_local std::map<std::pair<uint64_t, uint64_t>, HostGeo> cache;
+    auto key = std::make_pair(zl, nh);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    if (cache.size() >= 8) cache.clear();
+    HostGeo g;
+    g.zl = zl;
+    g.N = n_chunks_of(zl);
+    g.nh = nh;
+    g.coff.resize(nh);
+    uint64_t prev_end = 8, src = 0;
+    for (uint64_t i = 0; i < nh; ++i) {
+        g.coff[i] = bao_chunk_offset(i, g.N);
+        if (g.coff[i] > prev_end) {
+            g.runs.push_back({prev_end, src, g.coff[i] - prev_end});
+            src += g.coff[i] - prev_end;
+        }
+        prev_end = g.coff[i] + std::min<uint64_t>(1024, zl - 1024 * i);
+    }
+    g.t0 = prev_end;
+    g.nbytes = src;
+    return cache.emplace(key, std::move(g)).first->second;
+}
+
+// host copy threads for nc chunks: one per 128 KiB, at most 8
+int host_parts(uint64_t nc) { return (int)std::max<uint64_t>(1, std::min<uint64_t>(8, nc / 128)); }
+
+// CHIP_SINGLE_TRACE=1: the host-side phases of each call to stderr (us)
+struct Trace {
+    const char *what;
+    bool on;
+    std::chrono::steady_clock::time_point t0, last;
+    explicit Trace(const char *w) : what(w), on(enabled()) {
+        if (on) t0 = last = std::chrono::steady_clock::now();
+    }
+    static bool enabled() {
+        static const bool e = [] {
+            const char *v = std::getenv("CHIP_SINGLE_TRACE");
+            return v && v[0] == '1';
+        }();
+        return e;
+    }
+    void mark(const char *phase) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[single %s] %-12s +%7.1f us (%7.1f)\n", what, phase,
+                     std::chrono::duration<double, std::micro>(now - last).count(),
+                     std::chrono::duration<double, std::micro>(now - t0).count());
+        last = now;
+    }
+};
+
+}  // namespace
+
+namespace {
+
+// a pinned host allocation as the device addresses it
+template <class T>
+T *dev_ptr(void *host) {
+    void *d = nullptr;
+    return hipHostGetDevicePointer(&d, host, 0) == hipSuccess ? static_cast<T *>(d) : static_cast<T *>(host);
+}
+
+// n bytes into pinned memory on a few threads (streaming stores: only the
+// device reads them next)
+void copy_in(uint8_t *dst, const uint8_t *src, uint64_t n) {
+    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, n >> 18));  // 256 KiB a thread
+    host::par_for(parts, [&](int i) {
+        const uint64_t a = (n * i / parts) & ~uint64_t(63), b = i + 1 == parts ? n : (n * (i + 1) / parts) & ~uint64_t(63);
+        host::ring_copy(dst + a, src + a, b - a);
+    });
+}
+
+void copy_out(uint8_t *dst, const uint8_t *src, uint64_t n) {
+    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, n >> 18));
+    host::par_for(parts, [&](int i) {
+        const uint64_t a = n * i / parts, b = n * (i + 1) / parts;
+        std::memcpy(dst + a, src + a, b - a);
+    });
+}
+
+}  // namespace
+
+int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uint64_t final_len, uint8_t *out,
+                     uint8_t hash[32]) {
+    const bool zfec = C > 0;
+    const uint64_t zl = zfec ? (uint64_t)CHIP_FEC_M * C : cur_n;
+    const uint64_t N = n_chunks_of(zl), nh = zfec ? N / 2 : N;
+    const HostGeo &g = host_geo(zl, nh);
+    // pinned outputs: [the stream image from t0][the compact nodes][the hash]
+    const uint64_t tail_len = final_len - g.t0, nodes_at = (tail_len + 63) & ~uint64_t(63);
+    const uint64_t hash_at = (nodes_at + g.nbytes + 63) & ~uint64_t(63);
+    Trace trace("encode");
+    CHIP_HIP(grow_pinned_local(c->hin, cur_n + 16, zc_in_flags()));  // the kernels' 16-B source loads stay inside
+    CHIP_HIP(grow_pinned_local(c->hout, hash_at + 64));
+    if (zfec) CHIP_HIP(grow(c->out, final_len));
+    CHIP_HIP(grow(c->scratch, km_scratch_len(zl)));
+    uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
+    copy_in(hin, cur, cur_n);
+    trace.mark("copy in");
+    const uint8_t *d_in = dev_ptr<const uint8_t>(hin);
+    uint8_t *d_out = dev_ptr<uint8_t>(hout);
+    if (zfec)
+        CHIP_HIP(km_zfec_bao_dev(d_in, cur_n, C, static_cast<uint8_t *>(c->out.p), d_out + nodes_at, d_out, g.t0,
+                                 d_out + hash_at, c->scratch.p, c->stream));
+    else
+        CHIP_HIP(km_bao_encode_dev(d_in, cur_n, d_out + nodes_at, d_out + hash_at, c->scratch.p, c->stream));
+    trace.mark("launch");
+    // meanwhile: the header and the chunks the host holds, on a few threads
+    for (int b = 0; b < 8; ++b) out[b] = static_cast<uint8_t>(zl >> (8 * b));
+    const int parts = host_parts(nh);
+    host::par_for(parts, [&](int i) {
+        const uint64_t a = nh * i / parts, b = nh * (i + 1) / parts;
+        if (zfec) host::fill_chunk_range(out, g.coff.data(), a, b, cur, cur_n);
+        else host::gather_chunks_to_slots(out, g.coff.data() + a, cur + 1024 * a, std::min(cur_n, 1024 * b) - 1024 * a);
+    });
+    trace.mark("host chunks");
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    trace.mark("sync");
+    if (tail_len) copy_out(out + g.t0, hout, tail_len);
+    for (const HostGeo::Run &r : g.runs) std::memcpy(out + r.dst, hout + nodes_at + r.src, r.len);
+    std::memcpy(hash, hout + hash_at, 32);
+    trace.mark("copy out");
+    return CHIP_OK;
+}
+
+int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const uint8_t *hash, uint8_t *dst,
+                     uint64_t olen, const std::function<void()> &meanwhile) {
+    const uint64_t blen = bao_encoded_len(n);
+    if (blen > len) return CHIP_ERR_BAO_TRUNCATED;
+    // pinned: [the expected hash][the status word][the stream at 64]
+    CHIP_HIP(grow_pinned_local(c->hin, 64 + blen, zc_in_flags()));
+    CHIP_HIP(grow(c->scratch, km_scratch_len(n)));
+    uint8_t *hin = static_cast<uint8_t *>(c->hin.p);
+    Trace trace("decode");
+    std::memcpy(hin, hash, 32);
+    volatile uint32_t *status = reinterpret_cast<volatile uint32_t *>(hin + 32);
+    *status = 0;
+    copy_in(hin + 64, in, blen);
+    trace.mark("copy in");
+    uint8_t *d = dev_ptr<uint8_t>(hin);
+    CHIP_HIP(km_bao_decode_dev(d + 64, n, d, nullptr, 0, reinterpret_cast<uint32_t *>(d + 32), c->scratch.p,
+                               c->stream));
+    trace.mark("launch");
+    // meanwhile: the content from the caller's own copy of the stream
+    if (olen) {
+        const uint64_t nc = (olen + 1023) / 1024;
+        const HostGeo &g = host_geo(n, nc);
+        const int parts = host_parts(nc);
+        host::par_for(parts, [&](int i) {
+            const uint64_t a = nc * i / parts, b = nc * (i + 1) / parts;
+            host::gather_chunks(dst + 1024 * a, in, g.coff.data() + a, std::min(olen, 1024 * b) - 1024 * a);
+        });
+    }
+    trace.mark("host gather");
+    if (meanwhile) meanwhile();
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    trace.mark("sync");
+    const uint32_t verdict = *status;
+    if (verdict) {  // never hand back unverified content
+        if (olen) std::memset(dst, 0, olen);
+        return (int)verdict;
+    }
+    return CHIP_OK;
+}
+
+}  // namespace api
+}  // namespace chip

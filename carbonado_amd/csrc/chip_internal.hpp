@@ -77,6 +77,7 @@ hipError_t zfec_parity_table(uint32_t k, uint32_t m, const void **out);
 // QUEUE_K13, K3 from word QUEUE_K3 (two counters 32 words apart each).
 constexpr int QUEUE_K13 = 512;
 constexpr int QUEUE_K3 = 640;
+constexpr int QUEUE_KM = 768;  // KM's last-workgroup counter
 hipError_t stream_queue(hipStream_t stream, uint32_t **out);
 // Return a stream's block to the pool; call once the stream's work is done,
 // before the stream is destroyed (a later stream may get the same handle).
@@ -183,6 +184,33 @@ hipError_t small_zfec_bao_dev(const uint8_t *d_in, uint64_t in_stride, uint64_t 
 hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t in_stride, uint64_t n, uint64_t count,
                                 const uint8_t *d_hash, uint8_t *d_out, uint64_t out_stride, uint64_t out_limit,
                                 uint32_t *d_status, hipStream_t stream);
+
+// ---- KM: one single object over many workgroups (multi_kernels.hip) ----
+// Latency path for count == 1 and a bao stream of KS_TINY_N < N <= KM_MAX_N
+// chunks: a quad of lanes per compression, a 64-chunk subtree per workgroup,
+// the last workgroup to finish walks the tree top (CHIP_KM=0 turns it off).
+// Scratch: km_scratch_len(bao_n) bytes (the group CVs).
+constexpr uint64_t KM_MAX_N = 32768;
+bool km_ok(uint64_t bao_n, uint64_t count);
+uint64_t km_scratch_len(uint64_t bao_n);
+// bao of n content bytes at d_in (device or pinned host memory): the parent
+// nodes compactly into d_nodes (the node at stream offset o in front of chunk
+// s goes to o - 8 - 1024 s; null: none), the root hash to d_hash.
+hipError_t km_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_nodes, uint8_t *d_hash, void *d_scratch,
+                             hipStream_t stream);
+// encode() at Zfec|Bao of `valid` input bytes at d_in (16-B aligned, zero
+// padded to 4 C by the masked loads): the 8 shards into the chunk slots of
+// d_stream (device), the parity shards and the nodes past the data region
+// also into d_tail = the stream's image from byte t0 (null: none), the nodes
+// of the data region (chunks [0, 4 C / 1024)) compactly into d_nodes as
+// above, the hash.
+hipError_t km_zfec_bao_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint8_t *d_stream, uint8_t *d_nodes,
+                           uint8_t *d_tail, uint64_t t0, uint8_t *d_hash, void *d_scratch, hipStream_t stream);
+// verify-decode one stream of n content bytes; content [0, out_limit) to
+// d_out (null: verify only); d_status (zero at launch) = 0 or
+// CHIP_ERR_BAO_HASH_MISMATCH.
+hipError_t km_bao_decode_dev(const uint8_t *d_stream, uint64_t n, const uint8_t *d_hash, uint8_t *d_out,
+                             uint64_t out_limit, uint32_t *d_status, void *d_scratch, hipStream_t stream);
 
 // ---- batch buffers (hbm_alloc.hip) --------------------------------------
 // Class-balanced device memory for buffers >= 1 GiB (hbm_alloc.hpp); returns

@@ -796,5 +796,10 @@ void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint6
         std::memcpy(dst + 1024 * i, row + coff[i], (size_t)std::min<uint64_t>(1024, n - 1024 * i));
 }
 
+void gather_chunks_to_slots(uint8_t *row, const uint64_t *coff, const uint8_t *src, uint64_t n) {
+    for (uint64_t i = 0; 1024 * i < n; ++i)
+        std::memcpy(row + coff[i], src + 1024 * i, (size_t)std::min<uint64_t>(1024, n - 1024 * i));
+}
+
 }  // namespace host
 }  // namespace chip

@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 
 namespace chip {
 namespace host {
@@ -143,11 +144,17 @@ int ecies_decrypt_par(const uint8_t *secret, uint64_t secret_len, const uint8_t 
 // the key ahead (ecies_derive_key) does so only then: the one-thread paths
 // derive their own.
 bool ecies_par_eligible(uint64_t n);
+// f(0) .. f(parts - 1) on the stage pool's threads and the caller, claimed
+// one at a time (the caller alone when the pool is busy or single-threaded);
+// returns when all are done.  For one object's host copies (api_single.cpp).
+void par_for(int parts, const std::function<void(int)> &f);
 // The AES key of an envelope whose ephemeral public key (65 B) is eph.
 int ecies_derive_key(const uint8_t *secret, uint64_t secret_len, const uint8_t eph[65], uint8_t key[32]);
 void secure_wipe(void *p, size_t n);
 // the first n bytes of a stream's content from its chunk slots row + coff[i]
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n);
+// the reverse: content bytes [0, n) of src into their chunk slots row + coff[i]
+void gather_chunks_to_slots(uint8_t *row, const uint64_t *coff, const uint8_t *src, uint64_t n);
 
 }  // namespace host
 }  // namespace chip

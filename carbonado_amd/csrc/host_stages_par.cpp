@@ -278,6 +278,22 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
     return CHIP_OK;
 }
 
+void par_for(int parts, const std::function<void(int)> &f) {
+    StagePool &pool = StagePool::get();
+    if (parts <= 1 || !pool.try_acquire()) {
+        for (int i = 0; i < parts; ++i) f(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    auto run = [&](int) {
+        for (int i; (i = next.fetch_add(1, std::memory_order_relaxed)) < parts;) f(i);
+    };
+    pool.start(run);
+    run(0);
+    pool.wait();
+    pool.release();
+}
+
 bool ecies_par_eligible(uint64_t n) {
     return n >= ECIES_OVERHEAD + STAGE_PAR_MIN && n - ECIES_OVERHEAD <= GCM_MAX_BYTES && gcm_vaes_on();
 }

@@ -1,0 +1,374 @@
+// multi_kernels.hip — KM: one single object's bao stream over many
+// workgroups, for latency (gfx950).
+//
+// A single object's encode()/decode() is the reference's real unit (segments
+// of at most ~1 MB, README.md:107-111).  Of the two paths before KM, K13 /
+// K3 give one lane a whole 1 KiB chunk (16 dependent compressions of ~700
+// VALU): a 1 MiB object at Zfec|Bao is 2048 lanes = 32 waves on a 1024-SIMD
+// chip, 65-115 us of kernel, and its tree top another 15-23 us launch
+// (profiles/r10zm_session, r11a); KS (small_kernels.hip) puts a quad of lanes
+// on each compression but one workgroup on the object, so it stops at 512
+// chunks.  KM is KS spread over the chip:
+//
+//  * workgroup g (256 threads = 64 quads) owns the aligned group of 64 chunks
+//    [64 g, 64 g + 64): one quad per chunk computes its CV (four lanes per
+//    compression, quad_b3.hpp), then the group's own parent levels 1-6 (its
+//    subtree; the pairing with the odd last node promoted is bao's
+//    left-balanced tree, and group boundaries are aligned at every level <= 6)
+//    are hashed from LDS and stored (encode) or compared with the stored nodes
+//    (decode);
+//  * each group's level-6 CV goes to global scratch; the workgroup that
+//    finishes last (an agent-scope counter, released / acquired with fences:
+//    the eight XCDs' L2s are not coherent without them) walks levels 7 ..
+//    root over the G group CVs in LDS, four lanes per parent, and writes the
+//    root hash (encode) or checks it against the expected one (decode).  It
+//    resets the counter for the stream's next launch.
+//
+// Chunk bytes come from a contiguous source for chunks below `n_in` (bao of
+// the content: the content itself) and from the stream's chunk slots above it
+// (Zfec|Bao: every shard, written by km_parity_kernel; decode: the stream).
+// For a single call from host memory (api_single.cpp) the source, the stream
+// to verify, the expected hash and every output live in pinned host memory:
+// the kernels read and write them over PCIe themselves (zero-copy), so no
+// DMA hop and no copy-engine-to-kernel handoff (~10-14 us each, r11c) sits
+// on the call's critical path.  Encode writes the parent nodes in front of
+// the first `nd` chunks compactly (`nodes`) and the rest into the stream's
+// image from t0 on (`tail`); the host writes the chunks it holds itself.
+#include "bao_device.hpp"
+#include "chip_internal.hpp"
+#include "quad_b3.hpp"
+#include "zfec_device.hpp"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace chip {
+
+using namespace bao;
+
+namespace multi {
+
+constexpr int TPB = 256, S = TPB / 4, LOGS = 6;  // 64 chunks (one per quad) per workgroup
+static_assert((1 << LOGS) == S, "group = 2^LOGS chunks");
+constexpr int GMAX = (int)(KM_MAX_N / S);  // groups the last workgroup's walk holds in LDS
+
+struct MultiArgs {
+    const uint8_t *src;    // chunks [0, n_in): contiguous source (zero past `valid`)
+    const uint8_t *stream; // chunks [n_in, N) in their slots; decode: the whole stream (nodes too)
+    uint8_t *out;          // decode: content bytes [0, out_limit) (null: verify only)
+    uint8_t *nodes;        // encode: compact copy of the nodes in front of chunks [0, nd) (null: none)
+    uint8_t *tail;         // encode: the stream image from byte t0 on, the other nodes land there (null: none)
+    uint64_t t0;
+    uint64_t n, N;         // bao content bytes and chunks
+    uint64_t n_in, valid;  // source chunks, source bytes
+    uint64_t nd, out_limit;
+    uint8_t *hash;         // encode: root hash out; decode: expected
+    uint32_t *status;      // decode: 0 or CHIP_ERR_BAO_HASH_MISMATCH (zero at launch)
+    uint8_t *gcv;          // [G][32] group CVs
+    uint32_t *counter;     // zero at launch; the last workgroup resets it
+};
+
+// the 64-B node (l || r) of parent P at `level`: my 16 B are words 4q .. 4q+3
+__device__ __forceinline__ void node_out(const MultiArgs &a, uint64_t P, int level, int q, u32x4 mw) {
+    const uint64_t s = P << level, off = parent_stream_off(s, level, a.N);
+    if (s < a.nd) {
+        if (a.nodes) store16_a8<false>(a.nodes + (off - 8 - 1024 * s) + 16 * q, mw);
+    } else if (a.tail) {
+        store16_a8<false>(a.tail + (off - a.t0) + 16 * q, mw);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(TPB) void km_kernel(MultiArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t cvs[2][GMAX][8];  // a level and the next
+    __shared__ __attribute__((aligned(16))) uint32_t msg[S][16];       // each quad's message block
+    __shared__ uint32_t last;
+    __shared__ __attribute__((aligned(16))) u32x4 stored[MODE == 1 ? GMAX * 4 : 4];  // decode: the top's nodes
+    const int t = threadIdx.x, q = t & 3, g = t >> 2;
+    const uint64_t grp = blockIdx.x, G = gridDim.x, N = a.N, n = a.n;
+    const uint64_t c0 = grp * S, r = N - c0 < (uint64_t)S ? N - c0 : (uint64_t)S;  // my chunks
+    bool ok = true;
+
+    // ---- phase 1 (decode): the header checked, content bytes out
+    if (MODE == 1) {
+        if (grp == 0 && t == 0 && *reinterpret_cast<const uint64_t *>(a.stream) != n) ok = false;
+        const uint64_t lim = a.out ? (a.out_limit < (c0 + r) * 1024 ? a.out_limit : (c0 + r) * 1024) : 0;
+        for (uint64_t o = c0 * 1024 + 16 * (uint64_t)t; o < lim; o += 16 * TPB) {
+            const uint8_t *p = a.stream + chunk_stream_off(o / 1024, N) + o % 1024;
+            const uint64_t left = lim - o;
+            if (left >= 16) *glb(reinterpret_cast<u32x4 *>(a.out + o)) = load16_a8(p);
+            else store16_partial(a.out + o, load16_partial(p, (uint32_t)left), (uint32_t)left);
+        }
+    }
+
+    // ---- phase 2: chunk CVs, one quad per chunk
+    const uint32_t slot = (uint32_t)(reinterpret_cast<uintptr_t>(&msg[g][0]) - reinterpret_cast<uintptr_t>(&msg[0][0]));
+    const uint8_t *mbase = reinterpret_cast<const uint8_t *>(&msg[0][0]);
+    const small::MsgIdx mi(q, slot);
+    const uint32_t iv0 = q == 0 ? IV(0) : q == 1 ? IV(1) : q == 2 ? IV(2) : IV(3);
+    const uint32_t iv1 = q == 0 ? IV(4) : q == 1 ? IV(5) : q == 2 ? IV(6) : IV(7);
+    u32x4 stn[LOGS];  // decode: stored nodes (a zero-copy stream costs a PCIe round trip per load)
+    if ((uint64_t)g < r) {
+        const uint64_t c = c0 + g;
+        const uint64_t rem = n - c * 1024;
+        const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+        const uint32_t nb = (clen + 63) / 64;  // N >= 2: every chunk holds at least one byte
+        const bool from_src = c < a.n_in;
+        const uint8_t *cp = a.stream + chunk_stream_off(c, N);
+        if (MODE == 1) {  // the stored nodes this quad checks at levels 1 .. LOGS, in flight with the chunk
+            uint64_t cp_ = r;
+#pragma unroll
+            for (int l = 1; l <= LOGS; ++l) {
+                const uint64_t cn = (cp_ + 1) / 2;
+                if ((uint64_t)g < cn && 2 * (uint64_t)g + 1 < cp_)
+                    stn[l - 1] = load16_a8(a.stream + parent_stream_off(((c0 >> l) + g) << l, l, N) + 16 * q);
+                cp_ = cn;
+            }
+        }
+        u32x4 pc[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {  // my 16 B of every block of the chunk, all loads in flight
+            const uint32_t off = 64 * b + 16 * q;
+            if (off >= clen) pc[b] = u32x4{0u, 0u, 0u, 0u};
+            else if (from_src) pc[b] = zf::load16_masked(a.src, c * 1024 + off, a.valid);
+            else pc[b] = off + 16 <= clen ? load16_a8(cp + off) : small::load16_bytes(cp + off, clen - off);
+        }
+        uint32_t h0 = iv0, h1 = iv1;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            if ((uint32_t)b < nb) {
+                *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = pc[b];
+                wave_sync();
+                const bool lastb = (uint32_t)b + 1 == nb;
+                const uint32_t flags = (b == 0 ? F_CHUNK_START : 0u) | (lastb ? F_CHUNK_END : 0u);
+                small::compress4(h0, h1, mbase, mi, q, iv0, c, lastb ? clen - 64 * b : 64u, flags);
+                wave_sync();
+            }
+        }
+        cvs[0][g][q] = h0;
+        cvs[0][g][4 + q] = h1;
+    }
+    __syncthreads();
+
+    // ---- phase 3: the group's levels 1 .. LOGS, one quad per parent
+    int cur = 0;
+    uint64_t cnt_prev = r;
+    for (int level = 1; level <= LOGS && cnt_prev > 1; ++level) {
+        const uint64_t cnt = (cnt_prev + 1) / 2;
+        if ((uint64_t)g < cnt) {
+            const uint64_t p = g;
+            if (2 * p + 1 >= cnt_prev) {  // odd last node: promoted unchanged
+                cvs[cur ^ 1][p][q] = cvs[cur][2 * p][q];
+                cvs[cur ^ 1][p][4 + q] = cvs[cur][2 * p][4 + q];
+            } else {
+                const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cvs[cur][2 * p + (q >> 1)][4 * (q & 1)]);
+                *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = mw;
+                wave_sync();
+                uint32_t h0 = iv0, h1 = iv1;
+                small::compress4(h0, h1, mbase, mi, q, iv0, 0, 64, F_PARENT);
+                wave_sync();
+                const uint64_t P = (c0 >> level) + p;
+                if (MODE == 0) {
+                    node_out(a, P, level, q, mw);
+                } else {
+                    u32x4 s = stn[0];
+#pragma unroll
+                    for (int l = 2; l <= LOGS; ++l)
+                        if (level == l) s = stn[l - 1];
+                    ok &= s.x == mw.x && s.y == mw.y && s.z == mw.z && s.w == mw.w;
+                }
+                cvs[cur ^ 1][p][q] = h0;
+                cvs[cur ^ 1][p][4 + q] = h1;
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        cnt_prev = cnt;
+    }
+    if (MODE == 1 && !ok) flag_mismatch(a.status, 0);
+
+    // ---- phase 4: publish the group CV; the last workgroup walks the top
+    if (t < 8) *glb(reinterpret_cast<uint32_t *>(a.gcv + grp * 32) + t) = cvs[cur][0][t];
+    __syncthreads();
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // my group CV (and nodes) before the count
+        const uint32_t done = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = done + 1 == (uint32_t)G;
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every group's CV visible to every lane
+    for (uint64_t i = t; i < 8 * G; i += TPB)
+        cvs[0][i >> 3][i & 7] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(a.gcv) + i, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MODE == 1) {  // level by level: pairs floor(cnt / 2), 16 B per lane of a quad
+        uint64_t cnt = G, base = 0;
+        for (int level = LOGS + 1; cnt > 1; ++level) {
+            const uint64_t pairs = cnt / 2;
+            for (uint64_t i = t; i < 4 * pairs; i += TPB)
+                stored[4 * base + i] = load16_a8(a.stream + parent_stream_off((i >> 2) << level, level, N) + 16 * (i & 3));
+            base += pairs;
+            cnt = (cnt + 1) / 2;
+        }
+    }
+    __syncthreads();
+    uint64_t nbase = 0;  // decode: index of this level's first node in `stored`
+    cur = 0;
+    cnt_prev = G;
+    ok = true;
+    for (int level = LOGS + 1; cnt_prev > 1; ++level) {
+        const uint64_t cnt = (cnt_prev + 1) / 2;
+        for (uint64_t p = g; p < cnt; p += S) {
+            if (2 * p + 1 >= cnt_prev) {
+                cvs[cur ^ 1][p][q] = cvs[cur][2 * p][q];
+                cvs[cur ^ 1][p][4 + q] = cvs[cur][2 * p][4 + q];
+                continue;
+            }
+            const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cvs[cur][2 * p + (q >> 1)][4 * (q & 1)]);
+            *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = mw;
+            wave_sync();
+            const bool root = cnt == 1;
+            uint32_t h0 = iv0, h1 = iv1;
+            small::compress4(h0, h1, mbase, mi, q, iv0, 0, 64, F_PARENT | (root ? F_ROOT : 0u));
+            wave_sync();
+            if (MODE == 0) {
+                node_out(a, p, level, q, mw);
+            } else {
+                const u32x4 s = stored[4 * (nbase + p) + q];
+                ok &= s.x == mw.x && s.y == mw.y && s.z == mw.z && s.w == mw.w;
+            }
+            if (root) {
+                uint32_t *hp = reinterpret_cast<uint32_t *>(a.hash);
+                if (MODE == 0) {
+                    hp[q] = h0;
+                    hp[4 + q] = h1;
+                } else {
+                    ok &= hp[q] == h0 && hp[4 + q] == h1;
+                }
+            } else {
+                cvs[cur ^ 1][p][q] = h0;
+                cvs[cur ^ 1][p][4 + q] = h1;
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        nbase += cnt_prev / 2;
+        cnt_prev = cnt;
+    }
+    if (MODE == 1 && !ok) flag_mismatch(a.status, 0);
+}
+
+// A 4-of-8 zfec encode into the chunk slots of the Zfec|Bao stream: one 16-B
+// position of every shard per lane, the packed parity table ([4][256] dwords:
+// byte d of entry [j][x] = E[4 + d][j] * x) in LDS.  The input is read once
+// (from pinned host memory for a single call: zero-copy, no DMA hop); the
+// data and parity shards go to the device stream's slots for KM to hash, and
+// the parity shards also to the host-visible image of the stream from t0 on
+// (`tail`, null: none), which is everything of the stream past the data
+// region except its nodes.
+__global__ __launch_bounds__(256) void km_parity_kernel(const uint8_t *in, uint64_t valid, uint64_t C, uint8_t *stream,
+                                                        uint64_t N, const uint32_t *table, uint8_t *tail,
+                                                        uint64_t t0) {
+    __shared__ uint32_t tab[4 * 256];
+    for (int i = threadIdx.x; i < 4 * 256; i += 256) tab[i] = table[i];
+    const uint64_t o = 16 * ((uint64_t)blockIdx.x * 256 + threadIdx.x);
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = o < C ? zf::load16_masked(in, j * C + o, valid) : u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    if (o >= C) return;
+    u32x4 p[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t acc[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x ^= tab[j * 256 + ((zf::comp(v[j], d) >> (8 * b)) & 0xFFu)];
+            acc[b] = x;
+        }
+        uint32_t r0, r1, r2, r3;
+        zf::transpose4(acc[0], acc[1], acc[2], acc[3], r0, r1, r2, r3);
+        if (d == 0) { p[0].x = r0; p[1].x = r1; p[2].x = r2; p[3].x = r3; }
+        if (d == 1) { p[0].y = r0; p[1].y = r1; p[2].y = r2; p[3].y = r3; }
+        if (d == 2) { p[0].z = r0; p[1].z = r1; p[2].z = r2; p[3].z = r3; }
+        if (d == 3) { p[0].w = r0; p[1].w = r1; p[2].w = r2; p[3].w = r3; }
+    }
+    const uint64_t cols = C / 1024, u = o / 1024, w = o % 1024;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const uint64_t off = chunk_stream_off(s * cols + u, N) + w;
+        const u32x4 x = s < 4 ? v[s] : p[s - 4];
+        store16_a8<false>(stream + off, x);
+        if (s >= 4 && tail) store16_a8<false>(tail + (off - t0), x);
+    }
+}
+
+bool enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("CHIP_KM");
+        return !(e && !std::strcmp(e, "0"));
+    }();
+    return on;
+}
+
+hipError_t launch(int mode, MultiArgs a, hipStream_t stream) {
+    const uint64_t G = (a.N + S - 1) / S;
+    if (a.N <= (uint64_t)S || G > (uint64_t)GMAX) return hipErrorInvalidValue;
+    uint32_t *q = nullptr;
+    hipError_t e = stream_queue(stream, &q);
+    if (e != hipSuccess) return e;
+    a.counter = q + QUEUE_KM;
+    if (mode == 0) hipLaunchKernelGGL(km_kernel<0>, dim3((unsigned)G), dim3(TPB), 0, stream, a);
+    else hipLaunchKernelGGL(km_kernel<1>, dim3((unsigned)G), dim3(TPB), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace multi
+
+bool km_ok(uint64_t bao_n, uint64_t count) {
+    const uint64_t N = n_chunks(bao_n);
+    return multi::enabled() && count == 1 && N > (uint64_t)multi::S && N <= KM_MAX_N;
+}
+
+uint64_t km_scratch_len(uint64_t bao_n) { return 32 * ((n_chunks(bao_n) + multi::S - 1) / multi::S); }
+
+hipError_t km_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_nodes, uint8_t *d_hash, void *d_scratch,
+                             hipStream_t stream) {
+    multi::MultiArgs a{};
+    a.src = d_in; a.nodes = d_nodes;
+    a.n = n; a.N = n_chunks(n); a.n_in = a.N; a.valid = n; a.nd = a.N;
+    a.hash = d_hash; a.gcv = static_cast<uint8_t *>(d_scratch);
+    return multi::launch(0, a, stream);
+}
+
+hipError_t km_zfec_bao_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint8_t *d_stream, uint8_t *d_nodes,
+                           uint8_t *d_tail, uint64_t t0, uint8_t *d_hash, void *d_scratch, hipStream_t stream) {
+    if (C == 0 || C % 1024 || !d_stream) return hipErrorInvalidValue;
+    const void *tab = nullptr;
+    hipError_t e = zfec_parity_table(4, 8, &tab);
+    if (e != hipSuccess) return e;
+    const uint64_t N = 8 * C / 1024;
+    hipLaunchKernelGGL(multi::km_parity_kernel, dim3((unsigned)((C / 16 + 255) / 256)), dim3(256), 0, stream, d_in,
+                       valid, C, d_stream, N, static_cast<const uint32_t *>(tab), d_tail, t0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    multi::MultiArgs a{};
+    a.stream = d_stream; a.nodes = d_nodes; a.tail = d_tail; a.t0 = t0;
+    a.n = 8 * C; a.N = N; a.n_in = 0; a.nd = N / 2;
+    a.hash = d_hash; a.gcv = static_cast<uint8_t *>(d_scratch);
+    return multi::launch(0, a, stream);
+}
+
+hipError_t km_bao_decode_dev(const uint8_t *d_stream, uint64_t n, const uint8_t *d_hash, uint8_t *d_out,
+                             uint64_t out_limit, uint32_t *d_status, void *d_scratch, hipStream_t stream) {
+    multi::MultiArgs a{};
+    a.stream = d_stream; a.out = d_out;
+    a.n = n; a.N = n_chunks(n); a.out_limit = d_out ? out_limit : 0;
+    a.hash = const_cast<uint8_t *>(d_hash); a.status = d_status;
+    a.gcv = static_cast<uint8_t *>(d_scratch);
+    return multi::launch(1, a, stream);
+}
+
+}  // namespace chip

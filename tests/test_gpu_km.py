@@ -1,0 +1,146 @@
+"""GPU parity of KM (carbonado_amd/csrc/multi_kernels.hip, api_single.cpp):
+one object's encode()/decode() over many workgroups (a quad of lanes per
+compression, a 64-chunk subtree per workgroup, the last workgroup walks the
+tree top) with the split copies (the host writes the chunks it holds, gathers
+the content it returns).
+
+Bit-exact against the C oracle at every size class around KM's limits —
+N = 65 (the first KM stream), odd chunk counts, the level-15 shard length of a
+1 MiB segment (C = 257 KiB: shards not aligned to the 64-chunk groups),
+1 MiB, 4 MiB, N = KM_MAX_N (32768) and one past it (K13 again) — for
+encode() at Zfec|Bao (level 12) and Bao (level 4) and the stage functions;
+decode rejects a flipped byte in the header, a data chunk, a parity chunk, a
+node in the data region, a node in the tree top (above the groups) and the
+hash (decoding.rs:53-60: bao's HashMismatch), and returns nothing then."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# encode() level 12: N = 8 C / 1024, C = ceil(n / 4096) KiB
+L12 = [32769, 36864 + 1, 65536, 100_000, 1 << 20, (1 << 20) + 1, 1048811, 3 * (1 << 20) + 12345, 4 << 20,
+       16 << 20, (16 << 20) + 1]
+# bao of the content (level 4): N = ceil(n / 1024)
+L4 = [65537, 66560, 100_000, 1 << 20, (4 << 20) + 3, 32 << 20, (32 << 20) + 1]
+
+
+def _data(n, seed=0):
+    return np.random.default_rng(n * 11 + seed).integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+@pytest.mark.parametrize("n", L12)
+def test_km_level12_encode_decode(gpu, n):
+    import carbonado_amd as ca
+    d = _data(n)
+    enc, h, info = ca.encode(b"", d, 12)
+    oenc, oh, _ = O.encode(d, 12)
+    assert h == oh
+    assert enc == oenc
+    assert ca.decode(b"", h, enc, info.padding_len, 12) == d
+
+
+@pytest.mark.parametrize("n", L4)
+def test_km_level4_and_stage_functions(gpu, n):
+    import carbonado_amd as ca
+    d = _data(n, 4)
+    oenc, oh = O.bao_encode(d)
+    enc, h, info = ca.encode(b"", d, 4)
+    assert h == oh and enc == oenc
+    assert ca.decode(b"", h, enc, 0, 4) == d
+    senc, sh = ca.encoding.bao(d)  # chip_bao_encode / chip_bao_decode
+    assert sh == oh and senc == oenc
+    assert ca.decoding.bao(senc, sh) == d
+
+
+def _spots(enc, n_content):
+    """Byte offsets to flip: the header, the root node, a data chunk, the last
+    (parity) chunk, a node of the first group's subtree and a node above the
+    groups."""
+    N = (n_content + 1023) // 1024
+    root = 8
+    spots = {"header": 0, "root_node": root + 40, "last_chunk": len(enc) - 1}
+    # chunk 0 sits after the left spine of parents: 8 + 64 * depth
+    depth = (N - 1).bit_length()
+    spots["chunk0"] = 8 + 64 * depth + 100
+    # the parent of chunks 0-1 is the last node of the spine, level 1 (in group 0)
+    spots["group0_node"] = 8 + 64 * (depth - 1) + 3
+    # a level-7+ node: the spine's second node when the tree has > 7 levels
+    if depth > 7:
+        spots["top_node"] = 8 + 64 + 17
+    return spots
+
+
+@pytest.mark.parametrize("n", [100_000, 1 << 20, 1048811])
+def test_km_level12_decode_rejects_tampering(gpu, n):
+    import carbonado_amd as ca
+    from carbonado_amd.error import BaoDecodeError
+    d = _data(n, 7)
+    enc, h, info = ca.encode(b"", d, 12)
+    for name, pos in _spots(enc, info.bytes_ecc).items():
+        bad = bytearray(enc)
+        bad[pos] ^= 0x04
+        with pytest.raises(BaoDecodeError):
+            ca.decode(b"", h, bytes(bad), info.padding_len, 12)
+    bad_h = bytearray(h)
+    bad_h[0] ^= 1
+    with pytest.raises(BaoDecodeError):
+        ca.decode(b"", bytes(bad_h), enc, info.padding_len, 12)
+    assert ca.decode(b"", h, enc, info.padding_len, 12) == d
+
+
+@pytest.mark.parametrize("n", [65537, 1 << 20])
+def test_km_bao_decode_rejects_tampering(gpu, n):
+    import carbonado_amd as ca
+    from carbonado_amd.error import BaoDecodeError
+    d = _data(n, 9)
+    enc, h = ca.encoding.bao(d)
+    for name, pos in _spots(enc, n).items():
+        bad = bytearray(enc)
+        bad[pos] ^= 0x80
+        with pytest.raises(BaoDecodeError):
+            ca.decoding.bao(bytes(bad), h)
+
+
+def test_km_matches_the_batch_kernels(gpu):
+    """The same objects as single calls (KM) and as a device batch (K13 /
+    K1 + K3): identical streams and hashes at levels 4 and 12."""
+    import torch
+    import carbonado_amd as ca
+    from carbonado_amd import device as D
+    n, count = 300_001, 3
+    objs = [_data(n, s) for s in range(count)]
+    stride = (n + 255) // 256 * 256
+    inp = torch.zeros((count, stride), dtype=torch.uint8, device="cuda")
+    for i, o in enumerate(objs):
+        inp[i, :n] = torch.frombuffer(bytearray(o), dtype=torch.uint8).cuda()
+    for level in (4, 12):
+        single = [ca.encode(b"", o, level) for o in objs]
+        olen = len(single[0][0])
+        out = torch.zeros((count, (olen + 255) // 256 * 256), dtype=torch.uint8, device="cuda")
+        hashes = torch.zeros((count, 32), dtype=torch.uint8, device="cuda")
+        D.encode_batch(level, inp, n, out, hashes, D.encode_scratch(level, n, count))
+        torch.cuda.synchronize()
+        for i in range(count):
+            assert bytes(out[i, :olen].cpu().numpy()) == single[i][0]
+            assert bytes(hashes[i].cpu().numpy()) == single[i][1]
+
+
+def test_km_back_to_back_calls_reuse_the_counter(gpu):
+    """KM's last-workgroup counter lives in the stream's queue block and is
+    reset by each launch's last workgroup: many calls of different sizes in a
+    row (and an interleaved failing decode) all give the oracle's bytes."""
+    import carbonado_amd as ca
+    from carbonado_amd.error import BaoDecodeError
+    for i, n in enumerate([70_000, 1 << 20, 200_000, 65537, 3 << 20, 100_003] * 2):
+        d = _data(n, 100 + i)
+        level = 12 if i % 2 == 0 else 4
+        enc, h, info = ca.encode(b"", d, level)
+        oenc, oh, _ = O.encode(d, level)
+        assert enc == oenc and h == oh, (i, n)
+        bad = bytearray(enc)
+        bad[len(enc) // 3] ^= 1
+        with pytest.raises(BaoDecodeError):
+            ca.decode(b"", h, bytes(bad), info.padding_len, level)
+        assert ca.decode(b"", h, enc, info.padding_len, level) == d

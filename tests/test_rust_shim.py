@@ -10,7 +10,9 @@ This image has no Rust toolchain, so the crate is checked by parsing it:
   mapped types; the C sizes are the ones lib.rs's own unit test asserts;
 * the status codes and constants agree, and lib.rs maps every status;
 * carbonado-hip/reroute.patch applies to the reference crate and reroutes
-  the five seam functions (encoding.rs:39,48, decoding.rs:21,35,54).
+  the five seam functions (encoding.rs:39,48, decoding.rs:21,35,54), the
+  Zfec|Bao glue of encode()/decode() as one fused call each, and scrub /
+  verify_slice / extract_slice.
 """
 import re
 import shutil
@@ -186,23 +188,73 @@ def test_status_codes_and_constants_agree():
     assert rev == arms  # ChipError::status() maps every variant back
 
 
-def test_reroute_patch_targets_the_five_seams():
+def _added(patch: str) -> str:
+    return "\n".join(l[1:] for l in patch.splitlines() if l.startswith("+") and not l.startswith("+++"))
+
+
+def _top_level_args(argstr: str) -> int:
+    depth, n, cur = 0, 0, ""
+    for ch in argstr:
+        if ch in "([{<" and not (ch == "<" and cur.endswith(" ")):
+            depth += 1
+        elif ch in ")]}>" and depth:
+            depth -= 1
+        if ch == "," and depth == 0:
+            n += 1
+            cur = ""
+        else:
+            cur += ch
+    return n + (1 if cur.strip() else 0)
+
+
+def _calls(text: str, prefix: str = "carbonado_hip::") -> list:
+    """(name, arity) of every `carbonado_hip::name(...)` call in text."""
+    out = []
+    for m in re.finditer(re.escape(prefix) + r"(\w+)\(", text):
+        i, depth = m.end(), 1
+        while depth:
+            depth += {"(": 1, ")": -1}.get(text[i], 0)
+            i += 1
+        out.append((m.group(1), _top_level_args(text[m.end():i - 1])))
+    return out
+
+
+def _lib_arity() -> dict:
+    lib = _strip_comments(LIB.read_text())
+    return {name: _top_level_args(params) for name, params in
+            re.findall(r"pub fn (\w+)\(([^)]*)\)", lib)}
+
+
+def test_reroute_patch_targets_the_seams_and_the_glue():
+    """The five stage seams (encoding.rs:39,48, decoding.rs:21,35,54), the
+    Zfec|Bao glue of encode()/decode() as ONE fused call each
+    (encoding.rs:121-147, decoding.rs:89-99: no host Vec between the two
+    stages) and scrub / verify_slice / extract_slice (decoding.rs:116-212,
+    VERDICT r5 item 1), every call with the arity of the lib.rs wrapper."""
     patch = (CRATE / "reroute.patch").read_text()
     files = re.findall(r"^\+\+\+ b/(\S+)", patch, flags=re.M)
     assert files == ["Cargo.toml", "src/decoding.rs", "src/encoding.rs", "src/error.rs"]
-    added = "\n".join(l[1:] for l in patch.splitlines() if l.startswith("+") and not l.startswith("+++"))
+    added = _added(patch)
     for call in ("carbonado_hip::bao_encode(", "carbonado_hip::zfec_encode(", "carbonado_hip::zfec_decode(",
-                 "carbonado_hip::zfec_decode_shares(", "carbonado_hip::bao_decode("):
+                 "carbonado_hip::zfec_decode_shares(", "carbonado_hip::bao_decode(",
+                 "carbonado_hip::encode(&[], &encrypted, 12, None)",
+                 "carbonado_hip::decode(&[], hash, input, padding, 12)",
+                 "carbonado_hip::scrub(input, hash, encode_info.padding_len, encode_info.chunk_len)",
+                 "carbonado_hip::verify_slice(hash.as_bytes(), input, index as u64, count as u64)",
+                 "carbonado_hip::extract_slice(encoded, index as u64)"):
         assert call in added, call
     # every rerouted call sits behind the feature, the CPU path stays the default
-    assert added.count('#[cfg(feature = "hip")]') >= 5
+    assert added.count('#[cfg(feature = "hip")]') >= 10
     assert 'hip = ["dep:carbonado-hip"]' in added
     # the public API (lib.rs:21-29) is untouched
     assert "src/lib.rs" not in files
-    # each wrapper the patch calls exists in the crate
-    lib = LIB.read_text()
-    for fn in ("bao_encode", "zfec_encode", "zfec_decode", "zfec_decode_shares", "bao_decode"):
-        assert re.search(rf"pub fn {fn}\(", lib), fn
+    # each wrapper the patch calls exists in the crate, called with its arity
+    arity = _lib_arity()
+    calls = _calls(added)
+    assert {c for c, _ in calls} == {"bao_encode", "zfec_encode", "zfec_decode", "zfec_decode_shares", "bao_decode",
+                                     "encode", "decode", "scrub", "verify_slice", "extract_slice"}
+    for name, n in calls:
+        assert arity.get(name) == n, (name, n, arity.get(name))
 
 
 @pytest.mark.skipif(not (REFERENCE / "src" / "encoding.rs").exists() or shutil.which("patch") is None,
@@ -217,6 +269,26 @@ def test_reroute_patch_applies_to_the_reference(tmp_path):
     enc = (tmp_path / "src/encoding.rs").read_text()
     assert "pub fn zfec(input: &[u8]) -> Result<(Vec<u8>, u32, u32), CarbonadoError>" in enc
     assert "fn zfec_cpu(" in enc
+    # encode(): with both bits the fused call returns before zfec() and bao() run
+    body = enc[enc.index("pub fn encode("):]
+    assert body.index("carbonado_hip::encode(") < body.index("zfec(&encrypted)") < body.index("bao(&encoded)")
+    dec = (tmp_path / "src/decoding.rs").read_text()
+    body = dec[dec.index("pub fn decode("):]
+    assert body.index("carbonado_hip::decode(") < body.index("ecies(&decoded, secret_key)")
+    # the public signatures the crate re-exports (lib.rs:21-29) are unchanged
+    ref_dec = (REFERENCE / "src/decoding.rs").read_text()
+    for sig in (r"pub fn scrub\([^)]*\) -> Result<Vec<u8>, CarbonadoError>",
+                r"pub fn verify_slice\([^)]*\) -> Result<Vec<u8>, CarbonadoError>",
+                r"pub fn extract_slice\([^)]*\) -> Result<Vec<u8>, CarbonadoError>",
+                r"pub fn decode\([^)]*\) -> Result<Vec<u8>, CarbonadoError>"):
+        assert " ".join(re.search(sig, ref_dec).group(0).split()) == " ".join(re.search(sig, dec).group(0).split())
+    # scrub's device route comes first: the CPU body (zfec_chunks, positional
+    # indices) only runs without the feature
+    body = dec[dec.index("pub fn scrub("):]
+    assert body.index("carbonado_hip::scrub(") < body.index("fn scrub_cpu(") < body.index("zfec_chunks(chunks")
+    for fn in ("verify_slice", "extract_slice"):
+        body = dec[dec.index(f"pub fn {fn}("):]
+        assert body.index(f"carbonado_hip::{fn}(") < body.index(f"fn {fn}_cpu(")
 
 
 def test_c_to_rust_mapping_rules():
@@ -235,7 +307,7 @@ def test_reroute_error_mapping():
     ZfecError wraps a zfec_rs::Error that only the unvendored zfec-rs can
     build, so that arm is explicit and documented."""
     patch = (CRATE / "reroute.patch").read_text()
-    added = "\n".join(l[1:] for l in patch.splitlines() if l.startswith("+") and not l.startswith("+++"))
+    added = _added(patch)
     arms = dict(re.findall(r"C::(\w+)(?:\(\w+\))? => CarbonadoError::(\w+)", added))
     assert arms == {
         "UnevenZfecChunks": "UnevenZfecChunks",
@@ -261,3 +333,39 @@ def test_reroute_error_mapping():
         ref = err.read_text()
         for v in set(arms.values()) - {"HipError"}:
             assert re.search(rf"\n\s+{v}(\(|,)", ref), v
+
+
+def _wrapper_chip_calls() -> dict:
+    """lib.rs wrapper name -> the ffi::chip_* functions its body calls."""
+    lib = _strip_comments(LIB.read_text())
+    out = {}
+    for m in re.finditer(r"\npub fn (\w+)\(", lib):
+        i = lib.index("{", m.end())
+        depth, j = 1, i + 1
+        while depth:
+            depth += {"{": 1, "}": -1}.get(lib[j], 0)
+            j += 1
+        out[m.group(1)] = re.findall(r"ffi::(chip_\w+)\(", lib[i:j])
+    return out
+
+
+def test_replay_tables_are_the_patch_and_lib_rs():
+    """tests/rust_replay.py replays the patched crate on the GPU: its call
+    tables must be what the patch (which wrapper each reference function
+    calls) and lib.rs (which chip_* each wrapper calls) say."""
+    import rust_replay as R
+    w = _wrapper_chip_calls()
+    patch = (CRATE / "reroute.patch").read_text()
+    added = _added(patch)
+    fused_enc = w["encode"]
+    assert fused_enc == ["chip_encode"] and "carbonado_hip::encode(" in added
+    assert R.ENCODE_CALLS[R.ZFEC | R.BAO] == fused_enc
+    assert R.ENCODE_CALLS[R.ZFEC] == w["zfec_encode"] and R.ENCODE_CALLS[R.BAO] == w["bao_encode"]
+    assert R.DECODE_CALLS[R.ZFEC | R.BAO] == w["decode"] == ["chip_decode"]
+    assert R.DECODE_CALLS[R.ZFEC] == w["zfec_decode"] and R.DECODE_CALLS[R.BAO] == w["bao_decode"]
+    for fn, calls in R.SLICE_CALLS.items():
+        assert f"carbonado_hip::{fn}(" in added
+        assert w[fn] == calls, (fn, w[fn])
+    # round 5's patch: the two stage wrappers back to back
+    assert R.ENCODE_CALLS_R5[12] == w["zfec_encode"] + w["bao_encode"]
+    assert R.DECODE_CALLS_R5[12] == w["bao_decode"] + w["zfec_decode"]

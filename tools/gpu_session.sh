@@ -117,6 +117,15 @@ for s in "$@"; do
                CHIP_STAGE_THREADS=$t run latency_stage${t}_$i 300 python3 tools/latency_probe.py 60 ${STAGE_LEVELS:-15,3} 1048576,4194304
              done; done ;;
     abilat) run abi_latency 300 ./tools/abi_latency 50 ;;
+    abilat6) run abi_latency_patch 400 ./tools/abi_latency 40 12,4,8,15 1024,1048576,16777216 ;;
+    kmtests) run pytest_km 600 python3 -u -m pytest tests/test_gpu_km.py tests/test_gpu_reroute.py tests/test_gpu_small.py tests/test_gpu_pipeline.py tests/test_gpu_bao.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    kmab) for i in 1 2; do for km in 1 0; do CHIP_KM=$km run abi_latency_km${km}_$i 300 ./tools/abi_latency 40 ${KM_LEVELS:-12,4} ${KM_SIZES:-65536,262144,1048576,4194304}; done; done ;;
+    kmtl) CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12,4 1048576
+          run timeline_km_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tlkm -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
+    zcab) for i in 1 2; do for zc in default wc coherent noncoherent; do CHIP_ZC_IN=$zc run abi_latency_zc${zc}_$i 300 ./tools/abi_latency 40 12,4 262144,1048576,4194304; done; done
+          CHIP_ZC_IN=wc run timeline_km_wc 300 rocprofv3 --kernel-trace --stats -d $O/tlwc -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
+    r6tests) run pytest_r6 600 python3 -u -m pytest tests/test_gpu_reroute.py tests/test_gpu_rccl.py tests/test_gpu_small.py tests/test_gpu_scrub.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    timeline1m) run timeline_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tl -o tl --output-format csv -- ./tools/abi_latency 20 12 1048576 ;;
     topquadab) for i in 1 2; do for tq in 0 1; do CHIP_TOP_QUAD=$tq run abi_latency_tq${tq}_$i 300 ./tools/abi_latency 50; done; done ;;
     upperab) for i in 1 2; do for u in 1 0; do
                CHIP_UPPER_PASS=$u run bench_pipe12_1mib_up${u}_$i 300 python3 bench.py --mode pipeline --level 12 --object-bytes 1048576 --objects 16384 --no-cpu-baseline
