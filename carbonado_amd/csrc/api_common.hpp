@@ -87,6 +87,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     DevBuf in, mid, out, scratch, small, x1, x2, flags;
     DevBuf hin, hout;  // pinned, NUMA-local: a single object's zero-copy input / outputs (api_single.cpp)
+    hipEvent_t ev_km = nullptr;  // api_single.cpp: the parity kernel of a single encode done
     std::vector<Slot> slots;
     Staging stage;
     // pinned arena for the few-byte copies of a call (hashes, status words,

@@ -63,6 +63,8 @@ void Ctx::release() {
     stage.release();
     if (hs.p) (void)hipHostFree(hs.p);
     hs = DevBuf{};
+    if (ev_km) (void)hipEventDestroy(ev_km);
+    ev_km = nullptr;
     for (DevBuf *b : {&hin, &hout}) {
         if (b->p) (void)hipHostFree(b->p);
         *b = DevBuf{};

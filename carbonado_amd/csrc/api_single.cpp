@@ -38,11 +38,12 @@ namespace {
 // src: offset in KM's compact node buffer) and the end t0 of that region.
 struct HostGeo {
     uint64_t N = 0, nh = 0, zl = 0, t0 = 8, nbytes = 0;  // nbytes: compact node bytes
-    std::vector<uint64_t> coff;
+    std::vector<uint64_t> coff;  // slots of chunks [0, nh), then (tail) of chunks [nh, N)
     struct Run {
         uint64_t dst, src, len;
     };
-    std::vector<Run> runs;
+    std::vector<Run> runs;   // the nodes in front of t0: stream offset, compact offset, bytes
+    std::vector<Run> truns;  // the nodes past t0 (tail only): stream offset, -, bytes
 };
 
 const HostGeo &host_geo(uint64_t zl, uint64_t nh) {
@@ -67,6 +68,14 @@ const HostGeo &host_geo(uint64_t zl, uint64_t nh) {
     }
     g.t0 = prev_end;
     g.nbytes = src;
+    if (nh < g.N) {  // the tail: chunk slots and the node runs between them
+        g.coff.resize(g.N);
+        for (uint64_t i = nh; i < g.N; ++i) {
+            g.coff[i] = bao_chunk_offset(i, g.N);
+            if (g.coff[i] > prev_end) g.truns.push_back({prev_end, 0, g.coff[i] - prev_end});
+            prev_end = g.coff[i] + std::min<uint64_t>(1024, zl - 1024 * i);
+        }
+    }
     return cache.emplace(key, std::move(g)).first->second;
 }
 
@@ -148,10 +157,11 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
     trace.mark("copy in");
     const uint8_t *d_in = dev_ptr<const uint8_t>(hin);
     uint8_t *d_out = dev_ptr<uint8_t>(hout);
-    if (zfec)
+    if (zfec) {
+        if (!c->ev_km) CHIP_HIP(hipEventCreateWithFlags(&c->ev_km, hipEventDisableTiming));
         CHIP_HIP(km_zfec_bao_dev(d_in, cur_n, C, static_cast<uint8_t *>(c->out.p), d_out + nodes_at, d_out, g.t0,
-                                 d_out + hash_at, c->scratch.p, c->stream));
-    else
+                                 d_out + hash_at, c->scratch.p, c->stream, c->ev_km));
+    } else
         CHIP_HIP(km_bao_encode_dev(d_in, cur_n, d_out + nodes_at, d_out + hash_at, c->scratch.p, c->stream));
     trace.mark("launch");
     // meanwhile: the header and the chunks the host holds, on a few threads
@@ -163,9 +173,23 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
         else host::gather_chunks_to_slots(out, g.coff.data() + a, cur + 1024 * a, std::min(cur_n, 1024 * b) - 1024 * a);
     });
     trace.mark("host chunks");
+    if (zfec) {  // the parity chunks are final once the parity kernel is done: out while KM hashes
+        CHIP_HIP(hipEventSynchronize(c->ev_km));
+        trace.mark("parity done");
+        const int pp = host_parts(N - nh);
+        host::par_for(pp, [&](int i) {
+            const uint64_t a = nh + (N - nh) * i / pp, b = nh + (N - nh) * (i + 1) / pp;
+            for (uint64_t k = a; k < b; ++k) std::memcpy(out + g.coff[k], hout + (g.coff[k] - g.t0), 1024);
+        });
+        trace.mark("parity out");
+    }
     CHIP_HIP(hipStreamSynchronize(c->stream));
     trace.mark("sync");
-    if (tail_len) copy_out(out + g.t0, hout, tail_len);
+    if (zfec) {
+        for (const HostGeo::Run &r : g.truns) std::memcpy(out + r.dst, hout + (r.dst - g.t0), r.len);
+    } else if (tail_len) {
+        copy_out(out + g.t0, hout, tail_len);
+    }
     for (const HostGeo::Run &r : g.runs) std::memcpy(out + r.dst, hout + nodes_at + r.src, r.len);
     std::memcpy(hash, hout + hash_at, 32);
     trace.mark("copy out");

@@ -203,9 +203,11 @@ hipError_t km_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_nodes, 
 // d_stream (device), the parity shards and the nodes past the data region
 // also into d_tail = the stream's image from byte t0 (null: none), the nodes
 // of the data region (chunks [0, 4 C / 1024)) compactly into d_nodes as
-// above, the hash.
+// above, the hash.  parity_done (optional) is recorded once the shards are
+// written (d_tail's chunks final; the nodes follow with KM).
 hipError_t km_zfec_bao_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint8_t *d_stream, uint8_t *d_nodes,
-                           uint8_t *d_tail, uint64_t t0, uint8_t *d_hash, void *d_scratch, hipStream_t stream);
+                           uint8_t *d_tail, uint64_t t0, uint8_t *d_hash, void *d_scratch, hipStream_t stream,
+                           hipEvent_t parity_done = nullptr);
 // verify-decode one stream of n content bytes; content [0, out_limit) to
 // d_out (null: verify only); d_status (zero at launch) = 0 or
 // CHIP_ERR_BAO_HASH_MISMATCH.

@@ -48,8 +48,8 @@ using namespace bao;
 
 namespace multi {
 
-constexpr int TPB = 256, S = TPB / 4, LOGS = 6;  // 64 chunks (one per quad) per workgroup
-static_assert((1 << LOGS) == S, "group = 2^LOGS chunks");
+constexpr int TPB = 256, QUADS = TPB / 4;  // 64 quads per workgroup
+constexpr int S = 64;                      // chunks per workgroup (the default SG; at most QUADS)
 constexpr int GMAX = (int)(KM_MAX_N / S);  // groups the last workgroup's walk holds in LDS
 
 struct MultiArgs {
@@ -78,15 +78,19 @@ __device__ __forceinline__ void node_out(const MultiArgs &a, uint64_t P, int lev
     }
 }
 
-template <int MODE>
+// SG chunks per workgroup (a power of two <= QUADS; fewer spreads a small
+// object's loads over more CUs, the top walk then starts lower)
+template <int MODE, int SG>
 __global__ __launch_bounds__(TPB) void km_kernel(MultiArgs a) {
+    constexpr int LOGS = SG == 64 ? 6 : SG == 32 ? 5 : SG == 16 ? 4 : -1;
+    static_assert(LOGS > 0, "SG: 16, 32 or 64");
     __shared__ __attribute__((aligned(16))) uint32_t cvs[2][GMAX][8];  // a level and the next
-    __shared__ __attribute__((aligned(16))) uint32_t msg[S][16];       // each quad's message block
+    __shared__ __attribute__((aligned(16))) uint32_t msg[QUADS][16];   // each quad's message block
     __shared__ uint32_t last;
     __shared__ __attribute__((aligned(16))) u32x4 stored[MODE == 1 ? GMAX * 4 : 4];  // decode: the top's nodes
     const int t = threadIdx.x, q = t & 3, g = t >> 2;
     const uint64_t grp = blockIdx.x, G = gridDim.x, N = a.N, n = a.n;
-    const uint64_t c0 = grp * S, r = N - c0 < (uint64_t)S ? N - c0 : (uint64_t)S;  // my chunks
+    const uint64_t c0 = grp * SG, r = N - c0 < (uint64_t)SG ? N - c0 : (uint64_t)SG;  // my chunks
     bool ok = true;
 
     // ---- phase 1 (decode): the header checked, content bytes out
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(TPB) void km_kernel(MultiArgs a) {
     ok = true;
     for (int level = LOGS + 1; cnt_prev > 1; ++level) {
         const uint64_t cnt = (cnt_prev + 1) / 2;
-        for (uint64_t p = g; p < cnt; p += S) {
+        for (uint64_t p = g; p < cnt; p += QUADS) {
             if (2 * p + 1 >= cnt_prev) {
                 cvs[cur ^ 1][p][q] = cvs[cur][2 * p][q];
                 cvs[cur ^ 1][p][4 + q] = cvs[cur][2 * p][4 + q];
@@ -314,15 +318,30 @@ bool enabled() {
     return on;
 }
 
+// chunks per workgroup: CHIP_KM_SG (16 / 32 / 64, A/B runs), default 64;
+// never so few that the groups overflow the top walk's LDS
+int group_chunks(uint64_t N) {
+    static const int env = [] {
+        const char *e = std::getenv("CHIP_KM_SG");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 16 || v == 32 || v == 64 ? v : 0;
+    }();
+    int sg = env ? env : S;
+    while (sg < S && (N + sg - 1) / sg > (uint64_t)GMAX) sg *= 2;
+    return sg;
+}
+
 hipError_t launch(int mode, MultiArgs a, hipStream_t stream) {
-    const uint64_t G = (a.N + S - 1) / S;
+    const int sg = group_chunks(a.N);
+    const uint64_t G = (a.N + sg - 1) / sg;
     if (a.N <= (uint64_t)S || G > (uint64_t)GMAX) return hipErrorInvalidValue;
     uint32_t *q = nullptr;
     hipError_t e = stream_queue(stream, &q);
     if (e != hipSuccess) return e;
     a.counter = q + QUEUE_KM;
-    if (mode == 0) hipLaunchKernelGGL(km_kernel<0>, dim3((unsigned)G), dim3(TPB), 0, stream, a);
-    else hipLaunchKernelGGL(km_kernel<1>, dim3((unsigned)G), dim3(TPB), 0, stream, a);
+    auto k = mode == 0 ? (sg == 16 ? km_kernel<0, 16> : sg == 32 ? km_kernel<0, 32> : km_kernel<0, 64>)
+                       : (sg == 16 ? km_kernel<1, 16> : sg == 32 ? km_kernel<1, 32> : km_kernel<1, 64>);
+    hipLaunchKernelGGL(k, dim3((unsigned)G), dim3(TPB), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -333,7 +352,7 @@ bool km_ok(uint64_t bao_n, uint64_t count) {
     return multi::enabled() && count == 1 && N > (uint64_t)multi::S && N <= KM_MAX_N;
 }
 
-uint64_t km_scratch_len(uint64_t bao_n) { return 32 * ((n_chunks(bao_n) + multi::S - 1) / multi::S); }
+uint64_t km_scratch_len(uint64_t bao_n) { return 32 * (n_chunks(bao_n) + 15) / 16; }  // any group size
 
 hipError_t km_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_nodes, uint8_t *d_hash, void *d_scratch,
                              hipStream_t stream) {
@@ -345,7 +364,8 @@ hipError_t km_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_nodes, 
 }
 
 hipError_t km_zfec_bao_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint8_t *d_stream, uint8_t *d_nodes,
-                           uint8_t *d_tail, uint64_t t0, uint8_t *d_hash, void *d_scratch, hipStream_t stream) {
+                           uint8_t *d_tail, uint64_t t0, uint8_t *d_hash, void *d_scratch, hipStream_t stream,
+                           hipEvent_t parity_done) {
     if (C == 0 || C % 1024 || !d_stream) return hipErrorInvalidValue;
     const void *tab = nullptr;
     hipError_t e = zfec_parity_table(4, 8, &tab);
@@ -354,6 +374,7 @@ hipError_t km_zfec_bao_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint
     hipLaunchKernelGGL(multi::km_parity_kernel, dim3((unsigned)((C / 16 + 255) / 256)), dim3(256), 0, stream, d_in,
                        valid, C, d_stream, N, static_cast<const uint32_t *>(tab), d_tail, t0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (parity_done && (e = hipEventRecord(parity_done, stream)) != hipSuccess) return e;
     multi::MultiArgs a{};
     a.stream = d_stream; a.nodes = d_nodes; a.tail = d_tail; a.t0 = t0;
     a.n = 8 * C; a.N = N; a.n_in = 0; a.nd = N / 2;

@@ -5,27 +5,36 @@
 // OpenSSL has no dedicated secp256k1 code: its generic prime-field ladder set
 // most of the latency of a small level-15 encode() (~450 us on the GPU box,
 // DESIGN.md §6; ECIES does two scalar multiplications per encrypt and one
-// per decrypt).  This is a small dedicated implementation (on the 2 GHz build
-// container: k * P 194 us, k * G 53 us; ECIES encrypt 504 -> 401 us, decrypt
-// 355 -> 261 us through the Python mirror):
+// per decrypt).  This is a small dedicated implementation (on the GPU box's
+// CPU: k * P 34 us, k * G 15 us, tools/secp_field_check, r10h):
 //
-//  * field elements: 4 x 64-bit limbs, products through unsigned __int128 and
-//    carry chains through _addcarry_u64, reduced with 2^256 = 2^32 + 977
-//    (mod p), always to [0, p); every function runs the same
-//    instructions whatever the values (no branches or table indices on them);
+//  * field elements: five 52-bit limbs with lazy reduction (magnitudes, see
+//    Fe below), products through unsigned __int128, 2^256 = 2^32 + 977
+//    (mod p); fe_norm gives the canonical value for output and zero tests.
+//    Every function runs the same instructions whatever the values (no
+//    branches or table indices on them); fe_inv is a fixed addition chain;
 //  * points: projective (X : Y : Z) with the complete formulas of Renes,
 //    Costello and Batina (EUROCRYPT 2016), Algorithms 7 (addition) and 9
 //    (doubling) for a = 0, b3 = 21.  They have no exceptional cases, so the
 //    point at infinity and equal operands need no branches;
-//  * k * P: fixed 4-bit windows (256 doublings, 64 additions); the window's
+//  * k * P: k split with the endomorphism (GLV: k = k1 + k2 lambda, |k_i| <
+//    2^128, negative halves as n - k_i with the point's y negated by masks),
+//    33 joint 4-bit windows: 132 doublings and 66 additions; each window's
 //    multiple is read by scanning the whole 16-entry table with masks;
 //  * k * G: a precomputed table of i * 16^j * G (64 x 16 points, built once
-//    per process), 64 additions and no doublings.
+//    per process), 64 additions and no doublings, the same masked scans;
+//  * scalars mod n (BIP-340 signing): fixed limb loops, results chosen with
+//    masks.
 //
 // Scalars are 32-byte big-endian with 0 < k < n (the caller checks, as
-// libsecp256k1's SecretKey::parse).  tests/test_host_stages.py compares k * G
-// and the ECIES envelopes (k * P inside) with the C and Python oracles'
-// independent secp256k1 code on edge-case and random scalars.
+// libsecp256k1's SecretKey::parse).  tests/test_host_stages.py and
+// tests/test_secp_field.py compare k * G, the field and point arithmetic and
+// the ECIES envelopes (k * P inside) with the C and Python oracles'
+// independent secp256k1 code on edge-case and random scalars;
+// tests/test_constant_time.py (tests/dudect_ct.cpp) gives the timing
+// evidence: Welch's t over cycle counts, fixed vs random secret, 10^5
+// samples per class, |t| < 4.5 for k * P, k * G, fe_inv, the signing scalars,
+// BIP-340 signing end to end and the AES-GCM tag check.
 #pragma once
 
 #include <immintrin.h>
