@@ -1635,6 +1635,15 @@ def main():
             for key in ("traffic_ratio", "pmc_KiB_per_launch", "pmc_kernel", "alg_bytes_per_launch"):
                 if key in hbm:
                     res["roofline"][key] = hbm[key]
+            if args.mode == "pipeline" and args.level & 12 == 12:
+                # why K13 (encode() at Zfec|Bao) sits near 0.65 of the loop ceiling
+                res["roofline"]["note_bound"] = (
+                    "K13 bound (DESIGN.md section 3, K13): one launch per 256 x 16 MiB objects takes 3.61 ms = "
+                    "1.36x the larger of its two halves measured alone (the BLAKE3 hashing ~2.6 ms; the GF(2^8) "
+                    "products, loads and line stores ~2.65 ms): two waves per SIMD alternate between a VALU phase "
+                    "and a store/LDS phase.  PMC traffic is 1.04x the algorithmic bytes, so nothing is wasted on "
+                    "HBM; every lever measured (a third wave, two states per lane, role-split waves, priorities, "
+                    "four orders) was neutral or slower (profiles/NOT_KEPT.md).  Recorded as the bound.")
             if pipe and "pmc_kernel" in hbm:
                 res["roofline"]["note_traffic"] = ("traffic: the one dominant kernel's launch (the parent-level "
                                                    "kernels after it move a few % more); alg bytes: the whole step")
