@@ -82,7 +82,7 @@ def parse(argv=None):
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=8)
     ap.add_argument("--mode", choices=["encode", "decode", "bao", "bao-decode", "pipeline", "pipeline-decode", "e2e", "e2e-decode", "scrub",
-                                       "scrub-batch", "hasher", "file"],
+                                       "scrub-batch", "hasher", "file", "latency"],
                     default="encode",
                     help="bao-decode: device-resident decoding::bao (verify every node, return the content); "
                          "pipeline: device-resident encode() at --level (Bao/Zfec bits; 12 = zfec fused into "
@@ -91,7 +91,13 @@ def parse(argv=None):
                          "scrub-batch: scrub() of device-resident level-12 streams, every --scrub-every-th one damaged "
                          "(chip_scrub_batch_dev); "
                          "hasher: BaoHasher update()+finalize() over the objects in 4 MiB appends (utils.rs:104-137); "
-                         "file: file::encode of flat files on disk to .c<level> files (file.rs:409-440)")
+                         "file: file::encode of flat files on disk to .c<level> files (file.rs:409-440); "
+                         "latency: one object per call through the C-ABI (tools/abi_latency: the library call, the "
+                         "Rust patch's call sequence, round 5's) at --latency-levels x --latency-sizes, the C "
+                         "oracle's single-thread time per call beside each row")
+    ap.add_argument("--latency-levels", default="12,4,8,15", help="latency mode: Format levels")
+    ap.add_argument("--latency-sizes", default="1024,1048576,16777216", help="latency mode: object bytes")
+    ap.add_argument("--latency-reps", type=int, default=40, help="latency mode: calls per form and row")
     ap.add_argument("--file-dir", default=None, help="file mode: working directory (default $TMPDIR/carbonado_files)")
     ap.add_argument("--fsync", action="store_true", help="file mode: fsync every output file")
     ap.add_argument("--file-slice", type=int, default=64, help="file mode: files per pipeline slice")
@@ -1437,8 +1443,86 @@ class DryRun:
         return t1 - t0, [10.0] * steps
 
 
+def run_latency(args) -> None:
+    """--mode latency: single-object call latency (the reference's real unit,
+    a segment of about 1 MB, README.md:107-111).  The GPU side is
+    tools/abi_latency (C++ over the C-ABI only, no Python in the timed
+    calls); the cpu_baseline leg times oracle/carbonado_oracle.c (+
+    host_oracle.c at levels with Snappy/Ecies) on one thread per call for
+    the same rows.  One JSON line; `value` = level 12 at 1 MiB, lib encode."""
+    import statistics
+    import subprocess
+
+    import numpy as np
+    tool = ROOT / "tools" / "abi_latency"
+    if not tool.exists():
+        subprocess.run(["g++", "-std=c++17", "-O2", str(ROOT / "tools" / "abi_latency.cpp"), "-I" + str(ROOT / "include"),
+                        "-L" + str(ROOT / "carbonado_amd" / "lib"), "-lcarbonado_hip",
+                        "-Wl,-rpath," + str(ROOT / "carbonado_amd" / "lib"), "-o", str(tool)], check=True)
+    r = subprocess.run([str(tool), str(args.latency_reps), args.latency_levels, args.latency_sizes],
+                       capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise SystemExit("abi_latency failed: " + r.stdout[-2000:] + r.stderr[-2000:])
+    cols = ["lib_enc", "lib_dec", "patch_enc", "patch_dec", "r5_enc", "r5_dec"]
+    rows = []
+    for line in r.stdout.splitlines():
+        f = line.split()
+        if len(f) == 8 and f[0].isdigit():
+            row = {"level": int(f[0]), "bytes": int(f[1])}
+            row.update({c: (None if v == "-" else float(v)) for c, v in zip(cols, f[2:])})
+            rows.append(row)
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import host_oracle as H
+        from oracle import oracle as O
+        sk = H.sha256(b"latency receiver")
+        pub, eph, nonce = H.public_key(sk), H.sha256(b"latency eph"), H.sha256(b"latency nonce")[:16]
+        rng = np.random.default_rng(5)
+        for row in rows:
+            lv, nb = row["level"], row["bytes"]
+            d = rng.integers(0, 256, nb, dtype=np.uint8).tobytes()
+            te, td = [], []
+            budget = time.perf_counter() + 6.0  # bounded sample per row
+            for _ in range(5):
+                t0 = time.perf_counter()
+                if lv & 3:
+                    enc, h, info = O.c_encode_full(d, lv, pub, eph, nonce)
+                else:
+                    enc, h, info = O.encode(d, lv)
+                t1 = time.perf_counter()
+                if lv & 3:
+                    back = O.decode_full(sk, h, enc, info["padding_len"], lv)
+                else:
+                    back = O.decode(h, enc, info["padding_len"], lv) if lv & 12 else enc
+                t2 = time.perf_counter()
+                assert back == d
+                te.append((t1 - t0) * 1e6)
+                td.append((t2 - t1) * 1e6)
+                if time.perf_counter() > budget:
+                    break
+            row["cpu_enc"] = round(statistics.median(te), 1)
+            row["cpu_dec"] = round(statistics.median(td), 1)
+        cpu = {"unit": "us per call", "cores": 1, "kind": "port",
+               "sample": "median of up to 5 calls per row, 6 s per row at most: encode() through "
+                         "oracle/carbonado_oracle.c (+ host_oracle.c for Snappy/Ecies levels), decode() through "
+                         "its decode (+ the host oracle's ecies/snap)"}
+    head = next((x for x in rows if x["level"] == 12 and x["bytes"] == 1 << 20), rows[0] if rows else None)
+    print(json.dumps({
+        "metric": "single_object_latency", "value": head["lib_enc"] if head else None, "unit": "us",
+        "higher_is_better": False, "n_gpus": 1, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "one object per call through the C-ABI (tools/abi_latency)",
+                   "levels": args.latency_levels, "sizes": args.latency_sizes, "reps": args.latency_reps},
+        "columns": {"lib": "chip_encode / chip_decode, caller buffers reused",
+                    "patch": "carbonado-hip/reroute.patch's call sequence, a fresh buffer per output",
+                    "r5": "round 5's patch at Zfec|Bao: zfec -> host Vec -> bao",
+                    "cpu": "the C oracle, one thread (cpu_baseline)"},
+        "rows": rows, "cpu_baseline": cpu}))
+
+
 def main():
     args = parse()
+    if args.mode == "latency":
+        return run_latency(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     world, rank, local = setup_dist(args)

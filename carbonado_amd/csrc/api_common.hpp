@@ -209,6 +209,11 @@ int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const ui
 // the parity region and the parent nodes cross PCIe.  km_ok() must hold.
 int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uint64_t final_len, uint8_t *out,
                      uint8_t hash[32]);
+// encoding::zfec 4-of-8 of one object (n > 0 bytes, shard length C) into
+// out[0, 8 C): the host writes the data shards (the zero-padded input) while
+// zc_parity_kernel reads the input from pinned memory and writes the parity
+// shards into pinned memory (zero-copy), copied out after.
+int single_zfec_encode_zc(Ctx *c, const uint8_t *in, uint64_t n, uint64_t C, uint8_t *out);
 // decode of one bao stream `in` (len bytes, content n, every node verified on
 // the device by KM) with the content bytes [0, olen) gathered from `in` by the
 // host meanwhile, into dst; on a mismatch dst is wiped and the status

@@ -111,11 +111,23 @@ struct Trace {
 
 namespace {
 
-// a pinned host allocation as the device addresses it
+// a pinned host allocation as the device addresses it (looked up once per
+// allocation: the runtime call takes its allocation lock)
 template <class T>
 T *dev_ptr(void *host) {
+    thread_local void *last_host[2] = {nullptr, nullptr}, *last_dev[2] = {nullptr, nullptr};
+    for (int i = 0; i < 2; ++i)
+        if (last_host[i] == host) return static_cast<T *>(last_dev[i]);
     void *d = nullptr;
-    return hipHostGetDevicePointer(&d, host, 0) == hipSuccess ? static_cast<T *>(d) : static_cast<T *>(host);
+    if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        d = host;  // UVA: the same address
+    }
+    last_host[1] = last_host[0];
+    last_dev[1] = last_dev[0];
+    last_host[0] = host;
+    last_dev[0] = d;
+    return static_cast<T *>(d);
 }
 
 // n bytes into pinned memory on a few threads (streaming stores: only the
@@ -140,6 +152,7 @@ void copy_out(uint8_t *dst, const uint8_t *src, uint64_t n) {
 
 int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uint64_t final_len, uint8_t *out,
                      uint8_t hash[32]) {
+    Trace trace("encode");
     const bool zfec = C > 0;
     const uint64_t zl = zfec ? (uint64_t)CHIP_FEC_M * C : cur_n;
     const uint64_t N = n_chunks_of(zl), nh = zfec ? N / 2 : N;
@@ -147,11 +160,11 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
     // pinned outputs: [the stream image from t0][the compact nodes][the hash]
     const uint64_t tail_len = final_len - g.t0, nodes_at = (tail_len + 63) & ~uint64_t(63);
     const uint64_t hash_at = (nodes_at + g.nbytes + 63) & ~uint64_t(63);
-    Trace trace("encode");
     CHIP_HIP(grow_pinned_local(c->hin, cur_n + 16, zc_in_flags()));  // the kernels' 16-B source loads stay inside
     CHIP_HIP(grow_pinned_local(c->hout, hash_at + 64));
     if (zfec) CHIP_HIP(grow(c->out, final_len));
     CHIP_HIP(grow(c->scratch, km_scratch_len(zl)));
+    trace.mark("buffers");
     uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
     copy_in(hin, cur, cur_n);
     trace.mark("copy in");
@@ -196,15 +209,36 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
     return CHIP_OK;
 }
 
+int single_zfec_encode_zc(Ctx *c, const uint8_t *in, uint64_t n, uint64_t C, uint8_t *out) {
+    Trace trace("zfec");
+    CHIP_HIP(grow_pinned_local(c->hin, n + 16, zc_in_flags()));
+    CHIP_HIP(grow_pinned_local(c->hout, 4 * C));
+    uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
+    copy_in(hin, in, n);
+    trace.mark("copy in");
+    CHIP_HIP(zc_zfec_parity_dev(dev_ptr<const uint8_t>(hin), n, C, dev_ptr<uint8_t>(hout), c->stream));
+    trace.mark("launch");
+    // meanwhile: the data shards are the input, zero padded to 4 C
+    copy_out(out, in, n);
+    std::memset(out + n, 0, 4 * C - n);
+    trace.mark("data shards");
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    trace.mark("sync");
+    copy_out(out + 4 * C, hout, 4 * C);
+    trace.mark("copy out");
+    return CHIP_OK;
+}
+
 int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const uint8_t *hash, uint8_t *dst,
                      uint64_t olen, const std::function<void()> &meanwhile) {
+    Trace trace("decode");
     const uint64_t blen = bao_encoded_len(n);
     if (blen > len) return CHIP_ERR_BAO_TRUNCATED;
     // pinned: [the expected hash][the status word][the stream at 64]
     CHIP_HIP(grow_pinned_local(c->hin, 64 + blen, zc_in_flags()));
     CHIP_HIP(grow(c->scratch, km_scratch_len(n)));
     uint8_t *hin = static_cast<uint8_t *>(c->hin.p);
-    Trace trace("decode");
+    trace.mark("buffers");
     std::memcpy(hin, hash, 32);
     volatile uint32_t *status = reinterpret_cast<volatile uint32_t *>(hin + 32);
     *status = 0;

@@ -105,7 +105,10 @@ int chip_zfec_encode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t n, uint
     Ctx *c;
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    if (n) {
+    if (n && k == 4 && m == 8 && km_enabled()) {  // one 4-of-8 object: zero-copy parity, data shards by the host
+        st = single_zfec_encode_zc(c, in, n, C, out);
+        if (st != CHIP_OK) return st;
+    } else if (n) {
         CHIP_HIP(grow(c->in, n));
         CHIP_HIP(grow(c->out, total));
         CHIP_HIP(h2d(c->stage, c->in.p, in, n, c->stream));

@@ -192,6 +192,7 @@ hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t in_stride, uin
 // Scratch: km_scratch_len(bao_n) bytes (the group CVs).
 constexpr uint64_t KM_MAX_N = 32768;
 bool km_ok(uint64_t bao_n, uint64_t count);
+bool km_enabled();  // CHIP_KM (default on): also the single-object zero-copy zfec encode
 uint64_t km_scratch_len(uint64_t bao_n);
 // bao of n content bytes at d_in (device or pinned host memory): the parent
 // nodes compactly into d_nodes (the node at stream offset o in front of chunk
@@ -208,6 +209,9 @@ hipError_t km_bao_encode_dev(const uint8_t *d_in, uint64_t n, uint8_t *d_nodes, 
 hipError_t km_zfec_bao_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint8_t *d_stream, uint8_t *d_nodes,
                            uint8_t *d_tail, uint64_t t0, uint8_t *d_hash, void *d_scratch, hipStream_t stream,
                            hipEvent_t parity_done = nullptr);
+// encoding::zfec 4-of-8 of `valid` input bytes at d_in (pinned host or
+// device memory, 16-B aligned): the 4 parity shards, shard-major, to d_par.
+hipError_t zc_zfec_parity_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint8_t *d_par, hipStream_t stream);
 // verify-decode one stream of n content bytes; content [0, out_limit) to
 // d_out (null: verify only); d_status (zero at launch) = 0 or
 // CHIP_ERR_BAO_HASH_MISMATCH.

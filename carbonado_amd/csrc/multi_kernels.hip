@@ -310,6 +310,42 @@ __global__ __launch_bounds__(256) void km_parity_kernel(const uint8_t *in, uint6
     }
 }
 
+// encoding::zfec of one object from pinned host memory (zero-copy): one
+// 16-B position of every shard per lane, the 4 parity shards written
+// shard-major ([P0|P1|P2|P3], C bytes each) into pinned host memory; the data
+// shards are the zero-padded input, which the host writes itself.
+__global__ __launch_bounds__(256) void zc_parity_kernel(const uint8_t *in, uint64_t valid, uint64_t C, uint8_t *par,
+                                                        const uint32_t *table) {
+    __shared__ uint32_t tab[4 * 256];
+    for (int i = threadIdx.x; i < 4 * 256; i += 256) tab[i] = table[i];
+    const uint64_t o = 16 * ((uint64_t)blockIdx.x * 256 + threadIdx.x);
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = o < C ? zf::load16_masked(in, j * C + o, valid) : u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    if (o >= C) return;
+    u32x4 p[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t acc[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x ^= tab[j * 256 + ((zf::comp(v[j], d) >> (8 * b)) & 0xFFu)];
+            acc[b] = x;
+        }
+        uint32_t r0, r1, r2, r3;
+        zf::transpose4(acc[0], acc[1], acc[2], acc[3], r0, r1, r2, r3);
+        if (d == 0) { p[0].x = r0; p[1].x = r1; p[2].x = r2; p[3].x = r3; }
+        if (d == 1) { p[0].y = r0; p[1].y = r1; p[2].y = r2; p[3].y = r3; }
+        if (d == 2) { p[0].z = r0; p[1].z = r1; p[2].z = r2; p[3].z = r3; }
+        if (d == 3) { p[0].w = r0; p[1].w = r1; p[2].w = r2; p[3].w = r3; }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) *glb(reinterpret_cast<u32x4 *>(par + s * C + o)) = p[s];
+}
+
 bool enabled() {
     static const bool on = [] {
         const char *e = std::getenv("CHIP_KM");
@@ -347,6 +383,8 @@ hipError_t launch(int mode, MultiArgs a, hipStream_t stream) {
 
 }  // namespace multi
 
+bool km_enabled() { return multi::enabled(); }
+
 bool km_ok(uint64_t bao_n, uint64_t count) {
     const uint64_t N = n_chunks(bao_n);
     return multi::enabled() && count == 1 && N > (uint64_t)multi::S && N <= KM_MAX_N;
@@ -380,6 +418,16 @@ hipError_t km_zfec_bao_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint
     a.n = 8 * C; a.N = N; a.n_in = 0; a.nd = N / 2;
     a.hash = d_hash; a.gcv = static_cast<uint8_t *>(d_scratch);
     return multi::launch(0, a, stream);
+}
+
+hipError_t zc_zfec_parity_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint8_t *d_par, hipStream_t stream) {
+    if (C == 0 || C % 16) return hipErrorInvalidValue;
+    const void *tab = nullptr;
+    hipError_t e = zfec_parity_table(4, 8, &tab);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(multi::zc_parity_kernel, dim3((unsigned)((C / 16 + 255) / 256)), dim3(256), 0, stream, d_in,
+                       valid, C, d_par, static_cast<const uint32_t *>(tab));
+    return hipGetLastError();
 }
 
 hipError_t km_bao_decode_dev(const uint8_t *d_stream, uint64_t n, const uint8_t *d_hash, uint8_t *d_out,

@@ -144,3 +144,46 @@ def test_km_back_to_back_calls_reuse_the_counter(gpu):
         with pytest.raises(BaoDecodeError):
             ca.decode(b"", h, bytes(bad), info.padding_len, level)
         assert ca.decode(b"", h, enc, info.padding_len, level) == d
+
+
+_SG_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import carbonado_amd as ca
+from carbonado_amd.error import BaoDecodeError
+from oracle import oracle as O
+ca._lib.lib().chip_init(0)
+bad = []
+for n, level in ((100_000, 12), (1 << 20, 12), (1048811, 12), (300_001, 4), (5 << 20, 4)):
+    d = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+    enc, h, info = ca.encode(b"", d, level)
+    oenc, oh, _ = O.encode(d, level)
+    if enc != oenc or h != oh:
+        bad.append(("encode", n, level))
+    if ca.decode(b"", h, enc, info.padding_len, level) != d:
+        bad.append(("decode", n, level))
+    t = bytearray(enc)
+    t[len(enc) // 2] ^= 8
+    try:
+        ca.decode(b"", h, bytes(t), info.padding_len, level)
+        bad.append(("tamper accepted", n, level))
+    except BaoDecodeError:
+        pass
+print("BAD", bad) if bad else print("OK")
+"""
+
+
+@pytest.mark.parametrize("sg", ["16", "32"])
+def test_km_smaller_groups(gpu, sg):
+    """KM with 16 / 32 chunks per workgroup (CHIP_KM_SG, read once per
+    process: a child process): the group levels stop lower and the top walk
+    starts lower; same bytes, same verdicts."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parents[1])
+    out = subprocess.run([sys.executable, "-c", _SG_CHILD, root], env=dict(os.environ, CHIP_KM_SG=sg),
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0 and out.stdout.strip().endswith("OK"), out.stdout + out.stderr
