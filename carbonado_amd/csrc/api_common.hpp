@@ -109,9 +109,6 @@ hipError_t grow_pinned(DevBuf &b, size_t bytes);  // the same, pinned host memor
 // pinned host memory on the GPU's NUMA node (api_host_copy.cpp), for buffers
 // the kernels read or write over PCIe themselves (zero-copy)
 hipError_t grow_pinned_local(DevBuf &b, size_t bytes, unsigned flags = hipHostMallocDefault);
-// allocation flags of the zero-copy INPUT buffer (CHIP_ZC_IN=default|wc|
-// coherent|noncoherent, A/B of the GPU's PCIe read rate from it)
-unsigned zc_in_flags();
 // the calling thread's context on the process's device (created on first use)
 int ctx_get(Ctx **out);
 // few-byte copies of a call through the context's pinned arena; `dst` of a

@@ -315,17 +315,6 @@ hipError_t grow_pinned_local(DevBuf &b, size_t bytes, unsigned flags) {
     return hipSuccess;
 }
 
-unsigned zc_in_flags() {
-    static const unsigned f = [] {
-        const char *v = std::getenv("CHIP_ZC_IN");
-        if (!v) return (unsigned)hipHostMallocDefault;
-        if (!std::strcmp(v, "wc")) return (unsigned)hipHostMallocWriteCombined;
-        if (!std::strcmp(v, "coherent")) return (unsigned)hipHostMallocCoherent;
-        if (!std::strcmp(v, "noncoherent")) return (unsigned)hipHostMallocNonCoherent;
-        return (unsigned)hipHostMallocDefault;
-    }();
-    return f;
-}
 
 hipError_t stage_slot(Staging &sg, int k) {  // wait until ring slot k is free
     if (!sg.armed[k]) return hipSuccess;

@@ -133,7 +133,7 @@ T *dev_ptr(void *host) {
 // n bytes into pinned memory on a few threads (streaming stores: only the
 // device reads them next)
 void copy_in(uint8_t *dst, const uint8_t *src, uint64_t n) {
-    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, n >> 18));  // 256 KiB a thread
+    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, n >> 17));  // 128 KiB a thread
     host::par_for(parts, [&](int i) {
         const uint64_t a = (n * i / parts) & ~uint64_t(63), b = i + 1 == parts ? n : (n * (i + 1) / parts) & ~uint64_t(63);
         host::ring_copy(dst + a, src + a, b - a);
@@ -141,7 +141,7 @@ void copy_in(uint8_t *dst, const uint8_t *src, uint64_t n) {
 }
 
 void copy_out(uint8_t *dst, const uint8_t *src, uint64_t n) {
-    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, n >> 18));
+    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, n >> 17));
     host::par_for(parts, [&](int i) {
         const uint64_t a = n * i / parts, b = n * (i + 1) / parts;
         std::memcpy(dst + a, src + a, b - a);
@@ -160,7 +160,7 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
     // pinned outputs: [the stream image from t0][the compact nodes][the hash]
     const uint64_t tail_len = final_len - g.t0, nodes_at = (tail_len + 63) & ~uint64_t(63);
     const uint64_t hash_at = (nodes_at + g.nbytes + 63) & ~uint64_t(63);
-    CHIP_HIP(grow_pinned_local(c->hin, cur_n + 16, zc_in_flags()));  // the kernels' 16-B source loads stay inside
+    CHIP_HIP(grow_pinned_local(c->hin, cur_n + 16));  // the kernels' 16-B source loads stay inside
     CHIP_HIP(grow_pinned_local(c->hout, hash_at + 64));
     if (zfec) CHIP_HIP(grow(c->out, final_len));
     CHIP_HIP(grow(c->scratch, km_scratch_len(zl)));
@@ -198,12 +198,20 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
     }
     CHIP_HIP(hipStreamSynchronize(c->stream));
     trace.mark("sync");
-    if (zfec) {
-        for (const HostGeo::Run &r : g.truns) std::memcpy(out + r.dst, hout + (r.dst - g.t0), r.len);
-    } else if (tail_len) {
-        copy_out(out + g.t0, hout, tail_len);
-    }
-    for (const HostGeo::Run &r : g.runs) std::memcpy(out + r.dst, hout + nodes_at + r.src, r.len);
+    if (!zfec && tail_len) copy_out(out + g.t0, hout, tail_len);
+    // the node runs (thousands of 64-B pieces per MiB) on a few threads
+    const uint64_t nr = g.runs.size(), nt = zfec ? g.truns.size() : 0;
+    const int rp = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, (nr + nt) / 256));
+    host::par_for(rp, [&](int i) {
+        for (uint64_t k = nr * i / rp; k < nr * (i + 1) / rp; ++k) {
+            const HostGeo::Run &r = g.runs[k];
+            std::memcpy(out + r.dst, hout + nodes_at + r.src, r.len);
+        }
+        for (uint64_t k = nt * i / rp; k < nt * (i + 1) / rp; ++k) {
+            const HostGeo::Run &r = g.truns[k];
+            std::memcpy(out + r.dst, hout + (r.dst - g.t0), r.len);
+        }
+    });
     std::memcpy(hash, hout + hash_at, 32);
     trace.mark("copy out");
     return CHIP_OK;
@@ -211,7 +219,7 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
 
 int single_zfec_encode_zc(Ctx *c, const uint8_t *in, uint64_t n, uint64_t C, uint8_t *out) {
     Trace trace("zfec");
-    CHIP_HIP(grow_pinned_local(c->hin, n + 16, zc_in_flags()));
+    CHIP_HIP(grow_pinned_local(c->hin, n + 16));
     CHIP_HIP(grow_pinned_local(c->hout, 4 * C));
     uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
     copy_in(hin, in, n);
@@ -235,7 +243,7 @@ int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const 
     const uint64_t blen = bao_encoded_len(n);
     if (blen > len) return CHIP_ERR_BAO_TRUNCATED;
     // pinned: [the expected hash][the status word][the stream at 64]
-    CHIP_HIP(grow_pinned_local(c->hin, 64 + blen, zc_in_flags()));
+    CHIP_HIP(grow_pinned_local(c->hin, 64 + blen));
     CHIP_HIP(grow(c->scratch, km_scratch_len(n)));
     uint8_t *hin = static_cast<uint8_t *>(c->hin.p);
     trace.mark("buffers");
