@@ -132,6 +132,9 @@ for s in "$@"; do
            CHIP_ZC_IN=thp CHIP_SINGLE_TRACE=1 run km_single_trace_thp 120 ./tools/abi_latency 10 12 1048576
            CHIP_ZC_IN=thp run timeline_km_thp 300 rocprofv3 --kernel-trace --stats -d $O/tlthp -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576
            run timeline_km_def 300 rocprofv3 --kernel-trace --stats -d $O/tldef -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
+    zctests) run pytest_zc 600 python3 -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_written.py tests/test_gpu_zfec.py tests/test_gpu_km.py tests/test_gpu_reroute.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    thpout) cat /sys/kernel/mm/transparent_hugepage/enabled > $O/thp_setting.txt 2>&1 || true
+            for i in 1 2; do for t in 1 0; do CHIP_OUT_THP=$t run abi_latency_outthp${t}_$i 300 ./tools/abi_latency 12 12,4,8 4194304,16777216; done; done ;;
     latency) run bench_latency 900 python3 bench.py --mode latency ;;
     latencyq) run bench_latency_quick 300 python3 bench.py --mode latency --latency-levels 12,4 --latency-sizes 1048576 --latency-reps 20 ;;
     r6tests) run pytest_r6 600 python3 -u -m pytest tests/test_gpu_reroute.py tests/test_gpu_rccl.py tests/test_gpu_small.py tests/test_gpu_scrub.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
