@@ -31,6 +31,8 @@ ENCODE_CALLS = {ZFEC | BAO: ["chip_encode"], ZFEC: ["chip_zfec_encode"], BAO: ["
 DECODE_CALLS = {ZFEC | BAO: ["chip_decode"], ZFEC: ["chip_zfec_decode"], BAO: ["chip_bao_decode"], 0: []}
 SLICE_CALLS = {"scrub": ["chip_scrub"], "verify_slice": ["chip_bao_verify_slice"],
                "extract_slice": ["chip_bao_slice_len", "chip_bao_extract_slice"]}
+# the `hip-stages` feature: every level in one chip_encode / chip_decode
+STAGES_CALLS = ["chip_encode"], ["chip_decode"]
 # round 5's patch (stage reroutes only): encode() at Zfec|Bao went zfec ->
 # host Vec -> bao, decode() bao -> host Vec -> zfec
 ENCODE_CALLS_R5 = {ZFEC | BAO: ["chip_zfec_encode", "chip_bao_encode"]}
@@ -214,3 +216,25 @@ def decode(secret_key: bytes, hash: bytes, data: bytes, padding: int, level: int
             cur = zfec_decode(cur, padding)
             calls.append("chip_zfec_decode")
     return host_decode(cur, level, secret_key), calls
+
+
+# ---- the `hip-stages` feature: encode()/decode() whole in the library --------
+
+def encode_stages(data: bytes, level: int, pubkey: bytes = b"", eph_sk: bytes = bytes(32),
+                  nonce: bytes = bytes(16)) -> tuple[bytes, bytes, EncodeInfoC]:
+    """carbonado_hip::encode(pubkey, input, format, None) (inject given here
+    for bit-exact checks)."""
+    h = _buf(HASH_LEN)
+    info = EncodeInfoC()
+    e, nn = (ctypes.c_uint8 * 32).from_buffer_copy(eph_sk), (ctypes.c_uint8 * 16).from_buffer_copy(nonce)
+    inj = EciesInjectC(ctypes.addressof(e), ctypes.addressof(nn))
+    cap = _L().chip_encode_max_len(_L().chip_snap_max_len(len(data)) + 97)
+    enc = _into_vec("chip_encode", cap, lambda o, c, l: _L().chip_encode(
+        level, pubkey, len(pubkey), ctypes.byref(inj), data, len(data), o, c, l, h, ctypes.byref(info)))
+    return enc, bytes(h), info
+
+
+def decode_stages(secret_key: bytes, hash: bytes, data: bytes, padding: int, level: int, n_hint: int) -> bytes:
+    """carbonado_hip::decode(secret_key, hash, input, padding, format)."""
+    return _into_vec("chip_decode", max(len(data), 1024, n_hint + 1024), lambda o, c, l: _L().chip_decode(
+        secret_key, len(secret_key), hash, len(hash), data, len(data), padding, level, o, c, l))

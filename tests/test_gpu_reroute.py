@@ -8,6 +8,8 @@ through ctypes by tests/rust_replay.py, against the C oracle.
   device call per encode()/decode() (encoding.rs:121-147, decoding.rs:89-99);
 * round 5's sequence (zfec -> host Vec -> bao) still gives the same bytes,
   so the fused route changes cost, not output;
+* `--features hip-stages`: encode()/decode() as one library call each at the
+  Snappy/Ecies levels, bit-exact with the oracle's restatement;
 * scrub / verify_slice / extract_slice (decoding.rs:116-212) through their
   new routes: the reference's #[ignore]d apocalypse cases
   (tests/apocalypse.rs:22-40, byte 6400 flipped in content.png and code.tar)
@@ -118,3 +120,19 @@ def test_patched_slices_past_the_u16_wrap(gpu):
     for index in (0, 64, 100):
         sl = R.extract_slice(enc, index)
         assert sl[-1024:] == content[1024 * index:1024 * (index + 1)]
+
+
+@pytest.mark.parametrize("n", [1, 5000, 300_000, (1 << 20) + 1])
+@pytest.mark.parametrize("level", [2, 3, 13, 14, 15])
+def test_hip_stages_feature(gpu, level, n):
+    """`--features hip-stages`: encode()/decode() as one library call each,
+    the host stages on its pool (bit-exact with the oracle's restatement,
+    whose snappy the library's is)."""
+    d = _rnd(n, 5 * n + level)
+    enc, h, info = R.encode_stages(d, level, PUB, EPH, NONCE)
+    oenc, oh, oinfo = O.encode_full(d, level, PUB, EPH, NONCE)
+    assert enc == oenc and h == oh
+    for f in ("padding_len", "chunk_len", "bytes_ecc", "bytes_verifiable", "bytes_compressed", "bytes_encrypted",
+              "input_len", "output_len"):
+        assert getattr(info, f) == oinfo[f], (f, getattr(info, f), oinfo[f])
+    assert R.decode_stages(SK, h, enc, info.padding_len, level, n) == d

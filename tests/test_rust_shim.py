@@ -246,6 +246,11 @@ def test_reroute_patch_targets_the_seams_and_the_glue():
     # every rerouted call sits behind the feature, the CPU path stays the default
     assert added.count('#[cfg(feature = "hip")]') >= 10
     assert 'hip = ["dep:carbonado-hip"]' in added
+    # hip-stages: the whole encode()/decode() (host stages too) in one library call each
+    assert 'hip-stages = ["hip"]' in added
+    assert added.count('#[cfg(feature = "hip-stages")]') == 2
+    assert "carbonado_hip::encode(pubkey, input, format, None)" in added
+    assert "carbonado_hip::decode(secret_key, hash, input, padding, format)" in added
     # the public API (lib.rs:21-29) is untouched
     assert "src/lib.rs" not in files
     # each wrapper the patch calls exists in the crate, called with its arity
