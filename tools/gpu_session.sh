@@ -122,16 +122,9 @@ for s in "$@"; do
     kmab) for i in 1 2; do for km in 1 0; do CHIP_KM=$km run abi_latency_km${km}_$i 300 ./tools/abi_latency 40 ${KM_LEVELS:-12,4} ${KM_SIZES:-65536,262144,1048576,4194304}; done; done ;;
     kmtl) CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12,4 1048576
           run timeline_km_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tlkm -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
-    zcab) for i in 1 2; do for zc in default wc coherent noncoherent; do CHIP_ZC_IN=$zc run abi_latency_zc${zc}_$i 300 ./tools/abi_latency 40 12,4 262144,1048576,4194304; done; done
-          CHIP_ZC_IN=wc run timeline_km_wc 300 rocprofv3 --kernel-trace --stats -d $O/tlwc -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
     kmsg) for sg in 16 32; do CHIP_KM_SG=$sg run pytest_km_sg$sg 300 python3 -u -m pytest tests/test_gpu_km.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread; done ;;
     sgab) for i in 1 2; do for sg in 64 32 16; do CHIP_KM_SG=$sg run abi_latency_sg${sg}_$i 300 ./tools/abi_latency 40 12,4 262144,1048576,4194304; done; done
           CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12 1048576 ;;
-    thpab) cat /sys/kernel/mm/transparent_hugepage/enabled > $O/thp_setting.txt 2>&1 || true
-           for i in 1 2; do for zc in default thp; do CHIP_ZC_IN=$zc run abi_latency_zc${zc}_$i 300 ./tools/abi_latency 40 12,4 262144,1048576,4194304; done; done
-           CHIP_ZC_IN=thp CHIP_SINGLE_TRACE=1 run km_single_trace_thp 120 ./tools/abi_latency 10 12 1048576
-           CHIP_ZC_IN=thp run timeline_km_thp 300 rocprofv3 --kernel-trace --stats -d $O/tlthp -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576
-           run timeline_km_def 300 rocprofv3 --kernel-trace --stats -d $O/tldef -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
     zctests) run pytest_zc 600 python3 -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_written.py tests/test_gpu_zfec.py tests/test_gpu_km.py tests/test_gpu_reroute.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     thpout) cat /sys/kernel/mm/transparent_hugepage/enabled > $O/thp_setting.txt 2>&1 || true
             for i in 1 2; do for t in 1 0; do CHIP_OUT_THP=$t run abi_latency_outthp${t}_$i 300 ./tools/abi_latency 12 12,4,8 4194304,16777216; done; done ;;
