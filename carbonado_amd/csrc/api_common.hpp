@@ -211,6 +211,14 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
 // zc_parity_kernel reads the input from pinned memory and writes the parity
 // shards into pinned memory (zero-copy), copied out after.
 int single_zfec_encode_zc(Ctx *c, const uint8_t *in, uint64_t n, uint64_t C, uint8_t *out);
+// zfec decode of one object from k shares (shares[s] holds share sel[s], C
+// bytes): the host copies the shares into pinned memory, the decode kernel
+// reads them there and writes the k data shards there (zero-copy), and the
+// first olen bytes are copied to dst.  `meanwhile` (optional) runs on the host
+// while the kernel works.
+int single_zfec_decode_zc(Ctx *c, uint32_t k, uint32_t m, const uint8_t *const *shares,
+                          const std::vector<uint32_t> &sel, uint64_t C, uint8_t *dst, uint64_t olen,
+                          const std::function<void()> &meanwhile = {});
 // decode of one bao stream `in` (len bytes, content n, every node verified on
 // the device by KM) with the content bytes [0, olen) gathered from `in` by the
 // host meanwhile, into dst; on a mismatch dst is wiped and the status

@@ -327,6 +327,20 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             if (st != CHIP_OK) return st;
             cur = dst;
             cur_n = olen;
+        } else if (zfec && !bao && C && km_enabled()) {  // decoding.rs:95-99: shards by position
+            // zero-copy: the decode kernel reads the four primaries from pinned memory
+            auto prekey = [&] {
+                if (!ecies || !host::ecies_par_eligible(olen) || n < 65) return;
+                std::memcpy(pre_eph, in, 65);
+                have_pre = host::ecies_derive_key(secret_key, sk_len, pre_eph, pre_key) == CHIP_OK;
+            };
+            const uint8_t *sh[CHIP_FEC_K];
+            std::vector<uint32_t> sel(CHIP_FEC_K);
+            for (uint32_t s = 0; s < CHIP_FEC_K; ++s) { sh[s] = in + s * C; sel[s] = s; }
+            st = single_zfec_decode_zc(c, CHIP_FEC_K, CHIP_FEC_M, sh, sel, C, dst, olen, prekey);
+            if (st != CHIP_OK) return st;
+            cur = dst;
+            cur_n = olen;
         } else {
             const uint64_t in_bytes = bao ? bao_encoded_len(blen) : n;
             CHIP_HIP(grow(c->in, in_bytes));

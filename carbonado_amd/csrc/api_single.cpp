@@ -259,6 +259,41 @@ int single_zfec_encode_zc(Ctx *c, const uint8_t *in, uint64_t n, uint64_t C, uin
     return CHIP_OK;
 }
 
+int single_zfec_decode_zc(Ctx *c, uint32_t k, uint32_t m, const uint8_t *const *shares,
+                          const std::vector<uint32_t> &sel, uint64_t C, uint8_t *dst, uint64_t olen,
+                          const std::function<void()> &meanwhile) {
+    Trace trace("zfec decode");
+    const uint64_t kc = (uint64_t)k * C;
+    CHIP_HIP(grow_pinned_local(c->hin, kc));
+    CHIP_HIP(grow_pinned_local(c->hout, kc));
+    uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
+    // the k shares side by side at s * C, cut into equal runs across the copy threads
+    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, kc >> 17));
+    host::par_for(parts, [&](int i) {
+        uint64_t a = (kc * i / parts) & ~uint64_t(63);
+        const uint64_t b = i + 1 == parts ? kc : (kc * (i + 1) / parts) & ~uint64_t(63);
+        while (a < b) {
+            const uint64_t s = a / C, o = a % C, len = std::min(b - a, C - o);
+            host::ring_copy(hin + a, shares[s] + o, len);
+            a += len;
+        }
+    });
+    trace.mark("copy in");
+    std::vector<uint64_t> slot_off(k);
+    for (uint32_t s = 0; s < k; ++s) slot_off[s] = (uint64_t)s * C;
+    int st = zfec_decode_device(k, m, dev_ptr<const uint8_t>(hin), 0, slot_off, sel, C, 1, dev_ptr<uint8_t>(hout),
+                                0, c->stream);
+    if (st != CHIP_OK) return st;
+    trace.mark("launch");
+    advise_huge(dst, olen);
+    if (meanwhile) meanwhile();
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    trace.mark("sync");
+    copy_out(dst, hout, olen);
+    trace.mark("copy out");
+    return CHIP_OK;
+}
+
 int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const uint8_t *hash, uint8_t *dst,
                      uint64_t olen, const std::function<void()> &meanwhile) {
     Trace trace("decode");

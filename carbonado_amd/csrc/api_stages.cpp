@@ -139,7 +139,13 @@ int chip_zfec_decode_shares(uint32_t k, uint32_t m, const uint8_t *const *shares
     Ctx *c;
     st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    if (kc) {
+    if (kc && km_enabled()) {  // one object: zero-copy (the kernel reads and writes pinned memory)
+        std::vector<uint32_t> sel(k);
+        std::vector<const uint8_t *> src(k);
+        for (uint32_t s = 0; s < k; ++s) { sel[s] = idx[pos[s]]; src[s] = shares[pos[s]]; }
+        st = single_zfec_decode_zc(c, k, m, src.data(), sel, chunk_len, out, olen);
+        if (st != CHIP_OK) return st;
+    } else if (kc) {
         CHIP_HIP(grow(c->in, kc));
         CHIP_HIP(grow(c->out, kc));
         std::vector<uint32_t> sel(k);

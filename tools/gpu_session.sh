@@ -120,6 +120,7 @@ for s in "$@"; do
     abilat6) run abi_latency_patch 400 ./tools/abi_latency 40 12,4,8,15 1024,1048576,16777216 ;;
     kmtests) run pytest_km 600 python3 -u -m pytest tests/test_gpu_km.py tests/test_gpu_reroute.py tests/test_gpu_small.py tests/test_gpu_pipeline.py tests/test_gpu_bao.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     kmab) for i in 1 2; do for km in 1 0; do CHIP_KM=$km run abi_latency_km${km}_$i 300 ./tools/abi_latency 40 ${KM_LEVELS:-12,4} ${KM_SIZES:-65536,262144,1048576,4194304}; done; done ;;
+    zdtl) CHIP_SINGLE_TRACE=1 run zfec_decode_trace 120 ./tools/abi_latency 10 8 1048576 ;;
     kmtl) CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12,4 1048576
           run timeline_km_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tlkm -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
     kmsg) for sg in 16 32; do CHIP_KM_SG=$sg run pytest_km_sg$sg 300 python3 -u -m pytest tests/test_gpu_km.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread; done ;;
