@@ -137,6 +137,10 @@ struct D2h {
     bool direct = false;
 };
 hipError_t d2h_begin(Staging &sg, D2h &t, void *dst, const void *src, size_t n, hipStream_t s);
+// advise the 2 MiB-aligned interior of a host output of >= 4 MiB onto
+// transparent huge pages before the host threads first write it (d2h does
+// so for pageable destinations; CHIP_OUT_THP=0 turns it off)
+void advise_huge(void *p, uint64_t n);
 hipError_t d2h_issue(Staging &sg, const D2h &t, size_t j);
 hipError_t d2h_end(Staging &sg, const D2h &t);
 

@@ -327,7 +327,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             if (st != CHIP_OK) return st;
             cur = dst;
             cur_n = olen;
-        } else if (zfec && !bao && C && km_enabled()) {  // decoding.rs:95-99: shards by position
+        } else if (zfec && !bao && C && zc_ok(2 * CHIP_FEC_K * C)) {  // decoding.rs:95-99: shards by position
             // zero-copy: the decode kernel reads the four primaries from pinned memory
             auto prekey = [&] {
                 if (!ecies || !host::ecies_par_eligible(olen) || n < 65) return;

@@ -50,7 +50,7 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
         if (st != CHIP_OK) return st;
         st = single_encode_km(c, cur, cur_n, zfec ? inf.chunk_len : 0, final_len, out, hash);
         if (st != CHIP_OK) return st;
-    } else if (zfec && !bao && cur_n && km_enabled()) {  // encoding.rs:121-138 alone: zero-copy parity
+    } else if (zfec && !bao && cur_n && zc_ok((uint64_t)CHIP_FEC_M * inf.chunk_len)) {  // encoding.rs:121-138 alone: zero-copy parity
         Ctx *c;
         st = ctx_get(&c);
         if (st != CHIP_OK) return st;

@@ -3,6 +3,7 @@
 // chip_host_topology (where they sit).  Shared declarations: api_common.hpp.
 #include <pthread.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -354,6 +355,24 @@ hipError_t h2d(Staging &sg, void *dst, const void *src, size_t n, hipStream_t s)
     return e;
 }
 
+// The caller's output buffer, about to be written by the host threads: a
+// fresh allocation (a Rust Vec::with_capacity per call) takes a page fault per
+// 4 KiB on first touch, ~7 ms for a 35 MB level-12 stream of a 16 MiB object
+// (r11k).  Its 2 MiB-aligned interior is advised onto transparent huge pages
+// (advice only: no effect on pages already present, none on the bytes; a
+// failure is ignored).  CHIP_OUT_THP=0 turns it off.
+void advise_huge(void *p, uint64_t n) {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_OUT_THP");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    constexpr uintptr_t H = uintptr_t(2) << 20;
+    if (!on || n < 2 * H) return;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + H - 1) & ~(H - 1);
+    const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + n) & ~(H - 1);
+    if (b > a) (void)madvise(reinterpret_cast<void *>(a), b - a, MADV_HUGEPAGE);
+}
+
 // HBM -> host after the work already on s, in two halves so the caller can
 // work between them: d2h_begin enqueues the first ring pieces' DMA, d2h_end
 // copies every piece out (enqueuing the rest as ring slots free up) and
@@ -367,6 +386,7 @@ hipError_t d2h_begin(Staging &sg, D2h &t, void *dst, const void *src, size_t n, 
     }
     hipError_t e = stage_init(sg);
     if (e != hipSuccess) return e;
+    advise_huge(dst, n);  // the copy threads fault its pages in next
     t.np = (n + Staging::PIECE - 1) / Staging::PIECE;
     t.base = sg.next;
     sg.next += (unsigned)t.np;

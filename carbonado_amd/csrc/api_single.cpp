@@ -81,24 +81,6 @@ const HostGeo &host_geo(uint64_t zl, uint64_t nh) {
     return cache.emplace(key, std::move(g)).first->second;
 }
 
-// The caller's output buffer, about to be written by the host threads: a
-// fresh allocation (a Rust Vec::with_capacity per call) takes a page fault per
-// 4 KiB on first touch, ~7 ms for a 35 MB level-12 stream of a 16 MiB object
-// (r11k).  Its 2 MiB-aligned interior is advised onto transparent huge pages
-// (advice only: no effect on pages already present, none on the bytes; a
-// failure is ignored).  CHIP_OUT_THP=0 turns it off.
-void advise_huge(void *p, uint64_t n) {
-    static const bool on = [] {
-        const char *v = std::getenv("CHIP_OUT_THP");
-        return !(v && v[0] == '0' && v[1] == 0);
-    }();
-    constexpr uintptr_t H = uintptr_t(2) << 20;
-    if (!on || n < 2 * H) return;
-    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + H - 1) & ~(H - 1);
-    const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + n) & ~(H - 1);
-    if (b > a) (void)madvise(reinterpret_cast<void *>(a), b - a, MADV_HUGEPAGE);
-}
-
 // host copy threads for nc chunks: one per 128 KiB, at most 8
 int host_parts(uint64_t nc) { return (int)std::max<uint64_t>(1, std::min<uint64_t>(8, nc / 128)); }
 

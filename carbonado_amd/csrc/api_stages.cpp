@@ -25,14 +25,17 @@ int chip_snap_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t o
 int chip_ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const chip_ecies_inject *inject,
                        const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
     if (!pubkey || (!in && n) || !out || !out_len) return CHIP_ERR_INVALID_ARG;
-    return host::ecies_encrypt(pubkey, pubkey_len, inject ? inject->ephemeral_sk : nullptr,
-                               inject ? inject->nonce : nullptr, in, n, out, out_cap, out_len);
+    // a large message's AES-GCM on the stage pool (same bytes; small ones, or a busy pool, on this thread)
+    advise_huge(out, std::min(out_cap, n + host::ECIES_OVERHEAD));
+    return host::ecies_encrypt_par_plain(pubkey, pubkey_len, inject ? inject->ephemeral_sk : nullptr,
+                                         inject ? inject->nonce : nullptr, in, n, out, out_cap, out_len);
 }
 
 int chip_ecies_decrypt(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *in, uint64_t n, uint8_t *out,
                        uint64_t out_cap, uint64_t *out_len) {
     if (!secret_key || (!in && n) || !out_len) return CHIP_ERR_INVALID_ARG;
-    return host::ecies_decrypt(secret_key, sk_len, in, n, out, out_cap, out_len);
+    if (out) advise_huge(out, std::min(out_cap, n));
+    return host::ecies_decrypt_par(secret_key, sk_len, in, n, out, out_cap, out_len);
 }
 
 int chip_ecies_public_key(const uint8_t *secret_key, uint8_t pubkey[65]) {
@@ -105,7 +108,7 @@ int chip_zfec_encode(uint32_t k, uint32_t m, const uint8_t *in, uint64_t n, uint
     Ctx *c;
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    if (n && k == 4 && m == 8 && km_enabled()) {  // one 4-of-8 object: zero-copy parity, data shards by the host
+    if (n && k == 4 && m == 8 && zc_ok(total)) {  // one 4-of-8 object: zero-copy parity, data shards by the host
         st = single_zfec_encode_zc(c, in, n, C, out);
         if (st != CHIP_OK) return st;
     } else if (n) {
@@ -139,7 +142,7 @@ int chip_zfec_decode_shares(uint32_t k, uint32_t m, const uint8_t *const *shares
     Ctx *c;
     st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    if (kc && km_enabled()) {  // one object: zero-copy (the kernel reads and writes pinned memory)
+    if (kc && zc_ok(2 * kc)) {  // one object: zero-copy (the kernel reads and writes pinned memory)
         std::vector<uint32_t> sel(k);
         std::vector<const uint8_t *> src(k);
         for (uint32_t s = 0; s < k; ++s) { sel[s] = idx[pos[s]]; src[s] = shares[pos[s]]; }

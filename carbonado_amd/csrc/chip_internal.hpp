@@ -193,6 +193,11 @@ hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t in_stride, uin
 constexpr uint64_t KM_MAX_N = 32768;
 bool km_ok(uint64_t bao_n, uint64_t count);
 bool km_enabled();  // CHIP_KM (default on): also the single-object zero-copy zfec encode
+// the single-object zero-copy zfec paths (api_single.cpp) for a pinned
+// footprint of `bytes`: km_enabled() and at most ZC_MAX_BYTES (larger objects
+// take the staged copies through the 16 MiB ring instead of pinning their size)
+constexpr uint64_t ZC_MAX_BYTES = uint64_t(64) << 20;
+inline bool zc_ok(uint64_t bytes) { return bytes <= ZC_MAX_BYTES && km_enabled(); }
 uint64_t km_scratch_len(uint64_t bao_n);
 // bao of n content bytes at d_in (device or pinned host memory): the parent
 // nodes compactly into d_nodes (the node at stream offset o in front of chunk

@@ -187,3 +187,40 @@ def test_km_smaller_groups(gpu, sg):
     out = subprocess.run([sys.executable, "-c", _SG_CHILD, root], env=dict(os.environ, CHIP_KM_SG=sg),
                          capture_output=True, text=True, timeout=240)
     assert out.returncode == 0 and out.stdout.strip().endswith("OK"), out.stdout + out.stderr
+
+
+# zero-copy single-object zfec (api_single.cpp: single_zfec_encode_zc /
+# single_zfec_decode_zc) up to a pinned footprint of ZC_MAX_BYTES = 64 MiB,
+# the staged copies past it: the same bytes on both sides of the cap
+ZC = [1, 4095, 65536 + 17, 1 << 20, (8 << 20) - 3, 8 << 20, (8 << 20) + 1, 40 << 20]
+
+
+@pytest.mark.parametrize("n", ZC)
+def test_zero_copy_zfec_both_sides_of_the_cap(gpu, n):
+    import carbonado_amd as ca
+    d = _data(n, 21)
+    oshards, opad, oC = O.zfec_encode(d)
+    shards, pad, C = ca.encoding.zfec(d)
+    assert (shards, pad, C) == (oshards, opad, oC)
+    enc, h, info = ca.encode(b"", d, 8)  # encode() at Zfec alone
+    assert enc == oshards and info.padding_len == opad
+    assert ca.decoding.zfec(shards, pad) == d
+    assert ca.decode(b"", h, enc, pad, 8) == d
+    # two data shards lost: the decode kernel computes them from parity
+    keep = [2, 3, 5, 7]
+    parts = [shards[i * C:(i + 1) * C] for i in keep]
+    assert ca.decoding.zfec_chunks(parts, pad, keep) == d
+
+
+@pytest.mark.parametrize("k,m,lost", [(2, 3, [0]), (8, 16, [0, 1, 2, 3, 4, 5, 6, 7]), (11, 13, [0, 4]), (16, 20, [3, 9, 15])])
+def test_zero_copy_zfec_other_shapes(gpu, k, m, lost):
+    import carbonado_amd as ca
+    n = 300_001
+    d = _data(n, k * 100 + m)
+    shards, pad, C = ca.encoding.zfec(d, k, m)
+    oshards, opad, oC = O.zfec_encode(d, k, m)
+    assert (shards, pad, C) == (oshards, opad, oC)
+    keep = [i for i in range(m) if i not in lost][:k]
+    parts = [shards[i * C:(i + 1) * C] for i in keep]
+    out = ca.decoding.zfec_chunks(parts, pad, keep, k, m)
+    assert out == d == O.zfec_decode_shares(parts, keep, pad, k, m)

@@ -662,3 +662,25 @@ def test_compressed_receiver_keys(ca):
     for pk in bad:
         with pytest.raises(EciesError):
             ca.encoding.ecies(pk, msg, ephemeral_sk=eph, nonce=nonce)
+
+
+@pytest.mark.parametrize("n", [256 * 1024 - 97, 256 * 1024, 300_001, 5 << 20])
+def test_ecies_stage_functions_on_the_pool_match_oracle(ca, n):
+    """chip_ecies_encrypt / chip_ecies_decrypt (the stage functions) split a
+    large message's AES-GCM over the stage pool (host_stages_par.cpp,
+    ecies_encrypt_par_plain / ecies_decrypt_par, from STAGE_PAR_MIN = 256 KiB):
+    the envelope is byte-identical to the C oracle's with the same injected
+    key and nonce, it decrypts back, and a flipped ciphertext byte is refused
+    with the written plaintext wiped."""
+    from carbonado_amd.error import EciesError
+    sk = H.sha256(b"pool receiver")
+    pub = ca.encoding.public_key(sk)
+    eph, nonce = H.sha256(b"pool eph"), H.sha256(b"pool nonce")[:16]
+    d = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+    e = ca.encoding.ecies(pub, d, ephemeral_sk=eph, nonce=nonce)
+    assert e == O.c_ecies_encrypt(pub, d, eph, nonce)
+    assert ca.decoding.ecies(e, sk) == d == O.c_ecies_decrypt(sk, e)
+    bad = bytearray(e)
+    bad[len(bad) // 2] ^= 1
+    with pytest.raises(EciesError):
+        ca.decoding.ecies(bytes(bad), sk)

@@ -30,6 +30,18 @@ static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// ABI_LAT_STAGES=1: each patch-sequence step's time to stderr (us)
+static void stage_mark(const char *what, double *t) {
+    static const bool on = [] {
+        const char *v = std::getenv("ABI_LAT_STAGES");
+        return v && v[0] == '1';
+    }();
+    if (!on) return;
+    const double n = now_us();
+    std::fprintf(stderr, "[patch] %-14s %8.1f us\n", what, n - *t);
+    *t = n;
+}
+
 static std::vector<uint64_t> parse_list(const char *s, std::vector<uint64_t> def) {
     if (!s) return def;
     std::vector<uint64_t> v;
@@ -62,10 +74,12 @@ struct Obj {
 static int patch_encode(const Obj &o, std::vector<uint8_t> *keep, uint8_t hash[32], chip_encode_info *info) {
     const uint8_t *cur = o.in.data();
     uint64_t cur_n = o.in.size();
+    double t = now_us();
     Fresh snap(o.level & CHIP_FORMAT_SNAPPY ? chip_snap_max_len(cur_n) : 0);
     if (o.level & CHIP_FORMAT_SNAPPY) {
         uint64_t l = 0;
         if (int st = chip_snap_compress(cur, cur_n, snap.p, chip_snap_max_len(cur_n), &l)) return st;
+        stage_mark("enc snap", &t);
         cur = snap.p;
         cur_n = l;
     }
@@ -73,6 +87,7 @@ static int patch_encode(const Obj &o, std::vector<uint8_t> *keep, uint8_t hash[3
     if (o.level & CHIP_FORMAT_ECIES) {
         uint64_t l = 0;
         if (int st = chip_ecies_encrypt(o.pub, 65, &o.inj, cur, cur_n, ecies.p, cur_n + 97, &l)) return st;
+        stage_mark("enc ecies", &t);
         cur = ecies.p;
         cur_n = l;
     }
@@ -97,6 +112,7 @@ static int patch_encode(const Obj &o, std::vector<uint8_t> *keep, uint8_t hash[3
         st = chip_bao_encode(cur, cur_n, out.p, cap, &len, hash);
         if (st == CHIP_OK && keep) keep->assign(out.p, out.p + len);
     }
+    stage_mark("enc zfec/bao", &t);
     return st;
 }
 
@@ -106,6 +122,7 @@ static int patch_decode(const Obj &o, const std::vector<uint8_t> &enc, const uin
     const int zb = o.level & (CHIP_FORMAT_ZFEC | CHIP_FORMAT_BAO);
     const uint8_t *cur = enc.data();
     uint64_t cur_n = enc.size(), len = 0;
+    double t = now_us();
     Fresh dev(std::max<uint64_t>(cur_n, 1024));
     int st = CHIP_OK;
     if (zb == (CHIP_FORMAT_ZFEC | CHIP_FORMAT_BAO)) {
@@ -116,11 +133,13 @@ static int patch_decode(const Obj &o, const std::vector<uint8_t> &enc, const uin
         st = chip_bao_decode(cur, cur_n, hash, 32, dev.p, cur_n, &len);
     }
     if (st) return st;
+    stage_mark("dec zfec/bao", &t);
     cur = dev.p;
     cur_n = len;
     Fresh dec(o.level & CHIP_FORMAT_ECIES ? cur_n : 0);
     if (o.level & CHIP_FORMAT_ECIES) {
         if ((st = chip_ecies_decrypt(o.sk, 32, cur, cur_n, dec.p, cur_n, &len))) return st;
+        stage_mark("dec ecies", &t);
         cur = dec.p;
         cur_n = len;
     }
@@ -128,6 +147,7 @@ static int patch_decode(const Obj &o, const std::vector<uint8_t> &enc, const uin
     Fresh un(o.level & CHIP_FORMAT_SNAPPY ? ucap : 0);
     if (o.level & CHIP_FORMAT_SNAPPY) {
         if ((st = chip_snap_decompress(cur, cur_n, un.p, ucap, &len))) return st;
+        stage_mark("dec snap", &t);
         cur = un.p;
         cur_n = len;
     }

@@ -120,6 +120,11 @@ for s in "$@"; do
     abilat6) run abi_latency_patch 400 ./tools/abi_latency 40 12,4,8,15 1024,1048576,16777216 ;;
     kmtests) run pytest_km 600 python3 -u -m pytest tests/test_gpu_km.py tests/test_gpu_reroute.py tests/test_gpu_small.py tests/test_gpu_pipeline.py tests/test_gpu_bao.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     kmab) for i in 1 2; do for km in 1 0; do CHIP_KM=$km run abi_latency_km${km}_$i 300 ./tools/abi_latency 40 ${KM_LEVELS:-12,4} ${KM_SIZES:-65536,262144,1048576,4194304}; done; done ;;
+    thp9) cat /sys/kernel/mm/transparent_hugepage/enabled /sys/kernel/mm/transparent_hugepage/defrag > $O/thp_setting.txt 2>&1 || true
+          for i in 1 2; do for t in 1 0; do CHIP_OUT_THP=$t run abi_latency_thp9_${t}_$i 300 ./tools/abi_latency 12 9,8 16777216; done; done ;;
+    kmz) run pytest_kmz 600 python3 -u -m pytest tests/test_gpu_km.py tests/test_gpu_zfec.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    stg9) for km in 1 0; do CHIP_KM=$km ABI_LAT_STAGES=1 CHIP_SINGLE_TRACE=1 run patch_stages_km$km 120 ./tools/abi_latency 4 9,15 16777216,1048576; done ;;
+    thp15) for i in 1 2; do for t in 1 0; do CHIP_OUT_THP=$t run abi_latency_thp15_${t}_$i 300 ./tools/abi_latency 8 15,9,12 16777216,1048576; done; done ;;
     zdtl) CHIP_SINGLE_TRACE=1 run zfec_decode_trace 120 ./tools/abi_latency 10 8 1048576 ;;
     kmtl) CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12,4 1048576
           run timeline_km_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tlkm -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
