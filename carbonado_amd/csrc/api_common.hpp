@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
@@ -203,6 +204,31 @@ int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const ui
                      uint64_t *filled = nullptr, const host::EciesKey *prepared = nullptr, bool par = false);
 
 // ---- one object from host memory on KM (api_single.cpp) ---------------------
+// CHIP_SINGLE_TRACE=1: the host-side phases of each call to stderr (us)
+struct Trace {
+    const char *what;
+    bool on;
+    std::chrono::steady_clock::time_point t0, last;
+    explicit Trace(const char *w) : what(w), on(enabled()) {
+        if (on) t0 = last = std::chrono::steady_clock::now();
+    }
+    static bool enabled() {
+        static const bool e = [] {
+            const char *v = std::getenv("CHIP_SINGLE_TRACE");
+            return v && v[0] == '1';
+        }();
+        return e;
+    }
+    void mark(const char *phase) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[single %s] %-12s +%7.1f us (%7.1f)\n", what, phase,
+                     std::chrono::duration<double, std::micro>(now - last).count(),
+                     std::chrono::duration<double, std::micro>(now - t0).count());
+        last = now;
+    }
+};
+
 // encode() at Zfec|Bao (C > 0: the zfec shard length) or bao of the content
 // (C == 0) of cur_n bytes at `cur` into out[0, final_len) and the root hash,
 // with the split copy-back: the host writes the stream's header and the chunks

@@ -28,12 +28,14 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
     const uint8_t *cur = in;
     uint64_t cur_n = n, bc = 0, be = 0;
     if (has_host_stages(format)) {
+        Trace trace("host stages");
         t_stage.resize(host_stage_max(format, n) + 1);
         int st = host_stages_into(format, pubkey, pubkey_len, inject ? inject->ephemeral_sk : nullptr,
                                   inject ? inject->nonce : nullptr, in, n, t_stage.data(), t_stage.size(), t_tmp,
                                   &cur_n, &bc, &be, nullptr, nullptr, nullptr, true);
         if (st != CHIP_OK) return st;
         cur = t_stage.data();
+        trace.mark("encode");
     }
     chip_encode_info inf;
     uint64_t cur_len, final_len;

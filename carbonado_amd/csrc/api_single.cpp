@@ -81,33 +81,18 @@ const HostGeo &host_geo(uint64_t zl, uint64_t nh) {
     return cache.emplace(key, std::move(g)).first->second;
 }
 
-// host copy threads for nc chunks: one per 128 KiB, at most 8
-int host_parts(uint64_t nc) { return (int)std::max<uint64_t>(1, std::min<uint64_t>(8, nc / 128)); }
-
-// CHIP_SINGLE_TRACE=1: the host-side phases of each call to stderr (us)
-struct Trace {
-    const char *what;
-    bool on;
-    std::chrono::steady_clock::time_point t0, last;
-    explicit Trace(const char *w) : what(w), on(enabled()) {
-        if (on) t0 = last = std::chrono::steady_clock::now();
-    }
-    static bool enabled() {
-        static const bool e = [] {
-            const char *v = std::getenv("CHIP_SINGLE_TRACE");
-            return v && v[0] == '1';
-        }();
-        return e;
-    }
-    void mark(const char *phase) {
-        if (!on) return;
-        const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[single %s] %-12s +%7.1f us (%7.1f)\n", what, phase,
-                     std::chrono::duration<double, std::micro>(now - last).count(),
-                     std::chrono::duration<double, std::micro>(now - t0).count());
-        last = now;
-    }
-};
+// host copy threads for `bytes`: one per 128 KiB, at most CHIP_ZC_THREADS
+// (default 8; an A/B knob: one thread streams ~80 GB/s into pinned memory from
+// a cached source, tools/bar_probe)
+int copy_parts(uint64_t bytes) {
+    static const uint64_t cap = [] {
+        const char *v = std::getenv("CHIP_ZC_THREADS");
+        const int t = v ? std::atoi(v) : 8;
+        return (uint64_t)(t >= 1 && t <= 32 ? t : 8);
+    }();
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(cap, bytes >> 17));
+}
+int host_parts(uint64_t nc) { return copy_parts(nc * 1024); }
 
 }  // namespace
 
@@ -135,7 +120,7 @@ T *dev_ptr(void *host) {
 // n bytes into pinned memory on a few threads (streaming stores: only the
 // device reads them next)
 void copy_in(uint8_t *dst, const uint8_t *src, uint64_t n) {
-    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, n >> 17));  // 128 KiB a thread
+    const int parts = copy_parts(n);
     host::par_for(parts, [&](int i) {
         const uint64_t a = (n * i / parts) & ~uint64_t(63), b = i + 1 == parts ? n : (n * (i + 1) / parts) & ~uint64_t(63);
         host::ring_copy(dst + a, src + a, b - a);
@@ -143,7 +128,7 @@ void copy_in(uint8_t *dst, const uint8_t *src, uint64_t n) {
 }
 
 void copy_out(uint8_t *dst, const uint8_t *src, uint64_t n) {
-    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, n >> 17));
+    const int parts = copy_parts(n);
     host::par_for(parts, [&](int i) {
         const uint64_t a = n * i / parts, b = n * (i + 1) / parts;
         std::memcpy(dst + a, src + a, b - a);
@@ -250,7 +235,7 @@ int single_zfec_decode_zc(Ctx *c, uint32_t k, uint32_t m, const uint8_t *const *
     CHIP_HIP(grow_pinned_local(c->hout, kc));
     uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
     // the k shares side by side at s * C, cut into equal runs across the copy threads
-    const int parts = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, kc >> 17));
+    const int parts = copy_parts(kc);
     host::par_for(parts, [&](int i) {
         uint64_t a = (kc * i / parts) & ~uint64_t(63);
         const uint64_t b = i + 1 == parts ? kc : (kc * (i + 1) / parts) & ~uint64_t(63);

@@ -78,6 +78,87 @@ __device__ __forceinline__ void node_out(const MultiArgs &a, uint64_t P, int lev
     }
 }
 
+// Phase 4 of the KM kernels: publish this group's CV (word t of it in lanes
+// 0-7: `mycv`); the workgroup that finishes last walks levels LOGS + 1 ..
+// root over the G group CVs in `cv` (LDS [2][GMAX][8]), decode checking the
+// top's stored nodes staged in `stored` (LDS, GMAX * 4 x 16 B).
+template <int MODE, int LOGS>
+__device__ __forceinline__ void km_top(const MultiArgs &a, uint32_t mycv, uint32_t (*cv)[GMAX][8], u32x4 *stored,
+                                       uint32_t &last, const uint8_t *mbase, uint32_t (*msg)[16],
+                                       const small::MsgIdx &mi, uint32_t iv0, uint32_t iv1) {
+    const int t = threadIdx.x, q = t & 3, g = t >> 2;
+    const uint64_t grp = blockIdx.x, G = gridDim.x, N = a.N;
+    if (t < 8) *glb(reinterpret_cast<uint32_t *>(a.gcv + grp * 32) + t) = mycv;
+    __syncthreads();
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // my group CV (and nodes) before the count
+        const uint32_t done = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = done + 1 == (uint32_t)G;
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every group's CV visible to every lane
+    for (uint64_t i = t; i < 8 * G; i += TPB)
+        cv[0][i >> 3][i & 7] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(a.gcv) + i, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MODE == 1) {  // level by level: pairs floor(cnt / 2), 16 B per lane of a quad
+        uint64_t cnt = G, base = 0;
+        for (int level = LOGS + 1; cnt > 1; ++level) {
+            const uint64_t pairs = cnt / 2;
+            for (uint64_t i = t; i < 4 * pairs; i += TPB)
+                stored[4 * base + i] = load16_a8(a.stream + parent_stream_off((i >> 2) << level, level, N) + 16 * (i & 3));
+            base += pairs;
+            cnt = (cnt + 1) / 2;
+        }
+    }
+    __syncthreads();
+    uint64_t nbase = 0;  // decode: index of this level's first node in `stored`
+    int cur = 0;
+    uint64_t cnt_prev = G;
+    bool ok = true;
+    for (int level = LOGS + 1; cnt_prev > 1; ++level) {
+        const uint64_t cnt = (cnt_prev + 1) / 2;
+        for (uint64_t p = g; p < cnt; p += QUADS) {
+            if (2 * p + 1 >= cnt_prev) {
+                cv[cur ^ 1][p][q] = cv[cur][2 * p][q];
+                cv[cur ^ 1][p][4 + q] = cv[cur][2 * p][4 + q];
+                continue;
+            }
+            const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cv[cur][2 * p + (q >> 1)][4 * (q & 1)]);
+            *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = mw;
+            wave_sync();
+            const bool root = cnt == 1;
+            uint32_t h0 = iv0, h1 = iv1;
+            small::compress4(h0, h1, mbase, mi, q, iv0, 0, 64, F_PARENT | (root ? F_ROOT : 0u));
+            wave_sync();
+            if (MODE == 0) {
+                node_out(a, p, level, q, mw);
+            } else {
+                const u32x4 s = stored[4 * (nbase + p) + q];
+                ok &= s.x == mw.x && s.y == mw.y && s.z == mw.z && s.w == mw.w;
+            }
+            if (root) {
+                uint32_t *hp = reinterpret_cast<uint32_t *>(a.hash);
+                if (MODE == 0) {
+                    hp[q] = h0;
+                    hp[4 + q] = h1;
+                } else {
+                    ok &= hp[q] == h0 && hp[4 + q] == h1;
+                }
+            } else {
+                cv[cur ^ 1][p][q] = h0;
+                cv[cur ^ 1][p][4 + q] = h1;
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+        nbase += cnt_prev / 2;
+        cnt_prev = cnt;
+    }
+    if (MODE == 1 && !ok) flag_mismatch(a.status, 0);
+}
+
 // SG chunks per workgroup (a power of two <= QUADS; fewer spreads a small
 // object's loads over more CUs, the top walk then starts lower)
 template <int MODE, int SG>
@@ -89,7 +170,7 @@ __global__ __launch_bounds__(TPB) void km_kernel(MultiArgs a) {
     __shared__ uint32_t last;
     __shared__ __attribute__((aligned(16))) u32x4 stored[MODE == 1 ? GMAX * 4 : 4];  // decode: the top's nodes
     const int t = threadIdx.x, q = t & 3, g = t >> 2;
-    const uint64_t grp = blockIdx.x, G = gridDim.x, N = a.N, n = a.n;
+    const uint64_t grp = blockIdx.x, N = a.N, n = a.n;
     const uint64_t c0 = grp * SG, r = N - c0 < (uint64_t)SG ? N - c0 : (uint64_t)SG;  // my chunks
     bool ok = true;
 
@@ -192,75 +273,147 @@ __global__ __launch_bounds__(TPB) void km_kernel(MultiArgs a) {
     if (MODE == 1 && !ok) flag_mismatch(a.status, 0);
 
     // ---- phase 4: publish the group CV; the last workgroup walks the top
-    if (t < 8) *glb(reinterpret_cast<uint32_t *>(a.gcv + grp * 32) + t) = cvs[cur][0][t];
-    __syncthreads();
-    if (t == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // my group CV (and nodes) before the count
-        const uint32_t done = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        last = done + 1 == (uint32_t)G;
-    }
-    __syncthreads();
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every group's CV visible to every lane
-    for (uint64_t i = t; i < 8 * G; i += TPB)
-        cvs[0][i >> 3][i & 7] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(a.gcv) + i, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-    if (t == 0) __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (MODE == 1) {  // level by level: pairs floor(cnt / 2), 16 B per lane of a quad
-        uint64_t cnt = G, base = 0;
-        for (int level = LOGS + 1; cnt > 1; ++level) {
-            const uint64_t pairs = cnt / 2;
-            for (uint64_t i = t; i < 4 * pairs; i += TPB)
-                stored[4 * base + i] = load16_a8(a.stream + parent_stream_off((i >> 2) << level, level, N) + 16 * (i & 3));
-            base += pairs;
-            cnt = (cnt + 1) / 2;
+    km_top<MODE, LOGS>(a, t < 8 ? cvs[cur][0][t] : 0u, cvs, stored, last, mbase, msg, mi, iv0, iv1);
+}
+
+// ---- KM with each workgroup's range staged in LDS ----------------------------
+// km_kernel's quads load 16 B of each 64-B block of their chunk: a chunk's 16
+// loads sit 64 B apart and a wave's 16 chunks 1 KiB apart.  Over PCIe from
+// pinned host memory that pattern reads a 2.2 MB stream at ~39 GB/s, whole
+// contiguous rows at ~49 (tools/bar_probe, profiles/r11_session/r11v/r11t_bar.log).
+// So where the chunks come from pinned memory -- decode (the stream) and bao
+// of the content (the content) -- each workgroup first copies its contiguous
+// range into LDS, 4 KiB per instruction across the workgroup: decode, the
+// group's region of the stream (its left-spine nodes, then its chunks and
+// nodes in pre-order: 64 chunks + 63 nodes = 69,568 B for a full group);
+// encode, its 64 KiB of content.  The quads hash their chunks from LDS and
+// decode checks the group's stored nodes there; the top walk's buffers reuse
+// the staging area once the group's levels are done.  Same bytes and verdicts
+// as km_kernel (CHIP_KM_STAGE=0 keeps km_kernel for the A/B).
+constexpr int STAGE_VEC = 17;  // 16-B loads per lane
+static_assert(STAGE_VEC * TPB * 16 >= 64 * 1024 + 63 * 64 + 15, "a group's stream region and its alignment slack");
+static_assert(STAGE_VEC * TPB * 16 >= 2 * GMAX * 32 + GMAX * 64, "the top walk's CVs and stored nodes");
+
+template <int MODE>
+__global__ __launch_bounds__(TPB) void km_staged_kernel(MultiArgs a) {
+    constexpr int LOGS = 6;
+    __shared__ __attribute__((aligned(16))) u32x4 stage[STAGE_VEC * TPB];
+    __shared__ __attribute__((aligned(16))) uint32_t cvs[2][S][8];
+    __shared__ __attribute__((aligned(16))) uint32_t msg[QUADS][16];
+    __shared__ uint32_t last;
+    const int t = threadIdx.x, q = t & 3, g = t >> 2;
+    const uint64_t grp = blockIdx.x, N = a.N, n = a.n;
+    const uint64_t c0 = grp * S, r = N - c0 < (uint64_t)S ? N - c0 : (uint64_t)S;  // my chunks
+    bool ok = true;
+
+    // ---- phase 1 (decode): the header checked, content bytes out
+    if (MODE == 1) {
+        if (grp == 0 && t == 0 && *reinterpret_cast<const uint64_t *>(a.stream) != n) ok = false;
+        const uint64_t lim = a.out ? (a.out_limit < (c0 + r) * 1024 ? a.out_limit : (c0 + r) * 1024) : 0;
+        for (uint64_t o = c0 * 1024 + 16 * (uint64_t)t; o < lim; o += 16 * TPB) {
+            const uint8_t *p = a.stream + chunk_stream_off(o / 1024, N) + o % 1024;
+            const uint64_t left = lim - o;
+            if (left >= 16) *glb(reinterpret_cast<u32x4 *>(a.out + o)) = load16_a8(p);
+            else store16_partial(a.out + o, load16_partial(p, (uint32_t)left), (uint32_t)left);
         }
     }
+
+    // ---- phase 2a: my range [r0, r1) of the source into LDS (zeros past r1)
+    const uint64_t cl = c0 + r - 1;  // my last chunk
+    uint64_t r0, r1;
+    const uint8_t *src;
+    if (MODE == 1) {
+        const int sp = parents_at(c0, N);
+        r0 = chunk_stream_off(c0, N) - 64 * (uint64_t)(sp < LOGS ? sp : LOGS);  // my left spine's top node
+        r1 = chunk_stream_off(cl, N) + (n - 1024 * cl < 1024 ? n - 1024 * cl : 1024);
+        src = a.stream;
+    } else {
+        r0 = c0 * 1024;
+        r1 = (c0 + r) * 1024 < a.valid ? (c0 + r) * 1024 : a.valid;
+        src = a.src;
+    }
+    const uint8_t *const sb = reinterpret_cast<const uint8_t *>(stage);
+    const uint8_t *al = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(src + r0) & ~uintptr_t(15));
+    const uint32_t shift = (uint32_t)(src + r0 - al);  // LDS byte of source byte r0
+    {
+        const uint8_t *end = src + r1;
+        u32x4 v[STAGE_VEC];
+#pragma unroll
+        for (int j = 0; j < STAGE_VEC; ++j) {
+            const uint8_t *p = al + 16 * (uint64_t)(t + TPB * j);
+            v[j] = p + 16 <= end ? load16_a8(p) : p < end ? load16_partial(p, (uint32_t)(end - p)) : u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int j = 0; j < STAGE_VEC; ++j) stage[t + TPB * j] = v[j];
+    }
     __syncthreads();
-    uint64_t nbase = 0;  // decode: index of this level's first node in `stored`
-    cur = 0;
-    cnt_prev = G;
-    ok = true;
-    for (int level = LOGS + 1; cnt_prev > 1; ++level) {
+
+    // ---- phase 2b: chunk CVs from LDS, one quad per chunk
+    const uint32_t slot = (uint32_t)(reinterpret_cast<uintptr_t>(&msg[g][0]) - reinterpret_cast<uintptr_t>(&msg[0][0]));
+    const uint8_t *mbase = reinterpret_cast<const uint8_t *>(&msg[0][0]);
+    const small::MsgIdx mi(q, slot);
+    const uint32_t iv0 = q == 0 ? IV(0) : q == 1 ? IV(1) : q == 2 ? IV(2) : IV(3);
+    const uint32_t iv1 = q == 0 ? IV(4) : q == 1 ? IV(5) : q == 2 ? IV(6) : IV(7);
+    if ((uint64_t)g < r) {
+        const uint64_t c = c0 + g;
+        const uint64_t rem = n - c * 1024;
+        const uint32_t clen = rem < 1024 ? (uint32_t)rem : 1024u;
+        const uint32_t nb = (clen + 63) / 64;  // N >= 2: every chunk holds at least one byte
+        const small::MsgIdx mc(q, shift + (uint32_t)((MODE == 1 ? chunk_stream_off(c, N) : c * 1024) - r0));
+        uint32_t h0 = iv0, h1 = iv1;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            if ((uint32_t)b < nb) {
+                const bool lastb = (uint32_t)b + 1 == nb;
+                const uint32_t flags = (b == 0 ? F_CHUNK_START : 0u) | (lastb ? F_CHUNK_END : 0u);
+                small::compress4(h0, h1, sb + 64 * b, mc, q, iv0, c, lastb ? clen - 64 * b : 64u, flags);
+            }
+        }
+        cvs[0][g][q] = h0;
+        cvs[0][g][4 + q] = h1;
+    }
+    __syncthreads();
+
+    // ---- phase 3: the group's levels 1 .. 6, one quad per parent
+    int cur = 0;
+    uint64_t cnt_prev = r;
+    for (int level = 1; level <= LOGS && cnt_prev > 1; ++level) {
         const uint64_t cnt = (cnt_prev + 1) / 2;
-        for (uint64_t p = g; p < cnt; p += QUADS) {
-            if (2 * p + 1 >= cnt_prev) {
+        if ((uint64_t)g < cnt) {
+            const uint64_t p = g;
+            if (2 * p + 1 >= cnt_prev) {  // odd last node: promoted unchanged
                 cvs[cur ^ 1][p][q] = cvs[cur][2 * p][q];
                 cvs[cur ^ 1][p][4 + q] = cvs[cur][2 * p][4 + q];
-                continue;
-            }
-            const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cvs[cur][2 * p + (q >> 1)][4 * (q & 1)]);
-            *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = mw;
-            wave_sync();
-            const bool root = cnt == 1;
-            uint32_t h0 = iv0, h1 = iv1;
-            small::compress4(h0, h1, mbase, mi, q, iv0, 0, 64, F_PARENT | (root ? F_ROOT : 0u));
-            wave_sync();
-            if (MODE == 0) {
-                node_out(a, p, level, q, mw);
             } else {
-                const u32x4 s = stored[4 * (nbase + p) + q];
-                ok &= s.x == mw.x && s.y == mw.y && s.z == mw.z && s.w == mw.w;
-            }
-            if (root) {
-                uint32_t *hp = reinterpret_cast<uint32_t *>(a.hash);
+                const u32x4 mw = *reinterpret_cast<const u32x4 *>(&cvs[cur][2 * p + (q >> 1)][4 * (q & 1)]);
+                *reinterpret_cast<u32x4 *>(&msg[g][4 * q]) = mw;
+                wave_sync();
+                uint32_t h0 = iv0, h1 = iv1;
+                small::compress4(h0, h1, mbase, mi, q, iv0, 0, 64, F_PARENT);
+                wave_sync();
+                const uint64_t P = (c0 >> level) + p;
                 if (MODE == 0) {
-                    hp[q] = h0;
-                    hp[4 + q] = h1;
-                } else {
-                    ok &= hp[q] == h0 && hp[4 + q] == h1;
+                    node_out(a, P, level, q, mw);
+                } else {  // the stored node, staged with my region (4-B aligned words)
+                    const uint32_t *s = reinterpret_cast<const uint32_t *>(
+                        sb + shift + (parent_stream_off(P << level, level, N) - r0) + 16 * q);
+                    ok &= s[0] == mw.x && s[1] == mw.y && s[2] == mw.z && s[3] == mw.w;
                 }
-            } else {
                 cvs[cur ^ 1][p][q] = h0;
                 cvs[cur ^ 1][p][4 + q] = h1;
             }
         }
         __syncthreads();
         cur ^= 1;
-        nbase += cnt_prev / 2;
         cnt_prev = cnt;
     }
     if (MODE == 1 && !ok) flag_mismatch(a.status, 0);
+
+    // ---- phase 4: publish the group CV; the last workgroup walks the top in
+    // the staging area ([2][GMAX][8] CVs, then GMAX * 4 stored node quarters)
+    u32x4 *const top = stage;
+    km_top<MODE, LOGS>(a, t < 8 ? cvs[cur][0][t] : 0u, reinterpret_cast<uint32_t (*)[GMAX][8]>(top),
+                       top + 2 * GMAX * 8 / 4, last, mbase, msg, mi, iv0, iv1);
 }
 
 // A 4-of-8 zfec encode into the chunk slots of the Zfec|Bao stream: one 16-B
@@ -354,6 +507,15 @@ bool enabled() {
     return on;
 }
 
+// CHIP_KM_STAGE=0: km_kernel everywhere (the A/B against km_staged_kernel)
+bool staged_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("CHIP_KM_STAGE");
+        return !(e && !std::strcmp(e, "0"));
+    }();
+    return on;
+}
+
 // chunks per workgroup: CHIP_KM_SG (16 / 32 / 64, A/B runs), default 64;
 // never so few that the groups overflow the top walk's LDS
 int group_chunks(uint64_t N) {
@@ -377,6 +539,12 @@ hipError_t launch(int mode, MultiArgs a, hipStream_t stream) {
     a.counter = q + QUEUE_KM;
     auto k = mode == 0 ? (sg == 16 ? km_kernel<0, 16> : sg == 32 ? km_kernel<0, 32> : km_kernel<0, 64>)
                        : (sg == 16 ? km_kernel<1, 16> : sg == 32 ? km_kernel<1, 32> : km_kernel<1, 64>);
+    // the staged kernel where the chunks come from one contiguous source (the
+    // stream to verify, or the content), 4-B aligned
+    const uint8_t *from = mode == 1 ? a.stream : a.src;
+    if (sg == S && staged_on() && (mode == 1 || a.n_in == a.N) && from &&
+        (reinterpret_cast<uintptr_t>(from) & 3) == 0)
+        k = mode == 0 ? km_staged_kernel<0> : km_staged_kernel<1>;
     hipLaunchKernelGGL(k, dim3((unsigned)G), dim3(TPB), 0, stream, a);
     return hipGetLastError();
 }

@@ -174,17 +174,20 @@ print("BAD", bad) if bad else print("OK")
 """
 
 
-@pytest.mark.parametrize("sg", ["16", "32"])
-def test_km_smaller_groups(gpu, sg):
+@pytest.mark.parametrize("env", [{"CHIP_KM_SG": "16"}, {"CHIP_KM_SG": "32"}, {"CHIP_KM_STAGE": "0"}],
+                         ids=["sg16", "sg32", "unstaged"])
+def test_km_smaller_groups(gpu, env):
     """KM with 16 / 32 chunks per workgroup (CHIP_KM_SG, read once per
     process: a child process): the group levels stop lower and the top walk
-    starts lower; same bytes, same verdicts."""
+    starts lower; and km_kernel where km_staged_kernel runs by default
+    (CHIP_KM_STAGE=0: decode and bao of the content with each quad loading
+    its chunk itself).  Same bytes, same verdicts."""
     import os
     import subprocess
     import sys
     from pathlib import Path
     root = str(Path(__file__).resolve().parents[1])
-    out = subprocess.run([sys.executable, "-c", _SG_CHILD, root], env=dict(os.environ, CHIP_KM_SG=sg),
+    out = subprocess.run([sys.executable, "-c", _SG_CHILD, root], env=dict(os.environ, **env),
                          capture_output=True, text=True, timeout=240)
     assert out.returncode == 0 and out.stdout.strip().endswith("OK"), out.stdout + out.stderr
 

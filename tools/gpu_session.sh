@@ -125,6 +125,10 @@ for s in "$@"; do
     kmz) run pytest_kmz 600 python3 -u -m pytest tests/test_gpu_km.py tests/test_gpu_zfec.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     stg9) for km in 1 0; do CHIP_KM=$km ABI_LAT_STAGES=1 CHIP_SINGLE_TRACE=1 run patch_stages_km$km 120 ./tools/abi_latency 4 9,15 16777216,1048576; done ;;
     thp15) for i in 1 2; do for t in 1 0; do CHIP_OUT_THP=$t run abi_latency_thp15_${t}_$i 300 ./tools/abi_latency 8 15,9,12 16777216,1048576; done; done ;;
+    zcthr) for i in 1 2; do for t in 8 1 2 4; do CHIP_ZC_THREADS=$t run abi_latency_zcthr${t}_$i 300 ./tools/abi_latency 30 12,4,8 1048576,4194304; done; done
+           for t in 1 8; do CHIP_ZC_THREADS=$t CHIP_SINGLE_TRACE=1 run zcthr_trace$t 120 ./tools/abi_latency 6 12 1048576; done ;;
+    kmstage) for i in 1 2; do for st in 1 0; do CHIP_KM_STAGE=$st run abi_latency_stage${st}_$i 300 ./tools/abi_latency 30 12,4 66560,262144,1048576,4194304,16777216; done; done
+             for st in 1 0; do CHIP_KM_STAGE=$st run timeline_stage$st 300 rocprofv3 --kernel-trace --stats -d $O/tlst$st -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576; done ;;
     zdtl) CHIP_SINGLE_TRACE=1 run zfec_decode_trace 120 ./tools/abi_latency 10 8 1048576 ;;
     kmtl) CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12,4 1048576
           run timeline_km_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tlkm -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
