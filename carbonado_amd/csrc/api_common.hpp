@@ -234,6 +234,8 @@ struct Trace {
 // with the split copy-back: the host writes the stream's header and the chunks
 // it already holds (the content / data shards) while the device hashes; only
 // the parity region and the parent nodes cross PCIe.  km_ok() must hold.
+// `cur` may be c->hin itself (the host stages' output written there, hin
+// already grown to cur_n + 16): the copy into pinned memory is then skipped.
 int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uint64_t final_len, uint8_t *out,
                      uint8_t hash[32]);
 // encoding::zfec 4-of-8 of one object (n > 0 bytes, shard length C) into

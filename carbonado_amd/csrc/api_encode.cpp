@@ -29,12 +29,24 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
     uint64_t cur_n = n, bc = 0, be = 0;
     if (has_host_stages(format)) {
         Trace trace("host stages");
-        t_stage.resize(host_stage_max(format, n) + 1);
+        // straight into the context's pinned input when a device stage follows
+        // (the single-object paths then read it there, the others DMA it from
+        // there): no copy of the staged bytes into pinned memory afterwards
+        const uint64_t cap = host_stage_max(format, n) + 1;
+        uint8_t *dst = nullptr;
+        Ctx *c = nullptr;
+        if ((format & (CHIP_FORMAT_ZFEC | CHIP_FORMAT_BAO)) && zc_ok(cap + 16) && ctx_get(&c) == CHIP_OK &&
+            grow_pinned_local(c->hin, cap + 16) == hipSuccess)
+            dst = static_cast<uint8_t *>(c->hin.p);
+        if (!dst) {
+            t_stage.resize(cap);
+            dst = t_stage.data();
+        }
         int st = host_stages_into(format, pubkey, pubkey_len, inject ? inject->ephemeral_sk : nullptr,
-                                  inject ? inject->nonce : nullptr, in, n, t_stage.data(), t_stage.size(), t_tmp,
-                                  &cur_n, &bc, &be, nullptr, nullptr, nullptr, true);
+                                  inject ? inject->nonce : nullptr, in, n, dst, cap, t_tmp, &cur_n, &bc, &be, nullptr,
+                                  nullptr, nullptr, true);
         if (st != CHIP_OK) return st;
-        cur = t_stage.data();
+        cur = dst;
         trace.mark("encode");
     }
     chip_encode_info inf;

@@ -153,7 +153,7 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
     CHIP_HIP(grow(c->scratch, km_scratch_len(zl)));
     trace.mark("buffers");
     uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
-    copy_in(hin, cur, cur_n);
+    if (cur != hin) copy_in(hin, cur, cur_n);  // (the host stages may have written it there already)
     trace.mark("copy in");
     const uint8_t *d_in = dev_ptr<const uint8_t>(hin);
     uint8_t *d_out = dev_ptr<uint8_t>(hout);
@@ -210,7 +210,7 @@ int single_zfec_encode_zc(Ctx *c, const uint8_t *in, uint64_t n, uint64_t C, uin
     CHIP_HIP(grow_pinned_local(c->hin, n + 16));
     CHIP_HIP(grow_pinned_local(c->hout, 4 * C));
     uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
-    copy_in(hin, in, n);
+    if (in != hin) copy_in(hin, in, n);
     trace.mark("copy in");
     CHIP_HIP(zc_zfec_parity_dev(dev_ptr<const uint8_t>(hin), n, C, dev_ptr<uint8_t>(hout), c->stream));
     trace.mark("launch");
