@@ -539,11 +539,12 @@ hipError_t launch(int mode, MultiArgs a, hipStream_t stream) {
     a.counter = q + QUEUE_KM;
     auto k = mode == 0 ? (sg == 16 ? km_kernel<0, 16> : sg == 32 ? km_kernel<0, 32> : km_kernel<0, 64>)
                        : (sg == 16 ? km_kernel<1, 16> : sg == 32 ? km_kernel<1, 32> : km_kernel<1, 64>);
-    // the staged kernel where the chunks come from one contiguous source (the
-    // stream to verify, or the content), 4-B aligned
+    // the staged kernel where the chunks come from one contiguous source: the
+    // stream to verify (4-B aligned; every region starts >= 72 B into it, so
+    // the first 16-B load stays inside) or the content (16-B aligned)
     const uint8_t *from = mode == 1 ? a.stream : a.src;
     if (sg == S && staged_on() && (mode == 1 || a.n_in == a.N) && from &&
-        (reinterpret_cast<uintptr_t>(from) & 3) == 0)
+        (reinterpret_cast<uintptr_t>(from) & (mode == 1 ? 3 : 15)) == 0)
         k = mode == 0 ? km_staged_kernel<0> : km_staged_kernel<1>;
     hipLaunchKernelGGL(k, dim3((unsigned)G), dim3(TPB), 0, stream, a);
     return hipGetLastError();

@@ -117,6 +117,47 @@ __global__ __launch_bounds__(256) void read_rows(const uint4 *p, size_t chunks, 
     }
 }
 
+// one lane stores `v` to a pinned host word with system scope (vector store)
+__global__ void flag_kernel(unsigned *flag, unsigned v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// host-side completion latency of a trivial launch: hipStreamSynchronize
+// against spinning on a flag the kernel writes to pinned memory (then the
+// synchronize, which returns at once)
+static bool sync_latency(int reps) {
+    std::printf("== completion latency of a one-lane kernel\n");
+    unsigned *flag = nullptr;
+    CK(hipHostMalloc(reinterpret_cast<void **>(&flag), 64, hipHostMallocDefault));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    std::vector<double> ts, tf, tf2;
+    for (int r = 0; r < reps; ++r) {
+        __atomic_store_n(flag, 0u, __ATOMIC_RELEASE);
+        double a = now_us();
+        flag_kernel<<<1, 64, 0, s>>>(flag, 1u);
+        CK(hipStreamSynchronize(s));
+        ts.push_back(now_us() - a);
+        __atomic_store_n(flag, 0u, __ATOMIC_RELEASE);
+        a = now_us();
+        flag_kernel<<<1, 64, 0, s>>>(flag, 2u);
+        while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != 2u) _mm_pause();
+        tf.push_back(now_us() - a);
+        CK(hipStreamSynchronize(s));
+        tf2.push_back(now_us() - a);
+    }
+    std::sort(ts.begin(), ts.end());
+    std::sort(tf.begin(), tf.end());
+    std::sort(tf2.begin(), tf2.end());
+    std::printf("  launch + hipStreamSynchronize: median %.1f us (p10 %.1f, p90 %.1f)\n", ts[ts.size() / 2],
+                ts[ts.size() / 10], ts[ts.size() * 9 / 10]);
+    std::printf("  launch + spin on the flag:     median %.1f us (p10 %.1f, p90 %.1f); + the synchronize %.1f us\n",
+                tf[tf.size() / 2], tf[tf.size() / 10], tf[tf.size() * 9 / 10], tf2[tf2.size() / 2]);
+    CK(hipStreamDestroy(s));
+    CK(hipHostFree(flag));
+    return true;
+}
+
 template <class F>
 static bool time_kernel(const char *what, size_t n, int reps, unsigned long long want, unsigned long long *dsum, F launch) {
     hipEvent_t e0, e1;
@@ -233,6 +274,7 @@ int main(int argc, char **argv) {
         std::memcpy(&w, &src[i], 4);
         want += w;
     }
+    sync_latency(200);
     patterns(n, reps, src, want);
     probe("pinned host memory (the KM path today)", 0, true, n, reps, src, want);
     probe("VRAM fine-grained", hipDeviceMallocFinegrained, false, n, reps, src, want);
