@@ -402,6 +402,11 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         *out_len = cur_n;
         return CHIP_OK;
     }
+    Trace trace("host stages");
+    struct Mark {
+        Trace &t;
+        ~Mark() { t.mark("decode"); }
+    } mark{trace};
     if (ecies && snap)  // decoding.rs:101-111 in one pass (a large object on the stage's worker pool)
         return host::ecies_decrypt_snap_par(secret_key, sk_len, cur, cur_n, out, out_cap, out_len,
                                             have_pre ? pre_key : nullptr, pre_eph);
