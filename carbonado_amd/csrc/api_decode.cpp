@@ -312,7 +312,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         Ctx *c;
         int st = ctx_get(&c);
         if (st != CHIP_OK) return st;
-        if (bao && km_ok(blen, 1)) {  // KM verifies; the host gathers [0, olen) from `in` meanwhile
+        if (bao && single_ok(blen)) {  // KM / KS verifies; the host gathers [0, olen) from `in` meanwhile
             // (at Bao|Zfec the positional shares' primaries are the content's first 4 C bytes)
             // while the device verifies, also the ECIES key from the envelope header as `in` holds it
             auto prekey = [&] {

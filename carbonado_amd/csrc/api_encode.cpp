@@ -58,7 +58,7 @@ int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_len, cons
     if (!zfec && !bao) {
         if (cur_n) std::memcpy(out, cur, cur_n);
         std::memset(hash, 0, 32);
-    } else if (bao && km_ok(cur_len, 1)) {  // one object on KM, the split copy-back (api_single.cpp)
+    } else if (bao && single_ok(cur_len)) {  // one object on KM (split copy-back) or KS, zero-copy (api_single.cpp)
         Ctx *c;
         st = ctx_get(&c);
         if (st != CHIP_OK) return st;

@@ -137,8 +137,38 @@ void copy_out(uint8_t *dst, const uint8_t *src, uint64_t n) {
 
 }  // namespace
 
+namespace {
+
+// KS (small_kernels.hip, one workgroup) for a stream of at most 64 chunks,
+// zero-copy too: the input from pinned memory, the whole stream and the hash
+// written there by the kernel (at most ~70 KB), copied out after.
+int single_encode_ks(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uint64_t final_len, uint8_t *out,
+                     uint8_t hash[32]) {
+    Trace trace("encode ks");
+    const uint64_t hash_at = (final_len + 63) & ~uint64_t(63);
+    CHIP_HIP(grow_pinned_local(c->hin, cur_n + 16));  // the kernel's 16-B source loads stay inside
+    CHIP_HIP(grow_pinned_local(c->hout, hash_at + 64));
+    uint8_t *hin = static_cast<uint8_t *>(c->hin.p), *hout = static_cast<uint8_t *>(c->hout.p);
+    if (cur != hin) std::memcpy(hin, cur, cur_n);
+    const uint8_t *d_in = dev_ptr<const uint8_t>(hin);
+    uint8_t *d_out = dev_ptr<uint8_t>(hout);
+    if (C) CHIP_HIP(small_zfec_bao_dev(d_in, 0, cur_n, 1, C, d_out, 0, d_out + hash_at, c->stream));
+    else CHIP_HIP(small_bao_encode_dev(d_in, 0, cur_n, 1, d_out, 0, d_out + hash_at, c->stream));
+    trace.mark("launch");
+    CHIP_HIP(hipStreamSynchronize(c->stream));
+    trace.mark("sync");
+    std::memcpy(out, hout, final_len);
+    std::memcpy(hash, hout + hash_at, 32);
+    trace.mark("copy out");
+    return CHIP_OK;
+}
+
+}  // namespace
+
 int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uint64_t final_len, uint8_t *out,
                      uint8_t hash[32]) {
+    if (n_chunks_of(C ? (uint64_t)CHIP_FEC_M * C : cur_n) <= KS_TINY_N)
+        return single_encode_ks(c, cur, cur_n, C, final_len, out, hash);
     Trace trace("encode");
     const bool zfec = C > 0;
     const uint64_t zl = zfec ? (uint64_t)CHIP_FEC_M * C : cur_n;
@@ -277,8 +307,12 @@ int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const 
     copy_in(hin + 64, in, blen);
     trace.mark("copy in");
     uint8_t *d = dev_ptr<uint8_t>(hin);
-    CHIP_HIP(km_bao_decode_dev(d + 64, n, d, nullptr, 0, reinterpret_cast<uint32_t *>(d + 32), c->scratch.p,
-                               c->stream));
+    if (n_chunks_of(n) <= KS_TINY_N)  // KS: one workgroup verifies the whole stream
+        CHIP_HIP(small_bao_decode_dev(d + 64, 0, n, 1, d, nullptr, 0, 0, reinterpret_cast<uint32_t *>(d + 32),
+                                      c->stream));
+    else
+        CHIP_HIP(km_bao_decode_dev(d + 64, n, d, nullptr, 0, reinterpret_cast<uint32_t *>(d + 32), c->scratch.p,
+                                   c->stream));
     trace.mark("launch");
     // meanwhile: the content from the caller's own copy of the stream
     advise_huge(dst, olen);

@@ -355,7 +355,7 @@ int chip_bao_encode(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_ca
     Ctx *c;
     int st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    if (km_ok(n, 1)) {  // one object on KM: the host writes the content's chunks, only the nodes come back
+    if (single_ok(n)) {  // one object on KM (or KS), zero-copy: only the nodes come back from KM
         st = single_encode_km(c, in, n, 0, blen, out, hash);
         if (st != CHIP_OK) return st;
         *out_len = blen;
@@ -395,7 +395,7 @@ int chip_bao_decode(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint6
     Ctx *c;
     st = ctx_get(&c);
     if (st != CHIP_OK) return st;
-    if (km_ok(n, 1)) {  // KM verifies on the device while the host gathers the content from `enc`
+    if (single_ok(n)) {  // KM (or KS) verifies on the device while the host gathers the content from `enc`
         st = single_decode_km(c, enc, len, n, hash, out, n);
         if (st != CHIP_OK) return st;
         *out_len = n;

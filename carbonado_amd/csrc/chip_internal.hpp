@@ -192,6 +192,9 @@ hipError_t small_bao_decode_dev(const uint8_t *d_stream, uint64_t in_stride, uin
 // Scratch: km_scratch_len(bao_n) bytes (the group CVs).
 constexpr uint64_t KM_MAX_N = 32768;
 bool km_ok(uint64_t bao_n, uint64_t count);
+// one object from host memory on the zero-copy single-object paths
+// (api_single.cpp): KM for 64 < N <= KM_MAX_N, KS up to 64 chunks (n > 0)
+bool single_ok(uint64_t bao_n);
 bool km_enabled();  // CHIP_KM (default on): also the single-object zero-copy zfec encode
 // the single-object zero-copy zfec paths (api_single.cpp) for a pinned
 // footprint of `bytes`: km_enabled() and at most ZC_MAX_BYTES (larger objects

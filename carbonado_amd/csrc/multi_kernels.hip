@@ -541,9 +541,12 @@ hipError_t launch(int mode, MultiArgs a, hipStream_t stream) {
                        : (sg == 16 ? km_kernel<1, 16> : sg == 32 ? km_kernel<1, 32> : km_kernel<1, 64>);
     // the staged kernel where the chunks come from one contiguous source: the
     // stream to verify (4-B aligned; every region starts >= 72 B into it, so
-    // the first 16-B load stays inside) or the content (16-B aligned)
+    // the first 16-B load stays inside) or the content (16-B aligned).  Decode
+    // of up to 32 groups keeps km_kernel: with few workgroups its per-block
+    // waits overlap the reads better (r11v: 4-8 us faster at 64-256 KiB, even
+    // at 1 MiB; the staged rows win from 4 MiB on)
     const uint8_t *from = mode == 1 ? a.stream : a.src;
-    if (sg == S && staged_on() && (mode == 1 || a.n_in == a.N) && from &&
+    if (sg == S && staged_on() && (mode == 1 ? G > 32 : a.n_in == a.N) && from &&
         (reinterpret_cast<uintptr_t>(from) & (mode == 1 ? 3 : 15)) == 0)
         k = mode == 0 ? km_staged_kernel<0> : km_staged_kernel<1>;
     hipLaunchKernelGGL(k, dim3((unsigned)G), dim3(TPB), 0, stream, a);
@@ -557,6 +560,12 @@ bool km_enabled() { return multi::enabled(); }
 bool km_ok(uint64_t bao_n, uint64_t count) {
     const uint64_t N = n_chunks(bao_n);
     return multi::enabled() && count == 1 && N > (uint64_t)multi::S && N <= KM_MAX_N;
+}
+
+bool single_ok(uint64_t bao_n) {
+    if (!multi::enabled() || bao_n == 0) return false;
+    const uint64_t N = n_chunks(bao_n);
+    return N > (uint64_t)multi::S ? N <= KM_MAX_N : small_ok(bao_n, 1);
 }
 
 uint64_t km_scratch_len(uint64_t bao_n) { return 32 * (n_chunks(bao_n) + 15) / 16; }  // any group size

@@ -155,7 +155,8 @@ from carbonado_amd.error import BaoDecodeError
 from oracle import oracle as O
 ca._lib.lib().chip_init(0)
 bad = []
-for n, level in ((100_000, 12), (1 << 20, 12), (1048811, 12), (300_001, 4), (5 << 20, 4)):
+for n, level in ((1, 12), (5000, 12), (100_000, 12), (1 << 20, 12), (1048811, 12), (1, 4), (5000, 4), (65536, 4),
+                 (65537, 4), (300_001, 4), (5 << 20, 4)):
     d = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
     enc, h, info = ca.encode(b"", d, level)
     oenc, oh, _ = O.encode(d, level)
@@ -174,14 +175,17 @@ print("BAD", bad) if bad else print("OK")
 """
 
 
-@pytest.mark.parametrize("env", [{"CHIP_KM_SG": "16"}, {"CHIP_KM_SG": "32"}, {"CHIP_KM_STAGE": "0"}],
-                         ids=["sg16", "sg32", "unstaged"])
+@pytest.mark.parametrize("env", [{"CHIP_KM_SG": "16"}, {"CHIP_KM_SG": "32"}, {"CHIP_KM_STAGE": "0"}, {"CHIP_KM": "0"}],
+                         ids=["sg16", "sg32", "unstaged", "km_off"])
 def test_km_smaller_groups(gpu, env):
     """KM with 16 / 32 chunks per workgroup (CHIP_KM_SG, read once per
     process: a child process): the group levels stop lower and the top walk
     starts lower; and km_kernel where km_staged_kernel runs by default
     (CHIP_KM_STAGE=0: decode and bao of the content with each quad loading
-    its chunk itself).  Same bytes, same verdicts."""
+    its chunk itself); and with CHIP_KM=0 the staged device paths of round 5
+    for every size (KS and K13 through HBM buffers).  Small objects (N <= 64:
+    KS zero-copy by default) and both sides of N = 64 too.  Same bytes, same
+    verdicts."""
     import os
     import subprocess
     import sys
