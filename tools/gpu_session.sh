@@ -133,6 +133,7 @@ for s in "$@"; do
                              LD_LIBRARY_PATH=$PWD/tools/oldlib run abi_latency_old_$i 300 ./tools/abi_latency 30 12,15,4 1048576,4194304; done ;;
     tr15) CHIP_SINGLE_TRACE=1 run trace15_new 120 ./tools/abi_latency 8 15 1048576
           CHIP_SINGLE_TRACE=1 LD_LIBRARY_PATH=$PWD/tools/oldlib run trace15_old 120 ./tools/abi_latency 8 15 1048576 ;;
+    singleprof) run single_kernels 300 rocprofv3 --kernel-trace --stats -d $O/sp -o sp --output-format csv -- ./tools/abi_latency 10 12,4,8,15 1024,1048576,4194304 ;;
     zdtl) CHIP_SINGLE_TRACE=1 run zfec_decode_trace 120 ./tools/abi_latency 10 8 1048576 ;;
     kmtl) CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12,4 1048576
           run timeline_km_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tlkm -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
