@@ -72,6 +72,11 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[4 * 256];     // zfec parity products
     __shared__ __attribute__((aligned(16))) uint32_t cvs[2][MAXN][8];  // one tree level and the next
     __shared__ __attribute__((aligned(16))) uint32_t msg[QUADS][16];  // each quad's message block
+    // encode() at Zfec|Bao of one object of at most 64 chunks: the shards also
+    // kept here, so phase 2 hashes them without reading back the stream (a
+    // single call's stream is pinned host memory: a PCIe round trip)
+    constexpr int STG = MODE == 0 && MAXN > 64 ? 64 * 64 : 1;  // 16-B units: 64 chunks
+    __shared__ __attribute__((aligned(16))) u32x4 stg[STG];
     const int t = threadIdx.x, q = t & 3, g = t >> 2;
     const int GT = TPB / (int)a.per, GQ = GT / 4;  // threads and quads of one object
     const int ol = t / GT, tl = t - ol * GT, gl = tl >> 2;
@@ -82,6 +87,7 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
     const uint8_t *src = a.in + (live ? obj : 0) * a.in_stride;
     uint8_t *dst = a.out ? a.out + (live ? obj : 0) * a.out_stride : nullptr;
     const uint8_t *stream = MODE == 0 ? dst : src;
+    const bool staged = STG > 1 && a.C && N <= 64 && a.per == 1;
     bool ok = true;
 
     // ---- phase 1: header; zfec shards or content into their slots / content out
@@ -118,8 +124,10 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
                 }
                 const uint64_t u = o / 1024, w = o % 1024;
 #pragma unroll
-                for (int s = 0; s < 8; ++s)
+                for (int s = 0; s < 8; ++s) {
                     store16_a8<false>(dst + chunk_stream_off(s * cols + u, N) + w, s < 4 ? v[s] : p[s - 4]);
+                    if (staged) stg[(s * cols + u) * 64 + w / 16] = s < 4 ? v[s] : p[s - 4];
+                }
             }
         } else if (dst) {
             for (uint64_t o = 16 * (uint64_t)tl; live && o < n; o += 16 * GT) {
@@ -150,6 +158,26 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
     const uint32_t iv0 = q == 0 ? IV(0) : q == 1 ? IV(1) : q == 2 ? IV(2) : IV(3);
     const uint32_t iv1 = q == 0 ? IV(4) : q == 1 ? IV(5) : q == 2 ? IV(6) : IV(7);
     const bool content_in = MODE == 0 && a.C == 0;  // encode of the content: read it where it is
+    // verify, one object per workgroup: the stored node of my first parent at
+    // every level, in flight with my first chunk (one round of loads instead
+    // of one dependent wait per level: a single call's stream is pinned host
+    // memory, a PCIe round trip each).  Not in the tiny-batch shape, whose
+    // occupancy the extra registers would cut (168 -> 206 VGPRs, 3 -> 2 waves)
+    constexpr bool PF = MODE == 1 && MAXN > 64;
+    constexpr int LOGMAX = 9;
+    static_assert((1 << LOGMAX) >= MAXN, "levels of the walk");
+    u32x4 stn[PF ? LOGMAX : 1];
+    if (PF) {
+        uint64_t cp_ = N;
+#pragma unroll
+        for (int l = 1; l <= LOGMAX; ++l) {
+            const uint64_t cn = (cp_ + 1) / 2;
+            stn[l - 1] = u32x4{0u, 0u, 0u, 0u};
+            if (live && cp_ > 1 && (uint64_t)gl < cn && 2 * (uint64_t)gl + 1 < cp_)
+                stn[l - 1] = load16_a8(src + parent_stream_off((uint64_t)gl << l, l, N) + 16 * q);
+            cp_ = cn;
+        }
+    }
     for (uint64_t c = gl; live && c < N; c += GQ) {
         const uint64_t rem = n - c * 1024;
         const uint32_t clen = n == 0 ? 0u : (rem < 1024 ? (uint32_t)rem : 1024u);
@@ -160,6 +188,7 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
         for (int b = 0; b < 16; ++b) {  // my 16 B of every block of the chunk, all loads in flight
             const uint32_t off = 64 * b + 16 * q;
             if (off >= clen) pc[b] = u32x4{0u, 0u, 0u, 0u};
+            else if (staged) pc[b] = stg[c * 64 + off / 16];  // (zfec shards: whole chunks)
             else if (content_in) pc[b] = zf::load16_masked(src, c * 1024 + off, n);
             else pc[b] = off + 16 <= clen ? load16_a8(cp + off) : load16_bytes(cp + off, clen - off);
         }
@@ -214,7 +243,15 @@ __global__ __launch_bounds__(TPB) void small_kernel(SmallArgs a) {
             if (MODE == 0) {
                 if (dst) store16_a8<false>(node, mw);
             } else {
-                const u32x4 s = load16_a8(node);
+                u32x4 s;
+                if (PF && p == (uint64_t)gl) {
+                    s = stn[0];
+#pragma unroll
+                    for (int l = 2; l <= (PF ? LOGMAX : 1); ++l)
+                        if (level == l) s = stn[l - 1];
+                } else {
+                    s = load16_a8(node);  // tiny batches; a quad's second parent of a level (N > 2 GQ)
+                }
                 ok &= s.x == mw.x && s.y == mw.y && s.z == mw.z && s.w == mw.w;
             }
             if (root) {
