@@ -6,6 +6,20 @@
 using namespace chip;
 using namespace chip::api;
 
+namespace {
+
+// the one-pass verify of scrub / verify_slice (below): single-object streams
+// of up to 4096 chunks (r11zh: at 64 KiB - 1 MiB of content 26-39 % faster
+// than the DMA + per-node check, equal at 4 MiB, 9 % slower at 16 MiB)
+bool fast_verify_ok(uint64_t n) { return single_ok(n) && n_chunks_of(n) <= 4096; }
+
+// after a failed one-pass verify the stream already sits in the context's
+// pinned input (single_decode_km: at byte 64), so the per-node check's upload
+// is a direct DMA from there instead of a copy through the staging ring
+const uint8_t *pinned_stream(Ctx *c) { return static_cast<const uint8_t *>(c->hin.p) + 64; }
+
+}  // namespace
+
 extern "C" {
 
 // ---- slices and scrub (decoding.rs:116-212) ----------------------------------
@@ -58,9 +72,30 @@ int chip_bao_verify_slice(const uint8_t *hash, uint64_t hash_len, const uint8_t 
     Ctx *c;
     st = ctx_get(&c);
     if (st != CHIP_OK) return st;
+    // One verify pass of the whole stream on the single-object path (KM / KS,
+    // zero-copy): when every node checks out, so does the slice, and its bytes
+    // are the caller's own (gathered here); otherwise the per-node check below
+    // decides for this slice alone.  Streams of up to 4096 chunks: beyond, the
+    // DMA + per-node check is as fast (r11zh)
+    const uint8_t *src = enc;  // the stream the per-node check uploads
+    if (fast_verify_ok(n)) {
+        st = single_decode_km(c, enc, len, n, hash, nullptr, 0);
+        if (st == CHIP_OK) {
+            const uint64_t N = n_chunks_of(n);
+            for (uint64_t p = start; p < end;) {
+                const uint64_t k = p / 1024, o = p % 1024, m = std::min<uint64_t>(1024 - o, end - p);
+                std::memcpy(out + (p - start), enc + bao_chunk_offset(k, N) + o, m);
+                p += m;
+            }
+            *out_len = olen;
+            return CHIP_OK;
+        }
+        if (st != CHIP_ERR_BAO_HASH_MISMATCH) return st;
+        src = pinned_stream(c);
+    }
     const uint64_t blen = bao_encoded_len(n);
     CHIP_HIP(grow(c->in, blen));
-    CHIP_HIP(h2d(c->stage, c->in.p, enc, blen, c->stream));
+    CHIP_HIP(h2d(c->stage, c->in.p, src, blen, c->stream));
     std::vector<uint8_t> cf, pf;
     st = node_check_ctx(c, n, hash, &cf, &pf);
     if (st != CHIP_OK) return st;
@@ -89,9 +124,20 @@ int chip_scrub(const uint8_t *enc, uint64_t len, const uint8_t *hash, uint64_t h
     Ctx *c;
     st = ctx_get(&c);
     if (st != CHIP_OK) return st;
+    // A healthy stream (periodic scrubbing's usual case, decoding.rs:151-158)
+    // is answered by one verify pass of the whole stream on the single-object
+    // path (KM / KS, zero-copy); a damaged one takes the per-node check and
+    // the repair below (paying that pass too: ~115 us at 1 MiB of content).
+    const uint8_t *src = enc;  // the stream the per-node check uploads
+    if (fast_verify_ok(n)) {
+        st = single_decode_km(c, enc, len, n, hash, nullptr, 0);
+        if (st == CHIP_OK) return CHIP_ERR_UNNECESSARY_SCRUB;  // decoding.rs:169-170
+        if (st != CHIP_ERR_BAO_HASH_MISMATCH) return st;
+        src = pinned_stream(c);
+    }
     const uint64_t blen = bao_encoded_len(n);
     CHIP_HIP(grow(c->in, blen));
-    CHIP_HIP(h2d(c->stage, c->in.p, enc, blen, c->stream));
+    CHIP_HIP(h2d(c->stage, c->in.p, src, blen, c->stream));
     std::vector<uint8_t> cf, pf;
     st = node_check_ctx(c, n, hash, &cf, &pf);
     if (st != CHIP_OK) return st;
