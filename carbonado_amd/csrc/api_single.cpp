@@ -286,7 +286,7 @@ int single_zfec_decode_zc(Ctx *c, uint32_t k, uint32_t m, const uint8_t *const *
     if (meanwhile) meanwhile();
     CHIP_HIP(hipStreamSynchronize(c->stream));
     trace.mark("sync");
-    copy_out(dst, hout, olen);
+    if (olen) copy_out(dst, hout, olen);  // (dst may be null for an empty result)
     trace.mark("copy out");
     return CHIP_OK;
 }
