@@ -240,7 +240,7 @@ int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
                      uint8_t hash[32]);
 // encoding::zfec 4-of-8 of one object (n > 0 bytes, shard length C) into
 // out[0, 8 C): the host writes the data shards (the zero-padded input) while
-// zc_parity_kernel reads the input from pinned memory and writes the parity
+// parity_kernel<1> reads the input from pinned memory and writes the parity
 // shards into pinned memory (zero-copy), copied out after.
 int single_zfec_encode_zc(Ctx *c, const uint8_t *in, uint64_t n, uint64_t C, uint8_t *out);
 // zfec decode of one object from k shares (shares[s] holds share sel[s], C

@@ -1,7 +1,7 @@
 // api_single.cpp — one object from host memory, for latency: encode() at
 // Zfec|Bao or Bao and decode() of a bao stream on KM (multi_kernels.hip; KS,
 // small_kernels.hip, up to 64 chunks), and one object's zfec alone
-// (zc_parity_kernel / the K1 decode on pinned memory).
+// (parity_kernel<1> / the K1 decode on pinned memory).
 //
 // A single object's call was the kernel's own 65-115 us (K13: 32 waves for
 // a 1 MiB object) and PCIe for every stream byte both ways (profiles/

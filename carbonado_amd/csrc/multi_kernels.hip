@@ -26,7 +26,7 @@
 //
 // Chunk bytes come from a contiguous source for chunks below `n_in` (bao of
 // the content: the content itself) and from the stream's chunk slots above it
-// (Zfec|Bao: every shard, written by km_parity_kernel; decode: the stream).
+// (Zfec|Bao: every shard, written by parity_kernel<0>; decode: the stream).
 // For a single call from host memory (api_single.cpp) the source, the stream
 // to verify, the expected hash and every output live in pinned host memory:
 // the kernels read and write them over PCIe themselves (zero-copy), so no
@@ -416,26 +416,10 @@ __global__ __launch_bounds__(TPB) void km_staged_kernel(MultiArgs a) {
                        top + 2 * GMAX * 8 / 4, last, mbase, msg, mi, iv0, iv1);
 }
 
-// A 4-of-8 zfec encode into the chunk slots of the Zfec|Bao stream: one 16-B
-// position of every shard per lane, the packed parity table ([4][256] dwords:
-// byte d of entry [j][x] = E[4 + d][j] * x) in LDS.  The input is read once
-// (from pinned host memory for a single call: zero-copy, no DMA hop); the
-// data and parity shards go to the device stream's slots for KM to hash, and
-// the parity shards also to the host-visible image of the stream from t0 on
-// (`tail`, null: none), which is everything of the stream past the data
-// region except its nodes.
-__global__ __launch_bounds__(256) void km_parity_kernel(const uint8_t *in, uint64_t valid, uint64_t C, uint8_t *stream,
-                                                        uint64_t N, const uint32_t *table, uint8_t *tail,
-                                                        uint64_t t0) {
-    __shared__ uint32_t tab[4 * 256];
-    for (int i = threadIdx.x; i < 4 * 256; i += 256) tab[i] = table[i];
-    const uint64_t o = 16 * ((uint64_t)blockIdx.x * 256 + threadIdx.x);
-    u32x4 v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = o < C ? zf::load16_masked(in, j * C + o, valid) : u32x4{0u, 0u, 0u, 0u};
-    __syncthreads();
-    if (o >= C) return;
-    u32x4 p[4];
+// 16 B of the four parity shards from 16 B at the same position of each data
+// shard: the packed parity table ([4][256] dwords in LDS: byte d of entry
+// [j][x] = E[4 + d][j] * x), then a 4 x 4 transpose
+__device__ __forceinline__ void parity16(const uint32_t *tab, const u32x4 (&v)[4], u32x4 (&p)[4]) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         uint32_t acc[4];
@@ -452,51 +436,74 @@ __global__ __launch_bounds__(256) void km_parity_kernel(const uint8_t *in, uint6
         if (d == 1) { p[0].y = r0; p[1].y = r1; p[2].y = r2; p[3].y = r3; }
         if (d == 2) { p[0].z = r0; p[1].z = r1; p[2].z = r2; p[3].z = r3; }
         if (d == 3) { p[0].w = r0; p[1].w = r1; p[2].w = r2; p[3].w = r3; }
-    }
-    const uint64_t cols = C / 1024, u = o / 1024, w = o % 1024;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        const uint64_t off = chunk_stream_off(s * cols + u, N) + w;
-        const u32x4 x = s < 4 ? v[s] : p[s - 4];
-        store16_a8<false>(stream + off, x);
-        if (s >= 4 && tail) store16_a8<false>(tail + (off - t0), x);
     }
 }
 
-// encoding::zfec of one object from pinned host memory (zero-copy): one
-// 16-B position of every shard per lane, the 4 parity shards written
-// shard-major ([P0|P1|P2|P3], C bytes each) into pinned host memory; the data
-// shards are the zero-padded input, which the host writes itself.
-__global__ __launch_bounds__(256) void zc_parity_kernel(const uint8_t *in, uint64_t valid, uint64_t C, uint8_t *par,
-                                                        const uint32_t *table) {
+// A 4-of-8 zfec encode of one object read from pinned host memory (zero-copy:
+// no DMA hop), one 16-B position of every shard per lane (`tiles` > 1:
+// positions 4 KiB apart per lane, software-pipelined, the next tile's PCIe
+// reads in flight while this tile's results are written; measured slower,
+// see parity_tiles).
+//   ZC = 0 (km_parity): the data and parity shards into the device stream's
+//     chunk slots for KM to hash, the parity shards also into the host image
+//     of the stream from t0 on (`tail`, null: none), which is everything of
+//     the stream past the data region except its nodes;
+//   ZC = 1 (zc_parity, encoding::zfec alone): the 4 parity shards shard-major
+//     ([P0|P1|P2|P3], C bytes each) into pinned host memory `out`; the data
+//     shards are the zero-padded input, which the host writes itself.
+template <int ZC>
+__global__ __launch_bounds__(256) void parity_kernel(const uint8_t *in, uint64_t valid, uint64_t C, uint8_t *out,
+                                                     uint64_t N, const uint32_t *table, uint8_t *tail, uint64_t t0,
+                                                     uint32_t tiles) {
     __shared__ uint32_t tab[4 * 256];
     for (int i = threadIdx.x; i < 4 * 256; i += 256) tab[i] = table[i];
-    const uint64_t o = 16 * ((uint64_t)blockIdx.x * 256 + threadIdx.x);
+    uint64_t o = 16 * ((uint64_t)blockIdx.x * 256 * tiles + threadIdx.x);
     u32x4 v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = o < C ? zf::load16_masked(in, j * C + o, valid) : u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
-    if (o >= C) return;
-    u32x4 p[4];
+    const uint64_t cols = C / 1024;
+    for (uint32_t it = 0; it < tiles; ++it) {
+        const uint64_t on = o + 16 * 256;
+        u32x4 nv[4];
+        const bool more = it + 1 < tiles && on < C;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        uint32_t acc[4];
+        for (int j = 0; j < 4; ++j) nv[j] = more ? zf::load16_masked(in, j * C + on, valid) : u32x4{0u, 0u, 0u, 0u};
+        if (o < C) {
+            u32x4 p[4];
+            parity16(tab, v, p);
+            if (ZC) {
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            uint32_t x = 0;
+                for (int s = 0; s < 4; ++s) *glb(reinterpret_cast<u32x4 *>(out + s * C + o)) = p[s];
+            } else {
+                const uint64_t u = o / 1024, w = o % 1024;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) x ^= tab[j * 256 + ((zf::comp(v[j], d) >> (8 * b)) & 0xFFu)];
-            acc[b] = x;
+                for (int s = 0; s < 8; ++s) {
+                    const uint64_t off = chunk_stream_off(s * cols + u, N) + w;
+                    const u32x4 x = s < 4 ? v[s] : p[s - 4];
+                    store16_a8<false>(out + off, x);
+                    if (s >= 4 && tail) store16_a8<false>(tail + (off - t0), x);
+                }
+            }
         }
-        uint32_t r0, r1, r2, r3;
-        zf::transpose4(acc[0], acc[1], acc[2], acc[3], r0, r1, r2, r3);
-        if (d == 0) { p[0].x = r0; p[1].x = r1; p[2].x = r2; p[3].x = r3; }
-        if (d == 1) { p[0].y = r0; p[1].y = r1; p[2].y = r2; p[3].y = r3; }
-        if (d == 2) { p[0].z = r0; p[1].z = r1; p[2].z = r2; p[3].z = r3; }
-        if (d == 3) { p[0].w = r0; p[1].w = r1; p[2].w = r2; p[3].w = r3; }
-    }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) *glb(reinterpret_cast<u32x4 *>(par + s * C + o)) = p[s];
+        for (int j = 0; j < 4; ++j) v[j] = nv[j];
+        o = on;
+    }
+}
+
+// positions per lane of the parity kernels: CHIP_PARITY_TILES, default 1 (one
+// position per lane, the grid covering C).  More tiles pipeline each lane's
+// reads and writes but spread the object's PCIe reads over fewer workgroups,
+// which costs more than the overlap gains (profiles/NOT_KEPT.md r11zo)
+uint32_t parity_tiles(uint64_t C) {
+    static const uint32_t env = [] {
+        const char *e = std::getenv("CHIP_PARITY_TILES");
+        const int v = e ? std::atoi(e) : 1;
+        return (uint32_t)(v >= 1 && v <= 64 ? v : 1);
+    }();
+    const uint64_t tiles_needed = (C / 16 + 255) / 256;  // 4 KiB of every shard per tile
+    return (uint32_t)(tiles_needed < env ? (tiles_needed ? tiles_needed : 1) : env);
 }
 
 bool enabled() {
@@ -587,8 +594,9 @@ hipError_t km_zfec_bao_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, uint
     hipError_t e = zfec_parity_table(4, 8, &tab);
     if (e != hipSuccess) return e;
     const uint64_t N = 8 * C / 1024;
-    hipLaunchKernelGGL(multi::km_parity_kernel, dim3((unsigned)((C / 16 + 255) / 256)), dim3(256), 0, stream, d_in,
-                       valid, C, d_stream, N, static_cast<const uint32_t *>(tab), d_tail, t0);
+    const uint32_t tiles = multi::parity_tiles(C);
+    hipLaunchKernelGGL(multi::parity_kernel<0>, dim3((unsigned)((C / 16 + 256 * tiles - 1) / (256 * tiles))), dim3(256),
+                       0, stream, d_in, valid, C, d_stream, N, static_cast<const uint32_t *>(tab), d_tail, t0, tiles);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (parity_done && (e = hipEventRecord(parity_done, stream)) != hipSuccess) return e;
     multi::MultiArgs a{};
@@ -603,8 +611,9 @@ hipError_t zc_zfec_parity_dev(const uint8_t *d_in, uint64_t valid, uint64_t C, u
     const void *tab = nullptr;
     hipError_t e = zfec_parity_table(4, 8, &tab);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(multi::zc_parity_kernel, dim3((unsigned)((C / 16 + 255) / 256)), dim3(256), 0, stream, d_in,
-                       valid, C, d_par, static_cast<const uint32_t *>(tab));
+    const uint32_t tiles = multi::parity_tiles(C);
+    hipLaunchKernelGGL(multi::parity_kernel<1>, dim3((unsigned)((C / 16 + 256 * tiles - 1) / (256 * tiles))), dim3(256),
+                       0, stream, d_in, valid, C, d_par, 0, static_cast<const uint32_t *>(tab), nullptr, 0, tiles);
     return hipGetLastError();
 }
 

@@ -134,6 +134,8 @@ for s in "$@"; do
     tr15) CHIP_SINGLE_TRACE=1 run trace15_new 120 ./tools/abi_latency 8 15 1048576
           CHIP_SINGLE_TRACE=1 LD_LIBRARY_PATH=$PWD/tools/oldlib run trace15_old 120 ./tools/abi_latency 8 15 1048576 ;;
     singleprof) run single_kernels 300 rocprofv3 --kernel-trace --stats -d $O/sp -o sp --output-format csv -- ./tools/abi_latency 10 12,4,8,15 1024,1048576,4194304 ;;
+    ptiles) for i in 1 2; do for t in 4 1 2 8; do CHIP_PARITY_TILES=$t run abi_latency_ptiles${t}_$i 300 ./tools/abi_latency 30 12,8 262144,1048576,4194304; done; done
+            for t in 4 1; do CHIP_PARITY_TILES=$t run ptiles_kernels$t 300 rocprofv3 --kernel-trace --stats -d $O/pt$t -o pt --output-format csv -- ./tools/abi_latency 10 12,8 1048576; done ;;
     zdtl) CHIP_SINGLE_TRACE=1 run zfec_decode_trace 120 ./tools/abi_latency 10 8 1048576 ;;
     kmtl) CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12,4 1048576
           run timeline_km_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tlkm -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
