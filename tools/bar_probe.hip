@@ -158,6 +158,12 @@ static bool sync_latency(int reps) {
     return true;
 }
 
+// pinned -> pinned and pinned -> HBM copies, 16 B per lane, all loads first
+__global__ void copy16(const uint4 *src, uint4 *dst, size_t words) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i < words) dst[i] = src[i];
+}
+
 template <class F>
 static bool time_kernel(const char *what, size_t n, int reps, unsigned long long want, unsigned long long *dsum, F launch) {
     hipEvent_t e0, e1;
@@ -202,6 +208,24 @@ static bool patterns(size_t n, int reps, const std::vector<uint8_t> &src, unsign
     time_kernel("grid-stride 256 WG (pinned)", n, reps, want, dsum, [&] { read_sum<<<256, 256>>>(hp, n / 16, dsum); });
     time_kernel("grid-stride 32 WG (pinned)", n, reps, want, dsum, [&] { read_sum<<<32, 256>>>(hp, n / 16, dsum); });
     time_kernel("KM quads (HBM)", n, reps, want, dsum, [&] { read_km<<<G, 256>>>(vp, chunks, dsum); });
+    {
+        void *h2 = nullptr;
+        CK(hipHostMalloc(&h2, n, hipHostMallocDefault));
+        const unsigned cg = (unsigned)((n / 16 + 255) / 256);
+        time_kernel("copy pinned -> pinned (read+write)", n, reps, want, dsum, [&] {
+            copy16<<<cg, 256>>>(hp, static_cast<uint4 *>(h2), n / 16);
+            read_sum<<<256, 256>>>(vp, n / 16, dsum);  // (the checksum from HBM: the timing is the copy's + ~6 us)
+        });
+        time_kernel("copy pinned -> HBM", n, reps, want, dsum, [&] {
+            copy16<<<cg, 256>>>(hp, static_cast<uint4 *>(dv), n / 16);
+            read_sum<<<256, 256>>>(vp, n / 16, dsum);
+        });
+        time_kernel("copy HBM -> pinned", n, reps, want, dsum, [&] {
+            copy16<<<cg, 256>>>(vp, static_cast<uint4 *>(h2), n / 16);
+            read_sum<<<256, 256>>>(vp, n / 16, dsum);
+        });
+        CK(hipHostFree(h2));
+    }
     time_kernel("whole-chunk rows (HBM)", n, reps, want, dsum, [&] { read_rows<<<G, 256>>>(vp, chunks, dsum); });
     CK(hipFree(dsum));
     CK(hipFree(dv));
