@@ -139,6 +139,17 @@ void copy_out(uint8_t *dst, const uint8_t *src, uint64_t n) {
 
 namespace {
 
+// the largest stream (chunks) a single call runs on KS rather than KM:
+// CHIP_KS_SINGLE_MAX (64 .. 512, an A/B knob), default 64
+uint64_t ks_single_max() {
+    static const uint64_t v = [] {
+        const char *e = std::getenv("CHIP_KS_SINGLE_MAX");
+        const long x = e ? std::atol(e) : 64;
+        return (uint64_t)(x >= 64 && x <= (long)KS_MAX_N ? x : 64);
+    }();
+    return v;
+}
+
 // KS (small_kernels.hip, one workgroup) for a stream of at most 64 chunks,
 // zero-copy too: the input from pinned memory, the whole stream and the hash
 // written there by the kernel (at most ~70 KB), copied out after.
@@ -167,7 +178,7 @@ int single_encode_ks(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uin
 
 int single_encode_km(Ctx *c, const uint8_t *cur, uint64_t cur_n, uint64_t C, uint64_t final_len, uint8_t *out,
                      uint8_t hash[32]) {
-    if (n_chunks_of(C ? (uint64_t)CHIP_FEC_M * C : cur_n) <= KS_TINY_N)
+    if (n_chunks_of(C ? (uint64_t)CHIP_FEC_M * C : cur_n) <= ks_single_max())
         return single_encode_ks(c, cur, cur_n, C, final_len, out, hash);
     Trace trace("encode");
     const bool zfec = C > 0;
@@ -307,7 +318,7 @@ int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const 
     copy_in(hin + 64, in, blen);
     trace.mark("copy in");
     uint8_t *d = dev_ptr<uint8_t>(hin);
-    if (n_chunks_of(n) <= KS_TINY_N)  // KS: one workgroup verifies the whole stream
+    if (n_chunks_of(n) <= ks_single_max())  // KS: one workgroup verifies the whole stream
         CHIP_HIP(small_bao_decode_dev(d + 64, 0, n, 1, d, nullptr, 0, 0, reinterpret_cast<uint32_t *>(d + 32),
                                       c->stream));
     else
