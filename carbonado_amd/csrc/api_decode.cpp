@@ -316,7 +316,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             // (at Bao|Zfec the positional shares' primaries are the content's first 4 C bytes)
             // while the device verifies, also the ECIES key from the envelope header as `in` holds it
             auto prekey = [&] {
-                if (!ecies || !host::ecies_par_eligible(olen)) return;
+                if (!ecies) return;
                 const uint64_t h0 = bao_chunk_offset(0, (blen + 1023) / 1024);
                 if (h0 + 65 <= n && blen >= 65) {
                     std::memcpy(pre_eph, in + h0, 65);
@@ -330,7 +330,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         } else if (zfec && !bao && C && zc_ok(2 * CHIP_FEC_K * C)) {  // decoding.rs:95-99: shards by position
             // zero-copy: the decode kernel reads the four primaries from pinned memory
             auto prekey = [&] {
-                if (!ecies || !host::ecies_par_eligible(olen) || n < 65) return;
+                if (!ecies || n < 65) return;
                 std::memcpy(pre_eph, in, 65);
                 have_pre = host::ecies_derive_key(secret_key, sk_len, pre_eph, pre_key) == CHIP_OK;
             };
@@ -371,10 +371,9 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             }
             // While the device verifies: the ECIES key from the envelope header as the
             // input holds it (content bytes [0, 65): chunk 0 of the bao stream, or the
-            // first shard); decrypt uses it only if the verified header is the same.
-            // Only for an envelope the pool path decrypts: the one-thread paths
-            // derive their own key, so a key derived here would be paid twice
-            if (ecies && host::ecies_par_eligible(olen)) {
+            // first shard); decrypt uses it only if the verified header is the same
+            // (the pool path and the one-thread paths alike, so it is never paid twice)
+            if (ecies) {
                 const uint64_t h0 = bao ? bao_chunk_offset(0, (blen + 1023) / 1024) : 0;
                 if (h0 + 65 <= n && (!bao || blen >= 65)) {
                     std::memcpy(pre_eph, in + h0, 65);
@@ -419,7 +418,8 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
             cap = t_mid.size();
         }
         uint64_t got = 0;
-        int st = snap ? host::ecies_decrypt(secret_key, sk_len, cur, cur_n, dst, cap, &got)
+        int st = snap ? host::ecies_decrypt(secret_key, sk_len, cur, cur_n, dst, cap, &got,
+                                            have_pre ? pre_key : nullptr, pre_eph)
                       : host::ecies_decrypt_par(secret_key, sk_len, cur, cur_n, dst, cap, &got,
                                                 have_pre ? pre_key : nullptr, pre_eph);
         if (st != CHIP_OK) {

@@ -363,8 +363,20 @@ int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph
 }
 
 
+// the envelope's AES key: the one derived ahead when its ephemeral key is
+// this envelope's, else from the secret and the envelope's ephemeral key
+static bool envelope_key(const BnPtr &k, const uint8_t *in, const uint8_t *pre_key, const uint8_t *pre_eph,
+                         uint8_t key[32]) {
+    if (pre_key && pre_eph && std::memcmp(pre_eph, in, 65) == 0) {
+        std::memcpy(key, pre_key, 32);
+        return true;
+    }
+    PtPtr eph(parse_public(in, 65));
+    return eph.p && derive_key(k.p, eph.p, in, key);
+}
+
 int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
-                  uint64_t cap, uint64_t *out_len) {
+                  uint64_t cap, uint64_t *out_len, const uint8_t *pre_key, const uint8_t *pre_eph) {
     BnPtr k(parse_secret(secret, secret_len));
     if (!k.p) return CHIP_ERR_ECIES;
     if (n < ECIES_OVERHEAD) return CHIP_ERR_ECIES;  // InvalidMessage
@@ -373,10 +385,8 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
         *out_len = m;
         return CHIP_ERR_BUFFER_TOO_SMALL;
     }
-    PtPtr eph(parse_public(in, 65));
-    if (!eph.p) return CHIP_ERR_ECIES;
     uint8_t key[32];
-    if (!derive_key(k.p, eph.p, in, key)) return CHIP_ERR_ECIES;
+    if (!envelope_key(k, in, pre_key, pre_eph, key)) return CHIP_ERR_ECIES;
     const uint8_t *iv = in + 65, *tag = in + 81, *ct = in + 97;
     CipherCtx cc;
     bool ok = cc.init(key, iv, false) && cc.update(ct, m, out);
@@ -402,15 +412,14 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
 // longer than the window (never produced by a FrameEncoder) takes the
 // two-pass route.
 int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
-                       uint64_t cap, uint64_t *out_len, uint8_t *window) {
+                       uint64_t cap, uint64_t *out_len, uint8_t *window, const uint8_t *pre_key,
+                       const uint8_t *pre_eph) {
     BnPtr k(parse_secret(secret, secret_len));
     if (!k.p) return CHIP_ERR_ECIES;
     if (n < ECIES_OVERHEAD) return CHIP_ERR_ECIES;
     const uint64_t m = n - ECIES_OVERHEAD;
-    PtPtr eph(parse_public(in, 65));
-    if (!eph.p) return CHIP_ERR_ECIES;
     uint8_t key[32];
-    if (!derive_key(k.p, eph.p, in, key)) return CHIP_ERR_ECIES;
+    if (!envelope_key(k, in, pre_key, pre_eph, key)) return CHIP_ERR_ECIES;
     const uint8_t *iv = in + 65, *ct = in + 97;
     const uint8_t *tag = in + 81;
     CipherCtx cc;
@@ -500,7 +509,7 @@ int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t
         OPENSSL_cleanse(win, W);
         std::vector<uint8_t> tmp(m + 1);
         uint64_t got = 0;
-        int st = ecies_decrypt(secret, secret_len, in, n, tmp.data(), tmp.size(), &got);
+        int st = ecies_decrypt(secret, secret_len, in, n, tmp.data(), tmp.size(), &got, pre_key, pre_eph);
         if (st == CHIP_OK) st = snap_decompress(tmp.data(), got, out, cap, out_len);
         OPENSSL_cleanse(tmp.data(), tmp.size());
         return st;

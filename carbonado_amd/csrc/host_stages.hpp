@@ -31,8 +31,10 @@ constexpr uint64_t ECIES_OVERHEAD = 65 + 16 + 16;
 // for fresh random values (the reference draws both from thread_rng).
 int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk, const uint8_t *nonce,
                   const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+// pre_key / pre_eph (optional): a key already derived (ecies_derive_key) for
+// the ephemeral public key pre_eph, used when the envelope's own equals it.
 int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
-                  uint64_t cap, uint64_t *out_len);
+                  uint64_t cap, uint64_t *out_len, const uint8_t *pre_key = nullptr, const uint8_t *pre_eph = nullptr);
 // ecies_decrypt then snap_decompress (decoding.rs:101-111) in one pass over
 // the ciphertext: same output and status codes, no full-size plaintext buffer.
 // `window`: DECRYPT_SNAP_WINDOW bytes of caller scratch reused across calls
@@ -40,7 +42,8 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
 // the window are wiped.
 constexpr uint64_t DECRYPT_SNAP_WINDOW = 256u << 10;
 int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
-                       uint64_t cap, uint64_t *out_len, uint8_t *window = nullptr);
+                       uint64_t cap, uint64_t *out_len, uint8_t *window = nullptr, const uint8_t *pre_key = nullptr,
+                       const uint8_t *pre_eph = nullptr);
 // Public key (65 B uncompressed) of a 32-byte secret; for tests and tooling.
 int ecies_public_key(const uint8_t *secret, uint8_t out[65]);
 
@@ -140,9 +143,8 @@ int ecies_decrypt_par(const uint8_t *secret, uint64_t secret_len, const uint8_t 
                       const uint8_t *key_eph = nullptr);
 // An envelope of n bytes is decrypted on the pool (ecies_decrypt_par /
 // ecies_decrypt_snap_par) unless the pool is busy: at least STAGE_PAR_MIN of
-// ciphertext, within GCM's length limit, on the VAES path.  A caller deriving
-// the key ahead (ecies_derive_key) does so only then: the one-thread paths
-// derive their own.
+// ciphertext, within GCM's length limit, on the VAES path.  (A key derived
+// ahead, ecies_derive_key, is used by the pool and the one-thread paths alike.)
 bool ecies_par_eligible(uint64_t n);
 // f(0) .. f(parts - 1) on the stage pool's threads and the caller, claimed
 // one at a time (the caller alone when the pool is busy or single-threaded);

@@ -303,7 +303,7 @@ int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uin
                            const uint8_t *pre_eph) {
     StagePool &pool = StagePool::get();
     if (!ecies_par_eligible(n) || !pool.try_acquire())
-        return ecies_decrypt_snap(secret, secret_len, in, n, out, cap, out_len);
+        return ecies_decrypt_snap(secret, secret_len, in, n, out, cap, out_len, nullptr, pre_key, pre_eph);
     struct Hold {  // the pool until every return below
         StagePool &p;
         ~Hold() { p.release(); }
@@ -450,7 +450,7 @@ int ecies_decrypt_par(const uint8_t *secret, uint64_t secret_len, const uint8_t 
                       uint64_t cap, uint64_t *out_len, const uint8_t *pre_key, const uint8_t *pre_eph) {
     StagePool &pool = StagePool::get();
     if (!ecies_par_eligible(n) || !out || cap < n - ECIES_OVERHEAD || !pool.try_acquire())
-        return ecies_decrypt(secret, secret_len, in, n, out, cap, out_len);
+        return ecies_decrypt(secret, secret_len, in, n, out, cap, out_len, pre_key, pre_eph);
     struct Hold {
         StagePool &p;
         ~Hold() { p.release(); }
