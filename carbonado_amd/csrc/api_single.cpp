@@ -94,9 +94,6 @@ int copy_parts(uint64_t bytes) {
 }
 int host_parts(uint64_t nc) { return copy_parts(nc * 1024); }
 
-}  // namespace
-
-namespace {
 
 // a pinned host allocation as the device addresses it (looked up once per
 // allocation: the runtime call takes its allocation lock)
@@ -135,9 +132,6 @@ void copy_out(uint8_t *dst, const uint8_t *src, uint64_t n) {
     });
 }
 
-}  // namespace
-
-namespace {
 
 // the largest stream (chunks) a single call runs on KS rather than KM:
 // CHIP_KS_SINGLE_MAX (64 .. 512, an A/B knob), default 64
