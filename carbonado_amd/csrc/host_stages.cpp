@@ -301,6 +301,65 @@ static bool scalar_ok(const uint8_t k[32]) {
     return b && (x[0] | x[1] | x[2] | x[3]) != 0;
 }
 
+// sk * peer for an encryption's receiver key.  A storage client encrypts
+// segment after segment for one receiver, so a key seen before gets a comb
+// table of its own (k1::CombTable, built on its second use outside the lock,
+// ~0.3 ms, at most 8 receivers kept, 123 KB each): the ECDH then costs what
+// k * G does instead of the GLV ladder's 132 doublings.  The table is public
+// data (multiples of a public key); the scalar is used exactly as in mul_g
+// (full table scans, fixed step count: the same constant-time code).
+// CHIP_PEER_TABLES=0 turns it off.
+static k1::Pt peer_mul(const uint8_t peer[65], const uint8_t sk[32]) {
+    static const bool on = [] {
+        const char *v = std::getenv("CHIP_PEER_TABLES");
+        return !(v && v[0] == '0' && v[1] == 0);
+    }();
+    const k1::Fe px = k1::fe_from_be(peer + 1), py = k1::fe_from_be(peer + 33);
+    if (!on) return k1::mul(sk, px, py);
+    struct Entry {
+        uint8_t key[64];
+        uint32_t uses = 0;
+        uint64_t stamp = 0;
+        std::shared_ptr<const k1::CombTable> table;
+        bool building = false;
+    };
+    static std::mutex mu;
+    static Entry cache[8];
+    static uint64_t clock = 0;
+    std::shared_ptr<const k1::CombTable> table;
+    Entry *e = nullptr;
+    bool build = false;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (Entry &x : cache)
+            if (x.uses && std::memcmp(x.key, peer + 1, 64) == 0) e = &x;
+        if (!e) {  // a new receiver replaces the least recently used one
+            e = &cache[0];
+            for (Entry &x : cache)
+                if (!x.building && x.stamp < e->stamp) e = &x;
+            if (e->building) e = nullptr;  // every slot busy building: no table this time
+            else {
+                *e = Entry{};
+                std::memcpy(e->key, peer + 1, 64);
+            }
+        }
+        if (e) {
+            e->stamp = ++clock;
+            ++e->uses;
+            table = e->table;
+            if (!table && e->uses >= 2 && !e->building) build = e->building = true;
+        }
+    }
+    if (build) {
+        auto t = std::make_shared<const k1::CombTable>(px, py);
+        std::lock_guard<std::mutex> lk(mu);
+        if (std::memcmp(e->key, peer + 1, 64) == 0) e->table = t;  // (not replaced meanwhile)
+        e->building = false;
+        table = t;
+    }
+    return table ? k1::mul_comb(*table, sk) : k1::mul(sk, px, py);
+}
+
 int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out) {
     uint8_t sk[32];
     if (eph_sk) {
@@ -312,8 +371,7 @@ int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out) 
         } while (!scalar_ok(sk));
     }
     uint8_t master[130];
-    bool ok = k1::to65_pair(k1::mul_g(sk), k1::mul(sk, k1::fe_from_be(peer + 1), k1::fe_from_be(peer + 33)),
-                            out->eph_pub, master + 65);
+    bool ok = k1::to65_pair(k1::mul_g(sk), peer_mul(peer, sk), out->eph_pub, master + 65);
     std::memcpy(master, out->eph_pub, 65);
     OPENSSL_cleanse(sk, sizeof sk);
     ok = ok && hkdf_sha256_32(master, 130, out->key);

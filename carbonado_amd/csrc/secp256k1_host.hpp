@@ -352,11 +352,13 @@ inline const Fe &gy() {
     return f;
 }
 
-// i * 16^j * G for j < 64, i < 16 (built on first use, ~0.3 ms)
-struct GTable {
+// Fixed-base comb: i * 16^j * P for j < 64, i < 16 (~0.3 ms to build); k * P
+// is then 64 complete additions of full-table-scan picks, no doublings.  For
+// G (built on first use) and for a receiver key seen again (host_stages.cpp).
+struct CombTable {
     Pt t[64][16];
-    GTable() {
-        Pt base{gx(), gy(), {{1, 0, 0, 0, 0}}};
+    CombTable(const Fe &x, const Fe &y) {
+        Pt base{x, y, {{1, 0, 0, 0, 0}}};
         for (int j = 0; j < 64; ++j) {
             t[j][0] = pt_inf();
             t[j][1] = base;
@@ -366,17 +368,19 @@ struct GTable {
     }
 };
 
-inline const GTable &gtable() {
-    static const GTable *g = new GTable();  // never destroyed (used from host-stage threads)
+inline const CombTable &gtable() {
+    static const CombTable *g = new CombTable(gx(), gy());  // never destroyed (used from host-stage threads)
     return *g;
 }
 
-inline Pt mul_g(const uint8_t k[32]) {
-    const GTable &g = gtable();
+// k * P from P's comb table, 0 <= k < 2^256 (every step the same for every k)
+inline Pt mul_comb(const CombTable &tb, const uint8_t k[32]) {
     Pt r = pt_inf();
-    for (int j = 0; j < 64; ++j) r = pt_add(r, pt_select(g.t[j], nibble(k, j)));
+    for (int j = 0; j < 64; ++j) r = pt_add(r, pt_select(tb.t[j], nibble(k, j)));
     return r;
 }
+
+inline Pt mul_g(const uint8_t k[32]) { return mul_comb(gtable(), k); }
 
 // affine (x, y) of a point other than infinity, as 0x04 || x || y
 inline bool to65(const Pt &p, uint8_t out[65]) {

@@ -10,7 +10,7 @@
 // Welch's t-test on the cycle counts (raw, and cropped at the pooled 90th
 // and 99th percentile to take out interrupt noise).  A leak shows as a class
 // difference: |t| > 4.5.
-//   dudect_ct TEST SAMPLES_PER_CLASS      TEST: k1_mul k1_mul_g fe_inv sc_sign schnorr_sign gcm_tag all
+//   dudect_ct TEST SAMPLES_PER_CLASS      TEST: k1_mul k1_mul_g k1_mul_comb fe_inv sc_sign schnorr_sign gcm_tag all
 #include <openssl/crypto.h>
 #include <x86intrin.h>
 
@@ -135,6 +135,14 @@ int main(int argc, char **argv) {
         worst = std::max(worst, run("k1_mul_g", per,
             [&](int c, size_t i) { if (c == 0) std::memcpy(in[i].data(), one, 32); else rand_scalar(in[i].data()); },
             [&](size_t i) { sink += k1::mul_g(in[i].data()).x.v[0]; }));
+    // k * P from a comb table of P (ECIES encrypt for a receiver key seen
+    // before: host_stages.cpp peer_mul; the ephemeral scalar is secret)
+    if (want("k1_mul_comb")) {
+        const k1::CombTable tb(px, py);
+        worst = std::max(worst, run("k1_mul_comb", per,
+            [&](int c, size_t i) { if (c == 0) std::memcpy(in[i].data(), one, 32); else rand_scalar(in[i].data()); },
+            [&](size_t i) { sink += k1::mul_comb(tb, in[i].data()).x.v[0]; }));
+    }
     // field inversion (to65: the affine coordinates of a secret-dependent point)
     std::vector<k1::Fe> fe(2 * per);
     if (want("fe_inv"))

@@ -20,7 +20,7 @@ from pathlib import Path
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
-TESTS = ["k1_mul", "k1_mul_g", "fe_inv", "sc_sign", "schnorr_sign", "gcm_tag"]
+TESTS = ["k1_mul", "k1_mul_g", "k1_mul_comb", "fe_inv", "sc_sign", "schnorr_sign", "gcm_tag"]
 
 
 @pytest.fixture(scope="module")

@@ -684,3 +684,26 @@ def test_ecies_stage_functions_on_the_pool_match_oracle(ca, n):
     bad[len(bad) // 2] ^= 1
     with pytest.raises(EciesError):
         ca.decoding.ecies(bytes(bad), sk)
+
+
+def test_ecies_receiver_comb_tables_match_oracle(ca):
+    """ecies_prepare's ECDH for a receiver key seen before runs on a comb table
+    built for that key (host_stages.cpp peer_mul, from its second use; at most
+    8 receivers kept, least recently used replaced): the envelopes stay
+    byte-identical to the C oracle's for 11 receivers interleaved over many
+    rounds (first uses, table hits, evictions and rebuilds), both key forms."""
+    rng = np.random.default_rng(77)
+    receivers = []
+    for i in range(11):
+        sk = H.sha256(b"comb receiver %d" % i)
+        receivers.append((sk, ca.encoding.public_key(sk)))
+    order = [i % 11 for i in range(60)] + list(rng.integers(0, 11, 60))
+    for r, i in enumerate(order):
+        sk, pub = receivers[int(i)]
+        eph = H.sha256(b"comb eph %d" % r)
+        nonce = H.sha256(b"comb nonce %d" % r)[:16]
+        d = rng.integers(0, 256, 100 + r, dtype=np.uint8).tobytes()
+        pk = pub if r % 3 else (b"\x02" if H.parse_pubkey(pub)[1] % 2 == 0 else b"\x03") + pub[1:33]
+        e = ca.encoding.ecies(pk, d, ephemeral_sk=eph, nonce=nonce)
+        assert e == O.c_ecies_encrypt(pub, d, eph, nonce), (r, int(i))
+        assert ca.decoding.ecies(e, sk) == d
