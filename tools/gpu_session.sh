@@ -140,6 +140,7 @@ for s in "$@"; do
           CHIP_SINGLE_TRACE=1 run pdma_trace 120 ./tools/abi_latency 6 12 1048576 ;;
     ksmax) for i in 1 2; do for m in 64 128 256; do CHIP_KS_SINGLE_MAX=$m run abi_latency_ksmax${m}_$i 300 ./tools/abi_latency 30 12,4 49152,65536,131072,262144; done; done ;;
     pearly) for i in 1 2; do for e in 262144 0 99999999; do CHIP_KM_PARITY_EARLY=$e run abi_latency_pearly${e}_$i 300 ./tools/abi_latency 30 12,14 66560,131072,262144,524288,1048576,4194304; done; done ;;
+    peertab) for i in 1 2; do for t in 1 0; do CHIP_PEER_TABLES=$t run abi_latency_peertab${t}_$i 300 ./tools/abi_latency 30 15,13,9 1024,16384,1048576; done; done ;;
     zdtl) CHIP_SINGLE_TRACE=1 run zfec_decode_trace 120 ./tools/abi_latency 10 8 1048576 ;;
     kmtl) CHIP_SINGLE_TRACE=1 run km_single_trace 120 ./tools/abi_latency 10 12,4 1048576
           run timeline_km_1m 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tlkm -o tl --output-format csv -- ./tools/abi_latency 10 12,4 1048576 ;;
