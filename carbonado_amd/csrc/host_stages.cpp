@@ -371,7 +371,11 @@ int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out) 
         } while (!scalar_ok(sk));
     }
     uint8_t master[130];
-    bool ok = k1::to65_pair(k1::mul_g(sk), peer_mul(peer, sk), out->eph_pub, master + 65);
+    // the two scalar multiplications side by side (a stage-pool worker takes
+    // one unless the pool is busy: then both here, one after the other)
+    k1::Pt pts[2];
+    par_for(2, [&](int i) { pts[i] = i == 0 ? k1::mul_g(sk) : peer_mul(peer, sk); });
+    bool ok = k1::to65_pair(pts[0], pts[1], out->eph_pub, master + 65);
     std::memcpy(master, out->eph_pub, 65);
     OPENSSL_cleanse(sk, sizeof sk);
     ok = ok && hkdf_sha256_32(master, 130, out->key);
