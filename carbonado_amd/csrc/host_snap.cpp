@@ -223,7 +223,21 @@ size_t encode_block(uint8_t *dst, const uint8_t *src, size_t n) {
         for (;;) {
             const size_t base = s;
             s += 4;
-            for (size_t i = cand + 4; s < n && src[i] == src[s]; ++i, ++s) {
+            // extend the match 8 bytes at a time (the first differing byte from
+            // the XOR's trailing zeros), then bytewise at the block's end
+            size_t i = cand + 4;
+            for (;;) {
+                if (s + 8 > n) {
+                    while (s < n && src[i] == src[s]) ++i, ++s;
+                    break;
+                }
+                const uint64_t x = load64(src + s) ^ load64(src + i);
+                if (x) {
+                    s += (size_t)__builtin_ctzll(x) >> 3;
+                    break;
+                }
+                s += 8;
+                i += 8;
             }
             d += emit_copy(dst + d, base - cand, s - base);
             next_emit = s;
