@@ -333,7 +333,18 @@ bool decompress_raw(const uint8_t *src, size_t n, uint8_t *out, size_t cap, size
                 break;
         }
         if (off == 0 || off > d || len > dlen - d) return false;
-        for (size_t i = 0; i < len; ++i, ++d) out[d] = out[d - off];  // overlapping copies
+        uint8_t *dp = out + d;
+        const uint8_t *sp = dp - off;
+        if (off >= len) {  // source and destination apart
+            std::memcpy(dp, sp, len);
+        } else if (off >= 8) {  // 8-B pieces, each from bytes already written
+            size_t i = 0;
+            for (; i + 8 <= len; i += 8) std::memcpy(dp + i, sp + i, 8);
+            for (; i < len; ++i) dp[i] = sp[i];
+        } else {  // a pattern shorter than 8 bytes repeated: byte by byte
+            for (size_t i = 0; i < len; ++i) dp[i] = sp[i];
+        }
+        d += len;
     }
     if (d != dlen) return false;
     *out_len = d;
