@@ -198,6 +198,16 @@ int main(int argc, char **argv) {
         for (uint64_t n : sizes) {
             Obj o{(int)level, std::vector<uint8_t>(n), pub, sk, {eph, nonce}};
             for (auto &x : o.in) x = (uint8_t)rng();
+            if (const char *dk = std::getenv("ABI_LAT_DATA"); dk && !std::strcmp(dk, "text")) {
+                // compressible input for the snappy stage: words from a small vocabulary
+                static const char *words[] = {"carbonado ", "apocalypse ", "resistant ", "storage ", "segment ",
+                                              "zfec ", "bao ", "stream ", "verifiable ", "encode ", "0x3f, ",
+                                              "{\"id\": ", "\n", "return ", "hash(", ") "};
+                for (size_t p = 0; p < n;) {
+                    const char *w = words[rng() % 16];
+                    for (size_t k = 0; w[k] && p < n; ++k) o.in[p++] = (uint8_t)w[k];
+                }
+            }
             std::vector<uint8_t> enc(chip_encode_max_len(n)), dec(n + (n >> 3) + 4096);
             uint8_t hash[32], hp[32], h5[32];
             chip_encode_info info{}, pinfo{};
