@@ -429,8 +429,8 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         cur = dst;
         cur_n = got;
     }
-    if (snap) {  // decoding.rs:107-111
-        return host::snap_decompress(cur, cur_n, out, out_cap, out_len);
+    if (snap) {  // decoding.rs:107-111 (a large object's chunks on the stage pool)
+        return host::snap_decompress_par(cur, cur_n, out, out_cap, out_len);
     }
     *out_len = cur_n;
     return CHIP_OK;

@@ -354,7 +354,8 @@ int host_stages_into(uint8_t format, const uint8_t *pk, uint64_t pklen, const ui
             scap = host::snap_max_len(n) + 1;
             sd = tmp.get(scap);
         }
-        int st = host::snap_compress(in, n, sd, scap, &cur_n);
+        // one object alone (par): its blocks on the stage pool's threads
+        int st = par ? host::snap_compress_par(in, n, sd, scap, &cur_n) : host::snap_compress(in, n, sd, scap, &cur_n);
         if (st != CHIP_OK) return st;
         cur = sd;
         *bc = cur_n;

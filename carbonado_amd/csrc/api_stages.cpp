@@ -14,12 +14,12 @@ extern "C" {
 
 int chip_snap_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
     if ((!in && n) || !out_len || (n && !out)) return CHIP_ERR_INVALID_ARG;
-    return host::snap_compress(in, n, out, out_cap, out_len);
+    return host::snap_compress_par(in, n, out, out_cap, out_len);  // (a large input's blocks on the stage pool)
 }
 
 int chip_snap_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
     if ((!in && n) || !out_len) return CHIP_ERR_INVALID_ARG;
-    return host::snap_decompress(in, n, out, out_cap, out_len);
+    return host::snap_decompress_par(in, n, out, out_cap, out_len);
 }
 
 int chip_ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const chip_ecies_inject *inject,

@@ -141,6 +141,12 @@ int ecies_encrypt_par_plain(const uint8_t *pubkey, uint64_t pubkey_len, const ui
 int ecies_decrypt_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
                       uint64_t cap, uint64_t *out_len, const uint8_t *key = nullptr,
                       const uint8_t *key_eph = nullptr);
+// snap_compress / snap_decompress for one object of at least STAGE_PAR_MIN
+// bytes on the same pool: the 64 KiB blocks compressed (or the frame's
+// chunks decoded) on every thread; same bytes and statuses (a smaller object,
+// a short buffer or a busy pool: the one-thread functions).
+int snap_compress_par(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+int snap_decompress_par(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
 // An envelope of n bytes is decrypted on the pool (ecies_decrypt_par /
 // ecies_decrypt_snap_par) unless the pool is busy: at least STAGE_PAR_MIN of
 // ciphertext, within GCM's length limit, on the VAES path.  (A key derived

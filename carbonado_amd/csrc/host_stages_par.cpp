@@ -278,6 +278,72 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
     return CHIP_OK;
 }
 
+static int snap_frames_par(StagePool &pool, const uint8_t *P, uint64_t m, uint8_t *out, uint64_t cap,
+                           uint64_t *out_len);
+
+int snap_compress_par(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    StagePool &pool = StagePool::get();
+    if (n < STAGE_PAR_MIN || !out || cap < snap_max_len(n) || !pool.try_acquire())
+        return snap_compress(in, n, out, cap, out_len);
+    struct Hold {
+        StagePool &p;
+        ~Hold() { p.release(); }
+    } hold{pool};
+    struct Block {
+        uint8_t hdr[8];
+        const uint8_t *body;
+        size_t blen;
+    };
+    const uint64_t nb = (n + MAX_BLOCK - 1) / MAX_BLOCK;
+    static thread_local std::vector<uint8_t> t_scr;  // one compressed block per slot
+    if (t_scr.size() < nb * MAX_COMPRESS_BLOCK) t_scr.resize(nb * MAX_COMPRESS_BLOCK);
+    ScratchCap cap_scr{t_scr};
+    uint8_t *scr = t_scr.data();
+    std::vector<Block> blk(nb);
+    std::atomic<uint64_t> next{0};
+    // 1: the blocks on every thread (FrameEncoder's rule per block: snap_block)
+    auto compress = [&](int) {
+        for (uint64_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < nb;) {
+            const uint64_t o = j * MAX_BLOCK;
+            const size_t len = (size_t)std::min<uint64_t>(MAX_BLOCK, n - o);
+            blk[j].blen = snap_block(in + o, len, blk[j].hdr, scr + j * MAX_COMPRESS_BLOCK, &blk[j].body);
+        }
+    };
+    pool.start(compress);
+    compress(0);
+    pool.wait();
+    // 2: the frame: identifier, then each block's header and body at its offset, on every thread
+    std::vector<uint64_t> boff(nb);
+    uint64_t mf = sizeof(STREAM_ID);
+    for (uint64_t j = 0; j < nb; ++j) {
+        boff[j] = mf;
+        mf += 8 + blk[j].blen;
+    }
+    std::memcpy(out, STREAM_ID, sizeof(STREAM_ID));
+    next.store(0, std::memory_order_relaxed);
+    auto place = [&](int) {
+        for (uint64_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < nb;) {
+            std::memcpy(out + boff[j], blk[j].hdr, 8);
+            std::memcpy(out + boff[j] + 8, blk[j].body, blk[j].blen);
+        }
+    };
+    pool.start(place);
+    place(0);
+    pool.wait();
+    *out_len = mf;
+    return CHIP_OK;
+}
+
+int snap_decompress_par(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    StagePool &pool = StagePool::get();
+    if (n < STAGE_PAR_MIN || !pool.try_acquire()) return snap_decompress(in, n, out, cap, out_len);
+    struct Hold {
+        StagePool &p;
+        ~Hold() { p.release(); }
+    } hold{pool};
+    return snap_frames_par(pool, in, n, out, cap, out_len);
+}
+
 void par_for(int parts, const std::function<void(int)> &f) {
     StagePool &pool = StagePool::get();
     if (parts <= 1 || !pool.try_acquire()) {
@@ -298,45 +364,13 @@ bool ecies_par_eligible(uint64_t n) {
     return n >= ECIES_OVERHEAD + STAGE_PAR_MIN && n - ECIES_OVERHEAD <= GCM_MAX_BYTES && gcm_vaes_on();
 }
 
-int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n,
-                           uint8_t *out, uint64_t cap, uint64_t *out_len, const uint8_t *pre_key,
-                           const uint8_t *pre_eph) {
-    StagePool &pool = StagePool::get();
-    if (!ecies_par_eligible(n) || !pool.try_acquire())
-        return ecies_decrypt_snap(secret, secret_len, in, n, out, cap, out_len, nullptr, pre_key, pre_eph);
-    struct Hold {  // the pool until every return below
-        StagePool &p;
-        ~Hold() { p.release(); }
-    } hold{pool};
-    const uint64_t m = n - ECIES_OVERHEAD;
-    uint8_t key[32];
-    if (pre_key && pre_eph && std::memcmp(pre_eph, in, 65) == 0) {
-        std::memcpy(key, pre_key, 32);
-    } else {
-        const int st = ecies_derive_key(secret, secret_len, in, key);
-        if (st != CHIP_OK) return st;
-    }
-    const uint8_t *iv = in + 65, *tag = in + 81, *ct = in + 97;
-    Gcm msg;
-    msg.init(key, iv, 16, false);
-    OPENSSL_cleanse(key, 32);
-    // 1: the ciphertext in 16-B aligned pieces on the pool's threads into a
-    // plaintext buffer; the joined GHASH's tag checked first
-    static thread_local std::vector<uint8_t> t_plain;
-    if (t_plain.size() < m) t_plain.resize(m);
-    ScratchCap cap_plain{t_plain};  // every return below wipes it first
-    uint8_t *P = t_plain.data();
-    const bool parts_ok = gcm_parts(pool, msg, ct, P, m);
-    auto wipe_plain = [&] { wipe_parts(pool, P, m); };
-    uint8_t t[16];
-    msg.tag_joined(m, t);
-    msg.wipe();
-    const bool tag_ok = parts_ok && CRYPTO_memcmp(t, tag, 16) == 0;
-    if (!tag_ok) {
-        wipe_plain();
-        return CHIP_ERR_ECIES;
-    }
-    // 2: snap_walk's size pass over the chunk headers (framing errors first)
+// A snappy frame stream P[0, m) decoded on the pool (held by the caller):
+// snap_walk's size pass over the chunk headers, then the chunks (CRC, raw
+// copy or block decode) on every thread.  Status order as snap_decompress:
+// framing errors, then a short `out` (the required size in *out_len), then
+// CRC / block errors.
+static int snap_frames_par(StagePool &pool, const uint8_t *P, uint64_t m, uint8_t *out, uint64_t cap,
+                           uint64_t *out_len) {
     struct Chunk {
         uint64_t src, dl, doff, ulen;
         uint32_t want;
@@ -377,7 +411,6 @@ int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uin
         s += clen;
     }
     if (frame != CHIP_OK || d > cap || (d && !out)) {
-        wipe_plain();
         if (frame != CHIP_OK) return frame;
         *out_len = d;
         return CHIP_ERR_BUFFER_TOO_SMALL;
@@ -404,10 +437,54 @@ int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uin
     pool.start(content);
     content(0);
     pool.wait();
-    wipe_plain();
     if (bad.load()) return CHIP_ERR_SNAP;
     *out_len = d;
     return CHIP_OK;
+}
+
+
+int ecies_decrypt_snap_par(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n,
+                           uint8_t *out, uint64_t cap, uint64_t *out_len, const uint8_t *pre_key,
+                           const uint8_t *pre_eph) {
+    StagePool &pool = StagePool::get();
+    if (!ecies_par_eligible(n) || !pool.try_acquire())
+        return ecies_decrypt_snap(secret, secret_len, in, n, out, cap, out_len, nullptr, pre_key, pre_eph);
+    struct Hold {  // the pool until every return below
+        StagePool &p;
+        ~Hold() { p.release(); }
+    } hold{pool};
+    const uint64_t m = n - ECIES_OVERHEAD;
+    uint8_t key[32];
+    if (pre_key && pre_eph && std::memcmp(pre_eph, in, 65) == 0) {
+        std::memcpy(key, pre_key, 32);
+    } else {
+        const int st = ecies_derive_key(secret, secret_len, in, key);
+        if (st != CHIP_OK) return st;
+    }
+    const uint8_t *iv = in + 65, *tag = in + 81, *ct = in + 97;
+    Gcm msg;
+    msg.init(key, iv, 16, false);
+    OPENSSL_cleanse(key, 32);
+    // 1: the ciphertext in 16-B aligned pieces on the pool's threads into a
+    // plaintext buffer; the joined GHASH's tag checked first
+    static thread_local std::vector<uint8_t> t_plain;
+    if (t_plain.size() < m) t_plain.resize(m);
+    ScratchCap cap_plain{t_plain};  // every return below wipes it first
+    uint8_t *P = t_plain.data();
+    const bool parts_ok = gcm_parts(pool, msg, ct, P, m);
+    auto wipe_plain = [&] { wipe_parts(pool, P, m); };
+    uint8_t t[16];
+    msg.tag_joined(m, t);
+    msg.wipe();
+    const bool tag_ok = parts_ok && CRYPTO_memcmp(t, tag, 16) == 0;
+    if (!tag_ok) {
+        wipe_plain();
+        return CHIP_ERR_ECIES;
+    }
+    // 2, 3: the frame stream's chunk headers walked, the chunks decoded on every thread
+    const int st = snap_frames_par(pool, P, m, out, cap, out_len);
+    wipe_plain();
+    return st;
 }
 
 int ecies_encrypt_par_plain(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph_sk,

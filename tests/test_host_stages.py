@@ -707,3 +707,31 @@ def test_ecies_receiver_comb_tables_match_oracle(ca):
         e = ca.encoding.ecies(pk, d, ephemeral_sk=eph, nonce=nonce)
         assert e == O.c_ecies_encrypt(pub, d, eph, nonce), (r, int(i))
         assert ca.decoding.ecies(e, sk) == d
+
+
+@pytest.mark.parametrize("kind", ["random", "text", "mixed"])
+def test_snap_stage_functions_on_the_pool_match_oracle(ca, kind):
+    """chip_snap_compress / chip_snap_decompress (and the Snappy stage of a
+    single encode()/decode()) split an input of 256 KiB or more into its
+    64 KiB blocks on the stage pool (host_stages_par.cpp snap_compress_par /
+    snap_decompress_par): the frame is byte-identical to the C oracle's, it
+    decodes back, a flipped byte is refused."""
+    rng = np.random.default_rng({"random": 1, "text": 2, "mixed": 3}[kind])
+    n = (1 << 20) + 12345
+    if kind == "random":
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    else:
+        words = [b"carbonado ", b"segment ", b"zfec ", b"bao ", b"{\"id\": ", b"\n"]
+        d = b"".join(rng.choice(words, n // 4).tolist())[:n]
+        if kind == "mixed":  # incompressible stretches between the text
+            a = bytearray(d)
+            for o in range(0, n - 70_000, 200_000):
+                a[o:o + 70_000] = rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes()
+            d = bytes(a)
+    f = ca.encoding.snap(d)
+    assert f == O.c_snap_compress(d)
+    assert ca.decoding.snap(f) == d
+    bad = bytearray(f)
+    bad[len(bad) // 2] ^= 0x10
+    with pytest.raises(Exception):
+        ca.decoding.snap(bytes(bad))
