@@ -255,9 +255,13 @@ int single_zfec_decode_zc(Ctx *c, uint32_t k, uint32_t m, const uint8_t *const *
 // the device by KM) with the content bytes [0, olen) gathered from `in` by the
 // host meanwhile, into dst; on a mismatch dst is wiped and the status
 // returned.  km_ok() must hold.
-// `meanwhile` (optional) runs on the host after the gather, before the wait.
+// `meanwhile` (optional) runs on the host beside the gather (a pool task of
+// its own when the gather takes several) or after it, before the wait;
+// `gathered` (optional) after both, still before the wait: it may read
+// dst[0, olen), which is unverified until the call returns CHIP_OK.
 int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const uint8_t *hash, uint8_t *dst,
-                     uint64_t olen, const std::function<void()> &meanwhile = {});
+                     uint64_t olen, const std::function<void()> &meanwhile = {},
+                     const std::function<void()> &gathered = {});
 
 // K1 reads and writes 16-B vectors and its tail load relies on 16-B aligned
 // shard addresses (zfec_device.hpp load16_masked).

@@ -20,6 +20,37 @@ struct DecGeom {
     uint64_t olen = 0;  // bytes leaving zfec (k*C - padding, or blen)
 };
 
+// decode()'s host stages (decoding.rs:101-111) on the device stages' output
+// cur[0, cur_n): ECIES (with the key derived ahead, when there is one) then
+// snappy, or the two in one pass; a large object on the stage pool.
+int host_tail(const uint8_t *secret_key, uint64_t sk_len, bool ecies, bool snap, const uint8_t *cur, uint64_t cur_n,
+              uint8_t *out, uint64_t out_cap, uint64_t *out_len, const uint8_t *pre_key, const uint8_t *pre_eph) {
+    Trace trace("host stages");
+    struct Mark {
+        Trace &t;
+        ~Mark() { t.mark("decode"); }
+    } mark{trace};
+    if (ecies && snap)  // decoding.rs:101-111 in one pass
+        return host::ecies_decrypt_snap_par(secret_key, sk_len, cur, cur_n, out, out_cap, out_len, pre_key, pre_eph);
+    if (ecies) {  // decoding.rs:101-105
+        uint64_t got = 0;
+        const int st = host::ecies_decrypt_par(secret_key, sk_len, cur, cur_n, out, out_cap, &got, pre_key, pre_eph);
+        if (st == CHIP_OK || st == CHIP_ERR_BUFFER_TOO_SMALL) *out_len = got;
+        return st;
+    }
+    return host::snap_decompress_par(cur, cur_n, out, out_cap, out_len);  // decoding.rs:107-111
+}
+
+// CHIP_DEC_SPEC=0: a decode's host stages wait for the device's verdict
+// instead of running on the unverified content meanwhile (an A/B knob)
+bool dec_spec_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("CHIP_DEC_SPEC");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 DecGeom dec_geom(uint8_t format, const uint8_t *in, uint64_t n, uint32_t padding) {
     DecGeom g;
     const bool zfec = format & CHIP_FORMAT_ZFEC, bao = format & CHIP_FORMAT_BAO;
@@ -277,7 +308,7 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
     const bool ecies = format & CHIP_FORMAT_ECIES, snap = format & CHIP_FORMAT_SNAPPY;
     if (ecies && !secret_key) return CHIP_ERR_INVALID_ARG;
     // device stages write to `out` directly unless host stages follow
-    thread_local std::vector<uint8_t> t_dev, t_mid;
+    thread_local std::vector<uint8_t> t_dev;
     const uint8_t *cur = in;
     uint64_t cur_n = n;
     uint8_t pre_eph[65], pre_key[32];  // ECIES key derived while the device works
@@ -323,7 +354,20 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
                     have_pre = host::ecies_derive_key(secret_key, sk_len, pre_eph, pre_key) == CHIP_OK;
                 }
             };
-            st = single_decode_km(c, in, n, blen, hash, dst, olen, prekey);
+            // and then the host stages themselves on the gathered (still unverified) content,
+            // into `out`: released only with the device's verdict, wiped without it
+            int spec = -1;
+            const uint64_t out_len0 = *out_len;
+            auto stages = [&] {
+                if (!(ecies || snap) || !dec_spec_on() || (ecies && !have_pre)) return;
+                spec = host_tail(secret_key, sk_len, ecies, snap, dst, olen, out, out_cap, out_len, pre_key, pre_eph);
+            };
+            st = single_decode_km(c, in, n, blen, hash, dst, olen, prekey, stages);
+            if (spec >= 0) {
+                if (st == CHIP_OK) return spec;
+                if (out && out_cap) host::secure_wipe(out, spec == CHIP_OK ? *out_len : out_cap);
+                *out_len = out_len0;
+            }
             if (st != CHIP_OK) return st;
             cur = dst;
             cur_n = olen;
@@ -401,39 +445,8 @@ int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash,
         *out_len = cur_n;
         return CHIP_OK;
     }
-    Trace trace("host stages");
-    struct Mark {
-        Trace &t;
-        ~Mark() { t.mark("decode"); }
-    } mark{trace};
-    if (ecies && snap)  // decoding.rs:101-111 in one pass (a large object on the stage's worker pool)
-        return host::ecies_decrypt_snap_par(secret_key, sk_len, cur, cur_n, out, out_cap, out_len,
-                                            have_pre ? pre_key : nullptr, pre_eph);
-    if (ecies) {  // decoding.rs:101-105
-        uint8_t *dst = out;
-        uint64_t cap = out_cap;
-        if (snap) {
-            t_mid.resize(cur_n + 1);
-            dst = t_mid.data();
-            cap = t_mid.size();
-        }
-        uint64_t got = 0;
-        int st = snap ? host::ecies_decrypt(secret_key, sk_len, cur, cur_n, dst, cap, &got,
-                                            have_pre ? pre_key : nullptr, pre_eph)
-                      : host::ecies_decrypt_par(secret_key, sk_len, cur, cur_n, dst, cap, &got,
-                                                have_pre ? pre_key : nullptr, pre_eph);
-        if (st != CHIP_OK) {
-            if (st == CHIP_ERR_BUFFER_TOO_SMALL) *out_len = got;
-            return st;
-        }
-        cur = dst;
-        cur_n = got;
-    }
-    if (snap) {  // decoding.rs:107-111 (a large object's chunks on the stage pool)
-        return host::snap_decompress_par(cur, cur_n, out, out_cap, out_len);
-    }
-    *out_len = cur_n;
-    return CHIP_OK;
+    return host_tail(secret_key, sk_len, ecies, snap, cur, cur_n, out, out_cap, out_len, have_pre ? pre_key : nullptr,
+                     pre_eph);
 }
 
 }  // extern "C"

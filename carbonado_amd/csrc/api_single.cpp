@@ -133,6 +133,16 @@ void copy_out(uint8_t *dst, const uint8_t *src, uint64_t n) {
 }
 
 
+// a decode's `meanwhile` (the ECIES key) as a task beside the content gather
+// rather than after it: CHIP_DEC_SIDE=0 turns it off (an A/B knob)
+bool dec_side_task() {
+    static const bool on = [] {
+        const char *e = std::getenv("CHIP_DEC_SIDE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // the largest stream (chunks) a single call runs on KS rather than KM:
 // CHIP_KS_SINGLE_MAX (64 .. 512, an A/B knob), default 64
 uint64_t ks_single_max() {
@@ -297,7 +307,7 @@ int single_zfec_decode_zc(Ctx *c, uint32_t k, uint32_t m, const uint8_t *const *
 }
 
 int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const uint8_t *hash, uint8_t *dst,
-                     uint64_t olen, const std::function<void()> &meanwhile) {
+                     uint64_t olen, const std::function<void()> &meanwhile, const std::function<void()> &gathered) {
     Trace trace("decode");
     const uint64_t blen = bao_encoded_len(n);
     if (blen > len) return CHIP_ERR_BAO_TRUNCATED;
@@ -319,19 +329,26 @@ int single_decode_km(Ctx *c, const uint8_t *in, uint64_t len, uint64_t n, const 
         CHIP_HIP(km_bao_decode_dev(d + 64, n, d, nullptr, 0, reinterpret_cast<uint32_t *>(d + 32), c->scratch.p,
                                    c->stream));
     trace.mark("launch");
-    // meanwhile: the content from the caller's own copy of the stream
+    // meanwhile: the content from the caller's own copy of the stream, and
+    // `meanwhile` beside it as one more task of the same pool job
     advise_huge(dst, olen);
-    if (olen) {
-        const uint64_t nc = (olen + 1023) / 1024;
+    const uint64_t nc = (olen + 1023) / 1024;
+    const int parts = olen ? host_parts(nc) : 0;
+    const bool side = meanwhile && parts > 1 && dec_side_task();
+    if (parts) {
         const HostGeo &g = host_geo(n, nc);
-        const int parts = host_parts(nc);
-        host::par_for(parts, [&](int i) {
+        host::par_for(parts + side, [&](int i) {
+            if (side && i == 0) return meanwhile();
+            i -= side;
             const uint64_t a = nc * i / parts, b = nc * (i + 1) / parts;
             host::gather_chunks(dst + 1024 * a, in, g.coff.data() + a, std::min(olen, 1024 * b) - 1024 * a);
         });
     }
     trace.mark("host gather");
-    if (meanwhile) meanwhile();
+    if (meanwhile && !side) meanwhile();
+    trace.mark("meanwhile");
+    if (gathered) gathered();
+    trace.mark("gathered");
     CHIP_HIP(hipStreamSynchronize(c->stream));
     trace.mark("sync");
     const uint32_t verdict = *status;

@@ -307,7 +307,10 @@ CHIP_API int chip_encode(uint8_t format, const uint8_t *pubkey, uint64_t pubkey_
 /* decoding::decode (decoding.rs:80-114): bao -> zfec on the device, then
  * ecies -> snap on the host.  With the Snappy bit the output size is only
  * known after decompression: a short buffer returns CHIP_ERR_BUFFER_TOO_SMALL
- * with *out_len = the size needed. */
+ * with *out_len = the size needed.  After any other error out's bytes are
+ * unspecified: never content that failed verification (the host stages may
+ * run on the content while the device verifies it; a failed verdict wipes
+ * what they wrote). */
 CHIP_API int chip_decode(const uint8_t *secret_key, uint64_t sk_len, const uint8_t *hash, uint64_t hash_len,
                 const uint8_t *in, uint64_t n, uint32_t padding, uint8_t format, uint8_t *out,
                 uint64_t out_cap, uint64_t *out_len);

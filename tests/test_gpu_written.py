@@ -111,6 +111,44 @@ def test_encode_decode_write_every_byte(gpu, n, level):
     assert back == raw
 
 
+@pytest.mark.parametrize("n", [1000, 70_000 + 13, (1 << 20) + 5])
+@pytest.mark.parametrize("level", [5, 6, 7, 13, 14, 15])
+@pytest.mark.parametrize("where", ["node", "content"])
+def test_failed_verdict_leaves_no_plaintext(gpu, n, level, where):
+    """decode() at a level with host stages runs them on the content while
+    the device verifies; a failed verdict returns BaoDecodeError(HashMismatch)
+    (decoding.rs:89-93) and the caller's buffer holds no decoded byte:
+    every byte is the fill or wiped.  A damaged parent node (content intact,
+    so the host stages succeed) and a damaged content byte."""
+    from carbonado_amd import _lib
+    from carbonado_amd.encoding import public_key
+    L = gpu
+    raw = np.frombuffer(_rnd(n, n + level), np.uint8).copy()
+    raw[::3] = 0x41  # compressible: the snappy stage decodes real blocks
+    raw = raw.tobytes()
+    d = _u8(raw)
+    pk = _u8(public_key(SK))
+    inj, keep = _inject()
+    h = np.zeros(32, np.uint8)
+    info = _lib.EncodeInfoC()
+    enc = bytearray(_twice(L.chip_encode_max_len(n), lambda o, c, ln: L.chip_encode(
+        level, _p(pk), pk.size if level & 1 else 0, ctypes.byref(inj), _p(d), n, o, c, ln, _p(h),
+        ctypes.byref(info))))
+    if where == "node" and len(enc) > 8 + 1024 + 64:
+        enc[8 + 5] ^= 0x10  # the root's left child hash (pre-order: the first parent node)
+    else:
+        enc[len(enc) // 2] ^= 0x10
+    e, sk = _u8(enc), _u8(SK)
+    cap = n + 1024
+    buf = np.full(cap + 64, 0xA5, np.uint8)
+    olen = ctypes.c_uint64(7)
+    rc = L.chip_decode(_p(sk), 32, _p(h), 32, _p(e), len(enc), info.padding_len, level, _p(buf), cap,
+                       ctypes.byref(olen))
+    assert rc == 5, rc  # CHIP_ERR_BAO_HASH_MISMATCH
+    assert olen.value == 7
+    assert np.isin(buf, [0, 0xA5]).all(), "decoded bytes left behind after a failed verdict"
+
+
 def test_host_stages_write_every_byte(gpu):
     from carbonado_amd.encoding import public_key
     L = gpu
