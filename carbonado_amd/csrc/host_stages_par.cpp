@@ -74,7 +74,11 @@ class StagePool {
   private:
     static constexpr int SPIN = 1 << 15;  // ~0.1 ms of pause instructions
     StagePool() {
-        int t = 8;  // the calling thread + 7 workers; CHIP_STAGE_THREADS=1: one thread
+        // the calling thread + up to 15 workers, no more than the machine's
+        // hardware threads (r11zzd: 16 against 8, level 15 of 4 MiB of text
+        // 608-647 -> 407-438 us); CHIP_STAGE_THREADS=1: one thread
+        const int hw = (int)std::thread::hardware_concurrency();
+        int t = std::max(1, std::min(16, hw > 0 ? hw : 8));
         if (const char *e = std::getenv("CHIP_STAGE_THREADS")) t = std::max(1, std::min(32, std::atoi(e)));
         workers_ = t - 1;
         pid_ = getpid();
