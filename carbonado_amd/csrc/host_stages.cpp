@@ -361,6 +361,13 @@ static k1::Pt peer_mul(const uint8_t peer[65], const uint8_t sk[32]) {
 }
 
 int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out) {
+    // the two scalar multiplications side by side (a stage-pool worker takes
+    // one unless the pool is busy: then both here, one after the other)
+    return ecies_prepare_with(peer, eph_sk, out, [](const std::function<void(int)> &f) { par_for(2, f); });
+}
+
+int ecies_prepare_with(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out,
+                       const std::function<void(const std::function<void(int)> &)> &run2) {
     uint8_t sk[32];
     if (eph_sk) {
         std::memcpy(sk, eph_sk, 32);
@@ -371,10 +378,8 @@ int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out) 
         } while (!scalar_ok(sk));
     }
     uint8_t master[130];
-    // the two scalar multiplications side by side (a stage-pool worker takes
-    // one unless the pool is busy: then both here, one after the other)
     k1::Pt pts[2];
-    par_for(2, [&](int i) { pts[i] = i == 0 ? k1::mul_g(sk) : peer_mul(peer, sk); });
+    run2([&](int i) { pts[i] = i == 0 ? k1::mul_g(sk) : peer_mul(peer, sk); });
     bool ok = k1::to65_pair(pts[0], pts[1], out->eph_pub, master + 65);
     std::memcpy(master, out->eph_pub, 65);
     OPENSSL_cleanse(sk, sizeof sk);

@@ -60,6 +60,11 @@ struct EciesKey {
 };
 int ecies_peer(const uint8_t *pubkey, uint64_t pubkey_len, uint8_t peer[65]);
 int ecies_prepare(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out);
+// The same with its two scalar multiplications (k·G, k·P) handed to run2,
+// which calls f(0) and f(1), side by side or not, and returns once both are
+// done (a caller that holds the stage pool runs them on its workers).
+int ecies_prepare_with(const uint8_t peer[65], const uint8_t *eph_sk, EciesKey *out,
+                       const std::function<void(const std::function<void(int)> &)> &run2);
 void ecies_key_wipe(EciesKey *k);
 
 // memcpy into pinned staging memory that only the DMA engine reads next:

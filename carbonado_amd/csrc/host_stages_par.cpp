@@ -190,9 +190,9 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
     std::vector<Block> blk(nb);
     std::vector<uint64_t> boff(nb);  // frame offset of each block's chunk header
     std::atomic<uint64_t> next{0};
-    int key_st = CHIP_ERR_ECIES;
     EciesKey key;
-    // 1: the snappy blocks on every thread, the key agreement on one worker first
+    // 1: the snappy blocks on every thread, the key agreement's two scalar
+    // multiplications first: k·G here, k·P on one worker
     auto compress = [&] {
         for (uint64_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < nb;) {
             const uint64_t o = j * MAX_BLOCK;
@@ -200,16 +200,21 @@ int ecies_encrypt_par(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t 
             blk[j].blen = snap_block(in + o, len, blk[j].hdr, scr + j * MAX_COMPRESS_BLOCK, &blk[j].body);
         }
     };
-    pool.start([&](int w) {
-        if (w == 1) {
-            uint8_t peer[65];
-            key_st = ecies_peer(pubkey, pubkey_len, peer);
-            if (key_st == CHIP_OK) key_st = ecies_prepare(peer, eph_sk, &key);
-        }
+    bool compressed = false;
+    auto run2 = [&](const std::function<void(int)> &f) {
+        pool.start([&](int w) {
+            if (w == 1) f(1);
+            compress();
+        });
+        f(0);
         compress();
-    });
-    compress();
-    pool.wait();  // blk, boff and key_st are this thread's from here (the pool's mutex orders them)
+        pool.wait();  // blk is this thread's from here (the pool's mutex orders it)
+        compressed = true;
+    };
+    uint8_t peer[65];
+    int key_st = ecies_peer(pubkey, pubkey_len, peer);
+    if (key_st == CHIP_OK) key_st = ecies_prepare_with(peer, eph_sk, &key, run2);
+    if (key_st == CHIP_OK && !compressed) key_st = CHIP_ERR_ECIES;  // (run2 is called on every success)
     uint8_t *iv = out + 65;
     if (key_st == CHIP_OK) {
         std::memcpy(out, key.eph_pub, 65);
@@ -505,7 +510,16 @@ int ecies_encrypt_par_plain(const uint8_t *pubkey, uint64_t pubkey_len, const ui
     uint8_t peer[65];
     EciesKey key;
     int st = ecies_peer(pubkey, pubkey_len, peer);
-    if (st == CHIP_OK) st = ecies_prepare(peer, eph_sk, &key);
+    // k·G here and k·P on one of the held pool's workers (ecies_prepare's own
+    // par_for would find the pool taken and run them one after the other)
+    if (st == CHIP_OK)
+        st = ecies_prepare_with(peer, eph_sk, &key, [&](const std::function<void(int)> &f) {
+            pool.start([&](int w) {
+                if (w == 1) f(1);
+            });
+            f(0);
+            pool.wait();
+        });
     uint8_t *iv = out + 65;
     if (st == CHIP_OK) {
         std::memcpy(out, key.eph_pub, 65);
