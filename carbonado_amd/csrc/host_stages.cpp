@@ -275,6 +275,12 @@ int ecies_peer(const uint8_t *pubkey, uint64_t pubkey_len, uint8_t peer[65]) {
         k1::fe_to_be(y, peer + 33);
         return CHIP_OK;
     }
+    if (pubkey && (pubkey_len == 64 || (pubkey_len == 65 && pubkey[0] == 0x04))) {  // uncompressed / raw x || y
+        peer[0] = 0x04;
+        std::memcpy(peer + 1, pubkey + (pubkey_len - 64), 64);
+        k1::Fe x, y;
+        return k1::parse_full(peer, x, y) ? CHIP_OK : CHIP_ERR_ECIES;
+    }
     PtPtr pt(parse_public(pubkey, pubkey_len));
     if (!pt.p) return CHIP_ERR_ECIES;
     BnPtr x(BN_new()), y(BN_new());
@@ -430,22 +436,41 @@ int ecies_encrypt(const uint8_t *pubkey, uint64_t pubkey_len, const uint8_t *eph
 }
 
 
+// The AES key of an envelope whose ephemeral public key is eph (65 B as the
+// envelope holds it) for the receiver's secret (32 B, 0 < k < n: checked by
+// the caller): the usual uncompressed form parsed and checked here
+// (k1::parse_full; OpenSSL's BIGNUM route cost ~30 us more per call), the
+// hybrid 0x06 / 0x07 forms through OpenSSL; then HKDF(eph || (k * eph)65).
+static bool eph_key(const uint8_t secret[32], const uint8_t eph[65], uint8_t key[32]) {
+    if (eph[0] != 0x04) {
+        BnPtr k(parse_secret(secret, 32));
+        PtPtr pt(parse_public(eph, 65));
+        return k.p && pt.p && derive_key(k.p, pt.p, eph, key);
+    }
+    k1::Fe x, y;
+    if (!k1::parse_full(eph, x, y)) return false;
+    uint8_t master[130];
+    std::memcpy(master, eph, 65);
+    bool ok = k1::to65(k1::mul(secret, x, y), master + 65);
+    ok = ok && hkdf_sha256_32(master, 130, key);
+    OPENSSL_cleanse(master, sizeof master);
+    return ok;
+}
+
 // the envelope's AES key: the one derived ahead when its ephemeral key is
 // this envelope's, else from the secret and the envelope's ephemeral key
-static bool envelope_key(const BnPtr &k, const uint8_t *in, const uint8_t *pre_key, const uint8_t *pre_eph,
+static bool envelope_key(const uint8_t *secret, const uint8_t *in, const uint8_t *pre_key, const uint8_t *pre_eph,
                          uint8_t key[32]) {
     if (pre_key && pre_eph && std::memcmp(pre_eph, in, 65) == 0) {
         std::memcpy(key, pre_key, 32);
         return true;
     }
-    PtPtr eph(parse_public(in, 65));
-    return eph.p && derive_key(k.p, eph.p, in, key);
+    return eph_key(secret, in, key);
 }
 
 int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
                   uint64_t cap, uint64_t *out_len, const uint8_t *pre_key, const uint8_t *pre_eph) {
-    BnPtr k(parse_secret(secret, secret_len));
-    if (!k.p) return CHIP_ERR_ECIES;
+    if (!secret || secret_len != 32 || !scalar_ok(secret)) return CHIP_ERR_ECIES;  // SecretKey::parse
     if (n < ECIES_OVERHEAD) return CHIP_ERR_ECIES;  // InvalidMessage
     const uint64_t m = n - ECIES_OVERHEAD;
     if (cap < m || (m && !out)) {
@@ -453,7 +478,7 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
         return CHIP_ERR_BUFFER_TOO_SMALL;
     }
     uint8_t key[32];
-    if (!envelope_key(k, in, pre_key, pre_eph, key)) return CHIP_ERR_ECIES;
+    if (!envelope_key(secret, in, pre_key, pre_eph, key)) return CHIP_ERR_ECIES;
     const uint8_t *iv = in + 65, *tag = in + 81, *ct = in + 97;
     CipherCtx cc;
     bool ok = cc.init(key, iv, false) && cc.update(ct, m, out);
@@ -481,12 +506,11 @@ int ecies_decrypt(const uint8_t *secret, uint64_t secret_len, const uint8_t *in,
 int ecies_decrypt_snap(const uint8_t *secret, uint64_t secret_len, const uint8_t *in, uint64_t n, uint8_t *out,
                        uint64_t cap, uint64_t *out_len, uint8_t *window, const uint8_t *pre_key,
                        const uint8_t *pre_eph) {
-    BnPtr k(parse_secret(secret, secret_len));
-    if (!k.p) return CHIP_ERR_ECIES;
+    if (!secret || secret_len != 32 || !scalar_ok(secret)) return CHIP_ERR_ECIES;  // SecretKey::parse
     if (n < ECIES_OVERHEAD) return CHIP_ERR_ECIES;
     const uint64_t m = n - ECIES_OVERHEAD;
     uint8_t key[32];
-    if (!envelope_key(k, in, pre_key, pre_eph, key)) return CHIP_ERR_ECIES;
+    if (!envelope_key(secret, in, pre_key, pre_eph, key)) return CHIP_ERR_ECIES;
     const uint8_t *iv = in + 65, *ct = in + 97;
     const uint8_t *tag = in + 81;
     CipherCtx cc;
@@ -860,11 +884,8 @@ int snap_compress_stream(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t c
 void secure_wipe(void *p, size_t n) { OPENSSL_cleanse(p, n); }
 
 int ecies_derive_key(const uint8_t *secret, uint64_t secret_len, const uint8_t eph[65], uint8_t key[32]) {
-    BnPtr k(parse_secret(secret, secret_len));
-    if (!k.p) return CHIP_ERR_ECIES;
-    PtPtr pt(parse_public(eph, 65));
-    if (!pt.p) return CHIP_ERR_ECIES;
-    return derive_key(k.p, pt.p, eph, key) ? CHIP_OK : CHIP_ERR_ECIES;
+    if (!secret || secret_len != 32 || !scalar_ok(secret)) return CHIP_ERR_ECIES;  // SecretKey::parse
+    return eph_key(secret, eph, key) ? CHIP_OK : CHIP_ERR_ECIES;
 }
 
 void gather_chunks(uint8_t *dst, const uint8_t *row, const uint64_t *coff, uint64_t n) {

@@ -241,11 +241,12 @@ inline bool fe_is_zero(const Fe &f) {
 // A compressed point (0x02 / 0x03 || x, 33 bytes) -> affine x, y, as
 // libsecp256k1's PublicKey::parse and OpenSSL's oct2point accept it: false
 // unless x < p and x^3 + 7 is a square; y the root of the tag's parity.
+constexpr uint8_t P_BE[32] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                              0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                              0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFE, 0xFF, 0xFF, 0xFC, 0x2F};
+
 inline bool decompress(const uint8_t in[33], Fe &x, Fe &y) {
-    static const uint8_t P[32] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
-                                  0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
-                                  0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFE, 0xFF, 0xFF, 0xFC, 0x2F};
-    if ((in[0] != 0x02 && in[0] != 0x03) || std::memcmp(in + 1, P, 32) >= 0) return false;
+    if ((in[0] != 0x02 && in[0] != 0x03) || std::memcmp(in + 1, P_BE, 32) >= 0) return false;
     x = fe_from_be(in + 1);
     const Fe y2 = fe_add(fe_mul(fe_sqr(x), x), Fe{{7, 0, 0, 0, 0}});
     Fe r = fe_sqrt_cand(y2);
@@ -254,6 +255,16 @@ inline bool decompress(const uint8_t in[33], Fe &x, Fe &y) {
     if ((r.v[0] & 1) != (uint64_t)(in[0] & 1)) r = fe_norm(fe_sub(Fe{{0, 0, 0, 0, 0}}, r));
     y = r;
     return true;
+}
+
+// An uncompressed point (0x04 || x || y, 65 bytes), as libsecp256k1's
+// PublicKey::parse and OpenSSL's oct2point accept that form: false unless
+// x, y < p and y^2 = x^3 + 7.
+inline bool parse_full(const uint8_t in[65], Fe &x, Fe &y) {
+    if (in[0] != 0x04 || std::memcmp(in + 1, P_BE, 32) >= 0 || std::memcmp(in + 33, P_BE, 32) >= 0) return false;
+    x = fe_from_be(in + 1);
+    y = fe_from_be(in + 33);
+    return fe_is_zero(fe_sub(fe_sqr(y), fe_add(fe_mul(fe_sqr(x), x), Fe{{7, 0, 0, 0, 0}})));
 }
 
 struct Pt {

@@ -664,6 +664,43 @@ def test_compressed_receiver_keys(ca):
             ca.encoding.ecies(pk, msg, ephemeral_sk=eph, nonce=nonce)
 
 
+def test_uncompressed_keys_checked_natively(ca):
+    """65- and 64-byte keys (the receiver's on encrypt, the envelope's
+    ephemeral one on decrypt) are parsed by the native field code
+    (secp256k1_host.hpp parse_full: x, y < p and y^2 = x^3 + 7), as
+    PublicKey::parse_slice accepts them: the C oracle's envelope for valid
+    keys, EciesError for a point off the curve or a coordinate >= p; the
+    hybrid 0x06 / 0x07 forms (OpenSSL's route) give the 0x04 form's envelope
+    with the right parity tag and EciesError with the wrong one."""
+    from carbonado_amd.error import EciesError
+    P = 2**256 - 2**32 - 977
+    sk = H.sha256(b"full receiver")
+    pub = H.public_key(sk)
+    x, y = int.from_bytes(pub[1:33], "big"), int.from_bytes(pub[33:], "big")
+    eph, nonce = H.sha256(b"full eph"), H.sha256(b"full nonce")[:16]
+    msg = b"uncompressed receiver " * 40
+    good = H.ecies_encrypt(pub, msg, eph, nonce)
+    assert ca.encoding.ecies(pub, msg, ephemeral_sk=eph, nonce=nonce) == good
+    assert ca.encoding.ecies(pub[1:], msg, ephemeral_sk=eph, nonce=nonce) == good
+    hyb = bytes([6 + (y & 1)]) + pub[1:]
+    assert ca.encoding.ecies(hyb, msg, ephemeral_sk=eph, nonce=nonce) == good
+    pt = lambda a, b: b"\x04" + a.to_bytes(32, "big") + b.to_bytes(32, "big")
+    bad = [pt(x, (y + 1) % P), pt(x, P - y + 1), bytes([7 - (y & 1)]) + pub[1:], b"\x05" + pub[1:],
+           b"\x04" + bytes(64), pt((x + 1) % P, y)]
+    if y + P < 2**256:
+        bad.append(pt(x, y + P))
+    if x + P < 2**256:
+        bad.append(pt(x + P, y))
+    for pk in bad + [b[1:] for b in bad if b[0] == 4]:
+        with pytest.raises(EciesError):
+            ca.encoding.ecies(pk, msg, ephemeral_sk=eph, nonce=nonce)
+    assert ca.decoding.ecies(good, sk) == msg
+    ex, ey = int.from_bytes(good[1:33], "big"), int.from_bytes(good[33:65], "big")
+    for e65 in [pt(ex, (ey + 1) % P), pt(ex, P), b"\x04" + bytes(64)] + ([pt(ex, ey + P)] if ey + P < 2**256 else []):
+        with pytest.raises(EciesError):
+            ca.decoding.ecies(e65 + good[65:], sk)
+
+
 @pytest.mark.parametrize("n", [256 * 1024 - 97, 256 * 1024, 300_001, 5 << 20])
 def test_ecies_stage_functions_on_the_pool_match_oracle(ca, n):
     """chip_ecies_encrypt / chip_ecies_decrypt (the stage functions) split a
