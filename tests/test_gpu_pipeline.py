@@ -629,3 +629,29 @@ def test_decode_key_derived_during_device_work(gpu, level):
     with pytest.raises(BaoDecodeError if level & 4 else EciesError):
         ca.decode(SK, h, bytes(bad), info.padding_len, level)
     assert ca.decode(SK, h, enc, info.padding_len, level) == d  # the stale derived key is not reused
+
+
+@pytest.mark.parametrize("level", [5, 7, 13, 15])
+@pytest.mark.parametrize("n", [1000, 300_000])
+def test_verified_stream_with_a_bad_envelope(gpu, level, n):
+    """A stream that verifies but whose ECIES envelope does not: the content
+    of a level (level & 12) encoding is an envelope with its ephemeral key
+    moved off the curve, or with a flipped ciphertext byte; decode() at the
+    Ecies level verifies the stream (bao passes), runs the host stages on the
+    content meanwhile (no key derived ahead for the off-curve key) and
+    returns EciesError (decoding.rs:101-105), for the KS (1000 B) and KM
+    (300 kB) routes."""
+    import carbonado_amd as ca
+    from carbonado_amd.error import EciesError
+    d = np.random.default_rng(n + level).integers(0, 256, n, dtype=np.uint8).tobytes()
+    enc, h, info = ca.encode(PUB, d, level)
+    envelope = O.decode(h, enc, info.padding_len, level & 12)
+    P = 2**256 - 2**32 - 977
+    y = int.from_bytes(envelope[33:65], "big")
+    off_curve = envelope[:33] + ((y + 1) % P).to_bytes(32, "big") + envelope[65:]
+    flipped = bytearray(envelope)
+    flipped[-1] ^= 1
+    for bad in (off_curve, bytes(flipped)):
+        benc, bh, binfo = ca.encode(b"", bad, level & 12)
+        with pytest.raises(EciesError):
+            ca.decode(SK, bh, benc, binfo.padding_len, level)
